@@ -1,0 +1,250 @@
+/*
+ * gpusched.h — C-ABI of the MI355X (gfx950) provisioning-solve library.
+ *
+ * This is the drop-in boundary a Go `pkg/gpusched` (cgo) binds. It replaces,
+ * for one call, the in-process work that karpenter-core performs between
+ *   CloudProvider.GetInstanceTypes   (reference pkg/cloudprovider/cloudprovider.go:553-583)
+ * and the NodeClaims the provisioner creates, i.e. sigs.k8s.io/karpenter@v1.13.0
+ *   scheduling.NewScheduler(...).Solve(pods).TruncateInstanceTypes(60)
+ * (reached from reference cmd/controller/main.go:76-86; source not vendored,
+ * see SURVEY.md §8(b)/(c)).  The IBM catalog that feeds it is produced by
+ *   IBMInstanceTypeProvider.List / convertVPCProfileToInstanceType
+ *   (reference pkg/providers/common/instancetype/instancetype.go:221-246,659-790).
+ *
+ * Conventions
+ *  - Every string is referenced by an index into gs_problem.strings
+ *    (NUL-terminated UTF-8, compared bytewise like Go strings). The empty
+ *    string must be present when a field is "unset" (e.g. toleration key "").
+ *  - Quantities are int64 milli-units (resource.Quantity.MilliValue()).
+ *  - All arrays are caller-owned and only read during the call.
+ *  - Result memory (gs_result / gs_feas_result) is owned by the context and
+ *    stays valid until the next call on that context or gs_destroy.
+ *  - No exceptions cross the ABI; every entry point returns gs_status and
+ *    gs_last_error() holds a human-readable message for the last failure.
+ *  - One context is single-threaded and not reentrant.
+ */
+#ifndef GPUSCHED_H
+#define GPUSCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum gs_status {
+  GS_OK = 0,
+  GS_E_INVALID = 1,     /* malformed input (bad index, bad operator, ...) */
+  GS_E_UNSUPPORTED = 2, /* input uses a scheduling feature this build does not implement */
+  GS_E_CAPACITY = 3,    /* a device capacity limit was exceeded */
+  GS_E_HIP = 4,         /* HIP runtime error */
+  GS_E_RCCL = 5,        /* RCCL error */
+  GS_E_NO_DEVICE = 6    /* no gfx950 device visible */
+} gs_status;
+
+/* k8s NodeSelectorOperator (+ karpenter Gt/Lt).  Gte/Lte of the v1.13 CRD
+ * (charts/crds/karpenter.sh_nodepools.yaml:292-300) are rejected with
+ * GS_E_UNSUPPORTED until their upstream semantics are pinned. */
+enum {
+  GS_OP_IN = 0,
+  GS_OP_NOTIN = 1,
+  GS_OP_EXISTS = 2,
+  GS_OP_DOES_NOT_EXIST = 3,
+  GS_OP_GT = 4,
+  GS_OP_LT = 5,
+  GS_OP_GTE = 6,
+  GS_OP_LTE = 7
+};
+
+/* corev1.TolerationOperator ("" is Equal) */
+enum { GS_TOL_EQUAL = 0, GS_TOL_EXISTS = 1 };
+
+/* gs_pod.flags: scheduling features present on the pod that this build
+ * refuses (GS_E_UNSUPPORTED) rather than silently ignoring. */
+enum {
+  GS_POD_TOPOLOGY_SPREAD = 1u << 0,
+  GS_POD_AFFINITY = 1u << 1,
+  GS_POD_ANTI_AFFINITY = 1u << 2,
+  GS_POD_HOST_PORTS = 1u << 3,
+  GS_POD_VOLUMES = 1u << 4
+};
+
+typedef struct gs_range {
+  uint32_t begin;
+  uint32_t count;
+} gs_range;
+
+/* one NodeSelectorRequirementWithMinValues */
+typedef struct gs_requirement {
+  uint32_t key;          /* string id */
+  uint32_t op;           /* GS_OP_* */
+  gs_range values;       /* into gs_problem.value_ids (string ids) */
+  int32_t min_values;    /* -1 when unset */
+} gs_requirement;
+
+typedef struct gs_quantity {
+  uint32_t resource; /* string id, e.g. "cpu", "memory", "pods", "nvidia.com/gpu" */
+  int64_t milli;
+} gs_quantity;
+
+typedef struct gs_label {
+  uint32_t key;   /* string id */
+  uint32_t value; /* string id */
+} gs_label;
+
+typedef struct gs_taint {
+  uint32_t key, value, effect; /* string ids */
+} gs_taint;
+
+typedef struct gs_toleration {
+  uint32_t key;    /* string id ("" = any key) */
+  uint32_t op;     /* GS_TOL_* */
+  uint32_t value;  /* string id */
+  uint32_t effect; /* string id ("" = any effect) */
+} gs_toleration;
+
+/* a NodeSelectorTerm (required: weight ignored) or a
+ * PreferredSchedulingTerm (weight = its weight) */
+typedef struct gs_term {
+  gs_range requirements; /* into gs_problem.reqs */
+  int32_t weight;
+} gs_term;
+
+/* cloudprovider.Offering (reference instancetype.go:764-771) */
+typedef struct gs_offering {
+  gs_range requirements; /* zone In[z], capacity-type In[ct] */
+  double price;
+  uint32_t available;
+} gs_offering;
+
+/* cloudprovider.InstanceType (reference instancetype.go:778-789) */
+typedef struct gs_instance_type {
+  uint32_t name;         /* string id */
+  gs_range requirements; /* into reqs */
+  gs_range capacity;     /* into quantities */
+  gs_range overhead;     /* into quantities: Overhead.Total() = kube+system+eviction */
+  gs_range offerings;    /* into offerings, in reference order (zones x capacity types) */
+} gs_instance_type;
+
+/* karpv1.NodePool as seen by NewNodeClaimTemplate */
+typedef struct gs_nodepool {
+  uint32_t name;            /* string id */
+  int32_t weight;
+  gs_range requirements;    /* spec.template.spec.requirements */
+  gs_range labels;          /* spec.template.metadata.labels */
+  gs_range taints;          /* spec.template.spec.taints */
+  gs_range limits;          /* spec.limits minus current usage (remaining) */
+  uint32_t has_limits;
+  gs_range daemon_requests; /* RequestsForPods(compatible daemonset pods) */
+  gs_range instance_types;  /* into it_refs: GetInstanceTypes(nodePool) in order */
+} gs_nodepool;
+
+/* a pending pod; requests = resources.RequestsForPods(pod) (incl. pods=1) */
+typedef struct gs_pod {
+  uint32_t uid;             /* string id */
+  int64_t creation_ns;      /* metadata.creationTimestamp (ns) */
+  gs_range requests;        /* into quantities */
+  gs_range node_selector;   /* into labels */
+  gs_range required_terms;  /* into terms: requiredDuringScheduling nodeSelectorTerms (OR) */
+  gs_range preferred_terms; /* into terms: preferredDuringScheduling, with weights */
+  gs_range tolerations;     /* into tolerations */
+  uint32_t flags;           /* GS_POD_* */
+} gs_pod;
+
+/* an existing (state) node: ExistingNode inputs */
+typedef struct gs_node {
+  uint32_t name;        /* string id (also its hostname) */
+  uint32_t initialized;
+  gs_range labels;      /* node labels */
+  gs_range taints;
+  gs_range available;   /* StateNode.Available() */
+  gs_range requests;    /* remaining daemonset requests already owed */
+} gs_node;
+
+typedef struct gs_problem {
+  const char* const* strings; uint32_t n_strings;
+  const uint32_t* value_ids; uint32_t n_value_ids;
+  const gs_requirement* reqs; uint32_t n_reqs;
+  const gs_quantity* quantities; uint32_t n_quantities;
+  const gs_label* labels; uint32_t n_labels;
+  const gs_taint* taints; uint32_t n_taints;
+  const gs_toleration* tolerations; uint32_t n_tolerations;
+  const gs_term* terms; uint32_t n_terms;
+  const uint32_t* it_refs; uint32_t n_it_refs;
+  const gs_offering* offerings; uint32_t n_offerings;
+  const gs_instance_type* instance_types; uint32_t n_instance_types;
+  const gs_nodepool* nodepools; uint32_t n_nodepools;
+  const gs_pod* pods; uint32_t n_pods;
+  const gs_node* nodes; uint32_t n_nodes;
+} gs_problem;
+
+/* Results.TruncateInstanceTypes(60) of Scheduler.Solve */
+typedef struct gs_result {
+  uint32_t n_claims;                 /* new NodeClaims, creation order */
+  const uint32_t* claim_nodepool;    /* [n_claims] index into gs_problem.nodepools */
+  const uint32_t* claim_pod_offsets; /* [n_claims+1] */
+  const uint32_t* claim_pods;        /* pod indices, add order */
+  const uint32_t* claim_it_offsets;  /* [n_claims+1] */
+  const uint32_t* claim_its;         /* catalog indices, OrderByPrice, <= 60 each */
+  const char* const* claim_requirements; /* [n_claims] canonical text */
+  uint32_t n_resources;              /* resource vocabulary for claim_requests */
+  const uint32_t* resource_names;    /* [n_resources] string ids, ascending by name */
+  const int64_t* claim_requests;     /* [n_claims*n_resources] milli */
+  uint32_t n_nodes;
+  const uint32_t* node_pod_offsets;  /* [n_nodes+1] existing-node assignments */
+  const uint32_t* node_pods;
+  uint32_t n_errors;
+  const uint32_t* error_pods;        /* pods left unschedulable, ascending index */
+  /* instrumentation (product only; the oracle reports total only) */
+  uint64_t checks;                   /* pod x offering checks of the static matrix */
+  uint64_t pops;                     /* queue pops performed */
+  double t_encode_ms, t_upload_ms, t_feas_ms, t_ffd_ms, t_truncate_ms, t_fetch_ms, t_total_ms;
+} gs_result;
+
+/* Static pod x offering feasibility (K1/K2): for every (pod, nodepool) the
+ * instance types a NodeClaim opened for that pod alone could keep
+ * (filterInstanceTypesByRequirements of NodeClaim.CanAdd on a fresh
+ * NodeClaim) and the cheapest of them (first of OrderByPrice). */
+typedef struct gs_feas_result {
+  uint32_t n_pods, n_nodepools, n_its;
+  uint32_t words;                  /* u64 words per row = ceil(n_its/64) */
+  const uint64_t* rows;            /* [n_pods][n_nodepools][words], bit i = catalog IT i */
+  const int32_t* cheapest_it;      /* [n_pods][n_nodepools], -1 if row empty */
+  const uint32_t* n_feasible_offerings; /* [n_pods][n_nodepools] */
+  uint64_t checks;
+  double t_kernel_ms;
+} gs_feas_result;
+
+typedef struct gs_config {
+  int32_t device;        /* HIP device ordinal */
+  uint32_t max_claims;   /* 0 = default */
+  uint32_t flags;        /* reserved */
+} gs_config;
+
+typedef struct gs_ctx gs_ctx;
+
+gs_status gs_create(const gs_config* cfg, gs_ctx** out);
+void gs_destroy(gs_ctx* ctx);
+
+/* encode + upload (host -> HBM); inputs become device-resident */
+gs_status gs_prepare(gs_ctx* ctx, const gs_problem* problem);
+/* run the device solve on the prepared problem (no host<->device traffic
+ * except a completion flag); can be called repeatedly */
+gs_status gs_run(gs_ctx* ctx);
+/* fetch + decode the last run's result */
+gs_status gs_fetch(gs_ctx* ctx, gs_result* out);
+/* prepare + run + fetch */
+gs_status gs_solve(gs_ctx* ctx, const gs_problem* problem, gs_result* out);
+
+/* static feasibility matrix only (K1/K2) on a prepared problem */
+gs_status gs_feasibility(gs_ctx* ctx, gs_feas_result* out);
+
+size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);
+const char* gs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPUSCHED_H */

@@ -1,0 +1,149 @@
+"""ctypes / numpy mirror of include/gpusched.h (the C-ABI boundary).
+
+Struct layouts here must match the header byte for byte; tests/test_abi.py
+checks sizes against the compiled library's own sizeof table.
+"""
+import ctypes as C
+
+import numpy as np
+
+GS_OK, GS_E_INVALID, GS_E_UNSUPPORTED, GS_E_CAPACITY, GS_E_HIP, GS_E_RCCL, GS_E_NO_DEVICE = range(7)
+STATUS_NAMES = {
+    0: "GS_OK", 1: "GS_E_INVALID", 2: "GS_E_UNSUPPORTED", 3: "GS_E_CAPACITY",
+    4: "GS_E_HIP", 5: "GS_E_RCCL", 6: "GS_E_NO_DEVICE",
+}
+
+OP_IN, OP_NOTIN, OP_EXISTS, OP_DNE, OP_GT, OP_LT, OP_GTE, OP_LTE = range(8)
+OPS = {"In": OP_IN, "NotIn": OP_NOTIN, "Exists": OP_EXISTS, "DoesNotExist": OP_DNE,
+       "Gt": OP_GT, "Lt": OP_LT, "Gte": OP_GTE, "Lte": OP_LTE}
+TOL_EQUAL, TOL_EXISTS = 0, 1
+
+POD_TOPOLOGY_SPREAD = 1 << 0
+POD_AFFINITY = 1 << 1
+POD_ANTI_AFFINITY = 1 << 2
+POD_HOST_PORTS = 1 << 3
+POD_VOLUMES = 1 << 4
+
+# numpy dtypes (align=True reproduces the C layout on x86-64)
+RANGE = [("begin", "<u4"), ("count", "<u4")]
+DT_REQ = np.dtype([("key", "<u4"), ("op", "<u4"), ("values", RANGE), ("min_values", "<i4")], align=True)
+DT_QTY = np.dtype([("resource", "<u4"), ("milli", "<i8")], align=True)
+DT_LABEL = np.dtype([("key", "<u4"), ("value", "<u4")], align=True)
+DT_TAINT = np.dtype([("key", "<u4"), ("value", "<u4"), ("effect", "<u4")], align=True)
+DT_TOL = np.dtype([("key", "<u4"), ("op", "<u4"), ("value", "<u4"), ("effect", "<u4")], align=True)
+DT_TERM = np.dtype([("requirements", RANGE), ("weight", "<i4")], align=True)
+DT_OFFERING = np.dtype([("requirements", RANGE), ("price", "<f8"), ("available", "<u4")], align=True)
+DT_IT = np.dtype([("name", "<u4"), ("requirements", RANGE), ("capacity", RANGE), ("overhead", RANGE),
+                  ("offerings", RANGE)], align=True)
+DT_NODEPOOL = np.dtype([("name", "<u4"), ("weight", "<i4"), ("requirements", RANGE), ("labels", RANGE),
+                        ("taints", RANGE), ("limits", RANGE), ("has_limits", "<u4"),
+                        ("daemon_requests", RANGE), ("instance_types", RANGE)], align=True)
+DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), ("node_selector", RANGE),
+                   ("required_terms", RANGE), ("preferred_terms", RANGE), ("tolerations", RANGE),
+                   ("flags", "<u4")], align=True)
+DT_NODE = np.dtype([("name", "<u4"), ("initialized", "<u4"), ("labels", RANGE), ("taints", RANGE),
+                    ("available", RANGE), ("requests", RANGE)], align=True)
+
+_P = C.c_void_p
+_U32 = C.c_uint32
+
+
+class GsProblem(C.Structure):
+    _fields_ = [
+        ("strings", C.POINTER(C.c_char_p)), ("n_strings", _U32),
+        ("value_ids", _P), ("n_value_ids", _U32),
+        ("reqs", _P), ("n_reqs", _U32),
+        ("quantities", _P), ("n_quantities", _U32),
+        ("labels", _P), ("n_labels", _U32),
+        ("taints", _P), ("n_taints", _U32),
+        ("tolerations", _P), ("n_tolerations", _U32),
+        ("terms", _P), ("n_terms", _U32),
+        ("it_refs", _P), ("n_it_refs", _U32),
+        ("offerings", _P), ("n_offerings", _U32),
+        ("instance_types", _P), ("n_instance_types", _U32),
+        ("nodepools", _P), ("n_nodepools", _U32),
+        ("pods", _P), ("n_pods", _U32),
+        ("nodes", _P), ("n_nodes", _U32),
+    ]
+
+
+class GsResult(C.Structure):
+    _fields_ = [
+        ("n_claims", _U32),
+        ("claim_nodepool", C.POINTER(C.c_uint32)),
+        ("claim_pod_offsets", C.POINTER(C.c_uint32)),
+        ("claim_pods", C.POINTER(C.c_uint32)),
+        ("claim_it_offsets", C.POINTER(C.c_uint32)),
+        ("claim_its", C.POINTER(C.c_uint32)),
+        ("claim_requirements", C.POINTER(C.c_char_p)),
+        ("n_resources", _U32),
+        ("resource_names", C.POINTER(C.c_uint32)),
+        ("claim_requests", C.POINTER(C.c_int64)),
+        ("n_nodes", _U32),
+        ("node_pod_offsets", C.POINTER(C.c_uint32)),
+        ("node_pods", C.POINTER(C.c_uint32)),
+        ("n_errors", _U32),
+        ("error_pods", C.POINTER(C.c_uint32)),
+        ("checks", C.c_uint64),
+        ("pops", C.c_uint64),
+        ("t_encode_ms", C.c_double), ("t_upload_ms", C.c_double), ("t_feas_ms", C.c_double),
+        ("t_ffd_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
+        ("t_total_ms", C.c_double),
+    ]
+
+
+class GsFeasResult(C.Structure):
+    _fields_ = [
+        ("n_pods", _U32), ("n_nodepools", _U32), ("n_its", _U32), ("words", _U32),
+        ("rows", C.POINTER(C.c_uint64)),
+        ("cheapest_it", C.POINTER(C.c_int32)),
+        ("n_feasible_offerings", C.POINTER(C.c_uint32)),
+        ("checks", C.c_uint64),
+        ("t_kernel_ms", C.c_double),
+    ]
+
+
+class GsConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_claims", _U32), ("flags", _U32)]
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+def result_to_dict(res: GsResult, problem) -> dict:
+    """Canonical, comparable form of a gs_result (copied out of library memory)."""
+    nc = res.n_claims
+    cpo = _arr(res.claim_pod_offsets, nc + 1, np.uint32)
+    cpods = _arr(res.claim_pods, int(cpo[-1]) if nc else 0, np.uint32)
+    cio = _arr(res.claim_it_offsets, nc + 1, np.uint32)
+    cits = _arr(res.claim_its, int(cio[-1]) if nc else 0, np.uint32)
+    npool = _arr(res.claim_nodepool, nc, np.uint32)
+    nr = res.n_resources
+    rnames = [problem.strings[i] for i in _arr(res.resource_names, nr, np.uint32)]
+    creq = _arr(res.claim_requests, nc * nr, np.int64).reshape(nc, nr) if nr else np.zeros((nc, 0), np.int64)
+    claims = []
+    for c in range(nc):
+        claims.append({
+            "nodepool": int(npool[c]),
+            "pods": [int(x) for x in cpods[cpo[c]:cpo[c + 1]]],
+            "its": [int(x) for x in cits[cio[c]:cio[c + 1]]],
+            "requirements": res.claim_requirements[c].decode(),
+            "requests": {rnames[k]: int(creq[c, k]) for k in range(nr) if creq[c, k] != 0},
+        })
+    nn = res.n_nodes
+    npo = _arr(res.node_pod_offsets, nn + 1, np.uint32)
+    npods = _arr(res.node_pods, int(npo[-1]) if nn else 0, np.uint32)
+    nodes = [[int(x) for x in npods[npo[i]:npo[i + 1]]] for i in range(nn)]
+    errors = [int(x) for x in _arr(res.error_pods, res.n_errors, np.uint32)]
+    return {"claims": claims, "nodes": nodes, "errors": errors}
+
+
+def feas_to_dict(res: GsFeasResult) -> dict:
+    P, T, W = res.n_pods, res.n_nodepools, res.words
+    rows = _arr(res.rows, P * T * W, np.uint64).reshape(P, T, W) if P * T * W else np.zeros((P, T, W), np.uint64)
+    cheapest = _arr(res.cheapest_it, P * T, np.int32).reshape(P, T)
+    nfo = _arr(res.n_feasible_offerings, P * T, np.uint32).reshape(P, T)
+    return {"rows": rows, "cheapest": cheapest, "n_feasible_offerings": nfo, "checks": int(res.checks)}

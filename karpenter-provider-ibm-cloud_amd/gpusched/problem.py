@@ -1,0 +1,183 @@
+"""Builder for gs_problem: the Solve inputs a Go caller would marshal.
+
+Objects mirror what karpenter-core hands to scheduling.NewScheduler/Solve:
+instance types exactly as CloudProvider.GetInstanceTypes returns them
+(reference pkg/cloudprovider/cloudprovider.go:553-583), NodePools, pending
+pods (requests = resources.RequestsForPods) and existing state nodes.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+def _op(op):
+    return abi.OPS[op] if isinstance(op, str) else int(op)
+
+
+class ProblemBuilder:
+    def __init__(self):
+        self.strings = [""]
+        self._sid = {"": 0}
+        self.value_ids = []
+        self.reqs = []
+        self.quantities = []
+        self.labels = []
+        self.taints = []
+        self.tolerations = []
+        self.terms = []
+        self.it_refs = []
+        self.offerings = []
+        self.instance_types = []
+        self.nodepools = []
+        self.pods = []
+        self.nodes = []
+
+    # ------------------------------------------------------------ primitives
+    def s(self, x: str) -> int:
+        i = self._sid.get(x)
+        if i is None:
+            i = len(self.strings)
+            self.strings.append(x)
+            self._sid[x] = i
+        return i
+
+    def _reqs(self, reqs):
+        """reqs: iterable of (key, op, values[, minValues])"""
+        b = len(self.reqs)
+        for r in reqs:
+            key, op, values = r[0], r[1], r[2]
+            mv = r[3] if len(r) > 3 and r[3] is not None else -1
+            vb = len(self.value_ids)
+            self.value_ids.extend(self.s(v) for v in values)
+            self.reqs.append((self.s(key), _op(op), (vb, len(values)), mv))
+        return (b, len(self.reqs) - b)
+
+    def _qty(self, res):
+        b = len(self.quantities)
+        for k, v in res.items():
+            self.quantities.append((self.s(k), int(v)))
+        return (b, len(self.quantities) - b)
+
+    def _labels(self, labels):
+        b = len(self.labels)
+        for k, v in labels.items():
+            self.labels.append((self.s(k), self.s(v)))
+        return (b, len(self.labels) - b)
+
+    def _taints(self, taints):
+        b = len(self.taints)
+        for t in taints:
+            key, value, effect = t
+            self.taints.append((self.s(key), self.s(value), self.s(effect)))
+        return (b, len(self.taints) - b)
+
+    def _tols(self, tols):
+        b = len(self.tolerations)
+        for t in tols:
+            key, op, value, effect = t
+            opi = abi.TOL_EXISTS if op == "Exists" else abi.TOL_EQUAL
+            self.tolerations.append((self.s(key), opi, self.s(value), self.s(effect)))
+        return (b, len(self.tolerations) - b)
+
+    def _terms(self, terms):
+        b = len(self.terms)
+        for weight, reqs in terms:
+            self.terms.append((self._reqs(reqs), int(weight)))
+        return (b, len(self.terms) - b)
+
+    # --------------------------------------------------------------- objects
+    def add_instance_type(self, name, requirements, capacity, overhead, offerings):
+        """offerings: list of (zone, capacity_type, price, available)"""
+        ob = len(self.offerings)
+        for zone, ct, price, avail in offerings:
+            rq = self._reqs([("topology.kubernetes.io/zone", "In", [zone]),
+                             ("karpenter.sh/capacity-type", "In", [ct])])
+            self.offerings.append((rq, float(price), 1 if avail else 0))
+        idx = len(self.instance_types)
+        self.instance_types.append((self.s(name), self._reqs(requirements), self._qty(capacity),
+                                    self._qty(overhead), (ob, len(offerings))))
+        return idx
+
+    def add_nodepool(self, name, weight=0, requirements=(), labels=None, taints=(), limits=None,
+                     daemon=None, instance_types=None):
+        if instance_types is None:
+            instance_types = range(len(self.instance_types))
+        rb = len(self.it_refs)
+        self.it_refs.extend(int(i) for i in instance_types)
+        self.nodepools.append((self.s(name), int(weight), self._reqs(requirements), self._labels(labels or {}),
+                               self._taints(taints), self._qty(limits or {}), 1 if limits is not None else 0,
+                               self._qty(daemon or {}), (rb, len(self.it_refs) - rb)))
+        return len(self.nodepools) - 1
+
+    def add_pod(self, uid, creation_ns, requests, node_selector=None, required_terms=(), preferred_terms=(),
+                tolerations=(), flags=0):
+        """required_terms: list of reqs lists; preferred_terms: list of (weight, reqs)"""
+        self.pods.append((self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
+                          self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
+                          self._tols(tolerations), int(flags)))
+        return len(self.pods) - 1
+
+    def add_node(self, name, labels, available, requests=None, taints=(), initialized=True):
+        self.nodes.append((self.s(name), 1 if initialized else 0, self._labels(labels), self._taints(taints),
+                           self._qty(available), self._qty(requests or {})))
+        return len(self.nodes) - 1
+
+    def build(self):
+        return Problem(self)
+
+
+def _np(rows, dtype):
+    a = np.zeros(len(rows), dtype=dtype)
+    if rows:
+        a[:] = rows
+    return a
+
+
+class Problem:
+    """Owns the numpy arrays backing a gs_problem struct."""
+
+    def __init__(self, b: ProblemBuilder):
+        self.strings = list(b.strings)
+        self._bytes = [x.encode() for x in self.strings]
+        self._cstrs = (C.c_char_p * len(self._bytes))(*self._bytes)
+        self.value_ids = np.asarray(b.value_ids, dtype=np.uint32)
+        self.reqs = _np(b.reqs, abi.DT_REQ)
+        self.quantities = _np(b.quantities, abi.DT_QTY)
+        self.labels = _np(b.labels, abi.DT_LABEL)
+        self.taints = _np(b.taints, abi.DT_TAINT)
+        self.tolerations = _np(b.tolerations, abi.DT_TOL)
+        self.terms = _np(b.terms, abi.DT_TERM)
+        self.it_refs = np.asarray(b.it_refs, dtype=np.uint32)
+        self.offerings = _np(b.offerings, abi.DT_OFFERING)
+        self.instance_types = _np(b.instance_types, abi.DT_IT)
+        self.nodepools = _np(b.nodepools, abi.DT_NODEPOOL)
+        self.pods = _np(b.pods, abi.DT_POD)
+        self.nodes = _np(b.nodes, abi.DT_NODE)
+        self.struct = abi.GsProblem()
+        st = self.struct
+        st.strings = self._cstrs
+        st.n_strings = len(self._bytes)
+        for name in ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
+                     "offerings", "instance_types", "nodepools", "pods", "nodes"):
+            arr = getattr(self, name)
+            setattr(st, name, arr.ctypes.data if len(arr) else None)
+            setattr(st, "n_" + name, len(arr))
+
+    @property
+    def n_pods(self):
+        return len(self.pods)
+
+    @property
+    def n_offerings_per_pool(self):
+        """offerings reachable per NodePool (for checks accounting)"""
+        out = []
+        for np_ in self.nodepools:
+            b, c = np_["instance_types"]
+            its = self.it_refs[b:b + c]
+            out.append(int(self.instance_types["offerings"]["count"][its].sum()))
+        return out
+
+    def checks(self):
+        return self.n_pods * sum(self.n_offerings_per_pool)

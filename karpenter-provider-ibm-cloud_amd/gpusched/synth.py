@@ -1,0 +1,338 @@
+"""Deterministic synthetic Solve inputs for the BASELINE configs.
+
+C1  500 pods, the 8 fake IBM profiles (reference pkg/fake/zz_generated_ibm_test_data.go:27-243),
+    us-south-1..3, on-demand only, 1 NodePool like examples/nodepool.yaml
+C2  10k pods x ~200 synthetic profiles x 3 zones x {on-demand, spot}
+CM  100k pods x the C2 catalog (BASELINE metric workload)
+C3  50k pods, 4 weighted NodePools, taints/tolerations, node affinity (In/NotIn),
+    preferred affinity (topology spread is not supported yet and is omitted)
+C5  200k pods x 2,000 synthetic ITs x 6 zones x 2 capacity types
+random_problem(seed): small adversarial problems exercising the full
+    requirement algebra (complements, Gt/Lt, custom keys), limits, relaxation,
+    existing nodes.
+"""
+import uuid
+
+import numpy as np
+
+from . import catalog as cat
+from .problem import ProblemBuilder
+
+GI = 1 << 30
+MI = 1 << 20
+
+FAKE_PROFILES = [  # name, vcpu, memory GiB, gpu (pkg/fake/zz_generated_ibm_test_data.go:27-243)
+    ("bx2-2x8", 2, 8, None), ("bx2-4x16", 4, 16, None), ("bx2-8x32", 8, 32, None),
+    ("cx2-2x4", 2, 4, None), ("cx2-4x8", 4, 8, None),
+    ("mx2-2x16", 2, 16, None), ("mx2-4x32", 4, 32, None),
+    ("gx2-8x64x1v100", 8, 64, 1),
+]
+FAKE_ZONES = ["us-south-1", "us-south-2", "us-south-3"]  # zz_generated_ibm_test_data.go:286-314
+
+FAMILIES = ["bx2", "bx3d", "cx2", "cx3d", "mx2", "mx3d", "ux2d", "vx2d", "ox2", "gx2", "gx3"]  # webhook :333
+MEM_RATIO = {"b": 4, "c": 2, "m": 8, "o": 8, "v": 14, "u": 28, "g": 8}
+
+CPU_CHOICES = np.array([100, 250, 500, 1000, 2000], dtype=np.int64)
+CPU_W = np.array([30, 30, 20, 15, 5], dtype=np.float64)
+MEM_CHOICES = np.array([128 * MI, 256 * MI, 512 * MI, 1 * GI, 2 * GI, 4 * GI], dtype=np.int64) * 1000
+
+
+def price_table(profiles):
+    """committed synthetic price table: 0.0475/vCPU + 0.006/GiB + 1.25/GPU (4 dp)"""
+    out = {}
+    for name, v, m, g in profiles:
+        out[name] = round(0.0475 * v + 0.006 * m + 1.25 * (g or 0), 4)
+    return out
+
+
+def c2_profiles(n_target=200):
+    sizes = [2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 144, 160, 176, 192, 208, 224]
+    out = []
+    for fam in FAMILIES:
+        ratio = MEM_RATIO[fam[0]]
+        for v in sizes:
+            m = v * ratio
+            if fam.startswith("g"):
+                g = max(1, v // 16)
+                out.append((f"{fam}-{v}x{m}x{g}v100", v, m, g))
+            else:
+                out.append((f"{fam}-{v}x{m}", v, m, None))
+            if len(out) >= n_target:
+                return out
+    return out
+
+
+def c5_profiles(n_target=2000):
+    fams = []
+    for base in FAMILIES:
+        for suf in ["", "a", "b", "c", "e", "f", "h", "i", "k", "l", "n", "p", "q", "r", "s", "t", "w", "y"]:
+            fams.append(base + suf)
+    sizes = [2, 4, 6, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64, 72, 80, 96, 112, 128, 144, 160, 176]
+    out = []
+    for fam in fams:
+        ratio = MEM_RATIO[fam[0]]
+        for v in sizes:
+            m = v * ratio
+            if fam.startswith("g"):
+                g = max(1, v // 16)
+                out.append((f"{fam}-{v}x{m}x{g}v100", v, m, g))
+            else:
+                out.append((f"{fam}-{v}x{m}", v, m, None))
+            if len(out) >= n_target:
+                return out
+    return out
+
+
+def build_catalog(b: ProblemBuilder, profiles, zones, spot, prices, rng=None, unavailable_frac=0.0,
+                  missing_price=()):
+    unavailable = set()
+    if rng is not None and unavailable_frac > 0:
+        for name, *_ in profiles:
+            for z in zones:
+                for ct in (["on-demand", "spot"] if spot else ["on-demand"]):
+                    if rng.random() < unavailable_frac:
+                        unavailable.add(f"{name}:{z}:{ct}")
+    ac = ("enum", ["standard", "spot"]) if spot else None
+    profs = [cat.Profile(name, v, m, "amd64", g, ac) for name, v, m, g in profiles]
+
+    def price_of(name, zone):
+        if name in missing_price:
+            return None
+        return prices.get(name)
+
+    its = cat.list_instance_types(profs, zones, price_of, unavailable=unavailable)
+    for it in its:
+        b.add_instance_type(it.name, it.requirements, it.capacity, it.overhead, it.offerings)
+    return its
+
+
+def _uid(rng):
+    return str(uuid.UUID(bytes=rng.bytes(16), version=4))
+
+
+def _pods_basic(b, rng, n, its, gpu_frac=0.0, selector_frac=0.0):
+    cpu = rng.choice(CPU_CHOICES, size=n, p=CPU_W / CPU_W.sum())
+    mem = rng.choice(MEM_CHOICES, size=n)
+    ts = 1_700_000_000_000_000_000 + rng.integers(0, 8, size=n) * 1_000_000_000
+    fams = sorted({cat.instance_family(it.name) for it in its})
+    sizes = sorted({cat.instance_size(it.name) for it in its})
+    for i in range(n):
+        req = {"cpu": int(cpu[i]), "memory": int(mem[i]), "pods": 1000}
+        if gpu_frac and rng.random() < gpu_frac:
+            req["nvidia.com/gpu"] = 1000
+        sel = {}
+        if selector_frac and rng.random() < selector_frac:
+            k = rng.integers(0, 3)
+            if k == 0:
+                sel["kubernetes.io/arch"] = "amd64"
+            elif k == 1:
+                sel["karpenter-ibm.sh/instance-family"] = fams[rng.integers(0, len(fams))]
+            else:
+                sel["karpenter-ibm.sh/instance-size"] = sizes[rng.integers(0, len(sizes))]
+        b.add_pod(_uid(rng), int(ts[i]), req, node_selector=sel)
+
+
+def make_c1(n_pods=500, seed=0x5EED0001):
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    prices = price_table(FAKE_PROFILES)
+    prices.pop("gx2-8x64x1v100")  # no price -> 0.0 (instancetype.go:753)
+    its = build_catalog(b, FAKE_PROFILES, FAKE_ZONES, spot=False, prices=prices)
+    b.add_nodepool("default", weight=100,
+                   requirements=[("kubernetes.io/arch", "In", ["amd64"]), ("kubernetes.io/os", "In", ["linux"])])
+    _pods_basic(b, rng, n_pods, its)
+    return b.build()
+
+
+def make_c2(n_pods=10_000, seed=0x5EED0002, n_its=200):
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c2_profiles(n_its)
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng,
+                        unavailable_frac=0.02)
+    b.add_nodepool("default", weight=0,
+                   requirements=[("kubernetes.io/arch", "In", ["amd64"]), ("kubernetes.io/os", "In", ["linux"])],
+                   daemon={"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000})
+    _pods_basic(b, rng, n_pods, its, gpu_frac=0.01, selector_frac=0.10)
+    return b.build()
+
+
+def make_cm(n_pods=100_000, seed=0x5EED0006):
+    return make_c2(n_pods=n_pods, seed=seed)
+
+
+def make_c5(n_pods=200_000, seed=0x5EED0005, n_its=2000):
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c5_profiles(n_its)
+    zones = [f"us-south-{i}" for i in range(1, 7)]
+    its = build_catalog(b, profs, zones, spot=True, prices=price_table(profs), rng=rng, unavailable_frac=0.02)
+    b.add_nodepool("default", weight=0, requirements=[("kubernetes.io/arch", "In", ["amd64"])],
+                   daemon={"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000})
+    _pods_basic(b, rng, n_pods, its, gpu_frac=0.01, selector_frac=0.10)
+    return b.build()
+
+
+def make_c3(n_pods=50_000, seed=0x5EED0003):
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c2_profiles(200)
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng,
+                        unavailable_frac=0.02)
+    fams = sorted({cat.instance_family(it.name) for it in its})
+    daemon = {"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000}
+    b.add_nodepool("gpu", weight=100, requirements=[("karpenter-ibm.sh/instance-family", "In", ["gx2", "gx3"])],
+                   taints=[("nvidia.com/gpu", "true", "NoSchedule")], daemon=daemon)
+    b.add_nodepool("spot", weight=50, requirements=[("karpenter.sh/capacity-type", "In", ["spot"]),
+                                                    ("karpenter-ibm.sh/instance-family", "NotIn", ["gx2", "gx3"])],
+                   taints=[("spot", "true", "NoSchedule")], daemon=daemon)
+    b.add_nodepool("memory", weight=10, requirements=[("karpenter-ibm.sh/instance-family", "In",
+                                                       ["mx2", "mx3d", "ux2d", "vx2d", "ox2"])],
+                   labels={"tier": "memory"}, daemon=daemon, limits={"cpu": 4000 * 1000})
+    b.add_nodepool("default", weight=0, requirements=[("karpenter.sh/capacity-type", "In", ["on-demand"])],
+                   daemon=daemon)
+    cpu = rng.choice(CPU_CHOICES, size=n_pods, p=CPU_W / CPU_W.sum())
+    mem = rng.choice(MEM_CHOICES, size=n_pods)
+    ts = 1_700_000_000_000_000_000 + rng.integers(0, 8, size=n_pods) * 1_000_000_000
+    for i in range(n_pods):
+        req = {"cpu": int(cpu[i]), "memory": int(mem[i]), "pods": 1000}
+        tols, required, preferred, sel = [], [], [], {}
+        u = rng.random()
+        if u < 0.02:
+            req["nvidia.com/gpu"] = 1000
+            tols.append(("nvidia.com/gpu", "Exists", "", "NoSchedule"))
+        if rng.random() < 0.30:
+            tols.append(("spot", "Equal", "true", "NoSchedule"))
+        if rng.random() < 0.40:
+            z = FAKE_ZONES[rng.integers(0, 3)]
+            f = fams[rng.integers(0, len(fams))]
+            kind = rng.integers(0, 3)
+            if kind == 0:
+                required.append([("topology.kubernetes.io/zone", "In", [z])])
+            elif kind == 1:
+                required.append([("karpenter-ibm.sh/instance-family", "NotIn", [f])])
+            else:
+                required.append([("topology.kubernetes.io/zone", "NotIn", [z]),
+                                 ("karpenter-ibm.sh/instance-family", "In", [f, fams[rng.integers(0, len(fams))]])])
+                required.append([("topology.kubernetes.io/zone", "In", [z])])
+        if rng.random() < 0.10:
+            preferred.append((int(rng.integers(1, 100)),
+                              [("karpenter.sh/capacity-type", "In", ["spot"])]))
+            if rng.random() < 0.5:
+                preferred.append((int(rng.integers(1, 100)), [("tier", "In", ["memory"])]))
+        if rng.random() < 0.03:
+            sel["tier"] = "memory"
+        b.add_pod(_uid(rng), int(ts[i]), req, node_selector=sel, required_terms=required,
+                  preferred_terms=preferred, tolerations=tols)
+    return b.build()
+
+
+CONFIGS = {"C1": make_c1, "C2": make_c2, "CM": make_cm, "C3": make_c3, "C5": make_c5}
+
+
+# ---------------------------------------------------------------- fuzzing
+_KEYS_IT = ["node.kubernetes.io/instance-type", "kubernetes.io/arch", "karpenter-ibm.sh/instance-family",
+            "karpenter-ibm.sh/instance-size"]
+_KEYS_OFF = ["topology.kubernetes.io/zone", "karpenter.sh/capacity-type"]
+_KEYS_FREE = ["kubernetes.io/os", "karpenter.sh/nodepool", "team", "karpenter-ibm.sh/instance-cpu",
+              "kubernetes.io/hostname", "tier"]
+
+
+def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
+    """small adversarial problem over the whole supported feature set"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
+    fams = ["bx2", "cx2", "mx2"]
+    profs = []
+    for i in range(int(rng.integers(2, 9))):
+        f = fams[rng.integers(0, 3)]
+        v = int(rng.choice([2, 4, 8, 16]))
+        m = v * MEM_RATIO[f[0]] if rng.random() < 0.8 else 2
+        g = 1 if rng.random() < 0.15 else None
+        profs.append((f"{f}-{v}x{m}" + (f"x{i}" if rng.random() < 0.3 else ""), v, m, g))
+    seen = set()
+    profs = [p for p in profs if not (p[0] in seen or seen.add(p[0]))]
+    prices = {p[0]: float(rng.choice([0.1, 0.2, 0.2, 0.4, 0.8])) for p in profs}
+    spot = bool(rng.random() < 0.6)
+    its = build_catalog(b, profs, zones, spot=spot, prices=prices, rng=rng, unavailable_frac=0.15,
+                        missing_price={profs[0][0]} if rng.random() < 0.2 else ())
+    names = [it.name for it in its]
+    vocab = {
+        "node.kubernetes.io/instance-type": names + ["nope"],
+        "kubernetes.io/arch": ["amd64", "arm64"],
+        "karpenter-ibm.sh/instance-family": fams + ["gx2"],
+        "karpenter-ibm.sh/instance-size": sorted({cat.instance_size(n) for n in names}),
+        "topology.kubernetes.io/zone": zones + ["z9"],
+        "karpenter.sh/capacity-type": ["on-demand", "spot"],
+        "kubernetes.io/os": ["linux", "windows"],
+        "karpenter.sh/nodepool": ["np0", "np1", "np2"],
+        "team": ["a", "b", "c"],
+        "karpenter-ibm.sh/instance-cpu": ["2", "4", "8", "x"],
+        "kubernetes.io/hostname": ["host-a", "host-b"],
+        "tier": ["1", "2", "3"],
+    }
+    all_keys = _KEYS_IT + _KEYS_OFF + _KEYS_FREE
+
+    def rand_req(keys=all_keys):
+        k = keys[rng.integers(0, len(keys))]
+        vals = vocab[k]
+        op = rng.choice(["In", "In", "In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"],
+                        p=[0.3, 0.1, 0.1, 0.2, 0.1, 0.05, 0.075, 0.075])
+        if op in ("Gt", "Lt"):
+            return (k, op, [str(int(rng.integers(0, 10)))])
+        if op in ("Exists", "DoesNotExist"):
+            return (k, op, [])
+        n = int(rng.integers(1, min(3, len(vals)) + 1))
+        return (k, op, list(rng.choice(vals, size=n, replace=False)))
+
+    effects = ["NoSchedule", "PreferNoSchedule", "NoExecute"]
+    n_np = int(rng.integers(1, 4))
+    for j in range(n_np):
+        reqs = [rand_req(_KEYS_IT + _KEYS_OFF + ["kubernetes.io/os", "team"]) for _ in range(int(rng.integers(0, 3)))]
+        labels = {"team": vocab["team"][rng.integers(0, 3)]} if rng.random() < 0.4 else {}
+        taints = [("dedicated", str(rng.choice(["x", "y"])), str(rng.choice(effects)))] if rng.random() < 0.4 else []
+        limits = None
+        if with_limits and rng.random() < 0.3:
+            limits = {"cpu": int(rng.choice([8, 16, 32, 64])) * 1000}
+        daemon = {"cpu": int(rng.choice([0, 100, 500])), "pods": int(rng.integers(0, 3)) * 1000}
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10, 10, 50])), requirements=reqs, labels=labels,
+                       taints=taints, limits=limits, daemon=daemon)
+    if with_nodes and rng.random() < 0.5:
+        for k in range(int(rng.integers(1, 4))):
+            it = its[rng.integers(0, len(its))]
+            labels = {r[0]: r[2][0] for r in it.requirements}
+            labels["topology.kubernetes.io/zone"] = zones[rng.integers(0, len(zones))]
+            labels["karpenter.sh/capacity-type"] = "on-demand"
+            labels["kubernetes.io/hostname"] = f"node-{k}"
+            if rng.random() < 0.5:
+                labels["team"] = vocab["team"][rng.integers(0, 3)]
+            avail = {"cpu": int(rng.choice([500, 1000, 4000])), "memory": int(rng.choice([1, 4, 16])) * GI * 1000,
+                     "pods": 10_000}
+            taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.3 else []
+            b.add_node(f"node-{k}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.8))
+    n = int(n_pods if n_pods is not None else rng.integers(1, 40))
+    for i in range(n):
+        req = {"cpu": int(rng.choice([100, 500, 1000, 3000, 9000])),
+               "memory": int(rng.choice([128 * MI, GI, 4 * GI, 30 * GI])) * 1000, "pods": 1000}
+        if rng.random() < 0.1:
+            req["nvidia.com/gpu"] = 1000
+        if rng.random() < 0.05:
+            req["example.com/widget"] = 1000
+        sel = {}
+        if rng.random() < 0.2:
+            k = all_keys[rng.integers(0, len(all_keys))]
+            sel[k] = str(rng.choice(vocab[k]))
+        required = [[rand_req() for _ in range(int(rng.integers(1, 3)))] for _ in range(int(rng.integers(0, 3)))] \
+            if rng.random() < 0.4 else []
+        preferred = [(int(rng.integers(1, 4)), [rand_req()]) for _ in range(int(rng.integers(0, 3)))] \
+            if rng.random() < 0.3 else []
+        tols = []
+        if rng.random() < 0.4:
+            tols.append(("dedicated", str(rng.choice(["Equal", "Exists"])), str(rng.choice(["x", "y"])),
+                         str(rng.choice(effects + [""]))))
+        if rng.random() < 0.1:
+            tols.append(("", "Exists", "", ""))
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 4)) * 1_000_000_000, req,
+                  node_selector=sel, required_terms=required, preferred_terms=preferred, tolerations=tols)
+    return b.build()

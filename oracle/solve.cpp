@@ -1,0 +1,995 @@
+// solve.cpp — TEST INFRASTRUCTURE ONLY (parity oracle; see oracle.h).
+//
+// Literal CPU restatement of sigs.k8s.io/karpenter@v1.13.0 scheduling as the
+// IBM provider drives it.  Representation is deliberately naive (string
+// sets, string-keyed maps, copies on every CanAdd) so that it shares nothing
+// with the product's bitset encoding.  Every <U> item is upstream behaviour
+// restated from memory (the module is not in the container): "parity
+// unpinned" for those.  Reference call sites are cited where they exist.
+#include "oracle.h"
+#include "gosort.h"
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdio>
+#include <memory>
+#include <cstring>
+#include <map>
+#include <optional>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using std::optional;
+using std::string;
+using std::vector;
+
+const char* kHostname = "kubernetes.io/hostname";
+const char* kZone = "topology.kubernetes.io/zone";
+const char* kCapacityType = "karpenter.sh/capacity-type";
+const char* kNodePool = "karpenter.sh/nodepool";
+const char* kEffectPreferNoSchedule = "PreferNoSchedule";
+
+// <U> karpv1.WellKnownLabels + the 4 IBM keys inserted by
+// reference pkg/apis/v1alpha1/labels.go:37-45.
+const std::set<string>& well_known() {
+  static const std::set<string> s = {
+      "karpenter.sh/nodepool",
+      "topology.kubernetes.io/zone",
+      "topology.kubernetes.io/region",
+      "node.kubernetes.io/instance-type",
+      "kubernetes.io/arch",
+      "kubernetes.io/os",
+      "karpenter.sh/capacity-type",
+      "node.kubernetes.io/windows-build",
+      "karpenter-ibm.sh/instance-size",
+      "karpenter-ibm.sh/instance-family",
+      "karpenter-ibm.sh/instance-cpu",
+      "karpenter-ibm.sh/instance-memory",
+  };
+  return s;
+}
+
+// <U> karpv1.NormalizedLabels
+string normalize_key(const string& k) {
+  static const std::map<string, string> m = {
+      {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
+      {"failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region"},
+      {"beta.kubernetes.io/arch", "kubernetes.io/arch"},
+      {"beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type"},
+      {"beta.kubernetes.io/os", "kubernetes.io/os"},
+  };
+  auto it = m.find(k);
+  return it == m.end() ? k : it->second;
+}
+
+// Go strconv.Atoi (base 10, optional sign, int64 range)
+bool go_atoi(const string& s, int64_t* out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  __int128 v = 0;
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (s[i] - '0');
+    if (v > (__int128)INT64_MAX + 1) return false;
+  }
+  if (neg) v = -v;
+  if (v > INT64_MAX || v < INT64_MIN) return false;
+  *out = (int64_t)v;
+  return true;
+}
+
+struct Status {
+  gs_status code = GS_OK;
+  string msg;
+};
+
+struct Unsupported {
+  gs_status code;
+  string msg;
+};
+
+// ---------------------------------------------------------------- Requirement
+// <U> pkg/scheduling/requirement.go
+struct Req {
+  string key;
+  bool complement = true;
+  std::set<string> values;
+  optional<int64_t> gt, lt;
+  optional<int64_t> min_values;
+
+  int64_t len() const {
+    return complement ? INT64_MAX - (int64_t)values.size() : (int64_t)values.size();
+  }
+  int op() const {
+    if (complement) return len() < INT64_MAX ? GS_OP_NOTIN : GS_OP_EXISTS;
+    return len() > 0 ? GS_OP_IN : GS_OP_DOES_NOT_EXIST;
+  }
+  static bool within(const string& v, const optional<int64_t>& gt, const optional<int64_t>& lt) {
+    if (!gt && !lt) return true;
+    int64_t x;
+    if (!go_atoi(v, &x)) return false;
+    if (gt && *gt >= x) return false;
+    if (lt && *lt <= x) return false;
+    return true;
+  }
+  bool has(const string& v) const {
+    if (complement) return !values.count(v) && within(v, gt, lt);
+    return values.count(v) && within(v, gt, lt);
+  }
+  Req intersection(const Req& o) const {
+    bool comp = complement && o.complement;
+    optional<int64_t> g = gt, l = lt, mv = min_values;
+    if (o.gt && (!g || *o.gt > *g)) g = o.gt;
+    if (o.lt && (!l || *o.lt < *l)) l = o.lt;
+    if (o.min_values && (!mv || *o.min_values > *mv)) mv = o.min_values;
+    if (g && l && *g >= *l) {
+      Req r;
+      r.key = key;
+      r.complement = false;  // DoesNotExist
+      r.min_values = mv;
+      return r;
+    }
+    std::set<string> vals;
+    if (complement && o.complement) {
+      vals = values;
+      vals.insert(o.values.begin(), o.values.end());
+    } else if (complement && !o.complement) {
+      for (auto& v : o.values)
+        if (!values.count(v)) vals.insert(v);
+    } else if (!complement && o.complement) {
+      for (auto& v : values)
+        if (!o.values.count(v)) vals.insert(v);
+    } else {
+      for (auto& v : values)
+        if (o.values.count(v)) vals.insert(v);
+    }
+    for (auto it = vals.begin(); it != vals.end();) {
+      if (!within(*it, g, l)) it = vals.erase(it);
+      else ++it;
+    }
+    if (!comp) {
+      g.reset();
+      l.reset();
+    }
+    Req r;
+    r.key = key;
+    r.complement = comp;
+    r.values = std::move(vals);
+    r.gt = g;
+    r.lt = l;
+    r.min_values = mv;
+    return r;
+  }
+};
+
+Req make_req(const string& key_in, int op, const vector<string>& values, optional<int64_t> mv) {
+  Req r;
+  r.key = normalize_key(key_in);
+  r.complement = true;
+  r.min_values = mv;
+  if (op == GS_OP_IN || op == GS_OP_DOES_NOT_EXIST) r.complement = false;
+  if (op == GS_OP_IN || op == GS_OP_NOTIN) r.values.insert(values.begin(), values.end());
+  if (op == GS_OP_GT || op == GS_OP_LT) {
+    int64_t v = 0;
+    if (values.empty() || !go_atoi(values[0], &v)) throw Unsupported{GS_E_INVALID, "Gt/Lt value is not an integer"};
+    if (op == GS_OP_GT) r.gt = v;
+    else r.lt = v;
+  }
+  return r;
+}
+
+// <U> pkg/scheduling/requirements.go
+struct Reqs {
+  std::map<string, Req> m;
+
+  void add(const Req& r) {
+    auto it = m.find(r.key);
+    if (it != m.end()) {
+      Req x = r.intersection(it->second);
+      it->second = std::move(x);
+    } else {
+      m.emplace(r.key, r);
+    }
+  }
+  void add_all(const Reqs& o) {
+    for (auto& kv : o.m) add(kv.second);
+  }
+  bool has_key(const string& k) const { return m.count(k) != 0; }
+  Req get(const string& k) const {
+    auto it = m.find(k);
+    if (it != m.end()) return it->second;
+    return make_req(k, GS_OP_EXISTS, {}, std::nullopt);
+  }
+  // Intersects: for shared keys there must be some value, unless both
+  // operators are in {NotIn, DoesNotExist}
+  bool intersects(const Reqs& in) const {
+    for (auto& kv : m) {
+      auto it = in.m.find(kv.first);
+      if (it == in.m.end()) continue;
+      const Req& existing = kv.second;
+      const Req& incoming = it->second;
+      if (existing.intersection(incoming).len() == 0) {
+        int io = incoming.op(), eo = existing.op();
+        if ((io == GS_OP_NOTIN || io == GS_OP_DOES_NOT_EXIST) && (eo == GS_OP_NOTIN || eo == GS_OP_DOES_NOT_EXIST))
+          continue;
+        return false;
+      }
+    }
+    return true;
+  }
+  // Compatible(incoming, AllowUndefined = allow_wellknown ? WellKnownLabels : {})
+  bool compatible(const Reqs& in, bool allow_wellknown) const {
+    for (auto& kv : in.m) {
+      if (allow_wellknown && well_known().count(kv.first)) continue;
+      int o = kv.second.op();
+      if (has_key(kv.first) || o == GS_OP_NOTIN || o == GS_OP_DOES_NOT_EXIST) continue;
+      return false;
+    }
+    return intersects(in);
+  }
+};
+
+// canonical text: keys ascending, "key|Op|v1,v2|gt|lt|minValues"
+string canonical(const Reqs& r) {
+  static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+  string s;
+  for (auto& kv : r.m) {
+    const Req& q = kv.second;
+    if (!s.empty()) s += '\n';
+    s += kv.first;
+    s += '|';
+    s += opn[q.op()];
+    s += '|';
+    bool first = true;
+    for (auto& v : q.values) {
+      if (!first) s += ',';
+      s += v;
+      first = false;
+    }
+    s += '|';
+    s += q.gt ? std::to_string(*q.gt) : "-";
+    s += '|';
+    s += q.lt ? std::to_string(*q.lt) : "-";
+    s += '|';
+    s += q.min_values ? std::to_string(*q.min_values) : "-";
+  }
+  return s;
+}
+
+// ------------------------------------------------------------------ Resources
+// <U> pkg/utils/resources
+using Res = std::map<string, int64_t>;
+
+Res merge(const Res& a, const Res& b) {
+  Res r = a;
+  for (auto& kv : b) r[kv.first] += kv.second;
+  return r;
+}
+bool fits(const Res& cand, const Res& total) {
+  for (auto& kv : total)
+    if (kv.second < 0) return false;
+  for (auto& kv : cand) {
+    auto it = total.find(kv.first);
+    int64_t t = it == total.end() ? 0 : it->second;
+    if (kv.second > t) return false;
+  }
+  return true;
+}
+Res subtract(const Res& a, const Res& b) {
+  Res r = a;
+  for (auto& kv : a) {
+    auto it = b.find(kv.first);
+    if (it != b.end()) r[kv.first] = kv.second - it->second;
+  }
+  return r;
+}
+int64_t res_get(const Res& r, const string& k) {
+  auto it = r.find(k);
+  return it == r.end() ? 0 : it->second;
+}
+
+// --------------------------------------------------------------- Taints
+struct Taint {
+  string key, value, effect;
+};
+struct Toleration {
+  string key, value, effect;
+  int op;
+};
+// corev1 Toleration.ToleratesTaint
+bool tolerates_taint(const Toleration& t, const Taint& taint) {
+  if (!t.effect.empty() && t.effect != taint.effect) return false;
+  if (!t.key.empty() && t.key != taint.key) return false;
+  if (t.op == GS_TOL_EQUAL) return t.value == taint.value;
+  if (t.op == GS_TOL_EXISTS) return true;
+  return false;
+}
+// <U> scheduling.Taints.ToleratesPod: every taint tolerated by some toleration
+bool tolerates_all(const vector<Taint>& taints, const vector<Toleration>& tols) {
+  for (auto& tn : taints) {
+    bool ok = false;
+    for (auto& t : tols) ok = ok || tolerates_taint(t, tn);
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// ----------------------------------------------------------- model objects
+struct Offering {
+  Reqs reqs;
+  double price;
+  bool available;
+};
+struct InstanceType {
+  uint32_t index;
+  string name;
+  Reqs reqs;
+  Res capacity, overhead, allocatable;
+  vector<Offering> offerings;
+};
+
+struct Term {
+  vector<Req> reqs;  // raw NodeSelectorRequirements
+  int32_t weight;
+};
+
+struct Pod {
+  uint32_t index;
+  string uid;
+  int64_t ts;
+  Res requests;
+  std::map<string, string> node_selector;
+  vector<Term> required;   // mutable (relaxation)
+  vector<Term> preferred;  // mutable (relaxation)
+  vector<Toleration> tolerations;
+  Reqs reqs;  // cached PodData.Requirements
+};
+
+struct Template {
+  uint32_t np_index;
+  string name;
+  int32_t weight;
+  Reqs reqs;
+  vector<Taint> taints;
+  vector<const InstanceType*> options;
+  Res daemon;
+  bool has_limits;
+};
+
+struct NodeClaim {
+  const Template* tmpl;
+  Reqs reqs;
+  vector<const InstanceType*> options;
+  Res requests;
+  vector<const Pod*> pods;
+};
+
+struct ExistingNode {
+  uint32_t index;
+  string name;
+  bool initialized;
+  Reqs reqs;
+  vector<Taint> taints;
+  Res available, requests;
+  vector<const Pod*> pods;
+};
+
+// <U> NewPodRequirements: nodeSelector + heaviest preferred term (sort.Slice
+// by weight desc, mutating the pod's slice) + first required term.
+void update_pod_reqs(Pod& p) {
+  Reqs r;
+  for (auto& kv : p.node_selector) r.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
+  if (!p.preferred.empty()) {
+    struct D {
+      vector<Term>& t;
+      bool less(int i, int j) { return t[i].weight > t[j].weight; }
+      void swap(int i, int j) { std::swap(t[i], t[j]); }
+    } d{p.preferred};
+    gosort::slice(d, (int)p.preferred.size());
+    for (auto& q : p.preferred[0].reqs) r.add(q);
+  }
+  if (!p.required.empty()) {
+    for (auto& q : p.required[0].reqs) r.add(q);
+  }
+  p.reqs = std::move(r);
+}
+
+// <U> filterInstanceTypesByRequirements (no short-circuit across ITs)
+vector<const InstanceType*> filter_its(const vector<const InstanceType*>& its, const Reqs& reqs, const Res& requests) {
+  vector<const InstanceType*> out;
+  for (auto* it : its) {
+    bool compat = it->reqs.intersects(reqs);
+    bool f = fits(requests, it->allocatable);
+    bool has_off = false;
+    for (auto& of : it->offerings) {
+      if (of.available && reqs.compatible(of.reqs, true)) {
+        has_off = true;
+        break;
+      }
+    }
+    if (compat && f && has_off) out.push_back(it);
+  }
+  return out;
+}
+
+// <U> cloudprovider.InstanceTypes.OrderByPrice + Truncate(60)
+vector<const InstanceType*> order_by_price(vector<const InstanceType*> its, const Reqs& reqs, size_t max_items) {
+  auto cheapest = [&](const InstanceType* it) {
+    double best = 0;
+    bool any = false;
+    for (auto& of : it->offerings) {
+      if (!of.available || !reqs.compatible(of.reqs, true)) continue;
+      if (!any || of.price < best) {
+        best = of.price;
+        any = true;
+      }
+    }
+    return any ? best : __DBL_MAX__;
+  };
+  vector<std::pair<double, const InstanceType*>> keyed;
+  for (auto* it : its) keyed.push_back({cheapest(it), it});
+  // the comparator is a total order (names are unique) so any sort gives
+  // sort.Slice's result
+  std::sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& b) {
+    if (a.first == b.first) return a.second->name < b.second->name;
+    return a.first < b.first;
+  });
+  vector<const InstanceType*> out;
+  for (size_t i = 0; i < keyed.size() && i < max_items; i++) out.push_back(keyed[i].second);
+  return out;
+}
+
+struct OracleState {
+  vector<string> strings;
+  vector<InstanceType> its;
+  vector<Pod> pods;
+  vector<Template> templates;  // filtered + ordered
+  vector<ExistingNode> nodes;  // ordered
+  vector<uint32_t> node_order;
+  std::map<string, Res> remaining;  // nodepools with limits
+  bool tolerate_pns = false;
+  vector<string> resource_names;
+};
+
+struct Builder {
+  const gs_problem* p;
+  OracleState& st;
+
+  const string& str(uint32_t id) {
+    if (id >= p->n_strings) throw Unsupported{GS_E_INVALID, "string id out of range"};
+    return st.strings[id];
+  }
+  void check_range(gs_range r, uint32_t n, const char* what) {
+    if ((uint64_t)r.begin + r.count > n) throw Unsupported{GS_E_INVALID, string("range out of bounds: ") + what};
+  }
+  Req req_of(const gs_requirement& q) {
+    if (q.op > GS_OP_LT) throw Unsupported{GS_E_UNSUPPORTED, "Gte/Lte operators"};
+    if (normalize_key(str(q.key)) == kHostname)
+      for (uint32_t i = 0; i < q.values.count && q.values.begin + i < p->n_value_ids; i++)
+        if (str(p->value_ids[q.values.begin + i]).rfind("hostname-placeholder-", 0) == 0)
+          throw Unsupported{GS_E_UNSUPPORTED, "requirement names a hostname placeholder"};
+    if (q.min_values >= 0) throw Unsupported{GS_E_UNSUPPORTED, "minValues"};
+    check_range(q.values, p->n_value_ids, "values");
+    vector<string> vals;
+    for (uint32_t i = 0; i < q.values.count; i++) vals.push_back(str(p->value_ids[q.values.begin + i]));
+    return make_req(str(q.key), (int)q.op, vals, std::nullopt);
+  }
+  vector<Req> raw_reqs(gs_range r) {
+    check_range(r, p->n_reqs, "reqs");
+    vector<Req> out;
+    for (uint32_t i = 0; i < r.count; i++) out.push_back(req_of(p->reqs[r.begin + i]));
+    return out;
+  }
+  Reqs reqs_of(gs_range r) {
+    Reqs out;
+    for (auto& q : raw_reqs(r)) out.add(q);
+    return out;
+  }
+  Res res_of(gs_range r) {
+    check_range(r, p->n_quantities, "quantities");
+    Res out;
+    for (uint32_t i = 0; i < r.count; i++) {
+      auto& q = p->quantities[r.begin + i];
+      out[str(q.resource)] += q.milli;
+    }
+    return out;
+  }
+  vector<Taint> taints_of(gs_range r) {
+    check_range(r, p->n_taints, "taints");
+    vector<Taint> out;
+    for (uint32_t i = 0; i < r.count; i++) {
+      auto& t = p->taints[r.begin + i];
+      out.push_back({str(t.key), str(t.value), str(t.effect)});
+    }
+    return out;
+  }
+  std::map<string, string> labels_of(gs_range r) {
+    check_range(r, p->n_labels, "labels");
+    std::map<string, string> out;
+    for (uint32_t i = 0; i < r.count; i++) out[str(p->labels[r.begin + i].key)] = str(p->labels[r.begin + i].value);
+    return out;
+  }
+
+  void build() {
+    st.strings.clear();
+    for (uint32_t i = 0; i < p->n_strings; i++) st.strings.push_back(p->strings[i] ? p->strings[i] : "");
+    // catalog
+    st.its.resize(p->n_instance_types);
+    for (uint32_t i = 0; i < p->n_instance_types; i++) {
+      auto& g = p->instance_types[i];
+      auto& it = st.its[i];
+      it.index = i;
+      it.name = str(g.name);
+      it.reqs = reqs_of(g.requirements);
+      it.capacity = res_of(g.capacity);
+      it.overhead = res_of(g.overhead);
+      it.allocatable = subtract(it.capacity, it.overhead);
+      check_range(g.offerings, p->n_offerings, "offerings");
+      for (uint32_t k = 0; k < g.offerings.count; k++) {
+        auto& o = p->offerings[g.offerings.begin + k];
+        it.offerings.push_back({reqs_of(o.requirements), o.price, o.available != 0});
+      }
+    }
+    // templates: NodePools ordered by weight desc then name (<U> OrderByWeight)
+    vector<uint32_t> order(p->n_nodepools);
+    for (uint32_t i = 0; i < p->n_nodepools; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      auto& A = p->nodepools[a];
+      auto& B = p->nodepools[b];
+      if (A.weight == B.weight) return str(A.name) < str(B.name);
+      return A.weight > B.weight;
+    });
+    for (uint32_t npi : order) {
+      auto& np = p->nodepools[npi];
+      Template t;
+      t.np_index = npi;
+      t.name = str(np.name);
+      t.weight = np.weight;
+      Reqs npreqs = reqs_of(np.requirements);
+      t.reqs = npreqs;
+      auto labels = labels_of(np.labels);
+      labels[kNodePool] = t.name;
+      for (auto& kv : labels) t.reqs.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
+      t.taints = taints_of(np.taints);
+      t.daemon = res_of(np.daemon_requests);
+      t.has_limits = np.has_limits != 0;
+      // CloudProvider.GetInstanceTypes filter (reference cloudprovider.go:573-577)
+      check_range(np.instance_types, p->n_it_refs, "it_refs");
+      vector<const InstanceType*> its;
+      for (uint32_t k = 0; k < np.instance_types.count; k++) {
+        uint32_t idx = p->it_refs[np.instance_types.begin + k];
+        if (idx >= st.its.size()) throw Unsupported{GS_E_INVALID, "it_ref out of range"};
+        const InstanceType* it = &st.its[idx];
+        if (npreqs.compatible(it->reqs, true)) its.push_back(it);
+      }
+      // <U> NewScheduler: pre-filter instance types per template
+      t.options = filter_its(its, t.reqs, Res{});
+      if (t.has_limits) st.remaining[t.name] = res_of(np.limits);
+      if (t.options.empty()) continue;
+      st.templates.push_back(std::move(t));
+    }
+    for (auto& t : st.templates)
+      for (auto& tn : t.taints)
+        if (tn.effect == kEffectPreferNoSchedule) st.tolerate_pns = true;
+    // pods
+    st.pods.resize(p->n_pods);
+    std::set<string> uids;
+    for (uint32_t i = 0; i < p->n_pods; i++) {
+      auto& g = p->pods[i];
+      if (g.flags) throw Unsupported{GS_E_UNSUPPORTED, "pod topology/affinity/host ports/volumes"};
+      auto& pd = st.pods[i];
+      pd.index = i;
+      pd.uid = str(g.uid);
+      if (!uids.insert(pd.uid).second) throw Unsupported{GS_E_INVALID, "duplicate pod uid"};
+      pd.ts = g.creation_ns;
+      pd.requests = res_of(g.requests);
+      pd.node_selector = labels_of(g.node_selector);
+      check_range(g.required_terms, p->n_terms, "terms");
+      for (uint32_t k = 0; k < g.required_terms.count; k++) {
+        auto& tm = p->terms[g.required_terms.begin + k];
+        pd.required.push_back({raw_reqs(tm.requirements), tm.weight});
+      }
+      check_range(g.preferred_terms, p->n_terms, "terms");
+      for (uint32_t k = 0; k < g.preferred_terms.count; k++) {
+        auto& tm = p->terms[g.preferred_terms.begin + k];
+        pd.preferred.push_back({raw_reqs(tm.requirements), tm.weight});
+      }
+      check_range(g.tolerations, p->n_tolerations, "tolerations");
+      for (uint32_t k = 0; k < g.tolerations.count; k++) {
+        auto& t = p->tolerations[g.tolerations.begin + k];
+        pd.tolerations.push_back({str(t.key), str(t.value), str(t.effect), (int)t.op});
+      }
+      update_pod_reqs(pd);
+    }
+    // existing nodes: <U> initialized first, then by name (sort.SliceStable)
+    st.nodes.resize(p->n_nodes);
+    for (uint32_t i = 0; i < p->n_nodes; i++) {
+      auto& g = p->nodes[i];
+      auto& n = st.nodes[i];
+      n.index = i;
+      n.name = str(g.name);
+      n.initialized = g.initialized != 0;
+      for (auto& kv : labels_of(g.labels)) n.reqs.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
+      n.reqs.add(make_req(kHostname, GS_OP_IN, {n.name}, std::nullopt));
+      n.taints = taints_of(g.taints);
+      n.available = res_of(g.available);
+      n.requests = res_of(g.requests);
+    }
+    st.node_order.resize(p->n_nodes);
+    for (uint32_t i = 0; i < p->n_nodes; i++) st.node_order[i] = i;
+    std::stable_sort(st.node_order.begin(), st.node_order.end(), [&](uint32_t a, uint32_t b) {
+      auto& A = st.nodes[a];
+      auto& B = st.nodes[b];
+      if (A.initialized != B.initialized) return A.initialized;
+      return A.name < B.name;
+    });
+    // resource vocabulary (for dense claim requests)
+    std::set<string> rn;
+    for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(str(p->quantities[i].resource));
+    st.resource_names.assign(rn.begin(), rn.end());
+  }
+};
+
+// <U> Preferences.Relax: first applicable relaxation, in order
+bool relax(Pod& p, bool tolerate_pns) {
+  // removeRequiredNodeAffinityTerm
+  if (p.required.size() > 1) {
+    p.required.erase(p.required.begin());
+    return true;
+  }
+  // removePreferredPodAffinityTerm / AntiAffinity: pods with pod affinity are
+  // refused up front (GS_POD_AFFINITY), nothing to relax here
+  // removePreferredNodeAffinityTerm: sort.SliceStable by weight desc, drop [0]
+  if (!p.preferred.empty()) {
+    std::stable_sort(p.preferred.begin(), p.preferred.end(),
+                     [](const Term& a, const Term& b) { return a.weight > b.weight; });
+    p.preferred.erase(p.preferred.begin());
+    return true;
+  }
+  // removeTopologySpreadScheduleAnyway: refused up front
+  if (tolerate_pns) {
+    for (auto& t : p.tolerations)
+      if (t.key.empty() && t.op == GS_TOL_EXISTS && t.value.empty() && t.effect == kEffectPreferNoSchedule) return false;
+    p.tolerations.push_back({"", "", kEffectPreferNoSchedule, GS_TOL_EXISTS});
+    return true;
+  }
+  return false;
+}
+
+struct Scheduler {
+  OracleState& st;
+  vector<NodeClaim*> claims;  // s.newNodeClaims (sorted in place per pod)
+  vector<std::unique_ptr<NodeClaim>> owned;
+  vector<NodeClaim*> creation_order;
+  uint64_t pops = 0;
+  uint64_t node_id = 0;  // <U> package-level nodeID counter, per solve here
+
+  // <U> NodeClaim.CanAdd; returns true and fills the update on success
+  bool claim_can_add(const NodeClaim& n, const Pod& pod, Reqs* reqs_out, vector<const InstanceType*>* its_out,
+                     Res* req_out) {
+    if (!tolerates_all(n.tmpl->taints, pod.tolerations)) return false;
+    Reqs nr = n.reqs;  // NewRequirements(n.Requirements.Values()...)
+    if (!nr.compatible(pod.reqs, true)) return false;
+    nr.add_all(pod.reqs);
+    Res requests = merge(n.requests, pod.requests);
+    auto remaining = filter_its(n.options, nr, requests);
+    if (remaining.empty()) return false;
+    *reqs_out = std::move(nr);
+    *its_out = std::move(remaining);
+    *req_out = std::move(requests);
+    return true;
+  }
+
+  // <U> ExistingNode.CanAdd (strict Compatible: no AllowUndefined)
+  bool node_can_add(const ExistingNode& n, const Pod& pod, Reqs* reqs_out, Res* req_out) {
+    if (!tolerates_all(n.taints, pod.tolerations)) return false;
+    Res requests = merge(n.requests, pod.requests);
+    if (!fits(requests, n.available)) return false;
+    Reqs nr = n.reqs;
+    if (!nr.compatible(pod.reqs, false)) return false;
+    nr.add_all(pod.reqs);
+    *reqs_out = std::move(nr);
+    *req_out = std::move(requests);
+    return true;
+  }
+
+  bool add(Pod& pod) {
+    for (uint32_t ni : st.node_order) {
+      auto& n = st.nodes[ni];
+      Reqs r;
+      Res q;
+      if (node_can_add(n, pod, &r, &q)) {
+        n.reqs = std::move(r);
+        n.requests = std::move(q);
+        n.pods.push_back(&pod);
+        return true;
+      }
+    }
+    // sort.Slice(s.newNodeClaims, len(Pods) asc)
+    struct D {
+      vector<NodeClaim*>& c;
+      bool less(int i, int j) { return c[i]->pods.size() < c[j]->pods.size(); }
+      void swap(int i, int j) { std::swap(c[i], c[j]); }
+    } d{claims};
+    gosort::slice(d, (int)claims.size());
+    for (auto* nc : claims) {
+      Reqs r;
+      vector<const InstanceType*> its;
+      Res q;
+      if (claim_can_add(*nc, pod, &r, &its, &q)) {
+        nc->reqs = std::move(r);
+        nc->options = std::move(its);
+        nc->requests = std::move(q);
+        nc->pods.push_back(&pod);
+        return true;
+      }
+    }
+    for (auto& t : st.templates) {
+      vector<const InstanceType*> its = t.options;
+      auto rem = st.remaining.find(t.name);
+      if (rem != st.remaining.end()) {
+        // <U> filterByRemainingResources
+        vector<const InstanceType*> f;
+        for (auto* it : its) {
+          bool viable = true;
+          for (auto& kv : rem->second)
+            if (res_get(it->capacity, kv.first) > kv.second) viable = false;
+          if (viable) f.push_back(it);
+        }
+        its = std::move(f);
+        if (its.empty()) continue;
+      }
+      // <U> NewNodeClaim: template reqs + hostname placeholder, requests = daemon
+      auto nc = std::make_unique<NodeClaim>();
+      nc->tmpl = &t;
+      nc->reqs = t.reqs;
+      char hn[48];
+      std::snprintf(hn, sizeof hn, "hostname-placeholder-%04llu", (unsigned long long)++node_id);
+      nc->reqs.add(make_req(kHostname, GS_OP_IN, {hn}, std::nullopt));
+      nc->options = its;
+      nc->requests = t.daemon;
+      Reqs r;
+      vector<const InstanceType*> its2;
+      Res q;
+      if (!claim_can_add(*nc, pod, &r, &its2, &q)) continue;
+      nc->reqs = std::move(r);
+      nc->options = std::move(its2);
+      nc->requests = std::move(q);
+      nc->pods.push_back(&pod);
+      if (rem != st.remaining.end()) {
+        // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+        Res mx;
+        for (auto* it : nc->options)
+          for (auto& kv : it->capacity) {
+            auto f = mx.find(kv.first);
+            if (f == mx.end() || kv.second > f->second) mx[kv.first] = kv.second;
+          }
+        for (auto& kv : rem->second) kv.second -= res_get(mx, kv.first);
+      }
+      claims.push_back(nc.get());
+      creation_order.push_back(nc.get());
+      owned.push_back(std::move(nc));
+      return true;
+    }
+    return false;
+  }
+
+  // <U> Scheduler.Solve: queue + relax loop; returns error pods
+  std::set<uint32_t> solve() {
+    vector<Pod*> q;
+    for (auto& p : st.pods) q.push_back(&p);
+    // <U> NewQueue: byCPUAndMemoryDescending, then creationTimestamp, then UID
+    // (a total order, so std::sort reproduces sort.Slice)
+    std::sort(q.begin(), q.end(), [](const Pod* a, const Pod* b) {
+      int64_t ac = res_get(a->requests, "cpu"), bc = res_get(b->requests, "cpu");
+      if (ac != bc) return ac > bc;
+      int64_t am = res_get(a->requests, "memory"), bm = res_get(b->requests, "memory");
+      if (am != bm) return am > bm;
+      if (a->ts != b->ts) return a->ts < b->ts;
+      return a->uid < b->uid;
+    });
+    std::unordered_map<const Pod*, size_t> last_len;
+    std::set<uint32_t> errors;
+    size_t head = 0;
+    std::vector<Pod*> queue = q;  // queue[head..]
+    for (;;) {
+      if (head >= queue.size()) break;
+      Pod* p = queue[head];
+      size_t len = queue.size() - head;
+      auto ll = last_len.find(p);
+      if (ll != last_len.end() && ll->second == len) break;
+      head++;
+      pops++;
+      if (add(*p)) {
+        errors.erase(p->index);
+        continue;
+      }
+      errors.insert(p->index);
+      bool relaxed = relax(*p, st.tolerate_pns);
+      queue.push_back(p);
+      if (relaxed) {
+        last_len.clear();
+        update_pod_reqs(*p);
+      } else {
+        last_len[p] = queue.size() - head;
+      }
+    }
+    return errors;
+  }
+};
+
+// ------------------------------------------------------------- result memory
+struct ResultStore {
+  vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
+  vector<string> req_text;
+  vector<const char*> req_ptrs;
+  vector<uint32_t> resource_names;
+  vector<int64_t> claim_requests;
+  vector<uint32_t> node_pod_offsets, node_pods, error_pods;
+  // feasibility
+  vector<uint64_t> rows;
+  vector<int32_t> cheapest;
+  vector<uint32_t> nfeas;
+};
+ResultStore g_res;
+OracleState* g_state = nullptr;
+
+}  // namespace
+
+extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
+  auto t0 = std::chrono::steady_clock::now();
+  delete g_state;
+  g_state = new OracleState();
+  OracleState& st = *g_state;
+  try {
+    Builder b{problem, st};
+    b.build();
+  } catch (const Unsupported& u) {
+    return u.code;
+  }
+  Scheduler s{st};
+  auto errors = s.solve();
+  ResultStore& r = g_res;
+  r = ResultStore();
+  r.claim_pod_offsets.push_back(0);
+  r.claim_it_offsets.push_back(0);
+  std::map<string, uint32_t> name_to_id;
+  for (uint32_t i = 0; i < problem->n_strings; i++) name_to_id.emplace(st.strings[i], i);
+  for (auto& rn : st.resource_names) r.resource_names.push_back(name_to_id[rn]);
+  for (auto* nc : s.creation_order) {
+    // FinalizeScheduling: drop hostname requirement
+    nc->reqs.m.erase(kHostname);
+    r.claim_nodepool.push_back(nc->tmpl->np_index);
+    for (auto* p : nc->pods) r.claim_pods.push_back(p->index);
+    r.claim_pod_offsets.push_back((uint32_t)r.claim_pods.size());
+    for (auto* it : order_by_price(nc->options, nc->reqs, 60)) r.claim_its.push_back(it->index);
+    r.claim_it_offsets.push_back((uint32_t)r.claim_its.size());
+    r.req_text.push_back(canonical(nc->reqs));
+    for (auto& rn : st.resource_names) r.claim_requests.push_back(res_get(nc->requests, rn));
+  }
+  for (auto& t : r.req_text) r.req_ptrs.push_back(t.c_str());
+  r.node_pod_offsets.push_back(0);
+  for (auto& n : st.nodes) {
+    for (auto* p : n.pods) r.node_pods.push_back(p->index);
+    r.node_pod_offsets.push_back((uint32_t)r.node_pods.size());
+  }
+  r.error_pods.assign(errors.begin(), errors.end());
+  std::memset(out, 0, sizeof(*out));
+  out->n_claims = (uint32_t)s.creation_order.size();
+  out->claim_nodepool = r.claim_nodepool.data();
+  out->claim_pod_offsets = r.claim_pod_offsets.data();
+  out->claim_pods = r.claim_pods.data();
+  out->claim_it_offsets = r.claim_it_offsets.data();
+  out->claim_its = r.claim_its.data();
+  out->claim_requirements = r.req_ptrs.data();
+  out->n_resources = (uint32_t)r.resource_names.size();
+  out->resource_names = r.resource_names.data();
+  out->claim_requests = r.claim_requests.data();
+  out->n_nodes = (uint32_t)st.nodes.size();
+  out->node_pod_offsets = r.node_pod_offsets.data();
+  out->node_pods = r.node_pods.data();
+  out->n_errors = (uint32_t)r.error_pods.size();
+  out->error_pods = r.error_pods.data();
+  out->pops = s.pops;
+  out->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return GS_OK;
+}
+
+extern "C" gs_status oracle_feasibility(const gs_problem* problem, gs_feas_result* out) {
+  auto t0 = std::chrono::steady_clock::now();
+  delete g_state;
+  g_state = new OracleState();
+  OracleState& st = *g_state;
+  try {
+    Builder b{problem, st};
+    b.build();
+  } catch (const Unsupported& u) {
+    return u.code;
+  }
+  uint32_t P = problem->n_pods, T = problem->n_nodepools, N = problem->n_instance_types;
+  uint32_t W = (N + 63) / 64;
+  ResultStore& r = g_res;
+  r = ResultStore();
+  r.rows.assign((size_t)P * T * W, 0);
+  r.cheapest.assign((size_t)P * T, -1);
+  r.nfeas.assign((size_t)P * T, 0);
+  uint64_t checks = 0;
+  Scheduler s{st};
+  for (auto& t : st.templates) {
+    for (auto* it : t.options) checks += (uint64_t)it->offerings.size() * P;
+  }
+  for (uint32_t pi = 0; pi < P; pi++) {
+    const Pod& pod = st.pods[pi];
+    for (auto& t : st.templates) {
+      vector<const InstanceType*> its = t.options;
+      auto rem = st.remaining.find(t.name);
+      if (rem != st.remaining.end()) {
+        vector<const InstanceType*> f;
+        for (auto* it : its) {
+          bool viable = true;
+          for (auto& kv : rem->second)
+            if (res_get(it->capacity, kv.first) > kv.second) viable = false;
+          if (viable) f.push_back(it);
+        }
+        its = std::move(f);
+      }
+      NodeClaim nc;
+      nc.tmpl = &t;
+      nc.reqs = t.reqs;
+      nc.reqs.add(make_req(kHostname, GS_OP_IN, {"hostname-placeholder-0001"}, std::nullopt));
+      nc.options = its;
+      nc.requests = t.daemon;
+      Reqs rq;
+      vector<const InstanceType*> rem_its;
+      Res q;
+      if (its.empty() || !s.claim_can_add(nc, pod, &rq, &rem_its, &q)) continue;
+      size_t base = ((size_t)pi * T + t.np_index);
+      uint32_t nf = 0;
+      for (auto* it : rem_its) {
+        r.rows[base * W + it->index / 64] |= 1ull << (it->index % 64);
+        for (auto& of : it->offerings)
+          if (of.available && rq.compatible(of.reqs, true)) nf++;
+      }
+      r.nfeas[base] = nf;
+      rq.m.erase(kHostname);
+      auto ordered = order_by_price(rem_its, rq, 1);
+      r.cheapest[base] = ordered.empty() ? -1 : (int32_t)ordered[0]->index;
+    }
+  }
+  std::memset(out, 0, sizeof(*out));
+  out->n_pods = P;
+  out->n_nodepools = T;
+  out->n_its = N;
+  out->words = W;
+  out->rows = r.rows.data();
+  out->cheapest_it = r.cheapest.data();
+  out->n_feasible_offerings = r.nfeas.data();
+  out->checks = checks;
+  out->t_kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return GS_OK;
+}
+
+extern "C" void oracle_go_sort_ints(int64_t* keys, uint32_t* perm, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) perm[i] = i;
+  struct D {
+    int64_t* k;
+    uint32_t* p;
+    bool less(int i, int j) { return k[i] < k[j]; }
+    void swap(int i, int j) {
+      std::swap(k[i], k[j]);
+      std::swap(p[i], p[j]);
+    }
+  } d{keys, perm};
+  gosort::slice(d, (int)n);
+}
