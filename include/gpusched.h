@@ -240,6 +240,11 @@ gs_status gs_solve(gs_ctx* ctx, const gs_problem* problem, gs_result* out);
 /* static feasibility matrix only (K1/K2) on a prepared problem */
 gs_status gs_feasibility(gs_ctx* ctx, gs_feas_result* out);
 
+/* host-only: run the encoder (no device needed) and report whether this
+ * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.
+ * A Go caller uses it to choose between this library and upstream Solve. */
+gs_status gs_validate(const gs_problem* problem, char* err, size_t err_len);
+
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);
 const char* gs_version(void);
 

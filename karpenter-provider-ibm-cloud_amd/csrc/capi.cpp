@@ -1,0 +1,419 @@
+// capi.cpp — C-ABI of libgpusched.so (include/gpusched.h): context, HBM
+// buffers, kernel launches on one HIP stream, result decode.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpusched.h"
+#include "encode.hpp"
+#include "layout.hpp"
+
+extern "C" hipError_t gsk_init(uint32_t ffd_lds_bytes, uint32_t trunc_lds_bytes);
+extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
+extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, hipStream_t s);
+extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
+
+namespace {
+
+constexpr uint32_t kMaxClaimsLds = 16384;  // ord+sc u32 in LDS: 128 KiB
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
+struct HipError {
+  std::string msg;
+};
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+}  // namespace
+
+struct gs_ctx {
+  int device = 0;
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  std::vector<void*> allocs;
+  gsh::Encoded enc;
+  gsd::DevProblem dp{};
+  bool prepared = false, ran = false;
+  double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
+  const gs_problem* problem = nullptr;
+  // result storage
+  std::vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
+  std::vector<std::string> req_text;
+  std::vector<const char*> req_ptrs;
+  std::vector<int64_t> claim_requests;
+  std::vector<uint32_t> node_pod_offsets, node_pods, error_pods;
+  std::vector<uint64_t> f_rows;
+  std::vector<int32_t> f_cheapest;
+  std::vector<uint32_t> f_nfo;
+  gsd::Ctrl ctrl{};
+
+  void free_all() {
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+  }
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    allocs.push_back(p);
+    return (T*)p;
+  }
+  template <class T>
+  T* upload(const std::vector<T>& v) {
+    T* p = alloc<T>(v.size());
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+    return p;
+  }
+};
+
+namespace {
+
+gs_status fail(gs_ctx* c, gs_status s, const std::string& m) {
+  c->err = m;
+  return s;
+}
+
+void upload_problem(gs_ctx* c) {
+  auto& e = c->enc;
+  auto& d = c->dp;
+  c->free_all();
+  std::memset(&d, 0, sizeof d);
+  d.N = e.N;
+  d.W = e.W;
+  d.R = e.R;
+  d.Z = e.Z;
+  d.C = e.C;
+  d.T = e.T;
+  d.F = e.F;
+  d.V = e.V;
+  d.P = e.P;
+  d.K = e.K;
+  d.NT = e.NT;
+  d.wk_slots = e.wk_slots;
+  d.max_claims = std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
+  d.it_vid = c->upload(e.it_vid);
+  d.it_alloc = c->upload(e.it_alloc);
+  d.it_cap = c->upload(e.it_cap);
+  d.it_pair = c->upload(e.it_pair);
+  d.it_prank = c->upload(e.it_prank);
+  d.it_namerank = c->upload(e.it_namerank);
+  d.rank_to_it = c->upload(e.rank_to_it);
+  d.slot_set = c->upload(e.slot_set);
+  d.thr_val = c->upload(e.thr_val);
+  d.thr_off = c->upload(e.thr_off);
+  d.thr_set = c->upload(e.thr_set);
+  d.fk_ival = c->upload(e.fk_ival);
+  d.fk_isint = c->upload(e.fk_isint);
+  d.tmpl = c->upload(e.tmpl);
+  d.t_opts = c->upload(e.t_opts);
+  d.t_fk = c->upload(e.t_fk);
+  d.pod_req = c->upload(e.pod_req);
+  d.var_begin = c->upload(e.var_begin);
+  d.var_count = c->upload(e.var_count);
+  d.vars = c->upload(e.vars);
+  d.itmask = c->upload(e.itmask);
+  d.fk_entries = c->upload(e.fk_entries);
+  d.queue0 = c->upload(e.queue0);
+  const size_t VT = (size_t)e.V * e.T, MC = d.max_claims;
+  d.rows = c->alloc<uint64_t>(VT * e.W);
+  d.cheapest = c->alloc<uint32_t>(VT);
+  d.nfo = c->alloc<uint32_t>(VT);
+  d.queue = c->alloc<uint32_t>(e.P);
+  d.last_len = c->alloc<uint32_t>(e.P);
+  d.last_epoch = c->alloc<uint32_t>(e.P);
+  d.cur_var = c->alloc<uint32_t>(e.P);
+  d.c_hdr = c->alloc<gsd::ClaimHdr>(MC);
+  d.c_opts = c->alloc<uint64_t>(MC * e.W);
+  d.c_tot = c->alloc<int64_t>(MC * std::max<uint32_t>(e.R, 1));
+  d.c_fk = c->alloc<gsd::FK>(MC * std::max<uint32_t>(e.F, 1));
+  d.t_rem = c->alloc<int64_t>((size_t)e.T * std::max<uint32_t>(e.R, 1));
+  d.log = c->alloc<gsd::LogRec>(e.P);
+  d.c_sorted = c->alloc<uint32_t>(MC);
+  d.ctrl = c->alloc<gsd::Ctrl>(1);
+  d.c_its = c->alloc<uint32_t>(MC * 60);
+  d.c_nits = c->alloc<uint32_t>(MC);
+  HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+uint32_t trunc_lds_bytes(uint32_t N) {
+  uint32_t np2 = 1;
+  while (np2 < N) np2 <<= 1;
+  return np2 * 8;
+}
+
+void launch_feas(gs_ctx* c, uint32_t apply_limits) { HIPCHK(gsk_feas(&c->dp, apply_limits, c->stream)); }
+
+}  // namespace
+
+extern "C" {
+
+const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
+
+gs_status gs_validate(const gs_problem* p, char* err, size_t len) {
+  if (!p) return GS_E_INVALID;
+  gsh::Encoded enc;
+  gsh::Err er = gsh::encode(p, enc);
+  if (er.code == GS_OK && enc.N > 8192) er = gsh::Err{GS_E_CAPACITY, "more than 8192 instance types"};
+  if (err && len) {
+    size_t n = std::min(len - 1, er.msg.size());
+    std::memcpy(err, er.msg.data(), n);
+    err[n] = 0;
+  }
+  return er.code;
+}
+
+size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len) {
+  if (!ctx) return 0;
+  if (buf && len) {
+    size_t n = std::min(len - 1, ctx->err.size());
+    std::memcpy(buf, ctx->err.data(), n);
+    buf[n] = 0;
+  }
+  return ctx->err.size();
+}
+
+gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GS_E_NO_DEVICE;
+  auto* c = new gs_ctx();
+  c->device = cfg ? cfg->device : 0;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, c->device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      delete c;
+      return GS_E_NO_DEVICE;
+    }
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(gsk_init(kMaxClaimsLds * 8, 65536));
+  } catch (const HipError& e) {
+    delete c;
+    return GS_E_HIP;
+  }
+  *out = c;
+  return GS_OK;
+}
+
+void gs_destroy(gs_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  c->free_all();
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
+  if (!c || !p) return GS_E_INVALID;
+  c->prepared = c->ran = false;
+  auto t0 = Clock::now();
+  gsh::Err er = gsh::encode(p, c->enc);
+  c->t_encode = ms_since(t0);
+  if (er.code != GS_OK) return fail(c, er.code, er.msg);
+  if (c->enc.N > 8192) return fail(c, GS_E_CAPACITY, "more than 8192 instance types");
+  c->problem = p;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    auto t1 = Clock::now();
+    upload_problem(c);
+    c->t_upload = ms_since(t1);
+  } catch (const HipError& e) {
+    return fail(c, GS_E_HIP, e.msg);
+  }
+  c->prepared = true;
+  return GS_OK;
+}
+
+gs_status gs_run(gs_ctx* c) {
+  if (!c || !c->prepared) return GS_E_INVALID;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    auto& d = c->dp;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    launch_feas(c, 0);
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(gsk_ffd(&d, c->stream));
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), c->stream));
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+    float a = 0, b = 0, x = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    HIPCHK(hipEventElapsedTime(&x, c->ev[2], c->ev[3]));
+    c->t_feas = a;
+    c->t_ffd = b;
+    c->t_trunc = x;
+  } catch (const HipError& e) {
+    return fail(c, GS_E_HIP, e.msg);
+  }
+  c->ran = true;
+  return GS_OK;
+}
+
+gs_status gs_fetch(gs_ctx* c, gs_result* out) {
+  if (!c || !c->ran || !out) return GS_E_INVALID;
+  auto t0 = Clock::now();
+  auto& e = c->enc;
+  auto& d = c->dp;
+  std::vector<gsd::LogRec> log;
+  std::vector<gsd::ClaimHdr> hdr;
+  std::vector<int64_t> tot;
+  std::vector<uint32_t> its, nits, queue;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(&c->ctrl, d.ctrl, sizeof(gsd::Ctrl), hipMemcpyDeviceToHost));
+    const uint32_t M = c->ctrl.n_claims;
+    log.resize(c->ctrl.n_log);
+    hdr.resize(M);
+    tot.resize((size_t)M * e.R);
+    its.resize((size_t)M * 60);
+    nits.resize(M);
+    queue.resize(e.P);
+    if (!log.empty()) HIPCHK(hipMemcpy(log.data(), d.log, log.size() * sizeof(gsd::LogRec), hipMemcpyDeviceToHost));
+    if (M) {
+      HIPCHK(hipMemcpy(hdr.data(), d.c_hdr, M * sizeof(gsd::ClaimHdr), hipMemcpyDeviceToHost));
+      if (e.R) HIPCHK(hipMemcpy(tot.data(), d.c_tot, tot.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(its.data(), d.c_its, its.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(nits.data(), d.c_nits, M * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    if (e.P) HIPCHK(hipMemcpy(queue.data(), d.queue, e.P * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  } catch (const HipError& ex) {
+    return fail(c, GS_E_HIP, ex.msg);
+  }
+  if (c->ctrl.status == 1) return fail(c, GS_E_CAPACITY, "NodeClaim count exceeded the device capacity");
+  if (c->ctrl.status != 0) return fail(c, GS_E_HIP, "ffd kernel reported an internal error");
+  const uint32_t M = c->ctrl.n_claims;
+  // pods per claim in add order, and each claim's requirement set
+  std::vector<std::vector<uint32_t>> cp(M);
+  std::vector<gsh::Reqs> creq(M);
+  for (uint32_t j = 0; j < M; j++) creq[j] = e.tmpl_reqs[hdr[j].tmpl];
+  for (auto& l : log) {
+    if (l.target >= M) return fail(c, GS_E_HIP, "corrupt add log");
+    cp[l.target].push_back(l.pod);
+    for (auto& kv : e.variants[l.var].reqs) gsh::reqs_add(e, creq[l.target], kv.first, kv.second);
+  }
+  c->claim_nodepool.assign(M, 0);
+  c->claim_pod_offsets.assign(1, 0);
+  c->claim_pods.clear();
+  c->claim_it_offsets.assign(1, 0);
+  c->claim_its.clear();
+  c->req_text.assign(M, "");
+  c->claim_requests.assign((size_t)M * e.R, 0);
+  for (uint32_t j = 0; j < M; j++) {
+    c->claim_nodepool[j] = e.tmpl[hdr[j].tmpl].np_index;
+    c->claim_pods.insert(c->claim_pods.end(), cp[j].begin(), cp[j].end());
+    c->claim_pod_offsets.push_back((uint32_t)c->claim_pods.size());
+    c->claim_its.insert(c->claim_its.end(), its.begin() + (size_t)j * 60, its.begin() + (size_t)j * 60 + nits[j]);
+    c->claim_it_offsets.push_back((uint32_t)c->claim_its.size());
+    creq[j].erase(e.k_hostname);  // FinalizeScheduling
+    c->req_text[j] = gsh::canonical(e, creq[j]);
+    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = tot[(size_t)j * e.R + r];
+  }
+  c->req_ptrs.clear();
+  for (auto& s : c->req_text) c->req_ptrs.push_back(s.c_str());
+  c->error_pods.clear();
+  for (uint32_t i = 0; i < c->ctrl.qlen; i++) c->error_pods.push_back(queue[(c->ctrl.qhead + i) % e.P]);
+  std::sort(c->error_pods.begin(), c->error_pods.end());
+  c->node_pod_offsets.assign(1, 0);
+  c->node_pods.clear();
+  c->t_fetch = ms_since(t0);
+  std::memset(out, 0, sizeof(*out));
+  out->n_claims = M;
+  out->claim_nodepool = c->claim_nodepool.data();
+  out->claim_pod_offsets = c->claim_pod_offsets.data();
+  out->claim_pods = c->claim_pods.data();
+  out->claim_it_offsets = c->claim_it_offsets.data();
+  out->claim_its = c->claim_its.data();
+  out->claim_requirements = c->req_ptrs.data();
+  out->n_resources = e.R;
+  out->resource_names = e.res_name_ids.data();
+  out->claim_requests = c->claim_requests.data();
+  out->n_nodes = 0;
+  out->node_pod_offsets = c->node_pod_offsets.data();
+  out->node_pods = c->node_pods.data();
+  out->n_errors = (uint32_t)c->error_pods.size();
+  out->error_pods = c->error_pods.data();
+  out->checks = e.checks;
+  out->pops = c->ctrl.pops;
+  out->t_encode_ms = c->t_encode;
+  out->t_upload_ms = c->t_upload;
+  out->t_feas_ms = c->t_feas;
+  out->t_ffd_ms = c->t_ffd;
+  out->t_truncate_ms = c->t_trunc;
+  out->t_fetch_ms = c->t_fetch;
+  out->t_total_ms = c->t_encode + c->t_upload + c->t_feas + c->t_ffd + c->t_trunc + c->t_fetch;
+  return GS_OK;
+}
+
+gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
+  gs_status s = gs_prepare(c, p);
+  if (s != GS_OK) return s;
+  s = gs_run(c);
+  if (s != GS_OK) return s;
+  return gs_fetch(c, out);
+}
+
+gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
+  if (!c || !c->prepared || !out) return GS_E_INVALID;
+  auto& e = c->enc;
+  const uint32_t P = e.P, NP = c->problem->n_nodepools, W = e.W;
+  float ms = 0;
+  std::vector<uint64_t> rows((size_t)e.V * e.T * W);
+  std::vector<uint32_t> ch((size_t)e.V * e.T), nfo((size_t)e.V * e.T);
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    launch_feas(c, 1);
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[5]));
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
+    if (!rows.empty()) HIPCHK(hipMemcpy(rows.data(), c->dp.rows, rows.size() * 8, hipMemcpyDeviceToHost));
+    if (!ch.empty()) {
+      HIPCHK(hipMemcpy(ch.data(), c->dp.cheapest, ch.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(nfo.data(), c->dp.nfo, nfo.size() * 4, hipMemcpyDeviceToHost));
+    }
+  } catch (const HipError& ex) {
+    return fail(c, GS_E_HIP, ex.msg);
+  }
+  c->f_rows.assign((size_t)P * NP * W, 0);
+  c->f_cheapest.assign((size_t)P * NP, -1);
+  c->f_nfo.assign((size_t)P * NP, 0);
+  for (uint32_t p = 0; p < P; p++) {
+    const uint32_t v = e.var_begin[p];  // the pod as given (no relaxation)
+    for (uint32_t t = 0; t < e.T; t++) {
+      const uint32_t np = e.tmpl[t].np_index;
+      const size_t src = (size_t)v * e.T + t, dst = (size_t)p * NP + np;
+      std::memcpy(&c->f_rows[dst * W], &rows[src * W], W * 8);
+      c->f_cheapest[dst] = ch[src] == gsd::NONE ? -1 : (int32_t)ch[src];
+      c->f_nfo[dst] = nfo[src];
+    }
+  }
+  std::memset(out, 0, sizeof(*out));
+  out->n_pods = P;
+  out->n_nodepools = NP;
+  out->n_its = e.N;
+  out->words = W;
+  out->rows = c->f_rows.data();
+  out->cheapest_it = c->f_cheapest.data();
+  out->n_feasible_offerings = c->f_nfo.data();
+  out->checks = e.checks;
+  out->t_kernel_ms = ms;
+  return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,877 @@
+// encode.cpp — host encoder for the MI355X provisioning solve.
+//
+// Turns gs_problem (what Go's GetInstanceTypes + NewScheduler inputs carry,
+// reference pkg/cloudprovider/cloudprovider.go:553-583) into the bitset/SoA
+// layout of layout.hpp.  The requirement algebra here restates <U>
+// sigs.k8s.io/karpenter pkg/scheduling (Requirement.Intersection/Has/Len/
+// Operator, Requirements.Compatible/Intersects) on vocabulary bitsets; it is
+// independent of the oracle's string-set restatement (oracle/solve.cpp).
+#include "encode.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <functional>
+#include <tuple>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <set>
+#include <stdexcept>
+
+namespace gsh {
+namespace {
+
+const char* kZone = "topology.kubernetes.io/zone";
+const char* kCapacityType = "karpenter.sh/capacity-type";
+const char* kHostname = "kubernetes.io/hostname";
+const char* kNodePool = "karpenter.sh/nodepool";
+const char* kPNS = "PreferNoSchedule";
+const char* kOmega = "\x01<unmentioned>";
+
+// <U> v1.WellKnownLabels + IBM keys (reference pkg/apis/v1alpha1/labels.go:37-45)
+bool is_wellknown(const std::string& k) {
+  static const std::set<std::string> s = {
+      "karpenter.sh/nodepool",           "topology.kubernetes.io/zone",      "topology.kubernetes.io/region",
+      "node.kubernetes.io/instance-type", "kubernetes.io/arch",              "kubernetes.io/os",
+      "karpenter.sh/capacity-type",       "node.kubernetes.io/windows-build", "karpenter-ibm.sh/instance-size",
+      "karpenter-ibm.sh/instance-family", "karpenter-ibm.sh/instance-cpu",   "karpenter-ibm.sh/instance-memory"};
+  return s.count(k) != 0;
+}
+
+std::string normalize(const std::string& k) {
+  if (k == "failure-domain.beta.kubernetes.io/zone") return kZone;
+  if (k == "failure-domain.beta.kubernetes.io/region") return "topology.kubernetes.io/region";
+  if (k == "beta.kubernetes.io/arch") return "kubernetes.io/arch";
+  if (k == "beta.kubernetes.io/instance-type") return "node.kubernetes.io/instance-type";
+  if (k == "beta.kubernetes.io/os") return "kubernetes.io/os";
+  return k;
+}
+
+// strconv.Atoi
+bool atoi64(const std::string& s, int64_t* out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i == s.size()) return false;
+  unsigned __int128 v = 0;
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > (unsigned __int128)INT64_MAX + 1) return false;
+  }
+  if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+  *out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+struct Fail {
+  gs_status code;
+  std::string msg;
+};
+
+// values of a vocabulary within (gt, lt)
+Bits within_mask(const Vocab& v, bool hg, int64_t gt, bool hl, int64_t lt) {
+  Bits b(v.words());
+  for (size_t i = 0; i < v.size(); i++) {
+    if (!hg && !hl) {
+      b.set(i);
+      continue;
+    }
+    if (!v.isint[i]) continue;
+    if (hg && gt >= v.ival[i]) continue;
+    if (hl && lt <= v.ival[i]) continue;
+    b.set(i);
+  }
+  return b;
+}
+
+Bits all_bits(const Vocab& v) { return within_mask(v, false, 0, false, 0); }
+
+}  // namespace
+
+KReq kreq_intersect(const Vocab& v, const KReq& a, const KReq& b) {
+  KReq r;
+  r.comp = a.comp && b.comp;
+  r.hg = a.hg || b.hg;
+  r.gt = a.hg && b.hg ? std::max(a.gt, b.gt) : (a.hg ? a.gt : b.gt);
+  r.hl = a.hl || b.hl;
+  r.lt = a.hl && b.hl ? std::min(a.lt, b.lt) : (a.hl ? a.lt : b.lt);
+  if (r.hg && r.hl && r.gt >= r.lt) {  // DoesNotExist
+    KReq d;
+    d.comp = false;
+    d.has = Bits(v.words());
+    d.excl = Bits(v.words());
+    return d;
+  }
+  r.has = a.has;
+  r.has &= b.has;
+  r.excl = Bits(v.words());
+  if (r.comp) {
+    r.excl = a.excl;
+    r.excl |= b.excl;
+    r.excl &= within_mask(v, r.hg, r.gt, r.hl, r.lt);
+  } else {
+    r.hg = r.hl = false;
+    r.gt = r.lt = 0;
+  }
+  return r;
+}
+
+namespace {
+
+bool len_zero(const KReq& q) { return !q.comp && q.has.none(); }
+int op_of(const KReq& q) {
+  if (q.comp) return q.excl.none() ? GS_OP_EXISTS : GS_OP_NOTIN;
+  return q.has.none() ? GS_OP_DOES_NOT_EXIST : GS_OP_IN;
+}
+bool exempt(const KReq& q) {
+  int o = op_of(q);
+  return o == GS_OP_NOTIN || o == GS_OP_DOES_NOT_EXIST;
+}
+
+KReq make_kreq(const Vocab& v, int op, const std::vector<uint32_t>& vals, int64_t bound) {
+  KReq q;
+  q.has = Bits(v.words());
+  q.excl = Bits(v.words());
+  switch (op) {
+    case GS_OP_IN:
+      q.comp = false;
+      for (auto x : vals) q.has.set(x);
+      break;
+    case GS_OP_NOTIN:
+      q.comp = true;
+      for (auto x : vals) q.excl.set(x);
+      q.has = all_bits(v);
+      for (auto x : vals) q.has.reset(x);
+      break;
+    case GS_OP_EXISTS:
+      q.comp = true;
+      q.has = all_bits(v);
+      break;
+    case GS_OP_DOES_NOT_EXIST:
+      q.comp = false;
+      break;
+    case GS_OP_GT:
+      q.comp = true;
+      q.hg = true;
+      q.gt = bound;
+      q.has = within_mask(v, true, bound, false, 0);
+      break;
+    case GS_OP_LT:
+      q.comp = true;
+      q.hl = true;
+      q.lt = bound;
+      q.has = within_mask(v, false, 0, true, bound);
+      break;
+  }
+  return q;
+}
+
+}  // namespace
+
+void reqs_add(const Encoded& e, Reqs& r, uint32_t key, const KReq& q) {
+  auto it = r.find(key);
+  if (it == r.end()) r.emplace(key, q);
+  else it->second = kreq_intersect(e.keys[key].vocab, q, it->second);
+}
+
+namespace {
+
+void reqs_add_all(const Encoded& e, Reqs& r, const Reqs& o) {
+  for (auto& kv : o) reqs_add(e, r, kv.first, kv.second);
+}
+
+// <U> Requirements.Compatible(incoming, AllowUndefinedWellKnownLabels if allow_wk)
+bool reqs_compatible(const Encoded& e, const Reqs& r, const Reqs& in, bool allow_wk) {
+  for (auto& kv : in) {
+    if (allow_wk && e.keys[kv.first].wellknown) continue;
+    if (r.count(kv.first)) continue;
+    if (exempt(kv.second)) continue;
+    return false;
+  }
+  for (auto& kv : in) {
+    auto it = r.find(kv.first);
+    if (it == r.end()) continue;
+    KReq x = kreq_intersect(e.keys[kv.first].vocab, it->second, kv.second);
+    if (len_zero(x) && !(exempt(it->second) && exempt(kv.second))) return false;
+  }
+  return true;
+}
+
+struct Ctx {
+  const gs_problem* p;
+  Encoded& e;
+  std::vector<std::string> strs;
+
+  const std::string& S(uint32_t id) const {
+    if (id >= strs.size()) throw Fail{GS_E_INVALID, "string id out of range"};
+    return strs[id];
+  }
+  void chk(gs_range r, uint32_t n, const char* what) const {
+    if ((uint64_t)r.begin + r.count > n) throw Fail{GS_E_INVALID, std::string("range out of bounds: ") + what};
+  }
+
+  // ---------------------------------------------------------- vocabulary
+  std::map<std::string, std::set<std::string>> mentions;
+
+  void mention(const std::string& key, const std::string& val) { mentions[normalize(key)].insert(val); }
+  void mention_key(const std::string& key) { mentions[normalize(key)]; }
+  void mention_reqs(gs_range r) {
+    chk(r, p->n_reqs, "reqs");
+    for (uint32_t i = 0; i < r.count; i++) {
+      auto& q = p->reqs[r.begin + i];
+      if (q.op > GS_OP_LT) throw Fail{GS_E_UNSUPPORTED, "Gte/Lte requirement operators"};
+      if (q.min_values >= 0) throw Fail{GS_E_UNSUPPORTED, "minValues"};
+      chk(q.values, p->n_value_ids, "values");
+      mention_key(S(q.key));
+      if (q.op == GS_OP_IN || q.op == GS_OP_NOTIN)
+        for (uint32_t k = 0; k < q.values.count; k++) {
+          const std::string& v = S(p->value_ids[q.values.begin + k]);
+          if (normalize(S(q.key)) == kHostname && v.rfind("hostname-placeholder-", 0) == 0)
+            throw Fail{GS_E_UNSUPPORTED, "requirement names a hostname placeholder"};
+          mention(S(q.key), v);
+        }
+      if (q.op == GS_OP_GT || q.op == GS_OP_LT) {
+        int64_t x;
+        if (q.values.count < 1 || !atoi64(S(p->value_ids[q.values.begin]), &x))
+          throw Fail{GS_E_INVALID, "Gt/Lt value is not an integer"};
+      }
+    }
+  }
+  void mention_labels(gs_range r) {
+    chk(r, p->n_labels, "labels");
+    for (uint32_t i = 0; i < r.count; i++) mention(S(p->labels[r.begin + i].key), S(p->labels[r.begin + i].value));
+  }
+
+  void build_vocab() {
+    mention_key(kZone);
+    mention_key(kCapacityType);
+    mention_key(kHostname);
+    mention_key(kNodePool);
+    for (uint32_t i = 0; i < p->n_instance_types; i++) {
+      auto& it = p->instance_types[i];
+      mention_reqs(it.requirements);
+      chk(it.offerings, p->n_offerings, "offerings");
+      for (uint32_t k = 0; k < it.offerings.count; k++) mention_reqs(p->offerings[it.offerings.begin + k].requirements);
+    }
+    for (uint32_t i = 0; i < p->n_nodepools; i++) {
+      auto& np = p->nodepools[i];
+      mention_reqs(np.requirements);
+      mention_labels(np.labels);
+      mention(kNodePool, S(np.name));
+    }
+    for (uint32_t i = 0; i < p->n_pods; i++) {
+      auto& pd = p->pods[i];
+      mention_labels(pd.node_selector);
+      chk(pd.required_terms, p->n_terms, "terms");
+      chk(pd.preferred_terms, p->n_terms, "terms");
+      for (uint32_t k = 0; k < pd.required_terms.count; k++) mention_reqs(p->terms[pd.required_terms.begin + k].requirements);
+      for (uint32_t k = 0; k < pd.preferred_terms.count; k++)
+        mention_reqs(p->terms[pd.preferred_terms.begin + k].requirements);
+    }
+    for (auto& kv : mentions) {
+      Key k;
+      k.name = kv.first;
+      k.wellknown = is_wellknown(kv.first);
+      for (auto& v : kv.second) {
+        k.vocab.id[v] = (uint32_t)k.vocab.vals.size();
+        k.vocab.vals.push_back(v);
+      }
+      k.vocab.omega = (uint32_t)k.vocab.vals.size();
+      k.vocab.vals.push_back(kOmega);
+      for (auto& v : k.vocab.vals) {
+        int64_t x = 0;
+        bool ok = v != kOmega && atoi64(v, &x);
+        k.vocab.isint.push_back(ok);
+        k.vocab.ival.push_back(x);
+      }
+      e.key_id[k.name] = (uint32_t)e.keys.size();
+      e.keys.push_back(std::move(k));
+    }
+    e.k_zone = e.key_id[kZone];
+    e.k_ct = e.key_id[kCapacityType];
+    e.k_hostname = e.key_id[kHostname];
+    e.k_nodepool = e.key_id[kNodePool];
+  }
+
+  uint32_t key_of(uint32_t sid) const { return e.key_id.at(normalize(S(sid))); }
+
+  KReq kreq_of(const gs_requirement& q) const {
+    uint32_t k = key_of(q.key);
+    const Vocab& v = e.keys[k].vocab;
+    std::vector<uint32_t> vals;
+    int64_t bound = 0;
+    if (q.op == GS_OP_IN || q.op == GS_OP_NOTIN)
+      for (uint32_t i = 0; i < q.values.count; i++) vals.push_back(v.id.at(S(p->value_ids[q.values.begin + i])));
+    if (q.op == GS_OP_GT || q.op == GS_OP_LT) atoi64(S(p->value_ids[q.values.begin]), &bound);
+    return make_kreq(v, (int)q.op, vals, bound);
+  }
+  Reqs reqs_of(gs_range r) const {
+    Reqs out;
+    for (uint32_t i = 0; i < r.count; i++) {
+      auto& q = p->reqs[r.begin + i];
+      reqs_add(e, out, key_of(q.key), kreq_of(q));
+    }
+    return out;
+  }
+  KReq in_one(uint32_t key, const std::string& val) const {
+    const Vocab& v = e.keys[key].vocab;
+    return make_kreq(v, GS_OP_IN, {v.id.at(val)}, 0);
+  }
+  Reqs labels_reqs(gs_range r) const {
+    Reqs out;
+    for (uint32_t i = 0; i < r.count; i++) {
+      uint32_t k = key_of(p->labels[r.begin + i].key);
+      reqs_add(e, out, k, in_one(k, S(p->labels[r.begin + i].value)));
+    }
+    return out;
+  }
+
+  // ----------------------------------------------------------- catalog
+  void build_catalog() {
+    e.N = p->n_instance_types;
+    e.W = (e.N + 63) / 64;
+    if (e.N == 0) throw Fail{GS_E_INVALID, "empty catalog"};
+    // IT keys: the key set of IT 0; every IT must carry exactly those keys,
+    // each single-valued In (reference instancetype.go:721-726)
+    std::vector<uint32_t> k0;
+    for (uint32_t i = 0; i < e.N; i++) {
+      auto& it = p->instance_types[i];
+      std::vector<uint32_t> ks;
+      for (uint32_t k = 0; k < it.requirements.count; k++) {
+        auto& q = p->reqs[it.requirements.begin + k];
+        if (q.op != GS_OP_IN || q.values.count != 1)
+          throw Fail{GS_E_UNSUPPORTED, "instance type requirement is not single-valued In"};
+        ks.push_back(key_of(q.key));
+      }
+      std::sort(ks.begin(), ks.end());
+      if (std::adjacent_find(ks.begin(), ks.end()) != ks.end())
+        throw Fail{GS_E_UNSUPPORTED, "instance type repeats a requirement key"};
+      if (i == 0) k0 = ks;
+      else if (ks != k0) throw Fail{GS_E_UNSUPPORTED, "instance types carry different requirement keys"};
+    }
+    for (auto k : k0) {
+      if (k == e.k_zone || k == e.k_ct || k == e.k_hostname)
+        throw Fail{GS_E_UNSUPPORTED, "instance type requirement on zone/capacity-type/hostname"};
+      e.keys[k].cls = KEY_IT;
+      e.keys[k].slot = (int)e.it_keys.size();
+      e.it_keys.push_back(k);
+    }
+    e.K = (uint32_t)e.it_keys.size();
+    if (e.K > (uint32_t)gsd::KMAX_IT) throw Fail{GS_E_UNSUPPORTED, "too many instance-type keys"};
+    e.keys[e.k_zone].cls = KEY_ZONE;
+    e.keys[e.k_ct].cls = KEY_CT;
+    // catalog zones / capacity types in first-appearance order
+    std::map<uint32_t, uint32_t> zmap, cmap;
+    struct Off {
+      uint32_t z, c;
+      double price;
+      bool avail;
+    };
+    std::vector<std::vector<Off>> offs(e.N);
+    for (uint32_t i = 0; i < e.N; i++) {
+      auto& it = p->instance_types[i];
+      if (it.offerings.count > (uint32_t)gsd::SMAX) throw Fail{GS_E_UNSUPPORTED, "too many offerings per instance type"};
+      for (uint32_t s = 0; s < it.offerings.count; s++) {
+        auto& o = p->offerings[it.offerings.begin + s];
+        uint32_t zv = gsd::NONE, cv = gsd::NONE;
+        for (uint32_t k = 0; k < o.requirements.count; k++) {
+          auto& q = p->reqs[o.requirements.begin + k];
+          uint32_t key = key_of(q.key);
+          if (q.op != GS_OP_IN || q.values.count != 1) throw Fail{GS_E_UNSUPPORTED, "offering requirement not single In"};
+          uint32_t vid = e.keys[key].vocab.id.at(S(p->value_ids[q.values.begin]));
+          if (key == e.k_zone && zv == gsd::NONE) zv = vid;
+          else if (key == e.k_ct && cv == gsd::NONE) cv = vid;
+          else throw Fail{GS_E_UNSUPPORTED, "offering requirements other than one zone and one capacity type"};
+        }
+        if (zv == gsd::NONE || cv == gsd::NONE) throw Fail{GS_E_UNSUPPORTED, "offering without zone or capacity type"};
+        if (std::isnan(o.price)) throw Fail{GS_E_UNSUPPORTED, "NaN offering price"};
+        if (!zmap.count(zv)) {
+          uint32_t n = (uint32_t)zmap.size();
+          zmap[zv] = n;
+          e.cat_zone.push_back(zv);
+        }
+        if (!cmap.count(cv)) {
+          uint32_t n = (uint32_t)cmap.size();
+          cmap[cv] = n;
+          e.cat_ct.push_back(cv);
+        }
+        offs[i].push_back({zmap[zv], cmap[cv], o.price, o.available != 0});
+      }
+    }
+    e.Z = (uint32_t)e.cat_zone.size();
+    e.C = (uint32_t)e.cat_ct.size();
+    if (e.Z * e.C > 64) throw Fail{GS_E_UNSUPPORTED, "zones x capacity types > 64"};
+    // resources
+    std::set<std::string> rn;
+    for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(S(p->quantities[i].resource));
+    e.res_names.assign(rn.begin(), rn.end());
+    e.R = (uint32_t)e.res_names.size();
+    if (e.R > (uint32_t)gsd::RMAX) throw Fail{GS_E_UNSUPPORTED, "more than 8 distinct resources"};
+    std::unordered_map<std::string, uint32_t> rid;
+    for (uint32_t r = 0; r < e.R; r++) rid[e.res_names[r]] = r;
+    for (auto& nm : e.res_names) {
+      uint32_t sid = 0;
+      for (uint32_t i = 0; i < strs.size(); i++)
+        if (strs[i] == nm) {
+          sid = i;
+          break;
+        }
+      e.res_name_ids.push_back(sid);
+    }
+    rid_map = rid;
+    auto resvec = [this](gs_range r, int64_t* out, bool* present) { resvec_fn(r, out, present); };
+    // per IT arrays
+    e.it_vid.assign((size_t)e.K * e.N, 0);
+    e.it_alloc.assign((size_t)e.R * e.N, 0);
+    e.it_cap.assign((size_t)e.R * e.N, 0);
+    e.it_pair.assign(e.N, 0);
+    e.it_prank.assign((size_t)e.N * 64, gsd::NONE);
+    // price ranks
+    std::vector<double> prices;
+    for (auto& v : offs)
+      for (auto& o : v) prices.push_back(o.price);
+    std::sort(prices.begin(), prices.end());
+    prices.erase(std::unique(prices.begin(), prices.end(), [](double a, double b) { return a == b; }), prices.end());
+    auto prank = [&](double x) {
+      return (uint32_t)(std::lower_bound(prices.begin(), prices.end(), x) - prices.begin());
+    };
+    std::vector<uint8_t> ok(e.N, 1);
+    for (uint32_t i = 0; i < e.N; i++) {
+      auto& it = p->instance_types[i];
+      for (uint32_t k = 0; k < it.requirements.count; k++) {
+        auto& q = p->reqs[it.requirements.begin + k];
+        uint32_t key = key_of(q.key);
+        e.it_vid[(size_t)e.keys[key].slot * e.N + i] = e.keys[key].vocab.id.at(S(p->value_ids[q.values.begin]));
+      }
+      int64_t cap[gsd::RMAX] = {0}, ovh[gsd::RMAX] = {0};
+      bool capp[gsd::RMAX] = {false}, ovhp[gsd::RMAX] = {false};
+      resvec(it.capacity, cap, capp);
+      resvec(it.overhead, ovh, ovhp);
+      for (uint32_t r = 0; r < e.R; r++) {
+        // Allocatable = Subtract(Capacity, Overhead.Total()) over capacity keys
+        int64_t a = capp[r] ? cap[r] - (ovhp[r] ? ovh[r] : 0) : 0;
+        e.it_alloc[(size_t)r * e.N + i] = a;
+        e.it_cap[(size_t)r * e.N + i] = cap[r];
+        if (capp[r] && a < 0) ok[i] = 0;  // <U> Fits: any negative total never fits
+      }
+      uint64_t seen = 0;
+      for (auto& o : offs[i]) {
+        uint32_t g = o.z * e.C + o.c;
+        if (seen >> g & 1) throw Fail{GS_E_UNSUPPORTED, "instance type repeats a (zone, capacity type) offering"};
+        seen |= 1ull << g;
+        if (o.avail) {
+          e.it_pair[i] |= 1ull << g;
+          e.it_prank[(size_t)i * 64 + g] = prank(o.price);
+        }
+      }
+      if (!ok[i]) e.it_pair[i] = 0;  // never selectable
+    }
+    it_ok.assign(e.W, 0);
+    for (uint32_t i = 0; i < e.N; i++)
+      if (ok[i]) it_ok[i / 64] |= 1ull << (i % 64);
+    // name ranks (Go string order = bytewise)
+    std::vector<uint32_t> order(e.N);
+    std::iota(order.begin(), order.end(), 0);
+    std::vector<std::string> names(e.N);
+    for (uint32_t i = 0; i < e.N; i++) names[i] = S(p->instance_types[i].name);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return names[a] < names[b]; });
+    for (uint32_t i = 0; i + 1 < e.N; i++)
+      if (names[order[i]] == names[order[i + 1]]) throw Fail{GS_E_INVALID, "duplicate instance type name"};
+    e.it_namerank.assign(e.N, 0);
+    e.rank_to_it = order;
+    for (uint32_t r = 0; r < e.N; r++) e.it_namerank[order[r]] = r;
+    // slot sets
+    e.slot_set.assign((size_t)64 * e.W, 0);
+    for (uint32_t i = 0; i < e.N; i++)
+      for (uint32_t g = 0; g < 64; g++)
+        if (e.it_pair[i] >> g & 1) e.slot_set[(size_t)g * e.W + i / 64] |= 1ull << (i % 64);
+    // fit thresholds per resource over selectable ITs
+    e.thr_off.assign(e.R + 1, 0);
+    std::vector<std::vector<int64_t>> vals(e.R);
+    for (uint32_t r = 0; r < e.R; r++) {
+      for (uint32_t i = 0; i < e.N; i++)
+        if (ok[i]) vals[r].push_back(e.it_alloc[(size_t)r * e.N + i]);
+      std::sort(vals[r].begin(), vals[r].end());
+      vals[r].erase(std::unique(vals[r].begin(), vals[r].end()), vals[r].end());
+      e.thr_off[r + 1] = e.thr_off[r] + (uint32_t)vals[r].size();
+    }
+    e.thr_val.clear();
+    for (uint32_t r = 0; r < e.R; r++) e.thr_val.insert(e.thr_val.end(), vals[r].begin(), vals[r].end());
+    // thr_set: for resource r, m in [0, n_r]: rows at (thr_off[r] + r + m)
+    e.thr_set.assign((size_t)(e.thr_off[e.R] + e.R) * e.W, 0);
+    for (uint32_t r = 0; r < e.R; r++)
+      for (uint32_t m = 0; m < vals[r].size(); m++) {
+        uint64_t* row = &e.thr_set[(size_t)(e.thr_off[r] + r + m) * e.W];
+        for (uint32_t i = 0; i < e.N; i++)
+          if (ok[i] && e.it_alloc[(size_t)r * e.N + i] >= vals[r][m]) row[i / 64] |= 1ull << (i % 64);
+      }
+  }
+  std::vector<uint64_t> it_ok;
+  std::unordered_map<std::string, uint32_t> rid_map;
+  void resvec_fn(gs_range r, int64_t* out, bool* present) const {
+    chk(r, p->n_quantities, "quantities");
+    for (uint32_t k = 0; k < r.count; k++) {
+      auto& q = p->quantities[r.begin + k];
+      uint32_t x = rid_map.at(S(q.resource));
+      out[x] += q.milli;
+      if (present) present[x] = true;
+    }
+  }
+
+  // ----------------------------------------------------- helpers on Reqs
+  uint64_t zone_has(const Reqs& r) const {
+    auto it = r.find(e.k_zone);
+    uint64_t m = 0;
+    for (uint32_t z = 0; z < e.Z; z++)
+      if (it == r.end() || it->second.has.test(e.cat_zone[z])) m |= 1ull << z;
+    return m;
+  }
+  uint64_t ct_has(const Reqs& r) const {
+    auto it = r.find(e.k_ct);
+    uint64_t m = 0;
+    for (uint32_t c = 0; c < e.C; c++)
+      if (it == r.end() || it->second.has.test(e.cat_ct[c])) m |= 1ull << c;
+    return m;
+  }
+  uint64_t grid(uint64_t zm, uint64_t cm) const {
+    uint64_t g = 0;
+    for (uint32_t z = 0; z < e.Z; z++)
+      if (zm >> z & 1) g |= (cm & ((1ull << e.C) - 1)) << (z * e.C);
+    return g;
+  }
+  // compat(IT, reqs) over IT keys: <U> it.Requirements.Intersects(reqs)
+  bool it_compat(uint32_t i, const Reqs& r) const {
+    for (uint32_t k = 0; k < e.K; k++) {
+      auto f = r.find(e.it_keys[k]);
+      if (f == r.end()) continue;
+      if (!f->second.has.test(e.it_vid[(size_t)k * e.N + i])) return false;
+    }
+    return true;
+  }
+  gsd::FK to_fk(const KReq& q) const {
+    gsd::FK f{};
+    f.has = q.has.w.empty() ? 0 : q.has.w[0];
+    f.excl = q.excl.w.empty() ? 0 : q.excl.w[0];
+    f.gt = q.gt;
+    f.lt = q.lt;
+    f.flags = gsd::FK_PRESENT | (q.comp ? gsd::FK_COMP : 0) | (q.hg ? gsd::FK_GT : 0) | (q.hl ? gsd::FK_LT : 0);
+    return f;
+  }
+
+  // ----------------------------------------------------------- taints
+  struct TaintKey {
+    std::string k, v, eff;
+    bool operator<(const TaintKey& o) const { return std::tie(k, v, eff) < std::tie(o.k, o.v, o.eff); }
+  };
+  std::map<TaintKey, uint32_t> taint_id;
+  std::vector<TaintKey> taint_list;
+  uint64_t taint_mask(gs_range r) {
+    chk(r, p->n_taints, "taints");
+    uint64_t m = 0;
+    for (uint32_t i = 0; i < r.count; i++) {
+      auto& t = p->taints[r.begin + i];
+      TaintKey tk{S(t.key), S(t.value), S(t.effect)};
+      auto f = taint_id.find(tk);
+      uint32_t id;
+      if (f == taint_id.end()) {
+        id = (uint32_t)taint_list.size();
+        if (id >= 64) throw Fail{GS_E_UNSUPPORTED, "more than 64 distinct taints"};
+        taint_id[tk] = id;
+        taint_list.push_back(tk);
+      } else {
+        id = f->second;
+      }
+      m |= 1ull << id;
+    }
+    return m;
+  }
+  struct Tol {
+    std::string k, v, eff;
+    uint32_t op;
+  };
+  uint64_t tol_mask(const std::vector<Tol>& tols) const {
+    uint64_t m = 0;
+    for (uint32_t id = 0; id < taint_list.size(); id++) {
+      auto& tn = taint_list[id];
+      for (auto& t : tols) {
+        // corev1 Toleration.ToleratesTaint
+        if (!t.eff.empty() && t.eff != tn.eff) continue;
+        if (!t.k.empty() && t.k != tn.k) continue;
+        if (t.op == GS_TOL_EQUAL ? t.v == tn.v : t.op == GS_TOL_EXISTS) {
+          m |= 1ull << id;
+          break;
+        }
+      }
+    }
+    return m;
+  }
+
+  // --------------------------------------------------------- templates
+  bool tolerate_pns = false;
+  void build_templates() {
+    std::vector<uint32_t> order(p->n_nodepools);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      auto& A = p->nodepools[a];
+      auto& B = p->nodepools[b];
+      if (A.weight == B.weight) return S(A.name) < S(B.name);
+      return A.weight > B.weight;
+    });
+    for (uint32_t npi : order) {
+      auto& np = p->nodepools[npi];
+      Reqs npreqs = reqs_of(np.requirements);
+      // NewNodeClaimTemplate: spec requirements + labels + nodepool label
+      Reqs tr = npreqs;
+      std::map<std::string, std::string> labels;
+      for (uint32_t i = 0; i < np.labels.count; i++)
+        labels[S(p->labels[np.labels.begin + i].key)] = S(p->labels[np.labels.begin + i].value);
+      labels[kNodePool] = S(np.name);
+      for (auto& kv : labels) {
+        uint32_t k = e.key_id.at(normalize(kv.first));
+        reqs_add(e, tr, k, in_one(k, kv.second));
+      }
+      uint64_t zm = zone_has(tr), cm = ct_has(tr), G = grid(zm, cm);
+      // GetInstanceTypes filter + NewScheduler pre-filter (compat, fits({}), offering)
+      chk(np.instance_types, p->n_it_refs, "it_refs");
+      for (uint32_t k = 0; k < np.instance_types.count; k++) {
+        uint32_t i = p->it_refs[np.instance_types.begin + k];
+        if (i < e.N) e.checks_per_pod += p->instance_types[i].offerings.count;
+      }
+      std::vector<uint64_t> opts(e.W, 0);
+      bool any = false;
+      for (uint32_t k = 0; k < np.instance_types.count; k++) {
+        uint32_t i = p->it_refs[np.instance_types.begin + k];
+        if (i >= e.N) throw Fail{GS_E_INVALID, "it_ref out of range"};
+        if (!(it_ok[i / 64] >> (i % 64) & 1)) continue;
+        Reqs itr;
+        for (uint32_t kk = 0; kk < e.K; kk++)
+          itr.emplace(e.it_keys[kk], in_one(e.it_keys[kk], e.keys[e.it_keys[kk]].vocab.vals[e.it_vid[(size_t)kk * e.N + i]]));
+        if (!reqs_compatible(e, npreqs, itr, true)) continue;
+        if (!it_compat(i, tr)) continue;
+        if (!(e.it_pair[i] & G)) continue;
+        opts[i / 64] |= 1ull << (i % 64);
+        any = true;
+      }
+      uint64_t tm = taint_mask(np.taints);
+      if (!any) continue;
+      if (e.T >= (uint32_t)gsd::TMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 NodePools"};
+      gsd::TmplRec t{};
+      t.np_index = npi;
+      t.zm = zm;
+      t.cm = cm;
+      t.taints = tm;
+      bool present[gsd::RMAX] = {false};
+      resvec_fn(np.daemon_requests, t.daemon, nullptr);
+      if (np.has_limits) {
+        t.has_limits = 1;
+        resvec_fn(np.limits, t.limits, present);
+        for (uint32_t r = 0; r < e.R; r++)
+          if (present[r]) t.limit_rmask |= 1u << r;
+      }
+      for (uint32_t i = 0; i < np.taints.count; i++)
+        if (S(p->taints[np.taints.begin + i].effect) == kPNS) tolerate_pns = true;
+      // NewNodeClaim adds hostname In[placeholder]
+      reqs_add(e, tr, e.k_hostname, make_kreq(e.keys[e.k_hostname].vocab, GS_OP_IN, {e.keys[e.k_hostname].vocab.omega}, 0));
+      e.tmpl.push_back(t);
+      e.t_opts.insert(e.t_opts.end(), opts.begin(), opts.end());
+      e.tmpl_reqs.push_back(tr);
+      e.T++;
+    }
+  }
+
+  // --------------------------------------------------------------- pods
+  void build_free_slots() {
+    for (uint32_t k = 0; k < e.keys.size(); k++) {
+      if (e.keys[k].cls != KEY_FREE) continue;
+      if (e.keys[k].vocab.size() > 64) throw Fail{GS_E_UNSUPPORTED, "free key vocabulary > 63 values: " + e.keys[k].name};
+      if (e.free_keys.size() >= (size_t)gsd::FMAX) throw Fail{GS_E_UNSUPPORTED, "more than 16 free requirement keys"};
+      e.keys[k].slot = (int)e.free_keys.size();
+      if (e.keys[k].wellknown) e.wk_slots |= 1ull << e.free_keys.size();
+      e.free_keys.push_back(k);
+    }
+    e.F = (uint32_t)e.free_keys.size();
+    e.fk_ival.assign((size_t)std::max<uint32_t>(e.F, 1) * 64, 0);
+    e.fk_isint.assign(std::max<uint32_t>(e.F, 1), 0);
+    for (uint32_t s = 0; s < e.F; s++) {
+      auto& v = e.keys[e.free_keys[s]].vocab;
+      for (uint32_t i = 0; i < v.size(); i++) {
+        e.fk_ival[(size_t)s * 64 + i] = v.ival[i];
+        if (v.isint[i]) e.fk_isint[s] |= 1ull << i;
+      }
+    }
+    e.t_fk.assign((size_t)e.T * std::max<uint32_t>(e.F, 1), gsd::FK{});
+    for (uint32_t t = 0; t < e.T; t++)
+      for (auto& kv : e.tmpl_reqs[t])
+        if (e.keys[kv.first].cls == KEY_FREE)
+          e.t_fk[(size_t)t * e.F + e.keys[kv.first].slot] = to_fk(kv.second);
+  }
+
+  void build_pods() {
+    e.P = p->n_pods;
+    std::unordered_map<std::string, uint32_t> uid_seen;
+    e.pod_req.assign((size_t)e.P * e.R, 0);
+    std::vector<int64_t> cpu(e.P, 0), mem(e.P, 0);
+    auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
+    for (uint32_t i = 0; i < e.P; i++) {
+      auto& pd = p->pods[i];
+      if (pd.flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
+      if (!uid_seen.emplace(S(pd.uid), i).second) throw Fail{GS_E_INVALID, "duplicate pod uid"};
+      resvec_fn(pd.requests, &e.pod_req[(size_t)i * e.R], nullptr);
+      if (rc != rid_map.end()) cpu[i] = e.pod_req[(size_t)i * e.R + rc->second];
+      if (rmm != rid_map.end()) mem[i] = e.pod_req[(size_t)i * e.R + rmm->second];
+      // spec pieces
+      Reqs ns = labels_reqs(pd.node_selector);
+      std::vector<Reqs> req_terms;
+      for (uint32_t k = 0; k < pd.required_terms.count; k++)
+        req_terms.push_back(reqs_of(p->terms[pd.required_terms.begin + k].requirements));
+      std::vector<std::pair<int32_t, Reqs>> pref;
+      for (uint32_t k = 0; k < pd.preferred_terms.count; k++) {
+        auto& tm = p->terms[pd.preferred_terms.begin + k];
+        pref.push_back({tm.weight, reqs_of(tm.requirements)});
+      }
+      if (pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred node-affinity terms"};
+      // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
+      std::stable_sort(pref.begin(), pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+      chk(pd.tolerations, p->n_tolerations, "tolerations");
+      std::vector<Tol> tols;
+      for (uint32_t k = 0; k < pd.tolerations.count; k++) {
+        auto& t = p->tolerations[pd.tolerations.begin + k];
+        tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
+      }
+      e.var_begin.push_back((uint32_t)e.variants.size());
+      size_t ri = 0, pi = 0;
+      for (;;) {
+        // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
+        PodVariant v;
+        v.reqs = ns;
+        if (pi < pref.size()) reqs_add_all(e, v.reqs, pref[pi].second);
+        if (ri < req_terms.size()) reqs_add_all(e, v.reqs, req_terms[ri]);
+        v.tol = tol_mask(tols);
+        e.variants.push_back(std::move(v));
+        // <U> Preferences.Relax
+        if (req_terms.size() - ri > 1) {
+          ri++;
+          continue;
+        }
+        if (pi < pref.size()) {
+          pi++;
+          continue;
+        }
+        if (tolerate_pns) {
+          bool has = false;
+          for (auto& t : tols)
+            if (t.k.empty() && t.op == GS_TOL_EXISTS && t.v.empty() && t.eff == kPNS) has = true;
+          if (!has) {
+            tols.push_back({"", "", kPNS, GS_TOL_EXISTS});
+            continue;
+          }
+        }
+        break;
+      }
+      e.var_count.push_back((uint32_t)e.variants.size() - e.var_begin.back());
+    }
+    e.V = (uint32_t)e.variants.size();
+    // device variant records
+    e.vars.resize(e.V);
+    for (uint32_t i = 0; i < e.P; i++)
+      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
+        auto& pv = e.variants[v];
+        gsd::VarRec& vr = e.vars[v];
+        std::memset(&vr, 0, sizeof vr);
+        vr.pod = i;
+        for (int k = 0; k < gsd::KMAX_IT; k++) vr.itmask_off[k] = gsd::NONE;
+        for (uint32_t k = 0; k < e.K; k++) {
+          auto f = pv.reqs.find(e.it_keys[k]);
+          if (f == pv.reqs.end()) continue;
+          vr.itmask_off[k] = (uint32_t)e.itmask.size();
+          e.itmask.insert(e.itmask.end(), f->second.has.w.begin(), f->second.has.w.end());
+        }
+        vr.zm = zone_has(pv.reqs);
+        vr.cm = ct_has(pv.reqs);
+        vr.tol = pv.tol;
+        vr.fk_begin = (uint32_t)e.fk_entries.size();
+        for (auto& kv : pv.reqs)
+          if (e.keys[kv.first].cls == KEY_FREE) {
+            gsd::FKEntry fe{};
+            fe.slot = (uint32_t)e.keys[kv.first].slot;
+            fe.st = to_fk(kv.second);
+            e.fk_entries.push_back(fe);
+          }
+        vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
+      }
+    if (e.itmask.empty()) e.itmask.push_back(0);
+    if (e.fk_entries.empty()) e.fk_entries.push_back(gsd::FKEntry{});
+    // <U> NewQueue: cpu desc, memory desc, creationTimestamp asc, UID asc (total order)
+    e.queue0.resize(e.P);
+    std::iota(e.queue0.begin(), e.queue0.end(), 0);
+    std::sort(e.queue0.begin(), e.queue0.end(), [&](uint32_t a, uint32_t b) {
+      if (cpu[a] != cpu[b]) return cpu[a] > cpu[b];
+      if (mem[a] != mem[b]) return mem[a] > mem[b];
+      int64_t ta = p->pods[a].creation_ns, tb = p->pods[b].creation_ns;
+      if (ta != tb) return ta < tb;
+      return S(p->pods[a].uid) < S(p->pods[b].uid);
+    });
+    e.checks = (uint64_t)e.P * e.checks_per_pod;
+  }
+};
+
+}  // namespace
+
+std::string canonical(const Encoded& e, const Reqs& r) {
+  std::vector<std::pair<std::string, const KReq*>> items;
+  for (auto& kv : r) items.push_back({e.keys[kv.first].name, &kv.second});
+  std::sort(items.begin(), items.end(), [](auto& a, auto& b) { return a.first < b.first; });
+  static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+  std::string s;
+  for (auto& it : items) {
+    const KReq& q = *it.second;
+    const Vocab& v = e.keys[e.key_id.at(it.first)].vocab;
+    if (!s.empty()) s += '\n';
+    s += it.first;
+    s += '|';
+    s += opn[op_of(q)];
+    s += '|';
+    std::vector<std::string> vals;
+    const Bits& b = q.comp ? q.excl : q.has;
+    for (size_t i = 0; i < v.size(); i++)
+      if (b.test(i)) vals.push_back(v.vals[i]);
+    std::sort(vals.begin(), vals.end());
+    for (size_t i = 0; i < vals.size(); i++) {
+      if (i) s += ',';
+      s += vals[i];
+    }
+    s += '|';
+    s += q.comp && q.hg ? std::to_string(q.gt) : "-";
+    s += '|';
+    s += q.comp && q.hl ? std::to_string(q.lt) : "-";
+    s += "|-";
+  }
+  return s;
+}
+
+Err encode(const gs_problem* p, Encoded& e) {
+  e = Encoded();
+  Ctx c{p, e, {}};
+  try {
+    c.strs.reserve(p->n_strings);
+    for (uint32_t i = 0; i < p->n_strings; i++) c.strs.push_back(p->strings[i] ? p->strings[i] : "");
+    if (p->n_nodes) throw Fail{GS_E_UNSUPPORTED, "existing nodes are not supported by this build yet"};
+    c.build_vocab();
+    c.build_catalog();
+    c.build_templates();
+    c.build_free_slots();
+    c.build_pods();
+  } catch (const Fail& f) {
+    return Err{f.code, f.msg};
+  } catch (const std::out_of_range& ex) {
+    return Err{GS_E_INVALID, std::string("unknown vocabulary value: ") + ex.what()};
+  }
+  return Err{};
+}
+
+}  // namespace gsh

@@ -1,0 +1,129 @@
+// encode.hpp — host-side encoder: gs_problem (strings) -> label-vocabulary
+// bitsets + int64 SoA (layout.hpp), and the bitset requirement algebra used
+// to build templates / pod variants and to decode NodeClaim requirements.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gpusched.h"
+#include "layout.hpp"
+
+namespace gsh {
+
+// ------------------------------------------------------------------ bitsets
+struct Bits {
+  std::vector<uint64_t> w;
+  Bits() = default;
+  explicit Bits(size_t words) : w(words, 0) {}
+  bool test(size_t i) const { return (w[i >> 6] >> (i & 63)) & 1; }
+  void set(size_t i) { w[i >> 6] |= 1ull << (i & 63); }
+  void reset(size_t i) { w[i >> 6] &= ~(1ull << (i & 63)); }
+  bool none() const {
+    for (auto x : w)
+      if (x) return false;
+    return true;
+  }
+  size_t count() const {
+    size_t c = 0;
+    for (auto x : w) c += __builtin_popcountll(x);
+    return c;
+  }
+  Bits& operator&=(const Bits& o) {
+    for (size_t i = 0; i < w.size(); i++) w[i] &= o.w[i];
+    return *this;
+  }
+  Bits& operator|=(const Bits& o) {
+    for (size_t i = 0; i < w.size(); i++) w[i] |= o.w[i];
+    return *this;
+  }
+};
+
+// value vocabulary of one requirement key; the last entry is omega, a value
+// no requirement mentions (stands for hostname placeholders)
+struct Vocab {
+  std::vector<std::string> vals;
+  std::unordered_map<std::string, uint32_t> id;
+  std::vector<uint8_t> isint;
+  std::vector<int64_t> ival;
+  uint32_t omega = 0;
+  size_t words() const { return (vals.size() + 63) / 64; }
+  size_t size() const { return vals.size(); }
+};
+
+// Requirement on one key, as bitsets over the key's vocabulary.
+// Semantics follow <U> scheduling.Requirement: complement / values / bounds.
+struct KReq {
+  bool comp = true;
+  Bits has;   // Has(v) for every vocabulary value
+  Bits excl;  // complement sets: excluded values (after bound filtering)
+  bool hg = false, hl = false;
+  int64_t gt = 0, lt = 0;
+};
+
+enum KeyClass : uint8_t { KEY_IT = 0, KEY_ZONE = 1, KEY_CT = 2, KEY_FREE = 3 };
+
+struct Key {
+  std::string name;
+  Vocab vocab;
+  KeyClass cls = KEY_FREE;
+  bool wellknown = false;
+  int slot = -1;  // IT-key index or free slot
+};
+
+using Reqs = std::map<uint32_t, KReq>;  // key id -> requirement
+
+struct PodVariant {
+  Reqs reqs;
+  uint64_t tol = 0;
+};
+
+struct Encoded {
+  // vocabulary
+  std::vector<Key> keys;
+  std::unordered_map<std::string, uint32_t> key_id;
+  uint32_t k_zone = gsd::NONE, k_ct = gsd::NONE, k_hostname = gsd::NONE, k_nodepool = gsd::NONE;
+  std::vector<uint32_t> it_keys;    // key ids, IT key order
+  std::vector<uint32_t> free_keys;  // key ids, free slot order
+  std::vector<uint32_t> cat_zone;   // catalog zone id -> vocab id
+  std::vector<uint32_t> cat_ct;
+  std::vector<std::string> res_names;  // sorted
+  std::vector<uint32_t> res_name_ids;  // string ids
+  // sizes
+  uint32_t N = 0, W = 0, R = 0, Z = 0, C = 0, T = 0, F = 0, V = 0, P = 0, K = 0, NT = 0;
+  uint64_t wk_slots = 0;
+  uint64_t checks = 0;
+  uint64_t checks_per_pod = 0;
+  // device arrays (host copies)
+  std::vector<uint32_t> it_vid, it_prank, it_namerank, rank_to_it, thr_off;
+  std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
+  std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
+  std::vector<gsd::TmplRec> tmpl;
+  std::vector<uint64_t> t_opts;
+  std::vector<gsd::FK> t_fk;
+  std::vector<int64_t> pod_req;
+  std::vector<uint32_t> var_begin, var_count, queue0;
+  std::vector<gsd::VarRec> vars;
+  std::vector<uint64_t> itmask;
+  std::vector<gsd::FKEntry> fk_entries;
+  // host-only, for decode
+  std::vector<Reqs> tmpl_reqs;  // incl. hostname In[omega]
+  std::vector<PodVariant> variants;
+};
+
+// status + message
+struct Err {
+  gs_status code = GS_OK;
+  std::string msg;
+};
+
+Err encode(const gs_problem* p, Encoded& e);
+
+// algebra (exposed for decode)
+KReq kreq_intersect(const Vocab& v, const KReq& a, const KReq& b);
+void reqs_add(const Encoded& e, Reqs& r, uint32_t key, const KReq& q);
+std::string canonical(const Encoded& e, const Reqs& r);
+
+}  // namespace gsh

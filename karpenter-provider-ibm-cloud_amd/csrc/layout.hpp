@@ -1,0 +1,138 @@
+// layout.hpp — HBM layout shared by the host encoder and the gfx950 kernels.
+//
+// Everything the device touches is plain-old-data in structure-of-arrays form:
+//  * label vocabularies: every requirement key gets a value vocabulary; a
+//    requirement on a key becomes a "has" bitset over that vocabulary
+//    (Requirement.Has(v) for every vocabulary value) plus, for complement
+//    sets, the explicit excluded values and integer bounds;
+//  * instance types (ITs) are columns: one bit per IT in u64 words (W words);
+//  * offerings are folded per IT into a (zone x capacity-type) "pair" grid
+//    bitmask (Z*C <= 64 bits) of AVAILABLE offerings;
+//  * resources are int64 milli-units, R <= RMAX per vector.
+#pragma once
+#include <stdint.h>
+
+namespace gsd {
+
+constexpr int RMAX = 8;        // resource dimensions per vector
+constexpr int KMAX_IT = 8;     // requirement keys carried by instance types
+constexpr int FMAX = 16;       // "free" key slots (keys on neither ITs nor offerings)
+constexpr int TMAX = 64;       // NodeClaim templates (NodePools)
+constexpr int SMAX = 16;       // offerings per instance type
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// requirement on one free key, vocabulary <= 64 values (last one is the
+// "unmentioned value" omega used for hostname placeholders)
+enum : uint32_t { FK_PRESENT = 1u, FK_COMP = 2u, FK_GT = 4u, FK_LT = 8u };
+struct FK {
+  uint64_t has;   // Has(v) for each vocabulary value
+  uint64_t excl;  // complement: explicit excluded values (after bound filtering)
+  int64_t gt, lt; // bounds (complement sets only)
+  uint32_t flags;
+  uint32_t pad;
+};
+
+struct FKEntry {
+  uint32_t slot, pad;
+  FK st;
+};
+
+// one pod "variant": the pod's requirement set after k relaxations
+// (<U> Preferences.Relax is deterministic, so every variant is known up front)
+struct VarRec {
+  uint32_t pod;
+  uint32_t fk_begin, fk_count;
+  uint32_t pad;
+  uint32_t itmask_off[KMAX_IT];  // word offset into itmask arena, NONE = unconstrained
+  uint64_t zm, cm;               // Has over catalog zones / capacity types
+  uint64_t tol;                  // tolerated taint-vocabulary mask
+};
+
+struct TmplRec {
+  uint32_t np_index;
+  uint32_t has_limits;
+  uint32_t limit_rmask;  // resources present in the remaining-limits map
+  uint32_t pad;
+  uint64_t zm, cm;       // template Has over catalog zones / capacity types
+  uint64_t taints;       // taint-vocabulary mask
+  int64_t daemon[RMAX];
+  int64_t limits[RMAX];  // initial remaining limits
+};
+
+// per-claim record (device-owned, AoS so one lane reads one claim)
+struct ClaimHdr {
+  uint32_t tmpl;
+  uint32_t count;
+  uint64_t zm, cm;
+};
+
+// add-log entry: pod popped & placed, in order
+struct LogRec {
+  uint32_t pod, var, target, pad;  // target: claim id, or (node id | 0x80000000)
+};
+
+// FFD kernel control block (device <-> host)
+struct Ctrl {
+  uint32_t status;       // 0 ok, 1 claim capacity exceeded, 2 internal error
+  uint32_t n_claims;
+  uint32_t n_log;
+  uint32_t qhead, qlen;
+  uint32_t epoch;
+  uint64_t pops;
+  uint64_t generic_sorts, fast_sorts;
+};
+
+struct DevProblem {
+  // sizes
+  uint32_t N, W, R, Z, C, T, F, V, P, K, NT;  // K = IT keys, NT = taint vocab
+  uint32_t max_claims;
+  uint64_t wk_slots;  // free slots whose key is well-known
+  // catalog
+  const uint32_t* it_vid;      // [K][N]
+  const int64_t* it_alloc;     // [R][N]
+  const int64_t* it_cap;       // [R][N]
+  const uint64_t* it_pair;     // [N] available (zone,ct) pairs
+  const uint32_t* it_prank;    // [N][64] price rank per pair, NONE if none
+  const uint32_t* it_namerank; // [N]
+  const uint32_t* rank_to_it;  // [N]
+  const uint64_t* slot_set;    // [64][W] ITs with an available offering on pair g
+  const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
+  const uint32_t* thr_off;     // [R+1] offsets into thr_val
+  const uint64_t* thr_set;     // [(n_r+1) per r][W], offsets thr_off[r]+r
+  const int64_t* fk_ival;      // [F][64] integer value of vocabulary entries
+  const uint64_t* fk_isint;    // [F]
+  // templates
+  const TmplRec* tmpl;         // [T]
+  const uint64_t* t_opts;      // [T][W]
+  const FK* t_fk;              // [T][F]
+  // pods
+  const int64_t* pod_req;      // [P][R]
+  const uint32_t* var_begin;   // [P]
+  const uint32_t* var_count;   // [P]
+  const VarRec* vars;          // [V]
+  const uint64_t* itmask;      // arena
+  const FKEntry* fk_entries;
+  const uint32_t* queue0;      // [P] initial queue order
+  // feasibility outputs
+  uint64_t* rows;              // [V][T][W]
+  uint32_t* cheapest;          // [V][T] IT index or NONE
+  uint32_t* nfo;               // [V][T]
+  // FFD state
+  uint32_t* queue;             // [P]
+  uint32_t* last_len;          // [P]
+  uint32_t* last_epoch;        // [P]
+  uint32_t* cur_var;           // [P]
+  ClaimHdr* c_hdr;             // [max_claims]
+  uint64_t* c_opts;            // [max_claims][W]
+  int64_t* c_tot;              // [max_claims][R]
+  FK* c_fk;                    // [max_claims][F]
+  int64_t* t_rem;              // [T][R] remaining limits (dynamic)
+  LogRec* log;                 // [P]
+  uint32_t* c_sorted;          // [max_claims] final sort order (debug)
+  Ctrl* ctrl;
+  // truncation outputs
+  uint32_t* c_its;             // [max_claims][60]
+  uint32_t* c_nits;            // [max_claims]
+};
+
+}  // namespace gsd

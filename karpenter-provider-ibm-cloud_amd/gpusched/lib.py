@@ -1,0 +1,119 @@
+"""ctypes binding of libgpusched.so (the C-ABI in include/gpusched.h).
+
+This is the product path: it loads ONLY the in-tree HIP library and fails
+loudly when it is missing or no gfx950 device is visible.  There is no CPU
+fallback.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpusched.so")
+
+EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
+           "gs_last_error", "gs_version", "gs_validate"]
+
+
+class GpuSchedError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"{abi.STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GpuSchedError(abi.GS_E_NO_DEVICE, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.gs_create.argtypes = [C.POINTER(abi.GsConfig), C.POINTER(vp)]
+        L.gs_create.restype = C.c_int
+        L.gs_destroy.argtypes = [vp]
+        L.gs_destroy.restype = None
+        L.gs_prepare.argtypes = [vp, C.POINTER(abi.GsProblem)]
+        L.gs_prepare.restype = C.c_int
+        L.gs_run.argtypes = [vp]
+        L.gs_run.restype = C.c_int
+        L.gs_fetch.argtypes = [vp, C.POINTER(abi.GsResult)]
+        L.gs_fetch.restype = C.c_int
+        L.gs_solve.argtypes = [vp, C.POINTER(abi.GsProblem), C.POINTER(abi.GsResult)]
+        L.gs_solve.restype = C.c_int
+        L.gs_feasibility.argtypes = [vp, C.POINTER(abi.GsFeasResult)]
+        L.gs_feasibility.restype = C.c_int
+        L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
+        L.gs_last_error.restype = C.c_size_t
+        L.gs_version.argtypes = []
+        L.gs_version.restype = C.c_char_p
+        L.gs_validate.argtypes = [C.POINTER(abi.GsProblem), C.c_char_p, C.c_size_t]
+        L.gs_validate.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def validate(problem):
+    """host-only encode check (no device): (status, message)"""
+    buf = C.create_string_buffer(512)
+    st = load().gs_validate(C.byref(problem.struct), buf, 512)
+    return st, buf.value.decode()
+
+
+class Solver:
+    """One gs_ctx on one device (karpenter-core drives one provisioning
+    Solve and one consolidation simulation at a time per context)."""
+
+    def __init__(self, device=0):
+        self.L = load()
+        self.ctx = C.c_void_p()
+        cfg = abi.GsConfig(device, 0, 0)
+        st = self.L.gs_create(C.byref(cfg), C.byref(self.ctx))
+        if st != abi.GS_OK:
+            raise GpuSchedError(st, "gs_create failed (no gfx950 device?)")
+        self.problem = None
+
+    def close(self):
+        if self.ctx:
+            self.L.gs_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self):
+        buf = C.create_string_buffer(1024)
+        self.L.gs_last_error(self.ctx, buf, 1024)
+        return buf.value.decode()
+
+    def _check(self, st):
+        if st != abi.GS_OK:
+            raise GpuSchedError(st, self._err())
+
+    def prepare(self, problem):
+        self.problem = problem
+        self._check(self.L.gs_prepare(self.ctx, C.byref(problem.struct)))
+
+    def run(self):
+        self._check(self.L.gs_run(self.ctx))
+
+    def fetch(self):
+        res = abi.GsResult()
+        self._check(self.L.gs_fetch(self.ctx, C.byref(res)))
+        return abi.result_to_dict(res, self.problem), res
+
+    def solve(self, problem):
+        self.prepare(problem)
+        self.run()
+        return self.fetch()
+
+    def feasibility(self):
+        res = abi.GsFeasResult()
+        self._check(self.L.gs_feasibility(self.ctx, C.byref(res)))
+        return abi.feas_to_dict(res), res

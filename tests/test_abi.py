@@ -1,0 +1,75 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol
+include/gpusched.h declares, and its host-only encoder accepts/refuses the
+right inputs (no compute call needs a GPU here)."""
+import re
+import os
+
+import pytest
+
+from gpusched import abi, lib, synth
+
+HEADER = os.path.join(os.path.dirname(__file__), "..", "include", "gpusched.h")
+
+
+def declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(gs_[a-z_]+)\s*\(", txt)))
+
+
+def test_exports_every_declared_symbol():
+    L = lib.load()
+    names = declared()
+    assert set(names) == set(lib.EXPORTS)
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_version():
+    assert b"gfx950" in lib.load().gs_version()
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C3"])
+def test_validate_configs(name):
+    f = {"C1": synth.make_c1, "C2": lambda: synth.make_c2(500), "C3": lambda: synth.make_c3(500)}[name]
+    assert lib.validate(f()) == (abi.GS_OK, "")
+
+
+def _one_pod_problem(**pod):
+    b = synth.ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False, prices={})
+    b.add_nodepool("default")
+    b.add_pod("u1", 0, {"cpu": 100, "pods": 1000}, **pod)
+    return b
+
+
+def test_validate_refuses_topology():
+    b = _one_pod_problem(flags=abi.POD_TOPOLOGY_SPREAD)
+    st, msg = lib.validate(b.build())
+    assert st == abi.GS_E_UNSUPPORTED and "topology" in msg
+
+
+def test_validate_refuses_min_values():
+    b = _one_pod_problem(required_terms=[[("kubernetes.io/arch", "In", ["amd64"], 2)]])
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+def test_validate_refuses_gte():
+    b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", "Gte", ["4"])]])
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+def test_validate_invalid_gt_value():
+    b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", "Gt", ["four"])]])
+    assert lib.validate(b.build())[0] == abi.GS_E_INVALID
+
+
+def test_validate_duplicate_uid():
+    b = _one_pod_problem()
+    b.add_pod("u1", 0, {"cpu": 100})
+    assert lib.validate(b.build())[0] == abi.GS_E_INVALID
+
+
+def test_validate_random_accepts():
+    for s in range(100):
+        st, msg = lib.validate(synth.random_problem(s, with_nodes=False))
+        assert st == abi.GS_OK, (s, msg)

@@ -1,0 +1,107 @@
+"""GPU parity: the HIP library (through its C-ABI) against the oracle.
+
+Bit-exact equality of the whole Solve output: NodeClaims in creation order,
+their NodePool, pods in add order, canonical requirements, requests and the
+OrderByPrice/Truncate(60) instance-type lists, plus pod errors.
+"""
+import numpy as np
+import pytest
+
+from gpusched import abi, synth
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def solver():
+    from gpusched.lib import Solver
+    s = Solver(0)
+    yield s
+    s.close()
+
+
+def _diff(a, b):
+    if a == b:
+        return None
+    for k in ("errors", "nodes"):
+        if a[k] != b[k]:
+            return f"{k}: {a[k][:20]} vs {b[k][:20]}"
+    if len(a["claims"]) != len(b["claims"]):
+        n = min(len(a["claims"]), len(b["claims"]))
+        for i in range(n):
+            if a["claims"][i] != b["claims"][i]:
+                return f"claim {i} first differs; counts {len(a['claims'])} vs {len(b['claims'])}: {a['claims'][i]} vs {b['claims'][i]}"
+        return f"claim counts {len(a['claims'])} vs {len(b['claims'])}"
+    for i, (x, y) in enumerate(zip(a["claims"], b["claims"])):
+        if x != y:
+            fields = {k: (x[k], y[k]) for k in x if x[k] != y[k]}
+            return f"claim {i}: {fields}"
+    return "differs"
+
+
+def check_solve(solver, problem):
+    st, want, _ = pyoracle.solve(problem)
+    assert st == abi.GS_OK
+    got, res = solver.solve(problem)
+    d = _diff(got, want)
+    assert d is None, d
+    return got, res
+
+
+def check_feas(solver, problem):
+    st, want = pyoracle.feasibility(problem)
+    assert st == abi.GS_OK
+    solver.prepare(problem)
+    got, _ = solver.feasibility()
+    assert np.array_equal(got["rows"], want["rows"])
+    assert np.array_equal(got["cheapest"], want["cheapest"])
+    assert np.array_equal(got["n_feasible_offerings"], want["n_feasible_offerings"])
+
+
+def test_feasibility_c1(solver):
+    check_feas(solver, synth.make_c1())
+
+
+def test_feasibility_c2(solver):
+    check_feas(solver, synth.make_c2(n_pods=3000))
+
+
+def test_feasibility_c3(solver):
+    check_feas(solver, synth.make_c3(n_pods=3000))
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_feasibility_random(solver, seed):
+    check_feas(solver, synth.random_problem(seed, with_nodes=False))
+
+
+def test_solve_c1(solver):
+    check_solve(solver, synth.make_c1())
+
+
+def test_solve_c2(solver):
+    check_solve(solver, synth.make_c2(n_pods=10_000))
+
+
+def test_solve_c3(solver):
+    check_solve(solver, synth.make_c3(n_pods=5_000))
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_solve_random(solver, seed):
+    check_solve(solver, synth.random_problem(seed, with_nodes=False))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_solve_random_many_pods(solver, seed):
+    # enough NodeClaims that the Go pdqsort generic path and the fast path both run
+    check_solve(solver, synth.random_problem(1000 + seed, n_pods=400, with_nodes=False))
+
+
+def test_empty_pods(solver):
+    b = synth.ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False, prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("default")
+    got, _ = solver.solve(b.build())
+    assert got == {"claims": [], "nodes": [], "errors": []}
