@@ -128,6 +128,7 @@ void upload_problem(gs_ctx* c) {
   d.rows = c->alloc<uint64_t>(VT * e.W);
   d.cheapest = c->alloc<uint32_t>(VT);
   d.nfo = c->alloc<uint32_t>(VT);
+  d.fk_ok = c->alloc<uint32_t>(VT);
   d.queue = c->alloc<uint32_t>(e.P);
   d.last_len = c->alloc<uint32_t>(e.P);
   d.last_epoch = c->alloc<uint32_t>(e.P);

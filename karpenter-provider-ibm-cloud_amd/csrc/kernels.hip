@@ -139,7 +139,13 @@ __device__ __forceinline__ uint32_t lower_bound_i64(const int64_t* vals, uint32_
 
 // ===================================================================== K1/K2
 // one wave per (variant v, template t); lane i of step w = instance type w*64+i
-extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t apply_limits) {
+// static_mode = 1 (gs_feasibility): a NodeClaim opened for the pod alone, with
+// the free-key Compatible check and the NodePool limits folded into the row.
+// static_mode = 0 (FFD): rows carry only the monotone predicates (taints, IT
+// requirements, fits, offerings); the free-key check against the fresh
+// template goes to fk_ok[] because an in-flight NodeClaim can gain keys that
+// make a later pod compatible.
+extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t pair = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
   if (pair >= d.V * d.T) return;  // wave-uniform
@@ -150,12 +156,13 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
 
   // wave-uniform parts of NodeClaim.CanAdd on a fresh NodeClaim
   bool ok_all = (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
-  ok_all = ok_all && var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
+  const bool fk_ok = var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
+  if (static_mode) ok_all = ok_all && fk_ok;
   int64_t dem[RMAX];
   const int64_t* preq = d.pod_req + (size_t)vr.pod * d.R;
   for (uint32_t r = 0; r < d.R; r++) dem[r] = tr.daemon[r] + preq[r];  // Merge(daemon, pod)
   const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C);
-  const bool lim = apply_limits && tr.has_limits;
+  const bool lim = static_mode && tr.has_limits;
 
   uint64_t best = ~0ull;
   uint32_t nf = 0;
@@ -202,6 +209,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   best = wave_min_u64(best);
   nf = wave_sum_u32(nf);
   if (lane == 0) {
+    d.fk_ok[pair] = fk_ok ? 1u : 0u;
     d.nfo[pair] = nf;
     d.cheapest[pair] = best == ~0ull ? NONE : d.rank_to_it[(uint32_t)best];
   }
@@ -460,12 +468,17 @@ extern "C" __global__ __launch_bounds__(BLOCK) void ffd_kernel(DevProblem d) {
     S.status = 0;
   }
   __syncthreads();
+  // safety net only: the <U> loop performs at most (relaxations+2)*P pops
+  const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
 
   for (;;) {
     // ------------------------------------------------------------ Queue.Pop
     if (tid == 0) {
       uint32_t stop = 0;
-      if (S.qlen == 0) {
+      if (S.pops > max_pops) {
+        S.status = 2;
+        stop = 1;
+      } else if (S.qlen == 0) {
         stop = 1;
       } else {
         const uint32_t p = d.queue[S.qhead];
@@ -693,8 +706,9 @@ extern "C" __global__ __launch_bounds__(BLOCK) void ffd_kernel(DevProblem d) {
       const uint64_t* row = d.rows + ((size_t)v * T + t) * W;
       // row & limits mask (filterByRemainingResources), one IT per thread
       bool any = false;
-      for (uint32_t w = 0; w < W; w++)
-        if (row[w]) any = true;
+      if (d.fk_ok[(size_t)v * T + t])
+        for (uint32_t w = 0; w < W; w++)
+          if (row[w]) any = true;
       if (!any) continue;
       if (tr.has_limits) {
         if (tid == 0) S.first = 0;
@@ -882,11 +896,11 @@ extern "C" hipError_t gsk_init(uint32_t ffd_lds_bytes, uint32_t trunc_lds_bytes)
                              (int)trunc_lds_bytes);
 }
 
-extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t apply_limits, hipStream_t s) {
+extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, hipStream_t s) {
   const uint64_t pairs = (uint64_t)d->V * d->T;
   if (!pairs) return hipSuccess;
   const uint32_t blocks = (uint32_t)((pairs + (BLOCK / 64) - 1) / (BLOCK / 64));
-  hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(BLOCK), 0, s, *d, apply_limits);
+  hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(BLOCK), 0, s, *d, static_mode);
   return hipGetLastError();
 }
 

@@ -117,6 +117,7 @@ struct DevProblem {
   uint64_t* rows;              // [V][T][W]
   uint32_t* cheapest;          // [V][T] IT index or NONE
   uint32_t* nfo;               // [V][T]
+  uint32_t* fk_ok;             // [V][T] free-key Compatible vs the fresh template
   // FFD state
   uint32_t* queue;             // [P]
   uint32_t* last_len;          // [P]
