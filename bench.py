@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric on MI355X:
+pod x offering feasibility checks/sec + Solve latency (ms), 100k pods.
+
+A step = one device-resident Solve of the whole workload through the C-ABI
+(gs_run: K1/K2 feasibility -> K4 first-fit-decreasing -> K3 OrderByPrice/
+Truncate(60)); encode + host->HBM upload happen once before the timed region
+and are reported separately.  checks per step = pods x offerings reachable
+from the NodePool.  --gpus N runs N independent replicas
+(one independent cluster's Solve per rank, no data-path collective): weak
+scaling; value = sum of checks over ranks / max step time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "karpenter-provider-ibm-cloud_amd"))
+sys.path.insert(0, ROOT)
+
+from gpusched import synth  # noqa: E402
+from gpusched.lib import Solver  # noqa: E402
+
+METRIC = "pod×offering feasibility checks/sec + Solve latency (ms) at 100k pods, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(res, problem, n_claims):
+    """per-launch ALGORITHMIC bytes from the run's counters"""
+    V, T, W = res.n_variants, res.n_templates, res.words
+    R = res.n_resources
+    O = len(problem.offerings)
+    N = len(problem.instance_types)
+    feas = V * 128 + O * 48 + V * T * (W * 8 + 12)
+    per_cand = 24 + W * 8 * (2 + R) + R * 8      # header, opts, row, R threshold sets, totals
+    per_pop = R * 8 + 96                          # pod requests + variant record
+    adds = len(problem.pods) - res.n_errors
+    per_add = W * 8 + R * 8 + 24 + 16             # claim update + add-log record
+    ffd = res.pops * per_pop + res.cand_evals * per_cand + adds * per_add
+    trunc = n_claims * (W * 8 + 24 + 60 * 4) + N * 16
+    return {"feas": feas, "ffd": ffd, "trunc": trunc}
+
+
+def cpu_baseline(n_pods):
+    """oracle (C++ port of the reference algorithm, 1 thread) on a bounded
+    sample of the same workload; also checks the GPU result on that sample"""
+    from oracle import pyoracle
+    problem = synth.make_cm(n_pods=n_pods)
+    t0 = time.perf_counter()
+    st, want, _ = pyoracle.solve(problem)
+    dt = time.perf_counter() - t0
+    s = Solver(0)
+    try:
+        got, _ = s.solve(problem)
+    finally:
+        s.close()
+    return {
+        "value": problem.checks() / dt,
+        "unit": "checks/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"CM distribution, first {n_pods} pods (same C2 catalog, 1 NodePool); oracle Solve "
+                  f"{dt * 1e3:.0f} ms; GPU result on the sample bit-exact: {got == want}",
+        "solve_ms": dt * 1e3,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods", type=int, default=100_000)
+    ap.add_argument("--cpu-sample-pods", type=int, default=40_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (profiles/)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+
+    problem = synth.make_cm(n_pods=args.pods, seed=0x5EED0006 + rank)
+    solver = Solver(local)
+    t0 = time.perf_counter()
+    solver.prepare(problem)
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(args.warmup):
+        solver.run()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    kt = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solver.run()  # synchronous: returns after the stream's last event
+        kt.append(solver.last_run_ms())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    t1 = time.perf_counter()
+    out, res = solver.fetch()
+    fetch_ms = (time.perf_counter() - t1) * 1e3
+    checks = problem.checks()
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = checks * world / elapsed * args.steps
+
+    feas_ms = sum(k[0] for k in kt) / len(kt)
+    ffd_ms = sum(k[1] for k in kt) / len(kt)
+    trunc_ms = sum(k[2] for k in kt) / len(kt)
+    ab = algorithmic_bytes(res, problem, len(out["claims"]))
+    kms = {"feas": feas_ms, "ffd": ffd_ms, "trunc": trunc_ms}
+    dom = max(kms, key=kms.get)
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get(dom)
+
+    def roof(k):
+        ach = ab[k] / (kms[k] * 1e-3) / 1e9
+        return {"kernel": {"feas": "feas_kernel", "ffd": "ffd_kernel", "trunc": "trunc_kernel"}[k],
+                "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": ab[k], "avg_ms": round(kms[k], 4)}
+
+    roofline = roof(dom)
+    roofline["traffic"] = traffic
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "checks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic",
+        "config": {
+            "workload": "CM: 100k pods x C2 synthetic IBM VPC catalog (198 profiles x 3 zones x "
+                        "{on-demand, spot} = 1,188 offerings), 1 NodePool, 1% GPU pods, 10% nodeSelectors",
+            "pods": len(problem.pods),
+            "instance_types": len(problem.instance_types),
+            "offerings": len(problem.offerings),
+            "nodepools": len(problem.nodepools),
+            "checks_per_step": checks,
+            "parallelism": f"replicas{world}" if world > 1 else "single",
+        },
+        "solve_latency_ms": ms_per_step,
+        "kernel_ms": {k: round(v, 4) for k, v in kms.items()},
+        "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 2),
+        "fetch_decode_ms": round(fetch_ms, 2),
+        "new_nodeclaims": len(out["claims"]),
+        "pod_errors": len(out["errors"]),
+        "queue_pops": int(res.pops),
+        "ffd_candidates_scored": int(res.cand_evals),
+        "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
+        "roofline": roofline,
+        "roofline_feasibility_kernel": roof("feas"),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_pods)
+    solver.close()
+    if rank == 0:
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -199,6 +199,9 @@ typedef struct gs_result {
   /* instrumentation (product only; the oracle reports total only) */
   uint64_t checks;                   /* pod x offering checks of the static matrix */
   uint64_t pops;                     /* queue pops performed */
+  uint64_t cand_evals;               /* in-flight NodeClaim candidates scored */
+  uint64_t sorts_fast, sorts_generic;/* Go sort.Slice emulations by path */
+  uint32_t words, n_templates, n_variants; /* encoded sizes: IT words, templates, pod variants */
   double t_encode_ms, t_upload_ms, t_feas_ms, t_ffd_ms, t_truncate_ms, t_fetch_ms, t_total_ms;
 } gs_result;
 
@@ -232,6 +235,9 @@ gs_status gs_prepare(gs_ctx* ctx, const gs_problem* problem);
 /* run the device solve on the prepared problem (no host<->device traffic
  * except a completion flag); can be called repeatedly */
 gs_status gs_run(gs_ctx* ctx);
+/* device time (HIP events on the context's stream) of the last gs_run:
+ * out[0] feasibility (K1/K2), out[1] FFD (K4), out[2] truncate (K3), ms */
+gs_status gs_last_run_ms(const gs_ctx* ctx, double out[3]);
 /* fetch + decode the last run's result */
 gs_status gs_fetch(gs_ctx* ctx, gs_result* out);
 /* prepare + run + fetch */
@@ -244,6 +250,13 @@ gs_status gs_feasibility(gs_ctx* ctx, gs_feas_result* out);
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.
  * A Go caller uses it to choose between this library and upstream Solve. */
 gs_status gs_validate(const gs_problem* problem, char* err, size_t err_len);
+
+/* sizeof of every ABI struct, in this order: gs_range, gs_requirement,
+ * gs_quantity, gs_label, gs_taint, gs_toleration, gs_term, gs_offering,
+ * gs_instance_type, gs_nodepool, gs_pod, gs_node, gs_problem, gs_result,
+ * gs_feas_result, gs_config.  Bindings check their layouts against it.
+ * Returns the number of entries (16); writes min(n, 16). */
+uint32_t gs_abi_sizes(uint32_t* out, uint32_t n);
 
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);
 const char* gs_version(void);

@@ -160,6 +160,17 @@ extern "C" {
 
 const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
 
+uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
+  const uint32_t s[16] = {sizeof(gs_range),        sizeof(gs_requirement), sizeof(gs_quantity),
+                          sizeof(gs_label),        sizeof(gs_taint),       sizeof(gs_toleration),
+                          sizeof(gs_term),         sizeof(gs_offering),    sizeof(gs_instance_type),
+                          sizeof(gs_nodepool),     sizeof(gs_pod),         sizeof(gs_node),
+                          sizeof(gs_problem),      sizeof(gs_result),      sizeof(gs_feas_result),
+                          sizeof(gs_config)};
+  for (uint32_t i = 0; i < n && i < 16; i++) out[i] = s[i];
+  return 16;
+}
+
 gs_status gs_validate(const gs_problem* p, char* err, size_t len) {
   if (!p) return GS_E_INVALID;
   gsh::Encoded enc;
@@ -266,6 +277,14 @@ gs_status gs_run(gs_ctx* c) {
   return GS_OK;
 }
 
+gs_status gs_last_run_ms(const gs_ctx* c, double out[3]) {
+  if (!c || !c->ran || !out) return GS_E_INVALID;
+  out[0] = c->t_feas;
+  out[1] = c->t_ffd;
+  out[2] = c->t_trunc;
+  return GS_OK;
+}
+
 gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   if (!c || !c->ran || !out) return GS_E_INVALID;
   auto t0 = Clock::now();
@@ -351,6 +370,12 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->error_pods = c->error_pods.data();
   out->checks = e.checks;
   out->pops = c->ctrl.pops;
+  out->cand_evals = c->ctrl.cand_evals;
+  out->sorts_fast = c->ctrl.fast_sorts;
+  out->sorts_generic = c->ctrl.generic_sorts;
+  out->words = e.W;
+  out->n_templates = e.T;
+  out->n_variants = e.V;
   out->t_encode_ms = c->t_encode;
   out->t_upload_ms = c->t_upload;
   out->t_feas_ms = c->t_feas;

@@ -434,7 +434,7 @@ enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 struct FfdShared {
   uint32_t pod, var, stop, first, M, modkind, modpos, qhead, qlen, epoch, nlog, status;
   uint32_t found, fast_path, e0, e1;
-  uint64_t pops, generic, fast;
+  uint64_t pops, generic, fast, cand;
 };
 
 }  // namespace
@@ -465,6 +465,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void ffd_kernel(DevProblem d) {
     S.pops = 0;
     S.generic = 0;
     S.fast = 0;
+    S.cand = 0;
     S.status = 0;
   }
   __syncthreads();
@@ -651,7 +652,10 @@ extern "C" __global__ __launch_bounds__(BLOCK) void ffd_kernel(DevProblem d) {
           feas = any;
         }
       }
-      if (tid == 0) S.first = INF;
+      if (tid == 0) {
+        S.first = INF;
+        S.cand += (M - base) < BLOCK ? (M - base) : BLOCK;
+      }
       __syncthreads();
       if (feas) atomicMin(&S.first, pos);
       __syncthreads();
@@ -829,6 +833,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void ffd_kernel(DevProblem d) {
     c.pops = S.pops;
     c.generic_sorts = S.generic;
     c.fast_sorts = S.fast;
+    c.cand_evals = S.cand;
     *d.ctrl = c;
   }
 }

@@ -80,6 +80,7 @@ struct Ctrl {
   uint32_t epoch;
   uint64_t pops;
   uint64_t generic_sorts, fast_sorts;
+  uint64_t cand_evals;   // in-flight NodeClaim candidates scored
 };
 
 struct DevProblem {

@@ -1,7 +1,7 @@
 """ctypes / numpy mirror of include/gpusched.h (the C-ABI boundary).
 
 Struct layouts here must match the header byte for byte; tests/test_abi.py
-checks sizes against the compiled library's own sizeof table.
+checks sizes against the compiled library's own sizeof table (gs_abi_sizes).
 """
 import ctypes as C
 
@@ -86,6 +86,9 @@ class GsResult(C.Structure):
         ("error_pods", C.POINTER(C.c_uint32)),
         ("checks", C.c_uint64),
         ("pops", C.c_uint64),
+        ("cand_evals", C.c_uint64),
+        ("sorts_fast", C.c_uint64), ("sorts_generic", C.c_uint64),
+        ("words", _U32), ("n_templates", _U32), ("n_variants", _U32),
         ("t_encode_ms", C.c_double), ("t_upload_ms", C.c_double), ("t_feas_ms", C.c_double),
         ("t_ffd_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
         ("t_total_ms", C.c_double),

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgpusched.so")
 
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
-           "gs_last_error", "gs_version", "gs_validate"]
+           "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms"]
 
 
 class GpuSchedError(RuntimeError):
@@ -52,6 +52,10 @@ def load():
         L.gs_version.restype = C.c_char_p
         L.gs_validate.argtypes = [C.POINTER(abi.GsProblem), C.c_char_p, C.c_size_t]
         L.gs_validate.restype = C.c_int
+        L.gs_abi_sizes.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]
+        L.gs_abi_sizes.restype = C.c_uint32
+        L.gs_last_run_ms.argtypes = [vp, C.POINTER(C.c_double)]
+        L.gs_last_run_ms.restype = C.c_int
         _lib = L
     return _lib
 
@@ -102,6 +106,12 @@ class Solver:
 
     def run(self):
         self._check(self.L.gs_run(self.ctx))
+
+    def last_run_ms(self):
+        """(feasibility, ffd, truncate) device ms of the last run"""
+        out = (C.c_double * 3)()
+        self._check(self.L.gs_last_run_ms(self.ctx, out))
+        return tuple(out)
 
     def fetch(self):
         res = abi.GsResult()

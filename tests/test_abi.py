@@ -73,3 +73,14 @@ def test_validate_random_accepts():
     for s in range(100):
         st, msg = lib.validate(synth.random_problem(s, with_nodes=False))
         assert st == abi.GS_OK, (s, msg)
+
+
+def test_struct_layouts_match_library():
+    import ctypes as C
+    out = (C.c_uint32 * 16)()
+    assert lib.load().gs_abi_sizes(out, 16) == 16
+    mine = [8, abi.DT_REQ.itemsize, abi.DT_QTY.itemsize, abi.DT_LABEL.itemsize, abi.DT_TAINT.itemsize,
+            abi.DT_TOL.itemsize, abi.DT_TERM.itemsize, abi.DT_OFFERING.itemsize, abi.DT_IT.itemsize,
+            abi.DT_NODEPOOL.itemsize, abi.DT_POD.itemsize, abi.DT_NODE.itemsize, C.sizeof(abi.GsProblem),
+            C.sizeof(abi.GsResult), C.sizeof(abi.GsFeasResult), C.sizeof(abi.GsConfig)]
+    assert list(out) == mine
