@@ -169,6 +169,9 @@ def main():
         "pod_errors": len(out["errors"]),
         "queue_pops": int(res.pops),
         "ffd_candidates_scored": int(res.cand_evals),
+        "ffd_candidates_full_check": int(res.cand_full),
+        "ffd_phase_ms": {"sort": round(res.t_ffd_sort_ms, 2), "scan": round(res.t_ffd_scan_ms, 2),
+                         "template": round(res.t_ffd_template_ms, 2)},
         "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
         "roofline": roofline,
         "roofline_feasibility_kernel": roof("feas"),

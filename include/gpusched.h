@@ -200,9 +200,11 @@ typedef struct gs_result {
   uint64_t checks;                   /* pod x offering checks of the static matrix */
   uint64_t pops;                     /* queue pops performed */
   uint64_t cand_evals;               /* in-flight NodeClaim candidates scored */
+  uint64_t cand_full;                /* ... of which passed the slack prefilter */
   uint64_t sorts_fast, sorts_generic;/* Go sort.Slice emulations by path */
   uint32_t words, n_templates, n_variants; /* encoded sizes: IT words, templates, pod variants */
   double t_encode_ms, t_upload_ms, t_feas_ms, t_ffd_ms, t_truncate_ms, t_fetch_ms, t_total_ms;
+  double t_ffd_sort_ms, t_ffd_scan_ms, t_ffd_template_ms; /* in-kernel phase split of t_ffd_ms */
 } gs_result;
 
 /* Static pod x offering feasibility (K1/K2): for every (pod, nodepool) the

@@ -12,14 +12,16 @@
 #include "encode.hpp"
 #include "layout.hpp"
 
-extern "C" hipError_t gsk_init(uint32_t ffd_lds_bytes, uint32_t trunc_lds_bytes);
+extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
+extern "C" hipError_t gsk_init_ffd(uint32_t lds_bytes);
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
 
 namespace {
 
-constexpr uint32_t kMaxClaimsLds = 16384;  // ord+sc u32 in LDS: 128 KiB
+constexpr uint32_t kMaxClaimsLds = 16384;  // LDS: ord/sc/scratch u16 + tmpl u8 + thresholds
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
@@ -133,9 +135,8 @@ void upload_problem(gs_ctx* c) {
   d.last_len = c->alloc<uint32_t>(e.P);
   d.last_epoch = c->alloc<uint32_t>(e.P);
   d.cur_var = c->alloc<uint32_t>(e.P);
-  d.c_hdr = c->alloc<gsd::ClaimHdr>(MC);
+  d.c_rec = c->alloc<gsd::ClaimRec>(MC);
   d.c_opts = c->alloc<uint64_t>(MC * e.W);
-  d.c_tot = c->alloc<int64_t>(MC * std::max<uint32_t>(e.R, 1));
   d.c_fk = c->alloc<gsd::FK>(MC * std::max<uint32_t>(e.F, 1));
   d.t_rem = c->alloc<int64_t>((size_t)e.T * std::max<uint32_t>(e.R, 1));
   d.log = c->alloc<gsd::LogRec>(e.P);
@@ -210,7 +211,8 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(gsk_init(kMaxClaimsLds * 8, 65536));
+    HIPCHK(gsk_init_ffd(gsk_ffd_lds_bytes(kMaxClaimsLds)));
+    HIPCHK(gsk_init_trunc(65536));
   } catch (const HipError& e) {
     delete c;
     return GS_E_HIP;
@@ -277,6 +279,15 @@ gs_status gs_run(gs_ctx* c) {
   return GS_OK;
 }
 
+// diagnostic (not in the public header): FFD control block counters
+extern "C" gs_status gs_debug_ctrl(gs_ctx* c, uint64_t* out, uint32_t n) {
+  if (!c || !c->ran) return GS_E_INVALID;
+  gsd::Ctrl ctl;
+  if (hipMemcpy(&ctl, c->dp.ctrl, sizeof ctl, hipMemcpyDeviceToHost) != hipSuccess) return GS_E_HIP;
+  for (uint32_t i = 0; i < n && i < 8; i++) out[i] = ctl.dbg[i];
+  return GS_OK;
+}
+
 gs_status gs_last_run_ms(const gs_ctx* c, double out[3]) {
   if (!c || !c->ran || !out) return GS_E_INVALID;
   out[0] = c->t_feas;
@@ -291,8 +302,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   auto& e = c->enc;
   auto& d = c->dp;
   std::vector<gsd::LogRec> log;
-  std::vector<gsd::ClaimHdr> hdr;
-  std::vector<int64_t> tot;
+  std::vector<gsd::ClaimRec> hdr;
   std::vector<uint32_t> its, nits, queue;
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -300,14 +310,12 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     const uint32_t M = c->ctrl.n_claims;
     log.resize(c->ctrl.n_log);
     hdr.resize(M);
-    tot.resize((size_t)M * e.R);
     its.resize((size_t)M * 60);
     nits.resize(M);
     queue.resize(e.P);
     if (!log.empty()) HIPCHK(hipMemcpy(log.data(), d.log, log.size() * sizeof(gsd::LogRec), hipMemcpyDeviceToHost));
     if (M) {
-      HIPCHK(hipMemcpy(hdr.data(), d.c_hdr, M * sizeof(gsd::ClaimHdr), hipMemcpyDeviceToHost));
-      if (e.R) HIPCHK(hipMemcpy(tot.data(), d.c_tot, tot.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(hdr.data(), d.c_rec, M * sizeof(gsd::ClaimRec), hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(its.data(), d.c_its, its.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(nits.data(), d.c_nits, M * sizeof(uint32_t), hipMemcpyDeviceToHost));
     }
@@ -342,7 +350,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     c->claim_it_offsets.push_back((uint32_t)c->claim_its.size());
     creq[j].erase(e.k_hostname);  // FinalizeScheduling
     c->req_text[j] = gsh::canonical(e, creq[j]);
-    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = tot[(size_t)j * e.R + r];
+    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = hdr[j].tot[r];
   }
   c->req_ptrs.clear();
   for (auto& s : c->req_text) c->req_ptrs.push_back(s.c_str());
@@ -371,6 +379,10 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->checks = e.checks;
   out->pops = c->ctrl.pops;
   out->cand_evals = c->ctrl.cand_evals;
+  out->cand_full = c->ctrl.cand_full;
+  out->t_ffd_sort_ms = c->ctrl.t_sort * 1e-5;  // wall_clock64 runs at 100 MHz
+  out->t_ffd_scan_ms = c->ctrl.t_scan * 1e-5;
+  out->t_ffd_template_ms = c->ctrl.t_tmpl * 1e-5;
   out->sorts_fast = c->ctrl.fast_sorts;
   out->sorts_generic = c->ctrl.generic_sorts;
   out->words = e.W;

@@ -794,6 +794,9 @@ struct Ctx {
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
         vr.tol = pv.tol;
+        vr.tolt = 0;
+        for (uint32_t t = 0; t < e.T; t++)
+          if ((e.tmpl[t].taints & ~pv.tol) == 0) vr.tolt |= 1ull << t;
         vr.fk_begin = (uint32_t)e.fk_entries.size();
         for (auto& kv : pv.reqs)
           if (e.keys[kv.first].cls == KEY_FREE) {

@@ -46,6 +46,7 @@ struct VarRec {
   uint32_t itmask_off[KMAX_IT];  // word offset into itmask arena, NONE = unconstrained
   uint64_t zm, cm;               // Has over catalog zones / capacity types
   uint64_t tol;                  // tolerated taint-vocabulary mask
+  uint64_t tolt;                 // templates whose taints this variant tolerates
 };
 
 struct TmplRec {
@@ -59,12 +60,17 @@ struct TmplRec {
   int64_t limits[RMAX];  // initial remaining limits
 };
 
-// per-claim record (device-owned, AoS so one lane reads one claim)
-struct ClaimHdr {
-  uint32_t tmpl;
-  uint32_t count;
-  uint64_t zm, cm;
+// per-claim record (device-owned, AoS: one candidate = one 192-B record read
+// in a single round trip)
+struct alignas(64) ClaimRec {
+  int64_t tot[RMAX];    // requests: daemon overhead + pods (Merge)
+  int64_t maxa[RMAX];   // max allocatable over the claim's initial options (upper bound)
+  uint64_t zm, cm;      // Has over catalog zones / capacity types
+  uint16_t thr[RMAX];   // threshold cursors: lower_bound(thr_val_r, tot_r)
+  uint32_t tmpl, count;
+  uint32_t pad[6];
 };
+static_assert(sizeof(ClaimRec) == 192, "ClaimRec layout");
 
 // add-log entry: pod popped & placed, in order
 struct LogRec {
@@ -81,6 +87,9 @@ struct Ctrl {
   uint64_t pops;
   uint64_t generic_sorts, fast_sorts;
   uint64_t cand_evals;   // in-flight NodeClaim candidates scored
+  uint64_t cand_full;    // candidates that passed the slack prefilter
+  uint64_t t_sort, t_scan, t_tmpl, t_total;  // wall_clock64 ticks (100 MHz) per phase
+  uint64_t dbg[8];                            // diagnostic phase counters
 };
 
 struct DevProblem {
@@ -124,9 +133,8 @@ struct DevProblem {
   uint32_t* last_len;          // [P]
   uint32_t* last_epoch;        // [P]
   uint32_t* cur_var;           // [P]
-  ClaimHdr* c_hdr;             // [max_claims]
+  ClaimRec* c_rec;             // [max_claims]
   uint64_t* c_opts;            // [max_claims][W]
-  int64_t* c_tot;              // [max_claims][R]
   FK* c_fk;                    // [max_claims][F]
   int64_t* t_rem;              // [T][R] remaining limits (dynamic)
   LogRec* log;                 // [P]

@@ -87,11 +87,13 @@ class GsResult(C.Structure):
         ("checks", C.c_uint64),
         ("pops", C.c_uint64),
         ("cand_evals", C.c_uint64),
+        ("cand_full", C.c_uint64),
         ("sorts_fast", C.c_uint64), ("sorts_generic", C.c_uint64),
         ("words", _U32), ("n_templates", _U32), ("n_variants", _U32),
         ("t_encode_ms", C.c_double), ("t_upload_ms", C.c_double), ("t_feas_ms", C.c_double),
         ("t_ffd_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
         ("t_total_ms", C.c_double),
+        ("t_ffd_sort_ms", C.c_double), ("t_ffd_scan_ms", C.c_double), ("t_ffd_template_ms", C.c_double),
     ]
 
 
