@@ -14,14 +14,14 @@
 
 extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_bytes);
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims);
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
 
 namespace {
 
-constexpr uint32_t kMaxClaimsLds = 16384;  // LDS: ord/sc/scratch u16 + tmpl u8 + thresholds
+constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: ord/sc/scratch u16, tmpl u8, 4x u16 slack, thresholds
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
@@ -63,18 +63,39 @@ struct gs_ctx {
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
   }
-  template <class T>
-  T* alloc(size_t n) {
-    void* p = nullptr;
-    HIPCHK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
-    allocs.push_back(p);
-    return (T*)p;
+  // Device buffers of one prepared problem come from ONE allocation (an arena
+  // of 256-B aligned sub-buffers): large pages, few TLB entries for the
+  // single-workgroup FFD kernel's gathers.  plan() records, commit() places.
+  struct Planned {
+    void** dst;
+    size_t off, bytes;
+    std::vector<char> host;
+  };
+  std::vector<Planned> plan;
+  size_t plan_bytes = 0;
+  template <class P>
+  void alloc(P*& dst, size_t n) {
+    const size_t b = std::max<size_t>(n, 1) * sizeof(P);
+    plan.push_back(Planned{(void**)&dst, plan_bytes, b, {}});
+    plan_bytes += (b + 255) & ~(size_t)255;
   }
-  template <class T>
-  T* upload(const std::vector<T>& v) {
-    T* p = alloc<T>(v.size());
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
-    return p;
+  template <class P, class T>
+  void upload(P*& dst, const std::vector<T>& v) {
+    static_assert(sizeof(P) == sizeof(T), "upload type");
+    alloc(dst, v.size());
+    plan.back().host.assign((const char*)v.data(), (const char*)v.data() + v.size() * sizeof(T));
+  }
+  void commit() {
+    void* base = nullptr;
+    HIPCHK(hipMalloc(&base, std::max<size_t>(plan_bytes, 256)));
+    allocs.push_back(base);
+    for (auto& q : plan) {
+      *q.dst = (char*)base + q.off;
+      if (!q.host.empty()) HIPCHK(hipMemcpyAsync(*q.dst, q.host.data(), q.host.size(), hipMemcpyHostToDevice, stream));
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    plan.clear();
+    plan_bytes = 0;
   }
 };
 
@@ -88,6 +109,8 @@ gs_status fail(gs_ctx* c, gs_status s, const std::string& m) {
 void upload_problem(gs_ctx* c) {
   auto& e = c->enc;
   auto& d = c->dp;
+  c->plan.clear();
+  c->plan_bytes = 0;
   c->free_all();
   std::memset(&d, 0, sizeof d);
   d.N = e.N;
@@ -102,49 +125,68 @@ void upload_problem(gs_ctx* c) {
   d.K = e.K;
   d.NT = e.NT;
   d.wk_slots = e.wk_slots;
+  d.RQ = std::min<uint32_t>(e.R, 4);
+  d.n_thr = (uint32_t)e.thr_val.size();
+  for (uint32_t r = 0; r < gsd::RMAX; r++) {
+    int64_t mx = 1;
+    if (r < e.R)
+      for (uint32_t i = 0; i < e.N; i++) mx = std::max(mx, e.it_alloc[(size_t)r * e.N + i]);
+    int s = 0;  // power-of-two unit: shifts on the device, no 64-bit divides
+    while ((mx >> s) > 65535) s++;
+    d.q_shift[r] = (uint32_t)s;
+  }
   d.max_claims = std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
-  d.it_vid = c->upload(e.it_vid);
-  d.it_alloc = c->upload(e.it_alloc);
-  d.it_cap = c->upload(e.it_cap);
-  d.it_pair = c->upload(e.it_pair);
-  d.it_prank = c->upload(e.it_prank);
-  d.it_namerank = c->upload(e.it_namerank);
-  d.rank_to_it = c->upload(e.rank_to_it);
-  d.slot_set = c->upload(e.slot_set);
-  d.thr_val = c->upload(e.thr_val);
-  d.thr_off = c->upload(e.thr_off);
-  d.thr_set = c->upload(e.thr_set);
-  d.fk_ival = c->upload(e.fk_ival);
-  d.fk_isint = c->upload(e.fk_isint);
-  d.tmpl = c->upload(e.tmpl);
-  d.t_opts = c->upload(e.t_opts);
-  d.t_fk = c->upload(e.t_fk);
-  d.pod_req = c->upload(e.pod_req);
-  d.var_begin = c->upload(e.var_begin);
-  d.var_count = c->upload(e.var_count);
-  d.vars = c->upload(e.vars);
-  d.itmask = c->upload(e.itmask);
-  d.fk_entries = c->upload(e.fk_entries);
-  d.queue0 = c->upload(e.queue0);
+  c->upload(d.it_vid, e.it_vid);
+  c->upload(d.it_alloc, e.it_alloc);
+  c->upload(d.it_cap, e.it_cap);
+  c->upload(d.it_pair, e.it_pair);
+  c->upload(d.it_prank, e.it_prank);
+  c->upload(d.it_namerank, e.it_namerank);
+  c->upload(d.rank_to_it, e.rank_to_it);
+  c->upload(d.slot_set, e.slot_set);
+  {
+    std::vector<int64_t> tv = e.thr_val;  // 4 sentinels: the device reads a 4-wide window past each range
+    tv.insert(tv.end(), 4, INT64_MAX);
+    c->upload(d.thr_val, tv);
+  }
+  c->upload(d.thr_off, e.thr_off);
+  c->upload(d.thr_set, e.thr_set);
+  c->upload(d.fk_ival, e.fk_ival);
+  c->upload(d.fk_isint, e.fk_isint);
+  c->upload(d.tmpl, e.tmpl);
+  c->upload(d.t_opts, e.t_opts);
+  c->upload(d.t_fk, e.t_fk);
+  c->upload(d.pod_req, e.pod_req);
+  c->upload(d.var_begin, e.var_begin);
+  c->upload(d.var_count, e.var_count);
+  c->upload(d.vars, e.vars);
+  c->upload(d.itmask, e.itmask);
+  c->upload(d.fk_entries, e.fk_entries);
+  c->upload(d.queue0, e.queue0);
+  d.NN = e.NN;
+  c->upload(d.nodes0, e.nodes);
+  c->upload(d.n_fk0, e.n_fk);
+  c->alloc(d.nodes, std::max<uint32_t>(e.NN, 1));
+  c->alloc(d.n_fk, e.n_fk.size());
   const size_t VT = (size_t)e.V * e.T, MC = d.max_claims;
-  d.rows = c->alloc<uint64_t>(VT * e.W);
-  d.cheapest = c->alloc<uint32_t>(VT);
-  d.nfo = c->alloc<uint32_t>(VT);
-  d.fk_ok = c->alloc<uint32_t>(VT);
-  d.queue = c->alloc<uint32_t>(e.P);
-  d.last_len = c->alloc<uint32_t>(e.P);
-  d.last_epoch = c->alloc<uint32_t>(e.P);
-  d.cur_var = c->alloc<uint32_t>(e.P);
-  d.c_rec = c->alloc<gsd::ClaimRec>(MC);
-  d.c_opts = c->alloc<uint64_t>(MC * e.W);
-  d.c_fk = c->alloc<gsd::FK>(MC * std::max<uint32_t>(e.F, 1));
-  d.t_rem = c->alloc<int64_t>((size_t)e.T * std::max<uint32_t>(e.R, 1));
-  d.log = c->alloc<gsd::LogRec>(e.P);
-  d.c_sorted = c->alloc<uint32_t>(MC);
-  d.ctrl = c->alloc<gsd::Ctrl>(1);
-  d.c_its = c->alloc<uint32_t>(MC * 60);
-  d.c_nits = c->alloc<uint32_t>(MC);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  c->alloc(d.rows, VT * e.W);
+  c->alloc(d.cheapest, VT);
+  c->alloc(d.nfo, VT);
+  c->alloc(d.fk_ok, VT);
+  c->alloc(d.queue, e.P);
+  c->alloc(d.last_len, e.P);
+  c->alloc(d.last_epoch, e.P);
+  c->alloc(d.cur_var, e.P);
+  c->alloc(d.c_rec, MC);
+  c->alloc(d.c_opts, MC * e.W);
+  c->alloc(d.c_fk, MC * std::max<uint32_t>(e.F, 1));
+  c->alloc(d.t_rem, (size_t)e.T * std::max<uint32_t>(e.R, 1));
+  c->alloc(d.log, e.P);
+  c->alloc(d.c_sorted, MC);
+  c->alloc(d.ctrl, 1);
+  c->alloc(d.c_its, MC * 60);
+  c->alloc(d.c_nits, MC);
+  c->commit();
 }
 
 uint32_t trunc_lds_bytes(uint32_t N) {
@@ -172,11 +214,21 @@ uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
   return 16;
 }
 
+// device capacity of the encoded problem (the FFD kernel keeps these in LDS)
+static gsh::Err capacity_check(const gsh::Encoded& e) {
+  if (e.N > 8192) return gsh::Err{GS_E_CAPACITY, "more than 8192 instance types"};
+  if (e.thr_val.size() + 4 > gsd::THR_LDS_MAX)
+    return gsh::Err{GS_E_CAPACITY, "more than 2044 distinct allocatable values over the resources"};
+  if ((size_t)e.Z * e.C * e.W > gsd::SLOT_LDS_MAX)
+    return gsh::Err{GS_E_CAPACITY, "zones x capacity types x instance-type words exceeds 1024"};
+  return gsh::Err{GS_OK, ""};
+}
+
 gs_status gs_validate(const gs_problem* p, char* err, size_t len) {
   if (!p) return GS_E_INVALID;
   gsh::Encoded enc;
   gsh::Err er = gsh::encode(p, enc);
-  if (er.code == GS_OK && enc.N > 8192) er = gsh::Err{GS_E_CAPACITY, "more than 8192 instance types"};
+  if (er.code == GS_OK) er = capacity_check(enc);
   if (err && len) {
     size_t n = std::min(len - 1, er.msg.size());
     std::memcpy(err, er.msg.data(), n);
@@ -211,7 +263,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(gsk_init_ffd(gsk_ffd_lds_bytes(kMaxClaimsLds)));
+    HIPCHK(gsk_init_ffd(gsk_ffd_lds_bytes(kMaxClaimsLds, gsd::THR_LDS_MAX - 4)));
     HIPCHK(gsk_init_trunc(65536));
   } catch (const HipError& e) {
     delete c;
@@ -238,7 +290,8 @@ gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   gsh::Err er = gsh::encode(p, c->enc);
   c->t_encode = ms_since(t0);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
-  if (c->enc.N > 8192) return fail(c, GS_E_CAPACITY, "more than 8192 instance types");
+  er = capacity_check(c->enc);
+  if (er.code != GS_OK) return fail(c, er.code, er.msg);
   c->problem = p;
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -284,7 +337,7 @@ extern "C" gs_status gs_debug_ctrl(gs_ctx* c, uint64_t* out, uint32_t n) {
   if (!c || !c->ran) return GS_E_INVALID;
   gsd::Ctrl ctl;
   if (hipMemcpy(&ctl, c->dp.ctrl, sizeof ctl, hipMemcpyDeviceToHost) != hipSuccess) return GS_E_HIP;
-  for (uint32_t i = 0; i < n && i < 8; i++) out[i] = ctl.dbg[i];
+  for (uint32_t i = 0; i < n && i < 16; i++) out[i] = ctl.dbg[i];
   return GS_OK;
 }
 
@@ -330,7 +383,16 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   std::vector<std::vector<uint32_t>> cp(M);
   std::vector<gsh::Reqs> creq(M);
   for (uint32_t j = 0; j < M; j++) creq[j] = e.tmpl_reqs[hdr[j].tmpl];
+  c->node_pod_offsets.assign(1, 0);
+  c->node_pods.clear();
+  std::vector<std::vector<uint32_t>> np_(e.NN);
   for (auto& l : log) {
+    if (l.target & 0x80000000u) {
+      const uint32_t pos = l.target & 0x7FFFFFFFu;
+      if (pos >= e.NN) return fail(c, GS_E_HIP, "corrupt add log");
+      np_[e.node_order[pos]].push_back(l.pod);
+      continue;
+    }
     if (l.target >= M) return fail(c, GS_E_HIP, "corrupt add log");
     cp[l.target].push_back(l.pod);
     for (auto& kv : e.variants[l.var].reqs) gsh::reqs_add(e, creq[l.target], kv.first, kv.second);
@@ -357,8 +419,10 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   c->error_pods.clear();
   for (uint32_t i = 0; i < c->ctrl.qlen; i++) c->error_pods.push_back(queue[(c->ctrl.qhead + i) % e.P]);
   std::sort(c->error_pods.begin(), c->error_pods.end());
-  c->node_pod_offsets.assign(1, 0);
-  c->node_pods.clear();
+  for (auto& v : np_) {
+    c->node_pods.insert(c->node_pods.end(), v.begin(), v.end());
+    c->node_pod_offsets.push_back((uint32_t)c->node_pods.size());
+  }
   c->t_fetch = ms_since(t0);
   std::memset(out, 0, sizeof(*out));
   out->n_claims = M;
@@ -371,7 +435,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->n_resources = e.R;
   out->resource_names = e.res_name_ids.data();
   out->claim_requests = c->claim_requests.data();
-  out->n_nodes = 0;
+  out->n_nodes = e.NN;
   out->node_pod_offsets = c->node_pod_offsets.data();
   out->node_pods = c->node_pods.data();
   out->n_errors = (uint32_t)c->error_pods.size();

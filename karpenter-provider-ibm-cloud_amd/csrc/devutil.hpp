@@ -102,10 +102,21 @@ __device__ FK fk_intersect(const FK& a, const FK& b, const int64_t* ival, uint64
   return r;
 }
 
-__device__ __forceinline__ bool var_fk_ok(const DevProblem& d, const VarRec& vr, const FK* claim_fk) {
+template <class DP>
+__device__ __forceinline__ bool var_fk_ok(const DP& d, const VarRec& vr, const FK* claim_fk) {
   for (uint32_t k = 0; k < vr.fk_count; k++) {
     const FKEntry& e = d.fk_entries[vr.fk_begin + k];
     if (!fk_compatible(claim_fk[e.slot], e.st, (d.wk_slots >> e.slot) & 1)) return false;
+  }
+  return true;
+}
+
+// <U> strict Requirements.Compatible (ExistingNode: no AllowUndefined)
+template <class DP>
+__device__ __forceinline__ bool var_fk_ok_strict(const DP& d, const VarRec& vr, const FK* node_fk) {
+  for (uint32_t k = 0; k < vr.fk_count; k++) {
+    const FKEntry& e = d.fk_entries[vr.fk_begin + k];
+    if (!fk_compatible(node_fk[e.slot], e.st, false)) return false;
   }
   return true;
 }

@@ -264,6 +264,30 @@ struct Ctx {
       mention_labels(np.labels);
       mention(kNodePool, S(np.name));
     }
+    // node label values matter only where a requirement can tell them apart:
+    // on instance-type / offering keys, or as integers under Gt/Lt bounds.
+    // Any other value behaves exactly like the unmentioned value omega.
+    std::set<std::string> label_keys = {kZone, kCapacityType}, bounded;
+    if (p->n_instance_types) {
+      auto& it0 = p->instance_types[0];
+      chk(it0.requirements, p->n_reqs, "reqs");
+      for (uint32_t k = 0; k < it0.requirements.count; k++)
+        label_keys.insert(normalize(S(p->reqs[it0.requirements.begin + k].key)));
+    }
+    for (uint32_t i = 0; i < p->n_reqs; i++)
+      if (p->reqs[i].op == GS_OP_GT || p->reqs[i].op == GS_OP_LT) bounded.insert(normalize(S(p->reqs[i].key)));
+    auto node_mention = [&](const std::string& key, const std::string& val) {
+      const std::string k = normalize(key);
+      int64_t x;
+      if (label_keys.count(k) || (bounded.count(k) && atoi64(val, &x))) mention(k, val);
+      else mention_key(k);
+    };
+    for (uint32_t i = 0; i < p->n_nodes; i++) {
+      chk(p->nodes[i].labels, p->n_labels, "labels");
+      for (uint32_t k = 0; k < p->nodes[i].labels.count; k++)
+        node_mention(S(p->labels[p->nodes[i].labels.begin + k].key), S(p->labels[p->nodes[i].labels.begin + k].value));
+      node_mention(kHostname, S(p->nodes[i].name));
+    }
     for (uint32_t i = 0; i < p->n_pods; i++) {
       auto& pd = p->pods[i];
       mention_labels(pd.node_selector);
@@ -321,6 +345,19 @@ struct Ctx {
   KReq in_one(uint32_t key, const std::string& val) const {
     const Vocab& v = e.keys[key].vocab;
     return make_kreq(v, GS_OP_IN, {v.id.at(val)}, 0);
+  }
+  KReq in_one_or_omega(uint32_t key, const std::string& val) const {
+    const Vocab& v = e.keys[key].vocab;
+    auto f = v.id.find(val);
+    return make_kreq(v, GS_OP_IN, {f == v.id.end() ? v.omega : f->second}, 0);
+  }
+  Reqs node_labels_reqs(gs_range r) const {
+    Reqs out;
+    for (uint32_t i = 0; i < r.count; i++) {
+      uint32_t k = key_of(p->labels[r.begin + i].key);
+      reqs_add(e, out, k, in_one_or_omega(k, S(p->labels[r.begin + i].value)));
+    }
+    return out;
   }
   Reqs labels_reqs(gs_range r) const {
     Reqs out;
@@ -613,6 +650,7 @@ struct Ctx {
 
   // --------------------------------------------------------- templates
   bool tolerate_pns = false;
+  std::vector<std::vector<Tol>> variant_tols;
   void build_templates() {
     std::vector<uint32_t> order(p->n_nodepools);
     std::iota(order.begin(), order.end(), 0);
@@ -753,6 +791,7 @@ struct Ctx {
         if (ri < req_terms.size()) reqs_add_all(e, v.reqs, req_terms[ri]);
         v.tol = tol_mask(tols);
         e.variants.push_back(std::move(v));
+        variant_tols.push_back(tols);
         // <U> Preferences.Relax
         if (req_terms.size() - ri > 1) {
           ri++;
@@ -791,6 +830,13 @@ struct Ctx {
           vr.itmask_off[k] = (uint32_t)e.itmask.size();
           e.itmask.insert(e.itmask.end(), f->second.has.w.begin(), f->second.has.w.end());
         }
+        vr.zfull_off = vr.cfull_off = gsd::NONE;
+        for (int kk = 0; kk < 2; kk++) {
+          auto f = pv.reqs.find(kk ? e.k_ct : e.k_zone);
+          if (f == pv.reqs.end()) continue;
+          (kk ? vr.cfull_off : vr.zfull_off) = (uint32_t)e.itmask.size();
+          e.itmask.insert(e.itmask.end(), f->second.has.w.begin(), f->second.has.w.end());
+        }
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
         vr.tol = pv.tol;
@@ -821,8 +867,69 @@ struct Ctx {
     });
     e.checks = (uint64_t)e.P * e.checks_per_pod;
   }
+
+  // <U> ExistingNode: labels + hostname In[name]; initialized first, then name
+  void build_nodes() {
+    e.NN = p->n_nodes;
+    std::vector<uint32_t> order(e.NN);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      const bool ia = p->nodes[a].initialized != 0, ib = p->nodes[b].initialized != 0;
+      if (ia != ib) return ia;
+      return S(p->nodes[a].name) < S(p->nodes[b].name);
+    });
+    e.node_order = order;
+    e.nodes.assign(e.NN, gsd::NodeRec{});
+    e.n_fk.assign((size_t)std::max<uint32_t>(e.NN, 1) * std::max<uint32_t>(e.F, 1), gsd::FK{});
+    // keys some pod variant constrains with NotIn/DoesNotExist: a node lacking
+    // such a non-free key would gain dynamic state there (refused below)
+    std::set<uint32_t> exempt_keys;
+    for (auto& pv : e.variants)
+      for (auto& kv : pv.reqs)
+        if (e.keys[kv.first].cls != KEY_FREE && exempt(kv.second)) exempt_keys.insert(kv.first);
+    for (uint32_t pos = 0; pos < e.NN; pos++) {
+      const gs_node& g = p->nodes[order[pos]];
+      gsd::NodeRec& nr = e.nodes[pos];
+      for (int k = 0; k < gsd::KMAX_IT; k++) nr.vid[k] = gsd::NONE;
+      nr.zvid = nr.cvid = gsd::NONE;
+      Reqs reqs = node_labels_reqs(g.labels);
+      uint32_t hk = e.k_hostname;
+      reqs_add(e, reqs, hk, in_one_or_omega(hk, S(g.name)));
+      for (auto& kv : reqs) {
+        const Key& key = e.keys[kv.first];
+        if (key.cls == KEY_FREE) {
+          e.n_fk[(size_t)pos * e.F + key.slot] = to_fk(kv.second);
+          continue;
+        }
+        // a label is In[v]: exactly one has-bit
+        uint32_t vid = gsd::NONE;
+        for (size_t i = 0; i < key.vocab.size(); i++)
+          if (kv.second.has.test(i)) vid = (uint32_t)i;
+        if (key.cls == KEY_IT) nr.vid[key.slot] = vid;
+        else if (key.cls == KEY_ZONE) nr.zvid = vid;
+        else nr.cvid = vid;
+      }
+      for (uint32_t k : exempt_keys) {
+        bool has = reqs.count(k) != 0;
+        if (!has) throw Fail{GS_E_UNSUPPORTED, "existing node lacks a label that a pod constrains with NotIn/DoesNotExist"};
+      }
+      bool present[gsd::RMAX] = {false};
+      resvec_fn(g.available, nr.avail, present);
+      nr.ok = 1;
+      for (uint32_t r = 0; r < e.R; r++)
+        if (present[r] && nr.avail[r] < 0) nr.ok = 0;  // <U> Fits: negative total never fits
+      resvec_fn(g.requests, nr.req, nullptr);
+      nr.taints = taint_mask(g.taints);
+    }
+    // taints of nodes enter the vocabulary after the pods' tolerations were
+    // encoded: recompute the tolerated masks over the final vocabulary
+    for (uint32_t v = 0; v < e.V; v++) e.vars[v].tol = tol_mask(variant_tols[v]);
+  }
 };
 
+}  // namespace
+
+namespace {
 }  // namespace
 
 std::string canonical(const Encoded& e, const Reqs& r) {
@@ -863,12 +970,12 @@ Err encode(const gs_problem* p, Encoded& e) {
   try {
     c.strs.reserve(p->n_strings);
     for (uint32_t i = 0; i < p->n_strings; i++) c.strs.push_back(p->strings[i] ? p->strings[i] : "");
-    if (p->n_nodes) throw Fail{GS_E_UNSUPPORTED, "existing nodes are not supported by this build yet"};
     c.build_vocab();
     c.build_catalog();
     c.build_templates();
     c.build_free_slots();
     c.build_pods();
+    c.build_nodes();
   } catch (const Fail& f) {
     return Err{f.code, f.msg};
   } catch (const std::out_of_range& ex) {

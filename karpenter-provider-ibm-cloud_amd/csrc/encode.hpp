@@ -108,6 +108,10 @@ struct Encoded {
   std::vector<gsd::VarRec> vars;
   std::vector<uint64_t> itmask;
   std::vector<gsd::FKEntry> fk_entries;
+  uint32_t NN = 0;
+  std::vector<uint32_t> node_order;  // device position -> gs_problem node index
+  std::vector<gsd::NodeRec> nodes;
+  std::vector<gsd::FK> n_fk;
   // host-only, for decode
   std::vector<Reqs> tmpl_reqs;  // incl. hostname In[omega]
   std::vector<PodVariant> variants;

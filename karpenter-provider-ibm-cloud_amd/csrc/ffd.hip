@@ -30,7 +30,8 @@ namespace {
 constexpr int FB = 1024;
 constexpr int NWAVE = FB / 64;
 constexpr int SEQ_SORT = 128;  // subranges up to this length sort on thread 0
-constexpr uint32_t THR_LDS_MAX = 4096;
+
+constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
 enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 
 struct Frame {
@@ -44,11 +45,18 @@ struct Shared {
   int piv, hint;
   uint64_t pops, generic, fast, cand, cand_full;
   uint64_t t_sort, t_scan, t_tmpl, t0;
-  uint64_t dbg[8];
+  uint64_t dbg[16];
+  uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
   uint32_t red[2][NWAVE];
   unsigned long long red64[RMAX];
   Frame stk[48];
+  // next-pod pipeline: wave 1 prefetches the next pop during the current pod
+  uint32_t nx_valid, nx_pod, nx_le, nx_ll, nx_cv, cb, use_pf;
+  alignas(16) uint32_t vrb[2][(sizeof(VarRec) / 4 + 3) & ~3u];
+  alignas(16) int64_t reqb[2][RMAX];
 };
+constexpr uint32_t VR_DW = sizeof(VarRec) / 4;
+static_assert(VR_DW <= 32, "VarRec prefetch uses one lane per dword");
 
 __device__ __forceinline__ int bits_len(uint64_t x) { return x ? 64 - __clzll((long long)x) : 0; }
 
@@ -593,37 +601,76 @@ struct Blk {
 };
 
 // first m in [m0, n) with thr[m] >= x (thresholds ascending); n if none
-__device__ __forceinline__ uint32_t thr_probe(const int64_t* thr, uint32_t n, uint32_t m0, int64_t x) {
+// Cursor advance over one resource's ascending thresholds: the first m >= m0
+// with thr[m] >= x.  A 4-wide window read in one LDS round trip covers the
+// common case; thr has 4 readable entries past every range.
+__device__ __forceinline__ uint32_t thr_window(const int64_t* thr, uint32_t n, uint32_t m0, int64_t x) {
   uint32_t m = m0;
-  for (int s = 0; s < 4 && m < n && thr[m] < x; s++) m++;
-  if (m < n && thr[m] < x) {
-    uint32_t lo = m, hi = n;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (thr[mid] < x) lo = mid + 1;
-      else hi = mid;
-    }
-    m = lo;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const int64_t vk = thr[m0 + k];  // unconditional: the padded LDS copy covers m0 + 3
+    m += (m0 + k < n && vk < x) ? 1u : 0u;
   }
   return m;
 }
 
+__device__ __forceinline__ uint32_t thr_search(const int64_t* thr, uint32_t n, uint32_t lo, int64_t x) {
+  uint32_t hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (thr[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// the kernel argument block, addressed in the constant (kernarg) space
+typedef const __attribute__((address_space(4))) DevProblem* KArg;
+
+// wave-uniform 64-bit value into SGPRs (readfirstlane is 32-bit)
+__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// sound quantized slack: ceil((maxa - tot) / unit), clamped to u16
+template <class DP>
+__device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa, const int64_t* tot) {
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++) {
+    if (r >= d.RQ) break;
+    const int64_t sl = maxa[r] - tot[r];
+    const uint32_t sh = d.q_shift[r];
+    int64_t q = sl <= 0 ? 0 : (sl + ((int64_t)1 << sh) - 1) >> sh;
+    if (q > 65535) q = 65535;
+    s |= (uint64_t)q << (16 * r);
+  }
+  return s;
+}
+
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
+template <uint32_t RR>
+__global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Shared S;
   const uint32_t MC = d.max_claims;
   uint16_t* s_ord = (uint16_t*)lds64;
   uint16_t* s_sc = s_ord + MC;
   uint16_t* s_scr = s_sc + MC;
-  uint8_t* s_tmpl = (uint8_t*)(s_scr + MC);
-  int64_t* s_thr = (int64_t*)(((uintptr_t)(s_tmpl + MC) + 7) & ~(uintptr_t)7);
+  uint64_t* s_slk = (uint64_t*)(s_scr + MC);  // 4x u16 quantized slack per claim
+  uint8_t* s_tmpl = (uint8_t*)(s_slk + MC);
+  // byte offset arithmetic keeps the pointer in the LDS address space (ds_read, not flat)
+  int64_t* s_thr = (int64_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u));
   __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
+  __shared__ uint32_t s_thoff[RMAX + 1];
   const uint32_t tid = threadIdx.x;
-  const uint32_t W = d.W, R = d.R, F = d.F, T = d.T, P = d.P;
+  constexpr uint32_t R = RR;  // resource dimensions (= d.R), compile-time
+  const uint32_t W = d.W, F = d.F, T = d.T, P = d.P;
   const uint32_t nthr = d.thr_off[R];
-  const int64_t* thr = nthr <= THR_LDS_MAX ? s_thr : d.thr_val;
+  const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   Blk blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
 
   for (uint32_t i = tid; i < P; i += FB) {
@@ -632,9 +679,15 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     d.last_len[i] = 0;
     d.cur_var[i] = d.var_begin[i];
   }
-  if (nthr <= THR_LDS_MAX)
-    for (uint32_t i = tid; i < nthr; i += FB) s_thr[i] = d.thr_val[i];
+  for (uint32_t i = tid; i < nthr + 4; i += FB) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
+  __shared__ uint64_t s_slot[SLOT_LDS_MAX];
+  const uint32_t nslot = d.Z * d.C * W;
+  const uint64_t* slot = s_slot;  // gs_prepare refuses Z*C*W > SLOT_LDS_MAX
+  for (uint32_t i = tid; i < nslot; i += FB) s_slot[i] = d.slot_set[i];
   for (uint32_t i = tid; i < T * R; i += FB) d.t_rem[i] = d.tmpl[i / R].limits[i % R];
+  for (uint32_t i = tid; i < d.NN; i += FB) d.nodes[i] = d.nodes0[i];
+  for (uint32_t i = tid; i < d.NN * F; i += FB) d.n_fk[i] = d.n_fk0[i];
+  if (tid <= R) s_thoff[tid] = d.thr_off[tid];
   for (uint32_t t = tid; t < T; t += FB) {
     s_tzm[t] = d.tmpl[t].zm;
     s_tcm[t] = d.tmpl[t].cm;
@@ -648,15 +701,62 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     S.nlog = 0;
     S.pops = S.generic = S.fast = S.cand = S.cand_full = 0;
     S.t_sort = S.t_scan = S.t_tmpl = 0;
-    for (int q = 0; q < 8; q++) S.dbg[q] = 0;
+    for (int q = 0; q < 16; q++) S.dbg[q] = 0;
     S.t0 = wall_clock64();
+    S.dbg[7] = __builtin_amdgcn_s_memtime();
     S.status = 0;
   }
   __syncthreads();
   const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
 
   uint64_t tLoop = 0;
+  // wave-1 prefetch registers: stage 0 none, 1 pod id, 2 counters+variant, 3 records
+  const uint32_t wave = tid >> 6, lane = tid & 63;
+  uint32_t pf_state = 0, pf_pod = 0, pf_le = 0, pf_ll = 0, pf_cv = 0, pf_vr = 0, pf_rq = 0;
+  auto pf_stage2 = [&]() {
+    if (wave == 1 && lane == 0 && pf_state == 1) {
+      pf_le = d.last_epoch[pf_pod];
+      pf_ll = d.last_len[pf_pod];
+      pf_cv = d.cur_var[pf_pod];
+      pf_state = 2;
+    }
+  };
+  auto pf_stage3 = [&]() {
+    if (wave == 1) {
+      const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+      if (st == 2) {
+        const uint32_t cv = (uint32_t)__shfl((int)pf_cv, 0), pp = (uint32_t)__shfl((int)pf_pod, 0);
+        if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.vars + cv))[lane];
+        if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.pod_req + (size_t)pp * R))[lane - 32];
+        pf_state = 3;
+      }
+    }
+  };
+  if (tid == 0) {
+    S.nx_valid = 0;
+    S.cb = 0;
+  }
   for (;;) {
+    // publish last iteration's prefetch into the spare buffer
+    if (wave == 1) {
+      const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+      if (st == 3) {
+        const uint32_t nb = S.cb ^ 1u;
+        if (lane < VR_DW) S.vrb[nb][lane] = pf_vr;
+        if (lane >= 32 && lane < 32 + 2 * RR) ((uint32_t*)S.reqb[nb])[lane - 32] = pf_rq;
+        if (lane == 0) {
+          S.nx_valid = 1;
+          S.nx_pod = pf_pod;
+          S.nx_le = pf_le;
+          S.nx_ll = pf_ll;
+          S.nx_cv = pf_cv;
+        }
+      } else if (lane == 0) {
+        S.nx_valid = 0;
+      }
+      pf_state = 0;
+    }
+    __syncthreads();
     // ------------------------------------------------------------ Queue.Pop
     if (tid == 0) tLoop = wall_clock64();
     if (tid == 0) {
@@ -667,15 +767,29 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       } else if (S.qlen == 0) {
         stop = 1;
       } else {
-        const uint32_t p = d.queue[S.qhead];
-        if (d.last_epoch[p] == S.epoch && d.last_len[p] == S.qlen) {
+        uint32_t p, le, ll, cv;
+        const bool pf = S.nx_valid != 0;
+        if (pf) {
+          p = S.nx_pod;
+          le = S.nx_le;
+          ll = S.nx_ll;
+          cv = S.nx_cv;
+        } else {
+          p = d.queue[S.qhead];
+          le = d.last_epoch[p];
+          ll = d.last_len[p];
+          cv = d.cur_var[p];
+        }
+        if (le == S.epoch && ll == S.qlen) {
           stop = 1;
         } else {
           S.qhead = S.qhead + 1 == P ? 0 : S.qhead + 1;
           S.qlen--;
           S.pops++;
           S.pod = p;
-          S.var = d.cur_var[p];
+          S.var = cv;
+          S.use_pf = pf ? 1u : 0u;
+          if (pf) S.cb ^= 1u;
         }
       }
       S.stop = stop;
@@ -684,13 +798,84 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     __syncthreads();
     if (S.stop) break;
     const uint32_t p = S.pod, v = S.var;
-    const VarRec vr = d.vars[v];
-    const int64_t* preq = d.pod_req + (size_t)p * R;
+    if (!S.use_pf) {
+      // not prefetched: wave 0 stages the variant record and requests in LDS
+      if (wave == 0) {
+        if (lane < VR_DW) S.vrb[S.cb][lane] = ((const uint32_t*)(d.vars + v))[lane];
+        if (lane >= 32 && lane < 32 + 2 * RR)
+          ((uint32_t*)S.reqb[S.cb])[lane - 32] = ((const uint32_t*)(d.pod_req + (size_t)p * R))[lane - 32];
+      }
+      __syncthreads();
+    }
+    const VarRec& vr = *(const VarRec*)S.vrb[S.cb];
+    const int64_t* preq = S.reqb[S.cb];
+    // stage 1: the next pod id (its queue slot cannot change during this pod
+    // unless the queue is empty now, when this pod itself may come back)
+    if (wave == 1 && lane == 0 && S.qlen > 0) {
+      pf_pod = d.queue[S.qhead];
+      pf_state = 1;
+    }
     const uint32_t M = S.M;
     uint64_t tA = 0;
     if (tid == 0) {
       tA = wall_clock64();
       S.dbg[4] += tA - tLoop;  // pop + variant load
+    }
+
+    int64_t rq[RR];
+    int64_t rqq[4];
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++) rq[r] = r < R ? uniform_i64(preq[r]) : 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? rq[r] >> d.q_shift[r] : 0;
+
+    // --------------- existing nodes in order: first ExistingNode.CanAdd wins
+    if (d.NN) {
+      uint32_t fn = INF;
+      for (uint32_t base = 0; base < d.NN; base += FB) {
+        const uint32_t n = base + tid;
+        bool feas = false;
+        if (n < d.NN) {
+          const NodeRec& nr = d.nodes[n];
+          feas = nr.ok && (nr.taints & ~vr.tol) == 0;  // Taints.ToleratesPod
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++)
+            feas = feas && (r >= R || nr.req[r] + rq[r] <= nr.avail[r]);  // Fits(requests, available)
+          // strict Compatible on label keys: the node's label value must be Has()
+          for (uint32_t k = 0; k < d.K && feas; k++) {
+            const uint32_t off = vr.itmask_off[k];
+            if (off == NONE) continue;
+            const uint32_t vid = nr.vid[k];
+            feas = vid != NONE && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+          }
+          if (feas && vr.zfull_off != NONE)
+            feas = nr.zvid != NONE && ((d.itmask[vr.zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+          if (feas && vr.cfull_off != NONE)
+            feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+          if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, d.n_fk + (size_t)n * F);
+        }
+        fn = blk.bmin(feas ? n : INF);
+        if (fn != INF) break;
+      }
+      if (fn != INF) {
+        // ExistingNode.Add: requests and requirements
+        if (tid < R) d.nodes[fn].req[tid] += preq[tid];
+        if (tid >= 64 && tid < 64 + vr.fk_count) {
+          const FKEntry& e = d.fk_entries[vr.fk_begin + (tid - 64)];
+          FK* nf = d.n_fk + (size_t)fn * F + e.slot;
+          const FK cur = *nf;
+          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                                         : e.st;
+        }
+        if (tid == 0) {
+          d.log[S.nlog++] = LogRec{p, v, fn | 0x80000000u, 0};
+          S.found = 1;
+        }
+        pf_stage2();
+        pf_stage3();
+        __syncthreads();
+        continue;
+      }
     }
 
     // ------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
@@ -769,68 +954,158 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       tA = tB;
     }
 
+    pf_stage2();
     // ---------------------- in-flight NodeClaims, first that CanAdd wins
-    int64_t rq[RMAX];
-#pragma unroll
-    for (uint32_t r = 0; r < RMAX; r++) rq[r] = r < R ? preq[r] : 0;
+    // A lane that finds its NodeClaim feasible keeps everything NodeClaim.Add
+    // needs in registers (new option words for W <= WREG, totals, cursors);
+    // the first feasible position (block min) writes them back directly.
     uint32_t f = INF;
     for (uint32_t base = 0; base < M; base += FB) {
+      // kernel arguments re-read per chunk (scalar loads) instead of being
+      // held across the whole pod loop: keeps SGPR spills out of this path
+      KArg dpp = (KArg)__builtin_amdgcn_kernarg_segment_ptr();  // d is the only argument
+      asm volatile("" : "+s"(dpp));
+      const auto& dd = *dpp;
       const uint32_t pos = base + tid;
       bool feas = false, pre = false;
+      uint32_t j = 0, t = 0;
+      uint64_t G = 0, Gt = 0;
+      uint32_t mrow[RR];
+      int64_t tot[RR];
+      uint64_t nx[WREG];
+#ifdef GS_FFD_DIAG
+      const uint64_t c0 = __builtin_amdgcn_s_memtime();
+      uint64_t c1 = 0, c2 = 0, c3 = 0;
+#endif
       if (pos < M) {
-        const uint32_t j = s_ord[pos];
-        const uint32_t t = s_tmpl[j];
-        if ((vr.tolt >> t) & 1) {
-          // one record read: totals, max-allocatable bound, cursors, masks
-          const ClaimRec* cr = d.c_rec + j;
-          int64_t tot[RMAX], mx[RMAX];
-          uint32_t cur[RMAX];
+        j = s_ord[pos];
+        t = s_tmpl[j];
+        // LDS-only necessary test: template tolerated and, per resource,
+        // floor(req/unit) <= ceil(slack/unit)
+        bool lp = (vr.tolt >> t) & 1;
+        const uint64_t sq = s_slk[j];
 #pragma unroll
-          for (uint32_t r = 0; r < RMAX; r++) {
-            tot[r] = r < R ? cr->tot[r] : 0;
-            mx[r] = r < R ? cr->maxa[r] : 0;
-            cur[r] = r < R ? cr->thr[r] : 0;
+        for (uint32_t r = 0; r < 4; r++) lp = lp && (uint64_t)rqq[r] <= ((sq >> (16 * r)) & 0xFFFFu);
+        if (lp) {
+#ifdef GS_ASM_MARK
+          asm volatile("; MARK_FULL_BEGIN");
+#endif
+          // one record read: totals, max-allocatable bound, cursors, masks
+          const ClaimRec* cr = dd.c_rec + j;
+          int64_t mx[RR];
+          uint32_t cur[RR];
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            tot[r] = cr->tot[r];
+            mx[r] = cr->maxa[r];
+            cur[r] = cr->thr[r];
           }
           const uint64_t zm = cr->zm, cm = cr->cm;
+          // option words and the (variant, template) row, issued with the
+          // record: they depend only on j and t
+          const uint64_t* row = dd.rows + ((size_t)v * T + t) * W;
+          const uint64_t* opts = dd.c_opts + (size_t)j * W;
+          if (W <= WREG) {
+#pragma unroll
+            for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? opts[w] & row[w] : 0;
+          }
           pre = true;
 #pragma unroll
-          for (uint32_t r = 0; r < RMAX; r++) pre = pre && (r >= R || tot[r] + rq[r] <= mx[r]);
-          if (pre && vr.fk_count) pre = var_fk_ok(d, vr, d.c_fk + (size_t)j * F);
+          for (uint32_t r = 0; r < RR; r++) pre = pre && tot[r] + rq[r] <= mx[r];
+#ifdef GS_FFD_DIAG
+          c1 = __builtin_amdgcn_s_memtime();
+#endif
+          if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)j * F);
           if (pre) {
-            const uint64_t G = grid_of(zm & vr.zm, cm & vr.cm, d.Z, d.C);
-            const uint64_t Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, d.Z, d.C);
-            uint32_t mrow[RMAX];
+            G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
+            Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, dd.Z, dd.C);
+            uint32_t mm[RR];
 #pragma unroll
-            for (uint32_t r = 0; r < RMAX; r++) {
-              mrow[r] = 0;
-              if (r < R) {
-                const uint32_t o = d.thr_off[r], n = d.thr_off[r + 1] - o;
-                mrow[r] = o + r + thr_probe(thr + o, n, cur[r], tot[r] + rq[r]);
-              }
+            for (uint32_t r = 0; r < RR; r++) {
+              const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+              mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
             }
-            const uint64_t* row = d.rows + ((size_t)v * T + t) * W;
-            const uint64_t* opts = d.c_opts + (size_t)j * W;
-            bool any = false;
-            for (uint32_t w = 0; w < W && !any; w++) {
-              uint64_t x = opts[w] & row[w];
 #pragma unroll
-              for (uint32_t r = 0; r < RMAX; r++)
-                if (r < R) x &= d.thr_set[(size_t)mrow[r] * W + w];
-              if (x && G != Gt) {
-                uint64_t y = 0, m = x;
-                while (m) {
-                  const uint32_t b = __ffsll((long long)m) - 1;
-                  m &= m - 1;
-                  if (d.it_pair[w * 64 + b] & G) y |= 1ull << b;
+            for (uint32_t r = 0; r < RR; r++) {
+              const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+              if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
+              mrow[r] = o + r + mm[r];
+            }
+#ifdef GS_FFD_DIAG
+            c2 = __builtin_amdgcn_s_memtime();
+#endif
+            uint64_t acc = 0;
+            if (W <= WREG) {
+              // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
+              // whose cursor moves narrows the options further
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                if (mm[r] != cur[r]) {
+#pragma unroll
+                  for (uint32_t w = 0; w < WREG; w++)
+                    if (w < W) nx[w] &= dd.thr_set[(size_t)mrow[r] * W + w];
                 }
-                x = y;
               }
-              any = x != 0;
+              if (G != Gt) {
+                // keep the types with an available offering on the narrowed
+                // (zone, capacity-type) grid: OR of the per-pair type sets
+                uint64_t off[WREG] = {};
+                uint64_t gm = G;
+                while (gm) {
+                  const uint32_t g = __ffsll((long long)gm) - 1;
+                  gm &= gm - 1;
+#pragma unroll
+                  for (uint32_t w = 0; w < WREG; w++)
+                    if (w < W) off[w] |= slot[g * W + w];
+                }
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++) nx[w] &= off[w];
+              }
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++) acc |= nx[w];
+            } else {
+              for (uint32_t w = 0; w < W && !acc; w++) {
+                uint64_t x = opts[w] & row[w];
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * W + w];
+                if (x && G != Gt) {
+                  uint64_t off = 0, gm = G;
+                  while (gm) {
+                    const uint32_t g = __ffsll((long long)gm) - 1;
+                    gm &= gm - 1;
+                    off |= slot[(size_t)g * W + w];
+                  }
+                  x &= off;
+                }
+                acc |= x;
+              }
             }
-            feas = any;
+            feas = acc != 0;
+#ifdef GS_FFD_DIAG
+            c3 = __builtin_amdgcn_s_memtime();
+#endif
           }
         }
       }
+#ifdef GS_FFD_DIAG
+      {
+        // per wave: cycles to the record test, the cursor probe, the option words
+        const uint64_t b1 = __ballot(c1 != 0), b3 = __ballot(c3 != 0);
+        if (b1 && (tid & 63) == (uint32_t)(__ffsll((long long)b1) - 1)) {
+          atomicAdd((unsigned long long*)&S.dbg[8], (unsigned long long)(c1 - c0));
+          atomicAdd((unsigned long long*)&S.dbg[11], 1ull);
+        }
+        if (b3 && (tid & 63) == (uint32_t)(__ffsll((long long)b3) - 1)) {
+          atomicAdd((unsigned long long*)&S.dbg[9], (unsigned long long)(c2 - c1));
+          atomicAdd((unsigned long long*)&S.dbg[10], (unsigned long long)(c3 - c2));
+          atomicAdd((unsigned long long*)&S.dbg[12], 1ull);
+        }
+        if (tid == 0) atomicAdd((unsigned long long*)&S.dbg[13], (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
+      }
+#endif
+#ifdef GS_ASM_MARK
+      asm volatile("; MARK_FULL_END");
+#endif
       const uint64_t pm = __ballot(pre);
       if ((tid & 63) == 0 && pm) atomicAdd((unsigned long long*)&S.cand_full, (unsigned long long)__popcll(pm));
       uint64_t tq = 0;
@@ -844,66 +1119,64 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         tA = tr_;
         S.cand += (M - base) < FB ? (M - base) : FB;
       }
-      if (f != INF) break;
-    }
-    if (f != INF) {
-      // NodeClaim.Add, block-parallel: options words, totals/cursors, keys
-      const uint32_t j = s_ord[f], t = s_tmpl[j];
-      ClaimRec* cr = d.c_rec + j;
-      const uint64_t G = grid_of(cr->zm & vr.zm, cr->cm & vr.cm, d.Z, d.C);
-      const uint64_t Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, d.Z, d.C);
-      uint32_t mrow[RMAX];
+      if (f != INF) {
+        if (pos == f) {
+          // NodeClaim.Add by the winning lane: options, requests, requirements
+          ClaimRec* cr = dd.c_rec + j;
+          uint64_t* opts = dd.c_opts + (size_t)j * W;
+          if (W <= WREG) {
 #pragma unroll
-      for (uint32_t r = 0; r < RMAX; r++) {
-        mrow[r] = 0;
-        if (r < R) {
-          const uint32_t o = d.thr_off[r], n = d.thr_off[r + 1] - o;
-          mrow[r] = o + r + thr_probe(thr + o, n, cr->thr[r], cr->tot[r] + rq[r]);
-        }
-      }
-      __syncthreads();  // every lane has read the record before it changes
-      const uint64_t* row = d.rows + ((size_t)v * T + t) * W;
-      uint64_t* opts = d.c_opts + (size_t)j * W;
-      for (uint32_t w = tid; w < W; w += FB) {
-        uint64_t x = opts[w] & row[w];
+            for (uint32_t w = 0; w < WREG; w++)
+              if (w < W) opts[w] = nx[w];  // already narrowed to the grid
+          } else {
+            const uint64_t* row = dd.rows + ((size_t)v * T + t) * W;
+            for (uint32_t w = 0; w < W; w++) {
+              uint64_t x = opts[w] & row[w];
 #pragma unroll
-        for (uint32_t r = 0; r < RMAX; r++)
-          if (r < R) x &= d.thr_set[(size_t)mrow[r] * W + w];
-        if (G != Gt) {
-          uint64_t off = 0, gm = G;
-          while (gm) {
-            const uint32_t g = __ffsll((long long)gm) - 1;
-            gm &= gm - 1;
-            off |= d.slot_set[(size_t)g * W + w];
+              for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * W + w];
+              if (G != Gt) {
+                uint64_t off = 0, gm = G;
+                while (gm) {
+                  const uint32_t g = __ffsll((long long)gm) - 1;
+                  gm &= gm - 1;
+                  off |= slot[(size_t)g * W + w];
+                }
+                x &= off;
+              }
+              opts[w] = x;
+            }
           }
-          x &= off;
+          int64_t nt[RR], ma[RR];
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            nt[r] = tot[r] + rq[r];
+            ma[r] = cr->maxa[r];
+            cr->tot[r] = nt[r];
+            cr->thr[r] = (uint16_t)(mrow[r] - s_thoff[r] - r);
+          }
+          s_slk[j] = pack_slack(dd, ma, nt);
+          cr->zm &= vr.zm;
+          cr->cm &= vr.cm;
+          cr->count++;
+          FK* cf = dd.c_fk + (size_t)j * F;
+          for (uint32_t k = 0; k < vr.fk_count; k++) {
+            const FKEntry& e = dd.fk_entries[vr.fk_begin + k];
+            const FK cur = cf[e.slot];
+            cf[e.slot] = (cur.flags & FK_PRESENT)
+                             ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * 64, dd.fk_isint[e.slot])
+                             : e.st;
+          }
+          if (s_sc[f] == 0xFFFFu) S.status = 3;
+          s_sc[f]++;
+          S.modkind = MOD_INC;
+          S.modpos = f;
+          dd.log[S.nlog++] = LogRec{p, v, j, 0};
+          S.found = 1;
         }
-        opts[w] = x;
-      }
-      if (tid >= 64 && tid < 64 + R) {
-        const uint32_t r = tid - 64;
-        cr->tot[r] += preq[r];
-        cr->thr[r] = (uint16_t)(mrow[r] - d.thr_off[r] - r);
-      }
-      if (tid >= 128 && tid < 128 + vr.fk_count) {
-        const FKEntry& e = d.fk_entries[vr.fk_begin + (tid - 128)];
-        FK* cf = d.c_fk + (size_t)j * F + e.slot;
-        const FK cur = *cf;
-        *cf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
-                                       : e.st;
-      }
-      if (tid == 0) {
-        cr->zm &= vr.zm;
-        cr->cm &= vr.cm;
-        cr->count++;
-        if (s_sc[f] == 0xFFFFu) S.status = 3;
-        s_sc[f]++;
-        S.modkind = MOD_INC;
-        S.modpos = f;
-        d.log[S.nlog++] = LogRec{p, v, j, 0};
-        S.found = 1;
+        break;
       }
     }
+    pf_stage3();
     __syncthreads();
     if (tid == 0) {
       const uint64_t tB = wall_clock64();
@@ -943,8 +1216,16 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       }
       const uint32_t j = M;
       ClaimRec* cr = d.c_rec + j;
+      if (tid < R) {
+        const int64_t tot = tr.daemon[tid] + preq[tid];
+        const uint32_t o = s_thoff[tid], n = s_thoff[tid + 1] - o;
+        S.c0[tid] = thr_search(thr + o, n, 0, tot);
+      }
+      __syncthreads();
       for (uint32_t w = tid; w < W; w += FB) {
         uint64_t x = row[w];
+        // establish opts ⊆ thr_set[cursor] for the candidate scan
+        for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * W + w];
         if (tr.has_limits) {
           uint64_t y = 0, m = x;
           while (m) {
@@ -960,13 +1241,12 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         }
         d.c_opts[(size_t)j * W + w] = x;
       }
-      if (tid < RMAX) {
+      if (tid < RR) {
         int64_t tot = 0;
         uint32_t c0 = 0;
         if (tid < R) {
           tot = tr.daemon[tid] + preq[tid];
-          const uint32_t o = d.thr_off[tid], n = d.thr_off[tid + 1] - o;
-          c0 = thr_probe(thr + o, n, 0, tot);
+          c0 = S.c0[tid];
         }
         cr->tot[tid] = tot;
         cr->thr[tid] = (uint16_t)c0;
@@ -1001,7 +1281,17 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         for (uint32_t r = 0; r < R; r++) atomicMax(&S.red64[r], (unsigned long long)d.it_alloc[(size_t)r * d.N + i]);
       }
       __syncthreads();
-      if (tid < RMAX) cr->maxa[tid] = tid < R ? (int64_t)S.red64[tid] : 0;
+      if (tid < RR) cr->maxa[tid] = tid < R ? (int64_t)S.red64[tid] : 0;
+      __syncthreads();
+      if (tid == 0) {
+        int64_t nt[RR], ma[RR];
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) {
+          nt[r] = cr->tot[r];
+          ma[r] = cr->maxa[r];
+        }
+        s_slk[j] = pack_slack(d, ma, nt);
+      }
       __syncthreads();
       if (tr.has_limits) {
         // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
@@ -1065,20 +1355,39 @@ extern "C" __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     c.t_scan = S.t_scan;
     c.t_tmpl = S.t_tmpl;
     c.t_total = wall_clock64() - S.t0;
-    for (int q = 0; q < 8; q++) c.dbg[q] = S.dbg[q];
+    S.dbg[7] = __builtin_amdgcn_s_memtime() - S.dbg[7];  // shader clock cycles over the kernel
+    for (int q = 0; q < 16; q++) c.dbg[q] = S.dbg[q];
     *d.ctrl = c;
   }
 }
 
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims) {
-  return ((7u * max_claims + 7u) & ~7u) + THR_LDS_MAX * 8u;
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr) {
+  const uint32_t thr = nthr + 4;
+  return 15u * max_claims + 8u + thr * 8u;
+}
+
+template <uint32_t RR>
+static hipError_t ffd_attr(uint32_t lds_bytes) {
+  return hipFuncSetAttribute((const void*)ffd_kernel<RR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
 }
 
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_bytes) {
-  return hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {ffd_attr<1>(lds_bytes), ffd_attr<2>(lds_bytes), ffd_attr<3>(lds_bytes), ffd_attr<4>(lds_bytes),
+                       ffd_attr<5>(lds_bytes), ffd_attr<6>(lds_bytes), ffd_attr<7>(lds_bytes), ffd_attr<8>(lds_bytes)})
+    if (x != hipSuccess) e = x;
+  return e;
 }
 
 extern "C" hipError_t gsk_ffd(const DevProblem* d, hipStream_t s) {
-  hipLaunchKernelGGL(ffd_kernel, dim3(1), dim3(FB), gsk_ffd_lds_bytes(d->max_claims), s, *d);
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr);
+  switch (d->R) {
+#define GSK_CASE(n) \
+  case n: hipLaunchKernelGGL(ffd_kernel<n>, dim3(1), dim3(FB), lds, s, *d); break;
+    GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
+#undef GSK_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

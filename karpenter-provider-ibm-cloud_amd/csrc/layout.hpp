@@ -18,6 +18,8 @@ constexpr int RMAX = 8;        // resource dimensions per vector
 constexpr int KMAX_IT = 8;     // requirement keys carried by instance types
 constexpr int FMAX = 16;       // "free" key slots (keys on neither ITs nor offerings)
 constexpr int TMAX = 64;       // NodeClaim templates (NodePools)
+constexpr uint32_t THR_LDS_MAX = 2048;   // fit thresholds staged in the FFD kernel's LDS
+constexpr uint32_t SLOT_LDS_MAX = 1024;  // (zone, capacity-type) pair type-set words in LDS
 constexpr int SMAX = 16;       // offerings per instance type
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
@@ -44,6 +46,7 @@ struct VarRec {
   uint32_t fk_begin, fk_count;
   uint32_t pad;
   uint32_t itmask_off[KMAX_IT];  // word offset into itmask arena, NONE = unconstrained
+  uint32_t zfull_off, cfull_off; // full-vocabulary zone / capacity-type masks (existing nodes)
   uint64_t zm, cm;               // Has over catalog zones / capacity types
   uint64_t tol;                  // tolerated taint-vocabulary mask
   uint64_t tolt;                 // templates whose taints this variant tolerates
@@ -72,6 +75,17 @@ struct alignas(64) ClaimRec {
 };
 static_assert(sizeof(ClaimRec) == 192, "ClaimRec layout");
 
+// existing (state) node: <U> ExistingNode
+struct NodeRec {
+  int64_t avail[RMAX];   // StateNode.Available()
+  int64_t req[RMAX];     // remaining daemonset requests + pods added in this Solve
+  uint64_t taints;       // taint-vocabulary mask
+  uint32_t ok;           // 0 if any available quantity is negative (never fits)
+  uint32_t zvid, cvid;   // zone / capacity-type label value ids (NONE = unlabeled)
+  uint32_t vid[KMAX_IT]; // instance-type-key label value ids (NONE = unlabeled)
+  uint32_t pad;
+};
+
 // add-log entry: pod popped & placed, in order
 struct LogRec {
   uint32_t pod, var, target, pad;  // target: claim id, or (node id | 0x80000000)
@@ -89,12 +103,16 @@ struct Ctrl {
   uint64_t cand_evals;   // in-flight NodeClaim candidates scored
   uint64_t cand_full;    // candidates that passed the slack prefilter
   uint64_t t_sort, t_scan, t_tmpl, t_total;  // wall_clock64 ticks (100 MHz) per phase
-  uint64_t dbg[8];                            // diagnostic phase counters
+  uint64_t dbg[16];                            // diagnostic phase counters
 };
 
 struct DevProblem {
   // sizes
   uint32_t N, W, R, Z, C, T, F, V, P, K, NT;  // K = IT keys, NT = taint vocab
+  uint32_t NN;                                // existing nodes
+  uint32_t RQ;                                // resources in the LDS slack prefilter (<= 4)
+  uint32_t n_thr;                             // thr_off[R] (host copy: sizes the dynamic LDS)
+  uint32_t q_shift[RMAX];                     // LDS slack unit = 2^q_shift per resource
   uint32_t max_claims;
   uint64_t wk_slots;  // free slots whose key is well-known
   // catalog
@@ -123,6 +141,10 @@ struct DevProblem {
   const uint64_t* itmask;      // arena
   const FKEntry* fk_entries;
   const uint32_t* queue0;      // [P] initial queue order
+  const NodeRec* nodes0;       // [NN] in <U> order: initialized first, then name
+  const FK* n_fk0;             // [NN][F] free-key requirement state per node
+  NodeRec* nodes;              // working copies (reset at every run)
+  FK* n_fk;
   // feasibility outputs
   uint64_t* rows;              // [V][T][W]
   uint32_t* cheapest;          // [V][T] IT index or NONE

@@ -336,3 +336,35 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 4)) * 1_000_000_000, req,
                   node_selector=sel, required_terms=required, preferred_terms=preferred, tolerations=tols)
     return b.build()
+
+
+def make_c4_sim(n_nodes=500, n_pods=2000, seed=0x5EED0004):
+    """one consolidation-style simulation (SURVEY §3.2 SimulateScheduling):
+    existing nodes sampled from the C2 catalog at 60-90% cpu use, plus the
+    pods of removed candidates to reschedule onto them or onto new NodeClaims"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c2_profiles(200)
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng, unavailable_frac=0.02)
+    daemon = {"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000}
+    b.add_nodepool("default", weight=0, requirements=[("kubernetes.io/arch", "In", ["amd64"]),
+                                                      ("kubernetes.io/os", "In", ["linux"])], daemon=daemon)
+    cand = [it for it in its if it.capacity["nvidia.com/gpu"] == 0 and it.capacity["cpu"] <= 32000]
+    for k in range(n_nodes):
+        it = cand[rng.integers(0, len(cand))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        zone = FAKE_ZONES[rng.integers(0, 3)]
+        ct = "spot" if rng.random() < 0.3 else "on-demand"
+        labels.update({"topology.kubernetes.io/zone": zone, "karpenter.sh/capacity-type": ct,
+                       "karpenter.sh/nodepool": "default", "kubernetes.io/os": "linux",
+                       "kubernetes.io/hostname": f"node-{k:05d}"})
+        alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        used = float(rng.uniform(0.6, 0.9))
+        avail = {"cpu": int(alloc["cpu"] * (1 - used)), "memory": int(alloc["memory"] * (1 - used)),
+                 "pods": alloc["pods"] - int(rng.integers(10, 25)) * 1000, "nvidia.com/gpu": 0}
+        b.add_node(f"node-{k:05d}", labels, avail, initialized=bool(rng.random() < 0.95))
+    _pods_basic(b, rng, n_pods, its, gpu_frac=0.005, selector_frac=0.10)
+    return b.build()
+
+
+CONFIGS["C4sim"] = make_c4_sim

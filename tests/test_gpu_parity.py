@@ -90,7 +90,7 @@ def test_solve_c3(solver):
 
 @pytest.mark.parametrize("seed", range(150))
 def test_solve_random(solver, seed):
-    check_solve(solver, synth.random_problem(seed, with_nodes=False))
+    check_solve(solver, synth.random_problem(seed))
 
 
 @pytest.mark.parametrize("seed", range(10))
@@ -105,3 +105,12 @@ def test_empty_pods(solver):
     b.add_nodepool("default")
     got, _ = solver.solve(b.build())
     assert got == {"claims": [], "nodes": [], "errors": []}
+
+
+def test_solve_existing_nodes_c4sim(solver):
+    check_solve(solver, synth.make_c4_sim(n_nodes=500, n_pods=2000))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_solve_random_with_nodes(solver, seed):
+    check_solve(solver, synth.random_problem(5000 + seed, n_pods=60))
