@@ -127,14 +127,6 @@ void upload_problem(gs_ctx* c) {
   d.wk_slots = e.wk_slots;
   d.RQ = std::min<uint32_t>(e.R, 4);
   d.n_thr = (uint32_t)e.thr_val.size();
-  for (uint32_t r = 0; r < gsd::RMAX; r++) {
-    int64_t mx = 1;
-    if (r < e.R)
-      for (uint32_t i = 0; i < e.N; i++) mx = std::max(mx, e.it_alloc[(size_t)r * e.N + i]);
-    int s = 0;  // power-of-two unit: shifts on the device, no 64-bit divides
-    while ((mx >> s) > 65535) s++;
-    d.q_shift[r] = (uint32_t)s;
-  }
   d.max_claims = std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
   c->upload(d.it_vid, e.it_vid);
   c->upload(d.it_alloc, e.it_alloc);
@@ -150,7 +142,15 @@ void upload_problem(gs_ctx* c) {
     c->upload(d.thr_val, tv);
   }
   c->upload(d.thr_off, e.thr_off);
-  c->upload(d.thr_set, e.thr_set);
+  {
+    // threshold rows re-strided to OW words (16-B aligned rows for the scan)
+    const uint32_t OW = std::max<uint32_t>(4, (e.W + 1) & ~1u);
+    const size_t nrows = e.W ? e.thr_set.size() / e.W : 0;
+    std::vector<uint64_t> ts(std::max<size_t>(nrows, 1) * OW, 0);
+    for (size_t q = 0; q < nrows; q++)
+      std::copy(e.thr_set.begin() + q * e.W, e.thr_set.begin() + (q + 1) * e.W, ts.begin() + q * OW);
+    c->upload(d.thr_set, ts);
+  }
   c->upload(d.fk_ival, e.fk_ival);
   c->upload(d.fk_isint, e.fk_isint);
   c->upload(d.tmpl, e.tmpl);
@@ -169,7 +169,8 @@ void upload_problem(gs_ctx* c) {
   c->alloc(d.nodes, std::max<uint32_t>(e.NN, 1));
   c->alloc(d.n_fk, e.n_fk.size());
   const size_t VT = (size_t)e.V * e.T, MC = d.max_claims;
-  c->alloc(d.rows, VT * e.W);
+  d.OW = std::max<uint32_t>(4, (e.W + 1) & ~1u);
+  c->alloc(d.rows, VT * d.OW);
   c->alloc(d.cheapest, VT);
   c->alloc(d.nfo, VT);
   c->alloc(d.fk_ok, VT);
@@ -178,7 +179,7 @@ void upload_problem(gs_ctx* c) {
   c->alloc(d.last_epoch, e.P);
   c->alloc(d.cur_var, e.P);
   c->alloc(d.c_rec, MC);
-  c->alloc(d.c_opts, MC * e.W);
+  c->alloc(d.c_opts, MC * d.OW);
   c->alloc(d.c_fk, MC * std::max<uint32_t>(e.F, 1));
   c->alloc(d.t_rem, (size_t)e.T * std::max<uint32_t>(e.R, 1));
   c->alloc(d.log, e.P);
@@ -412,7 +413,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     c->claim_it_offsets.push_back((uint32_t)c->claim_its.size());
     creq[j].erase(e.k_hostname);  // FinalizeScheduling
     c->req_text[j] = gsh::canonical(e, creq[j]);
-    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = hdr[j].tot[r];
+    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = hdr[j].tot(r);
   }
   c->req_ptrs.clear();
   for (auto& s : c->req_text) c->req_ptrs.push_back(s.c_str());
@@ -475,7 +476,8 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
   auto& e = c->enc;
   const uint32_t P = e.P, NP = c->problem->n_nodepools, W = e.W;
   float ms = 0;
-  std::vector<uint64_t> rows((size_t)e.V * e.T * W);
+  const uint32_t OW = c->dp.OW;
+  std::vector<uint64_t> rows((size_t)e.V * e.T * OW);
   std::vector<uint32_t> ch((size_t)e.V * e.T), nfo((size_t)e.V * e.T);
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -500,7 +502,7 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
     for (uint32_t t = 0; t < e.T; t++) {
       const uint32_t np = e.tmpl[t].np_index;
       const size_t src = (size_t)v * e.T + t, dst = (size_t)p * NP + np;
-      std::memcpy(&c->f_rows[dst * W], &rows[src * W], W * 8);
+      std::memcpy(&c->f_rows[dst * W], &rows[src * OW], W * 8);
       c->f_cheapest[dst] = ch[src] == gsd::NONE ? -1 : (int32_t)ch[src];
       c->f_nfo[dst] = nfo[src];
     }

@@ -634,18 +634,35 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t x) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// sound quantized slack: ceil((maxa - tot) / unit), clamped to u16
+// Monotone 16-bit code of a non-negative quantity: exact below 1024, then a
+// 9-bit mantissa per binade (relative step <= 2^-9).  codes are consecutive
+// in value order, so floor/ceil differ by at most one.
+__device__ __forceinline__ uint32_t qcode_floor(int64_t v) {
+  if (v <= 0) return 0;
+  const uint64_t x = (uint64_t)v;
+  const uint32_t b = 64u - (uint32_t)__clzll((long long)x);
+  if (b <= 10) return (uint32_t)x;
+  const uint32_t s = b - 10;
+  return 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
+}
+__device__ __forceinline__ uint32_t qcode_ceil(int64_t v) {
+  if (v <= 0) return 0;
+  const uint64_t x = (uint64_t)v;
+  const uint32_t b = 64u - (uint32_t)__clzll((long long)x);
+  if (b <= 10) return (uint32_t)x;
+  const uint32_t s = b - 10;
+  const uint32_t c = 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
+  return c + ((x & ((1ull << s) - 1)) ? 1u : 0u);
+}
+
+// LDS slack of a NodeClaim: qcode_ceil(maxa - tot) per resource (<= 4)
 template <class DP>
 __device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa, const int64_t* tot) {
   uint64_t s = 0;
 #pragma unroll
   for (uint32_t r = 0; r < 4; r++) {
     if (r >= d.RQ) break;
-    const int64_t sl = maxa[r] - tot[r];
-    const uint32_t sh = d.q_shift[r];
-    int64_t q = sl <= 0 ? 0 : (sl + ((int64_t)1 << sh) - 1) >> sh;
-    if (q > 65535) q = 65535;
-    s |= (uint64_t)q << (16 * r);
+    s |= (uint64_t)qcode_ceil(maxa[r] - tot[r]) << (16 * r);
   }
   return s;
 }
@@ -669,6 +686,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t R = RR;  // resource dimensions (= d.R), compile-time
   const uint32_t W = d.W, F = d.F, T = d.T, P = d.P;
+  const uint32_t OW = d.OW;  // claim option stride (words, 16-B multiple)
   const uint32_t nthr = d.thr_off[R];
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   Blk blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
@@ -823,11 +841,8 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     }
 
     int64_t rq[RR];
-    int64_t rqq[4];
 #pragma unroll
     for (uint32_t r = 0; r < RR; r++) rq[r] = r < R ? uniform_i64(preq[r]) : 0;
-#pragma unroll
-    for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? rq[r] >> d.q_shift[r] : 0;
 
     // --------------- existing nodes in order: first ExistingNode.CanAdd wins
     if (d.NN) {
@@ -955,6 +970,10 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     }
 
     pf_stage2();
+    // request codes for the LDS slack test (computed here: not live across the sort)
+    uint32_t rqq[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? qcode_floor(rq[r]) : 0;
     // ---------------------- in-flight NodeClaims, first that CanAdd wins
     // A lane that finds its NodeClaim feasible keeps everything NodeClaim.Add
     // needs in registers (new option words for W <= WREG, totals, cursors);
@@ -981,7 +1000,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         j = s_ord[pos];
         t = s_tmpl[j];
         // LDS-only necessary test: template tolerated and, per resource,
-        // floor(req/unit) <= ceil(slack/unit)
+        // qcode_floor(request) <= qcode_ceil(slack)
         bool lp = (vr.tolt >> t) & 1;
         const uint64_t sq = s_slk[j];
 #pragma unroll
@@ -990,28 +1009,43 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
 #ifdef GS_ASM_MARK
           asm volatile("; MARK_FULL_BEGIN");
 #endif
-          // one record read: totals, max-allocatable bound, cursors, masks
+          // one 64-B header read (four 16-B loads): totals, cursors, masks
           const ClaimRec* cr = dd.c_rec + j;
-          int64_t mx[RR];
           uint32_t cur[RR];
+          uint64_t zm, cm;
+          {
+            const uint4* q = (const uint4*)cr;
+            const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+            const int64_t lo[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                   (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+            const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+            zm = ((uint64_t)h2.w << 32) | h2.z;
+            cm = ((uint64_t)h3.y << 32) | h3.x;
 #pragma unroll
-          for (uint32_t r = 0; r < RR; r++) {
-            tot[r] = cr->tot[r];
-            mx[r] = cr->maxa[r];
-            cur[r] = cr->thr[r];
+            for (uint32_t r = 0; r < RR; r++) {
+              tot[r] = r < 4 ? lo[r] : cr->tot_hi[r - 4];
+              cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+            }
           }
-          const uint64_t zm = cr->zm, cm = cr->cm;
-          // option words and the (variant, template) row, issued with the
-          // record: they depend only on j and t
-          const uint64_t* row = dd.rows + ((size_t)v * T + t) * W;
-          const uint64_t* opts = dd.c_opts + (size_t)j * W;
+          // option words (stride OW, 16-B aligned) and the (variant, template)
+          // row: they depend only on j and t, issued with the header
+          const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
+          const uint64_t* opts = dd.c_opts + (size_t)j * OW;
           if (W <= WREG) {
+            // unconditional 16-B loads (stride OW >= 4 words): no per-word branches
+            const uint4* oq = (const uint4*)opts;
+            const uint4* rq4 = (const uint4*)row;
+            const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+            const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                   (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                   (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                   (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
 #pragma unroll
-            for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? opts[w] & row[w] : 0;
+            for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
           }
+          // the exact fit test is implied by the threshold rows below; the
+          // LDS slack test above already rejected the clear misfits
           pre = true;
-#pragma unroll
-          for (uint32_t r = 0; r < RR; r++) pre = pre && tot[r] + rq[r] <= mx[r];
 #ifdef GS_FFD_DIAG
           c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1041,9 +1075,12 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
 #pragma unroll
               for (uint32_t r = 0; r < RR; r++) {
                 if (mm[r] != cur[r]) {
-#pragma unroll
-                  for (uint32_t w = 0; w < WREG; w++)
-                    if (w < W) nx[w] &= dd.thr_set[(size_t)mrow[r] * W + w];
+                  const uint4* tq = (const uint4*)(dd.thr_set + (size_t)mrow[r] * OW);
+                  const uint4 t0 = tq[0], t1 = tq[1];
+                  nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                  nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                  nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                  nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
                 }
               }
               if (G != Gt) {
@@ -1067,7 +1104,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
               for (uint32_t w = 0; w < W && !acc; w++) {
                 uint64_t x = opts[w] & row[w];
 #pragma unroll
-                for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * W + w];
+                for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
                 if (x && G != Gt) {
                   uint64_t off = 0, gm = G;
                   while (gm) {
@@ -1123,17 +1160,17 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         if (pos == f) {
           // NodeClaim.Add by the winning lane: options, requests, requirements
           ClaimRec* cr = dd.c_rec + j;
-          uint64_t* opts = dd.c_opts + (size_t)j * W;
+          uint64_t* opts = dd.c_opts + (size_t)j * OW;
           if (W <= WREG) {
 #pragma unroll
             for (uint32_t w = 0; w < WREG; w++)
               if (w < W) opts[w] = nx[w];  // already narrowed to the grid
           } else {
-            const uint64_t* row = dd.rows + ((size_t)v * T + t) * W;
+            const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
             for (uint32_t w = 0; w < W; w++) {
               uint64_t x = opts[w] & row[w];
 #pragma unroll
-              for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * W + w];
+              for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
               if (G != Gt) {
                 uint64_t off = 0, gm = G;
                 while (gm) {
@@ -1151,10 +1188,10 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
           for (uint32_t r = 0; r < RR; r++) {
             nt[r] = tot[r] + rq[r];
             ma[r] = cr->maxa[r];
-            cr->tot[r] = nt[r];
-            cr->thr[r] = (uint16_t)(mrow[r] - s_thoff[r] - r);
+            cr->tot(r) = nt[r];
+            cr->thr(r) = (uint16_t)(mrow[r] - s_thoff[r] - r);
           }
-          s_slk[j] = pack_slack(dd, ma, nt);
+          s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
           cr->zm &= vr.zm;
           cr->cm &= vr.cm;
           cr->count++;
@@ -1191,7 +1228,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     // ------------------------------- new NodeClaim from templates, in order
     for (uint32_t t = 0; t < T; t++) {
       const TmplRec& tr = d.tmpl[t];
-      const uint64_t* row = d.rows + ((size_t)v * T + t) * W;
+      const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
       bool any = false;
       if (d.fk_ok[(size_t)v * T + t])
         for (uint32_t w = 0; w < W; w++)
@@ -1225,7 +1262,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       for (uint32_t w = tid; w < W; w += FB) {
         uint64_t x = row[w];
         // establish opts ⊆ thr_set[cursor] for the candidate scan
-        for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * W + w];
+        for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * OW + w];
         if (tr.has_limits) {
           uint64_t y = 0, m = x;
           while (m) {
@@ -1239,7 +1276,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
           }
           x = y;
         }
-        d.c_opts[(size_t)j * W + w] = x;
+        d.c_opts[(size_t)j * OW + w] = x;
       }
       if (tid < RR) {
         int64_t tot = 0;
@@ -1248,8 +1285,8 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
           tot = tr.daemon[tid] + preq[tid];
           c0 = S.c0[tid];
         }
-        cr->tot[tid] = tot;
-        cr->thr[tid] = (uint16_t)c0;
+        cr->tot(tid) = tot;
+        cr->thr(tid) = (uint16_t)c0;
         S.red64[tid] = 0;
       }
       if (tid == 0) {
@@ -1277,18 +1314,18 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       __syncthreads();
       // max allocatable over the new claim's options (the slack bound)
       for (uint32_t i = tid; i < d.N; i += FB) {
-        if (!((d.c_opts[(size_t)j * W + (i >> 6)] >> (i & 63)) & 1)) continue;
+        if (!((d.c_opts[(size_t)j * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
         for (uint32_t r = 0; r < R; r++) atomicMax(&S.red64[r], (unsigned long long)d.it_alloc[(size_t)r * d.N + i]);
       }
       __syncthreads();
       if (tid < RR) cr->maxa[tid] = tid < R ? (int64_t)S.red64[tid] : 0;
-      __syncthreads();
       if (tid == 0) {
+        // LDS slack from the max allocatable over the new claim's options
         int64_t nt[RR], ma[RR];
 #pragma unroll
         for (uint32_t r = 0; r < RR; r++) {
-          nt[r] = cr->tot[r];
-          ma[r] = cr->maxa[r];
+          nt[r] = r < R ? tr.daemon[r] + preq[r] : 0;
+          ma[r] = r < R ? (int64_t)S.red64[r] : 0;
         }
         s_slk[j] = pack_slack(d, ma, nt);
       }
@@ -1298,7 +1335,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
         if (tid < R) S.red64[tid] = 0;
         __syncthreads();
         for (uint32_t i = tid; i < d.N; i += FB) {
-          if (!((d.c_opts[(size_t)j * W + (i >> 6)] >> (i & 63)) & 1)) continue;
+          if (!((d.c_opts[(size_t)j * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
           for (uint32_t r = 0; r < R; r++)
             if ((tr.limit_rmask >> r) & 1)
               atomicMax(&S.red64[r], (unsigned long long)(d.it_cap[(size_t)r * d.N + i] + (1ll << 62)));

@@ -41,7 +41,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   const uint32_t v = pair / d.T, t = pair % d.T;
   const VarRec vr = d.vars[v];
   const TmplRec& tr = d.tmpl[t];
-  uint64_t* rowout = d.rows + (size_t)pair * d.W;
+  uint64_t* rowout = d.rows + (size_t)pair * d.OW;
 
   // wave-uniform parts of NodeClaim.CanAdd on a fresh NodeClaim
   bool ok_all = (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
@@ -120,7 +120,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
   if (tid == 0) cnt = 0;
   __syncthreads();
   for (uint32_t i = tid; i < d.N; i += BLOCK) {
-    if (!((d.c_opts[(size_t)j * d.W + (i >> 6)] >> (i & 63)) & 1)) continue;
+    if (!((d.c_opts[(size_t)j * d.OW + (i >> 6)] >> (i & 63)) & 1)) continue;
     uint32_t minp = NONE;
     uint64_t m = d.it_pair[i] & G;
     while (m) {

@@ -11,6 +11,7 @@
 //  * resources are int64 milli-units, R <= RMAX per vector.
 #pragma once
 #include <stdint.h>
+#include <stddef.h>
 
 namespace gsd {
 
@@ -66,14 +67,24 @@ struct TmplRec {
 // per-claim record (device-owned, AoS: one candidate = one 192-B record read
 // in a single round trip)
 struct alignas(64) ClaimRec {
-  int64_t tot[RMAX];    // requests: daemon overhead + pods (Merge)
-  int64_t maxa[RMAX];   // max allocatable over the claim's initial options (upper bound)
-  uint64_t zm, cm;      // Has over catalog zones / capacity types
-  uint16_t thr[RMAX];   // threshold cursors: lower_bound(thr_val_r, tot_r)
+  // hot 64-B header: everything the candidate scan reads for R <= 4, one
+  // line and four 16-B loads per lane
+  int64_t tot_lo[4];     // requests: daemon overhead + pods (Merge), resources 0..3
+  uint16_t thr_lo[4];    // threshold cursors: lower_bound(thr_val_r, tot_r)
+  uint64_t zm, cm;       // Has over catalog zones / capacity types
   uint32_t tmpl, count;
+  // resources 4..7
+  int64_t tot_hi[RMAX - 4];
+  uint16_t thr_hi[RMAX - 4];
   uint32_t pad[6];
+  int64_t maxa[RMAX];    // max allocatable over the claim's initial options (slack bound)
+  __host__ __device__ int64_t& tot(uint32_t r) { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
+  __host__ __device__ int64_t tot(uint32_t r) const { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
+  __host__ __device__ uint16_t& thr(uint32_t r) { return r < 4 ? thr_lo[r] : thr_hi[r - 4]; }
+  __host__ __device__ uint16_t thr(uint32_t r) const { return r < 4 ? thr_lo[r] : thr_hi[r - 4]; }
 };
 static_assert(sizeof(ClaimRec) == 192, "ClaimRec layout");
+static_assert(offsetof(ClaimRec, tot_hi) == 64, "ClaimRec hot header");
 
 // existing (state) node: <U> ExistingNode
 struct NodeRec {
@@ -111,8 +122,8 @@ struct DevProblem {
   uint32_t N, W, R, Z, C, T, F, V, P, K, NT;  // K = IT keys, NT = taint vocab
   uint32_t NN;                                // existing nodes
   uint32_t RQ;                                // resources in the LDS slack prefilter (<= 4)
+  uint32_t OW;                                // c_opts stride: max(4, W rounded up to even)
   uint32_t n_thr;                             // thr_off[R] (host copy: sizes the dynamic LDS)
-  uint32_t q_shift[RMAX];                     // LDS slack unit = 2^q_shift per resource
   uint32_t max_claims;
   uint64_t wk_slots;  // free slots whose key is well-known
   // catalog
@@ -126,7 +137,7 @@ struct DevProblem {
   const uint64_t* slot_set;    // [64][W] ITs with an available offering on pair g
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
-  const uint64_t* thr_set;     // [(n_r+1) per r][W], offsets thr_off[r]+r
+  const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
   const int64_t* fk_ival;      // [F][64] integer value of vocabulary entries
   const uint64_t* fk_isint;    // [F]
   // templates
@@ -146,7 +157,7 @@ struct DevProblem {
   NodeRec* nodes;              // working copies (reset at every run)
   FK* n_fk;
   // feasibility outputs
-  uint64_t* rows;              // [V][T][W]
+  uint64_t* rows;              // [V][T][OW]
   uint32_t* cheapest;          // [V][T] IT index or NONE
   uint32_t* nfo;               // [V][T]
   uint32_t* fk_ok;             // [V][T] free-key Compatible vs the fresh template
@@ -156,7 +167,7 @@ struct DevProblem {
   uint32_t* last_epoch;        // [P]
   uint32_t* cur_var;           // [P]
   ClaimRec* c_rec;             // [max_claims]
-  uint64_t* c_opts;            // [max_claims][W]
+  uint64_t* c_opts;            // [max_claims][OW]
   FK* c_fk;                    // [max_claims][F]
   int64_t* t_rem;              // [T][R] remaining limits (dynamic)
   LogRec* log;                 // [P]
