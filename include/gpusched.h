@@ -221,13 +221,94 @@ typedef struct gs_feas_result {
   double t_kernel_ms;
 } gs_feas_result;
 
+typedef struct gs_ctx gs_ctx;
+
 typedef struct gs_config {
   int32_t device;        /* HIP device ordinal */
   uint32_t max_claims;   /* 0 = default */
   uint32_t flags;        /* reserved */
 } gs_config;
 
-typedef struct gs_ctx gs_ctx;
+/* ------------------------------------------------------------------------
+ * Consolidation (<U> pkg/controllers/disruption: SimulateScheduling +
+ * computeConsolidation, SingleNodeConsolidation, MultiNodeConsolidation;
+ * SURVEY.md §3.2).  Each simulation removes a candidate set of state nodes
+ * and re-Solves their reschedulable pods together with the pending pods
+ * against the remaining nodes.  Every simulation is an independent Solve:
+ * the device runs one workgroup per simulation.
+ * ------------------------------------------------------------------------ */
+enum {
+  GS_CONSOLIDATE_EVAL = 0,   /* evaluate the candidate sets in `sets` */
+  GS_CONSOLIDATE_SINGLE = 1, /* SingleNodeConsolidation: one set per candidate, in order */
+  GS_CONSOLIDATE_MULTI = 2   /* MultiNodeConsolidation: prefixes candidates[0:mid+1] of the binary search */
+};
+
+enum { GS_DECISION_NOOP = 0, GS_DECISION_DELETE = 1, GS_DECISION_REPLACE = 2, GS_DECISION_SKIPPED = 3 };
+
+/* why a simulation is a NoOp (computeConsolidation's early returns, in order) */
+enum {
+  GS_NOOP_NONE = 0,
+  GS_NOOP_UNSCHEDULABLE = 1,   /* !AllNonPendingPodsScheduled (incl. uninitialized-node placements) */
+  GS_NOOP_MULTIPLE_CLAIMS = 2, /* more than one new NodeClaim */
+  GS_NOOP_PRICE_UNKNOWN = 3,   /* getCandidatePrices: no offering of a candidate's type matches its labels */
+  GS_NOOP_SPOT_TO_SPOT = 4,    /* all candidates spot, replacement may be spot, SpotToSpotConsolidation off */
+  GS_NOOP_NOT_CHEAPER = 5,     /* RemoveInstanceTypeOptionsByPriceAndMinValues left no option */
+  GS_NOOP_SAME_TYPE = 6        /* multi-node: filterOutSameInstanceType left no option */
+};
+
+typedef struct gs_consolidation {
+  const gs_problem* cluster;        /* catalog, NodePools, ACTIVE state nodes, PENDING pods */
+  const gs_pod* bound_pods;         /* reschedulable pods bound to state nodes; their ranges index the */
+  uint32_t n_bound_pods;            /*   cluster's arrays (strings, quantities, labels, terms, ...) */
+  const uint32_t* bound_pod_node;   /* [n_bound_pods] index into cluster->nodes */
+  const uint32_t* candidates;       /* candidate node indices, disruption order (sortCandidates) */
+  uint32_t n_candidates;
+  const gs_range* sets;             /* GS_CONSOLIDATE_EVAL: candidate sets, ranges into candidates[] */
+  uint32_t n_sets;
+  uint32_t mode;                    /* GS_CONSOLIDATE_* */
+  uint32_t max_candidates;          /* MULTI: batch cap (upstream 100); 0 = 100 */
+  uint32_t shard_index, shard_count;/* evaluate only sims s with s % shard_count == shard_index (0,0 = all) */
+} gs_consolidation;
+
+/* one computeConsolidation outcome */
+typedef struct gs_command {
+  uint32_t decision;       /* GS_DECISION_* */
+  uint32_t reason;         /* GS_NOOP_* */
+  uint32_t n_new_claims;   /* NodeClaims the simulation opened */
+  uint32_t n_failed_pods;  /* non-pending pods left without a place */
+  uint32_t n_candidates;   /* size of the simulated candidate set */
+  uint32_t nodepool;       /* REPLACE: the replacement's NodePool index */
+  uint32_t spot_only;      /* REPLACE: capacity-type requirement narrowed to spot (OD -> [OD, spot]) */
+  gs_range options;        /* REPLACE: catalog IT indices in OrderByPrice order, into result.options */
+  double candidate_price;  /* getCandidatePrices */
+} gs_command;
+
+typedef struct gs_consolidation_result {
+  uint32_t n_commands;     /* one per simulation */
+  const gs_command* commands;
+  const uint32_t* options;        /* replacement options of all commands */
+  const double* option_prices;    /* [same] cheapest available compatible offering price */
+  int32_t chosen;          /* SINGLE/MULTI (unsharded): the command the policy returns, -1 = none */
+  uint32_t n_multi_options;/* MULTI: the chosen Replace's options after filterOutSameInstanceType */
+  const uint32_t* multi_options;
+  uint32_t pods_simulated; /* sum over simulations of the pods re-solved */
+  uint64_t checks;         /* sum over simulations of pod x (existing node + offering) checks */
+  double t_encode_ms, t_upload_ms, t_feas_ms, t_sim_ms, t_truncate_ms, t_fetch_ms;
+} gs_consolidation_result;
+
+/* evaluate consolidation simulations on the device (encode + upload + run + decide) */
+gs_status gs_consolidate(gs_ctx* ctx, const gs_consolidation* in, gs_consolidation_result* out);
+/* re-run the device part on the same input (bench: inputs stay resident) */
+gs_status gs_consolidate_rerun(gs_ctx* ctx, gs_consolidation_result* out);
+/* host-only policy replay over a complete command table (e.g. after an
+ * all-gather of sharded evaluations): SINGLE = first non-NoOp in order,
+ * MULTI = firstNConsolidationOption's binary search with filterOutSameInstanceType.
+ * `options`/`option_prices` back the commands' option ranges.  Writes the chosen index (-1 none)
+ * and, for MULTI, the surviving options of the chosen command into
+ * multi_options (capacity 60) / *n_multi_options. */
+gs_status gs_consolidation_choose(const gs_consolidation* in, const gs_command* commands, uint32_t n_commands,
+                                  const uint32_t* options, const double* option_prices, int32_t* chosen,
+                                  uint32_t* multi_options, uint32_t* n_multi_options);
 
 gs_status gs_create(const gs_config* cfg, gs_ctx** out);
 void gs_destroy(gs_ctx* ctx);
@@ -256,8 +337,9 @@ gs_status gs_validate(const gs_problem* problem, char* err, size_t err_len);
 /* sizeof of every ABI struct, in this order: gs_range, gs_requirement,
  * gs_quantity, gs_label, gs_taint, gs_toleration, gs_term, gs_offering,
  * gs_instance_type, gs_nodepool, gs_pod, gs_node, gs_problem, gs_result,
- * gs_feas_result, gs_config.  Bindings check their layouts against it.
- * Returns the number of entries (16); writes min(n, 16). */
+ * gs_feas_result, gs_config, gs_consolidation, gs_command,
+ * gs_consolidation_result.  Bindings check their layouts against it.
+ * Returns the number of entries (19); writes min(n, 19). */
 uint32_t gs_abi_sizes(uint32_t* out, uint32_t n);
 
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);

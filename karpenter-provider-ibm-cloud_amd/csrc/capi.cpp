@@ -1,112 +1,15 @@
 // capi.cpp — C-ABI of libgpusched.so (include/gpusched.h): context, HBM
 // buffers, kernel launches on one HIP stream, result decode.
-#include <hip/hip_runtime.h>
+#include "ctx.hpp"
 
-#include <algorithm>
-#include <chrono>
-#include <cstring>
-#include <string>
-#include <vector>
-
-#include "../../include/gpusched.h"
-#include "encode.hpp"
-#include "layout.hpp"
-
-extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
-extern "C" hipError_t gsk_init_ffd(uint32_t lds_bytes);
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr);
-extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
-extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, hipStream_t s);
-extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
-
-namespace {
-
-constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: ord/sc/scratch u16, tmpl u8, 4x u16 slack, thresholds
-
-using Clock = std::chrono::steady_clock;
-double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
-
-struct HipError {
-  std::string msg;
-};
-#define HIPCHK(x)                                                                        \
-  do {                                                                                   \
-    hipError_t e_ = (x);                                                                 \
-    if (e_ != hipSuccess) throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)}; \
-  } while (0)
-
-}  // namespace
-
-struct gs_ctx {
-  int device = 0;
-  std::string err;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[8] = {};
-  std::vector<void*> allocs;
-  gsh::Encoded enc;
-  gsd::DevProblem dp{};
-  bool prepared = false, ran = false;
-  double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
-  const gs_problem* problem = nullptr;
-  // result storage
-  std::vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
-  std::vector<std::string> req_text;
-  std::vector<const char*> req_ptrs;
-  std::vector<int64_t> claim_requests;
-  std::vector<uint32_t> node_pod_offsets, node_pods, error_pods;
-  std::vector<uint64_t> f_rows;
-  std::vector<int32_t> f_cheapest;
-  std::vector<uint32_t> f_nfo;
-  gsd::Ctrl ctrl{};
-
-  void free_all() {
-    for (void* p : allocs) (void)hipFree(p);
-    allocs.clear();
-  }
-  // Device buffers of one prepared problem come from ONE allocation (an arena
-  // of 256-B aligned sub-buffers): large pages, few TLB entries for the
-  // single-workgroup FFD kernel's gathers.  plan() records, commit() places.
-  struct Planned {
-    void** dst;
-    size_t off, bytes;
-    std::vector<char> host;
-  };
-  std::vector<Planned> plan;
-  size_t plan_bytes = 0;
-  template <class P>
-  void alloc(P*& dst, size_t n) {
-    const size_t b = std::max<size_t>(n, 1) * sizeof(P);
-    plan.push_back(Planned{(void**)&dst, plan_bytes, b, {}});
-    plan_bytes += (b + 255) & ~(size_t)255;
-  }
-  template <class P, class T>
-  void upload(P*& dst, const std::vector<T>& v) {
-    static_assert(sizeof(P) == sizeof(T), "upload type");
-    alloc(dst, v.size());
-    plan.back().host.assign((const char*)v.data(), (const char*)v.data() + v.size() * sizeof(T));
-  }
-  void commit() {
-    void* base = nullptr;
-    HIPCHK(hipMalloc(&base, std::max<size_t>(plan_bytes, 256)));
-    allocs.push_back(base);
-    for (auto& q : plan) {
-      *q.dst = (char*)base + q.off;
-      if (!q.host.empty()) HIPCHK(hipMemcpyAsync(*q.dst, q.host.data(), q.host.size(), hipMemcpyHostToDevice, stream));
-    }
-    HIPCHK(hipStreamSynchronize(stream));
-    plan.clear();
-    plan_bytes = 0;
-  }
-};
-
-namespace {
+namespace gsc {
 
 gs_status fail(gs_ctx* c, gs_status s, const std::string& m) {
   c->err = m;
   return s;
 }
 
-void upload_problem(gs_ctx* c) {
+void upload_problem(gs_ctx* c, const SimPlan* sims) {
   auto& e = c->enc;
   auto& d = c->dp;
   c->plan.clear();
@@ -127,7 +30,8 @@ void upload_problem(gs_ctx* c) {
   d.wk_slots = e.wk_slots;
   d.RQ = std::min<uint32_t>(e.R, 4);
   d.n_thr = (uint32_t)e.thr_val.size();
-  d.max_claims = std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
+  d.max_claims = sims ? std::max<uint32_t>(sims->max_pods, 1)
+                      : std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
   c->upload(d.it_vid, e.it_vid);
   c->upload(d.it_alloc, e.it_alloc);
   c->upload(d.it_cap, e.it_cap);
@@ -166,27 +70,47 @@ void upload_problem(gs_ctx* c) {
   d.NN = e.NN;
   c->upload(d.nodes0, e.nodes);
   c->upload(d.n_fk0, e.n_fk);
-  c->alloc(d.nodes, std::max<uint32_t>(e.NN, 1));
-  c->alloc(d.n_fk, e.n_fk.size());
-  const size_t VT = (size_t)e.V * e.T, MC = d.max_claims;
+  // the provisioning Solve works on a global copy of the nodes; simulations
+  // share nodes0 read-only and keep per-block overlays
+  c->alloc(d.nodes, sims ? 1 : std::max<uint32_t>(e.NN, 1));
+  c->alloc(d.n_fk, sims ? 1 : e.n_fk.size());
+  const size_t VT = (size_t)e.V * e.T, F1 = std::max<uint32_t>(e.F, 1), R1 = std::max<uint32_t>(e.R, 1);
+  // pod arenas (queue, log) and claim arenas: the whole problem, or the sum
+  // over simulations (a simulation opens at most one NodeClaim per pod)
+  const size_t PA = sims ? sims->pods.size() : e.P;
+  const size_t CA = sims ? sims->pods.size() : d.max_claims;
+  const size_t NS = sims ? sims->evaluated.size() : 0;
   d.OW = std::max<uint32_t>(4, (e.W + 1) & ~1u);
   c->alloc(d.rows, VT * d.OW);
   c->alloc(d.cheapest, VT);
   c->alloc(d.nfo, VT);
   c->alloc(d.fk_ok, VT);
-  c->alloc(d.queue, e.P);
-  c->alloc(d.last_len, e.P);
-  c->alloc(d.last_epoch, e.P);
-  c->alloc(d.cur_var, e.P);
-  c->alloc(d.c_rec, MC);
-  c->alloc(d.c_opts, MC * d.OW);
-  c->alloc(d.c_fk, MC * std::max<uint32_t>(e.F, 1));
-  c->alloc(d.t_rem, (size_t)e.T * std::max<uint32_t>(e.R, 1));
-  c->alloc(d.log, e.P);
-  c->alloc(d.c_sorted, MC);
+  c->alloc(d.queue, PA);
+  c->alloc(d.last_len, PA);
+  c->alloc(d.last_epoch, PA);
+  c->alloc(d.cur_var, PA);
+  c->alloc(d.c_rec, CA);
+  c->alloc(d.c_opts, CA * d.OW);
+  c->alloc(d.c_fk, CA * F1);
+  c->alloc(d.t_rem, (sims ? NS : 1) * e.T * R1);
+  c->alloc(d.log, PA);
+  c->alloc(d.c_sorted, sims ? 1 : CA);
   c->alloc(d.ctrl, 1);
-  c->alloc(d.c_its, MC * 60);
-  c->alloc(d.c_nits, MC);
+  c->alloc(d.c_its, (sims ? NS : CA) * 60);
+  c->alloc(d.c_nits, sims ? NS : CA);
+  if (sims) {
+    d.n_sims = (uint32_t)NS;
+    d.ov_cap = std::max<uint32_t>(sims->ov_cap, 1);
+    d.nb_words = (e.NN + 31) / 32;
+    c->upload(d.sim_pod_off, sims->pod_off);
+    c->upload(d.sim_pods, sims->pods);
+    c->upload(d.sim_cand_off, sims->cand_off);
+    c->upload(d.sim_cands, sims->cands);
+    c->alloc(d.ov_req, (size_t)sims->blocks * d.ov_cap * gsd::RMAX);
+    c->alloc(d.ov_fk, (size_t)sims->blocks * d.ov_cap * F1);
+    c->alloc(d.sim_ctrl, NS);
+    c->alloc(d.sim_next, 1);
+  }
   c->commit();
 }
 
@@ -198,31 +122,34 @@ uint32_t trunc_lds_bytes(uint32_t N) {
 
 void launch_feas(gs_ctx* c, uint32_t apply_limits) { HIPCHK(gsk_feas(&c->dp, apply_limits, c->stream)); }
 
-}  // namespace
-
-extern "C" {
-
-const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
-
-uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
-  const uint32_t s[16] = {sizeof(gs_range),        sizeof(gs_requirement), sizeof(gs_quantity),
-                          sizeof(gs_label),        sizeof(gs_taint),       sizeof(gs_toleration),
-                          sizeof(gs_term),         sizeof(gs_offering),    sizeof(gs_instance_type),
-                          sizeof(gs_nodepool),     sizeof(gs_pod),         sizeof(gs_node),
-                          sizeof(gs_problem),      sizeof(gs_result),      sizeof(gs_feas_result),
-                          sizeof(gs_config)};
-  for (uint32_t i = 0; i < n && i < 16; i++) out[i] = s[i];
-  return 16;
-}
-
 // device capacity of the encoded problem (the FFD kernel keeps these in LDS)
-static gsh::Err capacity_check(const gsh::Encoded& e) {
+gsh::Err capacity_check(const gsh::Encoded& e) {
   if (e.N > 8192) return gsh::Err{GS_E_CAPACITY, "more than 8192 instance types"};
   if (e.thr_val.size() + 4 > gsd::THR_LDS_MAX)
     return gsh::Err{GS_E_CAPACITY, "more than 2044 distinct allocatable values over the resources"};
   if ((size_t)e.Z * e.C * e.W > gsd::SLOT_LDS_MAX)
     return gsh::Err{GS_E_CAPACITY, "zones x capacity types x instance-type words exceeds 1024"};
   return gsh::Err{GS_OK, ""};
+}
+
+}  // namespace gsc
+
+using namespace gsc;
+
+extern "C" {
+
+const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
+
+uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
+  const uint32_t s[19] = {sizeof(gs_range),        sizeof(gs_requirement),         sizeof(gs_quantity),
+                          sizeof(gs_label),        sizeof(gs_taint),               sizeof(gs_toleration),
+                          sizeof(gs_term),         sizeof(gs_offering),            sizeof(gs_instance_type),
+                          sizeof(gs_nodepool),     sizeof(gs_pod),                 sizeof(gs_node),
+                          sizeof(gs_problem),      sizeof(gs_result),              sizeof(gs_feas_result),
+                          sizeof(gs_config),       sizeof(gs_consolidation),       sizeof(gs_command),
+                          sizeof(gs_consolidation_result)};
+  for (uint32_t i = 0; i < n && i < 19; i++) out[i] = s[i];
+  return 19;
 }
 
 gs_status gs_validate(const gs_problem* p, char* err, size_t len) {
@@ -264,7 +191,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(gsk_init_ffd(gsk_ffd_lds_bytes(kMaxClaimsLds, gsd::THR_LDS_MAX - 4)));
+    HIPCHK(gsk_init_ffd(kLdsBytes));
     HIPCHK(gsk_init_trunc(65536));
   } catch (const HipError& e) {
     delete c;
@@ -287,6 +214,7 @@ void gs_destroy(gs_ctx* c) {
 gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   if (!c || !p) return GS_E_INVALID;
   c->prepared = c->ran = false;
+  c->cons_ready = false;
   auto t0 = Clock::now();
   gsh::Err er = gsh::encode(p, c->enc);
   c->t_encode = ms_since(t0);
@@ -297,7 +225,7 @@ gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   try {
     HIPCHK(hipSetDevice(c->device));
     auto t1 = Clock::now();
-    upload_problem(c);
+    upload_problem(c, nullptr);
     c->t_upload = ms_since(t1);
   } catch (const HipError& e) {
     return fail(c, GS_E_HIP, e.msg);
@@ -314,7 +242,7 @@ gs_status gs_run(gs_ctx* c) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_feas(c, 0);
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    HIPCHK(gsk_ffd(&d, c->stream));
+    HIPCHK(gsk_ffd(&d, 1, c->stream));
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));

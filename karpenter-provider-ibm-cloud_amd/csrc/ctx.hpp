@@ -1,0 +1,145 @@
+// ctx.hpp — gs_ctx (one device context of libgpusched.so) and the host
+// helpers shared by the Solve (capi.cpp) and consolidation (consolidate.cpp)
+// entry points.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpusched.h"
+#include "encode.hpp"
+#include "layout.hpp"
+
+extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
+extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
+extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap);
+extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
+extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);
+extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
+
+namespace gsc {
+
+constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: ord/sc/scratch u16, tmpl u8, 4x u16 slack, thresholds
+constexpr uint32_t kLdsBytes = 160 * 1024; // gfx950 LDS per workgroup
+
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+struct HipError {
+  std::string msg;
+};
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+// The simulations of one gs_consolidate call (device-side layout: layout.hpp
+// DevProblem consolidation fields).
+struct SimPlan {
+  std::vector<std::vector<uint32_t>> sets;  // candidate node indices (gs_problem order) per simulation
+  std::vector<uint32_t> evaluated;          // simulations of this shard, in order
+  std::vector<uint32_t> pod_off, pods;      // per evaluated simulation: pod ids in queue order
+  std::vector<uint32_t> cand_off, cands;    // per evaluated simulation: device node positions removed
+  uint32_t max_pods = 0, ov_cap = 0, blocks = 0;
+  uint32_t multi_max = 0;                   // MULTI: firstNConsolidationOption's max
+};
+
+}  // namespace gsc
+
+struct gs_ctx {
+  int device = 0;
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  std::vector<void*> allocs;
+  gsh::Encoded enc;
+  gsd::DevProblem dp{};
+  bool prepared = false, ran = false;
+  double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
+  const gs_problem* problem = nullptr;
+  // result storage
+  std::vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
+  std::vector<std::string> req_text;
+  std::vector<const char*> req_ptrs;
+  std::vector<int64_t> claim_requests;
+  std::vector<uint32_t> node_pod_offsets, node_pods, error_pods;
+  std::vector<uint64_t> f_rows;
+  std::vector<int32_t> f_cheapest;
+  std::vector<uint32_t> f_nfo;
+  gsd::Ctrl ctrl{};
+  // consolidation: the combined problem (pending ++ bound pods), the plan,
+  // the input copy (rerun) and result storage
+  std::vector<gs_pod> cons_pods;
+  gs_problem cons_problem{};
+  gs_consolidation cons_in{};
+  std::vector<uint32_t> cons_cands, cons_bound_node;
+  std::vector<gs_range> cons_sets;
+  uint32_t n_pending = 0;
+  gsc::SimPlan sims;
+  std::vector<gs_command> commands;
+  std::vector<uint32_t> cmd_options;
+  std::vector<double> cmd_prices;
+  std::vector<uint32_t> multi_opts;
+  bool cons_ready = false;
+  double t_sim = 0;
+
+  void free_all() {
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+  }
+  // Device buffers of one prepared problem come from ONE allocation (an arena
+  // of 256-B aligned sub-buffers): large pages, few TLB entries for the
+  // single-workgroup FFD kernel's gathers.  plan() records, commit() places.
+  struct Planned {
+    void** dst;
+    size_t off, bytes;
+    std::vector<char> host;
+  };
+  std::vector<Planned> plan;
+  size_t plan_bytes = 0;
+  template <class P>
+  void alloc(P*& dst, size_t n) {
+    const size_t b = std::max<size_t>(n, 1) * sizeof(P);
+    plan.push_back(Planned{(void**)&dst, plan_bytes, b, {}});
+    plan_bytes += (b + 255) & ~(size_t)255;
+  }
+  template <class P, class T>
+  void upload(P*& dst, const std::vector<T>& v) {
+    static_assert(sizeof(P) == sizeof(T), "upload type");
+    alloc(dst, v.size());
+    plan.back().host.assign((const char*)v.data(), (const char*)v.data() + v.size() * sizeof(T));
+  }
+  void commit();
+};
+
+namespace gsc {
+
+gs_status fail(gs_ctx* c, gs_status s, const std::string& m);
+gsh::Err capacity_check(const gsh::Encoded& e);
+uint32_t trunc_lds_bytes(uint32_t N);
+// encode output -> device arena; `sims` non-null: consolidation arenas
+void upload_problem(gs_ctx* c, const SimPlan* sims);
+
+}  // namespace gsc
+
+inline void gs_ctx::commit() {
+  using gsc::HipError;
+  void* base = nullptr;
+  HIPCHK(hipMalloc(&base, std::max<size_t>(plan_bytes, 256)));
+  allocs.push_back(base);
+  for (auto& q : plan) {
+    *q.dst = (char*)base + q.off;
+    if (!q.host.empty()) HIPCHK(hipMemcpyAsync(*q.dst, q.host.data(), q.host.size(), hipMemcpyHostToDevice, stream));
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  plan.clear();
+  plan_bytes = 0;
+}

@@ -474,6 +474,7 @@ struct Ctx {
       for (auto& o : v) prices.push_back(o.price);
     std::sort(prices.begin(), prices.end());
     prices.erase(std::unique(prices.begin(), prices.end(), [](double a, double b) { return a == b; }), prices.end());
+    e.prices = prices;
     auto prank = [&](double x) {
       return (uint32_t)(std::lower_bound(prices.begin(), prices.end(), x) - prices.begin());
     };

@@ -100,6 +100,7 @@ struct Encoded {
   std::vector<uint32_t> it_vid, it_prank, it_namerank, rank_to_it, thr_off;
   std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
   std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
+  std::vector<double> prices;  // distinct offering prices ascending: price rank -> price
   std::vector<gsd::TmplRec> tmpl;
   std::vector<uint64_t> t_opts;
   std::vector<gsd::FK> t_fk;

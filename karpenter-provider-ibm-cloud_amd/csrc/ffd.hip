@@ -51,7 +51,10 @@ struct Shared {
   unsigned long long red64[RMAX];
   Frame stk[48];
   // next-pod pipeline: wave 1 prefetches the next pop during the current pod
-  uint32_t nx_valid, nx_pod, nx_le, nx_ll, nx_cv, cb, use_pf;
+  uint32_t nx_valid, nx_pod, nx_gp, nx_le, nx_ll, nx_cv, cb, use_pf;
+  // solve in this block: simulation id, pod/claim arena offset, global pod id,
+  // overlay entry count / the entry being written (and whether it is new)
+  uint32_t sim, qoff, gpod, nov, ove, ov_new;
   alignas(16) uint32_t vrb[2][(sizeof(VarRec) / 4 + 3) & ~3u];
   alignas(16) int64_t reqb[2][RMAX];
 };
@@ -669,11 +672,22 @@ __device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa,
 
 }  // namespace
 
-template <uint32_t RR>
+// The kernel serves two launch shapes:
+//  * SIM = false: ONE workgroup runs the provisioning Solve over all P pods;
+//    existing nodes live in a global working copy (nodes / n_fk).
+//  * SIM = true: a persistent grid, one consolidation simulation per
+//    workgroup at a time (work counter d.sim_next).  A simulation re-Solves
+//    its pod subset (pending pods + the candidates' pods, queue order) against
+//    the existing nodes minus its candidates: the shared read-only base
+//    nodes0 / n_fk0 plus an overlay of the nodes this simulation touched (LDS
+//    bitmap + overlay ids, global req/FK copies per block).
+constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
+
+template <uint32_t RR, bool SIM>
 __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Shared S;
-  const uint32_t MC = d.max_claims;
+  const uint32_t MC = d.max_claims;  // LDS claim capacity (SIM: the largest simulation's pod count)
   uint16_t* s_ord = (uint16_t*)lds64;
   uint16_t* s_sc = s_ord + MC;
   uint16_t* s_scr = s_sc + MC;
@@ -685,427 +699,578 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
   __shared__ uint32_t s_thoff[RMAX + 1];
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t R = RR;  // resource dimensions (= d.R), compile-time
-  const uint32_t W = d.W, F = d.F, T = d.T, P = d.P;
+  const uint32_t W = d.W, F = d.F, T = d.T;
   const uint32_t OW = d.OW;  // claim option stride (words, 16-B multiple)
   const uint32_t nthr = d.thr_off[R];
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
+  uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
+  uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
   Blk blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
 
-  for (uint32_t i = tid; i < P; i += FB) {
-    d.queue[i] = d.queue0[i];
-    d.last_epoch[i] = 0;
-    d.last_len[i] = 0;
-    d.cur_var[i] = d.var_begin[i];
-  }
   for (uint32_t i = tid; i < nthr + 4; i += FB) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
   const uint32_t nslot = d.Z * d.C * W;
   const uint64_t* slot = s_slot;  // gs_prepare refuses Z*C*W > SLOT_LDS_MAX
   for (uint32_t i = tid; i < nslot; i += FB) s_slot[i] = d.slot_set[i];
-  for (uint32_t i = tid; i < T * R; i += FB) d.t_rem[i] = d.tmpl[i / R].limits[i % R];
-  for (uint32_t i = tid; i < d.NN; i += FB) d.nodes[i] = d.nodes0[i];
-  for (uint32_t i = tid; i < d.NN * F; i += FB) d.n_fk[i] = d.n_fk0[i];
+  if (!SIM) {
+    for (uint32_t i = tid; i < d.NN; i += FB) d.nodes[i] = d.nodes0[i];
+    for (uint32_t i = tid; i < d.NN * F; i += FB) d.n_fk[i] = d.n_fk0[i];
+  }
   if (tid <= R) s_thoff[tid] = d.thr_off[tid];
   for (uint32_t t = tid; t < T; t += FB) {
     s_tzm[t] = d.tmpl[t].zm;
     s_tcm[t] = d.tmpl[t].cm;
   }
-  if (tid == 0) {
-    S.M = 0;
-    S.qhead = 0;
-    S.qlen = P;
-    S.epoch = 1;
-    S.modkind = MOD_NONE;
-    S.nlog = 0;
-    S.pops = S.generic = S.fast = S.cand = S.cand_full = 0;
-    S.t_sort = S.t_scan = S.t_tmpl = 0;
-    for (int q = 0; q < 16; q++) S.dbg[q] = 0;
-    S.t0 = wall_clock64();
-    S.dbg[7] = __builtin_amdgcn_s_memtime();
-    S.status = 0;
-  }
-  __syncthreads();
-  const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
-
-  uint64_t tLoop = 0;
-  // wave-1 prefetch registers: stage 0 none, 1 pod id, 2 counters+variant, 3 records
   const uint32_t wave = tid >> 6, lane = tid & 63;
-  uint32_t pf_state = 0, pf_pod = 0, pf_le = 0, pf_ll = 0, pf_cv = 0, pf_vr = 0, pf_rq = 0;
-  auto pf_stage2 = [&]() {
-    if (wave == 1 && lane == 0 && pf_state == 1) {
-      pf_le = d.last_epoch[pf_pod];
-      pf_ll = d.last_len[pf_pod];
-      pf_cv = d.cur_var[pf_pod];
-      pf_state = 2;
+
+  for (uint32_t iter = 0;; iter++) {
+    // ------------------------------------------------ next simulation (SIM)
+    if (tid == 0) S.sim = SIM ? atomicAdd(d.sim_next, 1u) : iter;
+    __syncthreads();
+    const uint32_t sim = S.sim;
+    if (sim >= (SIM ? d.n_sims : 1u)) break;  // block-uniform: every wave leaves
+    const uint32_t qoff = SIM ? d.sim_pod_off[sim] : 0u;
+    const uint32_t P = SIM ? d.sim_pod_off[sim + 1] - qoff : d.P;
+    const uint32_t MCs = SIM ? P : MC;  // claim arena of this solve (one claim per pod at most)
+    uint32_t* const queue = d.queue + qoff;
+    uint32_t* const last_len = d.last_len + qoff;
+    uint32_t* const last_epoch = d.last_epoch + qoff;
+    uint32_t* const cur_var = d.cur_var + qoff;
+    LogRec* const logp = d.log + qoff;
+    int64_t* const t_rem = d.t_rem + (SIM ? (size_t)sim * T * R : 0);
+    auto gpod = [&](uint32_t local) -> uint32_t { return SIM ? d.sim_pods[qoff + local] : local; };
+
+    for (uint32_t i = tid; i < P; i += FB) {
+      queue[i] = SIM ? i : d.queue0[i];  // simulation pods are listed in queue order
+      last_epoch[i] = 0;
+      last_len[i] = 0;
+      cur_var[i] = d.var_begin[gpod(i)];
     }
-  };
-  auto pf_stage3 = [&]() {
-    if (wave == 1) {
-      const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
-      if (st == 2) {
-        const uint32_t cv = (uint32_t)__shfl((int)pf_cv, 0), pp = (uint32_t)__shfl((int)pf_pod, 0);
-        if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.vars + cv))[lane];
-        if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.pod_req + (size_t)pp * R))[lane - 32];
-        pf_state = 3;
+    for (uint32_t i = tid; i < T * R; i += FB) t_rem[i] = d.tmpl[i / R].limits[i % R];
+    uint32_t ncand = 0;
+    if (SIM) {
+      const uint32_t c0 = d.sim_cand_off[sim];
+      ncand = d.sim_cand_off[sim + 1] - c0;
+      for (uint32_t i = tid; i < d.nb_words; i += FB) s_nb[i] = 0;
+      __syncthreads();
+      for (uint32_t k = tid; k < ncand; k += FB) {
+        const uint32_t n = d.sim_cands[c0 + k];
+        s_ovid[k] = n | OV_EXCL;
+        atomicOr(&s_nb[n >> 5], 1u << (n & 31));
       }
     }
-  };
-  if (tid == 0) {
-    S.nx_valid = 0;
-    S.cb = 0;
-  }
-  for (;;) {
-    // publish last iteration's prefetch into the spare buffer
-    if (wave == 1) {
-      const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
-      if (st == 3) {
-        const uint32_t nb = S.cb ^ 1u;
-        if (lane < VR_DW) S.vrb[nb][lane] = pf_vr;
-        if (lane >= 32 && lane < 32 + 2 * RR) ((uint32_t*)S.reqb[nb])[lane - 32] = pf_rq;
-        if (lane == 0) {
-          S.nx_valid = 1;
-          S.nx_pod = pf_pod;
-          S.nx_le = pf_le;
-          S.nx_ll = pf_ll;
-          S.nx_cv = pf_cv;
-        }
-      } else if (lane == 0) {
-        S.nx_valid = 0;
-      }
-      pf_state = 0;
+    if (tid == 0) {
+      S.M = 0;
+      S.qhead = 0;
+      S.qlen = P;
+      S.epoch = 1;
+      S.modkind = MOD_NONE;
+      S.nlog = 0;
+      S.nov = ncand;
+      S.qoff = qoff;
+      S.pops = S.generic = S.fast = S.cand = S.cand_full = 0;
+      S.t_sort = S.t_scan = S.t_tmpl = 0;
+      for (int q = 0; q < 16; q++) S.dbg[q] = 0;
+      S.t0 = wall_clock64();
+      S.dbg[7] = __builtin_amdgcn_s_memtime();
+      S.status = 0;
+      S.nx_valid = 0;
+      S.cb = 0;
     }
     __syncthreads();
-    // ------------------------------------------------------------ Queue.Pop
-    if (tid == 0) tLoop = wall_clock64();
-    if (tid == 0) {
-      uint32_t stop = 0;
-      if (S.pops > max_pops) {
-        S.status = 2;
-        stop = 1;
-      } else if (S.qlen == 0) {
-        stop = 1;
-      } else {
-        uint32_t p, le, ll, cv;
-        const bool pf = S.nx_valid != 0;
-        if (pf) {
-          p = S.nx_pod;
-          le = S.nx_le;
-          ll = S.nx_ll;
-          cv = S.nx_cv;
-        } else {
-          p = d.queue[S.qhead];
-          le = d.last_epoch[p];
-          ll = d.last_len[p];
-          cv = d.cur_var[p];
+    const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
+
+    uint64_t tLoop = 0;
+    // wave-1 prefetch registers: stage 0 none, 1 pod id, 2 counters+variant, 3 records
+    uint32_t pf_state = 0, pf_pod = 0, pf_gp = 0, pf_le = 0, pf_ll = 0, pf_cv = 0, pf_vr = 0, pf_rq = 0;
+    auto pf_stage2 = [&]() {
+      if (wave == 1 && lane == 0 && pf_state == 1) {
+        pf_le = last_epoch[pf_pod];
+        pf_ll = last_len[pf_pod];
+        pf_cv = cur_var[pf_pod];
+        pf_gp = gpod(pf_pod);
+        pf_state = 2;
+      }
+    };
+    auto pf_stage3 = [&]() {
+      if (wave == 1) {
+        const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+        if (st == 2) {
+          const uint32_t cv = (uint32_t)__shfl((int)pf_cv, 0), gp = (uint32_t)__shfl((int)pf_gp, 0);
+          if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.vars + cv))[lane];
+          if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.pod_req + (size_t)gp * R))[lane - 32];
+          pf_state = 3;
         }
-        if (le == S.epoch && ll == S.qlen) {
+      }
+    };
+    for (;;) {
+      // publish last iteration's prefetch into the spare buffer
+      if (wave == 1) {
+        const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+        if (st == 3) {
+          const uint32_t nb = S.cb ^ 1u;
+          if (lane < VR_DW) S.vrb[nb][lane] = pf_vr;
+          if (lane >= 32 && lane < 32 + 2 * RR) ((uint32_t*)S.reqb[nb])[lane - 32] = pf_rq;
+          if (lane == 0) {
+            S.nx_valid = 1;
+            S.nx_pod = pf_pod;
+            S.nx_gp = pf_gp;
+            S.nx_le = pf_le;
+            S.nx_ll = pf_ll;
+            S.nx_cv = pf_cv;
+          }
+        } else if (lane == 0) {
+          S.nx_valid = 0;
+        }
+        pf_state = 0;
+      }
+      __syncthreads();
+      // ------------------------------------------------------------ Queue.Pop
+      if (tid == 0) tLoop = wall_clock64();
+      if (tid == 0) {
+        uint32_t stop = 0;
+        if (S.pops > max_pops) {
+          S.status = 2;
+          stop = 1;
+        } else if (S.qlen == 0) {
           stop = 1;
         } else {
-          S.qhead = S.qhead + 1 == P ? 0 : S.qhead + 1;
-          S.qlen--;
-          S.pops++;
-          S.pod = p;
-          S.var = cv;
-          S.use_pf = pf ? 1u : 0u;
-          if (pf) S.cb ^= 1u;
-        }
-      }
-      S.stop = stop;
-      S.found = 0;
-    }
-    __syncthreads();
-    if (S.stop) break;
-    const uint32_t p = S.pod, v = S.var;
-    if (!S.use_pf) {
-      // not prefetched: wave 0 stages the variant record and requests in LDS
-      if (wave == 0) {
-        if (lane < VR_DW) S.vrb[S.cb][lane] = ((const uint32_t*)(d.vars + v))[lane];
-        if (lane >= 32 && lane < 32 + 2 * RR)
-          ((uint32_t*)S.reqb[S.cb])[lane - 32] = ((const uint32_t*)(d.pod_req + (size_t)p * R))[lane - 32];
-      }
-      __syncthreads();
-    }
-    const VarRec& vr = *(const VarRec*)S.vrb[S.cb];
-    const int64_t* preq = S.reqb[S.cb];
-    // stage 1: the next pod id (its queue slot cannot change during this pod
-    // unless the queue is empty now, when this pod itself may come back)
-    if (wave == 1 && lane == 0 && S.qlen > 0) {
-      pf_pod = d.queue[S.qhead];
-      pf_state = 1;
-    }
-    const uint32_t M = S.M;
-    uint64_t tA = 0;
-    if (tid == 0) {
-      tA = wall_clock64();
-      S.dbg[4] += tA - tLoop;  // pop + variant load
-    }
-
-    int64_t rq[RR];
-#pragma unroll
-    for (uint32_t r = 0; r < RR; r++) rq[r] = r < R ? uniform_i64(preq[r]) : 0;
-
-    // --------------- existing nodes in order: first ExistingNode.CanAdd wins
-    if (d.NN) {
-      uint32_t fn = INF;
-      for (uint32_t base = 0; base < d.NN; base += FB) {
-        const uint32_t n = base + tid;
-        bool feas = false;
-        if (n < d.NN) {
-          const NodeRec& nr = d.nodes[n];
-          feas = nr.ok && (nr.taints & ~vr.tol) == 0;  // Taints.ToleratesPod
-#pragma unroll
-          for (uint32_t r = 0; r < RR; r++)
-            feas = feas && (r >= R || nr.req[r] + rq[r] <= nr.avail[r]);  // Fits(requests, available)
-          // strict Compatible on label keys: the node's label value must be Has()
-          for (uint32_t k = 0; k < d.K && feas; k++) {
-            const uint32_t off = vr.itmask_off[k];
-            if (off == NONE) continue;
-            const uint32_t vid = nr.vid[k];
-            feas = vid != NONE && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
-          }
-          if (feas && vr.zfull_off != NONE)
-            feas = nr.zvid != NONE && ((d.itmask[vr.zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
-          if (feas && vr.cfull_off != NONE)
-            feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
-          if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, d.n_fk + (size_t)n * F);
-        }
-        fn = blk.bmin(feas ? n : INF);
-        if (fn != INF) break;
-      }
-      if (fn != INF) {
-        // ExistingNode.Add: requests and requirements
-        if (tid < R) d.nodes[fn].req[tid] += preq[tid];
-        if (tid >= 64 && tid < 64 + vr.fk_count) {
-          const FKEntry& e = d.fk_entries[vr.fk_begin + (tid - 64)];
-          FK* nf = d.n_fk + (size_t)fn * F + e.slot;
-          const FK cur = *nf;
-          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
-                                         : e.st;
-        }
-        if (tid == 0) {
-          d.log[S.nlog++] = LogRec{p, v, fn | 0x80000000u, 0};
-          S.found = 1;
-        }
-        pf_stage2();
-        pf_stage3();
-        __syncthreads();
-        continue;
-      }
-    }
-
-    // ------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
-    if (M > 1) {
-      if (tid == 0) {
-        SeqSort ss{s_sc, s_ord};
-        uint32_t fast = 0, generic = 0;
-        bool inversion = false;
-        if (S.modkind == MOD_INC) {
-          const uint32_t q = S.modpos;
-          inversion = q + 1 < M && s_sc[q + 1] < s_sc[q];
-        } else if (S.modkind == MOD_APPEND) {
-          inversion = s_sc[M - 2] > s_sc[M - 1];
-        }
-        if (!inversion) {
-          // sorted input: pdqsort_func / insertionSort leave it untouched
-        } else if (M <= 12) {
-          ss.insertion_sort(0, (int)M);
-        } else {
-          int hint;
-          ss.choose_pivot_fast(0, (int)M, &hint);
-          if (hint == 1 && M >= 50) {
-            // partialInsertionSort fixes the single inversion;
-            // the landing position is found by the block below
-            fast = S.modkind;
-            S.fast++;
+          uint32_t p, gp, le, ll, cv;
+          const bool pf = S.nx_valid != 0;
+          if (pf) {
+            p = S.nx_pod;
+            gp = S.nx_gp;
+            le = S.nx_le;
+            ll = S.nx_ll;
+            cv = S.nx_cv;
           } else {
-            generic = 1;
-            S.generic++;
+            p = queue[S.qhead];
+            gp = gpod(p);
+            le = last_epoch[p];
+            ll = last_len[p];
+            cv = cur_var[p];
+          }
+          if (le == S.epoch && ll == S.qlen) {
+            stop = 1;
+          } else {
+            S.qhead = S.qhead + 1 == P ? 0 : S.qhead + 1;
+            S.qlen--;
+            S.pops++;
+            S.pod = p;
+            S.gpod = gp;
+            S.var = cv;
+            S.use_pf = pf ? 1u : 0u;
+            if (pf) S.cb ^= 1u;
           }
         }
-        S.fast_path = fast | (generic << 4);
-        S.modpos_sorted = S.modpos;
-        S.modkind = MOD_NONE;
+        S.stop = stop;
+        S.found = 0;
       }
       __syncthreads();
+      if (S.stop) break;
+      const uint32_t p = S.pod, gp = S.gpod, v = S.var;
+      if (!S.use_pf) {
+        // not prefetched: wave 0 stages the variant record and requests in LDS
+        if (wave == 0) {
+          if (lane < VR_DW) S.vrb[S.cb][lane] = ((const uint32_t*)(d.vars + v))[lane];
+          if (lane >= 32 && lane < 32 + 2 * RR)
+            ((uint32_t*)S.reqb[S.cb])[lane - 32] = ((const uint32_t*)(d.pod_req + (size_t)gp * R))[lane - 32];
+        }
+        __syncthreads();
+      }
+      const VarRec& vr = *(const VarRec*)S.vrb[S.cb];
+      const int64_t* preq = S.reqb[S.cb];
+      // stage 1: the next pod id (its queue slot cannot change during this pod
+      // unless the queue is empty now, when this pod itself may come back)
+      if (wave == 1 && lane == 0 && S.qlen > 0) {
+        pf_pod = queue[S.qhead];
+        pf_state = 1;
+      }
+      const uint32_t M = S.M;
+      uint64_t tA = 0;
       if (tid == 0) {
-        const uint64_t tq = wall_clock64();
-        S.dbg[3] += tq - tA;
+        tA = wall_clock64();
+        S.dbg[4] += tA - tLoop;  // pop + variant load
       }
-      const uint32_t fp = S.fast_path;
-      if (fp == MOD_INC) {
-        // X (at q, count x) moves right past the run of counts < x
-        const uint32_t q = S.modpos_sorted, x = s_sc[q];
-        uint32_t e = M;
-        for (uint32_t base = q + 1; base < M; base += FB) {
-          const uint32_t k = base + tid;
-          const uint32_t m = blk.bmin((k < M && s_sc[k] >= x) ? k : INF);
-          if (m != INF) {
-            e = m;
-            break;
-          }
-        }
-        blk.rotate_left((int)q, (int)e - 1);
-      } else if (fp == MOD_APPEND) {
-        // X (at M-1, count x) moves left past the counts > x
-        const uint16_t x = s_sc[M - 1];
-        int e = 0;
-        for (int top = (int)M - 2; top >= 0; top -= FB) {
-          const int k = top - (int)tid;
-          const int32_t m = blk.bmax((k >= 0 && s_sc[k] <= x) ? k : -1);
-          if (m >= 0) {
-            e = m + 1;
-            break;
-          }
-        }
-        blk.rotate_right(e, (int)M - 1);
-      } else if (fp >> 4) {
-        blk.pdqsort((int)M);
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const uint64_t tB = wall_clock64();
-      S.t_sort += tB - tA;
-      tA = tB;
-    }
 
-    pf_stage2();
-    // request codes for the LDS slack test (computed here: not live across the sort)
-    uint32_t rqq[4];
+      int64_t rq[RR];
 #pragma unroll
-    for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? qcode_floor(rq[r]) : 0;
-    // ---------------------- in-flight NodeClaims, first that CanAdd wins
-    // A lane that finds its NodeClaim feasible keeps everything NodeClaim.Add
-    // needs in registers (new option words for W <= WREG, totals, cursors);
-    // the first feasible position (block min) writes them back directly.
-    uint32_t f = INF;
-    for (uint32_t base = 0; base < M; base += FB) {
-      // kernel arguments re-read per chunk (scalar loads) instead of being
-      // held across the whole pod loop: keeps SGPR spills out of this path
-      KArg dpp = (KArg)__builtin_amdgcn_kernarg_segment_ptr();  // d is the only argument
-      asm volatile("" : "+s"(dpp));
-      const auto& dd = *dpp;
-      const uint32_t pos = base + tid;
-      bool feas = false, pre = false;
-      uint32_t j = 0, t = 0;
-      uint64_t G = 0, Gt = 0;
-      uint32_t mrow[RR];
-      int64_t tot[RR];
-      uint64_t nx[WREG];
+      for (uint32_t r = 0; r < RR; r++) rq[r] = r < R ? uniform_i64(preq[r]) : 0;
+
+      // --------------- existing nodes in order: first ExistingNode.CanAdd wins
+      if (d.NN) {
+        uint32_t fn = INF;
+        for (uint32_t base = 0; base < d.NN; base += FB) {
+          const uint32_t n = base + tid;
+          bool feas = false;
+          if (n < d.NN) {
+            const NodeRec& nr = SIM ? d.nodes0[n] : d.nodes[n];
+            const int64_t* nreq = nr.req;
+            const FK* nfk = (SIM ? d.n_fk0 : d.n_fk) + (size_t)n * F;
+            feas = nr.ok && (nr.taints & ~vr.tol) == 0;  // Taints.ToleratesPod
+            if (SIM && feas && ((s_nb[n >> 5] >> (n & 31)) & 1)) {
+              // touched by this simulation: removed candidate, or overlay copy
+              uint32_t e = 0;
+              while ((s_ovid[e] & ~OV_EXCL) != n) e++;
+              if (s_ovid[e] & OV_EXCL) {
+                feas = false;
+              } else {
+                const size_t oe = (size_t)blockIdx.x * d.ov_cap + e;
+                nreq = d.ov_req + oe * RMAX;
+                nfk = d.ov_fk + oe * F;
+              }
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < RR; r++)
+              feas = feas && (r >= R || nreq[r] + rq[r] <= nr.avail[r]);  // Fits(requests, available)
+            // strict Compatible on label keys: the node's label value must be Has()
+            for (uint32_t k = 0; k < d.K && feas; k++) {
+              const uint32_t off = vr.itmask_off[k];
+              if (off == NONE) continue;
+              const uint32_t vid = nr.vid[k];
+              feas = vid != NONE && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+            }
+            if (feas && vr.zfull_off != NONE)
+              feas = nr.zvid != NONE && ((d.itmask[vr.zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+            if (feas && vr.cfull_off != NONE)
+              feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+            if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
+          }
+          fn = blk.bmin(feas ? n : INF);
+          if (fn != INF) break;
+        }
+        if (fn != INF) {
+          // ExistingNode.Add: requests and requirements
+          int64_t* areq;
+          FK* afk;
+          if (SIM) {
+            // copy-on-write overlay entry for the node
+            if (tid == 0) {
+              uint32_t e = INF;
+              if ((s_nb[fn >> 5] >> (fn & 31)) & 1) {
+                e = 0;
+                while ((s_ovid[e] & ~OV_EXCL) != fn) e++;
+                S.ov_new = 0;
+              } else {
+                e = S.nov++;
+                s_ovid[e] = fn;
+                s_nb[fn >> 5] |= 1u << (fn & 31);
+                S.ov_new = 1;
+              }
+              S.ove = e;
+            }
+            __syncthreads();
+            const size_t oe = (size_t)blockIdx.x * d.ov_cap + S.ove;
+            areq = d.ov_req + oe * RMAX;
+            afk = d.ov_fk + oe * F;
+            if (S.ov_new) {
+              if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
+              if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
+            }
+            __syncthreads();
+          } else {
+            areq = d.nodes[fn].req;
+            afk = d.n_fk + (size_t)fn * F;
+          }
+          if (tid < R) areq[tid] += preq[tid];
+          if (tid >= 64 && tid < 64 + vr.fk_count) {
+            const FKEntry& e = d.fk_entries[vr.fk_begin + (tid - 64)];
+            FK* nf = afk + e.slot;
+            const FK cur = *nf;
+            *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                                           : e.st;
+          }
+          if (tid == 0) {
+            logp[S.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
+            S.found = 1;
+          }
+          pf_stage2();
+          pf_stage3();
+          __syncthreads();
+          continue;
+        }
+      }
+
+      // ------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
+      if (M > 1) {
+        if (tid == 0) {
+          SeqSort ss{s_sc, s_ord};
+          uint32_t fast = 0, generic = 0;
+          bool inversion = false;
+          if (S.modkind == MOD_INC) {
+            const uint32_t q = S.modpos;
+            inversion = q + 1 < M && s_sc[q + 1] < s_sc[q];
+          } else if (S.modkind == MOD_APPEND) {
+            inversion = s_sc[M - 2] > s_sc[M - 1];
+          }
+          if (!inversion) {
+            // sorted input: pdqsort_func / insertionSort leave it untouched
+          } else if (M <= 12) {
+            ss.insertion_sort(0, (int)M);
+          } else {
+            int hint;
+            ss.choose_pivot_fast(0, (int)M, &hint);
+            if (hint == 1 && M >= 50) {
+              // partialInsertionSort fixes the single inversion;
+              // the landing position is found by the block below
+              fast = S.modkind;
+              S.fast++;
+            } else {
+              generic = 1;
+              S.generic++;
+            }
+          }
+          S.fast_path = fast | (generic << 4);
+          S.modpos_sorted = S.modpos;
+          S.modkind = MOD_NONE;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          const uint64_t tq = wall_clock64();
+          S.dbg[3] += tq - tA;
+        }
+        const uint32_t fp = S.fast_path;
+        if (fp == MOD_INC) {
+          // X (at q, count x) moves right past the run of counts < x
+          const uint32_t q = S.modpos_sorted, x = s_sc[q];
+          uint32_t e = M;
+          for (uint32_t base = q + 1; base < M; base += FB) {
+            const uint32_t k = base + tid;
+            const uint32_t m = blk.bmin((k < M && s_sc[k] >= x) ? k : INF);
+            if (m != INF) {
+              e = m;
+              break;
+            }
+          }
+          blk.rotate_left((int)q, (int)e - 1);
+        } else if (fp == MOD_APPEND) {
+          // X (at M-1, count x) moves left past the counts > x
+          const uint16_t x = s_sc[M - 1];
+          int e = 0;
+          for (int top = (int)M - 2; top >= 0; top -= FB) {
+            const int k = top - (int)tid;
+            const int32_t m = blk.bmax((k >= 0 && s_sc[k] <= x) ? k : -1);
+            if (m >= 0) {
+              e = m + 1;
+              break;
+            }
+          }
+          blk.rotate_right(e, (int)M - 1);
+        } else if (fp >> 4) {
+          blk.pdqsort((int)M);
+        }
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const uint64_t tB = wall_clock64();
+        S.t_sort += tB - tA;
+        tA = tB;
+      }
+
+      pf_stage2();
+      // request codes for the LDS slack test (computed here: not live across the sort)
+      uint32_t rqq[4];
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? qcode_floor(rq[r]) : 0;
+      // ---------------------- in-flight NodeClaims, first that CanAdd wins
+      // A lane that finds its NodeClaim feasible keeps everything NodeClaim.Add
+      // needs in registers (new option words for W <= WREG, totals, cursors);
+      // the first feasible position (block min) writes them back directly.
+      uint32_t f = INF;
+      for (uint32_t base = 0; base < M; base += FB) {
+        // kernel arguments re-read per chunk (scalar loads) instead of being
+        // held across the whole pod loop: keeps SGPR spills out of this path
+        KArg dpp = (KArg)__builtin_amdgcn_kernarg_segment_ptr();  // d is the only argument
+        asm volatile("" : "+s"(dpp));
+        const auto& dd = *dpp;
+        const uint32_t cb = SIM ? S.qoff : 0u;  // this solve's claim arena
+        const uint32_t pos = base + tid;
+        bool feas = false, pre = false;
+        uint32_t j = 0, t = 0;
+        uint64_t G = 0, Gt = 0;
+        uint32_t mrow[RR];
+        int64_t tot[RR];
+        uint64_t nx[WREG];
 #ifdef GS_FFD_DIAG
-      const uint64_t c0 = __builtin_amdgcn_s_memtime();
-      uint64_t c1 = 0, c2 = 0, c3 = 0;
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+        uint64_t c1 = 0, c2 = 0, c3 = 0;
 #endif
-      if (pos < M) {
-        j = s_ord[pos];
-        t = s_tmpl[j];
-        // LDS-only necessary test: template tolerated and, per resource,
-        // qcode_floor(request) <= qcode_ceil(slack)
-        bool lp = (vr.tolt >> t) & 1;
-        const uint64_t sq = s_slk[j];
+        if (pos < M) {
+          j = s_ord[pos];
+          t = s_tmpl[j];
+          // LDS-only necessary test: template tolerated and, per resource,
+          // qcode_floor(request) <= qcode_ceil(slack)
+          bool lp = (vr.tolt >> t) & 1;
+          const uint64_t sq = s_slk[j];
 #pragma unroll
-        for (uint32_t r = 0; r < 4; r++) lp = lp && (uint64_t)rqq[r] <= ((sq >> (16 * r)) & 0xFFFFu);
-        if (lp) {
+          for (uint32_t r = 0; r < 4; r++) lp = lp && (uint64_t)rqq[r] <= ((sq >> (16 * r)) & 0xFFFFu);
+          if (lp) {
 #ifdef GS_ASM_MARK
-          asm volatile("; MARK_FULL_BEGIN");
+            asm volatile("; MARK_FULL_BEGIN");
 #endif
-          // one 64-B header read (four 16-B loads): totals, cursors, masks
-          const ClaimRec* cr = dd.c_rec + j;
-          uint32_t cur[RR];
-          uint64_t zm, cm;
-          {
-            const uint4* q = (const uint4*)cr;
-            const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
-            const int64_t lo[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
-                                   (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
-            const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
-            zm = ((uint64_t)h2.w << 32) | h2.z;
-            cm = ((uint64_t)h3.y << 32) | h3.x;
-#pragma unroll
-            for (uint32_t r = 0; r < RR; r++) {
-              tot[r] = r < 4 ? lo[r] : cr->tot_hi[r - 4];
-              cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
-            }
-          }
-          // option words (stride OW, 16-B aligned) and the (variant, template)
-          // row: they depend only on j and t, issued with the header
-          const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
-          const uint64_t* opts = dd.c_opts + (size_t)j * OW;
-          if (W <= WREG) {
-            // unconditional 16-B loads (stride OW >= 4 words): no per-word branches
-            const uint4* oq = (const uint4*)opts;
-            const uint4* rq4 = (const uint4*)row;
-            const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
-            const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
-                                   (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
-                                   (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
-                                   (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
-#pragma unroll
-            for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
-          }
-          // the exact fit test is implied by the threshold rows below; the
-          // LDS slack test above already rejected the clear misfits
-          pre = true;
-#ifdef GS_FFD_DIAG
-          c1 = __builtin_amdgcn_s_memtime();
-#endif
-          if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)j * F);
-          if (pre) {
-            G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
-            Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, dd.Z, dd.C);
-            uint32_t mm[RR];
-#pragma unroll
-            for (uint32_t r = 0; r < RR; r++) {
-              const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
-              mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
-            }
-#pragma unroll
-            for (uint32_t r = 0; r < RR; r++) {
-              const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
-              if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
-              mrow[r] = o + r + mm[r];
-            }
-#ifdef GS_FFD_DIAG
-            c2 = __builtin_amdgcn_s_memtime();
-#endif
-            uint64_t acc = 0;
-            if (W <= WREG) {
-              // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
-              // whose cursor moves narrows the options further
+            // one 64-B header read (four 16-B loads): totals, cursors, masks
+            const ClaimRec* cr = dd.c_rec + cb + j;
+            uint32_t cur[RR];
+            uint64_t zm, cm;
+            {
+              const uint4* q = (const uint4*)cr;
+              const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+              const int64_t lo[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                     (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+              const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+              zm = ((uint64_t)h2.w << 32) | h2.z;
+              cm = ((uint64_t)h3.y << 32) | h3.x;
 #pragma unroll
               for (uint32_t r = 0; r < RR; r++) {
-                if (mm[r] != cur[r]) {
-                  const uint4* tq = (const uint4*)(dd.thr_set + (size_t)mrow[r] * OW);
-                  const uint4 t0 = tq[0], t1 = tq[1];
-                  nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
-                  nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
-                  nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
-                  nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
+                tot[r] = r < 4 ? lo[r] : cr->tot_hi[r - 4];
+                cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+              }
+            }
+            // option words (stride OW, 16-B aligned) and the (variant, template)
+            // row: they depend only on j and t, issued with the header
+            const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
+            const uint64_t* opts = dd.c_opts + (size_t)(cb + j) * OW;
+            if (W <= WREG) {
+              // unconditional 16-B loads (stride OW >= 4 words): no per-word branches
+              const uint4* oq = (const uint4*)opts;
+              const uint4* rq4 = (const uint4*)row;
+              const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+              const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                     (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                     (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                     (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
+            }
+            // the exact fit test is implied by the threshold rows below; the
+            // LDS slack test above already rejected the clear misfits
+            pre = true;
+#ifdef GS_FFD_DIAG
+            c1 = __builtin_amdgcn_s_memtime();
+#endif
+            if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)(cb + j) * F);
+            if (pre) {
+              G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
+              Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, dd.Z, dd.C);
+              uint32_t mm[RR];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+                mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
+              }
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+                if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
+                mrow[r] = o + r + mm[r];
+              }
+#ifdef GS_FFD_DIAG
+              c2 = __builtin_amdgcn_s_memtime();
+#endif
+              uint64_t acc = 0;
+              if (W <= WREG) {
+                // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
+                // whose cursor moves narrows the options further
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) {
+                  if (mm[r] != cur[r]) {
+                    const uint4* tq = (const uint4*)(dd.thr_set + (size_t)mrow[r] * OW);
+                    const uint4 t0 = tq[0], t1 = tq[1];
+                    nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                    nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                    nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                    nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
+                  }
+                }
+                if (G != Gt) {
+                  // keep the types with an available offering on the narrowed
+                  // (zone, capacity-type) grid: OR of the per-pair type sets
+                  uint64_t off[WREG] = {};
+                  uint64_t gm = G;
+                  while (gm) {
+                    const uint32_t g = __ffsll((long long)gm) - 1;
+                    gm &= gm - 1;
+#pragma unroll
+                    for (uint32_t w = 0; w < WREG; w++)
+                      if (w < W) off[w] |= slot[g * W + w];
+                  }
+#pragma unroll
+                  for (uint32_t w = 0; w < WREG; w++) nx[w] &= off[w];
+                }
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++) acc |= nx[w];
+              } else {
+                for (uint32_t w = 0; w < W && !acc; w++) {
+                  uint64_t x = opts[w] & row[w];
+#pragma unroll
+                  for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
+                  if (x && G != Gt) {
+                    uint64_t off = 0, gm = G;
+                    while (gm) {
+                      const uint32_t g = __ffsll((long long)gm) - 1;
+                      gm &= gm - 1;
+                      off |= slot[(size_t)g * W + w];
+                    }
+                    x &= off;
+                  }
+                  acc |= x;
                 }
               }
-              if (G != Gt) {
-                // keep the types with an available offering on the narrowed
-                // (zone, capacity-type) grid: OR of the per-pair type sets
-                uint64_t off[WREG] = {};
-                uint64_t gm = G;
-                while (gm) {
-                  const uint32_t g = __ffsll((long long)gm) - 1;
-                  gm &= gm - 1;
+              feas = acc != 0;
+#ifdef GS_FFD_DIAG
+              c3 = __builtin_amdgcn_s_memtime();
+#endif
+            }
+          }
+        }
+#ifdef GS_FFD_DIAG
+        {
+          // per wave: cycles to the record test, the cursor probe, the option words
+          const uint64_t b1 = __ballot(c1 != 0), b3 = __ballot(c3 != 0);
+          if (b1 && (tid & 63) == (uint32_t)(__ffsll((long long)b1) - 1)) {
+            atomicAdd((unsigned long long*)&S.dbg[8], (unsigned long long)(c1 - c0));
+            atomicAdd((unsigned long long*)&S.dbg[11], 1ull);
+          }
+          if (b3 && (tid & 63) == (uint32_t)(__ffsll((long long)b3) - 1)) {
+            atomicAdd((unsigned long long*)&S.dbg[9], (unsigned long long)(c2 - c1));
+            atomicAdd((unsigned long long*)&S.dbg[10], (unsigned long long)(c3 - c2));
+            atomicAdd((unsigned long long*)&S.dbg[12], 1ull);
+          }
+          if (tid == 0) atomicAdd((unsigned long long*)&S.dbg[13], (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
+        }
+#endif
+#ifdef GS_ASM_MARK
+        asm volatile("; MARK_FULL_END");
+#endif
+        const uint64_t pm = __ballot(pre);
+        if ((tid & 63) == 0 && pm) atomicAdd((unsigned long long*)&S.cand_full, (unsigned long long)__popcll(pm));
+        uint64_t tq = 0;
+        if (tid == 0) tq = wall_clock64();
+        f = blk.bmin(feas ? pos : INF);
+        if (tid == 0) {
+          const uint64_t tr_ = wall_clock64();
+          S.dbg[0] += tq - tA;
+          S.dbg[1] += tr_ - tq;
+          S.dbg[2]++;
+          tA = tr_;
+          S.cand += (M - base) < FB ? (M - base) : FB;
+        }
+        if (f != INF) {
+          if (pos == f) {
+            // NodeClaim.Add by the winning lane: options, requests, requirements
+            ClaimRec* cr = dd.c_rec + cb + j;
+            uint64_t* opts = dd.c_opts + (size_t)(cb + j) * OW;
+            if (W <= WREG) {
 #pragma unroll
-                  for (uint32_t w = 0; w < WREG; w++)
-                    if (w < W) off[w] |= slot[g * W + w];
-                }
-#pragma unroll
-                for (uint32_t w = 0; w < WREG; w++) nx[w] &= off[w];
-              }
-#pragma unroll
-              for (uint32_t w = 0; w < WREG; w++) acc |= nx[w];
+              for (uint32_t w = 0; w < WREG; w++)
+                if (w < W) opts[w] = nx[w];  // already narrowed to the grid
             } else {
-              for (uint32_t w = 0; w < W && !acc; w++) {
+              const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
+              for (uint32_t w = 0; w < W; w++) {
                 uint64_t x = opts[w] & row[w];
 #pragma unroll
                 for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
-                if (x && G != Gt) {
+                if (G != Gt) {
                   uint64_t off = 0, gm = G;
                   while (gm) {
                     const uint32_t g = __ffsll((long long)gm) - 1;
@@ -1114,313 +1279,273 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
                   }
                   x &= off;
                 }
-                acc |= x;
+                opts[w] = x;
               }
             }
-            feas = acc != 0;
-#ifdef GS_FFD_DIAG
-            c3 = __builtin_amdgcn_s_memtime();
-#endif
+            int64_t nt[RR], ma[RR];
+#pragma unroll
+            for (uint32_t r = 0; r < RR; r++) {
+              nt[r] = tot[r] + rq[r];
+              ma[r] = cr->maxa[r];
+              cr->tot(r) = nt[r];
+              cr->thr(r) = (uint16_t)(mrow[r] - s_thoff[r] - r);
+            }
+            s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
+            cr->zm &= vr.zm;
+            cr->cm &= vr.cm;
+            cr->count++;
+            FK* cf = dd.c_fk + (size_t)(cb + j) * F;
+            for (uint32_t k = 0; k < vr.fk_count; k++) {
+              const FKEntry& e = dd.fk_entries[vr.fk_begin + k];
+              const FK cur = cf[e.slot];
+              cf[e.slot] = (cur.flags & FK_PRESENT)
+                               ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * 64, dd.fk_isint[e.slot])
+                               : e.st;
+            }
+            if (s_sc[f] == 0xFFFFu) S.status = 3;
+            s_sc[f]++;
+            S.modkind = MOD_INC;
+            S.modpos = f;
+            dd.log[cb + S.nlog++] = LogRec{gp, v, j, 0};
+            S.found = 1;
           }
+          break;
         }
       }
-#ifdef GS_FFD_DIAG
-      {
-        // per wave: cycles to the record test, the cursor probe, the option words
-        const uint64_t b1 = __ballot(c1 != 0), b3 = __ballot(c3 != 0);
-        if (b1 && (tid & 63) == (uint32_t)(__ffsll((long long)b1) - 1)) {
-          atomicAdd((unsigned long long*)&S.dbg[8], (unsigned long long)(c1 - c0));
-          atomicAdd((unsigned long long*)&S.dbg[11], 1ull);
-        }
-        if (b3 && (tid & 63) == (uint32_t)(__ffsll((long long)b3) - 1)) {
-          atomicAdd((unsigned long long*)&S.dbg[9], (unsigned long long)(c2 - c1));
-          atomicAdd((unsigned long long*)&S.dbg[10], (unsigned long long)(c3 - c2));
-          atomicAdd((unsigned long long*)&S.dbg[12], 1ull);
-        }
-        if (tid == 0) atomicAdd((unsigned long long*)&S.dbg[13], (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
-      }
-#endif
-#ifdef GS_ASM_MARK
-      asm volatile("; MARK_FULL_END");
-#endif
-      const uint64_t pm = __ballot(pre);
-      if ((tid & 63) == 0 && pm) atomicAdd((unsigned long long*)&S.cand_full, (unsigned long long)__popcll(pm));
-      uint64_t tq = 0;
-      if (tid == 0) tq = wall_clock64();
-      f = blk.bmin(feas ? pos : INF);
+      pf_stage3();
+      __syncthreads();
       if (tid == 0) {
-        const uint64_t tr_ = wall_clock64();
-        S.dbg[0] += tq - tA;
-        S.dbg[1] += tr_ - tq;
-        S.dbg[2]++;
-        tA = tr_;
-        S.cand += (M - base) < FB ? (M - base) : FB;
+        const uint64_t tB = wall_clock64();
+        S.t_scan += tB - tA;
+        tA = tB;
       }
-      if (f != INF) {
-        if (pos == f) {
-          // NodeClaim.Add by the winning lane: options, requests, requirements
-          ClaimRec* cr = dd.c_rec + j;
-          uint64_t* opts = dd.c_opts + (size_t)j * OW;
-          if (W <= WREG) {
-#pragma unroll
-            for (uint32_t w = 0; w < WREG; w++)
-              if (w < W) opts[w] = nx[w];  // already narrowed to the grid
-          } else {
-            const uint64_t* row = dd.rows + ((size_t)v * T + t) * OW;
-            for (uint32_t w = 0; w < W; w++) {
-              uint64_t x = opts[w] & row[w];
-#pragma unroll
-              for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
-              if (G != Gt) {
-                uint64_t off = 0, gm = G;
-                while (gm) {
-                  const uint32_t g = __ffsll((long long)gm) - 1;
-                  gm &= gm - 1;
-                  off |= slot[(size_t)g * W + w];
-                }
-                x &= off;
-              }
-              opts[w] = x;
-            }
+      if (S.found) {
+        if (S.status) break;
+        continue;
+      }
+
+      // ------------------------------- new NodeClaim from templates, in order
+      const uint32_t cbase = SIM ? qoff : 0u;
+      for (uint32_t t = 0; t < T; t++) {
+        const TmplRec& tr = d.tmpl[t];
+        const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+        bool any = false;
+        if (d.fk_ok[(size_t)v * T + t])
+          for (uint32_t w = 0; w < W; w++)
+            if (row[w]) any = true;
+        if (!any) continue;
+        if (tr.has_limits) {
+          // <U> filterByRemainingResources on the template's options
+          uint32_t hit = INF;
+          for (uint32_t i = tid; i < d.N; i += FB) {
+            if (!((row[i >> 6] >> (i & 63)) & 1)) continue;
+            bool ok = true;
+            for (uint32_t r = 0; r < R; r++)
+              if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= t_rem[(size_t)t * R + r];
+            if (ok) hit = 0;
           }
+          if (blk.bmin(hit) == INF) continue;
+        }
+        if (M >= MCs) {
+          if (tid == 0) S.status = 1;
+          __syncthreads();
+          break;
+        }
+        const uint32_t j = M;
+        ClaimRec* cr = d.c_rec + cbase + j;
+        if (tid < R) {
+          const int64_t tot = tr.daemon[tid] + preq[tid];
+          const uint32_t o = s_thoff[tid], n = s_thoff[tid + 1] - o;
+          S.c0[tid] = thr_search(thr + o, n, 0, tot);
+        }
+        __syncthreads();
+        for (uint32_t w = tid; w < W; w += FB) {
+          uint64_t x = row[w];
+          // establish opts ⊆ thr_set[cursor] for the candidate scan
+          for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * OW + w];
+          if (tr.has_limits) {
+            uint64_t y = 0, m = x;
+            while (m) {
+              const uint32_t b = __ffsll((long long)m) - 1;
+              m &= m - 1;
+              const uint32_t i = w * 64 + b;
+              bool ok = true;
+              for (uint32_t r = 0; r < R; r++)
+                if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= t_rem[(size_t)t * R + r];
+              if (ok) y |= 1ull << b;
+            }
+            x = y;
+          }
+          d.c_opts[(size_t)(cbase + j) * OW + w] = x;
+        }
+        if (tid < RR) {
+          int64_t tot = 0;
+          uint32_t c0 = 0;
+          if (tid < R) {
+            tot = tr.daemon[tid] + preq[tid];
+            c0 = S.c0[tid];
+          }
+          cr->tot(tid) = tot;
+          cr->thr(tid) = (uint16_t)c0;
+          S.red64[tid] = 0;
+        }
+        if (tid == 0) {
+          cr->tmpl = t;
+          cr->count = 1;
+          cr->zm = tr.zm & vr.zm;
+          cr->cm = tr.cm & vr.cm;
+          FK* cf = d.c_fk + (size_t)(cbase + j) * F;
+          for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
+          for (uint32_t k = 0; k < vr.fk_count; k++) {
+            const FKEntry& e = d.fk_entries[vr.fk_begin + k];
+            const FK cur = cf[e.slot];
+            cf[e.slot] = (cur.flags & FK_PRESENT)
+                             ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                             : e.st;
+          }
+          s_ord[M] = (uint16_t)M;
+          s_sc[M] = 1;
+          s_tmpl[M] = (uint8_t)t;
+          S.M = M + 1;
+          S.modkind = MOD_APPEND;
+          logp[S.nlog++] = LogRec{gp, v, j, 0};
+          S.found = 1;
+        }
+        __syncthreads();
+        // max allocatable over the new claim's options (the slack bound)
+        for (uint32_t i = tid; i < d.N; i += FB) {
+          if (!((d.c_opts[(size_t)(cbase + j) * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
+          for (uint32_t r = 0; r < R; r++) atomicMax(&S.red64[r], (unsigned long long)d.it_alloc[(size_t)r * d.N + i]);
+        }
+        __syncthreads();
+        if (tid < RR) cr->maxa[tid] = tid < R ? (int64_t)S.red64[tid] : 0;
+        if (tid == 0) {
+          // LDS slack from the max allocatable over the new claim's options
           int64_t nt[RR], ma[RR];
 #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
-            nt[r] = tot[r] + rq[r];
-            ma[r] = cr->maxa[r];
-            cr->tot(r) = nt[r];
-            cr->thr(r) = (uint16_t)(mrow[r] - s_thoff[r] - r);
+            nt[r] = r < R ? tr.daemon[r] + preq[r] : 0;
+            ma[r] = r < R ? (int64_t)S.red64[r] : 0;
           }
-          s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
-          cr->zm &= vr.zm;
-          cr->cm &= vr.cm;
-          cr->count++;
-          FK* cf = dd.c_fk + (size_t)j * F;
-          for (uint32_t k = 0; k < vr.fk_count; k++) {
-            const FKEntry& e = dd.fk_entries[vr.fk_begin + k];
-            const FK cur = cf[e.slot];
-            cf[e.slot] = (cur.flags & FK_PRESENT)
-                             ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * 64, dd.fk_isint[e.slot])
-                             : e.st;
-          }
-          if (s_sc[f] == 0xFFFFu) S.status = 3;
-          s_sc[f]++;
-          S.modkind = MOD_INC;
-          S.modpos = f;
-          dd.log[S.nlog++] = LogRec{p, v, j, 0};
-          S.found = 1;
+          s_slk[j] = pack_slack(d, ma, nt);
         }
-        break;
-      }
-    }
-    pf_stage3();
-    __syncthreads();
-    if (tid == 0) {
-      const uint64_t tB = wall_clock64();
-      S.t_scan += tB - tA;
-      tA = tB;
-    }
-    if (S.found) {
-      if (S.status) break;
-      continue;
-    }
-
-    // ------------------------------- new NodeClaim from templates, in order
-    for (uint32_t t = 0; t < T; t++) {
-      const TmplRec& tr = d.tmpl[t];
-      const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
-      bool any = false;
-      if (d.fk_ok[(size_t)v * T + t])
-        for (uint32_t w = 0; w < W; w++)
-          if (row[w]) any = true;
-      if (!any) continue;
-      if (tr.has_limits) {
-        // <U> filterByRemainingResources on the template's options
-        uint32_t hit = INF;
-        for (uint32_t i = tid; i < d.N; i += FB) {
-          if (!((row[i >> 6] >> (i & 63)) & 1)) continue;
-          bool ok = true;
-          for (uint32_t r = 0; r < R; r++)
-            if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
-          if (ok) hit = 0;
-        }
-        if (blk.bmin(hit) == INF) continue;
-      }
-      if (M >= MC) {
-        if (tid == 0) S.status = 1;
         __syncthreads();
-        break;
-      }
-      const uint32_t j = M;
-      ClaimRec* cr = d.c_rec + j;
-      if (tid < R) {
-        const int64_t tot = tr.daemon[tid] + preq[tid];
-        const uint32_t o = s_thoff[tid], n = s_thoff[tid + 1] - o;
-        S.c0[tid] = thr_search(thr + o, n, 0, tot);
-      }
-      __syncthreads();
-      for (uint32_t w = tid; w < W; w += FB) {
-        uint64_t x = row[w];
-        // establish opts ⊆ thr_set[cursor] for the candidate scan
-        for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * OW + w];
         if (tr.has_limits) {
-          uint64_t y = 0, m = x;
-          while (m) {
-            const uint32_t b = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const uint32_t i = w * 64 + b;
-            bool ok = true;
+          // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+          if (tid < R) S.red64[tid] = 0;
+          __syncthreads();
+          for (uint32_t i = tid; i < d.N; i += FB) {
+            if (!((d.c_opts[(size_t)(cbase + j) * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
             for (uint32_t r = 0; r < R; r++)
-              if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
-            if (ok) y |= 1ull << b;
+              if ((tr.limit_rmask >> r) & 1)
+                atomicMax(&S.red64[r], (unsigned long long)(d.it_cap[(size_t)r * d.N + i] + (1ll << 62)));
           }
-          x = y;
-        }
-        d.c_opts[(size_t)j * OW + w] = x;
-      }
-      if (tid < RR) {
-        int64_t tot = 0;
-        uint32_t c0 = 0;
-        if (tid < R) {
-          tot = tr.daemon[tid] + preq[tid];
-          c0 = S.c0[tid];
-        }
-        cr->tot(tid) = tot;
-        cr->thr(tid) = (uint16_t)c0;
-        S.red64[tid] = 0;
-      }
-      if (tid == 0) {
-        cr->tmpl = t;
-        cr->count = 1;
-        cr->zm = tr.zm & vr.zm;
-        cr->cm = tr.cm & vr.cm;
-        FK* cf = d.c_fk + (size_t)j * F;
-        for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
-        for (uint32_t k = 0; k < vr.fk_count; k++) {
-          const FKEntry& e = d.fk_entries[vr.fk_begin + k];
-          const FK cur = cf[e.slot];
-          cf[e.slot] = (cur.flags & FK_PRESENT)
-                           ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
-                           : e.st;
-        }
-        s_ord[M] = (uint16_t)M;
-        s_sc[M] = 1;
-        s_tmpl[M] = (uint8_t)t;
-        S.M = M + 1;
-        S.modkind = MOD_APPEND;
-        d.log[S.nlog++] = LogRec{p, v, j, 0};
-        S.found = 1;
-      }
-      __syncthreads();
-      // max allocatable over the new claim's options (the slack bound)
-      for (uint32_t i = tid; i < d.N; i += FB) {
-        if (!((d.c_opts[(size_t)j * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
-        for (uint32_t r = 0; r < R; r++) atomicMax(&S.red64[r], (unsigned long long)d.it_alloc[(size_t)r * d.N + i]);
-      }
-      __syncthreads();
-      if (tid < RR) cr->maxa[tid] = tid < R ? (int64_t)S.red64[tid] : 0;
-      if (tid == 0) {
-        // LDS slack from the max allocatable over the new claim's options
-        int64_t nt[RR], ma[RR];
-#pragma unroll
-        for (uint32_t r = 0; r < RR; r++) {
-          nt[r] = r < R ? tr.daemon[r] + preq[r] : 0;
-          ma[r] = r < R ? (int64_t)S.red64[r] : 0;
-        }
-        s_slk[j] = pack_slack(d, ma, nt);
-      }
-      __syncthreads();
-      if (tr.has_limits) {
-        // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
-        if (tid < R) S.red64[tid] = 0;
-        __syncthreads();
-        for (uint32_t i = tid; i < d.N; i += FB) {
-          if (!((d.c_opts[(size_t)j * OW + (i >> 6)] >> (i & 63)) & 1)) continue;
-          for (uint32_t r = 0; r < R; r++)
-            if ((tr.limit_rmask >> r) & 1)
-              atomicMax(&S.red64[r], (unsigned long long)(d.it_cap[(size_t)r * d.N + i] + (1ll << 62)));
+          __syncthreads();
+          if (tid < R && ((tr.limit_rmask >> tid) & 1) && S.red64[tid] != 0)
+            t_rem[(size_t)t * R + tid] -= (int64_t)(S.red64[tid] - (1ull << 62));
         }
         __syncthreads();
-        if (tid < R && ((tr.limit_rmask >> tid) & 1) && S.red64[tid] != 0)
-          d.t_rem[(size_t)t * R + tid] -= (int64_t)(S.red64[tid] - (1ull << 62));
+        break;
       }
       __syncthreads();
-      break;
-    }
-    __syncthreads();
-    if (tid == 0) S.t_tmpl += wall_clock64() - tA;
-    if (S.status) break;
-    if (S.found) continue;
+      if (tid == 0) S.t_tmpl += wall_clock64() - tA;
+      if (S.status) break;
+      if (S.found) continue;
 
-    // ------------------------------------ failed: Relax, then Queue.Push
+      // ------------------------------------ failed: Relax, then Queue.Push
+      if (tid == 0) {
+        bool relaxed = false;
+        if (v + 1 < d.var_begin[gp] + d.var_count[gp]) {
+          cur_var[p] = v + 1;
+          relaxed = true;
+        }
+        uint32_t tail = S.qhead + S.qlen;
+        if (tail >= P) tail -= P;
+        queue[tail] = p;
+        S.qlen++;
+        if (relaxed) {
+          S.epoch++;
+        } else {
+          last_epoch[p] = S.epoch;
+          last_len[p] = S.qlen;
+        }
+      }
+      __syncthreads();
+    }
+
+    __syncthreads();
+    if (!SIM)
+      for (uint32_t i = tid; i < S.M; i += FB) d.c_sorted[i] = s_ord[i];
     if (tid == 0) {
-      bool relaxed = false;
-      if (v + 1 < d.var_begin[p] + d.var_count[p]) {
-        d.cur_var[p] = v + 1;
-        relaxed = true;
-      }
-      uint32_t tail = S.qhead + S.qlen;
-      if (tail >= P) tail -= P;
-      d.queue[tail] = p;
-      S.qlen++;
-      if (relaxed) {
-        S.epoch++;
-      } else {
-        d.last_epoch[p] = S.epoch;
-        d.last_len[p] = S.qlen;
-      }
+      Ctrl c;
+      c.status = S.status;
+      c.n_claims = S.M;
+      c.n_log = S.nlog;
+      c.qhead = S.qhead;
+      c.qlen = S.qlen;
+      c.epoch = S.epoch;
+      c.pops = S.pops;
+      c.generic_sorts = S.generic;
+      c.fast_sorts = S.fast;
+      c.cand_evals = S.cand;
+      c.cand_full = S.cand_full;
+      c.t_sort = S.t_sort;
+      c.t_scan = S.t_scan;
+      c.t_tmpl = S.t_tmpl;
+      c.t_total = wall_clock64() - S.t0;
+      S.dbg[7] = __builtin_amdgcn_s_memtime() - S.dbg[7];  // shader clock cycles over the solve
+      for (int q = 0; q < 16; q++) c.dbg[q] = S.dbg[q];
+      *(SIM ? d.sim_ctrl + sim : d.ctrl) = c;
     }
     __syncthreads();
   }
-
-  __syncthreads();
-  for (uint32_t i = tid; i < S.M; i += FB) d.c_sorted[i] = s_ord[i];
-  if (tid == 0) {
-    Ctrl c;
-    c.status = S.status;
-    c.n_claims = S.M;
-    c.n_log = S.nlog;
-    c.qhead = S.qhead;
-    c.qlen = S.qlen;
-    c.epoch = S.epoch;
-    c.pops = S.pops;
-    c.generic_sorts = S.generic;
-    c.fast_sorts = S.fast;
-    c.cand_evals = S.cand;
-    c.cand_full = S.cand_full;
-    c.t_sort = S.t_sort;
-    c.t_scan = S.t_scan;
-    c.t_tmpl = S.t_tmpl;
-    c.t_total = wall_clock64() - S.t0;
-    S.dbg[7] = __builtin_amdgcn_s_memtime() - S.dbg[7];  // shader clock cycles over the kernel
-    for (int q = 0; q < 16; q++) c.dbg[q] = S.dbg[q];
-    *d.ctrl = c;
-  }
 }
 
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr) {
+// dynamic LDS: ord/sc/scr u16 + slack u64 + tmpl u8 per claim, thresholds,
+// and (simulations) the touched-node bitmap + overlay ids
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap) {
   const uint32_t thr = nthr + 4;
-  return 15u * max_claims + 8u + thr * 8u;
+  return ((15u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u;
 }
 
-template <uint32_t RR>
-static hipError_t ffd_attr(uint32_t lds_bytes) {
-  return hipFuncSetAttribute((const void*)ffd_kernel<RR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+// every instantiation may use all LDS its static footprint leaves free
+static uint32_t g_ffd_dyn_max = 0;
+
+template <uint32_t RR, bool SIM>
+static hipError_t ffd_attr(uint32_t lds_total) {
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM>);
+  if (e != hipSuccess) return e;
+  const uint32_t dyn = lds_total > a.sharedSizeBytes ? lds_total - (uint32_t)a.sharedSizeBytes : 0;
+  if (!g_ffd_dyn_max || dyn < g_ffd_dyn_max) g_ffd_dyn_max = dyn;
+  return hipFuncSetAttribute((const void*)ffd_kernel<RR, SIM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
 }
 
-extern "C" hipError_t gsk_init_ffd(uint32_t lds_bytes) {
+extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
   hipError_t e = hipSuccess;
-  for (hipError_t x : {ffd_attr<1>(lds_bytes), ffd_attr<2>(lds_bytes), ffd_attr<3>(lds_bytes), ffd_attr<4>(lds_bytes),
-                       ffd_attr<5>(lds_bytes), ffd_attr<6>(lds_bytes), ffd_attr<7>(lds_bytes), ffd_attr<8>(lds_bytes)})
+  for (hipError_t x : {ffd_attr<1, false>(lds_total), ffd_attr<2, false>(lds_total), ffd_attr<3, false>(lds_total),
+                       ffd_attr<4, false>(lds_total), ffd_attr<5, false>(lds_total), ffd_attr<6, false>(lds_total),
+                       ffd_attr<7, false>(lds_total), ffd_attr<8, false>(lds_total), ffd_attr<1, true>(lds_total),
+                       ffd_attr<2, true>(lds_total), ffd_attr<3, true>(lds_total), ffd_attr<4, true>(lds_total),
+                       ffd_attr<5, true>(lds_total), ffd_attr<6, true>(lds_total), ffd_attr<7, true>(lds_total),
+                       ffd_attr<8, true>(lds_total)})
     if (x != hipSuccess) e = x;
   return e;
 }
 
-extern "C" hipError_t gsk_ffd(const DevProblem* d, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr);
-  switch (d->R) {
-#define GSK_CASE(n) \
-  case n: hipLaunchKernelGGL(ffd_kernel<n>, dim3(1), dim3(FB), lds, s, *d); break;
+// dynamic LDS available to every ffd_kernel instantiation (after gsk_init_ffd)
+extern "C" uint32_t gsk_ffd_dyn_lds_max(void) { return g_ffd_dyn_max; }
+
+// grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
+// draining the simulation counter (consolidation)
+extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap);
+  if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
+  const bool sim = d->n_sims > 0;
+  switch (d->R * 2 + (sim ? 1 : 0)) {
+#define GSK_CASE(n)                                                                            \
+  case 2 * n: hipLaunchKernelGGL((ffd_kernel<n, false>), dim3(1), dim3(FB), lds, s, *d); break; \
+  case 2 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, true>), dim3(blocks), dim3(FB), lds, s, *d); break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

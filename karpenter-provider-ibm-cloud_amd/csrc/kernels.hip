@@ -4,10 +4,9 @@
 //                      (one wave per (variant, template); lane = instance type;
 //                      __ballot packs 64 ITs per word) + wave argmin of the
 //                      cheapest compatible offering, key (price_rank<<32|name_rank)
-//  K4    ffd_kernel    the sequential Scheduler.Solve queue loop as ONE
-//                      persistent workgroup: in-flight NodeClaims are scored in
-//                      parallel (256 candidates per step) in the exact order an
-//                      emulated Go sort.Slice leaves them
+//  K4    ffd_kernel    (ffd.hip) the sequential Scheduler.Solve queue loop as
+//                      ONE persistent workgroup, or one workgroup per
+//                      consolidation simulation
 //  K3    trunc_kernel  per NodeClaim: OrderByPrice + Truncate(60)
 //
 // All integer/bitset work: no MFMA.  Semantics cited as <U> restate
@@ -109,11 +108,20 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
 // ========================================================================= K3
 // <U> InstanceTypes.OrderByPrice(reqs) + Truncate(60): key per option IT =
 // (rank of its cheapest available compatible offering price, name rank)
+// Consolidation simulations (n_sims > 0): block s truncates the NodeClaim of
+// simulation s when it opened exactly one (the only case computeConsolidation
+// prices); output slot s.
 extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
   extern __shared__ uint64_t keys[];
   __shared__ uint32_t cnt;
-  const uint32_t j = blockIdx.x;
-  if (j >= d.ctrl->n_claims) return;
+  uint32_t j = blockIdx.x;  // claim
+  const uint32_t o = blockIdx.x;  // output slot
+  if (d.n_sims) {
+    if (o >= d.n_sims || d.sim_ctrl[o].status != 0 || d.sim_ctrl[o].n_claims != 1) return;
+    j = d.sim_pod_off[o];
+  } else if (j >= d.ctrl->n_claims) {
+    return;
+  }
   const uint32_t tid = threadIdx.x;
   const ClaimRec& h = d.c_rec[j];
   const uint64_t G = grid_of(h.zm, h.cm, d.Z, d.C);
@@ -156,8 +164,8 @@ extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
     }
   }
   const uint32_t take = n < 60 ? n : 60;
-  for (uint32_t i = tid; i < take; i += BLOCK) d.c_its[(size_t)j * 60 + i] = d.rank_to_it[(uint32_t)keys[i]];
-  if (tid == 0) d.c_nits[j] = take;
+  for (uint32_t i = tid; i < take; i += BLOCK) d.c_its[(size_t)o * 60 + i] = d.rank_to_it[(uint32_t)keys[i]];
+  if (tid == 0) d.c_nits[o] = take;
 }
 
 // ------------------------------------------------------------ host launchers
@@ -176,6 +184,8 @@ extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, hipStr
 
 
 extern "C" hipError_t gsk_trunc(const DevProblem* d, uint32_t lds_bytes, hipStream_t s) {
-  hipLaunchKernelGGL(trunc_kernel, dim3(d->max_claims), dim3(BLOCK), lds_bytes, s, *d);
+  const uint32_t grid = d->n_sims ? d->n_sims : d->max_claims;
+  if (!grid) return hipSuccess;
+  hipLaunchKernelGGL(trunc_kernel, dim3(grid), dim3(BLOCK), lds_bytes, s, *d);
   return hipGetLastError();
 }

@@ -174,8 +174,26 @@ struct DevProblem {
   uint32_t* c_sorted;          // [max_claims] final sort order (debug)
   Ctrl* ctrl;
   // truncation outputs
-  uint32_t* c_its;             // [max_claims][60]
-  uint32_t* c_nits;            // [max_claims]
+  uint32_t* c_its;             // [max_claims][60] (simulations: [n_sims][60])
+  uint32_t* c_nits;            // [max_claims]     (simulations: [n_sims])
+  // consolidation simulations (n_sims > 0: one workgroup per simulation).
+  // Per simulation s the pod range [sim_pod_off[s], sim_pod_off[s+1]) indexes
+  // sim_pods and is also the simulation's arena in queue/last_len/last_epoch/
+  // cur_var/log and in the claim arrays (a simulation opens at most one
+  // NodeClaim per pod).  Existing nodes are the shared read-only nodes0/n_fk0
+  // plus a per-block overlay of the nodes the simulation touched.
+  uint32_t n_sims;
+  uint32_t ov_cap;             // overlay entries per block (candidates + pods of a simulation)
+  uint32_t nb_words;           // ceil(NN / 32): LDS touched-node bitmap
+  uint32_t pad_sim;
+  const uint32_t* sim_pod_off; // [n_sims + 1]
+  const uint32_t* sim_pods;    // pod ids, queue order within each simulation
+  const uint32_t* sim_cand_off;// [n_sims + 1]
+  const uint32_t* sim_cands;   // node positions removed by each simulation
+  int64_t* ov_req;             // [grid][ov_cap][RMAX]
+  FK* ov_fk;                   // [grid][ov_cap][F]
+  Ctrl* sim_ctrl;              // [n_sims]
+  uint32_t* sim_next;          // work counter (reset before each launch)
 };
 
 }  // namespace gsd

@@ -152,3 +152,66 @@ def feas_to_dict(res: GsFeasResult) -> dict:
     cheapest = _arr(res.cheapest_it, P * T, np.int32).reshape(P, T)
     nfo = _arr(res.n_feasible_offerings, P * T, np.uint32).reshape(P, T)
     return {"rows": rows, "cheapest": cheapest, "n_feasible_offerings": nfo, "checks": int(res.checks)}
+
+
+# ------------------------------------------------------------ consolidation
+CONSOLIDATE_EVAL, CONSOLIDATE_SINGLE, CONSOLIDATE_MULTI = 0, 1, 2
+DECISION_NOOP, DECISION_DELETE, DECISION_REPLACE, DECISION_SKIPPED = 0, 1, 2, 3
+DECISION_NAMES = {0: "NoOp", 1: "Delete", 2: "Replace", 3: "Skipped"}
+(NOOP_NONE, NOOP_UNSCHEDULABLE, NOOP_MULTIPLE_CLAIMS, NOOP_PRICE_UNKNOWN, NOOP_SPOT_TO_SPOT,
+ NOOP_NOT_CHEAPER, NOOP_SAME_TYPE) = range(7)
+
+
+class GsRange(C.Structure):
+    _fields_ = [("begin", _U32), ("count", _U32)]
+
+
+class GsConsolidation(C.Structure):
+    _fields_ = [
+        ("cluster", C.POINTER(GsProblem)),
+        ("bound_pods", _P), ("n_bound_pods", _U32),
+        ("bound_pod_node", _P),
+        ("candidates", _P), ("n_candidates", _U32),
+        ("sets", _P), ("n_sets", _U32),
+        ("mode", _U32), ("max_candidates", _U32),
+        ("shard_index", _U32), ("shard_count", _U32),
+    ]
+
+
+class GsCommand(C.Structure):
+    _fields_ = [
+        ("decision", _U32), ("reason", _U32), ("n_new_claims", _U32), ("n_failed_pods", _U32),
+        ("n_candidates", _U32), ("nodepool", _U32), ("spot_only", _U32), ("options", GsRange),
+        ("candidate_price", C.c_double),
+    ]
+
+
+class GsConsolidationResult(C.Structure):
+    _fields_ = [
+        ("n_commands", _U32),
+        ("commands", C.POINTER(GsCommand)),
+        ("options", C.POINTER(C.c_uint32)),
+        ("option_prices", C.POINTER(C.c_double)),
+        ("chosen", C.c_int32),
+        ("n_multi_options", _U32),
+        ("multi_options", C.POINTER(C.c_uint32)),
+        ("pods_simulated", _U32),
+        ("checks", C.c_uint64),
+        ("t_encode_ms", C.c_double), ("t_upload_ms", C.c_double), ("t_feas_ms", C.c_double),
+        ("t_sim_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
+    ]
+
+
+def commands_to_list(res: GsConsolidationResult) -> list:
+    """Canonical, comparable form of the commands (copied out of library memory)."""
+    out = []
+    for i in range(res.n_commands):
+        c = res.commands[i]
+        opts = [int(res.options[c.options.begin + k]) for k in range(c.options.count)]
+        prices = [float(res.option_prices[c.options.begin + k]) for k in range(c.options.count)]
+        out.append({"decision": int(c.decision), "reason": int(c.reason), "n_new_claims": int(c.n_new_claims),
+                    "n_failed_pods": int(c.n_failed_pods), "n_candidates": int(c.n_candidates),
+                    "nodepool": int(c.nodepool) if c.decision == DECISION_REPLACE else None,
+                    "spot_only": int(c.spot_only), "options": opts, "option_prices": prices,
+                    "candidate_price": float(c.candidate_price)})
+    return out

@@ -13,7 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgpusched.so")
 
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
-           "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms"]
+           "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
+           "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose"]
 
 
 class GpuSchedError(RuntimeError):
@@ -56,8 +57,47 @@ def load():
         L.gs_abi_sizes.restype = C.c_uint32
         L.gs_last_run_ms.argtypes = [vp, C.POINTER(C.c_double)]
         L.gs_last_run_ms.restype = C.c_int
+        L.gs_consolidate.argtypes = [vp, C.POINTER(abi.GsConsolidation), C.POINTER(abi.GsConsolidationResult)]
+        L.gs_consolidate.restype = C.c_int
+        L.gs_consolidate_rerun.argtypes = [vp, C.POINTER(abi.GsConsolidationResult)]
+        L.gs_consolidate_rerun.restype = C.c_int
+        L.gs_consolidation_choose.argtypes = [C.POINTER(abi.GsConsolidation), C.POINTER(abi.GsCommand), C.c_uint32,
+                                              C.POINTER(C.c_uint32), C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.gs_consolidation_choose.restype = C.c_int
         _lib = L
     return _lib
+
+
+def _multi(res):
+    return [int(res.multi_options[i]) for i in range(res.n_multi_options)]
+
+
+def choose(cin, commands):
+    """gs_consolidation_choose (host only): replay SINGLE/MULTI over a complete
+    command table, e.g. gathered from sharded evaluations -> (chosen, multi_options)"""
+    n = len(commands)
+    cmds = (abi.GsCommand * max(n, 1))()
+    opts, prices = [], []
+    for i, c in enumerate(commands):
+        x = cmds[i]
+        x.decision, x.reason, x.n_new_claims = c["decision"], c["reason"], c["n_new_claims"]
+        x.n_failed_pods, x.n_candidates = c["n_failed_pods"], c["n_candidates"]
+        x.nodepool = c["nodepool"] if c["nodepool"] is not None else 0
+        x.spot_only = c["spot_only"]
+        x.options.begin, x.options.count = len(opts), len(c["options"])
+        x.candidate_price = c["candidate_price"]
+        opts += c["options"]
+        prices += c["option_prices"]
+    oa = (C.c_uint32 * max(len(opts), 1))(*opts)
+    pa = (C.c_double * max(len(prices), 1))(*prices)
+    chosen = C.c_int32(-1)
+    mo = (C.c_uint32 * 60)()
+    nmo = C.c_uint32(0)
+    st = load().gs_consolidation_choose(C.byref(cin.struct), cmds, n, oa, pa, C.byref(chosen), mo, C.byref(nmo))
+    if st != abi.GS_OK:
+        raise GpuSchedError(st, "gs_consolidation_choose failed")
+    return int(chosen.value), [int(mo[i]) for i in range(nmo.value)]
 
 
 def validate(problem):
@@ -122,6 +162,17 @@ class Solver:
         self.prepare(problem)
         self.run()
         return self.fetch()
+
+    def consolidate(self, cin):
+        """gs_consolidate: (commands, chosen, multi_options, raw result)"""
+        res = abi.GsConsolidationResult()
+        self._check(self.L.gs_consolidate(self.ctx, C.byref(cin.struct), C.byref(res)))
+        return abi.commands_to_list(res), int(res.chosen), _multi(res), res
+
+    def consolidate_rerun(self):
+        res = abi.GsConsolidationResult()
+        self._check(self.L.gs_consolidate_rerun(self.ctx, C.byref(res)))
+        return abi.commands_to_list(res), int(res.chosen), _multi(res), res
 
     def feasibility(self):
         res = abi.GsFeasResult()

@@ -33,6 +33,8 @@ class ProblemBuilder:
         self.nodepools = []
         self.pods = []
         self.nodes = []
+        self.bound_pods = []  # reschedulable pods bound to state nodes (consolidation)
+        self.bound_node = []
 
     # ------------------------------------------------------------ primitives
     def s(self, x: str) -> int:
@@ -119,6 +121,15 @@ class ProblemBuilder:
                           self._tols(tolerations), int(flags)))
         return len(self.pods) - 1
 
+    def add_bound_pod(self, node, uid, creation_ns, requests, node_selector=None, required_terms=(),
+                      preferred_terms=(), tolerations=(), flags=0):
+        """a reschedulable pod bound to state node `node` (disruption candidates' pods)"""
+        self.bound_pods.append((self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
+                                self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
+                                self._tols(tolerations), int(flags)))
+        self.bound_node.append(int(node))
+        return len(self.bound_pods) - 1
+
     def add_node(self, name, labels, available, requests=None, taints=(), initialized=True):
         self.nodes.append((self.s(name), 1 if initialized else 0, self._labels(labels), self._taints(taints),
                            self._qty(available), self._qty(requests or {})))
@@ -155,6 +166,8 @@ class Problem:
         self.nodepools = _np(b.nodepools, abi.DT_NODEPOOL)
         self.pods = _np(b.pods, abi.DT_POD)
         self.nodes = _np(b.nodes, abi.DT_NODE)
+        self.bound_pods = _np(b.bound_pods, abi.DT_POD)
+        self.bound_node = np.asarray(b.bound_node, dtype=np.uint32)
         self.struct = abi.GsProblem()
         st = self.struct
         st.strings = self._cstrs

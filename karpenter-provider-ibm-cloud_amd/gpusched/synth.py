@@ -368,3 +368,128 @@ def make_c4_sim(n_nodes=500, n_pods=2000, seed=0x5EED0004):
 
 
 CONFIGS["C4sim"] = make_c4_sim
+
+
+BIG_CPU = np.array([1000, 2000, 3000, 4000, 6000], dtype=np.int64)
+
+
+def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=200, full_frac=0.15, big_frac=0.3):
+    """C4 consolidation cluster: state nodes sampled from the C2
+    catalog in 2 NodePools, each carrying bound reschedulable pods that use
+    `util` of its allocatable cpu (a `full_frac` share of nodes run at ~97 %;
+    a `big_frac` share of nodes carry 1-6 vCPU pods),
+    plus `n_pending` pending pods.  Node available = allocatable - daemon -
+    bound pods (StateNode.Available)."""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c2_profiles(n_its)
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng, unavailable_frac=0.02)
+    daemon = {"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000}
+    b.add_nodepool("general", weight=10, requirements=[("kubernetes.io/arch", "In", ["amd64"]),
+                                                       ("kubernetes.io/os", "In", ["linux"])],
+                   labels={"team": "general"}, daemon=daemon)
+    b.add_nodepool("spot-batch", weight=0, requirements=[("karpenter.sh/capacity-type", "In", ["spot"])],
+                   daemon=daemon)
+    cand = [it for it in its if it.capacity["nvidia.com/gpu"] == 0 and it.capacity["cpu"] <= 32000]
+    for k in range(n_nodes):
+        it = cand[rng.integers(0, len(cand))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        zone = FAKE_ZONES[rng.integers(0, 3)]
+        pool = "spot-batch" if rng.random() < 0.25 else "general"
+        ct = "spot" if pool == "spot-batch" or rng.random() < 0.2 else "on-demand"
+        labels.update({"topology.kubernetes.io/zone": zone, "karpenter.sh/capacity-type": ct,
+                       "karpenter.sh/nodepool": pool, "kubernetes.io/os": "linux",
+                       "kubernetes.io/hostname": f"node-{k:05d}"})
+        if pool == "general":
+            labels["team"] = "general"
+        alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        target = float(rng.uniform(*util)) if rng.random() >= full_frac else 0.97
+        used = {"cpu": daemon["cpu"], "memory": daemon["memory"], "pods": daemon["pods"]}
+        ts = 1_700_000_000_000_000_000 + int(rng.integers(0, 8)) * 1_000_000_000
+        big = rng.random() < big_frac
+        while True:
+            if big:
+                cpu = int(rng.choice(BIG_CPU))
+                mem = int(rng.choice(MEM_CHOICES[2:]))
+            else:
+                cpu = int(rng.choice(CPU_CHOICES, p=CPU_W / CPU_W.sum()))
+                mem = int(rng.choice(MEM_CHOICES[:4]))
+            if used["cpu"] + cpu > target * alloc["cpu"] or used["memory"] + mem > alloc["memory"] \
+                    or used["pods"] + 1000 > alloc["pods"]:
+                break
+            used["cpu"] += cpu
+            used["memory"] += mem
+            used["pods"] += 1000
+            b.add_bound_pod(k, _uid(rng), ts, {"cpu": cpu, "memory": mem, "pods": 1000})
+        avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
+        b.add_node(f"node-{k:05d}", labels, avail, initialized=bool(rng.random() < 0.97))
+    _pods_basic(b, rng, n_pending, its, gpu_frac=0.0, selector_frac=0.05)
+    return b.build()
+
+
+CONFIGS["C4"] = make_c4
+
+
+def random_consolidation(seed, n_nodes=None, n_pending=None):
+    """small adversarial consolidation cluster: nodes with taints, custom
+    labels, spot/on-demand, uninitialized nodes and bound pods with
+    selectors/tolerations; pending pods; 1-3 NodePools (taints, limits)"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = FAKE_ZONES[: int(rng.integers(1, 4))]
+    profs = []
+    for fam in ["bx2", "cx2", "mx2"]:
+        for v in [2, 4, 8, 16]:
+            if rng.random() < 0.6:
+                profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    if len(profs) < 2:
+        profs = [("bx2-2x8", 2, 8, None), ("bx2-8x32", 8, 32, None)]
+    prices = {p[0]: round(float(rng.choice([0.05, 0.1, 0.1, 0.2, 0.4])) * p[1] / 2, 4) for p in profs}
+    its = build_catalog(b, profs, zones, spot=True, prices=prices, rng=rng, unavailable_frac=0.1)
+    effects = ["NoSchedule", "PreferNoSchedule"]
+    n_np = int(rng.integers(1, 4))
+    for j in range(n_np):
+        reqs = []
+        if rng.random() < 0.3:
+            reqs.append(("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))]))
+        if rng.random() < 0.2:
+            reqs.append(("karpenter-ibm.sh/instance-family", "NotIn", ["mx2"]))
+        taints = [("dedicated", "x", str(rng.choice(effects)))] if rng.random() < 0.3 else []
+        limits = {"cpu": int(rng.choice([16, 64, 256])) * 1000} if rng.random() < 0.2 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10, 50])), requirements=reqs,
+                       labels={"team": str(rng.choice(["a", "b"]))} if rng.random() < 0.4 else {},
+                       taints=taints, limits=limits, daemon={"cpu": 100, "pods": 1000})
+    nn = int(n_nodes if n_nodes is not None else rng.integers(2, 16))
+    for k in range(nn):
+        it = its[rng.integers(0, len(its))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels["topology.kubernetes.io/zone"] = zones[rng.integers(0, len(zones))]
+        labels["karpenter.sh/capacity-type"] = str(rng.choice(["spot", "on-demand"]))
+        labels["karpenter.sh/nodepool"] = f"np{rng.integers(0, n_np)}"
+        labels["kubernetes.io/hostname"] = f"n-{k:03d}"
+        if rng.random() < 0.4:
+            labels["team"] = str(rng.choice(["a", "b"]))
+        alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        used = {"cpu": 100, "memory": 0, "pods": 1000}
+        target = float(rng.uniform(0.3, 1.0))
+        ts = 1_700_000_000_000_000_000 + int(rng.integers(0, 4)) * 1_000_000_000
+        for _ in range(int(rng.integers(0, 12))):
+            cpu = int(rng.choice([100, 250, 500, 1000, 2000, 4000]))
+            mem = int(rng.choice([128 * MI, GI, 4 * GI])) * 1000
+            if used["cpu"] + cpu > target * alloc["cpu"] or used["memory"] + mem > alloc["memory"]:
+                break
+            used["cpu"] += cpu
+            used["memory"] += mem
+            used["pods"] += 1000
+            sel = {"team": labels["team"]} if "team" in labels and rng.random() < 0.3 else {}
+            tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+            b.add_bound_pod(k, _uid(rng), ts, {"cpu": cpu, "memory": mem, "pods": 1000}, node_selector=sel,
+                            tolerations=tols)
+        avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
+        taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.15 else []
+        b.add_node(f"n-{k:03d}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.85))
+    npend = int(n_pending if n_pending is not None else rng.choice([0, 0, 1, 3]))
+    for i in range(npend):
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000, {"cpu": int(rng.choice([100, 1000, 3000])),
+                                                         "memory": int(GI) * 1000, "pods": 1000})
+    return b.build()

@@ -75,6 +75,13 @@ const char* oracle_capacity_type(const char* availability_class);
 /* calculateInstanceTypeScore (instancetype.go:90-110) for cpu/memory quantities */
 double oracle_instance_score(int64_t cpu_milli, int64_t memory_bytes, double price);
 
+/* <U> disruption consolidation (SimulateScheduling + computeConsolidation and
+ * the single/multi-node policies), one naive Solve per simulation.  For MULTI
+ * the surviving options of the chosen command (after filterOutSameInstanceType)
+ * go to multi_opts (capacity 60). */
+gs_status oracle_consolidate(const gs_consolidation* in, gs_consolidation_result* out, int32_t* chosen,
+                             uint32_t* multi_opts, uint32_t* n_multi_opts);
+
 /* Go sort.Slice (pdqsort_func) applied to an int array with Less = a[i] < a[j];
  * perm receives the resulting permutation of original indices. */
 void oracle_go_sort_ints(int64_t* keys, uint32_t* perm, uint32_t n);

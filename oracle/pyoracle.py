@@ -63,6 +63,9 @@ def lib():
             getattr(L, f).restype = C.c_char_p
         L.oracle_instance_score.argtypes = [C.c_int64, C.c_int64, C.c_double]
         L.oracle_instance_score.restype = C.c_double
+        L.oracle_consolidate.argtypes = [C.POINTER(abi.GsConsolidation), C.POINTER(abi.GsConsolidationResult),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.oracle_consolidate.restype = C.c_int
         L.oracle_go_sort_ints.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_uint32), C.c_uint32]
         _lib = L
     return _lib
@@ -82,6 +85,18 @@ def feasibility(problem):
     if st != abi.GS_OK:
         return st, None
     return st, abi.feas_to_dict(res)
+
+
+def consolidate(cin):
+    """cin: gpusched.consolidation.ConsolidationInput -> (status, commands, chosen, multi_options)"""
+    res = abi.GsConsolidationResult()
+    chosen = C.c_int32(-1)
+    mo = (C.c_uint32 * 60)()
+    nmo = C.c_uint32(0)
+    st = lib().oracle_consolidate(C.byref(cin.struct), C.byref(res), C.byref(chosen), mo, C.byref(nmo))
+    if st != abi.GS_OK:
+        return st, None, None, None
+    return st, abi.commands_to_list(res), int(chosen.value), [int(mo[i]) for i in range(nmo.value)]
 
 
 def _cstrs(xs):

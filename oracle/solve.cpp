@@ -993,3 +993,279 @@ extern "C" void oracle_go_sort_ints(int64_t* keys, uint32_t* perm, uint32_t n) {
   } d{keys, perm};
   gosort::slice(d, (int)n);
 }
+
+// ===================================================================== consolidation
+// <U> pkg/controllers/disruption (karpenter v1.13.0): SimulateScheduling,
+// computeConsolidation, getCandidatePrices, filterByPrice,
+// filterOutSameInstanceType, SingleNodeConsolidation.ComputeCommand (first
+// non-NoOp in candidate order) and MultiNodeConsolidation
+// .firstNConsolidationOption (binary search over candidates[0:mid+1]).
+// SpotToSpotConsolidation is off (feature-gate default).  Each simulation is
+// a fresh Builder + Scheduler over the reduced problem: deliberately naive.
+namespace {
+
+struct ConsStore {
+  vector<gs_command> cmds;
+  vector<uint32_t> opts;
+  vector<double> prices;
+};
+ConsStore g_cons;
+
+const char* kInstanceType = "node.kubernetes.io/instance-type";
+
+struct Candidate {
+  bool priced = false;  // getCandidatePrices found an offering
+  double price = 0;
+  string it_name;
+  bool it_found = false;
+  bool spot = false;
+};
+
+// <U> Candidate construction + getCandidatePrices for one state node:
+// c.instanceType.Offerings.Compatible(NewLabelRequirements(labels)).Cheapest()
+Candidate candidate_of(const gs_problem* p, const OracleState& st, uint32_t node) {
+  Candidate c;
+  Builder b{p, const_cast<OracleState&>(st)};
+  auto labels = b.labels_of(p->nodes[node].labels);
+  Reqs lr;
+  for (auto& kv : labels) lr.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
+  auto ct = labels.find(kCapacityType);
+  c.spot = ct != labels.end() && ct->second == "spot";
+  auto itn = labels.find(kInstanceType);
+  if (itn == labels.end()) return c;
+  c.it_name = itn->second;
+  for (auto& it : st.its) {
+    if (it.name != c.it_name) continue;
+    c.it_found = true;
+    for (auto& of : it.offerings) {
+      if (!lr.compatible(of.reqs, true)) continue;
+      if (!c.priced || of.price < c.price) {
+        c.price = of.price;
+        c.priced = true;
+      }
+    }
+    break;
+  }
+  return c;
+}
+
+// cheapest available offering compatible with reqs (OrderByPrice's key)
+double cheapest_available(const InstanceType* it, const Reqs& reqs) {
+  double best = __DBL_MAX__;
+  bool any = false;
+  for (auto& of : it->offerings) {
+    if (!of.available || !reqs.compatible(of.reqs, true)) continue;
+    if (!any || of.price < best) {
+      best = of.price;
+      any = true;
+    }
+  }
+  return best;
+}
+
+// one computeConsolidation over a candidate set
+gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, const OracleState& base,
+                    vector<uint32_t>* opts_out, vector<double>* prices_out) {
+  const gs_problem* cl = in->cluster;
+  gs_command cmd;
+  std::memset(&cmd, 0, sizeof cmd);
+  cmd.n_candidates = (uint32_t)cands.size();
+  std::set<uint32_t> cset(cands.begin(), cands.end());
+  // SimulateScheduling: pending pods + the candidates' reschedulable pods,
+  // state nodes minus the candidates
+  vector<gs_pod> pods(cl->pods, cl->pods + cl->n_pods);
+  const uint32_t n_pending = cl->n_pods;
+  for (uint32_t c : cands)
+    for (uint32_t b = 0; b < in->n_bound_pods; b++)
+      if (in->bound_pod_node[b] == c) pods.push_back(in->bound_pods[b]);
+  vector<gs_node> nodes;
+  for (uint32_t n = 0; n < cl->n_nodes; n++)
+    if (!cset.count(n)) nodes.push_back(cl->nodes[n]);
+  gs_problem sub = *cl;
+  sub.pods = pods.data();
+  sub.n_pods = (uint32_t)pods.size();
+  sub.nodes = nodes.data();
+  sub.n_nodes = (uint32_t)nodes.size();
+  OracleState st;
+  Builder b{&sub, st};
+  b.build();
+  Scheduler s{st};
+  auto errors = s.solve();
+  uint32_t failed = 0;
+  for (uint32_t e : errors)
+    if (e >= n_pending) failed++;
+  // pods scheduled against an uninitialized node are errors too
+  for (auto& n : st.nodes)
+    if (!n.initialized)
+      for (auto* p : n.pods)
+        if (p->index >= n_pending) failed++;
+  cmd.n_failed_pods = failed;
+  cmd.n_new_claims = (uint32_t)s.creation_order.size();
+  if (failed) {
+    cmd.reason = GS_NOOP_UNSCHEDULABLE;
+    return cmd;
+  }
+  if (cmd.n_new_claims == 0) {
+    cmd.decision = GS_DECISION_DELETE;
+    return cmd;
+  }
+  if (cmd.n_new_claims > 1) {
+    cmd.reason = GS_NOOP_MULTIPLE_CLAIMS;
+    return cmd;
+  }
+  double cp = 0;
+  bool all_spot = true;
+  for (uint32_t c : cands) {
+    Candidate k = candidate_of(cl, base, c);
+    if (!k.priced) {
+      cmd.reason = GS_NOOP_PRICE_UNKNOWN;
+      return cmd;
+    }
+    cp += k.price;
+    all_spot = all_spot && k.spot;
+  }
+  cmd.candidate_price = cp;
+  NodeClaim* nc = s.creation_order[0];
+  nc->reqs.m.erase(kHostname);  // FinalizeScheduling
+  auto ordered = order_by_price(nc->options, nc->reqs, 60);  // TruncateInstanceTypes + OrderByPrice
+  Req ctr = nc->reqs.get(kCapacityType);
+  if (all_spot && ctr.has("spot")) {
+    cmd.reason = GS_NOOP_SPOT_TO_SPOT;
+    return cmd;
+  }
+  // RemoveInstanceTypeOptionsByPriceAndMinValues (no minValues: refused up front)
+  vector<const InstanceType*> keep;
+  vector<double> kp;
+  for (auto* it : ordered) {
+    double pr = cheapest_available(it, nc->reqs);
+    if (pr < cp) {
+      keep.push_back(it);
+      kp.push_back(pr);
+    }
+  }
+  if (keep.empty()) {
+    cmd.reason = GS_NOOP_NOT_CHEAPER;
+    return cmd;
+  }
+  cmd.decision = GS_DECISION_REPLACE;
+  cmd.nodepool = nc->tmpl->np_index;
+  cmd.spot_only = ctr.has("spot") && ctr.has("on-demand") ? 1u : 0u;
+  cmd.options.begin = (uint32_t)opts_out->size();
+  cmd.options.count = (uint32_t)keep.size();
+  for (size_t i = 0; i < keep.size(); i++) {
+    opts_out->push_back(keep[i]->index);
+    prices_out->push_back(kp[i]);
+  }
+  return cmd;
+}
+
+// <U> filterOutSameInstanceType on a Replace command's options
+vector<uint32_t> filter_out_same_type(const gs_consolidation* in, const OracleState& base, const vector<uint32_t>& cands,
+                                      const uint32_t* opts, const double* prices, uint32_t n) {
+  std::set<string> existing;
+  std::map<string, double> price_by_type;
+  for (uint32_t c : cands) {
+    Candidate k = candidate_of(in->cluster, base, c);
+    existing.insert(k.it_name);
+    if (!k.priced) continue;
+    auto f = price_by_type.find(k.it_name);
+    double ex = f == price_by_type.end() ? __DBL_MAX__ : f->second;
+    if (k.price < ex) price_by_type[k.it_name] = k.price;
+  }
+  double max_price = __DBL_MAX__;
+  for (uint32_t i = 0; i < n; i++) {
+    const string& nm = base.its[opts[i]].name;
+    if (!existing.count(nm)) continue;
+    auto f = price_by_type.find(nm);
+    double pr = f == price_by_type.end() ? 0.0 : f->second;  // Go map zero value
+    if (pr < max_price) max_price = pr;
+  }
+  vector<uint32_t> out;
+  for (uint32_t i = 0; i < n; i++)
+    if (prices[i] < max_price) out.push_back(i);  // filterByPrice
+  return out;
+}
+
+}  // namespace
+
+extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolidation_result* out, int32_t* chosen_out,
+                                        uint32_t* multi_opts, uint32_t* n_multi_opts) {
+  if (!in || !in->cluster || !out) return GS_E_INVALID;
+  OracleState base;
+  vector<vector<uint32_t>> sets;
+  uint32_t mx = 0;
+  try {
+    Builder b{in->cluster, base};
+    b.build();
+    for (uint32_t i = 0; i < in->n_candidates; i++)
+      if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
+    for (uint32_t i = 0; i < in->n_bound_pods; i++)
+      if (in->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
+    if (in->mode == GS_CONSOLIDATE_EVAL) {
+      for (uint32_t s = 0; s < in->n_sets; s++) {
+        if ((uint64_t)in->sets[s].begin + in->sets[s].count > in->n_candidates) return GS_E_INVALID;
+        sets.emplace_back(in->candidates + in->sets[s].begin, in->candidates + in->sets[s].begin + in->sets[s].count);
+      }
+    } else if (in->mode == GS_CONSOLIDATE_SINGLE) {
+      for (uint32_t i = 0; i < in->n_candidates; i++) sets.push_back({in->candidates[i]});
+    } else if (in->mode == GS_CONSOLIDATE_MULTI) {
+      const uint32_t n = in->n_candidates, cap = in->max_candidates ? in->max_candidates : 100;
+      mx = n < cap ? n : cap;  // lo.Clamp(len, 0, 100)
+      if (n >= 2) {
+        if (n <= mx) mx = n - 1;
+        for (uint32_t mid = 1; mid <= mx; mid++) sets.emplace_back(in->candidates, in->candidates + mid + 1);
+      }
+    } else {
+      return GS_E_INVALID;
+    }
+    ConsStore& r = g_cons;
+    r = ConsStore();
+    for (auto& set : sets) r.cmds.push_back(simulate(in, set, base, &r.opts, &r.prices));
+  } catch (const Unsupported& u) {
+    return u.code;
+  }
+  ConsStore& r = g_cons;
+  int32_t chosen = -1;
+  if (n_multi_opts) *n_multi_opts = 0;
+  if (in->mode == GS_CONSOLIDATE_SINGLE) {
+    for (size_t i = 0; i < r.cmds.size(); i++)
+      if (r.cmds[i].decision != GS_DECISION_NOOP) {
+        chosen = (int32_t)i;
+        break;
+      }
+  } else if (in->mode == GS_CONSOLIDATE_MULTI && !sets.empty()) {
+    int lo = 1, hi = (int)mx;
+    vector<uint32_t> saved;
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      const gs_command& c = r.cmds[mid - 1];
+      bool valid = false;
+      vector<uint32_t> keep;
+      if (c.decision == GS_DECISION_REPLACE) {
+        auto idx = filter_out_same_type(in, base, sets[mid - 1], r.opts.data() + c.options.begin,
+                                        r.prices.data() + c.options.begin, c.options.count);
+        for (uint32_t i : idx) keep.push_back(r.opts[c.options.begin + i]);
+        valid = !keep.empty();
+      }
+      if (valid || c.decision == GS_DECISION_DELETE) {
+        chosen = mid - 1;
+        saved = keep;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    if (multi_opts && n_multi_opts) {
+      for (size_t i = 0; i < saved.size() && i < 60; i++) multi_opts[i] = saved[i];
+      *n_multi_opts = (uint32_t)std::min<size_t>(saved.size(), 60);
+    }
+  }
+  if (chosen_out) *chosen_out = chosen;
+  std::memset(out, 0, sizeof(*out));
+  out->n_commands = (uint32_t)r.cmds.size();
+  out->commands = r.cmds.data();
+  out->options = r.opts.data();
+  out->option_prices = r.prices.data();
+  out->chosen = chosen;
+  return GS_OK;
+}
