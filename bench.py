@@ -2,13 +2,20 @@
 """bench.py — BASELINE.json metric on MI355X:
 pod x offering feasibility checks/sec + Solve latency (ms), 100k pods.
 
-A step = one device-resident Solve of the whole workload through the C-ABI
-(gs_run: K1/K2 feasibility -> K4 first-fit-decreasing -> K3 OrderByPrice/
-Truncate(60)); encode + host->HBM upload happen once before the timed region
-and are reported separately.  checks per step = pods x offerings reachable
-from the NodePool.  --gpus N runs N independent replicas
-(one independent cluster's Solve per rank, no data-path collective): weak
-scaling; value = sum of checks over ranks / max step time.
+Headline (`value`): a step = one device-resident provisioning Solve of the CM
+workload through the C-ABI (gs_run: K1/K2 feasibility -> K4 first-fit-
+decreasing -> K3 OrderByPrice/Truncate(60)); encode + host->HBM upload happen
+once before the timed region and are reported separately.  checks per step =
+pods x offerings reachable from the NodePool.  The Solve is
+sequential in pod order, so --gpus N runs N independent replicas (one
+independent cluster's Solve per rank, no data-path collective): weak scaling;
+value = sum of checks over ranks / max step time.
+
+`consolidation`: the C4 workload (BASELINE configs[3]): a SingleNodeConsolidation
+sweep over all 5,000 state nodes, each an independent SimulateScheduling Solve
+(one workgroup per simulation).  Simulations are sharded round-robin over the
+N ranks, their commands all-gathered (RCCL over xGMI), and the policy replayed
+on every rank: strong scaling.
 """
 import argparse
 import json
@@ -20,7 +27,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "karpenter-provider-ibm-cloud_amd"))
 sys.path.insert(0, ROOT)
 
-from gpusched import synth  # noqa: E402
+from gpusched import abi, synth  # noqa: E402
+from gpusched.consolidation import (ConsolidationInput, arrays_to_list, choose_arrays, gather_arrays,  # noqa: E402
+                                    result_arrays)
 from gpusched.lib import Solver  # noqa: E402
 
 METRIC = "pod×offering feasibility checks/sec + Solve latency (ms) at 100k pods, 1/2/4/8 GPU"
@@ -41,6 +50,12 @@ def algorithmic_bytes(res, problem, n_claims):
     ffd = res.pops * per_pop + res.cand_evals * per_cand + adds * per_add
     trunc = n_claims * (W * 8 + 24 + 60 * 4) + N * 16
     return {"feas": feas, "ffd": ffd, "trunc": trunc}
+
+
+def node_check_bytes(R, K=4):
+    """algorithmic bytes of one ExistingNode.CanAdd: available + requests (R x i64),
+    taints (8), ok flag (4), K label value ids (4 each), zone/capacity-type ids (8)"""
+    return 16 * R + 8 + 4 + 4 * K + 8
 
 
 def cpu_baseline(n_pods):
@@ -67,6 +82,105 @@ def cpu_baseline(n_pods):
     }
 
 
+def cpu_baseline_consolidation(problem, cmds, n_sample):
+    """oracle SingleNodeConsolidation simulations (1 thread) on a bounded sample
+    of the candidates; checks the GPU commands on that sample"""
+    from oracle import pyoracle
+    n = len(problem.nodes)
+    sub = list(range(0, n, max(1, n // n_sample)))[:n_sample]
+    t0 = time.perf_counter()
+    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(problem, sub, mode=abi.CONSOLIDATE_SINGLE))
+    dt = time.perf_counter() - t0
+    return {
+        "value": len(sub) / dt,
+        "unit": "simulations/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"C4 cluster, {len(sub)} evenly spaced single-node candidates; oracle {dt * 1e3:.0f} ms; "
+                  f"GPU commands on the sample identical: {st == 0 and [cmds[i] for i in sub] == want}",
+    }
+
+
+def bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks):
+    problem = synth.make_c4(n_nodes=args.c4_nodes)
+    n = len(problem.nodes)
+    cands = list(range(n))
+    shard = (rank, world) if world > 1 else (0, 0)
+    cin = ConsolidationInput(problem, cands, mode=abi.CONSOLIDATE_SINGLE, shard=shard)
+    full = ConsolidationInput(problem, cands, mode=abi.CONSOLIDATE_SINGLE)
+    solver = Solver(local)
+    t0 = time.perf_counter()
+    cmds, _, _, res = solver.consolidate(cin)  # encode + upload + first run
+    prep_ms = (time.perf_counter() - t0) * 1e3
+
+    def sweep():
+        # device simulations + host decisions, then (N > 1) the all-gather of
+        # every rank's commands and the policy replay
+        r = solver.consolidate_rerun(raw=True)
+        if world == 1:
+            return None, int(r.chosen), r
+        merged = gather_arrays(*result_arrays(r), rank, world, dist, device)
+        chosen, _ = choose_arrays(full, *merged)
+        return merged, chosen, r
+
+    for _ in range(args.warmup):
+        sweep()
+    kt = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        merged, chosen, r = sweep()
+        kt.append((r.t_feas_ms, r.t_sim_ms, r.t_truncate_ms, r.t_fetch_ms))
+    if merged is None:
+        merged = result_arrays(r)
+    merged = arrays_to_list(*merged)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    ms = elapsed * 1e3 / args.steps
+    feas_ms = sum(k[0] for k in kt) / len(kt)
+    sim_ms = sum(k[1] for k in kt) / len(kt)
+    trunc_ms = sum(k[2] for k in kt) / len(kt)
+    decide_ms = sum(k[3] for k in kt) / len(kt)
+    R = len(set(int(x) for x in problem.quantities["resource"]))  # encoded resource dimensions
+    nb = node_check_bytes(R)
+    # per-launch algorithmic bytes of the simulation kernel on THIS rank: the
+    # node records a sequential first-fit visits + per pop (variant record
+    # 104 B + requests 8R) + per simulation (candidate ids, control block)
+    n_local = (n + world - 1) // world
+    sim_bytes = r.node_prefix * nb + r.pops * (104 + 8 * R) + n_local * 256
+    ach = sim_bytes / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else 0.0
+    counts = {}
+    for c in merged:
+        k = abi.DECISION_NAMES[c["decision"]]
+        counts[k] = counts.get(k, 0) + 1
+    out = {
+        "workload": f"C4: {n} state nodes (C2 catalog, 2 NodePools, 60-90% cpu used, {len(problem.bound_pods)} "
+                    f"bound pods), SingleNodeConsolidation over all {n} candidates",
+        "simulations": n,
+        "value": n / (ms * 1e-3),
+        "unit": "simulations/s",
+        "ms_per_sweep": ms,
+        "scaling": "strong",
+        "node_checks_per_s": r.checks * world / (ms * 1e-3),
+        "kernel_ms": {"feas": round(feas_ms, 4), "sim": round(sim_ms, 4), "trunc": round(trunc_ms, 4)},
+        "host_decide_fetch_ms": round(decide_ms, 3),
+        "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
+        "pods_simulated": int(r.pods_simulated),
+        "node_evals": int(r.node_evals),
+        "node_prefix": int(r.node_prefix),
+        "chosen": chosen,
+        "decisions": counts,
+        "roofline": {"kernel": "ffd_kernel<SIM>", "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(sim_bytes),
+                     "avg_ms": round(sim_ms, 4), "traffic": None},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_consolidation(problem, merged, args.cpu_sample_sims)
+    solver.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -74,7 +188,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pods", type=int, default=100_000)
     ap.add_argument("--cpu-sample-pods", type=int, default=40_000)
+    ap.add_argument("--c4-nodes", type=int, default=5000)
+    ap.add_argument("--cpu-sample-sims", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-consolidation", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (profiles/)")
     args = ap.parse_args()
 
@@ -82,10 +199,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     dist = None
+    device = None
     if world > 1:
+        import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        if torch.cuda.is_available():
+            # RCCL over xGMI: barriers, the max-over-ranks time and the
+            # consolidation all-gather
+            torch.cuda.set_device(local)
+            device = torch.device("cuda", local)
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     problem = synth.make_cm(n_pods=args.pods, seed=0x5EED0006 + rank)
     solver = Solver(local)
@@ -95,10 +233,6 @@ def main():
     for _ in range(args.warmup):
         solver.run()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     kt = []
     barrier()
     t0 = time.perf_counter()
@@ -106,12 +240,7 @@ def main():
         solver.run()  # synchronous: returns after the stream's last event
         kt.append(solver.last_run_ms())
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     t1 = time.perf_counter()
     out, res = solver.fetch()
@@ -180,6 +309,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample_pods)
     solver.close()
+    if not args.no_consolidation:
+        line["consolidation"] = bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

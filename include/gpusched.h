@@ -293,6 +293,9 @@ typedef struct gs_consolidation_result {
   const uint32_t* multi_options;
   uint32_t pods_simulated; /* sum over simulations of the pods re-solved */
   uint64_t checks;         /* sum over simulations of pod x (existing node + offering) checks */
+  uint64_t node_evals;     /* ExistingNode.CanAdd evaluations the device performed (first-fit scans) */
+  uint64_t node_prefix;    /* node positions a sequential first-fit visits */
+  uint64_t pops;           /* queue pops over all simulations */
   double t_encode_ms, t_upload_ms, t_feas_ms, t_sim_ms, t_truncate_ms, t_fetch_ms;
 } gs_consolidation_result;
 

@@ -109,7 +109,19 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->alloc(d.ov_req, (size_t)sims->blocks * d.ov_cap * gsd::RMAX);
     c->alloc(d.ov_fk, (size_t)sims->blocks * d.ov_cap * F1);
     c->alloc(d.sim_ctrl, NS);
+    c->alloc(d.sim_hdr, NS);
     c->alloc(d.sim_next, 1);
+    d.n_pending = c->n_pending;
+    auto pinned = [&](auto*& dst, size_t n) {
+      void* h = nullptr;
+      HIPCHK(hipHostMalloc(&h, std::max<size_t>(n, 1) * sizeof(*dst), hipHostMallocDefault));
+      c->host_allocs.push_back(h);
+      dst = (std::remove_reference_t<decltype(dst)>)h;
+    };
+    pinned(c->h_ctrl, NS);
+    pinned(c->h_hdr, NS);
+    pinned(c->h_its, NS * 60);
+    pinned(c->h_nits, NS);
   }
   c->commit();
 }

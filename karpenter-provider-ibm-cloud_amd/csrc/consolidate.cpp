@@ -262,10 +262,10 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   const gs_problem* cl = in->cluster;
   auto& d = c->dp;
   const size_t NS = sp.evaluated.size();
-  std::vector<gsd::Ctrl> ctrl(NS);
-  std::vector<gsd::LogRec> log(sp.pods.size());
-  std::vector<uint32_t> queue(sp.pods.size()), its(NS * 60), nits(NS);
-  std::vector<gsd::ClaimRec> hdr(sp.pods.size());
+  const gsd::Ctrl* ctrl = c->h_ctrl;
+  const gsd::ClaimRec* hdr = c->h_hdr;
+  const uint32_t* its = c->h_its;
+  const uint32_t* nits = c->h_nits;
   float a = 0, b = 0, x = 0;
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -292,17 +292,17 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   auto t0 = Clock::now();
   try {
     if (NS) {
-      HIPCHK(hipMemcpy(ctrl.data(), d.sim_ctrl, NS * sizeof(gsd::Ctrl), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(log.data(), d.log, log.size() * sizeof(gsd::LogRec), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(queue.data(), d.queue, queue.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(hdr.data(), d.c_rec, hdr.size() * sizeof(gsd::ClaimRec), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(its.data(), d.c_its, its.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(nits.data(), d.c_nits, nits.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+      // per simulation: control block (NodeClaim count, failed pods), the
+      // single NodeClaim's header and its OrderByPrice/Truncate(60) list
+      HIPCHK(hipMemcpyAsync(c->h_ctrl, d.sim_ctrl, NS * sizeof(gsd::Ctrl), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_hdr, d.sim_hdr, NS * sizeof(gsd::ClaimRec), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_its, d.c_its, NS * 60 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_nits, d.c_nits, NS * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
     }
   } catch (const HipError& ex) {
     return fail(c, GS_E_HIP, ex.msg);
   }
-  const uint32_t np = c->n_pending;
   c->commands.assign(sp.sets.size(), gs_command{});
   c->cmd_options.clear();
   c->cmd_prices.clear();
@@ -310,32 +310,22 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     c->commands[s].decision = GS_DECISION_SKIPPED;
     c->commands[s].n_candidates = (uint32_t)sp.sets[s].size();
   }
-  const gsh::Key& ctk = e.keys[e.k_ct];
-  auto vid_of = [&](const char* v) {
-    auto f = ctk.vocab.id.find(v);
-    return f == ctk.vocab.id.end() ? ctk.vocab.omega : f->second;
-  };
-  const uint32_t v_spot = vid_of("spot"), v_od = vid_of("on-demand");
-  uint64_t checks = 0;
+  uint64_t checks = 0, node_evals = 0, pops = 0, node_prefix = 0;
   for (size_t k = 0; k < NS; k++) {
     const uint32_t s = sp.evaluated[k];
     const gsd::Ctrl& ct = ctrl[k];
     if (ct.status != 0) return fail(c, GS_E_HIP, "simulation kernel reported an internal error");
     const uint32_t q0 = sp.pod_off[k], P = sp.pod_off[k + 1] - q0;
     checks += (uint64_t)P * (e.NN - sp.sets[s].size() + e.checks_per_pod);
+    node_evals += ct.node_evals;
+    node_prefix += ct.node_prefix;
+    pops += ct.pops;
     gs_command& cmd = c->commands[s];
     cmd.decision = GS_DECISION_NOOP;
     cmd.n_new_claims = ct.n_claims;
     // !AllNonPendingPodsScheduled: unplaced non-pending pods, and non-pending
-    // pods placed on uninitialized nodes (SimulateScheduling)
-    uint32_t failed = 0;
-    for (uint32_t i = 0; i < ct.qlen; i++)
-      if (sp.pods[q0 + queue[q0 + (ct.qhead + i) % P]] >= np) failed++;
-    for (uint32_t i = 0; i < ct.n_log; i++) {
-      const gsd::LogRec& l = log[q0 + i];
-      if (!(l.target & 0x80000000u) || l.pod < np) continue;
-      if (!cl->nodes[e.node_order[l.target & 0x7FFFFFFFu]].initialized) failed++;
-    }
+    // pods placed on uninitialized nodes (SimulateScheduling; counted on device)
+    const uint32_t failed = ct.failed;
     cmd.n_failed_pods = failed;
     if (failed) {
       cmd.reason = GS_NOOP_UNSCHEDULABLE;
@@ -362,17 +352,10 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
       continue;
     }
     cmd.candidate_price = cp;
-    // the NodeClaim's requirements: template + every added pod's variant
-    const gsd::ClaimRec& h = hdr[q0];
-    gsh::Reqs creq = e.tmpl_reqs[h.tmpl];
-    for (uint32_t i = 0; i < ct.n_log; i++) {
-      const gsd::LogRec& l = log[q0 + i];
-      if (l.target & 0x80000000u) continue;
-      for (auto& kv : e.variants[l.var].reqs) gsh::reqs_add(e, creq, kv.first, kv.second);
-    }
-    auto ctr = creq.find(e.k_ct);
-    const bool has_spot = ctr == creq.end() || ctr->second.has.test(v_spot);
-    const bool has_od = ctr == creq.end() || ctr->second.has.test(v_od);
+    // the NodeClaim's capacity-type requirement: template AND every added pod
+    const gsd::ClaimRec& h = hdr[k];
+    const bool has_spot = (h.ctb & gsd::CT_SPOT) != 0;
+    const bool has_od = (h.ctb & gsd::CT_OD) != 0;
     if (all_spot && has_spot) {  // SpotToSpotConsolidation disabled
       cmd.reason = GS_NOOP_SPOT_TO_SPOT;
       continue;
@@ -421,6 +404,9 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   out->multi_options = c->multi_opts.data();
   out->pods_simulated = (uint32_t)sp.pods.size();
   out->checks = checks;
+  out->node_evals = node_evals;
+  out->node_prefix = node_prefix;
+  out->pops = pops;
   out->t_encode_ms = c->t_encode;
   out->t_upload_ms = c->t_upload;
   out->t_feas_ms = c->t_feas;

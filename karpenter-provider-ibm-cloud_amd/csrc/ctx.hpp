@@ -89,11 +89,19 @@ struct gs_ctx {
   std::vector<double> cmd_prices;
   std::vector<uint32_t> multi_opts;
   bool cons_ready = false;
+  // pinned per-simulation result staging (allocated with the plan)
+  gsd::Ctrl* h_ctrl = nullptr;
+  gsd::ClaimRec* h_hdr = nullptr;
+  uint32_t* h_its = nullptr;
+  uint32_t* h_nits = nullptr;
   double t_sim = 0;
 
+  std::vector<void*> host_allocs;  // pinned staging buffers (consolidation results)
   void free_all() {
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
+    for (void* p : host_allocs) (void)hipHostFree(p);
+    host_allocs.clear();
   }
   // Device buffers of one prepared problem come from ONE allocation (an arena
   // of 256-B aligned sub-buffers): large pages, few TLB entries for the

@@ -576,6 +576,20 @@ struct Ctx {
       if (it == r.end() || it->second.has.test(e.cat_ct[c])) m |= 1ull << c;
     return m;
   }
+  // CT_SPOT | CT_OD: Requirement.Has("spot") / Has("on-demand") of the
+  // capacity-type key (an absent key is Exists: both); values nobody
+  // mentions behave like omega
+  uint32_t ct_bits(const Reqs& r) {
+    auto f = r.find(e.k_ct);
+    if (f == r.end()) return gsd::CT_SPOT | gsd::CT_OD;
+    const Vocab& v = e.keys[e.k_ct].vocab;
+    auto vid = [&](const char* x) {
+      auto g = v.id.find(x);
+      return g == v.id.end() ? v.omega : g->second;
+    };
+    return (f->second.has.test(vid("spot")) ? gsd::CT_SPOT : 0u) | (f->second.has.test(vid("on-demand")) ? gsd::CT_OD : 0u);
+  }
+
   uint64_t grid(uint64_t zm, uint64_t cm) const {
     uint64_t g = 0;
     for (uint32_t z = 0; z < e.Z; z++)
@@ -716,6 +730,7 @@ struct Ctx {
         if (S(p->taints[np.taints.begin + i].effect) == kPNS) tolerate_pns = true;
       // NewNodeClaim adds hostname In[placeholder]
       reqs_add(e, tr, e.k_hostname, make_kreq(e.keys[e.k_hostname].vocab, GS_OP_IN, {e.keys[e.k_hostname].vocab.omega}, 0));
+      t.ctb = ct_bits(tr);
       e.tmpl.push_back(t);
       e.t_opts.insert(e.t_opts.end(), opts.begin(), opts.end());
       e.tmpl_reqs.push_back(tr);
@@ -840,6 +855,7 @@ struct Ctx {
         }
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
+        vr.ctb = ct_bits(pv.reqs);
         vr.tol = pv.tol;
         vr.tolt = 0;
         for (uint32_t t = 0; t < e.T; t++)
@@ -921,6 +937,7 @@ struct Ctx {
         if (present[r] && nr.avail[r] < 0) nr.ok = 0;  // <U> Fits: negative total never fits
       resvec_fn(g.requests, nr.req, nullptr);
       nr.taints = taint_mask(g.taints);
+      nr.init = g.initialized ? 1u : 0u;
     }
     // taints of nodes enter the vocabulary after the pods' tolerations were
     // encoded: recompute the tolerated masks over the final vocabulary

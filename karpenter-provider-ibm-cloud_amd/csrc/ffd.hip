@@ -43,7 +43,8 @@ struct Shared {
   uint32_t pod, var, stop, M, modkind, modpos, qhead, qlen, epoch, nlog, status, found;
   uint32_t fast_path, modpos_sorted;
   int piv, hint;
-  uint64_t pops, generic, fast, cand, cand_full;
+  uint64_t pops, generic, fast, cand, cand_full, node_evals, node_prefix;
+  uint32_t failed;
   uint64_t t_sort, t_scan, t_tmpl, t0;
   uint64_t dbg[16];
   uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
@@ -768,7 +769,8 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       S.nlog = 0;
       S.nov = ncand;
       S.qoff = qoff;
-      S.pops = S.generic = S.fast = S.cand = S.cand_full = 0;
+      S.pops = S.generic = S.fast = S.cand = S.cand_full = S.node_evals = S.node_prefix = 0;
+      S.failed = 0;
       S.t_sort = S.t_scan = S.t_tmpl = 0;
       for (int q = 0; q < 16; q++) S.dbg[q] = 0;
       S.t0 = wall_clock64();
@@ -899,11 +901,13 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
 
       // --------------- existing nodes in order: first ExistingNode.CanAdd wins
       if (d.NN) {
+        // first-fit: a 64-node window first (the common hit), then full-width
+        // chunks; every chunk ends in one block min over node positions
         uint32_t fn = INF;
-        for (uint32_t base = 0; base < d.NN; base += FB) {
+        for (uint32_t base = 0, width = 64; base < d.NN; base += width, width = FB) {
           const uint32_t n = base + tid;
           bool feas = false;
-          if (n < d.NN) {
+          if (tid < width && n < d.NN) {
             const NodeRec& nr = SIM ? d.nodes0[n] : d.nodes[n];
             const int64_t* nreq = nr.req;
             const FK* nfk = (SIM ? d.n_fk0 : d.n_fk) + (size_t)n * F;
@@ -937,8 +941,10 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
           }
           fn = blk.bmin(feas ? n : INF);
+          if (tid == 0) S.node_evals += d.NN - base < width ? d.NN - base : width;
           if (fn != INF) break;
         }
+        if (tid == 0) S.node_prefix += fn != INF ? fn + 1 : d.NN;
         if (fn != INF) {
           // ExistingNode.Add: requests and requirements
           int64_t* areq;
@@ -1293,6 +1299,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
             s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
             cr->zm &= vr.zm;
             cr->cm &= vr.cm;
+            cr->ctb &= vr.ctb;
             cr->count++;
             FK* cf = dd.c_fk + (size_t)(cb + j) * F;
             for (uint32_t k = 0; k < vr.fk_count; k++) {
@@ -1394,6 +1401,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
           cr->count = 1;
           cr->zm = tr.zm & vr.zm;
           cr->cm = tr.cm & vr.cm;
+          cr->ctb = tr.ctb & vr.ctb;
           FK* cf = d.c_fk + (size_t)(cbase + j) * F;
           for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
           for (uint32_t k = 0; k < vr.fk_count; k++) {
@@ -1476,6 +1484,23 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
     __syncthreads();
     if (!SIM)
       for (uint32_t i = tid; i < S.M; i += FB) d.c_sorted[i] = s_ord[i];
+    if (SIM) {
+      // SimulateScheduling's error pods that are not pending: still queued,
+      // or placed on an uninitialized existing node
+      uint32_t cnt = 0;
+      for (uint32_t i = tid; i < S.qlen; i += FB) {
+        uint32_t slot = S.qhead + i;
+        if (slot >= P) slot -= P;
+        cnt += gpod(queue[slot]) >= d.n_pending ? 1u : 0u;
+      }
+      for (uint32_t i = tid; i < S.nlog; i += FB) {
+        const LogRec l = logp[i];
+        cnt += ((l.target & 0x80000000u) && l.pod >= d.n_pending && !d.nodes0[l.target & 0x7FFFFFFFu].init) ? 1u : 0u;
+      }
+      cnt = wave_sum_u32(cnt);
+      if (lane == 0 && cnt) atomicAdd(&S.failed, cnt);
+      __syncthreads();
+    }
     if (tid == 0) {
       Ctrl c;
       c.status = S.status;
@@ -1489,6 +1514,10 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
       c.fast_sorts = S.fast;
       c.cand_evals = S.cand;
       c.cand_full = S.cand_full;
+      c.node_evals = S.node_evals;
+      c.node_prefix = S.node_prefix;
+      c.failed = S.failed;
+      c.pad = 0;
       c.t_sort = S.t_sort;
       c.t_scan = S.t_scan;
       c.t_tmpl = S.t_tmpl;

@@ -164,6 +164,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
     }
   }
   const uint32_t take = n < 60 ? n : 60;
+  if (d.n_sims && tid < sizeof(ClaimRec) / 4) ((uint32_t*)(d.sim_hdr + o))[tid] = ((const uint32_t*)&h)[tid];
   for (uint32_t i = tid; i < take; i += BLOCK) d.c_its[(size_t)o * 60 + i] = d.rank_to_it[(uint32_t)keys[i]];
   if (tid == 0) d.c_nits[o] = take;
 }

@@ -23,6 +23,8 @@ constexpr uint32_t THR_LDS_MAX = 2048;   // fit thresholds staged in the FFD ker
 constexpr uint32_t SLOT_LDS_MAX = 1024;  // (zone, capacity-type) pair type-set words in LDS
 constexpr int SMAX = 16;       // offerings per instance type
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+// capacity-type requirement bits (consolidation's spot-to-spot rule)
+enum : uint32_t { CT_SPOT = 1u, CT_OD = 2u };
 
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)
@@ -45,7 +47,7 @@ struct FKEntry {
 struct VarRec {
   uint32_t pod;
   uint32_t fk_begin, fk_count;
-  uint32_t pad;
+  uint32_t ctb;                  // CT_SPOT | CT_OD: capacity-type requirement Has(spot) / Has(on-demand)
   uint32_t itmask_off[KMAX_IT];  // word offset into itmask arena, NONE = unconstrained
   uint32_t zfull_off, cfull_off; // full-vocabulary zone / capacity-type masks (existing nodes)
   uint64_t zm, cm;               // Has over catalog zones / capacity types
@@ -57,7 +59,7 @@ struct TmplRec {
   uint32_t np_index;
   uint32_t has_limits;
   uint32_t limit_rmask;  // resources present in the remaining-limits map
-  uint32_t pad;
+  uint32_t ctb;          // CT_SPOT | CT_OD of the template requirements
   uint64_t zm, cm;       // template Has over catalog zones / capacity types
   uint64_t taints;       // taint-vocabulary mask
   int64_t daemon[RMAX];
@@ -76,7 +78,8 @@ struct alignas(64) ClaimRec {
   // resources 4..7
   int64_t tot_hi[RMAX - 4];
   uint16_t thr_hi[RMAX - 4];
-  uint32_t pad[6];
+  uint32_t ctb;          // CT_SPOT | CT_OD of the claim requirements (template AND pods)
+  uint32_t pad[5];
   int64_t maxa[RMAX];    // max allocatable over the claim's initial options (slack bound)
   __host__ __device__ int64_t& tot(uint32_t r) { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
   __host__ __device__ int64_t tot(uint32_t r) const { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
@@ -94,7 +97,7 @@ struct NodeRec {
   uint32_t ok;           // 0 if any available quantity is negative (never fits)
   uint32_t zvid, cvid;   // zone / capacity-type label value ids (NONE = unlabeled)
   uint32_t vid[KMAX_IT]; // instance-type-key label value ids (NONE = unlabeled)
-  uint32_t pad;
+  uint32_t init;         // StateNode.Initialized()
 };
 
 // add-log entry: pod popped & placed, in order
@@ -113,6 +116,10 @@ struct Ctrl {
   uint64_t generic_sorts, fast_sorts;
   uint64_t cand_evals;   // in-flight NodeClaim candidates scored
   uint64_t cand_full;    // candidates that passed the slack prefilter
+  uint64_t node_evals;   // existing-node ExistingNode.CanAdd evaluations (whole scan chunks)
+  uint64_t node_prefix;  // node positions a sequential first-fit visits (found index + 1, or all)
+  uint32_t failed;       // simulations: non-pending pods unplaced or placed on uninitialized nodes
+  uint32_t pad;
   uint64_t t_sort, t_scan, t_tmpl, t_total;  // wall_clock64 ticks (100 MHz) per phase
   uint64_t dbg[16];                            // diagnostic phase counters
 };
@@ -185,7 +192,7 @@ struct DevProblem {
   uint32_t n_sims;
   uint32_t ov_cap;             // overlay entries per block (candidates + pods of a simulation)
   uint32_t nb_words;           // ceil(NN / 32): LDS touched-node bitmap
-  uint32_t pad_sim;
+  uint32_t n_pending;          // pod ids < n_pending are pending (their errors do not count)
   const uint32_t* sim_pod_off; // [n_sims + 1]
   const uint32_t* sim_pods;    // pod ids, queue order within each simulation
   const uint32_t* sim_cand_off;// [n_sims + 1]
@@ -193,6 +200,7 @@ struct DevProblem {
   int64_t* ov_req;             // [grid][ov_cap][RMAX]
   FK* ov_fk;                   // [grid][ov_cap][F]
   Ctrl* sim_ctrl;              // [n_sims]
+  ClaimRec* sim_hdr;           // [n_sims] header of the single NodeClaim (trunc_kernel copies it)
   uint32_t* sim_next;          // work counter (reset before each launch)
 };
 

@@ -197,6 +197,9 @@ class GsConsolidationResult(C.Structure):
         ("multi_options", C.POINTER(C.c_uint32)),
         ("pods_simulated", _U32),
         ("checks", C.c_uint64),
+        ("node_evals", C.c_uint64),
+        ("node_prefix", C.c_uint64),
+        ("pops", C.c_uint64),
         ("t_encode_ms", C.c_double), ("t_upload_ms", C.c_double), ("t_feas_ms", C.c_double),
         ("t_sim_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
     ]

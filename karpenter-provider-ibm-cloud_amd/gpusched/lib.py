@@ -169,9 +169,13 @@ class Solver:
         self._check(self.L.gs_consolidate(self.ctx, C.byref(cin.struct), C.byref(res)))
         return abi.commands_to_list(res), int(res.chosen), _multi(res), res
 
-    def consolidate_rerun(self):
+    def consolidate_rerun(self, raw=False):
+        """re-run the device simulations on the resident input; raw=True
+        returns only the gs_consolidation_result (no Python-side copy)"""
         res = abi.GsConsolidationResult()
         self._check(self.L.gs_consolidate_rerun(self.ctx, C.byref(res)))
+        if raw:
+            return res
         return abi.commands_to_list(res), int(res.chosen), _multi(res), res
 
     def feasibility(self):
