@@ -52,6 +52,13 @@ def algorithmic_bytes(res, problem, n_claims):
     return {"feas": feas, "ffd": ffd, "trunc": trunc}
 
 
+def load_traffic(path):
+    """{kernel: HBM bytes per launch} from the committed PMC profile (null when absent)"""
+    if not path or not os.path.exists(path):
+        return {}
+    return {k: v["bytes"] for k, v in json.load(open(path)).items()}
+
+
 def node_check_bytes(R, K=4):
     """algorithmic bytes of one ExistingNode.CanAdd: available + requests (R x i64),
     taints (8), ok flag (4), K label value ids (4 each), zone/capacity-type ids (8)"""
@@ -172,7 +179,7 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
         "decisions": counts,
         "roofline": {"kernel": "ffd_kernel<SIM>", "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(sim_bytes),
-                     "avg_ms": round(sim_ms, 4), "traffic": None},
+                     "avg_ms": round(sim_ms, 4), "traffic": load_traffic(args.traffic_json).get("sim")},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -192,7 +199,8 @@ def main():
     ap.add_argument("--cpu-sample-sims", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (profiles/)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output, committed under profiles/)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -255,9 +263,7 @@ def main():
     ab = algorithmic_bytes(res, problem, len(out["claims"]))
     kms = {"feas": feas_ms, "ffd": ffd_ms, "trunc": trunc_ms}
     dom = max(kms, key=kms.get)
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get(dom)
+    traffic = load_traffic(args.traffic_json)
 
     def roof(k):
         ach = ab[k] / (kms[k] * 1e-3) / 1e9
@@ -266,7 +272,7 @@ def main():
                 "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": ab[k], "avg_ms": round(kms[k], 4)}
 
     roofline = roof(dom)
-    roofline["traffic"] = traffic
+    roofline["traffic"] = traffic.get(dom)
     line = {
         "metric": METRIC,
         "value": value,
@@ -303,7 +309,7 @@ def main():
                          "template": round(res.t_ffd_template_ms, 2)},
         "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
         "roofline": roofline,
-        "roofline_feasibility_kernel": roof("feas"),
+        "roofline_feasibility_kernel": dict(roof("feas"), traffic=traffic.get("feas")),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

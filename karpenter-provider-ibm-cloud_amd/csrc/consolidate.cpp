@@ -241,16 +241,18 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     *err = "a simulation holds more than 65535 pods";
     return GS_E_CAPACITY;
   }
-  int cus = 256;
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  // persistent workgroups draining the simulation counter: up to 2 per CU
-  sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * 2);
   const uint32_t lds = gsk_ffd_lds_bytes(std::max<uint32_t>(sp.max_pods, 1), (uint32_t)e.thr_val.size(),
                                          (e.NN + 31) / 32, std::max<uint32_t>(sp.ov_cap, 1));
   if (lds > gsk_ffd_dyn_lds_max()) {
     *err = "simulation exceeds the workgroup LDS (pods per simulation or state nodes)";
     return GS_E_CAPACITY;
   }
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  // persistent workgroups draining the simulation counter: as many as stay
+  // resident (occupancy of the simulation kernel at this LDS size)
+  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds);
+  sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
   return GS_OK;
 }
 

@@ -27,8 +27,9 @@ using namespace gsd;
 
 namespace {
 
-constexpr int FB = 1024;
-constexpr int NWAVE = FB / 64;
+constexpr int FB_MAX = 1024;  // workgroup size of the provisioning Solve
+constexpr int FB_SIM = 256;   // workgroup size of one consolidation simulation
+constexpr int NWAVE_MAX = FB_MAX / 64;
 constexpr int SEQ_SORT = 128;  // subranges up to this length sort on thread 0
 
 constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
@@ -48,7 +49,7 @@ struct Shared {
   uint64_t t_sort, t_scan, t_tmpl, t0;
   uint64_t dbg[16];
   uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
-  uint32_t red[2][NWAVE];
+  uint32_t red[2][NWAVE_MAX];
   unsigned long long red64[RMAX];
   Frame stk[48];
   // next-pod pipeline: wave 1 prefetches the next pop during the current pod
@@ -304,7 +305,10 @@ struct SeqSort {
 };
 
 // ------------------------------------------------------------ block-parallel
+template <uint32_t NT>
 struct Blk {
+  static constexpr int FB = (int)NT;
+  static constexpr int NWAVE = (int)NT / 64;
   uint16_t* sc;
   uint16_t* ord;
   uint16_t* scr;  // >= max_claims entries
@@ -684,8 +688,9 @@ __device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa,
 //    bitmap + overlay ids, global req/FK copies per block).
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
 
-template <uint32_t RR, bool SIM>
-__global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
+template <uint32_t RR, bool SIM, uint32_t NT>
+__global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
+  constexpr uint32_t FB = NT;  // threads of this workgroup
   extern __shared__ uint64_t lds64[];
   __shared__ Shared S;
   const uint32_t MC = d.max_claims;  // LDS claim capacity (SIM: the largest simulation's pod count)
@@ -706,7 +711,7 @@ __global__ __launch_bounds__(FB) void ffd_kernel(DevProblem d) {
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
-  Blk blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
+  Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
 
   for (uint32_t i = tid; i < nthr + 4; i += FB) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
@@ -1542,12 +1547,13 @@ static uint32_t g_ffd_dyn_max = 0;
 
 template <uint32_t RR, bool SIM>
 static hipError_t ffd_attr(uint32_t lds_total) {
+  constexpr uint32_t NT = SIM ? FB_SIM : FB_MAX;
   hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM>);
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM, NT>);
   if (e != hipSuccess) return e;
   const uint32_t dyn = lds_total > a.sharedSizeBytes ? lds_total - (uint32_t)a.sharedSizeBytes : 0;
   if (!g_ffd_dyn_max || dyn < g_ffd_dyn_max) g_ffd_dyn_max = dyn;
-  return hipFuncSetAttribute((const void*)ffd_kernel<RR, SIM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  return hipFuncSetAttribute((const void*)ffd_kernel<RR, SIM, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
 }
 
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
@@ -1565,6 +1571,19 @@ extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
 // dynamic LDS available to every ffd_kernel instantiation (after gsk_init_ffd)
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void) { return g_ffd_dyn_max; }
 
+// resident simulation workgroups per CU for a given dynamic LDS size
+extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds) {
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (R) {
+#define GSK_OCC(k) \
+  case k: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM>, FB_SIM, lds); break;
+    GSK_OCC(1) GSK_OCC(2) GSK_OCC(3) GSK_OCC(4) GSK_OCC(5) GSK_OCC(6) GSK_OCC(7) GSK_OCC(8)
+#undef GSK_OCC
+  }
+  return e == hipSuccess && n > 0 ? (uint32_t)n : 1u;
+}
+
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
@@ -1573,8 +1592,8 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   const bool sim = d->n_sims > 0;
   switch (d->R * 2 + (sim ? 1 : 0)) {
 #define GSK_CASE(n)                                                                            \
-  case 2 * n: hipLaunchKernelGGL((ffd_kernel<n, false>), dim3(1), dim3(FB), lds, s, *d); break; \
-  case 2 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, true>), dim3(blocks), dim3(FB), lds, s, *d); break;
+  case 2 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
+  case 2 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

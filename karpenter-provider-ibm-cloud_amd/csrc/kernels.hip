@@ -35,10 +35,12 @@ constexpr int BLOCK = 256;
 // make a later pod compatible.
 extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t pair = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  // wave-uniform in SGPRs: the variant record is read in place (scalar
+  // loads), never copied into a dynamically indexed private array (scratch)
+  const uint32_t pair = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
   if (pair >= d.V * d.T) return;  // wave-uniform
   const uint32_t v = pair / d.T, t = pair % d.T;
-  const VarRec vr = d.vars[v];
+  const VarRec& vr = d.vars[v];
   const TmplRec& tr = d.tmpl[t];
   uint64_t* rowout = d.rows + (size_t)pair * d.OW;
 

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+(tools/profile_round.sh), corrected as MI355X_MICROARCH.md "HBM" prescribes:
+FETCH_SIZE reports half the bytes of a wide coalesced read on gfx950 (x2);
+WRITE_SIZE is read as is; both are in KiB.  Writes {kernel: bytes per launch}
+for the bench's kernels: ffd (provisioning ffd_kernel), sim (consolidation
+ffd_kernel), feas, trunc.
+
+usage: tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> > traffic.json
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def kernel_key(name):
+    if name.startswith("void ffd_kernel"):
+        return "sim" if ", true," in name else "ffd"
+    if name.startswith("feas_kernel"):
+        return "feas"
+    if name.startswith("trunc_kernel"):
+        return "trunc"
+    return None
+
+
+def per_launch(path, counter):
+    """bench.py order: the provisioning Solve (feas, ffd, trunc) runs before
+    the consolidation sweep, so feas/trunc launches after the first simulation
+    launch belong to the sweep (keys feas_sim, trunc_sim)"""
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+    vals = collections.defaultdict(list)
+    seen_sim = False
+    for r in rows:
+        k = kernel_key(r["Kernel_Name"])
+        if k == "sim":
+            seen_sim = True
+        if k in ("feas", "trunc") and (seen_sim or any(kernel_key(x["Kernel_Name"]) == "sim" and
+                                                       int(x["Dispatch_Id"]) == int(r["Dispatch_Id"]) + 1 for x in rows)):
+            k += "_sim"
+        if k and r["Counter_Name"] == counter:
+            vals[k].append(float(r["Counter_Value"]) * 1024.0)
+    return vals
+
+
+def main(fetch_csv, write_csv):
+    f = per_launch(fetch_csv, "FETCH_SIZE")
+    w = per_launch(write_csv, "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(f) | set(w)):
+        fb = sum(f[k]) / len(f[k]) if f[k] else 0.0
+        wb = sum(w[k]) / len(w[k]) if w[k] else 0.0
+        out[k] = {"bytes": int(2 * fb + wb), "fetch_bytes_x2": int(2 * fb), "write_bytes": int(wb),
+                  "launches": [len(f[k]), len(w[k])]}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
