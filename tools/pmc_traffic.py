@@ -26,19 +26,19 @@ def kernel_key(name):
 
 def per_launch(path, counter):
     """bench.py order: the provisioning Solve (feas, ffd, trunc) runs before
-    the consolidation sweep, so feas/trunc launches after the first simulation
-    launch belong to the sweep (keys feas_sim, trunc_sim)"""
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+    the consolidation sweep; a feas launch whose next kernel is a simulation
+    launch, and every trunc launch right after one, belong to the sweep
+    (keys feas_sim, trunc_sim)"""
+    rows = [r for r in sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+            if kernel_key(r["Kernel_Name"])]
     vals = collections.defaultdict(list)
-    seen_sim = False
-    for r in rows:
+    for i, r in enumerate(rows):
         k = kernel_key(r["Kernel_Name"])
-        if k == "sim":
-            seen_sim = True
-        if k in ("feas", "trunc") and (seen_sim or any(kernel_key(x["Kernel_Name"]) == "sim" and
-                                                       int(x["Dispatch_Id"]) == int(r["Dispatch_Id"]) + 1 for x in rows)):
-            k += "_sim"
-        if k and r["Counter_Name"] == counter:
+        if k == "feas" and i + 1 < len(rows) and kernel_key(rows[i + 1]["Kernel_Name"]) == "sim":
+            k = "feas_sim"
+        if k == "trunc" and i > 0 and kernel_key(rows[i - 1]["Kernel_Name"]) == "sim":
+            k = "trunc_sim"
+        if r["Counter_Name"] == counter:
             vals[k].append(float(r["Counter_Value"]) * 1024.0)
     return vals
 
