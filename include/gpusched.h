@@ -140,7 +140,24 @@ typedef struct gs_nodepool {
   gs_range instance_types;  /* into it_refs: GetInstanceTypes(nodePool) in order */
 } gs_nodepool;
 
-/* a pending pod; requests = resources.RequestsForPods(pod) (incl. pods=1) */
+/* corev1.TopologySpreadConstraint (<U> karpenter Topology: spread groups on
+ * topology.kubernetes.io/zone or kubernetes.io/hostname; other keys, a
+ * Honor nodeTaintsPolicy and matchLabelKeys are refused) */
+enum { GS_SPREAD_DO_NOT_SCHEDULE = 0, GS_SPREAD_SCHEDULE_ANYWAY = 1 };
+enum { GS_POLICY_HONOR = 0, GS_POLICY_IGNORE = 1 };
+typedef struct gs_spread {
+  uint32_t topology_key;         /* string id */
+  int32_t max_skew;              /* >= 1 */
+  uint32_t when_unsatisfiable;   /* GS_SPREAD_* */
+  int32_t min_domains;           /* <= 0: unset */
+  uint32_t has_selector;         /* 0: nil labelSelector (selects no pod) */
+  gs_range match_labels;         /* into labels */
+  gs_range match_expressions;    /* into reqs: In / NotIn / Exists / DoesNotExist over pod labels */
+  uint32_t node_affinity_policy; /* GS_POLICY_HONOR (default) or GS_POLICY_IGNORE */
+  uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is refused */
+} gs_spread;
+
+/* a pod; requests = resources.RequestsForPods(pod) (incl. pods=1) */
 typedef struct gs_pod {
   uint32_t uid;             /* string id */
   int64_t creation_ns;      /* metadata.creationTimestamp (ns) */
@@ -150,6 +167,9 @@ typedef struct gs_pod {
   gs_range preferred_terms; /* into terms: preferredDuringScheduling, with weights */
   gs_range tolerations;     /* into tolerations */
   uint32_t flags;           /* GS_POD_* */
+  uint32_t ns;              /* metadata.namespace (string id) */
+  gs_range labels;          /* metadata.labels, into labels (topology selectors) */
+  gs_range spreads;         /* spec.topologySpreadConstraints, into spreads */
 } gs_pod;
 
 /* an existing (state) node: ExistingNode inputs */
@@ -175,8 +195,13 @@ typedef struct gs_problem {
   const gs_offering* offerings; uint32_t n_offerings;
   const gs_instance_type* instance_types; uint32_t n_instance_types;
   const gs_nodepool* nodepools; uint32_t n_nodepools;
-  const gs_pod* pods; uint32_t n_pods;
+  const gs_pod* pods; uint32_t n_pods;       /* pending pods (the Solve's pods) */
   const gs_node* nodes; uint32_t n_nodes;
+  const gs_spread* spreads; uint32_t n_spreads;
+  /* pods bound to state nodes: counted by topology spread selectors; the
+   * reschedulable ones are what consolidation simulations move */
+  const gs_pod* bound_pods; uint32_t n_bound_pods;
+  const uint32_t* bound_pod_node;             /* [n_bound_pods] index into nodes */
 } gs_problem;
 
 /* Results.TruncateInstanceTypes(60) of Scheduler.Solve */
@@ -257,10 +282,8 @@ enum {
 };
 
 typedef struct gs_consolidation {
-  const gs_problem* cluster;        /* catalog, NodePools, ACTIVE state nodes, PENDING pods */
-  const gs_pod* bound_pods;         /* reschedulable pods bound to state nodes; their ranges index the */
-  uint32_t n_bound_pods;            /*   cluster's arrays (strings, quantities, labels, terms, ...) */
-  const uint32_t* bound_pod_node;   /* [n_bound_pods] index into cluster->nodes */
+  const gs_problem* cluster;        /* catalog, NodePools, ACTIVE state nodes, PENDING pods and the
+                                       reschedulable bound pods (cluster->bound_pods) */
   const uint32_t* candidates;       /* candidate node indices, disruption order (sortCandidates) */
   uint32_t n_candidates;
   const gs_range* sets;             /* GS_CONSOLIDATE_EVAL: candidate sets, ranges into candidates[] */

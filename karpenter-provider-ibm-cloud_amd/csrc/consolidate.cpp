@@ -213,7 +213,8 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   std::iota(pend.begin(), pend.end(), 0);
   std::sort(pend.begin(), pend.end(), [&](uint32_t a, uint32_t b) { return rank[a] < rank[b]; });
   std::vector<std::vector<uint32_t>> bound_by_node(e.NN);
-  for (uint32_t b = 0; b < in->n_bound_pods; b++) bound_by_node[in->bound_pod_node[b]].push_back(np + b);
+  const gs_problem* cl = in->cluster;
+  for (uint32_t b = 0; b < cl->n_bound_pods; b++) bound_by_node[cl->bound_pod_node[b]].push_back(np + b);
   sp.pod_off.assign(1, 0);
   sp.pods.clear();
   sp.cand_off.assign(1, 0);
@@ -429,8 +430,12 @@ gs_status check_input(const gs_consolidation* in, std::string* err) {
       *err = "candidate node index out of range";
       return GS_E_INVALID;
     }
-  for (uint32_t i = 0; i < in->n_bound_pods; i++)
-    if (in->bound_pod_node[i] >= p->n_nodes) {
+  if (p->n_bound_pods && !p->bound_pod_node) {
+    *err = "bound pods without their nodes";
+    return GS_E_INVALID;
+  }
+  for (uint32_t i = 0; i < p->n_bound_pods; i++)
+    if (p->bound_pod_node[i] >= p->n_nodes) {
       *err = "bound pod node index out of range";
       return GS_E_INVALID;
     }
@@ -456,20 +461,22 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   c->prepared = c->ran = false;
   // own copies of the caller's candidate arrays (gs_consolidate_rerun)
   c->cons_cands.assign(in->candidates, in->candidates + in->n_candidates);
-  c->cons_bound_node.assign(in->bound_pod_node, in->bound_pod_node + in->n_bound_pods);
   c->cons_sets.assign(in->sets, in->sets + (in->mode == GS_CONSOLIDATE_EVAL ? in->n_sets : 0));
   c->cons_in = *in;
   c->cons_in.candidates = c->cons_cands.data();
-  c->cons_in.bound_pod_node = c->cons_bound_node.data();
   c->cons_in.sets = c->cons_sets.data();
   // the combined pod list: pending pods, then every bound pod
   const gs_problem* cl = in->cluster;
   c->n_pending = cl->n_pods;
   c->cons_pods.assign(cl->pods, cl->pods + cl->n_pods);
-  c->cons_pods.insert(c->cons_pods.end(), in->bound_pods, in->bound_pods + in->n_bound_pods);
+  c->cons_pods.insert(c->cons_pods.end(), cl->bound_pods, cl->bound_pods + cl->n_bound_pods);
   c->cons_problem = *cl;
   c->cons_problem.pods = c->cons_pods.data();
   c->cons_problem.n_pods = (uint32_t)c->cons_pods.size();
+  c->cons_problem.bound_pods = nullptr;  // every bound pod is in the combined pod list
+  c->cons_problem.n_bound_pods = 0;
+  c->cons_problem.bound_pod_node = nullptr;
+  if (cl->n_spreads) return fail(c, GS_E_UNSUPPORTED, "topology spread constraints in consolidation simulations");
   c->problem = &c->cons_problem;
   auto t0 = Clock::now();
   gsh::Err er = gsh::encode(&c->cons_problem, c->enc);

@@ -81,7 +81,7 @@ struct gs_ctx {
   std::vector<gs_pod> cons_pods;
   gs_problem cons_problem{};
   gs_consolidation cons_in{};
-  std::vector<uint32_t> cons_cands, cons_bound_node;
+  std::vector<uint32_t> cons_cands;
   std::vector<gs_range> cons_sets;
   uint32_t n_pending = 0;
   gsc::SimPlan sims;

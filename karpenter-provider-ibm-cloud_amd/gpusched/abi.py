@@ -40,7 +40,13 @@ DT_NODEPOOL = np.dtype([("name", "<u4"), ("weight", "<i4"), ("requirements", RAN
                         ("daemon_requests", RANGE), ("instance_types", RANGE)], align=True)
 DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), ("node_selector", RANGE),
                    ("required_terms", RANGE), ("preferred_terms", RANGE), ("tolerations", RANGE),
-                   ("flags", "<u4")], align=True)
+                   ("flags", "<u4"), ("ns", "<u4"), ("labels", RANGE), ("spreads", RANGE)], align=True)
+SPREAD_DO_NOT_SCHEDULE, SPREAD_SCHEDULE_ANYWAY = 0, 1
+POLICY_HONOR, POLICY_IGNORE = 0, 1
+DT_SPREAD = np.dtype([("topology_key", "<u4"), ("max_skew", "<i4"), ("when_unsatisfiable", "<u4"),
+                      ("min_domains", "<i4"), ("has_selector", "<u4"), ("match_labels", RANGE),
+                      ("match_expressions", RANGE), ("node_affinity_policy", "<u4"),
+                      ("node_taints_policy", "<u4")], align=True)
 DT_NODE = np.dtype([("name", "<u4"), ("initialized", "<u4"), ("labels", RANGE), ("taints", RANGE),
                     ("available", RANGE), ("requests", RANGE)], align=True)
 
@@ -64,6 +70,9 @@ class GsProblem(C.Structure):
         ("nodepools", _P), ("n_nodepools", _U32),
         ("pods", _P), ("n_pods", _U32),
         ("nodes", _P), ("n_nodes", _U32),
+        ("spreads", _P), ("n_spreads", _U32),
+        ("bound_pods", _P), ("n_bound_pods", _U32),
+        ("bound_pod_node", _P),
     ]
 
 
@@ -169,8 +178,6 @@ class GsRange(C.Structure):
 class GsConsolidation(C.Structure):
     _fields_ = [
         ("cluster", C.POINTER(GsProblem)),
-        ("bound_pods", _P), ("n_bound_pods", _U32),
-        ("bound_pod_node", _P),
         ("candidates", _P), ("n_candidates", _U32),
         ("sets", _P), ("n_sets", _U32),
         ("mode", _U32), ("max_candidates", _U32),

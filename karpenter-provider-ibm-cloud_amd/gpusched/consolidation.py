@@ -30,10 +30,6 @@ class ConsolidationInput:
         self.struct = abi.GsConsolidation()
         st = self.struct
         st.cluster = C.pointer(problem.struct)
-        bp, bn = problem.bound_pods, problem.bound_node
-        st.bound_pods = bp.ctypes.data if len(bp) else None
-        st.n_bound_pods = len(bp)
-        st.bound_pod_node = bn.ctypes.data if len(bn) else None
         st.candidates = self.candidates.ctypes.data if len(self.candidates) else None
         st.n_candidates = len(self.candidates)
         st.sets = self.sets.ctypes.data if len(self.sets) else None

@@ -33,8 +33,9 @@ class ProblemBuilder:
         self.nodepools = []
         self.pods = []
         self.nodes = []
-        self.bound_pods = []  # reschedulable pods bound to state nodes (consolidation)
+        self.bound_pods = []  # pods bound to state nodes (topology counts; consolidation moves them)
         self.bound_node = []
+        self.spreads = []
 
     # ------------------------------------------------------------ primitives
     def s(self, x: str) -> int:
@@ -113,20 +114,43 @@ class ProblemBuilder:
                                self._qty(daemon or {}), (rb, len(self.it_refs) - rb)))
         return len(self.nodepools) - 1
 
+    def _spreads(self, spreads):
+        """spreads: dicts with key, max_skew, when ("DoNotSchedule"|"ScheduleAnyway"),
+        selector (None = nil, else {"labels": {...}, "exprs": [(key, op, values)]}),
+        min_domains, node_affinity_policy ("Honor"|"Ignore"), node_taints_policy"""
+        b = len(self.spreads)
+        for sp in spreads:
+            sel = sp.get("selector")
+            ml = self._labels((sel or {}).get("labels", {}))
+            me = self._reqs((sel or {}).get("exprs", []))
+            self.spreads.append((self.s(sp["key"]), int(sp.get("max_skew", 1)),
+                                 abi.SPREAD_SCHEDULE_ANYWAY if sp.get("when") == "ScheduleAnyway"
+                                 else abi.SPREAD_DO_NOT_SCHEDULE,
+                                 int(sp.get("min_domains", 0)), 0 if sel is None else 1, ml, me,
+                                 abi.POLICY_IGNORE if sp.get("node_affinity_policy") == "Ignore" else abi.POLICY_HONOR,
+                                 abi.POLICY_HONOR if sp.get("node_taints_policy") == "Honor" else abi.POLICY_IGNORE))
+        return (b, len(self.spreads) - b)
+
+    def _pod(self, uid, creation_ns, requests, node_selector, required_terms, preferred_terms, tolerations, flags,
+             namespace, labels, spreads):
+        return (self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
+                self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
+                self._tols(tolerations), int(flags), self.s(namespace), self._labels(labels or {}),
+                self._spreads(spreads))
+
     def add_pod(self, uid, creation_ns, requests, node_selector=None, required_terms=(), preferred_terms=(),
-                tolerations=(), flags=0):
+                tolerations=(), flags=0, namespace="default", labels=None, spreads=()):
         """required_terms: list of reqs lists; preferred_terms: list of (weight, reqs)"""
-        self.pods.append((self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
-                          self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
-                          self._tols(tolerations), int(flags)))
+        self.pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
+                                   tolerations, flags, namespace, labels, spreads))
         return len(self.pods) - 1
 
     def add_bound_pod(self, node, uid, creation_ns, requests, node_selector=None, required_terms=(),
-                      preferred_terms=(), tolerations=(), flags=0):
-        """a reschedulable pod bound to state node `node` (disruption candidates' pods)"""
-        self.bound_pods.append((self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
-                                self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
-                                self._tols(tolerations), int(flags)))
+                      preferred_terms=(), tolerations=(), flags=0, namespace="default", labels=None, spreads=()):
+        """a pod bound to state node `node` (counted by topology selectors;
+        consolidation reschedules the candidates' pods)"""
+        self.bound_pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
+                                         tolerations, flags, namespace, labels, spreads))
         self.bound_node.append(int(node))
         return len(self.bound_pods) - 1
 
@@ -168,15 +192,17 @@ class Problem:
         self.nodes = _np(b.nodes, abi.DT_NODE)
         self.bound_pods = _np(b.bound_pods, abi.DT_POD)
         self.bound_node = np.asarray(b.bound_node, dtype=np.uint32)
+        self.spreads = _np(b.spreads, abi.DT_SPREAD)
         self.struct = abi.GsProblem()
         st = self.struct
         st.strings = self._cstrs
         st.n_strings = len(self._bytes)
         for name in ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
-                     "offerings", "instance_types", "nodepools", "pods", "nodes"):
+                     "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods"):
             arr = getattr(self, name)
             setattr(st, name, arr.ctypes.data if len(arr) else None)
             setattr(st, "n_" + name, len(arr))
+        st.bound_pod_node = self.bound_node.ctypes.data if len(self.bound_node) else None
 
     @property
     def n_pods(self):

@@ -1076,16 +1076,31 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
   vector<gs_pod> pods(cl->pods, cl->pods + cl->n_pods);
   const uint32_t n_pending = cl->n_pods;
   for (uint32_t c : cands)
-    for (uint32_t b = 0; b < in->n_bound_pods; b++)
-      if (in->bound_pod_node[b] == c) pods.push_back(in->bound_pods[b]);
+    for (uint32_t b = 0; b < cl->n_bound_pods; b++)
+      if (cl->bound_pod_node[b] == c) pods.push_back(cl->bound_pods[b]);
   vector<gs_node> nodes;
+  vector<uint32_t> new_index(cl->n_nodes, UINT32_MAX);
   for (uint32_t n = 0; n < cl->n_nodes; n++)
-    if (!cset.count(n)) nodes.push_back(cl->nodes[n]);
+    if (!cset.count(n)) {
+      new_index[n] = (uint32_t)nodes.size();
+      nodes.push_back(cl->nodes[n]);
+    }
+  // the other bound pods stay where they are (topology counts)
+  vector<gs_pod> bound;
+  vector<uint32_t> bound_node;
+  for (uint32_t b = 0; b < cl->n_bound_pods; b++)
+    if (!cset.count(cl->bound_pod_node[b])) {
+      bound.push_back(cl->bound_pods[b]);
+      bound_node.push_back(new_index[cl->bound_pod_node[b]]);
+    }
   gs_problem sub = *cl;
   sub.pods = pods.data();
   sub.n_pods = (uint32_t)pods.size();
   sub.nodes = nodes.data();
   sub.n_nodes = (uint32_t)nodes.size();
+  sub.bound_pods = bound.data();
+  sub.n_bound_pods = (uint32_t)bound.size();
+  sub.bound_pod_node = bound_node.data();
   OracleState st;
   Builder b{&sub, st};
   b.build();
@@ -1199,8 +1214,9 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
     b.build();
     for (uint32_t i = 0; i < in->n_candidates; i++)
       if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
-    for (uint32_t i = 0; i < in->n_bound_pods; i++)
-      if (in->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
+    for (uint32_t i = 0; i < in->cluster->n_bound_pods; i++)
+      if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
+    if (in->cluster->n_spreads) return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
     if (in->mode == GS_CONSOLIDATE_EVAL) {
       for (uint32_t s = 0; s < in->n_sets; s++) {
         if ((uint64_t)in->sets[s].begin + in->sets[s].count > in->n_candidates) return GS_E_INVALID;
