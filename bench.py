@@ -135,8 +135,11 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
     kt = []
     barrier()
     t0 = time.perf_counter()
+    steps_ms = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         merged, chosen, r = sweep()
+        steps_ms.append((time.perf_counter() - ts) * 1e3)
         kt.append((r.t_feas_ms, r.t_sim_ms, r.t_truncate_ms, r.t_fetch_ms))
     if merged is None:
         merged = result_arrays(r)
@@ -171,6 +174,7 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
         "node_checks_per_s": r.checks * world / (ms * 1e-3),
         "kernel_ms": {"feas": round(feas_ms, 4), "sim": round(sim_ms, 4), "trunc": round(trunc_ms, 4)},
         "host_decide_fetch_ms": round(decide_ms, 3),
+        "sweep_ms_each": [round(x, 3) for x in steps_ms],
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "pods_simulated": int(r.pods_simulated),
         "node_evals": int(r.node_evals),

@@ -30,8 +30,16 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.wk_slots = e.wk_slots;
   d.RQ = std::min<uint32_t>(e.R, 4);
   d.n_thr = (uint32_t)e.thr_val.size();
-  d.max_claims = sims ? std::max<uint32_t>(sims->max_pods, 1)
-                      : std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds);
+  if (sims) {
+    d.max_claims = std::max<uint32_t>(sims->max_pods, 1);
+  } else {
+    // NodeClaims the LDS holds next to the thresholds and topology state
+    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, e.TG) + 8;
+    const uint32_t dyn = gsk_ffd_dyn_lds_max();
+    const uint32_t fit = dyn > other ? (dyn - other) / 15 : 0;
+    d.max_claims = std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
+    if (!d.max_claims) throw HipError{"topology / threshold state leaves no LDS for NodeClaims"};
+  }
   c->upload(d.it_vid, e.it_vid);
   c->upload(d.it_alloc, e.it_alloc);
   c->upload(d.it_cap, e.it_cap);
@@ -68,6 +76,18 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.fk_entries, e.fk_entries);
   c->upload(d.queue0, e.queue0);
   d.NN = e.NN;
+  // topology spread groups
+  d.TG = e.TG;
+  d.TGH = e.TGH;
+  d.NZV = e.NZV;
+  d.tg_zone = e.tg_zone;
+  d.tg_host = e.tg_host;
+  c->upload(d.tgroups, e.tgroups);
+  c->upload(d.tg_cnt0, e.tg_cnt0);
+  c->upload(d.zone_order, e.zone_order);
+  c->upload(d.zone_cat, e.zone_cat);
+  c->upload(d.hn0, e.hn0);
+  c->alloc(d.hn, e.hn0.size());
   c->upload(d.nodes0, e.nodes);
   c->upload(d.n_fk0, e.n_fk);
   // the provisioning Solve works on a global copy of the nodes; simulations
@@ -98,6 +118,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->alloc(d.ctrl, 1);
   c->alloc(d.c_its, (sims ? NS : CA) * 60);
   c->alloc(d.c_nits, sims ? NS : CA);
+  c->alloc(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
   if (sims) {
     d.n_sims = (uint32_t)NS;
     d.ov_cap = std::max<uint32_t>(sims->ov_cap, 1);
@@ -351,6 +372,16 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     c->claim_pod_offsets.push_back((uint32_t)c->claim_pods.size());
     c->claim_its.insert(c->claim_its.end(), its.begin() + (size_t)j * 60, its.begin() + (size_t)j * 60 + nits[j]);
     c->claim_it_offsets.push_back((uint32_t)c->claim_its.size());
+    if (e.TG && e.keys[e.k_zone].vocab.size() <= (size_t)gsd::ZVMAX && !(hdr[j].zflags & gsd::ZF_COMP)) {
+      // topology spread narrowed the zone to In[domain]: the device's zone
+      // Has already includes it (template AND pods AND topology)
+      gsh::KReq q;
+      q.comp = false;
+      q.has = gsh::Bits(e.keys[e.k_zone].vocab.words());
+      q.excl = gsh::Bits(e.keys[e.k_zone].vocab.words());
+      q.has.w[0] = hdr[j].zfull;
+      gsh::reqs_add(e, creq[j], e.k_zone, q);
+    }
     creq[j].erase(e.k_hostname);  // FinalizeScheduling
     c->req_text[j] = gsh::canonical(e, creq[j]);
     for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = hdr[j].tot(r);

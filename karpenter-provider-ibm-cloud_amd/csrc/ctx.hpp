@@ -18,7 +18,8 @@ extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
 extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds);
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap);
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+                                      uint32_t TG);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);

@@ -576,6 +576,179 @@ struct Ctx {
       if (it == r.end() || it->second.has.test(e.cat_ct[c])) m |= 1ull << c;
     return m;
   }
+  // zone Has over the zone vocabulary (first word; topology needs <= 64
+  // values) and the complement flag of the zone requirement
+  uint64_t zone_full(const Reqs& r) const {
+    auto f = r.find(e.k_zone);
+    return f == r.end() ? ~0ull : f->second.has.w[0];
+  }
+  uint32_t zone_flags(const Reqs& r) const {
+    auto f = r.find(e.k_zone);
+    return f == r.end() || f->second.comp ? gsd::ZF_COMP : 0u;
+  }
+
+  // ------------------------------------------------ topology spread (<U>)
+  struct SpreadEnc {
+    std::string key;
+    int32_t skew = 1, mind = 0;
+    bool sa = false, has_sel = false, ignore_aff = false;
+    std::map<std::string, std::string> ml;
+    std::vector<std::tuple<std::string, uint32_t, std::set<std::string>>> ex;
+    // metav1.LabelSelector (nil selects nothing)
+    bool matches(const std::map<std::string, std::string>& labels) const {
+      if (!has_sel) return false;
+      for (auto& kv : ml) {
+        auto f = labels.find(kv.first);
+        if (f == labels.end() || f->second != kv.second) return false;
+      }
+      for (auto& x : ex) {
+        auto f = labels.find(std::get<0>(x));
+        const bool present = f != labels.end();
+        const uint32_t op = std::get<1>(x);
+        const auto& vals = std::get<2>(x);
+        if (op == GS_OP_IN && !(present && vals.count(f->second))) return false;
+        if (op == GS_OP_NOTIN && present && vals.count(f->second)) return false;
+        if (op == GS_OP_EXISTS && !present) return false;
+        if (op == GS_OP_DOES_NOT_EXIST && present) return false;
+      }
+      return true;
+    }
+    std::string hash(const std::string& ns) const {
+      std::string h = key + "|" + std::to_string(skew) + "|" + std::to_string(mind) + "|" + ns + "|" +
+                      (has_sel ? "1" : "0") + (ignore_aff ? "I" : "H");
+      for (auto& kv : ml) h += "|l:" + kv.first + "=" + kv.second;
+      for (auto& x : ex) {
+        h += "|e:" + std::get<0>(x) + ":" + std::to_string(std::get<1>(x));
+        for (auto& v : std::get<2>(x)) h += "," + v;
+      }
+      return h;
+    }
+  };
+  struct GroupEnc {
+    SpreadEnc sp;
+    std::string ns;
+  };
+  std::vector<GroupEnc> groups;
+  std::map<std::string, uint32_t> group_idx;
+  std::vector<std::string> pod_ns;
+  std::vector<std::map<std::string, std::string>> pod_labels;
+  std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
+
+  std::map<std::string, std::string> label_map(gs_range r) const {
+    chk(r, p->n_labels, "labels");
+    std::map<std::string, std::string> m;
+    for (uint32_t i = 0; i < r.count; i++) m[S(p->labels[r.begin + i].key)] = S(p->labels[r.begin + i].value);
+    return m;
+  }
+  std::vector<SpreadEnc> spreads_of(const gs_pod& pd) const {
+    chk(pd.spreads, p->n_spreads, "spreads");
+    std::vector<SpreadEnc> out;
+    for (uint32_t k = 0; k < pd.spreads.count; k++) {
+      const gs_spread& q = p->spreads[pd.spreads.begin + k];
+      SpreadEnc sp;
+      sp.key = normalize(S(q.topology_key));
+      if (sp.key != kZone && sp.key != kHostname)
+        throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / hostname"};
+      if (q.max_skew < 1) throw Fail{GS_E_INVALID, "maxSkew < 1"};
+      if (q.node_taints_policy != GS_POLICY_IGNORE) throw Fail{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor"};
+      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE)
+        throw Fail{GS_E_INVALID, "bad topology spread enum"};
+      sp.skew = q.max_skew;
+      sp.mind = q.min_domains > 0 ? q.min_domains : 0;
+      sp.sa = q.when_unsatisfiable == GS_SPREAD_SCHEDULE_ANYWAY;
+      sp.has_sel = q.has_selector != 0;
+      sp.ignore_aff = q.node_affinity_policy == GS_POLICY_IGNORE;
+      sp.ml = label_map(q.match_labels);
+      chk(q.match_expressions, p->n_reqs, "reqs");
+      for (uint32_t x = 0; x < q.match_expressions.count; x++) {
+        const gs_requirement& r = p->reqs[q.match_expressions.begin + x];
+        if (r.op > GS_OP_DOES_NOT_EXIST) throw Fail{GS_E_INVALID, "label selector operator"};
+        chk(r.values, p->n_value_ids, "values");
+        std::set<std::string> vals;
+        for (uint32_t v = 0; v < r.values.count; v++) vals.insert(S(p->value_ids[r.values.begin + v]));
+        sp.ex.emplace_back(S(r.key), r.op, std::move(vals));
+      }
+      out.push_back(std::move(sp));
+    }
+    return out;
+  }
+  bool group_selects(const GroupEnc& g, const std::string& ns, const std::map<std::string, std::string>& labels) const {
+    return ns == g.ns && g.sp.matches(labels);
+  }
+
+  // <U> NewTopology: domain universe (In values of NodePool requirements of
+  // NodePools that have instance types, existing nodes' labels) and the
+  // counts of the selected bound pods; selection masks per pod
+  void build_topology() {
+    e.TG = (uint32_t)groups.size();
+    if (!e.TG) return;
+    if (e.TG > (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups"};
+    const Vocab& zv = e.keys[e.k_zone].vocab;
+    bool any_zone = false;
+    for (auto& g : groups) any_zone = any_zone || g.sp.key == kZone;
+    if (any_zone && zv.size() > (size_t)gsd::ZVMAX)
+      throw Fail{GS_E_UNSUPPORTED, "zone topology spread over more than 63 zone values"};
+    e.NZV = (uint32_t)std::min<size_t>(zv.size() - 1, gsd::ZVMAX);
+    e.zone_order.resize(e.NZV);
+    std::iota(e.zone_order.begin(), e.zone_order.end(), 0);
+    std::sort(e.zone_order.begin(), e.zone_order.end(), [&](uint32_t a, uint32_t b) { return zv.vals[a] < zv.vals[b]; });
+    e.zone_cat.assign(gsd::ZVMAX, gsd::NONE);
+    for (uint32_t z = 0; z < e.Z; z++)
+      if (e.cat_zone[z] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_zone[z]] = z;
+    uint64_t known_zone = 0;
+    for (auto& u : np_universe) {
+      if (!u.second) continue;
+      auto f = u.first.find(e.k_zone);
+      if (f != u.first.end() && !f->second.comp) known_zone |= f->second.has.w[0];  // operator In
+    }
+    for (auto& nr : e.nodes)
+      if (nr.zvid != gsd::NONE && nr.zvid < (uint32_t)gsd::ZVMAX) known_zone |= 1ull << nr.zvid;
+    e.tgroups.assign(e.TG, gsd::TGroupRec{});
+    e.tg_cnt0.assign((size_t)e.TG * gsd::ZVMAX, 0);
+    for (uint32_t g = 0; g < e.TG; g++) {
+      gsd::TGroupRec& t = e.tgroups[g];
+      t.skew = groups[g].sp.skew;
+      t.mind = groups[g].sp.mind;
+      t.host = groups[g].sp.key == kHostname ? 1u : 0u;
+      if (t.host) {
+        t.hslot = e.TGH++;
+        e.tg_host |= 1ull << g;
+      } else {
+        t.known0 = known_zone;
+        e.tg_zone |= 1ull << g;
+      }
+    }
+    e.hn0.assign((size_t)std::max<uint32_t>(e.TGH, 1) * std::max<uint32_t>(e.NN, 1), 0);
+    std::vector<uint32_t> pos_of(e.NN);
+    for (uint32_t i = 0; i < e.NN; i++) pos_of[e.node_order[i]] = i;
+    if (p->n_bound_pods && !p->bound_pod_node) throw Fail{GS_E_INVALID, "bound pods without their nodes"};
+    for (uint32_t b = 0; b < p->n_bound_pods; b++) {
+      const gs_pod& bp = p->bound_pods[b];
+      if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
+      const uint32_t pos = pos_of[p->bound_pod_node[b]];
+      const std::string ns = S(bp.ns);
+      const auto labels = label_map(bp.labels);
+      for (uint32_t g = 0; g < e.TG; g++) {
+        if (!group_selects(groups[g], ns, labels)) continue;
+        gsd::TGroupRec& t = e.tgroups[g];
+        if (t.host) {
+          e.hn0[(size_t)t.hslot * e.NN + pos]++;
+        } else {
+          const uint32_t z = e.nodes[pos].zvid;
+          if (z == gsd::NONE || z >= (uint32_t)gsd::ZVMAX) continue;
+          e.tg_cnt0[(size_t)g * gsd::ZVMAX + z]++;
+          t.known0 |= 1ull << z;
+        }
+      }
+    }
+    for (uint32_t i = 0; i < e.P; i++) {
+      uint64_t sel = 0;
+      for (uint32_t g = 0; g < e.TG; g++)
+        if (group_selects(groups[g], pod_ns[i], pod_labels[i])) sel |= 1ull << g;
+      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) e.vars[v].t_sel = sel;
+    }
+  }
+
   // CT_SPOT | CT_OD: Requirement.Has("spot") / Has("on-demand") of the
   // capacity-type key (an absent key is Exists: both); values nobody
   // mentions behave like omega
@@ -696,21 +869,23 @@ struct Ctx {
         if (i < e.N) e.checks_per_pod += p->instance_types[i].offerings.count;
       }
       std::vector<uint64_t> opts(e.W, 0);
-      bool any = false;
+      bool any = false, has_its = false;
       for (uint32_t k = 0; k < np.instance_types.count; k++) {
         uint32_t i = p->it_refs[np.instance_types.begin + k];
         if (i >= e.N) throw Fail{GS_E_INVALID, "it_ref out of range"};
-        if (!(it_ok[i / 64] >> (i % 64) & 1)) continue;
         Reqs itr;
         for (uint32_t kk = 0; kk < e.K; kk++)
           itr.emplace(e.it_keys[kk], in_one(e.it_keys[kk], e.keys[e.it_keys[kk]].vocab.vals[e.it_vid[(size_t)kk * e.N + i]]));
         if (!reqs_compatible(e, npreqs, itr, true)) continue;
+        has_its = true;  // CloudProvider.GetInstanceTypes keeps it (topology universe)
+        if (!(it_ok[i / 64] >> (i % 64) & 1)) continue;
         if (!it_compat(i, tr)) continue;
         if (!(e.it_pair[i] & G)) continue;
         opts[i / 64] |= 1ull << (i % 64);
         any = true;
       }
       uint64_t tm = taint_mask(np.taints);
+      np_universe.emplace_back(tr, has_its);
       if (!any) continue;
       if (e.T >= (uint32_t)gsd::TMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 NodePools"};
       gsd::TmplRec t{};
@@ -731,6 +906,8 @@ struct Ctx {
       // NewNodeClaim adds hostname In[placeholder]
       reqs_add(e, tr, e.k_hostname, make_kreq(e.keys[e.k_hostname].vocab, GS_OP_IN, {e.keys[e.k_hostname].vocab.omega}, 0));
       t.ctb = ct_bits(tr);
+      t.zfull = zone_full(tr);
+      t.zflags = zone_flags(tr);
       e.tmpl.push_back(t);
       e.t_opts.insert(e.t_opts.end(), opts.begin(), opts.end());
       e.tmpl_reqs.push_back(tr);
@@ -791,6 +968,27 @@ struct Ctx {
       if (pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred node-affinity terms"};
       // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
       std::stable_sort(pref.begin(), pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+      // topology spread constraints -> groups (owners); namespace / labels for selectors
+      pod_ns.push_back(S(pd.ns));
+      pod_labels.push_back(label_map(pd.labels));
+      const std::vector<SpreadEnc> sps = spreads_of(pd);
+      if (!sps.empty() && (pd.node_selector.count || pd.required_terms.count))
+        for (auto& sp : sps)
+          if (!sp.ignore_aff)
+            throw Fail{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
+      std::vector<uint32_t> sgid;
+      for (auto& sp : sps) {
+        const std::string h = sp.hash(pod_ns.back());
+        auto f = group_idx.find(h);
+        if (f == group_idx.end()) {
+          f = group_idx.emplace(h, (uint32_t)groups.size()).first;
+          groups.push_back(GroupEnc{sp, pod_ns.back()});
+        }
+        if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups"};
+        sgid.push_back(f->second);
+      }
+      std::vector<uint32_t> cur(sps.size());  // current constraints (swap-remove order)
+      std::iota(cur.begin(), cur.end(), 0);
       chk(pd.tolerations, p->n_tolerations, "tolerations");
       std::vector<Tol> tols;
       for (uint32_t k = 0; k < pd.tolerations.count; k++) {
@@ -803,9 +1001,14 @@ struct Ctx {
         // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
         PodVariant v;
         v.reqs = ns;
+        v.strict = ns;
         if (pi < pref.size()) reqs_add_all(e, v.reqs, pref[pi].second);
-        if (ri < req_terms.size()) reqs_add_all(e, v.reqs, req_terms[ri]);
+        if (ri < req_terms.size()) {
+          reqs_add_all(e, v.reqs, req_terms[ri]);
+          reqs_add_all(e, v.strict, req_terms[ri]);
+        }
         v.tol = tol_mask(tols);
+        for (uint32_t k : cur) v.own |= 1ull << sgid[k];
         e.variants.push_back(std::move(v));
         variant_tols.push_back(tols);
         // <U> Preferences.Relax
@@ -817,6 +1020,15 @@ struct Ctx {
           pi++;
           continue;
         }
+        // removeTopologySpreadScheduleAnyway: swap-remove the first one
+        bool removed = false;
+        for (size_t k = 0; k < cur.size() && !removed; k++)
+          if (sps[cur[k]].sa) {
+            cur[k] = cur.back();
+            cur.pop_back();
+            removed = true;
+          }
+        if (removed) continue;
         if (tolerate_pns) {
           bool has = false;
           for (auto& t : tols)
@@ -856,6 +1068,10 @@ struct Ctx {
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
         vr.ctb = ct_bits(pv.reqs);
+        vr.t_own = pv.own;
+        vr.zs = zone_full(pv.strict);
+        vr.zn = zone_full(pv.reqs);
+        vr.zflags = zone_flags(pv.reqs);
         vr.tol = pv.tol;
         vr.tolt = 0;
         for (uint32_t t = 0; t < e.T; t++)
@@ -994,6 +1210,7 @@ Err encode(const gs_problem* p, Encoded& e) {
     c.build_free_slots();
     c.build_pods();
     c.build_nodes();
+    c.build_topology();
   } catch (const Fail& f) {
     return Err{f.code, f.msg};
   } catch (const std::out_of_range& ex) {

@@ -77,7 +77,9 @@ using Reqs = std::map<uint32_t, KReq>;  // key id -> requirement
 
 struct PodVariant {
   Reqs reqs;
+  Reqs strict;      // PodData.StrictRequirements: no preferred term (topology podDomains)
   uint64_t tol = 0;
+  uint64_t own = 0; // topology spread groups owned (after relaxations)
 };
 
 struct Encoded {
@@ -113,6 +115,14 @@ struct Encoded {
   std::vector<uint32_t> node_order;  // device position -> gs_problem node index
   std::vector<gsd::NodeRec> nodes;
   std::vector<gsd::FK> n_fk;
+  // topology spread (layout.hpp DevProblem topology fields)
+  uint32_t TG = 0, TGH = 0, NZV = 0;
+  uint64_t tg_zone = 0, tg_host = 0;
+  std::vector<gsd::TGroupRec> tgroups;
+  std::vector<int32_t> tg_cnt0;      // [TG][64]
+  std::vector<uint32_t> zone_order;  // zone vocabulary ids by name
+  std::vector<uint32_t> zone_cat;    // [64]
+  std::vector<int32_t> hn0;          // [TGH][NN]
   // host-only, for decode
   std::vector<Reqs> tmpl_reqs;  // incl. hostname In[omega]
   std::vector<PodVariant> variants;

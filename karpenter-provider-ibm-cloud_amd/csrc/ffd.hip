@@ -711,6 +711,11 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
+  // topology spread: zone-domain counts [TG][64], known domains, per-pod minimum counts
+  const uint32_t tg_off = (((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + d.ov_cap * 4u + 7u) & ~7u;
+  uint64_t* s_known = (uint64_t*)((char*)lds64 + tg_off);
+  int64_t* s_tmin = (int64_t*)(s_known + d.TG);
+  int32_t* s_zcnt = (int32_t*)(s_tmin + d.TG);
   Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
 
   for (uint32_t i = tid; i < nthr + 4; i += FB) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
@@ -753,6 +758,12 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       cur_var[i] = d.var_begin[gpod(i)];
     }
     for (uint32_t i = tid; i < T * R; i += FB) t_rem[i] = d.tmpl[i / R].limits[i % R];
+    if (d.TG) {
+      // <U> Topology: counts before the Solve (selected bound pods)
+      for (uint32_t i = tid; i < d.TG * ZVMAX; i += FB) s_zcnt[i] = d.tg_cnt0[i];
+      for (uint32_t g = tid; g < d.TG; g += FB) s_known[g] = d.tgroups[g].known0;
+      for (uint32_t i = tid; i < d.TGH * d.NN; i += FB) d.hn[i] = d.hn0[i];
+    }
     uint32_t ncand = 0;
     if (SIM) {
       const uint32_t c0 = d.sim_cand_off[sim];
@@ -904,6 +915,26 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
 #pragma unroll
       for (uint32_t r = 0; r < RR; r++) rq[r] = r < R ? uniform_i64(preq[r]) : 0;
 
+      // <U> Topology.AddRequirements, per pod: the minimum domain count of every
+      // zone group the pod owns over its strict zone domains (domainMinCount)
+      const uint64_t own = vr.t_own;
+      if (own) {
+        if (tid < 64 && ((own & d.tg_zone) >> tid) & 1) {
+          const uint64_t cand = s_known[tid] & vr.zs;
+          int64_t mn = INT32_MAX;
+          int32_t n = 0;
+          for (uint64_t m = cand; m; m &= m - 1) {
+            n++;
+            const int64_t c = s_zcnt[tid * ZVMAX + (uint32_t)__ffsll((long long)m) - 1];
+            mn = c < mn ? c : mn;
+          }
+          if (d.tgroups[tid].mind && n < d.tgroups[tid].mind) mn = 0;
+          s_tmin[tid] = mn;
+        }
+        __syncthreads();
+      }
+      const uint64_t tself = own & vr.t_sel;  // self-selecting groups
+
       // --------------- existing nodes in order: first ExistingNode.CanAdd wins
       if (d.NN) {
         // first-fit: a 64-node window first (the common hit), then full-width
@@ -944,6 +975,21 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             if (feas && vr.cfull_off != NONE)
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
+            if (feas && own) {
+              // zone groups: the node's own zone is the only candidate domain
+              // (a node without the label fails the strict Compatible)
+              for (uint64_t m = own & d.tg_zone; m && feas; m &= m - 1) {
+                const uint32_t g = __ffsll((long long)m) - 1, z = nr.zvid;
+                feas = z < (uint32_t)ZVMAX && ((s_known[g] >> z) & 1) &&
+                       (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= d.tgroups[g].skew;
+              }
+              // hostname groups: min count 0
+              for (uint64_t m = own & d.tg_host; m && feas; m &= m - 1) {
+                const uint32_t g = __ffsll((long long)m) - 1;
+                feas = (int64_t)d.hn[(size_t)d.tgroups[g].hslot * d.NN + n] + (int64_t)((tself >> g) & 1) <=
+                       d.tgroups[g].skew;
+              }
+            }
           }
           fn = blk.bmin(feas ? n : INF);
           if (tid == 0) S.node_evals += d.NN - base < width ? d.NN - base : width;
@@ -994,6 +1040,19 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           if (tid == 0) {
             logp[S.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
             S.found = 1;
+            // <U> Topology.Record: the node's labels are single domains
+            for (uint64_t m = vr.t_sel; m; m &= m - 1) {
+              const uint32_t g = __ffsll((long long)m) - 1;
+              if ((d.tg_host >> g) & 1) {
+                d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
+              } else {
+                const uint32_t z = d.nodes0[fn].zvid;
+                if (z < (uint32_t)ZVMAX) {
+                  s_zcnt[g * ZVMAX + z]++;
+                  s_known[g] |= 1ull << z;
+                }
+              }
+            }
           }
           pf_stage2();
           pf_stage3();
@@ -1099,6 +1158,10 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         bool feas = false, pre = false;
         uint32_t j = 0, t = 0;
         uint64_t G = 0, Gt = 0;
+        uint64_t zm = 0, cm = 0;  // the NodeClaim's catalog zone / capacity-type masks
+        uint32_t tz = NONE;  // zone domain topology spread picked for this NodeClaim
+        uint64_t czf = 0;    // the NodeClaim's zone Has / flags (read only under topology)
+        uint32_t czfl = 0;
         uint32_t mrow[RR];
         int64_t tot[RR];
         uint64_t nx[WREG];
@@ -1122,7 +1185,6 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             // one 64-B header read (four 16-B loads): totals, cursors, masks
             const ClaimRec* cr = dd.c_rec + cb + j;
             uint32_t cur[RR];
-            uint64_t zm, cm;
             {
               const uint4* q = (const uint4*)cr;
               const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
@@ -1160,6 +1222,42 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             c1 = __builtin_amdgcn_s_memtime();
 #endif
             if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)(cb + j) * F);
+            if (pre && own) {
+              // <U> Topology.AddRequirements on the NodeClaim: every owned zone
+              // group picks the minimum-count known domain within maxSkew among
+              // the NodeClaim's (claim AND pod) zone domains, ties by name; the
+              // picks must agree.  Hostname groups: this NodeClaim's count.
+              czf = cr->zfull;
+              czfl = cr->zflags;
+              const uint64_t D = czf & vr.zn;
+              for (uint64_t m = own & dd.tg_zone; m && pre; m &= m - 1) {
+                const uint32_t g = __ffsll((long long)m) - 1;
+                const uint64_t cand = D & s_known[g];
+                const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = dd.tgroups[g].skew;
+                uint32_t best = NONE;
+                int64_t bc = INT32_MAX;
+                for (uint32_t k = 0; k < dd.NZV && cand; k++) {
+                  const uint32_t z = dd.zone_order[k];
+                  if (!((cand >> z) & 1)) continue;
+                  const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
+                  if (c - mn <= skew && c < bc) {
+                    best = z;
+                    bc = c;
+                  }
+                }
+                if (best == NONE || (tz != NONE && tz != best)) pre = false;
+                tz = best;
+              }
+              for (uint64_t m = own & dd.tg_host; m && pre; m &= m - 1) {
+                const uint32_t g = __ffsll((long long)m) - 1;
+                pre = (int64_t)dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j] + (int64_t)((tself >> g) & 1) <=
+                      dd.tgroups[g].skew;
+              }
+              if (pre && tz != NONE) {
+                const uint32_t zc = dd.zone_cat[tz];
+                zm = zc < 64 ? (zm & (1ull << zc)) : 0;
+              }
+            }
             if (pre) {
               G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
               Gt = grid_of(s_tzm[t] & vr.zm, s_tcm[t] & vr.cm, dd.Z, dd.C);
@@ -1302,10 +1400,32 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               cr->thr(r) = (uint16_t)(mrow[r] - s_thoff[r] - r);
             }
             s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
-            cr->zm &= vr.zm;
+            cr->zm = zm & vr.zm;  // zm carries the topology narrowing
             cr->cm &= vr.cm;
             cr->ctb &= vr.ctb;
             cr->count++;
+            if (dd.TG) {
+              // zone requirement after Add (+ the topology domain), then
+              // <U> Topology.Record for every group selecting the pod
+              if (!own) {
+                czf = cr->zfull;
+                czfl = cr->zflags;
+              }
+              const uint64_t zf = czf & vr.zn & (tz != NONE ? 1ull << tz : ~0ull);
+              const uint32_t zl = tz != NONE ? 0u : (czfl & vr.zflags);
+              cr->zfull = zf;
+              cr->zflags = zl;
+              for (uint64_t m = vr.t_sel; m; m &= m - 1) {
+                const uint32_t g = __ffsll((long long)m) - 1;
+                if ((dd.tg_host >> g) & 1) {
+                  dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j]++;
+                } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
+                  const uint32_t z = __ffsll((long long)zf) - 1;
+                  s_zcnt[g * ZVMAX + z]++;
+                  s_known[g] |= 1ull << z;
+                }
+              }
+            }
             FK* cf = dd.c_fk + (size_t)(cb + j) * F;
             for (uint32_t k = 0; k < vr.fk_count; k++) {
               const FKEntry& e = dd.fk_entries[vr.fk_begin + k];
@@ -1341,16 +1461,58 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       for (uint32_t t = 0; t < T; t++) {
         const TmplRec& tr = d.tmpl[t];
         const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+        // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
+        // a new hostname domain has count 0, always within maxSkew >= 1):
+        // the picked zone narrows the K1 row to that zone's offerings
+        uint32_t ttz = NONE, tzc = NONE;
+        if (own) {
+          const uint64_t D = tr.zfull & vr.zn;
+          bool ok = true;
+          for (uint64_t m = own & d.tg_zone; m && ok; m &= m - 1) {
+            const uint32_t g = __ffsll((long long)m) - 1;
+            const uint64_t cand = D & s_known[g];
+            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
+            uint32_t best = NONE;
+            int64_t bc = INT32_MAX;
+            for (uint32_t k = 0; k < d.NZV && cand; k++) {
+              const uint32_t z = d.zone_order[k];
+              if (!((cand >> z) & 1)) continue;
+              const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
+              if (c - mn <= skew && c < bc) {
+                best = z;
+                bc = c;
+              }
+            }
+            if (best == NONE || (ttz != NONE && ttz != best)) ok = false;
+            ttz = best;
+          }
+          if (ok && ttz != NONE) {
+            tzc = d.zone_cat[ttz];
+            ok = tzc < 64;
+          }
+          if (!ok) continue;
+        }
+        const uint64_t tcm = tr.cm & vr.cm;
+        auto rowx = [&](uint32_t w) -> uint64_t {
+          uint64_t x = row[w];
+          if (ttz != NONE) {
+            uint64_t off = 0;
+            for (uint32_t c = 0; c < d.C; c++)
+              if ((tcm >> c) & 1) off |= slot[(tzc * d.C + c) * W + w];
+            x &= off;
+          }
+          return x;
+        };
         bool any = false;
         if (d.fk_ok[(size_t)v * T + t])
           for (uint32_t w = 0; w < W; w++)
-            if (row[w]) any = true;
+            if (rowx(w)) any = true;
         if (!any) continue;
         if (tr.has_limits) {
           // <U> filterByRemainingResources on the template's options
           uint32_t hit = INF;
           for (uint32_t i = tid; i < d.N; i += FB) {
-            if (!((row[i >> 6] >> (i & 63)) & 1)) continue;
+            if (!((rowx(i >> 6) >> (i & 63)) & 1)) continue;
             bool ok = true;
             for (uint32_t r = 0; r < R; r++)
               if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= t_rem[(size_t)t * R + r];
@@ -1372,7 +1534,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         }
         __syncthreads();
         for (uint32_t w = tid; w < W; w += FB) {
-          uint64_t x = row[w];
+          uint64_t x = rowx(w);
           // establish opts ⊆ thr_set[cursor] for the candidate scan
           for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * OW + w];
           if (tr.has_limits) {
@@ -1404,9 +1566,25 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         if (tid == 0) {
           cr->tmpl = t;
           cr->count = 1;
-          cr->zm = tr.zm & vr.zm;
+          cr->zm = tr.zm & vr.zm & (ttz != NONE ? 1ull << tzc : ~0ull);
           cr->cm = tr.cm & vr.cm;
           cr->ctb = tr.ctb & vr.ctb;
+          cr->zfull = tr.zfull & vr.zn & (ttz != NONE ? 1ull << ttz : ~0ull);
+          cr->zflags = ttz != NONE ? 0u : (tr.zflags & vr.zflags);
+          if (d.TG) {
+            // <U> Topology.Register(hostname placeholder) + Record
+            for (uint32_t h = 0; h < d.TGH; h++) d.hc[(size_t)h * d.max_claims + cbase + j] = 0;
+            for (uint64_t m = vr.t_sel; m; m &= m - 1) {
+              const uint32_t g = __ffsll((long long)m) - 1;
+              if ((d.tg_host >> g) & 1) {
+                d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + cbase + j]++;
+              } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
+                const uint32_t z = __ffsll((long long)cr->zfull) - 1;
+                s_zcnt[g * ZVMAX + z]++;
+                s_known[g] |= 1ull << z;
+              }
+            }
+          }
           FK* cf = d.c_fk + (size_t)(cbase + j) * F;
           for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
           for (uint32_t k = 0; k < vr.fk_count; k++) {
@@ -1536,10 +1714,13 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
 }
 
 // dynamic LDS: ord/sc/scr u16 + slack u64 + tmpl u8 per claim, thresholds,
-// and (simulations) the touched-node bitmap + overlay ids
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap) {
+// (simulations) the touched-node bitmap + overlay ids, and the topology
+// spread state (known domains, per-pod minimum, zone counts) of TG groups
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+                                      uint32_t TG) {
   const uint32_t thr = nthr + 4;
-  return ((15u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u;
+  const uint32_t base = (((15u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u + 7u) & ~7u;
+  return base + TG * 16u + TG * ZVMAX * 4u;
 }
 
 // every instantiation may use all LDS its static footprint leaves free
@@ -1587,7 +1768,7 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds) {
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap);
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, d->TG);
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   switch (d->R * 2 + (sim ? 1 : 0)) {

@@ -22,6 +22,9 @@ constexpr int TMAX = 64;       // NodeClaim templates (NodePools)
 constexpr uint32_t THR_LDS_MAX = 2048;   // fit thresholds staged in the FFD kernel's LDS
 constexpr uint32_t SLOT_LDS_MAX = 1024;  // (zone, capacity-type) pair type-set words in LDS
 constexpr int SMAX = 16;       // offerings per instance type
+constexpr int TGMAX = 64;      // topology spread groups
+constexpr int ZVMAX = 64;      // zone vocabulary (topology domains) when zone spread is used
+enum : uint32_t { ZF_COMP = 1u };  // zone requirement is a complement (Exists / NotIn / absent)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 // capacity-type requirement bits (consolidation's spot-to-spot rule)
 enum : uint32_t { CT_SPOT = 1u, CT_OD = 2u };
@@ -53,7 +56,15 @@ struct VarRec {
   uint64_t zm, cm;               // Has over catalog zones / capacity types
   uint64_t tol;                  // tolerated taint-vocabulary mask
   uint64_t tolt;                 // templates whose taints this variant tolerates
+  // topology spread (<U> Topology): groups the variant owns, groups that
+  // select the pod, zone Has over the zone vocabulary of the strict
+  // (podDomains) and full (nodeDomains) requirements
+  uint64_t t_own, t_sel;
+  uint64_t zs, zn;
+  uint32_t zflags;               // ZF_COMP of the full zone requirement
+  uint32_t pad2;
 };
+static_assert(sizeof(VarRec) == 128, "VarRec layout");
 
 struct TmplRec {
   uint32_t np_index;
@@ -64,6 +75,18 @@ struct TmplRec {
   uint64_t taints;       // taint-vocabulary mask
   int64_t daemon[RMAX];
   int64_t limits[RMAX];  // initial remaining limits
+  uint64_t zfull;        // zone Has over the zone vocabulary
+  uint32_t zflags;       // ZF_COMP
+  uint32_t pad2;
+};
+
+// one topology spread group (<U> TopologyGroup, type spread, empty node filter)
+struct TGroupRec {
+  int32_t skew;          // maxSkew
+  int32_t mind;          // minDomains (0 = unset)
+  uint32_t hslot;        // hostname groups: row in hn / hc
+  uint32_t host;         // 1: kubernetes.io/hostname, 0: topology.kubernetes.io/zone
+  uint64_t known0;       // zone groups: domains known before the Solve (universe + counted)
 };
 
 // per-claim record (device-owned, AoS: one candidate = one 192-B record read
@@ -79,7 +102,9 @@ struct alignas(64) ClaimRec {
   int64_t tot_hi[RMAX - 4];
   uint16_t thr_hi[RMAX - 4];
   uint32_t ctb;          // CT_SPOT | CT_OD of the claim requirements (template AND pods)
-  uint32_t pad[5];
+  uint32_t zflags;       // ZF_COMP of the claim's zone requirement
+  uint64_t zfull;        // zone Has over the zone vocabulary (topology spread)
+  uint32_t pad[2];
   int64_t maxa[RMAX];    // max allocatable over the claim's initial options (slack bound)
   __host__ __device__ int64_t& tot(uint32_t r) { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
   __host__ __device__ int64_t tot(uint32_t r) const { return r < 4 ? tot_lo[r] : tot_hi[r - 4]; }
@@ -180,6 +205,17 @@ struct DevProblem {
   LogRec* log;                 // [P]
   uint32_t* c_sorted;          // [max_claims] final sort order (debug)
   Ctrl* ctrl;
+  // topology spread
+  uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size
+  uint32_t pad_tg;
+  uint64_t tg_zone, tg_host;   // group masks by key
+  const TGroupRec* tgroups;    // [TG]
+  const int32_t* tg_cnt0;      // [TG][64] zone counts before the Solve
+  const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)
+  const uint32_t* zone_cat;    // [64] zone vocabulary id -> catalog zone index (NONE)
+  const int32_t* hn0;          // [TGH][NN] hostname counts per existing node before the Solve
+  int32_t* hn;                 // [TGH][NN] working copy
+  int32_t* hc;                 // [TGH][max_claims] per NodeClaim
   // truncation outputs
   uint32_t* c_its;             // [max_claims][60] (simulations: [n_sims][60])
   uint32_t* c_nits;            // [max_claims]     (simulations: [n_sims])

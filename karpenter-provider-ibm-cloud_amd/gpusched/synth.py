@@ -173,7 +173,13 @@ def make_c5(n_pods=200_000, seed=0x5EED0005, n_its=2000):
     return b.build()
 
 
-def make_c3(n_pods=50_000, seed=0x5EED0003):
+APPS = ["web", "api", "batch", "cache"]
+
+
+def make_c3(n_pods=50_000, seed=0x5EED0003, spread_frac=0.2):
+    """C3: 4 weighted NodePools, taints/tolerations, required node affinity
+    (In/NotIn), preferred affinity and a `spread_frac` share of pods with a
+    zone topology spread (maxSkew 1 on their app label, ScheduleAnyway on half)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     profs = c2_profiles(200)
@@ -189,7 +195,8 @@ def make_c3(n_pods=50_000, seed=0x5EED0003):
     b.add_nodepool("memory", weight=10, requirements=[("karpenter-ibm.sh/instance-family", "In",
                                                        ["mx2", "mx3d", "ux2d", "vx2d", "ox2"])],
                    labels={"tier": "memory"}, daemon=daemon, limits={"cpu": 4000 * 1000})
-    b.add_nodepool("default", weight=0, requirements=[("karpenter.sh/capacity-type", "In", ["on-demand"])],
+    b.add_nodepool("default", weight=0, requirements=[("karpenter.sh/capacity-type", "In", ["on-demand"]),
+                                                      ("topology.kubernetes.io/zone", "In", FAKE_ZONES)],
                    daemon=daemon)
     cpu = rng.choice(CPU_CHOICES, size=n_pods, p=CPU_W / CPU_W.sum())
     mem = rng.choice(MEM_CHOICES, size=n_pods)
@@ -222,8 +229,14 @@ def make_c3(n_pods=50_000, seed=0x5EED0003):
                 preferred.append((int(rng.integers(1, 100)), [("tier", "In", ["memory"])]))
         if rng.random() < 0.03:
             sel["tier"] = "memory"
+        app = APPS[rng.integers(0, len(APPS))]
+        spreads = []
+        if rng.random() < spread_frac and not required and not sel:
+            spreads.append({"key": "topology.kubernetes.io/zone", "max_skew": 1,
+                            "when": "ScheduleAnyway" if rng.random() < 0.5 else "DoNotSchedule",
+                            "selector": {"labels": {"app": app}}})
         b.add_pod(_uid(rng), int(ts[i]), req, node_selector=sel, required_terms=required,
-                  preferred_terms=preferred, tolerations=tols)
+                  preferred_terms=preferred, tolerations=tols, labels={"app": app}, spreads=spreads)
     return b.build()
 
 
@@ -492,4 +505,86 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
     for i in range(npend):
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000, {"cpu": int(rng.choice([100, 1000, 3000])),
                                                          "memory": int(GI) * 1000, "pods": 1000})
+    return b.build()
+
+
+def random_topology(seed, n_pods=None):
+    """small adversarial topology-spread problems: zone / hostname spreads
+    (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
+    and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
+    with node affinity), NodePools with and without zone requirements,
+    existing nodes with labelled bound pods, taints and relaxation"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
+    profs = []
+    for fam in ["bx2", "cx2", "mx2"]:
+        for v in [2, 4, 8]:
+            if rng.random() < 0.7:
+                profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    if not profs:
+        profs = [("bx2-4x16", 4, 16, None)]
+    prices = {p_[0]: round(0.05 * p_[1] + 0.01 * float(rng.random()), 4) for p_ in profs}
+    its = build_catalog(b, profs, zones, spot=bool(rng.random() < 0.5), prices=prices, rng=rng,
+                        unavailable_frac=0.1)
+    n_np = int(rng.integers(1, 3))
+    for j in range(n_np):
+        reqs = []
+        if rng.random() < 0.7:
+            zs = sorted(rng.choice(zones, size=int(rng.integers(1, len(zones) + 1)), replace=False).tolist())
+            reqs.append(("topology.kubernetes.io/zone", "In", zs))
+        taints = [("dedicated", "x", "PreferNoSchedule")] if rng.random() < 0.3 else []
+        limits = {"cpu": int(rng.choice([8, 32])) * 1000} if rng.random() < 0.2 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, taints=taints, limits=limits,
+                       daemon={"cpu": 100, "pods": 1000})
+    nn = int(rng.integers(0, 5))
+    for k in range(nn):
+        it = its[rng.integers(0, len(its))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(zones + ["z9"]))
+        labels["karpenter.sh/capacity-type"] = "on-demand"
+        labels["kubernetes.io/hostname"] = f"n{k}"
+        avail = {"cpu": int(rng.choice([1000, 3000, 6000])), "memory": 8 * GI * 1000, "pods": 20_000}
+        b.add_node(f"n{k}", labels, avail, initialized=True)
+        for q in range(int(rng.integers(0, 4))):
+            b.add_bound_pod(k, _uid(rng), 0, {"cpu": 100, "pods": 1000},
+                            labels={"app": str(rng.choice(APPS[:3]))},
+                            namespace=str(rng.choice(["default", "default", "other"])))
+    # a palette of constraints (deployments share them): at most 16 groups
+    palette = []
+    for _ in range(int(rng.integers(1, 9))):
+        key = "topology.kubernetes.io/zone" if rng.random() < 0.7 else "kubernetes.io/hostname"
+        tgt = str(rng.choice(APPS[:3]))
+        r = rng.random()
+        if r < 0.6:
+            selector = {"labels": {"app": tgt}}
+        elif r < 0.8:
+            selector = {"exprs": [("app", str(rng.choice(["In", "NotIn"])), [tgt, "cache"])]}
+        elif r < 0.9:
+            selector = {"exprs": [("app", "Exists", [])]}
+        else:
+            selector = None
+        sp = {"key": key, "max_skew": int(rng.choice([1, 1, 2, 3])),
+              "when": "ScheduleAnyway" if rng.random() < 0.4 else "DoNotSchedule", "selector": selector}
+        if rng.random() < 0.15:
+            sp["min_domains"] = int(rng.integers(2, 6))
+        palette.append(sp)
+    n = int(n_pods if n_pods is not None else rng.integers(1, 40))
+    for i in range(n):
+        app = str(rng.choice(APPS[:3]))
+        req = {"cpu": int(rng.choice([250, 500, 1000, 2000])), "memory": int(rng.choice([1, 2, 4])) * GI * 1000,
+               "pods": 1000}
+        required, sel = [], {}
+        spreads = [dict(palette[k]) for k in rng.choice(len(palette), size=int(rng.choice([0, 1, 1, 2])))]
+        if rng.random() < 0.2:
+            if spreads:
+                for sp in spreads:
+                    sp["node_affinity_policy"] = "Ignore"
+            required.append([("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(zones))])])
+        if rng.random() < 0.1 and not spreads:
+            sel["topology.kubernetes.io/zone"] = str(rng.choice(zones))
+        tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000, req,
+                  node_selector=sel, required_terms=required, tolerations=tols, labels={"app": app},
+                  namespace=str(rng.choice(["default", "default", "other"])), spreads=spreads)
     return b.build()

@@ -344,6 +344,51 @@ struct Term {
   int32_t weight;
 };
 
+// corev1.TopologySpreadConstraint (zone / hostname keys)
+struct Spread {
+  string key;
+  int32_t max_skew = 1;
+  bool schedule_anyway = false;
+  optional<int32_t> min_domains;
+  bool has_selector = false;
+  std::map<string, string> match_labels;
+  struct Expr {
+    string key;
+    int op;
+    std::set<string> values;
+  };
+  vector<Expr> exprs;
+  bool ignore_affinity = false;
+  // metav1.LabelSelector over a pod's labels (nil selects nothing)
+  bool matches(const std::map<string, string>& labels) const {
+    if (!has_selector) return false;
+    for (auto& kv : match_labels) {
+      auto f = labels.find(kv.first);
+      if (f == labels.end() || f->second != kv.second) return false;
+    }
+    for (auto& e : exprs) {
+      auto f = labels.find(e.key);
+      const bool present = f != labels.end();
+      if (e.op == GS_OP_IN && !(present && e.values.count(f->second))) return false;
+      if (e.op == GS_OP_NOTIN && present && e.values.count(f->second)) return false;
+      if (e.op == GS_OP_EXISTS && !present) return false;
+      if (e.op == GS_OP_DOES_NOT_EXIST && present) return false;
+    }
+    return true;
+  }
+  // TopologyGroup identity (whenUnsatisfiable is not part of it)
+  string hash(const string& ns) const {
+    string h = key + "|" + std::to_string(max_skew) + "|" + (min_domains ? std::to_string(*min_domains) : "-") + "|" +
+               ns + "|" + (has_selector ? "1" : "0") + "|" + (ignore_affinity ? "I" : "H");
+    for (auto& kv : match_labels) h += "|l:" + kv.first + "=" + kv.second;
+    for (auto& e : exprs) {
+      h += "|e:" + e.key + ":" + std::to_string(e.op);
+      for (auto& v : e.values) h += "," + v;
+    }
+    return h;
+  }
+};
+
 struct Pod {
   uint32_t index;
   string uid;
@@ -353,7 +398,11 @@ struct Pod {
   vector<Term> required;   // mutable (relaxation)
   vector<Term> preferred;  // mutable (relaxation)
   vector<Toleration> tolerations;
-  Reqs reqs;  // cached PodData.Requirements
+  Reqs reqs;    // cached PodData.Requirements
+  Reqs strict;  // cached PodData.StrictRequirements (no preferred term)
+  string ns;
+  std::map<string, string> labels;
+  vector<Spread> spreads;  // mutable (relaxation)
 };
 
 struct Template {
@@ -399,10 +448,14 @@ void update_pod_reqs(Pod& p) {
     gosort::slice(d, (int)p.preferred.size());
     for (auto& q : p.preferred[0].reqs) r.add(q);
   }
+  Reqs strict;
+  for (auto& kv : p.node_selector) strict.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
   if (!p.required.empty()) {
     for (auto& q : p.required[0].reqs) r.add(q);
+    for (auto& q : p.required[0].reqs) strict.add(q);
   }
   p.reqs = std::move(r);
+  p.strict = std::move(strict);
 }
 
 // <U> filterInstanceTypesByRequirements (no short-circuit across ITs)
@@ -450,6 +503,18 @@ vector<const InstanceType*> order_by_price(vector<const InstanceType*> its, cons
   return out;
 }
 
+// <U> scheduling.TopologyGroup (TopologyTypeSpread) with an empty node filter
+struct TGroup {
+  string key;
+  int32_t max_skew;
+  optional<int32_t> min_domains;
+  string ns;
+  Spread sel;
+  std::map<string, int64_t> domains;  // known domains and their counts
+  std::set<uint32_t> owners;          // pod indices
+  bool selects(const Pod& p) const { return p.ns == ns && sel.matches(p.labels); }
+};
+
 struct OracleState {
   vector<string> strings;
   vector<InstanceType> its;
@@ -460,6 +525,8 @@ struct OracleState {
   std::map<string, Res> remaining;  // nodepools with limits
   bool tolerate_pns = false;
   vector<string> resource_names;
+  vector<TGroup> groups;            // creation order
+  std::map<string, size_t> group_index;
 };
 
 struct Builder {
@@ -521,6 +588,95 @@ struct Builder {
     return out;
   }
 
+  // namespace, labels and topology spread constraints of a pod
+  void pod_meta(const gs_pod& g, Pod& pd) {
+    pd.ns = str(g.ns);
+    pd.labels = labels_of(g.labels);
+    check_range(g.spreads, p->n_spreads, "spreads");
+    for (uint32_t k = 0; k < g.spreads.count; k++) {
+      const gs_spread& q = p->spreads[g.spreads.begin + k];
+      Spread sp;
+      sp.key = normalize_key(str(q.topology_key));
+      if (sp.key != kZone && sp.key != kHostname)
+        throw Unsupported{GS_E_UNSUPPORTED, "topology spread key other than zone / hostname"};
+      if (q.max_skew < 1) throw Unsupported{GS_E_INVALID, "maxSkew < 1"};
+      if (q.node_taints_policy != GS_POLICY_IGNORE) throw Unsupported{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor"};
+      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE)
+        throw Unsupported{GS_E_INVALID, "bad topology spread enum"};
+      sp.max_skew = q.max_skew;
+      sp.schedule_anyway = q.when_unsatisfiable == GS_SPREAD_SCHEDULE_ANYWAY;
+      if (q.min_domains > 0) sp.min_domains = q.min_domains;
+      sp.has_selector = q.has_selector != 0;
+      sp.match_labels = labels_of(q.match_labels);
+      check_range(q.match_expressions, p->n_reqs, "reqs");
+      for (uint32_t e = 0; e < q.match_expressions.count; e++) {
+        const gs_requirement& r = p->reqs[q.match_expressions.begin + e];
+        if (r.op > GS_OP_DOES_NOT_EXIST) throw Unsupported{GS_E_INVALID, "label selector operator"};
+        check_range(r.values, p->n_value_ids, "values");
+        Spread::Expr x{str(r.key), (int)r.op, {}};
+        for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
+        sp.exprs.push_back(std::move(x));
+      }
+      sp.ignore_affinity = q.node_affinity_policy == GS_POLICY_IGNORE;
+      pd.spreads.push_back(std::move(sp));
+    }
+  }
+
+  // <U> NewTopology: one group per distinct constraint of the pods being
+  // scheduled; domain universe = In values of NodePool (+labels, + instance
+  // type) requirements of NodePools that have instance types, plus existing
+  // nodes' labels; counts = selected bound pods on existing nodes
+  void build_topology(const vector<Reqs>& np_reqs, const vector<bool>& np_has_its) {
+    for (auto& pd : st.pods)
+      for (auto& sp : pd.spreads) {
+        const string h = sp.hash(pd.ns);
+        auto f = st.group_index.find(h);
+        size_t gi;
+        if (f == st.group_index.end()) {
+          gi = st.groups.size();
+          st.group_index[h] = gi;
+          TGroup g;
+          g.key = sp.key;
+          g.max_skew = sp.max_skew;
+          g.min_domains = sp.min_domains;
+          g.ns = pd.ns;
+          g.sel = sp;
+          st.groups.push_back(std::move(g));
+        } else {
+          gi = f->second;
+        }
+        st.groups[gi].owners.insert(pd.index);
+      }
+    if (st.groups.empty()) return;
+    for (auto& g : st.groups) {
+      for (size_t i = 0; i < np_reqs.size(); i++) {
+        if (!np_has_its[i] || !np_reqs[i].has_key(g.key)) continue;
+        const Req q = np_reqs[i].get(g.key);
+        if (q.op() == GS_OP_IN)
+          for (auto& v : q.values) g.domains.emplace(v, 0);
+      }
+      for (auto& n : st.nodes) {
+        if (!n.reqs.has_key(g.key)) continue;
+        const Req q = n.reqs.get(g.key);
+        if (q.op() == GS_OP_IN)
+          for (auto& v : q.values) g.domains.emplace(v, 0);
+      }
+    }
+    check_range(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
+    for (uint32_t b = 0; b < p->n_bound_pods; b++) {
+      if (p->bound_pod_node[b] >= st.nodes.size()) throw Unsupported{GS_E_INVALID, "bound pod node out of range"};
+      Pod bp;
+      bp.index = UINT32_MAX;
+      pod_meta(p->bound_pods[b], bp);
+      const ExistingNode& n = st.nodes[p->bound_pod_node[b]];
+      for (auto& g : st.groups) {
+        if (!g.selects(bp) || !n.reqs.has_key(g.key)) continue;
+        const Req q = n.reqs.get(g.key);
+        if (q.op() == GS_OP_IN && q.values.size() == 1) g.domains[*q.values.begin()]++;
+      }
+    }
+  }
+
   void build() {
     st.strings.clear();
     for (uint32_t i = 0; i < p->n_strings; i++) st.strings.push_back(p->strings[i] ? p->strings[i] : "");
@@ -550,6 +706,8 @@ struct Builder {
       if (A.weight == B.weight) return str(A.name) < str(B.name);
       return A.weight > B.weight;
     });
+    vector<Reqs> np_reqs;
+    vector<bool> np_has_its;
     for (uint32_t npi : order) {
       auto& np = p->nodepools[npi];
       Template t;
@@ -573,6 +731,8 @@ struct Builder {
         const InstanceType* it = &st.its[idx];
         if (npreqs.compatible(it->reqs, true)) its.push_back(it);
       }
+      np_reqs.push_back(t.reqs);
+      np_has_its.push_back(!its.empty());
       // <U> NewScheduler: pre-filter instance types per template
       t.options = filter_its(its, t.reqs, Res{});
       if (t.has_limits) st.remaining[t.name] = res_of(np.limits);
@@ -610,6 +770,11 @@ struct Builder {
         auto& t = p->tolerations[g.tolerations.begin + k];
         pd.tolerations.push_back({str(t.key), str(t.value), str(t.effect), (int)t.op});
       }
+      pod_meta(g, pd);
+      if (!pd.spreads.empty() && (!pd.node_selector.empty() || !pd.required.empty()))
+        for (auto& sp : pd.spreads)
+          if (!sp.ignore_affinity)
+            throw Unsupported{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
       update_pod_reqs(pd);
     }
     // existing nodes: <U> initialized first, then by name (sort.SliceStable)
@@ -634,6 +799,7 @@ struct Builder {
       if (A.initialized != B.initialized) return A.initialized;
       return A.name < B.name;
     });
+    build_topology(np_reqs, np_has_its);
     // resource vocabulary (for dense claim requests)
     std::set<string> rn;
     for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(str(p->quantities[i].resource));
@@ -657,7 +823,13 @@ bool relax(Pod& p, bool tolerate_pns) {
     p.preferred.erase(p.preferred.begin());
     return true;
   }
-  // removeTopologySpreadScheduleAnyway: refused up front
+  // removeTopologySpreadScheduleAnyway: swap-remove the first ScheduleAnyway
+  for (size_t i = 0; i < p.spreads.size(); i++)
+    if (p.spreads[i].schedule_anyway) {
+      p.spreads[i] = p.spreads.back();
+      p.spreads.pop_back();
+      return true;
+    }
   if (tolerate_pns) {
     for (auto& t : p.tolerations)
       if (t.key.empty() && t.op == GS_TOL_EXISTS && t.value.empty() && t.effect == kEffectPreferNoSchedule) return false;
@@ -669,6 +841,85 @@ bool relax(Pod& p, bool tolerate_pns) {
 
 struct Scheduler {
   OracleState& st;
+
+  // ---------------------------------------------------------- <U> Topology
+  // TopologyGroup.domainMinCount
+  int64_t domain_min_count(const TGroup& g, const Req& pod_domains) const {
+    if (g.key == kHostname) return 0;
+    int64_t mn = INT32_MAX;
+    int32_t n = 0;
+    for (auto& kv : g.domains)
+      if (pod_domains.has(kv.first)) {
+        n++;
+        mn = std::min(mn, kv.second);
+      }
+    if (g.min_domains && n < *g.min_domains) mn = 0;
+    return mn;
+  }
+  // TopologyGroup.nextDomainTopologySpread: the minimum-count domain among
+  // the node's domains within maxSkew.  Upstream iterates a Go map / an
+  // unsorted set, so ties fall in random order; restated: smallest name.
+  Req next_domain(const TGroup& g, const Pod& pod, const Req& pod_domains, const Req& node_domains) const {
+    const int64_t mn = domain_min_count(g, pod_domains);
+    const int64_t self = g.selects(pod) ? 1 : 0;
+    string best;
+    int64_t best_count = INT32_MAX;
+    auto consider = [&](const string& d, int64_t count) {
+      count += self;
+      if (count - mn <= g.max_skew && count < best_count) {
+        best = d;
+        best_count = count;
+      }
+    };
+    if (node_domains.op() == GS_OP_IN) {
+      for (auto& d : node_domains.values) {
+        auto f = g.domains.find(d);
+        if (f != g.domains.end()) consider(d, f->second);
+      }
+    } else {
+      for (auto& kv : g.domains)
+        if (node_domains.has(kv.first)) consider(kv.first, kv.second);
+    }
+    if (best_count == INT32_MAX) return make_req(g.key, GS_OP_DOES_NOT_EXIST, {}, std::nullopt);
+    return make_req(g.key, GS_OP_IN, {best}, std::nullopt);
+  }
+  // Topology.AddRequirements over the groups the pod owns
+  bool topology = true;  // off for the static (fresh NodeClaim) feasibility matrix
+  bool topo_requirements(const Pod& pod, const Reqs& node_reqs, Reqs* out) const {
+    if (!topology) return true;
+    for (auto& g : st.groups) {
+      if (!g.owners.count(pod.index)) continue;
+      const Req pd = pod.strict.has_key(g.key) ? pod.strict.get(g.key) : make_req(g.key, GS_OP_EXISTS, {}, std::nullopt);
+      const Req nd = node_reqs.has_key(g.key) ? node_reqs.get(g.key) : make_req(g.key, GS_OP_EXISTS, {}, std::nullopt);
+      const Req d = next_domain(g, pod, pd, nd);
+      if (d.len() == 0) return false;
+      out->add(d);
+    }
+    return true;
+  }
+  // Topology.Record: every group that selects the pod counts the domain it
+  // landed in, when that domain is known (a single value)
+  void topo_record(const Pod& pod, const Reqs& reqs) {
+    for (auto& g : st.groups) {
+      if (!g.selects(pod) || !reqs.has_key(g.key)) continue;
+      const Req d = reqs.get(g.key);
+      if (!d.complement && d.values.size() == 1) g.domains[*d.values.begin()]++;
+    }
+  }
+  // Topology.Register(hostname, placeholder)
+  void topo_register_hostname(const string& h) {
+    for (auto& g : st.groups)
+      if (g.key == kHostname) g.domains.emplace(h, 0);
+  }
+  // Topology.Update after a relaxation: ownership follows the remaining constraints
+  void topo_update(const Pod& pod) {
+    for (auto& g : st.groups) g.owners.erase(pod.index);
+    for (auto& sp : pod.spreads) {
+      auto f = st.group_index.find(sp.hash(pod.ns));
+      if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
+    }
+  }
+
   vector<NodeClaim*> claims;  // s.newNodeClaims (sorted in place per pod)
   vector<std::unique_ptr<NodeClaim>> owned;
   vector<NodeClaim*> creation_order;
@@ -682,6 +933,10 @@ struct Scheduler {
     Reqs nr = n.reqs;  // NewRequirements(n.Requirements.Values()...)
     if (!nr.compatible(pod.reqs, true)) return false;
     nr.add_all(pod.reqs);
+    Reqs topo;
+    if (!topo_requirements(pod, nr, &topo)) return false;
+    if (!nr.compatible(topo, true)) return false;
+    nr.add_all(topo);
     Res requests = merge(n.requests, pod.requests);
     auto remaining = filter_its(n.options, nr, requests);
     if (remaining.empty()) return false;
@@ -699,6 +954,10 @@ struct Scheduler {
     Reqs nr = n.reqs;
     if (!nr.compatible(pod.reqs, false)) return false;
     nr.add_all(pod.reqs);
+    Reqs topo;
+    if (!topo_requirements(pod, nr, &topo)) return false;
+    if (!nr.compatible(topo, false)) return false;
+    nr.add_all(topo);
     *reqs_out = std::move(nr);
     *req_out = std::move(requests);
     return true;
@@ -713,6 +972,7 @@ struct Scheduler {
         n.reqs = std::move(r);
         n.requests = std::move(q);
         n.pods.push_back(&pod);
+        topo_record(pod, n.reqs);
         return true;
       }
     }
@@ -732,6 +992,7 @@ struct Scheduler {
         nc->options = std::move(its);
         nc->requests = std::move(q);
         nc->pods.push_back(&pod);
+        topo_record(pod, nc->reqs);
         return true;
       }
     }
@@ -756,6 +1017,7 @@ struct Scheduler {
       nc->reqs = t.reqs;
       char hn[48];
       std::snprintf(hn, sizeof hn, "hostname-placeholder-%04llu", (unsigned long long)++node_id);
+      topo_register_hostname(hn);
       nc->reqs.add(make_req(kHostname, GS_OP_IN, {hn}, std::nullopt));
       nc->options = its;
       nc->requests = t.daemon;
@@ -767,6 +1029,7 @@ struct Scheduler {
       nc->options = std::move(its2);
       nc->requests = std::move(q);
       nc->pods.push_back(&pod);
+      topo_record(pod, nc->reqs);
       if (rem != st.remaining.end()) {
         // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
         Res mx;
@@ -821,6 +1084,7 @@ struct Scheduler {
       if (relaxed) {
         last_len.clear();
         update_pod_reqs(*p);
+        topo_update(*p);
       } else {
         last_len[p] = queue.size() - head;
       }
@@ -926,6 +1190,7 @@ extern "C" gs_status oracle_feasibility(const gs_problem* problem, gs_feas_resul
   r.nfeas.assign((size_t)P * T, 0);
   uint64_t checks = 0;
   Scheduler s{st};
+  s.topology = false;
   for (auto& t : st.templates) {
     for (auto* it : t.options) checks += (uint64_t)it->offerings.size() * P;
   }
