@@ -688,7 +688,7 @@ __device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa,
 //    bitmap + overlay ids, global req/FK copies per block).
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
 
-template <uint32_t RR, bool SIM, uint32_t NT>
+template <uint32_t RR, bool SIM, uint32_t NT, bool TOPO>
 __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
   constexpr uint32_t FB = NT;  // threads of this workgroup
   extern __shared__ uint64_t lds64[];
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       cur_var[i] = d.var_begin[gpod(i)];
     }
     for (uint32_t i = tid; i < T * R; i += FB) t_rem[i] = d.tmpl[i / R].limits[i % R];
-    if (d.TG) {
+    if (TOPO) {
       // <U> Topology: counts before the Solve (selected bound pods)
       for (uint32_t i = tid; i < d.TG * ZVMAX; i += FB) s_zcnt[i] = d.tg_cnt0[i];
       for (uint32_t g = tid; g < d.TG; g += FB) s_known[g] = d.tgroups[g].known0;
@@ -917,8 +917,8 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
 
       // <U> Topology.AddRequirements, per pod: the minimum domain count of every
       // zone group the pod owns over its strict zone domains (domainMinCount)
-      const uint64_t own = vr.t_own;
-      if (own) {
+      const uint64_t own = TOPO ? vr.t_own : 0;  // topology spread groups the pod owns
+      if (TOPO && own) {
         if (tid < 64 && ((own & d.tg_zone) >> tid) & 1) {
           const uint64_t cand = s_known[tid] & vr.zs;
           int64_t mn = INT32_MAX;
@@ -975,7 +975,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             if (feas && vr.cfull_off != NONE)
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
-            if (feas && own) {
+            if (TOPO && feas && own) {
               // zone groups: the node's own zone is the only candidate domain
               // (a node without the label fails the strict Compatible)
               for (uint64_t m = own & d.tg_zone; m && feas; m &= m - 1) {
@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             logp[S.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
             S.found = 1;
             // <U> Topology.Record: the node's labels are single domains
-            for (uint64_t m = vr.t_sel; m; m &= m - 1) {
+            for (uint64_t m = TOPO ? vr.t_sel : 0; m; m &= m - 1) {
               const uint32_t g = __ffsll((long long)m) - 1;
               if ((d.tg_host >> g) & 1) {
                 d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
@@ -1222,7 +1222,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             c1 = __builtin_amdgcn_s_memtime();
 #endif
             if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)(cb + j) * F);
-            if (pre && own) {
+            if (TOPO && pre && own) {
               // <U> Topology.AddRequirements on the NodeClaim: every owned zone
               // group picks the minimum-count known domain within maxSkew among
               // the NodeClaim's (claim AND pod) zone domains, ties by name; the
@@ -1404,7 +1404,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             cr->cm &= vr.cm;
             cr->ctb &= vr.ctb;
             cr->count++;
-            if (dd.TG) {
+            if (TOPO) {
               // zone requirement after Add (+ the topology domain), then
               // <U> Topology.Record for every group selecting the pod
               if (!own) {
@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         // a new hostname domain has count 0, always within maxSkew >= 1):
         // the picked zone narrows the K1 row to that zone's offerings
         uint32_t ttz = NONE, tzc = NONE;
-        if (own) {
+        if (TOPO && own) {
           const uint64_t D = tr.zfull & vr.zn;
           bool ok = true;
           for (uint64_t m = own & d.tg_zone; m && ok; m &= m - 1) {
@@ -1571,7 +1571,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           cr->ctb = tr.ctb & vr.ctb;
           cr->zfull = tr.zfull & vr.zn & (ttz != NONE ? 1ull << ttz : ~0ull);
           cr->zflags = ttz != NONE ? 0u : (tr.zflags & vr.zflags);
-          if (d.TG) {
+          if (TOPO) {
             // <U> Topology.Register(hostname placeholder) + Record
             for (uint32_t h = 0; h < d.TGH; h++) d.hc[(size_t)h * d.max_claims + cbase + j] = 0;
             for (uint64_t m = vr.t_sel; m; m &= m - 1) {
@@ -1726,15 +1726,16 @@ extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32
 // every instantiation may use all LDS its static footprint leaves free
 static uint32_t g_ffd_dyn_max = 0;
 
-template <uint32_t RR, bool SIM>
+template <uint32_t RR, bool SIM, bool TOPO = false>
 static hipError_t ffd_attr(uint32_t lds_total) {
   constexpr uint32_t NT = SIM ? FB_SIM : FB_MAX;
   hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM, NT>);
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM, NT, TOPO>);
   if (e != hipSuccess) return e;
   const uint32_t dyn = lds_total > a.sharedSizeBytes ? lds_total - (uint32_t)a.sharedSizeBytes : 0;
   if (!g_ffd_dyn_max || dyn < g_ffd_dyn_max) g_ffd_dyn_max = dyn;
-  return hipFuncSetAttribute((const void*)ffd_kernel<RR, SIM, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  return hipFuncSetAttribute((const void*)ffd_kernel<RR, SIM, NT, TOPO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)dyn);
 }
 
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
@@ -1744,7 +1745,11 @@ extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
                        ffd_attr<7, false>(lds_total), ffd_attr<8, false>(lds_total), ffd_attr<1, true>(lds_total),
                        ffd_attr<2, true>(lds_total), ffd_attr<3, true>(lds_total), ffd_attr<4, true>(lds_total),
                        ffd_attr<5, true>(lds_total), ffd_attr<6, true>(lds_total), ffd_attr<7, true>(lds_total),
-                       ffd_attr<8, true>(lds_total)})
+                       ffd_attr<8, true>(lds_total), ffd_attr<1, false, true>(lds_total),
+                       ffd_attr<2, false, true>(lds_total), ffd_attr<3, false, true>(lds_total),
+                       ffd_attr<4, false, true>(lds_total), ffd_attr<5, false, true>(lds_total),
+                       ffd_attr<6, false, true>(lds_total), ffd_attr<7, false, true>(lds_total),
+                       ffd_attr<8, false, true>(lds_total)})
     if (x != hipSuccess) e = x;
   return e;
 }
@@ -1758,7 +1763,9 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds) {
   hipError_t e = hipErrorInvalidValue;
   switch (R) {
 #define GSK_OCC(k) \
-  case k: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM>, FB_SIM, lds); break;
+  case k:                                                                                                    \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM, false>, FB_SIM, lds); \
+    break;
     GSK_OCC(1) GSK_OCC(2) GSK_OCC(3) GSK_OCC(4) GSK_OCC(5) GSK_OCC(6) GSK_OCC(7) GSK_OCC(8)
 #undef GSK_OCC
   }
@@ -1771,10 +1778,13 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, d->TG);
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
-  switch (d->R * 2 + (sim ? 1 : 0)) {
-#define GSK_CASE(n)                                                                            \
-  case 2 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
-  case 2 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break;
+  if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread
+  // shape: 0 provisioning, 1 provisioning with topology spread, 2 simulations
+  switch (d->R * 4 + (sim ? 2 : (d->TG ? 1 : 0))) {
+#define GSK_CASE(n)                                                                                          \
+  case 4 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
+  case 4 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
+  case 4 * n + 2: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, false>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:
