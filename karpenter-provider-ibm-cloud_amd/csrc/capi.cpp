@@ -48,6 +48,8 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.it_namerank, e.it_namerank);
   c->upload(d.rank_to_it, e.rank_to_it);
   c->upload(d.slot_set, e.slot_set);
+  c->upload(d.off_sorted, e.off_sorted);
+  d.n_off = (uint32_t)e.off_sorted.size();
   {
     std::vector<int64_t> tv = e.thr_val;  // 4 sentinels: the device reads a 4-wide window past each range
     tv.insert(tv.end(), 4, INT64_MAX);
@@ -56,7 +58,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.thr_off, e.thr_off);
   {
     // threshold rows re-strided to OW words (16-B aligned rows for the scan)
-    const uint32_t OW = std::max<uint32_t>(4, (e.W + 1) & ~1u);
+    const uint32_t OW = std::max<uint32_t>(4, (e.W + 3) & ~3u);
     const size_t nrows = e.W ? e.thr_set.size() / e.W : 0;
     std::vector<uint64_t> ts(std::max<size_t>(nrows, 1) * OW, 0);
     for (size_t q = 0; q < nrows; q++)
@@ -67,6 +69,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.fk_isint, e.fk_isint);
   c->upload(d.tmpl, e.tmpl);
   c->upload(d.t_opts, e.t_opts);
+  c->upload(d.t_limopts, e.t_limopts);
   c->upload(d.t_fk, e.t_fk);
   c->upload(d.pod_req, e.pod_req);
   c->upload(d.var_begin, e.var_begin);
@@ -100,7 +103,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   const size_t PA = sims ? sims->pods.size() : e.P;
   const size_t CA = sims ? sims->pods.size() : d.max_claims;
   const size_t NS = sims ? sims->evaluated.size() : 0;
-  d.OW = std::max<uint32_t>(4, (e.W + 1) & ~1u);
+  d.OW = std::max<uint32_t>(4, (e.W + 3) & ~3u);
   c->alloc(d.rows, VT * d.OW);
   c->alloc(d.cheapest, VT);
   c->alloc(d.nfo, VT);

@@ -43,6 +43,7 @@ struct Frame {
 struct Shared {
   uint32_t pod, var, stop, M, modkind, modpos, qhead, qlen, epoch, nlog, status, found;
   uint32_t fast_path, modpos_sorted;
+  uint32_t rot_lo, rot_hi;  // fast path: the one rotation partialInsertionSort performs
   int piv, hint;
   uint64_t pops, generic, fast, cand, cand_full, node_evals, node_prefix;
   uint32_t failed;
@@ -377,6 +378,34 @@ struct Blk {
     }
     sync();
     return total;
+  }
+  // One rotation of [lo, hi] staged through registers across a single
+  // barrier: left = the element at lo moves to hi (the rest shift left),
+  // otherwise the element at hi moves to lo.  Each thread owns destinations
+  // lo + tid + i*FB (i < KR); returns false when the range is too long.
+  static constexpr int KR = 8;
+  __device__ bool rotate1(int lo, int hi, bool left) {
+    if (hi - lo + 1 > KR * FB) return false;
+    uint16_t vs[KR], vo[KR];
+#pragma unroll
+    for (int i = 0; i < KR; i++) {
+      const int k = lo + (int)tid + i * FB;
+      if (k <= hi) {
+        const int src = left ? (k == hi ? lo : k + 1) : (k == lo ? hi : k - 1);
+        vs[i] = sc[src];
+        vo[i] = ord[src];
+      }
+    }
+    sync();
+#pragma unroll
+    for (int i = 0; i < KR; i++) {
+      const int k = lo + (int)tid + i * FB;
+      if (k <= hi) {
+        sc[k] = vs[i];
+        ord[k] = vo[i];
+      }
+    }
+    return true;
   }
   // shift [lo,hi) right by one; the element at hi lands at lo
   __device__ void rotate_right(int lo, int hi) {
@@ -1081,10 +1110,34 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             int hint;
             ss.choose_pivot_fast(0, (int)M, &hint);
             if (hint == 1 && M >= 50) {
-              // partialInsertionSort fixes the single inversion;
-              // the landing position is found by the block below
+              // partialInsertionSort fixes the single inversion:
+              // one rotation; its far end by binary search over the sorted
+              // remainder (INC: first k > q with count >= x; APPEND: first
+              // k < M-1 with count > x)
               fast = S.modkind;
               S.fast++;
+              if (S.modkind == MOD_INC) {
+                const uint32_t q = S.modpos;
+                const uint16_t x = s_sc[q];
+                uint32_t lo = q + 1, hi = M;
+                while (lo < hi) {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (s_sc[mid] < x) lo = mid + 1;
+                  else hi = mid;
+                }
+                S.rot_lo = q;
+                S.rot_hi = lo - 1;
+              } else {
+                const uint16_t x = s_sc[M - 1];
+                uint32_t lo = 0, hi = M - 1;
+                while (lo < hi) {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (s_sc[mid] <= x) lo = mid + 1;
+                  else hi = mid;
+                }
+                S.rot_lo = lo;
+                S.rot_hi = M - 1;
+              }
             } else {
               generic = 1;
               S.generic++;
@@ -1100,7 +1153,9 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           S.dbg[3] += tq - tA;
         }
         const uint32_t fp = S.fast_path;
-        if (fp == MOD_INC) {
+        if ((fp == MOD_INC || fp == MOD_APPEND) && blk.rotate1((int)S.rot_lo, (int)S.rot_hi, fp == MOD_INC)) {
+          // done: one staged rotation
+        } else if (fp == MOD_INC) {
           // X (at q, count x) moves right past the run of counts < x
           const uint32_t q = S.modpos_sorted, x = s_sc[q];
           uint32_t e = M;
@@ -1309,20 +1364,40 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
 #pragma unroll
                 for (uint32_t w = 0; w < WREG; w++) acc |= nx[w];
               } else {
-                for (uint32_t w = 0; w < W && !acc; w++) {
-                  uint64_t x = opts[w] & row[w];
+                // 4 words per round trip (16-B loads; strides are multiples of
+                // 4 words), stop at the first batch with a surviving type
+                for (uint32_t w0 = 0; w0 < W && !acc; w0 += 4) {
+                  const uint4* oq = (const uint4*)(opts + w0);
+                  const uint4* rq4 = (const uint4*)(row + w0);
+                  const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+                  uint64_t x[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                   (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                   (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                   (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
 #pragma unroll
-                  for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
-                  if (x && G != Gt) {
-                    uint64_t off = 0, gm = G;
-                    while (gm) {
-                      const uint32_t g = __ffsll((long long)gm) - 1;
-                      gm &= gm - 1;
-                      off |= slot[(size_t)g * W + w];
-                    }
-                    x &= off;
+                  for (uint32_t r = 0; r < RR; r++) {
+                    if (mm[r] == cur[r]) continue;  // opts ⊆ thr_set[cur] already
+                    const uint4* tq = (const uint4*)(dd.thr_set + (size_t)mrow[r] * OW + w0);
+                    const uint4 t0 = tq[0], t1 = tq[1];
+                    x[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                    x[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                    x[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                    x[3] &= ((uint64_t)t1.w << 32) | t1.z;
                   }
-                  acc |= x;
+#pragma unroll
+                  for (uint32_t w = 0; w < 4; w++) {
+                    if (w0 + w >= W) x[w] = 0;  // padding words are not written
+                    if (x[w] && G != Gt) {
+                      uint64_t off = 0, gm = G;
+                      while (gm) {
+                        const uint32_t g = __ffsll((long long)gm) - 1;
+                        gm &= gm - 1;
+                        off |= slot[(size_t)g * W + w0 + w];
+                      }
+                      x[w] &= off;
+                    }
+                    acc |= x[w];
+                  }
                 }
               }
               feas = acc != 0;

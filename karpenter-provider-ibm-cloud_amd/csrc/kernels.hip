@@ -26,84 +26,115 @@ constexpr int BLOCK = 256;
 }  // namespace
 
 // ===================================================================== K1/K2
-// one wave per (variant v, template t); lane i of step w = instance type w*64+i
+// One wave per (variant v, template t).  The row is word-parallel bitset
+// algebra over instance types (lane w holds IT word w):
+//   row = template options (static: within NodePool limits)
+//       AND_r  thr_set[r][lower_bound(thr_val_r, daemon_r + pod_r)]   (Fits)
+//       AND    OR_{pair g in grid(template, pod)} slot_set[g]          (offering)
+//       AND    IT-key requirement bits (only for variants that have IT-key
+//              requirements: lane = IT, __ballot per word)
+// nfo = sum_g popcount(row AND slot_set[g]); the cheapest instance type is
+// the first entry of the (price rank, name rank)-sorted offering list whose
+// IT is in the row and whose pair is in the grid (= OrderByPrice(...)[0]).
 // static_mode = 1 (gs_feasibility): a NodeClaim opened for the pod alone, with
 // the free-key Compatible check and the NodePool limits folded into the row.
-// static_mode = 0 (FFD): rows carry only the monotone predicates (taints, IT
-// requirements, fits, offerings); the free-key check against the fresh
-// template goes to fk_ok[] because an in-flight NodeClaim can gain keys that
-// make a later pod compatible.
+// static_mode = 0 (FFD): rows carry only the monotone predicates; the
+// free-key check against the fresh template goes to fk_ok[] because an
+// in-flight NodeClaim can gain keys that make a later pod compatible.
 extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode) {
-  const uint32_t lane = threadIdx.x & 63;
-  // wave-uniform in SGPRs: the variant record is read in place (scalar
-  // loads), never copied into a dynamically indexed private array (scratch)
-  const uint32_t pair = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+  __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's row (N <= 8192)
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave-uniform in SGPRs: the variant record is read in place
+  const uint32_t pair = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + wv);
   if (pair >= d.V * d.T) return;  // wave-uniform
   const uint32_t v = pair / d.T, t = pair % d.T;
   const VarRec& vr = d.vars[v];
   const TmplRec& tr = d.tmpl[t];
-  uint64_t* rowout = d.rows + (size_t)pair * d.OW;
+  const uint32_t W = d.W, OW = d.OW, R = d.R;
+  uint64_t* rowout = d.rows + (size_t)pair * OW;
 
   // wave-uniform parts of NodeClaim.CanAdd on a fresh NodeClaim
   bool ok_all = (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
   const bool fk_ok = var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
   if (static_mode) ok_all = ok_all && fk_ok;
-  int64_t dem[RMAX];
-  const int64_t* preq = d.pod_req + (size_t)vr.pod * d.R;
-#pragma unroll
-  for (uint32_t r = 0; r < RMAX; r++) dem[r] = r < d.R ? tr.daemon[r] + preq[r] : 0;  // Merge(daemon, pod)
   const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C);
-  const bool lim = static_mode && tr.has_limits;
-
-  uint64_t best = ~0ull;
-  uint32_t nf = 0;
-  for (uint32_t w = 0; w < d.W; w++) {
-    const uint32_t i = w * 64 + lane;
-    bool ok = ok_all && i < d.N && ((d.t_opts[(size_t)t * d.W + w] >> lane) & 1);
-    if (ok) {
-      // <U> compatible(it, reqs): it.Requirements.Intersects(reqs) on IT keys
-      for (uint32_t k = 0; k < d.K; k++) {
-        const uint32_t off = vr.itmask_off[k];
-        if (off == NONE) continue;
-        const uint32_t vid = d.it_vid[(size_t)k * d.N + i];
-        ok = ok && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
-      }
-    }
-    if (ok) {
-      // <U> resources.Fits(requests, it.Allocatable())
+  if (!G) ok_all = false;
+  // <U> resources.Fits(Merge(daemon, pod), allocatable): lane r finds the
+  // first threshold >= the demand of resource r
+  uint32_t cur = 0;
+  if (lane < R) {
+    const int64_t dem = tr.daemon[lane] + d.pod_req[(size_t)vr.pod * R + lane];
+    const uint32_t o = d.thr_off[lane];
+    cur = o + lane + lower_bound_i64(d.thr_val + o, d.thr_off[lane + 1] - o, dem);
+  }
+  // every lane gets every cursor (shuffles in wave-uniform control flow)
+  uint32_t curs[RMAX];
 #pragma unroll
-      for (uint32_t r = 0; r < RMAX; r++) ok = ok && (r >= d.R || d.it_alloc[(size_t)r * d.N + i] >= dem[r]);
+  for (uint32_t r = 0; r < RMAX; r++) curs[r] = (uint32_t)__shfl((int)cur, (int)r);
+  bool itkeys = false;
+  for (uint32_t k = 0; k < d.K; k++) itkeys = itkeys || vr.itmask_off[k] != NONE;
+  const uint64_t* topts = (static_mode && tr.has_limits ? d.t_limopts : d.t_opts) + (size_t)t * W;
+
+  uint32_t nf = 0;
+  uint64_t any = 0;
+  for (uint32_t w0 = 0; w0 < W; w0 += 64) {
+    const uint32_t w = w0 + lane;
+    uint64_t x = 0;
+    if (ok_all && w < W) {
+      x = topts[w];
+#pragma unroll
+      for (uint32_t r = 0; r < RMAX; r++)
+        if (r < R) x &= d.thr_set[(size_t)curs[r] * OW + w];
+      uint64_t off = 0;
+      for (uint64_t m = G; m; m &= m - 1) off |= d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w];
+      x &= off;
     }
-    if (ok && lim) {
-      // <U> filterByRemainingResources
-      for (uint32_t r = 0; r < d.R; r++)
-        if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= tr.limits[r];
-    }
-    // <U> offering.Available && reqs.IsCompatible(offering.Requirements)
-    const uint64_t pm = ok ? (d.it_pair[i] & G) : 0;
-    ok = pm != 0;
-    const uint64_t word = __ballot(ok);
-    if (lane == 0) rowout[w] = word;
-    if (ok) {
-      nf += __popcll(pm);
-      uint32_t minp = NONE;
-      uint64_t m = pm;
-      while (m) {
-        const uint32_t g = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const uint32_t pr = d.it_prank[(size_t)i * 64 + g];
-        minp = pr < minp ? pr : minp;
+    if (itkeys && ok_all) {
+      // <U> compatible(it, reqs): it.Requirements.Intersects(reqs) on IT keys
+      const uint32_t wend = W - w0 < 64 ? W - w0 : 64;
+      for (uint32_t q = 0; q < wend; q++) {
+        const uint64_t wx = (uint64_t)__shfl((long long)x, q);
+        if (!wx) continue;  // wave-uniform
+        const uint32_t i = (w0 + q) * 64 + lane;
+        bool ok = (wx >> lane) & 1;
+        for (uint32_t k = 0; k < d.K && ok; k++) {
+          const uint32_t off = vr.itmask_off[k];
+          if (off == NONE) continue;
+          const uint32_t vid = d.it_vid[(size_t)k * d.N + i];
+          ok = (d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1;
+        }
+        const uint64_t bits = __ballot(ok);
+        if (lane == q) x = bits;
       }
-      const uint64_t key = ((uint64_t)minp << 32) | d.it_namerank[i];
-      best = key < best ? key : best;
+    }
+    if (w < W) {
+      rowout[w] = x;
+      if (w < 128) s_row[wv][w] = x;
+      // offerings: sum over grid pairs of row AND slot_set[g]
+      for (uint64_t m = G; m; m &= m - 1) nf += __popcll(x & d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w]);
+    }
+    any |= x;
+  }
+  nf = wave_sum_u32(nf);
+  uint32_t cheapest = NONE;
+  if (__ballot(any != 0)) {
+    // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
+    // IT is in the row and whose (zone, capacity type) pair is in the grid
+    for (uint32_t base = 0; base < d.n_off; base += 64) {
+      const uint32_t e = base + lane < d.n_off ? d.off_sorted[base + lane] : NONE;
+      const uint32_t i = e & 0xFFFFu, g = e >> 16;
+      const bool hit = e != NONE && ((G >> g) & 1) && ((s_row[wv][i >> 6] >> (i & 63)) & 1);
+      const uint64_t b = __ballot(hit);
+      if (b) {
+        cheapest = (uint32_t)__shfl((int)i, (int)(__ffsll((long long)b) - 1));
+        break;
+      }
     }
   }
-  best = wave_min_u64(best);
-  nf = wave_sum_u32(nf);
   if (lane == 0) {
     d.fk_ok[pair] = fk_ok ? 1u : 0u;
     d.nfo[pair] = nf;
-    d.cheapest[pair] = best == ~0ull ? NONE : d.rank_to_it[(uint32_t)best];
+    d.cheapest[pair] = cheapest;
   }
 }
 

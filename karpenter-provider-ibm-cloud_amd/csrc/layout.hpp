@@ -154,7 +154,7 @@ struct DevProblem {
   uint32_t N, W, R, Z, C, T, F, V, P, K, NT;  // K = IT keys, NT = taint vocab
   uint32_t NN;                                // existing nodes
   uint32_t RQ;                                // resources in the LDS slack prefilter (<= 4)
-  uint32_t OW;                                // c_opts stride: max(4, W rounded up to even)
+  uint32_t OW;                                // row / option / threshold stride: max(4, W rounded up to 4)
   uint32_t n_thr;                             // thr_off[R] (host copy: sizes the dynamic LDS)
   uint32_t max_claims;
   uint64_t wk_slots;  // free slots whose key is well-known
@@ -167,6 +167,8 @@ struct DevProblem {
   const uint32_t* it_namerank; // [N]
   const uint32_t* rank_to_it;  // [N]
   const uint64_t* slot_set;    // [64][W] ITs with an available offering on pair g
+  const uint32_t* off_sorted;  // [n_off] available offerings (it | pair << 16) in (price rank, name rank) order
+  uint32_t n_off, pad_off;
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
   const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
@@ -175,6 +177,7 @@ struct DevProblem {
   // templates
   const TmplRec* tmpl;         // [T]
   const uint64_t* t_opts;      // [T][W]
+  const uint64_t* t_limopts;   // [T][W] t_opts within the NodePool limits (static matrix)
   const FK* t_fk;              // [T][F]
   // pods
   const int64_t* pod_req;      // [P][R]
