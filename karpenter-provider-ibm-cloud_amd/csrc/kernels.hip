@@ -57,7 +57,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   bool ok_all = (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
   const bool fk_ok = var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
   if (static_mode) ok_all = ok_all && fk_ok;
-  const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C);
+  const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C), Gt = grid_of(tr.zm, tr.cm, d.Z, d.C);
   if (!G) ok_all = false;
   // <U> resources.Fits(Merge(daemon, pod), allocatable): lane r finds the
   // first threshold >= the demand of resource r
@@ -85,9 +85,11 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
 #pragma unroll
       for (uint32_t r = 0; r < RMAX; r++)
         if (r < R) x &= d.thr_set[(size_t)curs[r] * OW + w];
-      uint64_t off = 0;
-      for (uint64_t m = G; m; m &= m - 1) off |= d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w];
-      x &= off;
+      if (G != Gt) {  // template options already have an offering on the template's grid
+        uint64_t off = 0;
+        for (uint64_t m = G; m; m &= m - 1) off |= d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w];
+        x &= off;
+      }
     }
     if (itkeys && ok_all) {
       // <U> compatible(it, reqs): it.Requirements.Intersects(reqs) on IT keys
@@ -111,13 +113,15 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
       rowout[w] = x;
       if (w < 128) s_row[wv][w] = x;
       // offerings: sum over grid pairs of row AND slot_set[g]
-      for (uint64_t m = G; m; m &= m - 1) nf += __popcll(x & d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w]);
+      // (the Solve's rows need neither the offering count nor the cheapest type)
+      if (static_mode)
+        for (uint64_t m = G; m; m &= m - 1) nf += __popcll(x & d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w]);
     }
     any |= x;
   }
   nf = wave_sum_u32(nf);
   uint32_t cheapest = NONE;
-  if (__ballot(any != 0)) {
+  if (static_mode && __ballot(any != 0)) {
     // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
     // IT is in the row and whose (zone, capacity type) pair is in the grid
     for (uint32_t base = 0; base < d.n_off; base += 64) {

@@ -21,6 +21,8 @@ for _ in range(5):
     f, r = s.feasibility()
     ts.append(r.t_kernel_ms)
 print("feas_kernel_ms", [round(x, 3) for x in ts], "checks", r.checks, flush=True)
+s.run()
+print("solve_feas_kernel_ms (rows only)", round(s.last_run_ms()[0], 4), flush=True) if "--solve" not in sys.argv else None
 if "--solve" in sys.argv:
     t0 = time.time()
     s.run()
