@@ -78,6 +78,20 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.itmask, e.itmask);
   c->upload(d.fk_entries, e.fk_entries);
   c->upload(d.queue0, e.queue0);
+  if (!sims) {
+    // the first pass over the queue pops pods in queue0 order with their first
+    // variant: records laid out in that order let the kernel prefetch the next
+    // pod in one round trip
+    std::vector<gsd::VarRec> qv(std::max<uint32_t>(e.P, 1));
+    std::vector<int64_t> qr((size_t)std::max<uint32_t>(e.P, 1) * std::max<uint32_t>(e.R, 1), 0);
+    for (uint32_t k = 0; k < e.P; k++) {
+      const uint32_t p = e.queue0[k];
+      qv[k] = e.vars[e.var_begin[p]];
+      for (uint32_t r = 0; r < e.R; r++) qr[(size_t)k * e.R + r] = e.pod_req[(size_t)p * e.R + r];
+    }
+    c->upload(d.qvars, qv);
+    c->upload(d.qreqs, qr);
+  }
   d.NN = e.NN;
   // topology spread groups
   d.TG = e.TG;

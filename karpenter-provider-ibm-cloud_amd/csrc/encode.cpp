@@ -1094,6 +1094,7 @@ struct Ctx {
         vr.zs = zone_full(pv.strict);
         vr.zn = zone_full(pv.reqs);
         vr.zflags = zone_flags(pv.reqs);
+        vr.vix = v;
         vr.tol = pv.tol;
         vr.tolt = 0;
         for (uint32_t t = 0; t < e.T; t++)

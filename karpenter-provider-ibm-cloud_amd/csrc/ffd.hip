@@ -58,6 +58,7 @@ struct Shared {
   // solve in this block: simulation id, pod/claim arena offset, global pod id,
   // overlay entry count / the entry being written (and whether it is new)
   uint32_t sim, qoff, gpod, nov, ove, ov_new;
+  uint32_t wrapped;  // the queue head has wrapped: pods now come back from Push
   alignas(16) uint32_t vrb[2][(sizeof(VarRec) / 4 + 3) & ~3u];
   alignas(16) int64_t reqb[2][RMAX];
 };
@@ -823,6 +824,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       S.status = 0;
       S.nx_valid = 0;
       S.cb = 0;
+      S.wrapped = 0;
     }
     __syncthreads();
     const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
@@ -854,17 +856,20 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       // publish last iteration's prefetch into the spare buffer
       if (wave == 1) {
         const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
-        if (st == 3) {
+        if (st == 3 || st == 4) {
           const uint32_t nb = S.cb ^ 1u;
           if (lane < VR_DW) S.vrb[nb][lane] = pf_vr;
           if (lane >= 32 && lane < 32 + 2 * RR) ((uint32_t*)S.reqb[nb])[lane - 32] = pf_rq;
+          // first-pass records carry their pod and variant ids; such a pod
+          // was never pushed (last epoch / length 0)
+          const uint32_t rpod = (uint32_t)__shfl((int)pf_vr, 0), rvix = (uint32_t)__shfl((int)pf_vr, VR_DW - 1);
           if (lane == 0) {
             S.nx_valid = 1;
-            S.nx_pod = pf_pod;
-            S.nx_gp = pf_gp;
-            S.nx_le = pf_le;
-            S.nx_ll = pf_ll;
-            S.nx_cv = pf_cv;
+            S.nx_pod = st == 4 ? rpod : pf_pod;
+            S.nx_gp = st == 4 ? rpod : pf_gp;
+            S.nx_le = st == 4 ? 0u : pf_le;
+            S.nx_ll = st == 4 ? 0u : pf_ll;
+            S.nx_cv = st == 4 ? rvix : pf_cv;
           }
         } else if (lane == 0) {
           S.nx_valid = 0;
@@ -900,6 +905,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           if (le == S.epoch && ll == S.qlen) {
             stop = 1;
           } else {
+            if (S.qhead + 1 == P) S.wrapped = 1;
             S.qhead = S.qhead + 1 == P ? 0 : S.qhead + 1;
             S.qlen--;
             S.pops++;
@@ -929,9 +935,18 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       const int64_t* preq = S.reqb[S.cb];
       // stage 1: the next pod id (its queue slot cannot change during this pod
       // unless the queue is empty now, when this pod itself may come back)
-      if (wave == 1 && lane == 0 && S.qlen > 0) {
-        pf_pod = queue[S.qhead];
-        pf_state = 1;
+      if (wave == 1 && S.qlen > 0) {
+        if (!SIM && !S.wrapped) {
+          // first pass: the next pod is queue0[qhead] with its first variant,
+          // its records are contiguous in queue order: one round trip
+          const uint32_t k = S.qhead;
+          if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.qvars + k))[lane];
+          if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.qreqs + (size_t)k * R))[lane - 32];
+          pf_state = 4;
+        } else if (lane == 0) {
+          pf_pod = queue[S.qhead];
+          pf_state = 1;
+        }
       }
       const uint32_t M = S.M;
       uint64_t tA = 0;

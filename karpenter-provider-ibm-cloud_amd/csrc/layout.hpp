@@ -62,7 +62,7 @@ struct VarRec {
   uint64_t t_own, t_sel;
   uint64_t zs, zn;
   uint32_t zflags;               // ZF_COMP of the full zone requirement
-  uint32_t pad2;
+  uint32_t vix;                  // this record's own variant index
 };
 static_assert(sizeof(VarRec) == 128, "VarRec layout");
 
@@ -187,6 +187,8 @@ struct DevProblem {
   const uint64_t* itmask;      // arena
   const FKEntry* fk_entries;
   const uint32_t* queue0;      // [P] initial queue order
+  const VarRec* qvars;         // [P] first variant of queue0[k], in queue order (first-pass prefetch)
+  const int64_t* qreqs;        // [P][R] requests of queue0[k]
   const NodeRec* nodes0;       // [NN] in <U> order: initialized first, then name
   const FK* n_fk0;             // [NN][F] free-key requirement state per node
   NodeRec* nodes;              // working copies (reset at every run)
