@@ -244,6 +244,12 @@ typedef struct gs_feas_result {
   const uint32_t* n_feasible_offerings; /* [n_pods][n_nodepools] */
   uint64_t checks;
   double t_kernel_ms;
+  /* OrderByPrice key of the cheapest type: (price_rank << 32) | name_rank,
+   * UINT64_MAX when the row is empty.  Keys order exactly like Go's
+   * (price, name) comparison, so a MIN over shards is the global cheapest. */
+  const uint64_t* cheapest_key;   /* [n_pods][n_nodepools] */
+  const uint32_t* it_name_rank;   /* [n_its] bytewise rank of each type's name */
+  uint32_t word_begin, word_end;  /* instance-type words this result covers */
 } gs_feas_result;
 
 typedef struct gs_ctx gs_ctx;
@@ -354,6 +360,12 @@ gs_status gs_solve(gs_ctx* ctx, const gs_problem* problem, gs_result* out);
 
 /* static feasibility matrix only (K1/K2) on a prepared problem */
 gs_status gs_feasibility(gs_ctx* ctx, gs_feas_result* out);
+/* one instance-type column shard of it: only words
+ * [word_begin, word_end) are evaluated; rows carry only those words,
+ * n_feasible_offerings counts only those types and cheapest_key is the
+ * shard's minimum.  Shards combine exactly: rows OR (disjoint words, so an
+ * integer SUM all-reduce works), offering counts SUM, cheapest_key MIN. */
+gs_status gs_feasibility_shard(gs_ctx* ctx, uint32_t word_begin, uint32_t word_end, gs_feas_result* out);
 
 /* host-only: run the encoder (no device needed) and report whether this
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.

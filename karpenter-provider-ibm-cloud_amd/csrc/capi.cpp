@@ -120,6 +120,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.OW = std::max<uint32_t>(4, (e.W + 3) & ~3u);
   c->alloc(d.rows, VT * d.OW);
   c->alloc(d.cheapest, VT);
+  c->alloc(d.cheapest_key, VT);
   c->alloc(d.nfo, VT);
   c->alloc(d.fk_ok, VT);
   c->alloc(d.queue, PA);
@@ -170,7 +171,9 @@ uint32_t trunc_lds_bytes(uint32_t N) {
   return np2 * 8;
 }
 
-void launch_feas(gs_ctx* c, uint32_t apply_limits) { HIPCHK(gsk_feas(&c->dp, apply_limits, c->stream)); }
+void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u) {
+  HIPCHK(gsk_feas(&c->dp, apply_limits, w_lo, w_hi, c->stream));
+}
 
 // device capacity of the encoded problem (the FFD kernel keeps these in LDS)
 gsh::Err capacity_check(const gsh::Encoded& e) {
@@ -459,18 +462,20 @@ gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
   return gs_fetch(c, out);
 }
 
-gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
+gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
   auto& e = c->enc;
   const uint32_t P = e.P, NP = c->problem->n_nodepools, W = e.W;
+  word_end = std::min(word_end, W);
+  if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
   float ms = 0;
   const uint32_t OW = c->dp.OW;
-  std::vector<uint64_t> rows((size_t)e.V * e.T * OW);
+  std::vector<uint64_t> rows((size_t)e.V * e.T * OW), key((size_t)e.V * e.T);
   std::vector<uint32_t> ch((size_t)e.V * e.T), nfo((size_t)e.V * e.T);
   try {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    launch_feas(c, 1);
+    launch_feas(c, 1, word_begin, word_end);
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[5]));
     HIPCHK(hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
@@ -478,6 +483,7 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
     if (!ch.empty()) {
       HIPCHK(hipMemcpy(ch.data(), c->dp.cheapest, ch.size() * 4, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(nfo.data(), c->dp.nfo, nfo.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(key.data(), c->dp.cheapest_key, key.size() * 8, hipMemcpyDeviceToHost));
     }
   } catch (const HipError& ex) {
     return fail(c, GS_E_HIP, ex.msg);
@@ -485,6 +491,7 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
   c->f_rows.assign((size_t)P * NP * W, 0);
   c->f_cheapest.assign((size_t)P * NP, -1);
   c->f_nfo.assign((size_t)P * NP, 0);
+  c->f_key.assign((size_t)P * NP, ~0ull);
   for (uint32_t p = 0; p < P; p++) {
     const uint32_t v = e.var_begin[p];  // the pod as given (no relaxation)
     for (uint32_t t = 0; t < e.T; t++) {
@@ -493,6 +500,7 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
       std::memcpy(&c->f_rows[dst * W], &rows[src * OW], W * 8);
       c->f_cheapest[dst] = ch[src] == gsd::NONE ? -1 : (int32_t)ch[src];
       c->f_nfo[dst] = nfo[src];
+      c->f_key[dst] = key[src];
     }
   }
   std::memset(out, 0, sizeof(*out));
@@ -505,7 +513,13 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) {
   out->n_feasible_offerings = c->f_nfo.data();
   out->checks = e.checks;
   out->t_kernel_ms = ms;
+  out->cheapest_key = c->f_key.data();
+  out->it_name_rank = e.it_namerank.data();
+  out->word_begin = word_begin;
+  out->word_end = word_end;
   return GS_OK;
 }
+
+gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) { return gs_feasibility_shard(c, 0, ~0u, out); }
 
 }  // extern "C"

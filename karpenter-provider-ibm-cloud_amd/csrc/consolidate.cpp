@@ -273,7 +273,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   try {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(gsk_feas(&d, 0, c->stream));
+    HIPCHK(gsk_feas(&d, 0, 0, ~0u, c->stream));
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (NS) {
       HIPCHK(hipMemsetAsync(d.sim_next, 0, sizeof(uint32_t), c->stream));

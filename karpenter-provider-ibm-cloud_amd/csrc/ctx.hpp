@@ -20,7 +20,8 @@ extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
 extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds);
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
                                       uint32_t TG);
-extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, hipStream_t s);
+extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
+                               hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
 
@@ -76,6 +77,7 @@ struct gs_ctx {
   std::vector<uint64_t> f_rows;
   std::vector<int32_t> f_cheapest;
   std::vector<uint32_t> f_nfo;
+  std::vector<uint64_t> f_key;
   gsd::Ctrl ctrl{};
   // consolidation: the combined problem (pending ++ bound pods), the plan,
   // the input copy (rerun) and result storage

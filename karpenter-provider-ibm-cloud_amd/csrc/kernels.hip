@@ -41,7 +41,8 @@ constexpr int BLOCK = 256;
 // static_mode = 0 (FFD): rows carry only the monotone predicates; the
 // free-key check against the fresh template goes to fk_ok[] because an
 // in-flight NodeClaim can gain keys that make a later pod compatible.
-extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode) {
+extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode, uint32_t w_lo,
+                                                                uint32_t w_hi) {
   __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's row (N <= 8192)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // wave-uniform in SGPRs: the variant record is read in place
@@ -80,7 +81,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   for (uint32_t w0 = 0; w0 < W; w0 += 64) {
     const uint32_t w = w0 + lane;
     uint64_t x = 0;
-    if (ok_all && w < W) {
+    if (ok_all && w >= w_lo && w < w_hi) {  // this instance-type column shard
       x = topts[w];
 #pragma unroll
       for (uint32_t r = 0; r < RMAX; r++)
@@ -121,6 +122,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   }
   nf = wave_sum_u32(nf);
   uint32_t cheapest = NONE;
+  uint64_t ckey = ~0ull;
   if (static_mode && __ballot(any != 0)) {
     // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
     // IT is in the row and whose (zone, capacity type) pair is in the grid
@@ -130,7 +132,10 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
       const bool hit = e != NONE && ((G >> g) & 1) && ((s_row[wv][i >> 6] >> (i & 63)) & 1);
       const uint64_t b = __ballot(hit);
       if (b) {
-        cheapest = (uint32_t)__shfl((int)i, (int)(__ffsll((long long)b) - 1));
+        const int src = (int)(__ffsll((long long)b) - 1);
+        cheapest = (uint32_t)__shfl((int)i, src);
+        const uint32_t gg = (uint32_t)__shfl((int)g, src);
+        ckey = ((uint64_t)d.it_prank[(size_t)cheapest * 64 + gg] << 32) | d.it_namerank[cheapest];
         break;
       }
     }
@@ -139,6 +144,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
     d.fk_ok[pair] = fk_ok ? 1u : 0u;
     d.nfo[pair] = nf;
     d.cheapest[pair] = cheapest;
+    if (static_mode) d.cheapest_key[pair] = ckey;
   }
 }
 
@@ -212,11 +218,12 @@ extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes) {
                              (int)trunc_lds_bytes);
 }
 
-extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, hipStream_t s) {
+extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, uint32_t w_lo, uint32_t w_hi,
+                               hipStream_t s) {
   const uint64_t pairs = (uint64_t)d->V * d->T;
   if (!pairs) return hipSuccess;
   const uint32_t blocks = (uint32_t)((pairs + (BLOCK / 64) - 1) / (BLOCK / 64));
-  hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(BLOCK), 0, s, *d, static_mode);
+  hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(BLOCK), 0, s, *d, static_mode, w_lo, w_hi);
   return hipGetLastError();
 }
 

@@ -114,6 +114,9 @@ class GsFeasResult(C.Structure):
         ("n_feasible_offerings", C.POINTER(C.c_uint32)),
         ("checks", C.c_uint64),
         ("t_kernel_ms", C.c_double),
+        ("cheapest_key", C.POINTER(C.c_uint64)),
+        ("it_name_rank", C.POINTER(C.c_uint32)),
+        ("word_begin", _U32), ("word_end", _U32),
     ]
 
 
@@ -160,7 +163,12 @@ def feas_to_dict(res: GsFeasResult) -> dict:
     rows = _arr(res.rows, P * T * W, np.uint64).reshape(P, T, W) if P * T * W else np.zeros((P, T, W), np.uint64)
     cheapest = _arr(res.cheapest_it, P * T, np.int32).reshape(P, T)
     nfo = _arr(res.n_feasible_offerings, P * T, np.uint32).reshape(P, T)
-    return {"rows": rows, "cheapest": cheapest, "n_feasible_offerings": nfo, "checks": int(res.checks)}
+    out = {"rows": rows, "cheapest": cheapest, "n_feasible_offerings": nfo, "checks": int(res.checks)}
+    if res.cheapest_key:  # product results (the oracle reports no keys)
+        out["cheapest_key"] = _arr(res.cheapest_key, P * T, np.uint64).reshape(P, T)
+        out["it_name_rank"] = _arr(res.it_name_rank, res.n_its, np.uint32)
+        out["word_range"] = (int(res.word_begin), int(res.word_end))
+    return out
 
 
 # ------------------------------------------------------------ consolidation

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(HERE, "libgpusched.so")
 
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
-           "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose"]
+           "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard"]
 
 
 class GpuSchedError(RuntimeError):
@@ -47,6 +47,8 @@ def load():
         L.gs_solve.restype = C.c_int
         L.gs_feasibility.argtypes = [vp, C.POINTER(abi.GsFeasResult)]
         L.gs_feasibility.restype = C.c_int
+        L.gs_feasibility_shard.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.GsFeasResult)]
+        L.gs_feasibility_shard.restype = C.c_int
         L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.gs_last_error.restype = C.c_size_t
         L.gs_version.argtypes = []
@@ -181,4 +183,10 @@ class Solver:
     def feasibility(self):
         res = abi.GsFeasResult()
         self._check(self.L.gs_feasibility(self.ctx, C.byref(res)))
+        return abi.feas_to_dict(res), res
+
+    def feasibility_shard(self, word_begin, word_end):
+        """gs_feasibility_shard: the static matrix over instance-type words [begin, end)"""
+        res = abi.GsFeasResult()
+        self._check(self.L.gs_feasibility_shard(self.ctx, word_begin, word_end, C.byref(res)))
         return abi.feas_to_dict(res), res

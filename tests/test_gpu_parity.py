@@ -114,3 +114,32 @@ def test_solve_existing_nodes_c4sim(solver):
 @pytest.mark.parametrize("seed", range(40))
 def test_solve_random_with_nodes(solver, seed):
     check_solve(solver, synth.random_problem(5000 + seed, n_pods=60))
+
+
+# ------------------------------------------ IT-column shards
+@pytest.mark.parametrize("name,world", [("c2", 3), ("c3", 2), ("rand", 4)])
+def test_feasibility_shards_combine_to_whole(solver, name, world):
+    from gpusched.feasibility import combine, word_range
+    p = {"c2": lambda: synth.make_c2(n_pods=2000), "c3": lambda: synth.make_c3(n_pods=2000),
+         "rand": lambda: synth.random_problem(77, n_pods=200)}[name]()
+    st, want = pyoracle.feasibility(p)
+    assert st == abi.GS_OK
+    solver.prepare(p)
+    whole, _ = solver.feasibility()
+    W = whole["rows"].shape[-1]
+    acc = None
+    for r in range(world):
+        f, _ = solver.feasibility_shard(*word_range(W, r, world))
+        part = combine(f["rows"], f["n_feasible_offerings"], f["cheapest_key"], f["it_name_rank"], 0, 1, None)
+        if acc is None:
+            acc = part
+        else:
+            acc["rows"] = acc["rows"] + part["rows"]
+            acc["n_feasible_offerings"] = acc["n_feasible_offerings"] + part["n_feasible_offerings"]
+            take = part["cheapest_key"] < acc["cheapest_key"]
+            acc["cheapest_key"] = np.where(take, part["cheapest_key"], acc["cheapest_key"])
+            acc["cheapest"] = np.where(take, part["cheapest"], acc["cheapest"])
+    assert np.array_equal(acc["rows"], want["rows"])
+    assert np.array_equal(acc["n_feasible_offerings"], want["n_feasible_offerings"])
+    assert np.array_equal(acc["cheapest"], want["cheapest"])
+    assert np.array_equal(acc["cheapest"], whole["cheapest"])
