@@ -16,12 +16,19 @@ sweep over all 5,000 state nodes, each an independent SimulateScheduling Solve
 (one workgroup per simulation).  Simulations are sharded round-robin over the
 N ranks, their commands all-gathered (RCCL over xGMI), and the policy replayed
 on every rank: strong scaling.
+
+`stress`: the C5 workload (BASELINE configs[4]): the static pod x offering
+matrix of 200k pods x 2,000 instance types x 6 zones x 2 capacity types with
+instance-type columns sharded over the ranks and combined by RCCL all-reduces
+(SUM rows / SUM offering counts / MIN OrderByPrice key): strong scaling.
 """
 import argparse
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "karpenter-provider-ibm-cloud_amd"))
@@ -192,6 +199,103 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
     return out
 
 
+def feas_bytes(V, T, O, words):
+    """per-launch algorithmic bytes of feas_kernel over `words` instance-type
+    words: variant records, the offering list, rows + counts + keys written"""
+    return V * 128 + O * 48 + V * T * (words * 8 + 12)
+
+
+def cpu_baseline_stress(n_pods):
+    """oracle static matrix (1 thread) on the first n_pods of the C5 workload;
+    checks the GPU matrix on that sample"""
+    from oracle import pyoracle
+    problem = synth.make_c5(n_pods=n_pods)
+    t0 = time.perf_counter()
+    st, want = pyoracle.feasibility(problem)
+    dt = time.perf_counter() - t0
+    s = Solver(0)
+    try:
+        s.prepare(problem)
+        got, _ = s.feasibility()
+    finally:
+        s.close()
+    same = all(np.array_equal(got[k], want[k]) for k in ("rows", "cheapest", "n_feasible_offerings"))
+    return {"value": problem.checks() / dt, "unit": "checks/s", "cores": 1, "kind": "port",
+            "sample": f"C5, first {n_pods} pods; oracle static matrix {dt * 1e3:.0f} ms; GPU matrix on the "
+                      f"sample bit-exact: {bool(same)}"}
+
+
+def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks):
+    """C5 (BASELINE configs[4]): the static pod x offering matrix of 200k pods x
+    2,000 types x 6 zones x 2 capacity types, instance-type words sharded over
+    the ranks and combined in place by three RCCL all-reduces: strong scaling"""
+    from gpusched.feasibility import device_combine, word_range
+    problem = synth.make_c5(n_pods=args.c5_pods)
+    solver = Solver(local)
+    t0 = time.perf_counter()
+    solver.prepare(problem)
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    W = (len(problem.instance_types) + 63) // 64
+    wb, we = word_range(W, rank, world)
+
+    def step():
+        r = solver.feasibility_shard_device(wb, we)  # returns after the kernel
+        if world > 1:
+            device_combine(r, dist, device)
+            import torch
+            torch.cuda.synchronize(device)
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    kms = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+        kms.append(r.t_kernel_ms)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    ms = elapsed * 1e3 / args.steps
+    k_ms = sum(kms) / len(kms)
+    equal = None
+    if world > 1:
+        import torch
+        from gpusched.feasibility import device_views
+        got = [x.clone() for x in device_views(r, device)]
+        whole = solver.feasibility_shard_device(0, W)
+        ref = device_views(whole, device)
+        S = r.row_stride
+        equal = bool(torch.equal(got[0].view(-1, S)[:, :W], ref[0].view(-1, S)[:, :W]) and
+                     torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]))
+        equal = bool(max_over_ranks(0.0 if equal else 1.0) == 0.0)
+    ab = feas_bytes(r.n_variants, r.n_templates, len(problem.offerings), we - wb)
+    ach = ab / (k_ms * 1e-3) / 1e9
+    out = {
+        "workload": f"C5: {len(problem.pods)} pods x {len(problem.instance_types)} instance types x 6 zones x "
+                    f"2 capacity types ({len(problem.offerings)} offerings), static feasibility matrix + cheapest "
+                    f"offering per pod and NodePool",
+        "value": r.checks / (ms * 1e-3),
+        "unit": "checks/s",
+        "ms_per_step": ms,
+        "scaling": "strong",
+        "parallelism": f"it-columns{world}" if world > 1 else "single",
+        "words_per_rank": we - wb,
+        "variants": r.n_variants,
+        "kernel_ms": round(k_ms, 4),
+        "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
+        "shards_equal_whole": equal,
+        "roofline": {"kernel": "feas_kernel", "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(ab),
+                     "avg_ms": round(k_ms, 4), "traffic": load_traffic(args.traffic_json).get("feas_c5")},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_stress(args.cpu_sample_c5_pods)
+    solver.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,6 +307,9 @@ def main():
     ap.add_argument("--cpu-sample-sims", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--c5-pods", type=int, default=200_000)
+    ap.add_argument("--cpu-sample-c5-pods", type=int, default=1000)
+    ap.add_argument("--no-stress", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output, committed under profiles/)")
     args = ap.parse_args()
@@ -321,6 +428,8 @@ def main():
     solver.close()
     if not args.no_consolidation:
         line["consolidation"] = bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks)
+    if not args.no_stress:
+        line["stress"] = bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

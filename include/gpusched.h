@@ -245,8 +245,9 @@ typedef struct gs_feas_result {
   uint64_t checks;
   double t_kernel_ms;
   /* OrderByPrice key of the cheapest type: (price_rank << 32) | name_rank,
-   * UINT64_MAX when the row is empty.  Keys order exactly like Go's
-   * (price, name) comparison, so a MIN over shards is the global cheapest. */
+   * INT64_MAX when the row is empty.  Keys order exactly like Go's
+   * (price, name) comparison, signed or unsigned, so a MIN over shards is
+   * the global cheapest. */
   const uint64_t* cheapest_key;   /* [n_pods][n_nodepools] */
   const uint32_t* it_name_rank;   /* [n_its] bytewise rank of each type's name */
   uint32_t word_begin, word_end;  /* instance-type words this result covers */
@@ -366,6 +367,32 @@ gs_status gs_feasibility(gs_ctx* ctx, gs_feas_result* out);
  * shard's minimum.  Shards combine exactly: rows OR (disjoint words, so an
  * integer SUM all-reduce works), offering counts SUM, cheapest_key MIN. */
 gs_status gs_feasibility_shard(gs_ctx* ctx, uint32_t word_begin, uint32_t word_end, gs_feas_result* out);
+
+/* The same shard left in HBM for an in-place collective (one process per
+ * GPU): the matrix at pod-variant granularity (pods with equal scheduling
+ * inputs share a variant), device pointers owned by the context and valid
+ * until the next call.  Combine over ranks with
+ *   ncclAllReduce(rows, rows, n_variants*n_templates*row_stride, ncclUint64, ncclSum)
+ *   ncclAllReduce(n_feasible_offerings, ..., n_variants*n_templates, ncclUint32, ncclSum)
+ *   ncclAllReduce(cheapest_key, ..., n_variants*n_templates, ncclInt64, ncclMin)
+ * then pod p, NodePool template t reads [variant_of_pod[p]][t].  The call
+ * returns after the kernel has finished (the buffers are ready for any
+ * stream). */
+typedef struct gs_feas_device {
+  uint32_t n_variants, n_templates, words, row_stride; /* row_stride >= words (u64 units) */
+  uint32_t word_begin, word_end;
+  uint64_t* rows;                  /* device [n_variants][n_templates][row_stride] */
+  uint32_t* n_feasible_offerings;  /* device [n_variants][n_templates] */
+  int64_t* cheapest_key;           /* device [n_variants][n_templates] */
+  const uint32_t* variant_of_pod;  /* host [n_pods] */
+  const uint32_t* template_nodepool; /* host [n_templates] */
+  const uint32_t* it_name_rank;    /* host [n_its] */
+  uint32_t n_pods, n_its;
+  uint64_t checks;                 /* pod x offering checks of the WHOLE matrix */
+  double t_kernel_ms;
+} gs_feas_device;
+
+gs_status gs_feasibility_shard_device(gs_ctx* ctx, uint32_t word_begin, uint32_t word_end, gs_feas_device* out);
 
 /* host-only: run the encoder (no device needed) and report whether this
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.

@@ -491,7 +491,7 @@ gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end
   c->f_rows.assign((size_t)P * NP * W, 0);
   c->f_cheapest.assign((size_t)P * NP, -1);
   c->f_nfo.assign((size_t)P * NP, 0);
-  c->f_key.assign((size_t)P * NP, ~0ull);
+  c->f_key.assign((size_t)P * NP, 0x7FFFFFFFFFFFFFFFull);
   for (uint32_t p = 0; p < P; p++) {
     const uint32_t v = e.var_begin[p];  // the pod as given (no relaxation)
     for (uint32_t t = 0; t < e.T; t++) {
@@ -521,5 +521,45 @@ gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end
 }
 
 gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) { return gs_feasibility_shard(c, 0, ~0u, out); }
+
+gs_status gs_feasibility_shard_device(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_device* out) {
+  if (!c || !c->prepared || !out) return GS_E_INVALID;
+  auto& e = c->enc;
+  word_end = std::min(word_end, e.W);
+  if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
+  float ms = 0;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    launch_feas(c, 1, word_begin, word_end);
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    HIPCHK(hipEventSynchronize(c->ev[5]));
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
+  } catch (const HipError& ex) {
+    return fail(c, GS_E_HIP, ex.msg);
+  }
+  c->f_tmpl_np.resize(e.T);
+  for (uint32_t t = 0; t < e.T; t++) c->f_tmpl_np[t] = e.tmpl[t].np_index;
+  c->f_var_of_pod.resize(e.P);
+  for (uint32_t p = 0; p < e.P; p++) c->f_var_of_pod[p] = e.var_begin[p];
+  std::memset(out, 0, sizeof(*out));
+  out->n_variants = e.V;
+  out->n_templates = e.T;
+  out->words = e.W;
+  out->row_stride = c->dp.OW;
+  out->word_begin = word_begin;
+  out->word_end = word_end;
+  out->rows = c->dp.rows;
+  out->n_feasible_offerings = c->dp.nfo;
+  out->cheapest_key = reinterpret_cast<int64_t*>(c->dp.cheapest_key);
+  out->variant_of_pod = c->f_var_of_pod.data();
+  out->template_nodepool = c->f_tmpl_np.data();
+  out->it_name_rank = e.it_namerank.data();
+  out->n_pods = e.P;
+  out->n_its = e.N;
+  out->checks = e.checks;
+  out->t_kernel_ms = ms;
+  return GS_OK;
+}
 
 }  // extern "C"

@@ -78,6 +78,7 @@ struct gs_ctx {
   std::vector<int32_t> f_cheapest;
   std::vector<uint32_t> f_nfo;
   std::vector<uint64_t> f_key;
+  std::vector<uint32_t> f_var_of_pod, f_tmpl_np;
   gsd::Ctrl ctrl{};
   // consolidation: the combined problem (pending ++ bound pods), the plan,
   // the input copy (rerun) and result storage

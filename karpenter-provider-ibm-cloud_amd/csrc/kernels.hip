@@ -61,17 +61,21 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C), Gt = grid_of(tr.zm, tr.cm, d.Z, d.C);
   if (!G) ok_all = false;
   // <U> resources.Fits(Merge(daemon, pod), allocatable): lane r finds the
-  // first threshold >= the demand of resource r
-  uint32_t cur = 0;
-  if (lane < R) {
-    const int64_t dem = tr.daemon[lane] + d.pod_req[(size_t)vr.pod * R + lane];
-    const uint32_t o = d.thr_off[lane];
-    cur = o + lane + lower_bound_i64(d.thr_val + o, d.thr_off[lane + 1] - o, dem);
-  }
-  // every lane gets every cursor (shuffles in wave-uniform control flow)
+  // first threshold >= the demand of resource r (a two-level ballot search
+  // issuing all resources' loads together measured slower on C5: more
+  // memory instructions for the same latency)
   uint32_t curs[RMAX];
+  {
+    uint32_t cur = 0;
+    if (lane < R) {
+      const int64_t dem = tr.daemon[lane] + d.pod_req[(size_t)vr.pod * R + lane];
+      const uint32_t o = d.thr_off[lane];
+      cur = o + lane + lower_bound_i64(d.thr_val + o, d.thr_off[lane + 1] - o, dem);
+    }
+    // every lane gets every cursor (shuffles in wave-uniform control flow)
 #pragma unroll
-  for (uint32_t r = 0; r < RMAX; r++) curs[r] = (uint32_t)__shfl((int)cur, (int)r);
+    for (uint32_t r = 0; r < RMAX; r++) curs[r] = (uint32_t)__shfl((int)cur, (int)r);
+  }
   bool itkeys = false;
   for (uint32_t k = 0; k < d.K; k++) itkeys = itkeys || vr.itmask_off[k] != NONE;
   const uint64_t* topts = (static_mode && tr.has_limits ? d.t_limopts : d.t_opts) + (size_t)t * W;
@@ -122,19 +126,40 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
   }
   nf = wave_sum_u32(nf);
   uint32_t cheapest = NONE;
-  uint64_t ckey = ~0ull;
+  uint64_t ckey = 0x7FFFFFFFFFFFFFFFull;  // INT64_MAX: none
   if (static_mode && __ballot(any != 0)) {
     // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
     // IT is in the row and whose (zone, capacity type) pair is in the grid
-    for (uint32_t base = 0; base < d.n_off; base += 64) {
-      const uint32_t e = base + lane < d.n_off ? d.off_sorted[base + lane] : NONE;
-      const uint32_t i = e & 0xFFFFu, g = e >> 16;
-      const bool hit = e != NONE && ((G >> g) & 1) && ((s_row[wv][i >> 6] >> (i & 63)) & 1);
-      const uint64_t b = __ballot(hit);
+    // four 64-entry chunks in flight per step (deep scans are latency-bound)
+    constexpr uint32_t KS = 4;
+    for (uint32_t base = 0; base < d.n_off; base += 64 * KS) {
+      uint32_t e[KS];
+#pragma unroll
+      for (uint32_t k = 0; k < KS; k++) {
+        const uint32_t j = base + k * 64 + lane;
+        e[k] = j < d.n_off ? d.off_sorted[j] : NONE;
+      }
+      uint64_t b = 0;
+      uint32_t kk = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < KS; k++) {
+        const uint32_t i = e[k] & 0xFFFFu, g = e[k] >> 16;
+        const bool hit = e[k] != NONE && ((G >> g) & 1) && ((s_row[wv][i >> 6] >> (i & 63)) & 1);
+        const uint64_t bk = __ballot(hit);
+        if (!b && bk) {
+          b = bk;
+          kk = k;
+        }
+      }
       if (b) {
         const int src = (int)(__ffsll((long long)b) - 1);
-        cheapest = (uint32_t)__shfl((int)i, src);
-        const uint32_t gg = (uint32_t)__shfl((int)g, src);
+        uint32_t ek = e[0];
+#pragma unroll
+        for (uint32_t k = 1; k < KS; k++)
+          if (kk == k) ek = e[k];
+        const uint32_t esrc = (uint32_t)__shfl((int)ek, src);
+        cheapest = esrc & 0xFFFFu;
+        const uint32_t gg = esrc >> 16;
         ckey = ((uint64_t)d.it_prank[(size_t)cheapest * 64 + gg] << 32) | d.it_namerank[cheapest];
         break;
       }

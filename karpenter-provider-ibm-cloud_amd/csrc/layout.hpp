@@ -196,7 +196,7 @@ struct DevProblem {
   // feasibility outputs
   uint64_t* rows;              // [V][T][OW]
   uint32_t* cheapest;          // [V][T] IT index or NONE
-  uint64_t* cheapest_key;      // [V][T] (price_rank << 32 | name_rank), ~0 = none
+  uint64_t* cheapest_key;      // [V][T] (price_rank << 32 | name_rank), INT64_MAX = none
   uint32_t* nfo;               // [V][T]
   uint32_t* fk_ok;             // [V][T] free-key Compatible vs the fresh template
   // FFD state

@@ -106,6 +106,20 @@ class GsResult(C.Structure):
     ]
 
 
+class GsFeasDevice(C.Structure):
+    """gs_feas_device: one shard of the static matrix left in HBM (variant granularity)"""
+    _fields_ = [
+        ("n_variants", _U32), ("n_templates", _U32), ("words", _U32), ("row_stride", _U32),
+        ("word_begin", _U32), ("word_end", _U32),
+        ("rows", C.c_void_p), ("n_feasible_offerings", C.c_void_p), ("cheapest_key", C.c_void_p),
+        ("variant_of_pod", C.POINTER(C.c_uint32)), ("template_nodepool", C.POINTER(C.c_uint32)),
+        ("it_name_rank", C.POINTER(C.c_uint32)),
+        ("n_pods", _U32), ("n_its", _U32),
+        ("checks", C.c_uint64),
+        ("t_kernel_ms", C.c_double),
+    ]
+
+
 class GsFeasResult(C.Structure):
     _fields_ = [
         ("n_pods", _U32), ("n_nodepools", _U32), ("n_its", _U32), ("words", _U32),

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "libgpusched.so")
 
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
-           "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard"]
+           "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard",
+           "gs_feasibility_shard_device"]
 
 
 class GpuSchedError(RuntimeError):
@@ -49,6 +50,8 @@ def load():
         L.gs_feasibility.restype = C.c_int
         L.gs_feasibility_shard.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.GsFeasResult)]
         L.gs_feasibility_shard.restype = C.c_int
+        L.gs_feasibility_shard_device.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.GsFeasDevice)]
+        L.gs_feasibility_shard_device.restype = C.c_int
         L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.gs_last_error.restype = C.c_size_t
         L.gs_version.argtypes = []
@@ -190,3 +193,9 @@ class Solver:
         res = abi.GsFeasResult()
         self._check(self.L.gs_feasibility_shard(self.ctx, word_begin, word_end, C.byref(res)))
         return abi.feas_to_dict(res), res
+
+    def feasibility_shard_device(self, word_begin, word_end):
+        """gs_feasibility_shard_device: the shard left in HBM (gs_feas_device, pointers valid until the next call)"""
+        res = abi.GsFeasDevice()
+        self._check(self.L.gs_feasibility_shard_device(self.ctx, word_begin, word_end, C.byref(res)))
+        return res

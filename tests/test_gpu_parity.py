@@ -143,3 +143,28 @@ def test_feasibility_shards_combine_to_whole(solver, name, world):
     assert np.array_equal(acc["n_feasible_offerings"], want["n_feasible_offerings"])
     assert np.array_equal(acc["cheapest"], want["cheapest"])
     assert np.array_equal(acc["cheapest"], whole["cheapest"])
+
+
+@pytest.mark.parametrize("name,world", [("c3", 3), ("rand", 2)])
+def test_feasibility_device_shards(solver, name, world):
+    """gs_feasibility_shard_device: shards summed / min-ed in HBM (the
+    in-place collective's algebra) and expanded to pods equal the oracle"""
+    import torch
+    from gpusched.feasibility import expand_to_pods, device_views, word_range
+    p = {"c3": lambda: synth.make_c3(n_pods=2000), "rand": lambda: synth.random_problem(91, n_pods=200)}[name]()
+    st, want = pyoracle.feasibility(p)
+    assert st == abi.GS_OK
+    solver.prepare(p)
+    dev = torch.device("cuda", 0)
+    acc = None
+    for r in range(world):
+        res = solver.feasibility_shard_device(*word_range(solver.feasibility_shard_device(0, 0).words, r, world))
+        rows, nfo, key = (x.clone() for x in device_views(res, dev))
+        if acc is None:
+            acc = [rows, nfo, key]
+        else:
+            acc = [acc[0] + rows, acc[1] + nfo, torch.minimum(acc[2], key)]
+    got = expand_to_pods(res, *acc, len(p.nodepools))
+    assert np.array_equal(got["rows"], want["rows"])
+    assert np.array_equal(got["n_feasible_offerings"], want["n_feasible_offerings"])
+    assert np.array_equal(got["cheapest"], want["cheapest"])

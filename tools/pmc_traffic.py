@@ -24,20 +24,31 @@ def kernel_key(name):
     return None
 
 
+def phase_keys(names):
+    """bench.py order: the provisioning Solve (feas, ffd, trunc), the
+    consolidation sweep, then the C5 stress matrix.  A feas launch whose next
+    kernel is a simulation launch, and every trunc launch right after one,
+    belong to the sweep (feas_sim, trunc_sim); a feas launch followed by
+    neither ffd nor sim is a static-matrix launch of the stress (feas_c5)."""
+    keys = [kernel_key(n) for n in names]
+    out = []
+    for i, k in enumerate(keys):
+        nxt = keys[i + 1] if i + 1 < len(keys) else None
+        if k == "feas" and nxt == "sim":
+            k = "feas_sim"
+        elif k == "feas" and nxt != "ffd":
+            k = "feas_c5"
+        if k == "trunc" and i > 0 and keys[i - 1] == "sim":
+            k = "trunc_sim"
+        out.append(k)
+    return out
+
+
 def per_launch(path, counter):
-    """bench.py order: the provisioning Solve (feas, ffd, trunc) runs before
-    the consolidation sweep; a feas launch whose next kernel is a simulation
-    launch, and every trunc launch right after one, belong to the sweep
-    (keys feas_sim, trunc_sim)"""
     rows = [r for r in sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
             if kernel_key(r["Kernel_Name"])]
     vals = collections.defaultdict(list)
-    for i, r in enumerate(rows):
-        k = kernel_key(r["Kernel_Name"])
-        if k == "feas" and i + 1 < len(rows) and kernel_key(rows[i + 1]["Kernel_Name"]) == "sim":
-            k = "feas_sim"
-        if k == "trunc" and i > 0 and kernel_key(rows[i - 1]["Kernel_Name"]) == "sim":
-            k = "trunc_sim"
+    for r, k in zip(rows, phase_keys([r["Kernel_Name"] for r in rows])):
         if r["Counter_Name"] == counter:
             vals[k].append(float(r["Counter_Value"]) * 1024.0)
     return vals

@@ -14,4 +14,6 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
   python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/bench_fetch.json 2> $O/fetch.err
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o write -- \
   python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/bench_write.json 2> $O/write.err
+python3 $R/tools/kernel_phases.py $O/kt/kt_kernel_trace.csv > $O/phases.json
+python3 $R/tools/pmc_traffic.py $O/fetch/fetch_counter_collection.csv $O/write/write_counter_collection.csv > $O/traffic.json
 find $O -name "*.csv" | head -50
