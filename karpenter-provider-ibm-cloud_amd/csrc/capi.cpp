@@ -36,7 +36,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     // NodeClaims the LDS holds next to the thresholds and topology state
     const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, e.TG) + 8;
     const uint32_t dyn = gsk_ffd_dyn_lds_max();
-    const uint32_t fit = dyn > other ? (dyn - other) / 15 : 0;
+    const uint32_t fit = dyn > other ? (dyn - other) / 23 : 0;
     d.max_claims = std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
     if (!d.max_claims) throw HipError{"topology / threshold state leaves no LDS for NodeClaims"};
   }

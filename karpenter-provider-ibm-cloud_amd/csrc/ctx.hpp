@@ -27,7 +27,7 @@ extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hi
 
 namespace gsc {
 
-constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: ord/sc/scratch u16, tmpl u8, 4x u16 slack, thresholds
+constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: 4x u16 slack + room, ord/sc/scratch u16, tmpl u8, thresholds
 constexpr uint32_t kLdsBytes = 160 * 1024; // gfx950 LDS per workgroup
 
 using Clock = std::chrono::steady_clock;

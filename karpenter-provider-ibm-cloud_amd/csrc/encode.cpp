@@ -1089,7 +1089,7 @@ struct Ctx {
         }
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
-        vr.ctb = ct_bits(pv.reqs);
+        vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && !pv.own ? gsd::VF_SIMPLE : 0u);
         vr.t_own = pv.own;
         vr.zs = zone_full(pv.strict);
         vr.zn = zone_full(pv.reqs);

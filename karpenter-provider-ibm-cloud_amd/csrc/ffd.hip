@@ -27,7 +27,26 @@ using namespace gsd;
 
 namespace {
 
-constexpr int FB_MAX = 1024;  // workgroup size of the provisioning Solve
+// GS_FFD_TL (diagnostic build): tid 0 accumulates shader cycles per segment
+// of the pod loop into S.tl[k], reported through Ctrl.dbg
+#ifdef GS_FFD_TL
+#define TL(k)                                              \
+  do {                                                     \
+    if (tid == 0) {                                        \
+      const uint64_t tl_t_ = __builtin_amdgcn_s_memtime(); \
+      S.tl[k] += tl_t_ - S.tl_last;                        \
+      S.tl_last = tl_t_;                                   \
+    }                                                      \
+  } while (0)
+#else
+#define TL(k) \
+  do {        \
+  } while (0)
+#endif
+#ifndef GS_FB_MAX
+#define GS_FB_MAX 512
+#endif
+constexpr int FB_MAX = GS_FB_MAX;  // workgroup size of the provisioning Solve (512: 256 VGPRs, no spills)
 constexpr int FB_SIM = 256;   // workgroup size of one consolidation simulation
 constexpr int NWAVE_MAX = FB_MAX / 64;
 constexpr int SEQ_SORT = 128;  // subranges up to this length sort on thread 0
@@ -40,25 +59,41 @@ struct Frame {
   int wb, wp;  // wasBalanced, wasPartitioned
 };
 
+// Block-uniform state of the pod loop.  Every wave reads it once per pod
+// right after the loop-top barrier and then keeps its own register copy,
+// computing the pop, the sort decision and the scan's bookkeeping
+// identically; thread 0 writes every change to the other buffer (read by the
+// next pod, and by the paths that still share state through LDS: existing
+// nodes, new NodeClaims, Relax/Push), so no wave can see a half-updated copy.
+struct alignas(16) Hot {
+  uint32_t qhead, qlen, epoch, M;
+  uint32_t modkind, modpos, nlog, cb;  // cb: which vrb/reqb buffer holds the current pod
+  uint32_t wrapped, status, nx_valid, nx_pod;  // wrapped: pods now come back from Push
+  uint32_t nx_gp, nx_le, nx_ll, nx_cv;         // next-pod pipeline (published by wave 1)
+  uint64_t pops, pad;
+};
+
 struct Shared {
-  uint32_t pod, var, stop, M, modkind, modpos, qhead, qlen, epoch, nlog, status, found;
+  Hot hb[2];  // the pod loop's block-uniform state, double-buffered per pod
+  uint32_t found;
   uint32_t fast_path, modpos_sorted;
   uint32_t rot_lo, rot_hi;  // fast path: the one rotation partialInsertionSort performs
   int piv, hint;
-  uint64_t pops, generic, fast, cand, cand_full, node_evals, node_prefix;
+  uint64_t generic, fast, cand, cand_full, node_evals, node_prefix;
   uint32_t failed;
   uint64_t t_sort, t_scan, t_tmpl, t0;
   uint64_t dbg[16];
+  uint64_t tl[16], tl_last;  // GS_FFD_TL: shader cycles per loop segment (tid 0)
   uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
   uint32_t red[2][NWAVE_MAX];
+  alignas(16) uint32_t red2[2][NWAVE_MAX];  // Wg reductions (own double buffer: never adjacent to a Blk one)
   unsigned long long red64[RMAX];
   Frame stk[48];
   // next-pod pipeline: wave 1 prefetches the next pop during the current pod
-  uint32_t nx_valid, nx_pod, nx_gp, nx_le, nx_ll, nx_cv, cb, use_pf;
+  uint32_t use_pf;
   // solve in this block: simulation id, pod/claim arena offset, global pod id,
   // overlay entry count / the entry being written (and whether it is new)
   uint32_t sim, qoff, gpod, nov, ove, ov_new;
-  uint32_t wrapped;  // the queue head has wrapped: pods now come back from Push
   alignas(16) uint32_t vrb[2][(sizeof(VarRec) / 4 + 3) & ~3u];
   alignas(16) int64_t reqb[2][RMAX];
 };
@@ -306,6 +341,96 @@ struct SeqSort {
   }
 };
 
+// ------------------------------------------------------- hot block helpers
+// The per-pod reductions and the one-step rotation.  Only force-inlined
+// methods and never passed by address, so the object stays in registers and
+// every pointer keeps its LDS address space (ds_* instructions; Blk below is
+// materialized in scratch by its out-of-line sort methods, which costs
+// scratch + flat round trips per call).
+template <uint32_t NT>
+struct Wg {
+  static constexpr int NWAVE = (int)NT / 64;
+  static constexpr int KR = 8;  // rotate1 handles up to KR * NT elements
+  uint32_t* red;                // [2][NWAVE_MAX]
+  uint16_t* sc;
+  uint16_t* ord;
+  uint32_t tid, lane, wave;
+  uint32_t tog;
+  // Reductions over lane-ordered positions: thread t stands for position
+  // base + t, so a wave's first flagged position is one ballot (no lane
+  // shuffles: ds_bpermute chains cost ~60 cycles per step); one LDS slot per
+  // wave, one barrier, one vector read of all slots.
+  __device__ __forceinline__ uint32_t wave_first(bool flag, uint32_t base) const {
+    const uint64_t b = __ballot(flag);
+    return b ? base + wave * 64u + (uint32_t)__ffsll((long long)b) - 1u : INF;
+  }
+  __device__ __forceinline__ uint32_t cross_min(uint32_t v) {
+    uint32_t* r = red + tog * NWAVE_MAX;
+    if (lane == 0) r[wave] = v;
+    __syncthreads();
+    uint32_t x = INF;
+#pragma unroll
+    for (int w = 0; w < NWAVE; w += 4) {
+      const uint4 q = *(const uint4*)(r + w);
+      x = q.x < x ? q.x : x;
+      if (w + 1 < NWAVE) x = q.y < x ? q.y : x;
+      if (w + 2 < NWAVE) x = q.z < x ? q.z : x;
+      if (w + 3 < NWAVE) x = q.w < x ? q.w : x;
+    }
+    tog ^= 1u;
+    return x;
+  }
+  // first position base + t whose flag is set (INF if none)
+  __device__ __forceinline__ uint32_t first(bool flag, uint32_t base) { return cross_min(wave_first(flag, base)); }
+  // the first positions of two flags (16-bit positions) in one barrier
+  __device__ __forceinline__ uint2 first2(bool fa, bool fb, uint32_t base) {
+    const uint32_t a = wave_first(fa, base), b = wave_first(fb, base);
+    const uint32_t v = ((a < 0xFFFFu ? a : 0xFFFFu) << 16) | (b < 0xFFFFu ? b : 0xFFFFu);
+    uint32_t* r = red + tog * NWAVE_MAX;
+    if (lane == 0) r[wave] = v;
+    __syncthreads();
+    uint32_t ra = 0xFFFFu, rb = 0xFFFFu;
+#pragma unroll
+    for (int w = 0; w < NWAVE; w += 4) {
+      const uint4 q = *(const uint4*)(r + w);
+      const uint32_t xs[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (w + k >= NWAVE) break;
+        ra = (xs[k] >> 16) < ra ? (xs[k] >> 16) : ra;
+        rb = (xs[k] & 0xFFFFu) < rb ? (xs[k] & 0xFFFFu) : rb;
+      }
+    }
+    tog ^= 1u;
+    return make_uint2(ra == 0xFFFFu ? INF : ra, rb == 0xFFFFu ? INF : rb);
+  }
+  // rotate [lo, hi] by one (left: lo's element lands at hi; right: hi's at lo)
+  // in one staged read / barrier / write; false if the range is too long
+  __device__ __forceinline__ bool rotate1(int lo, int hi, bool left) {
+    if (hi - lo + 1 > KR * (int)NT) return false;
+    uint16_t vs[KR], vo[KR];
+#pragma unroll
+    for (int i = 0; i < KR; i++) {
+      const int k = lo + (int)tid + i * (int)NT;
+      if (k <= hi) {
+        const int src = left ? (k == hi ? lo : k + 1) : (k == lo ? hi : k - 1);
+        vs[i] = sc[src];
+        vo[i] = ord[src];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < KR; i++) {
+      const int k = lo + (int)tid + i * (int)NT;
+      if (k <= hi) {
+        sc[k] = vs[i];
+        ord[k] = vo[i];
+      }
+    }
+    return true;
+  }
+};
+
 // ------------------------------------------------------------ block-parallel
 template <uint32_t NT>
 struct Blk {
@@ -340,6 +465,26 @@ struct Blk {
     for (int w = 1; w < NWAVE; w++) r = S.red[tog][w] < r ? S.red[tog][w] : r;
     tog ^= 1;
     return r;
+  }
+  // two independent minima of 16-bit positions (INF = none) in one barrier
+  __device__ uint2 bmin2(uint32_t a, uint32_t b) {
+    a = a < 0xFFFFu ? a : 0xFFFFu;
+    b = b < 0xFFFFu ? b : 0xFFFFu;
+    for (int m = 32; m >= 1; m >>= 1) {
+      const uint32_t ya = (uint32_t)__shfl_xor((int)a, m), yb = (uint32_t)__shfl_xor((int)b, m);
+      a = ya < a ? ya : a;
+      b = yb < b ? yb : b;
+    }
+    if (lane == 0) S.red[tog][wave] = (a << 16) | b;
+    sync();
+    uint32_t ra = 0xFFFFu, rb = 0xFFFFu;
+    for (int w = 0; w < NWAVE; w++) {
+      const uint32_t x = S.red[tog][w];
+      ra = (x >> 16) < ra ? (x >> 16) : ra;
+      rb = (x & 0xFFFFu) < rb ? (x & 0xFFFFu) : rb;
+    }
+    tog ^= 1;
+    return make_uint2(ra == 0xFFFFu ? INF : ra, rb == 0xFFFFu ? INF : rb);
   }
   __device__ int32_t bmax(int32_t v) {
     for (int m = 32; m >= 1; m >>= 1) {
@@ -662,6 +807,67 @@ __device__ __forceinline__ uint32_t thr_search(const int64_t* thr, uint32_t n, u
   return lo;
 }
 
+// choosePivot's hint for sort.Slice over sc[0, M), M > 12: the (up to) nine
+// sampled keys read by nine lanes in one LDS round trip, the median-of-three
+// comparisons on scalars (same swap count as SeqSort::choose_pivot)
+__device__ __forceinline__ int pivot_hint_wave(const uint16_t* sc, int l, uint32_t lane) {
+  const int i0 = l / 4 * 1, j0 = l / 4 * 2, k0 = l / 4 * 3;
+  const int idx[9] = {i0 - 1, i0, i0 + 1, j0 - 1, j0, j0 + 1, k0 - 1, k0, k0 + 1};
+  int mine = 0;
+#pragma unroll
+  for (int t = 0; t < 9; t++)
+    if ((int)lane == t) mine = idx[t];
+  const uint32_t kl = lane < 9 && (l >= 50 || lane % 3 == 1) ? sc[mine] : 0u;
+  uint32_t key[9];
+#pragma unroll
+  for (int t = 0; t < 9; t++) key[t] = __builtin_amdgcn_readlane(kl, t);
+  int swaps = 0;
+  auto med = [&](uint32_t kx, uint32_t ky, uint32_t kz) {
+    // order2(x,y); order2(y,z); order2(x,y); the middle key
+    if (ky < kx) { swaps++; const uint32_t u = kx; kx = ky; ky = u; }
+    if (kz < ky) { swaps++; const uint32_t u = ky; ky = kz; kz = u; }
+    if (ky < kx) { swaps++; const uint32_t u = kx; kx = ky; ky = u; }
+    return ky;
+  };
+  uint32_t ki = key[1], kj = key[4], kk = key[7];
+  if (l >= 50) {
+    ki = med(key[0], key[1], key[2]);
+    kj = med(key[3], key[4], key[5]);
+    kk = med(key[6], key[7], key[8]);
+  }
+  med(ki, kj, kk);
+  return swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+}
+
+// first k in [lo, hi) with pred(k) for a monotone pred (false...true), hi if
+// none: a 64-ary search, one LDS round trip per level (two up to 4096)
+template <class Pred>
+__device__ __forceinline__ uint32_t wave_first(uint32_t lo, uint32_t hi, uint32_t lane, Pred pred) {
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t k = lo + lane * step + step - 1;  // last index of this lane's segment
+    const uint64_t b = __ballot(k >= hi || pred(k));
+    if (!b) return hi;
+    const uint32_t i = (uint32_t)__ffsll((long long)b) - 1;
+    lo = lo + i * step;
+    hi = lo + step < hi ? lo + step : hi;
+  }
+  const uint32_t k = lo + lane;
+  const uint64_t b = __ballot(k < hi && pred(k));
+  return b ? lo + (uint32_t)__ffsll((long long)b) - 1 : hi;
+}
+
+// phase timers (t_sort / t_scan / t_tmpl, Ctrl.dbg): s_memrealtime costs
+// hundreds of cycles on the pod loop's critical path, so only GS_FFD_PHASES
+// builds read the clock
+__device__ __forceinline__ uint64_t phase_clock() {
+#ifdef GS_FFD_PHASES
+  return wall_clock64();
+#else
+  return 0;
+#endif
+}
+
 // the kernel argument block, addressed in the constant (kernarg) space
 typedef const __attribute__((address_space(4))) DevProblem* KArg;
 
@@ -691,6 +897,29 @@ __device__ __forceinline__ uint32_t qcode_ceil(int64_t v) {
   const uint32_t s = b - 10;
   const uint32_t c = 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
   return c + ((x & ((1ull << s) - 1)) ? 1u : 0u);
+}
+
+// the value a code stands for: qcode_floor(v) <= v's code <= qcode_ceil(v)
+// and qcode_value(qcode_floor(v)) <= v <= qcode_value(qcode_ceil(v))
+__device__ __forceinline__ int64_t qcode_value(uint32_t c) {
+  if (c < 1024u) return (int64_t)c;
+  const uint32_t s = (c - 1024u) / 512u + 1u, m = (c - 1024u) % 512u + 512u;
+  return (int64_t)((uint64_t)m << s);
+}
+
+// LDS room of a NodeClaim: qcode_floor(thr[cursor] - tot) per resource (<= 4),
+// a lower bound of what a pod may add before any threshold cursor moves
+__device__ __forceinline__ uint64_t pack_room(const int64_t* thr, const uint32_t* thoff, const uint32_t* cur,
+                                              const int64_t* tot, uint32_t RQ) {
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++) {
+    if (r >= RQ) break;
+    const uint32_t o = thoff[r], n = thoff[r + 1] - o;
+    const int64_t room = cur[r] < n ? thr[o + cur[r]] - tot[r] : 0;
+    s |= (uint64_t)qcode_floor(room) << (16 * r);
+  }
+  return s;
 }
 
 // LDS slack of a NodeClaim: qcode_ceil(maxa - tot) per resource (<= 4)
@@ -724,13 +953,14 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Shared S;
   const uint32_t MC = d.max_claims;  // LDS claim capacity (SIM: the largest simulation's pod count)
-  uint16_t* s_ord = (uint16_t*)lds64;
+  uint64_t* s_slk = lds64;      // 4x u16 quantized slack per claim (upper bound)
+  uint64_t* s_rm = s_slk + MC;  // 4x u16 quantized room before a cursor moves (lower bound)
+  uint16_t* s_ord = (uint16_t*)(s_rm + MC);
   uint16_t* s_sc = s_ord + MC;
   uint16_t* s_scr = s_sc + MC;
-  uint64_t* s_slk = (uint64_t*)(s_scr + MC);  // 4x u16 quantized slack per claim
-  uint8_t* s_tmpl = (uint8_t*)(s_slk + MC);
+  uint8_t* s_tmpl = (uint8_t*)(s_scr + MC);
   // byte offset arithmetic keeps the pointer in the LDS address space (ds_read, not flat)
-  int64_t* s_thr = (int64_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u));
+  int64_t* s_thr = (int64_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u));
   __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
   __shared__ uint32_t s_thoff[RMAX + 1];
   const uint32_t tid = threadIdx.x;
@@ -739,14 +969,15 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
   const uint32_t OW = d.OW;  // claim option stride (words, 16-B multiple)
   const uint32_t nthr = d.thr_off[R];
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
-  uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
+  uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
   // topology spread: zone-domain counts [TG][64], known domains, per-pod minimum counts
-  const uint32_t tg_off = (((15u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + d.ov_cap * 4u + 7u) & ~7u;
+  const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + d.ov_cap * 4u + 7u) & ~7u;
   uint64_t* s_known = (uint64_t*)((char*)lds64 + tg_off);
   int64_t* s_tmin = (int64_t*)(s_known + d.TG);
   int32_t* s_zcnt = (int32_t*)(s_tmin + d.TG);
   Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
+  Wg<NT> wg{&S.red2[0][0], s_sc, s_ord, tid, tid & 63, tid >> 6, 0};
 
   for (uint32_t i = tid; i < nthr + 4; i += FB) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
@@ -807,27 +1038,31 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       }
     }
     if (tid == 0) {
-      S.M = 0;
-      S.qhead = 0;
-      S.qlen = P;
-      S.epoch = 1;
-      S.modkind = MOD_NONE;
-      S.nlog = 0;
+      S.hb[0].M = 0;
+      S.hb[0].qhead = 0;
+      S.hb[0].qlen = P;
+      S.hb[0].epoch = 1;
+      S.hb[0].modkind = MOD_NONE;
+      S.hb[0].nlog = 0;
       S.nov = ncand;
       S.qoff = qoff;
-      S.pops = S.generic = S.fast = S.cand = S.cand_full = S.node_evals = S.node_prefix = 0;
+      S.hb[0].pops = S.generic = S.fast = S.cand = S.cand_full = S.node_evals = S.node_prefix = 0;
       S.failed = 0;
       S.t_sort = S.t_scan = S.t_tmpl = 0;
-      for (int q = 0; q < 16; q++) S.dbg[q] = 0;
+      for (int q = 0; q < 16; q++) S.dbg[q] = S.tl[q] = 0;
+      S.tl_last = __builtin_amdgcn_s_memtime();
       S.t0 = wall_clock64();
       S.dbg[7] = __builtin_amdgcn_s_memtime();
-      S.status = 0;
-      S.nx_valid = 0;
-      S.cb = 0;
-      S.wrapped = 0;
+      S.hb[0].status = 0;
+      S.hb[0].nx_valid = 0;
+      S.hb[0].cb = 0;
+      S.hb[0].wrapped = 0;
     }
     __syncthreads();
     const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
+    // per-wave copy of the uniform state; par: the buffer this pod reads
+    Hot h = S.hb[0];
+    uint32_t par = 1;
 
     uint64_t tLoop = 0;
     // wave-1 prefetch registers: stage 0 none, 1 pod id, 2 counters+variant, 3 records
@@ -843,9 +1078,9 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
     };
     auto pf_stage3 = [&]() {
       if (wave == 1) {
-        const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+        const uint32_t st = __builtin_amdgcn_readfirstlane(pf_state);
         if (st == 2) {
-          const uint32_t cv = (uint32_t)__shfl((int)pf_cv, 0), gp = (uint32_t)__shfl((int)pf_gp, 0);
+          const uint32_t cv = __builtin_amdgcn_readfirstlane(pf_cv), gp = __builtin_amdgcn_readfirstlane(pf_gp);
           if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.vars + cv))[lane];
           if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.pod_req + (size_t)gp * R))[lane - 32];
           pf_state = 3;
@@ -853,105 +1088,133 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       }
     };
     for (;;) {
+      TL(0);  // end of the previous pod -> loop top
+      par ^= 1u;
+      Hot& HN = S.hb[par ^ 1u];  // thread 0 writes this pod's changes here
       // publish last iteration's prefetch into the spare buffer
       if (wave == 1) {
-        const uint32_t st = (uint32_t)__shfl((int)pf_state, 0);
+        const uint32_t st = __builtin_amdgcn_readfirstlane(pf_state);
         if (st == 3 || st == 4) {
-          const uint32_t nb = S.cb ^ 1u;
+          const uint32_t nb = h.cb ^ 1u;  // the buffer the current pod does not use
           if (lane < VR_DW) S.vrb[nb][lane] = pf_vr;
           if (lane >= 32 && lane < 32 + 2 * RR) ((uint32_t*)S.reqb[nb])[lane - 32] = pf_rq;
           // first-pass records carry their pod and variant ids; such a pod
           // was never pushed (last epoch / length 0)
-          const uint32_t rpod = (uint32_t)__shfl((int)pf_vr, 0), rvix = (uint32_t)__shfl((int)pf_vr, VR_DW - 1);
+          const uint32_t rpod = __builtin_amdgcn_readfirstlane(pf_vr), rvix = __builtin_amdgcn_readlane(pf_vr, VR_DW - 1);
           if (lane == 0) {
-            S.nx_valid = 1;
-            S.nx_pod = st == 4 ? rpod : pf_pod;
-            S.nx_gp = st == 4 ? rpod : pf_gp;
-            S.nx_le = st == 4 ? 0u : pf_le;
-            S.nx_ll = st == 4 ? 0u : pf_ll;
-            S.nx_cv = st == 4 ? rvix : pf_cv;
+            S.hb[par].nx_valid = 1;
+            S.hb[par].nx_pod = st == 4 ? rpod : pf_pod;
+            S.hb[par].nx_gp = st == 4 ? rpod : pf_gp;
+            S.hb[par].nx_le = st == 4 ? 0u : pf_le;
+            S.hb[par].nx_ll = st == 4 ? 0u : pf_ll;
+            S.hb[par].nx_cv = st == 4 ? rvix : pf_cv;
           }
         } else if (lane == 0) {
-          S.nx_valid = 0;
+          S.hb[par].nx_valid = 0;
         }
         pf_state = 0;
       }
       __syncthreads();
+      TL(1);  // publish + barrier
       // ------------------------------------------------------------ Queue.Pop
-      if (tid == 0) tLoop = wall_clock64();
+      // computed identically by every wave from one read of the uniform state
       if (tid == 0) {
-        uint32_t stop = 0;
-        if (S.pops > max_pops) {
-          S.status = 2;
-          stop = 1;
-        } else if (S.qlen == 0) {
-          stop = 1;
+        tLoop = phase_clock();
+        if (S.dbg[14]) S.dbg[5] += tLoop - S.dbg[14];  // iteration end -> pop (prefetch publish)
+      }
+      h = S.hb[par];
+      h.qhead = __builtin_amdgcn_readfirstlane(h.qhead);
+      h.qlen = __builtin_amdgcn_readfirstlane(h.qlen);
+      h.epoch = __builtin_amdgcn_readfirstlane(h.epoch);
+      h.M = __builtin_amdgcn_readfirstlane(h.M);
+      h.modkind = __builtin_amdgcn_readfirstlane(h.modkind);
+      h.modpos = __builtin_amdgcn_readfirstlane(h.modpos);
+      h.nlog = __builtin_amdgcn_readfirstlane(h.nlog);
+      h.cb = __builtin_amdgcn_readfirstlane(h.cb);
+      h.wrapped = __builtin_amdgcn_readfirstlane(h.wrapped);
+      h.status = __builtin_amdgcn_readfirstlane(h.status);
+      h.pops = (uint64_t)uniform_i64((int64_t)h.pops);
+      bool stop = false, pf = false;
+      uint32_t p = 0, gp = 0, v = 0;
+      if (h.status) {
+        stop = true;  // set by a NodeClaim update of the previous pod
+      } else if (h.pops > max_pops) {
+        h.status = 2;
+        stop = true;
+      } else if (h.qlen == 0) {
+        stop = true;
+      } else {
+        uint32_t le, ll;
+        pf = __builtin_amdgcn_readfirstlane(h.nx_valid) != 0;
+        if (pf) {
+          p = __builtin_amdgcn_readfirstlane(h.nx_pod);
+          gp = __builtin_amdgcn_readfirstlane(h.nx_gp);
+          le = __builtin_amdgcn_readfirstlane(h.nx_le);
+          ll = __builtin_amdgcn_readfirstlane(h.nx_ll);
+          v = __builtin_amdgcn_readfirstlane(h.nx_cv);
         } else {
-          uint32_t p, gp, le, ll, cv;
-          const bool pf = S.nx_valid != 0;
-          if (pf) {
-            p = S.nx_pod;
-            gp = S.nx_gp;
-            le = S.nx_le;
-            ll = S.nx_ll;
-            cv = S.nx_cv;
-          } else {
-            p = queue[S.qhead];
-            gp = gpod(p);
-            le = last_epoch[p];
-            ll = last_len[p];
-            cv = cur_var[p];
-          }
-          if (le == S.epoch && ll == S.qlen) {
-            stop = 1;
-          } else {
-            if (S.qhead + 1 == P) S.wrapped = 1;
-            S.qhead = S.qhead + 1 == P ? 0 : S.qhead + 1;
-            S.qlen--;
-            S.pops++;
-            S.pod = p;
-            S.gpod = gp;
-            S.var = cv;
-            S.use_pf = pf ? 1u : 0u;
-            if (pf) S.cb ^= 1u;
-          }
+          p = __builtin_amdgcn_readfirstlane(queue[h.qhead]);
+          gp = __builtin_amdgcn_readfirstlane(gpod(p));
+          le = __builtin_amdgcn_readfirstlane(last_epoch[p]);
+          ll = __builtin_amdgcn_readfirstlane(last_len[p]);
+          v = __builtin_amdgcn_readfirstlane(cur_var[p]);
         }
-        S.stop = stop;
+        if (le == h.epoch && ll == h.qlen) {
+          stop = true;
+        } else {
+          if (h.qhead + 1 == P) h.wrapped = 1;
+          h.qhead = h.qhead + 1 == P ? 0 : h.qhead + 1;
+          h.qlen--;
+          h.pops++;
+          if (pf) h.cb ^= 1u;
+        }
+      }
+      if (tid == 0) {
+        HN.qhead = h.qhead;
+        HN.qlen = h.qlen;
+        HN.epoch = h.epoch;
+        HN.M = h.M;
+        HN.modkind = h.modkind;
+        HN.modpos = h.modpos;
+        HN.nlog = h.nlog;
+        HN.cb = h.cb;
+        HN.wrapped = h.wrapped;
+        HN.status = h.status;
+        HN.pops = h.pops;
         S.found = 0;
       }
-      __syncthreads();
-      if (S.stop) break;
-      const uint32_t p = S.pod, gp = S.gpod, v = S.var;
-      if (!S.use_pf) {
+      TL(2);  // pop
+      if (stop) break;
+      if (!pf) {
         // not prefetched: wave 0 stages the variant record and requests in LDS
         if (wave == 0) {
-          if (lane < VR_DW) S.vrb[S.cb][lane] = ((const uint32_t*)(d.vars + v))[lane];
+          if (lane < VR_DW) S.vrb[h.cb][lane] = ((const uint32_t*)(d.vars + v))[lane];
           if (lane >= 32 && lane < 32 + 2 * RR)
-            ((uint32_t*)S.reqb[S.cb])[lane - 32] = ((const uint32_t*)(d.pod_req + (size_t)gp * R))[lane - 32];
+            ((uint32_t*)S.reqb[h.cb])[lane - 32] = ((const uint32_t*)(d.pod_req + (size_t)gp * R))[lane - 32];
         }
         __syncthreads();
       }
-      const VarRec& vr = *(const VarRec*)S.vrb[S.cb];
-      const int64_t* preq = S.reqb[S.cb];
+      const VarRec& vr = *(const VarRec*)S.vrb[h.cb];
+      const int64_t* preq = S.reqb[h.cb];
       // stage 1: the next pod id (its queue slot cannot change during this pod
       // unless the queue is empty now, when this pod itself may come back)
-      if (wave == 1 && S.qlen > 0) {
-        if (!SIM && !S.wrapped) {
+      if (wave == 1 && h.qlen > 0) {
+        if (!SIM && !h.wrapped) {
           // first pass: the next pod is queue0[qhead] with its first variant,
           // its records are contiguous in queue order: one round trip
-          const uint32_t k = S.qhead;
+          const uint32_t k = h.qhead;
           if (lane < VR_DW) pf_vr = ((const uint32_t*)(d.qvars + k))[lane];
           if (lane >= 32 && lane < 32 + 2 * RR) pf_rq = ((const uint32_t*)(d.qreqs + (size_t)k * R))[lane - 32];
           pf_state = 4;
         } else if (lane == 0) {
-          pf_pod = queue[S.qhead];
+          pf_pod = queue[h.qhead];
           pf_state = 1;
         }
       }
-      const uint32_t M = S.M;
+      const uint32_t M = h.M;
       uint64_t tA = 0;
       if (tid == 0) {
-        tA = wall_clock64();
+        tA = phase_clock();
         S.dbg[4] += tA - tLoop;  // pop + variant load
       }
 
@@ -1035,7 +1298,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               }
             }
           }
-          fn = blk.bmin(feas ? n : INF);
+          fn = wg.first(feas, base);
           if (tid == 0) S.node_evals += d.NN - base < width ? d.NN - base : width;
           if (fn != INF) break;
         }
@@ -1082,7 +1345,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                                            : e.st;
           }
           if (tid == 0) {
-            logp[S.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
+            logp[HN.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
             S.found = 1;
             // <U> Topology.Record: the node's labels are single domains
             for (uint64_t m = TOPO ? vr.t_sel : 0; m; m &= m - 1) {
@@ -1105,74 +1368,61 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         }
       }
 
+      TL(3);  // variant staging, prefetch issue, existing nodes
       // ------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
       if (M > 1) {
-        if (tid == 0) {
-          SeqSort ss{s_sc, s_ord};
-          uint32_t fast = 0, generic = 0;
-          bool inversion = false;
-          if (S.modkind == MOD_INC) {
-            const uint32_t q = S.modpos;
-            inversion = q + 1 < M && s_sc[q + 1] < s_sc[q];
-          } else if (S.modkind == MOD_APPEND) {
-            inversion = s_sc[M - 2] > s_sc[M - 1];
-          }
-          if (!inversion) {
-            // sorted input: pdqsort_func / insertionSort leave it untouched
-          } else if (M <= 12) {
-            ss.insertion_sort(0, (int)M);
+        // the decision, identical in every wave: at most one NodeClaim changed
+        // since the last sort (one pod added at modpos, or one appended)
+        constexpr uint32_t FP_SMALL = 8, FP_GENERIC = 16;
+        const uint32_t mk = h.modkind, q = h.modpos;
+        bool inversion = false;
+        if (mk == MOD_INC) inversion = q + 1 < M && s_sc[q + 1] < s_sc[q];
+        else if (mk == MOD_APPEND) inversion = s_sc[M - 2] > s_sc[M - 1];
+        inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
+        uint32_t fp = 0, rlo = 0, rhi = 0;
+        if (!inversion) {
+          // sorted input: pdqsort_func / insertionSort leave it untouched
+        } else if (M <= 12) {
+          fp = FP_SMALL;
+        } else if (pivot_hint_wave(s_sc, (int)M, lane) == 1 && M >= 50) {
+          // partialInsertionSort fixes the single inversion: one
+          // rotation; its far end by a 64-ary search over the sorted remainder
+          // (INC: first k > q with count >= x; APPEND: first k < M-1 with
+          // count > x)
+          fp = mk;
+          if (mk == MOD_INC) {
+            const uint16_t x = s_sc[q];
+            const uint32_t lo = wave_first(q + 1, M, lane, [&](uint32_t k) { return s_sc[k] >= x; });
+            rlo = q;
+            rhi = lo - 1;
           } else {
-            int hint;
-            ss.choose_pivot_fast(0, (int)M, &hint);
-            if (hint == 1 && M >= 50) {
-              // partialInsertionSort fixes the single inversion:
-              // one rotation; its far end by binary search over the sorted
-              // remainder (INC: first k > q with count >= x; APPEND: first
-              // k < M-1 with count > x)
-              fast = S.modkind;
-              S.fast++;
-              if (S.modkind == MOD_INC) {
-                const uint32_t q = S.modpos;
-                const uint16_t x = s_sc[q];
-                uint32_t lo = q + 1, hi = M;
-                while (lo < hi) {
-                  const uint32_t mid = (lo + hi) >> 1;
-                  if (s_sc[mid] < x) lo = mid + 1;
-                  else hi = mid;
-                }
-                S.rot_lo = q;
-                S.rot_hi = lo - 1;
-              } else {
-                const uint16_t x = s_sc[M - 1];
-                uint32_t lo = 0, hi = M - 1;
-                while (lo < hi) {
-                  const uint32_t mid = (lo + hi) >> 1;
-                  if (s_sc[mid] <= x) lo = mid + 1;
-                  else hi = mid;
-                }
-                S.rot_lo = lo;
-                S.rot_hi = M - 1;
-              }
-            } else {
-              generic = 1;
-              S.generic++;
-            }
+            const uint16_t x = s_sc[M - 1];
+            rlo = wave_first(0, M - 1, lane, [&](uint32_t k) { return s_sc[k] > x; });
+            rhi = M - 1;
           }
-          S.fast_path = fast | (generic << 4);
-          S.modpos_sorted = S.modpos;
-          S.modkind = MOD_NONE;
+        } else {
+          fp = FP_GENERIC;
         }
-        __syncthreads();
+        h.modkind = MOD_NONE;
         if (tid == 0) {
-          const uint64_t tq = wall_clock64();
+          if (fp == MOD_INC || fp == MOD_APPEND) S.fast++;
+          if (fp == FP_GENERIC) S.generic++;
+          HN.modkind = MOD_NONE;
+          const uint64_t tq = phase_clock();
           S.dbg[3] += tq - tA;
         }
-        const uint32_t fp = S.fast_path;
-        if ((fp == MOD_INC || fp == MOD_APPEND) && blk.rotate1((int)S.rot_lo, (int)S.rot_hi, fp == MOD_INC)) {
+        TL(4);  // sort decision
+        if (fp == FP_SMALL || fp == FP_GENERIC) __syncthreads();  // every wave has decided before the order changes
+        if (fp == FP_SMALL) {
+          if (tid == 0) {
+            SeqSort ss{s_sc, s_ord};
+            ss.insertion_sort(0, (int)M);
+          }
+        } else if ((fp == MOD_INC || fp == MOD_APPEND) && wg.rotate1((int)rlo, (int)rhi, fp == MOD_INC)) {
           // done: one staged rotation
         } else if (fp == MOD_INC) {
           // X (at q, count x) moves right past the run of counts < x
-          const uint32_t q = S.modpos_sorted, x = s_sc[q];
+          const uint32_t x = s_sc[q];
           uint32_t e = M;
           for (uint32_t base = q + 1; base < M; base += FB) {
             const uint32_t k = base + tid;
@@ -1196,22 +1446,36 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             }
           }
           blk.rotate_right(e, (int)M - 1);
-        } else if (fp >> 4) {
+        } else if (fp == FP_GENERIC) {
           blk.pdqsort((int)M);
         }
-        __syncthreads();
+        if (fp) __syncthreads();  // the new order before the scan reads it
+        TL(5);  // rotation / pdqsort + barrier
       }
       if (tid == 0) {
-        const uint64_t tB = wall_clock64();
+        const uint64_t tB = phase_clock();
         S.t_sort += tB - tA;
         tA = tB;
       }
 
       pf_stage2();
       // request codes for the LDS slack test (computed here: not live across the sort)
-      uint32_t rqq[4];
+      uint32_t rqq[4], rqc[4];
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) rqq[r] = r < d.RQ ? qcode_floor(rq[r]) : 0;
+      for (uint32_t r = 0; r < 4; r++) {
+        rqq[r] = r < d.RQ ? qcode_floor(rq[r]) : 0;
+        rqc[r] = r < d.RQ ? qcode_ceil(rq[r]) : 0;
+      }
+      // fast accept (simple pods): NodeClaim.Add changes only the requests, so
+      // a claim whose threshold cursors do not move keeps its (non-empty)
+      // options -- CanAdd holds without reading the claim (room test in LDS)
+#ifdef GS_NO_FAST
+      bool simple = false;
+#else
+      bool simple = !TOPO && (vr.ctb & VF_SIMPLE);
+#endif
+#pragma unroll
+      for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
       // ---------------------- in-flight NodeClaims, first that CanAdd wins
       // A lane that finds its NodeClaim feasible keeps everything NodeClaim.Add
       // needs in registers (new option words for W <= WREG, totals, cursors);
@@ -1239,16 +1503,48 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
         uint64_t c1 = 0, c2 = 0, c3 = 0;
 #endif
+        bool lp = false, fa = false;
         if (pos < M) {
           j = s_ord[pos];
           t = s_tmpl[j];
           // LDS-only necessary test: template tolerated and, per resource,
           // qcode_floor(request) <= qcode_ceil(slack)
-          bool lp = (vr.tolt >> t) & 1;
+          lp = (vr.tolt >> t) & 1;
           const uint64_t sq = s_slk[j];
 #pragma unroll
           for (uint32_t r = 0; r < 4; r++) lp = lp && (uint64_t)rqq[r] <= ((sq >> (16 * r)) & 0xFFFFu);
-          if (lp) {
+          if (simple && lp) {
+            // LDS-only sufficient test: qcode_ceil(request) <= qcode_floor(room)
+            const uint64_t rm = s_rm[j];
+            fa = true;
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) fa = fa && (uint64_t)rqc[r] <= ((rm >> (16 * r)) & 0xFFFFu);
+          }
+        }
+        // simple pods: the first fast-accept position and the first position
+        // that needs the exact check, in one reduction; the exact checks run
+        // only before the first fast accept (usually none)
+        TL(6);
+        uint32_t mfa = INF;
+        bool skip_full = false;
+        uint4 ph0 = make_uint4(0, 0, 0, 0), ph1 = ph0, ph3 = ph0;
+        if (simple) {
+          const uint64_t fam = __ballot(fa);
+          if (fa && (tid & 63) == (uint32_t)(__ffsll((long long)fam) - 1)) {
+            // the wave's first fast accept reads its requests now: if it wins,
+            // the update needs no further round trip
+            const uint4* q = (const uint4*)(dd.c_rec + cb + j);
+            ph0 = q[0];
+            ph1 = q[1];
+            ph3 = q[3];
+          }
+          const uint2 m2 = wg.first2(fa, lp && !fa, base);
+          mfa = m2.x;
+          skip_full = m2.y == INF || (m2.x != INF && m2.y > m2.x);
+        }
+        TL(7);
+        if (pos < M) {
+          if (lp && !fa && !skip_full && pos < mfa) {
 #ifdef GS_ASM_MARK
             asm volatile("; MARK_FULL_BEGIN");
 #endif
@@ -1444,10 +1740,15 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         const uint64_t pm = __ballot(pre);
         if ((tid & 63) == 0 && pm) atomicAdd((unsigned long long*)&S.cand_full, (unsigned long long)__popcll(pm));
         uint64_t tq = 0;
-        if (tid == 0) tq = wall_clock64();
-        f = blk.bmin(feas ? pos : INF);
+        if (tid == 0) tq = phase_clock();
+        TL(8);  // exact checks
+        if (skip_full) {
+          f = mfa;  // block-uniform (from the reduction)
+        } else {
+          f = wg.first(feas || (fa && pos == mfa), base);
+        }
         if (tid == 0) {
-          const uint64_t tr_ = wall_clock64();
+          const uint64_t tr_ = phase_clock();
           S.dbg[0] += tq - tA;
           S.dbg[1] += tr_ - tq;
           S.dbg[2]++;
@@ -1455,7 +1756,32 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           S.cand += (M - base) < FB ? (M - base) : FB;
         }
         if (f != INF) {
-          if (pos == f) {
+          if (pos == f && fa) {
+            // NodeClaim.Add of a simple pod on a fast-accepted claim: requests
+            // only (options, cursors and requirements stay); LDS room and
+            // slack shrink by the request (still a lower / upper bound)
+            ClaimRec* cr = dd.c_rec + cb + j;
+            const int64_t t4[4] = {(int64_t)(((uint64_t)ph0.y << 32) | ph0.x), (int64_t)(((uint64_t)ph0.w << 32) | ph0.z),
+                                   (int64_t)(((uint64_t)ph1.y << 32) | ph1.x), (int64_t)(((uint64_t)ph1.w << 32) | ph1.z)};
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++)
+              if (r < R) cr->tot_lo[r] = t4[r] + rq[r];
+            cr->count = ph3.w + 1;
+            const uint64_t rm = s_rm[j], sl = s_slk[j];
+            uint64_t rm2 = 0, sl2 = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) {
+              if (r >= dd.RQ) break;
+              rm2 |= (uint64_t)qcode_floor(qcode_value((uint32_t)(rm >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
+              sl2 |= (uint64_t)qcode_ceil(qcode_value((uint32_t)(sl >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
+            }
+            s_rm[j] = rm2;
+            s_slk[j] = sl2;
+            if (s_sc[f] == 0xFFFFu) HN.status = 3;
+            s_sc[f]++;
+            dd.log[cb + h.nlog] = LogRec{gp, v, j, 0};
+            S.dbg[15]++;
+          } else if (pos == f) {
             // NodeClaim.Add by the winning lane: options, requests, requirements
             ClaimRec* cr = dd.c_rec + cb + j;
             uint64_t* opts = dd.c_opts + (size_t)(cb + j) * OW;
@@ -1482,14 +1808,17 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               }
             }
             int64_t nt[RR], ma[RR];
+            uint32_t cu[RR];
 #pragma unroll
             for (uint32_t r = 0; r < RR; r++) {
               nt[r] = tot[r] + rq[r];
               ma[r] = cr->maxa[r];
+              cu[r] = mrow[r] - s_thoff[r] - r;
               cr->tot(r) = nt[r];
-              cr->thr(r) = (uint16_t)(mrow[r] - s_thoff[r] - r);
+              cr->thr(r) = (uint16_t)cu[r];
             }
             s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
+            s_rm[j] = pack_room(thr, s_thoff, cu, nt, dd.RQ);
             cr->zm = zm & vr.zm;  // zm carries the topology narrowing
             cr->cm &= vr.cm;
             cr->ctb &= vr.ctb;
@@ -1524,27 +1853,33 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                                ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * 64, dd.fk_isint[e.slot])
                                : e.st;
             }
-            if (s_sc[f] == 0xFFFFu) S.status = 3;
+            if (s_sc[f] == 0xFFFFu) HN.status = 3;
             s_sc[f]++;
-            S.modkind = MOD_INC;
-            S.modpos = f;
-            dd.log[cb + S.nlog++] = LogRec{gp, v, j, 0};
-            S.found = 1;
+            dd.log[cb + h.nlog] = LogRec{gp, v, j, 0};
           }
           break;
         }
       }
       pf_stage3();
-      __syncthreads();
+      TL(9);  // reduction + winner update
       if (tid == 0) {
-        const uint64_t tB = wall_clock64();
+        const uint64_t tB = phase_clock();
         S.t_scan += tB - tA;
+        S.dbg[14] = tB;
         tA = tB;
       }
-      if (S.found) {
-        if (S.status) break;
+      if (f != INF) {
+        // every wave knows the pod went to the NodeClaim at sorted position f;
+        // the next pod's loop-top barrier orders this pod's LDS and claim
+        // updates before anything reads them
+        if (tid == 0) {
+          HN.modkind = MOD_INC;
+          HN.modpos = f;
+          HN.nlog = h.nlog + 1;
+        }
         continue;
       }
+      __syncthreads();
 
       // ------------------------------- new NodeClaim from templates, in order
       const uint32_t cbase = SIM ? qoff : 0u;
@@ -1608,10 +1943,10 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= t_rem[(size_t)t * R + r];
             if (ok) hit = 0;
           }
-          if (blk.bmin(hit) == INF) continue;
+          if (wg.first(hit == 0, 0) == INF) continue;
         }
         if (M >= MCs) {
-          if (tid == 0) S.status = 1;
+          if (tid == 0) HN.status = 1;
           __syncthreads();
           break;
         }
@@ -1687,9 +2022,9 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           s_ord[M] = (uint16_t)M;
           s_sc[M] = 1;
           s_tmpl[M] = (uint8_t)t;
-          S.M = M + 1;
-          S.modkind = MOD_APPEND;
-          logp[S.nlog++] = LogRec{gp, v, j, 0};
+          HN.M = M + 1;
+          HN.modkind = MOD_APPEND;
+          logp[HN.nlog++] = LogRec{gp, v, j, 0};
           S.found = 1;
         }
         __syncthreads();
@@ -1709,6 +2044,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             ma[r] = r < R ? (int64_t)S.red64[r] : 0;
           }
           s_slk[j] = pack_slack(d, ma, nt);
+          s_rm[j] = pack_room(thr, s_thoff, S.c0, nt, d.RQ);
         }
         __syncthreads();
         if (tr.has_limits) {
@@ -1729,8 +2065,12 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         break;
       }
       __syncthreads();
-      if (tid == 0) S.t_tmpl += wall_clock64() - tA;
-      if (S.status) break;
+      if (tid == 0) {
+        S.dbg[14] = phase_clock();
+        S.t_tmpl += S.dbg[14] - tA;
+      }
+      TL(10);  // new NodeClaim
+      if (HN.status) break;
       if (S.found) continue;
 
       // ------------------------------------ failed: Relax, then Queue.Push
@@ -1740,15 +2080,15 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           cur_var[p] = v + 1;
           relaxed = true;
         }
-        uint32_t tail = S.qhead + S.qlen;
+        uint32_t tail = HN.qhead + HN.qlen;
         if (tail >= P) tail -= P;
         queue[tail] = p;
-        S.qlen++;
+        HN.qlen++;
         if (relaxed) {
-          S.epoch++;
+          HN.epoch++;
         } else {
-          last_epoch[p] = S.epoch;
-          last_len[p] = S.qlen;
+          last_epoch[p] = HN.epoch;
+          last_len[p] = HN.qlen;
         }
       }
       __syncthreads();
@@ -1756,17 +2096,17 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
 
     __syncthreads();
     if (!SIM)
-      for (uint32_t i = tid; i < S.M; i += FB) d.c_sorted[i] = s_ord[i];
+      for (uint32_t i = tid; i < S.hb[par ^ 1u].M; i += FB) d.c_sorted[i] = s_ord[i];
     if (SIM) {
       // SimulateScheduling's error pods that are not pending: still queued,
       // or placed on an uninitialized existing node
       uint32_t cnt = 0;
-      for (uint32_t i = tid; i < S.qlen; i += FB) {
-        uint32_t slot = S.qhead + i;
+      for (uint32_t i = tid; i < S.hb[par ^ 1u].qlen; i += FB) {
+        uint32_t slot = S.hb[par ^ 1u].qhead + i;
         if (slot >= P) slot -= P;
         cnt += gpod(queue[slot]) >= d.n_pending ? 1u : 0u;
       }
-      for (uint32_t i = tid; i < S.nlog; i += FB) {
+      for (uint32_t i = tid; i < S.hb[par ^ 1u].nlog; i += FB) {
         const LogRec l = logp[i];
         cnt += ((l.target & 0x80000000u) && l.pod >= d.n_pending && !d.nodes0[l.target & 0x7FFFFFFFu].init) ? 1u : 0u;
       }
@@ -1776,13 +2116,13 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
     }
     if (tid == 0) {
       Ctrl c;
-      c.status = S.status;
-      c.n_claims = S.M;
-      c.n_log = S.nlog;
-      c.qhead = S.qhead;
-      c.qlen = S.qlen;
-      c.epoch = S.epoch;
-      c.pops = S.pops;
+      c.status = S.hb[par ^ 1u].status;
+      c.n_claims = S.hb[par ^ 1u].M;
+      c.n_log = S.hb[par ^ 1u].nlog;
+      c.qhead = S.hb[par ^ 1u].qhead;
+      c.qlen = S.hb[par ^ 1u].qlen;
+      c.epoch = S.hb[par ^ 1u].epoch;
+      c.pops = S.hb[par ^ 1u].pops;
       c.generic_sorts = S.generic;
       c.fast_sorts = S.fast;
       c.cand_evals = S.cand;
@@ -1796,20 +2136,24 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       c.t_tmpl = S.t_tmpl;
       c.t_total = wall_clock64() - S.t0;
       S.dbg[7] = __builtin_amdgcn_s_memtime() - S.dbg[7];  // shader clock cycles over the solve
+#ifdef GS_FFD_TL
+      for (int q = 0; q < 16; q++) c.dbg[q] = S.tl[q];
+#else
       for (int q = 0; q < 16; q++) c.dbg[q] = S.dbg[q];
+#endif
       *(SIM ? d.sim_ctrl + sim : d.ctrl) = c;
     }
     __syncthreads();
   }
 }
 
-// dynamic LDS: ord/sc/scr u16 + slack u64 + tmpl u8 per claim, thresholds,
+// dynamic LDS: slack + room u64, ord/sc/scr u16, tmpl u8 per claim, thresholds,
 // (simulations) the touched-node bitmap + overlay ids, and the topology
 // spread state (known domains, per-pod minimum, zone counts) of TG groups
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
                                       uint32_t TG) {
   const uint32_t thr = nthr + 4;
-  const uint32_t base = (((15u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u + 7u) & ~7u;
+  const uint32_t base = (((23u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u + 7u) & ~7u;
   return base + TG * 16u + TG * ZVMAX * 4u;
 }
 

@@ -28,6 +28,10 @@ enum : uint32_t { ZF_COMP = 1u };  // zone requirement is a complement (Exists /
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 // capacity-type requirement bits (consolidation's spot-to-spot rule)
 enum : uint32_t { CT_SPOT = 1u, CT_OD = 2u };
+// VarRec.ctb flag: the variant has no requirements and no topology spread, so
+// NodeClaim.Add changes nothing but the requests (claims never carry it:
+// their ctb is the template's AND the pods')
+enum : uint32_t { VF_SIMPLE = 1u << 31 };
 
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)
