@@ -84,6 +84,7 @@ struct Shared {
   uint64_t t_sort, t_scan, t_tmpl, t0;
   uint64_t dbg[16];
   uint64_t tl[16], tl_last;  // GS_FFD_TL: shader cycles per loop segment (tid 0)
+  uint64_t tl_arr[NWAVE_MAX];  // GS_FFD_TL: per-wave arrival at the loop-top barrier
   uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
   uint32_t red[2][NWAVE_MAX];
   alignas(16) uint32_t red2[2][NWAVE_MAX];  // Wg reductions (own double buffer: never adjacent to a Blk one)
@@ -1114,7 +1115,24 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         }
         pf_state = 0;
       }
+#ifdef GS_FFD_TL
+      if (lane == 0) S.tl_arr[wave] = __builtin_amdgcn_s_memtime();
+#endif
       __syncthreads();
+#ifdef GS_FFD_TL
+      if (tid == 0) {
+        // the last wave to arrive and how much later than wave 0 it came
+        uint64_t last = S.tl_arr[0];
+        uint32_t lw = 0;
+        for (uint32_t w = 1; w < (uint32_t)(FB / 64); w++)
+          if (S.tl_arr[w] > last) {
+            last = S.tl_arr[w];
+            lw = w;
+          }
+        S.tl[11] += last - S.tl_arr[0];
+        S.tl[12 + (lw < 3 ? lw : 3)]++;
+      }
+#endif
       TL(1);  // publish + barrier
       // ------------------------------------------------------------ Queue.Pop
       // computed identically by every wave from one read of the uniform state

@@ -27,6 +27,8 @@ if "--tl" in sys.argv:
              "winner_end", "new_claim"]
     base["cycles_per_pop"] = {n: round(out[i] / max(res.pops, 1), 1) for i, n in enumerate(names)}
     base["cycles_per_pop_total"] = round(sum(out[i] for i in range(11)) / max(res.pops, 1), 1)
+    base["last_wave_lateness_vs_wave0"] = round(out[11] / max(res.pops, 1), 1)
+    base["last_wave_hist_w0_w1_w2_w3plus"] = [out[12], out[13], out[14], out[15]]
 else:
     base.update({"sort": res.t_ffd_sort_ms, "scan": res.t_ffd_scan_ms, "tmpl": res.t_ffd_template_ms,
                  "scan_tid0_work_ms": out[0] * 1e-5, "scan_wait_ms": out[1] * 1e-5, "chunks": out[2],
