@@ -394,6 +394,31 @@ typedef struct gs_feas_device {
 
 gs_status gs_feasibility_shard_device(gs_ctx* ctx, uint32_t word_begin, uint32_t word_end, gs_feas_device* out);
 
+/* Autoplacement ranking.  Replaces
+ * IBMInstanceTypeProvider.FilterInstanceTypes (pkg/providers/common/instancetype/
+ * instancetype.go:259-356) + rankInstanceTypes (:358-379); with every filter
+ * off it is RankInstanceTypes (:381-420).  Input: n instance types in List
+ * order (host buffers): capacity cpu (milli) and memory (bytes), both >= 0,
+ * the GetPrice result (0 when the lookup failed), an architecture id.
+ * Type i is kept when
+ *   (want_arch == GS_ARCH_ANY || arch[i] == want_arch)           :321
+ *   && (min_cpu <= 0 || ceil(cpu_milli/1000) >= min_cpu)           :326
+ *   && (min_memory_gb <= 0 || bytes / 2^30 >= min_memory_gb)       :331-335 (float64)
+ *   && (max_price <= 0 || price <= max_price)                      :339
+ * (max_price is the parsed MaximumHourlyPrice; the caller parses the string,
+ * as :311-317 does).  The kept types are ordered by calculateInstanceTypeScore
+ * (:90-110, float64, lower first) with Go's sort.Slice (pdqsort_func), so
+ * ties come out exactly as the reference's.  Writes out_order[0..*out_n)
+ * (List indices, ranked) and out_score (same order).  One workgroup on the
+ * current device; n <= GS_RANK_MAX (GS_E_CAPACITY above), negative
+ * quantities GS_E_INVALID. */
+#define GS_ARCH_ANY 0xFFFFFFFFu
+#define GS_RANK_MAX 4096u
+gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,
+                                 const double* price, const uint32_t* arch, uint32_t want_arch, int64_t min_cpu,
+                                 int64_t min_memory_gb, double max_price, uint32_t* out_order, uint32_t* out_n,
+                                 double* out_score);
+
 /* host-only: run the encoder (no device needed) and report whether this
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.
  * A Go caller uses it to choose between this library and upstream Solve. */

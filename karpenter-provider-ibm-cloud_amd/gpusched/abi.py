@@ -247,3 +247,31 @@ def commands_to_list(res: GsConsolidationResult) -> list:
                     "spot_only": int(c.spot_only), "options": opts, "option_prices": prices,
                     "candidate_price": float(c.candidate_price)})
     return out
+
+
+# gs_rank_instance_types / oracle_rank_instance_types (include/gpusched.h)
+GS_ARCH_ANY = 0xFFFFFFFF
+GS_RANK_MAX = 4096
+RANK_ARGTYPES = [C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                 C.POINTER(C.c_uint32), C.c_uint32, C.c_int64, C.c_int64, C.c_double,
+                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
+
+
+def call_rank(fn, cpu_milli, memory_bytes, price, arch, want_arch=GS_ARCH_ANY, min_cpu=0, min_memory_gb=0,
+              max_price=0.0):
+    """marshal one ranking call -> (status, List indices in ranked order, scores)"""
+    n = len(cpu_milli)
+    m = max(n, 1)
+    cpu = np.ascontiguousarray(cpu_milli, dtype=np.int64)
+    mem = np.ascontiguousarray(memory_bytes, dtype=np.int64)
+    pr = np.ascontiguousarray(price, dtype=np.float64)
+    ar = np.ascontiguousarray(arch, dtype=np.uint32)
+    order = np.zeros(m, dtype=np.uint32)
+    score = np.zeros(m, dtype=np.float64)
+    kept = C.c_uint32(0)
+    p = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    st = fn(n, p(cpu, C.c_int64), p(mem, C.c_int64), p(pr, C.c_double), p(ar, C.c_uint32), want_arch,
+            int(min_cpu), int(min_memory_gb), float(max_price), p(order, C.c_uint32), C.byref(kept),
+            p(score, C.c_double))
+    k = kept.value
+    return st, order[:k].tolist(), score[:k].tolist()

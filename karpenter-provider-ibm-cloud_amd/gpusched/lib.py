@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libgpusched.so")
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
            "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard",
-           "gs_feasibility_shard_device"]
+           "gs_feasibility_shard_device", "gs_rank_instance_types"]
 
 
 class GpuSchedError(RuntimeError):
@@ -52,6 +52,8 @@ def load():
         L.gs_feasibility_shard.restype = C.c_int
         L.gs_feasibility_shard_device.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.GsFeasDevice)]
         L.gs_feasibility_shard_device.restype = C.c_int
+        L.gs_rank_instance_types.argtypes = abi.RANK_ARGTYPES
+        L.gs_rank_instance_types.restype = C.c_int
         L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.gs_last_error.restype = C.c_size_t
         L.gs_version.argtypes = []
@@ -72,6 +74,17 @@ def load():
         L.gs_consolidation_choose.restype = C.c_int
         _lib = L
     return _lib
+
+
+def rank_instance_types(cpu_milli, memory_bytes, price, arch, want_arch=abi.GS_ARCH_ANY, min_cpu=0,
+                        min_memory_gb=0, max_price=0.0):
+    """gs_rank_instance_types (FilterInstanceTypes + rankInstanceTypes,
+    instancetype.go:259-379) -> (List indices ranked, scores)"""
+    st, order, score = abi.call_rank(load().gs_rank_instance_types, cpu_milli, memory_bytes, price, arch,
+                                     want_arch, min_cpu, min_memory_gb, max_price)
+    if st != abi.GS_OK:
+        raise GpuSchedError(st, "gs_rank_instance_types")
+    return order, score
 
 
 def _multi(res):

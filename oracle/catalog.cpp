@@ -8,6 +8,7 @@
 //   GetSupportedCapacityTypes         pkg/providers/common/capacitytype/capacitytype.go:48-85
 // Pinned by the reference's known-answer tests (tests/test_oracle_kats.py).
 #include "oracle.h"
+#include "gosort.h"
 
 #include <cmath>
 #include <cstdio>
@@ -150,6 +151,45 @@ extern "C" double oracle_instance_score(int64_t cpu_milli, int64_t memory_bytes,
   double a = price / cpu;
   double b = price / memGB;
   return (a + b) / 2;
+}
+
+// FilterInstanceTypes (instancetype.go:259-356): the four filters in List
+// order (:319-344), then rankInstanceTypes (:358-379): sort.Slice over
+// (type, score) records with Less = score[i] < score[j].
+extern "C" gs_status oracle_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,
+                                                const double* price, const uint32_t* arch, uint32_t want_arch,
+                                                int64_t min_cpu, int64_t min_memory_gb, double max_price,
+                                                uint32_t* out_order, uint32_t* out_n, double* out_score) {
+  if (!out_n || (n && (!cpu_milli || !memory_bytes || !price || !arch || !out_order || !out_score)))
+    return GS_E_INVALID;
+  if (n > GS_RANK_MAX) return GS_E_CAPACITY;
+  for (uint32_t i = 0; i < n; i++)
+    if (cpu_milli[i] < 0 || memory_bytes[i] < 0) return GS_E_INVALID;
+  struct Rankings {
+    std::vector<double> score;
+    std::vector<uint32_t> idx;
+    bool less(int i, int j) const { return score[i] < score[j]; }
+    void swap(int i, int j) {
+      std::swap(score[i], score[j]);
+      std::swap(idx[i], idx[j]);
+    }
+  } r;
+  for (uint32_t i = 0; i < n; i++) {
+    if (want_arch != GS_ARCH_ANY && arch[i] != want_arch) continue;                  // :321
+    if (min_cpu > 0 && (cpu_milli[i] + 999) / 1000 < min_cpu) continue;                // :326
+    if (min_memory_gb > 0 && (double)memory_bytes[i] / (1024.0 * 1024 * 1024) < (double)min_memory_gb)
+      continue;                                                                          // :331-335
+    if (max_price > 0 && price[i] > max_price) continue;                                // :339
+    r.score.push_back(oracle_instance_score(cpu_milli[i], memory_bytes[i], price[i]));
+    r.idx.push_back(i);
+  }
+  gosort::slice(r, (int)r.idx.size());
+  for (size_t k = 0; k < r.idx.size(); k++) {
+    out_order[k] = r.idx[k];
+    out_score[k] = r.score[k];
+  }
+  *out_n = (uint32_t)r.idx.size();
+  return GS_OK;
 }
 
 extern "C" gs_status oracle_convert_profile(const oracle_profile* pr, const oracle_catalog_env* env,

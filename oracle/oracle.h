@@ -74,6 +74,13 @@ const char* oracle_instance_size(const char* name);
 const char* oracle_capacity_type(const char* availability_class);
 /* calculateInstanceTypeScore (instancetype.go:90-110) for cpu/memory quantities */
 double oracle_instance_score(int64_t cpu_milli, int64_t memory_bytes, double price);
+/* FilterInstanceTypes (instancetype.go:259-356) + rankInstanceTypes (:358-379):
+ * the CPU restatement of gs_rank_instance_types (same arguments and result;
+ * GS_E_INVALID / GS_E_CAPACITY on the same inputs, no device needed). */
+gs_status oracle_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,
+                                     const double* price, const uint32_t* arch, uint32_t want_arch, int64_t min_cpu,
+                                     int64_t min_memory_gb, double max_price, uint32_t* out_order, uint32_t* out_n,
+                                     double* out_score);
 
 /* <U> disruption consolidation (SimulateScheduling + computeConsolidation and
  * the single/multi-node policies), one naive Solve per simulation.  For MULTI

@@ -63,6 +63,8 @@ def lib():
             getattr(L, f).restype = C.c_char_p
         L.oracle_instance_score.argtypes = [C.c_int64, C.c_int64, C.c_double]
         L.oracle_instance_score.restype = C.c_double
+        L.oracle_rank_instance_types.argtypes = abi.RANK_ARGTYPES
+        L.oracle_rank_instance_types.restype = C.c_int
         L.oracle_consolidate.argtypes = [C.POINTER(abi.GsConsolidation), C.POINTER(abi.GsConsolidationResult),
                                          C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_consolidate.restype = C.c_int
@@ -171,3 +173,10 @@ def parse_text(text):
         else:
             it[k] = v
     return it
+
+
+def rank_instance_types(cpu_milli, memory_bytes, price, arch, want_arch=abi.GS_ARCH_ANY, min_cpu=0,
+                        min_memory_gb=0, max_price=0.0):
+    """oracle_rank_instance_types -> (status, List indices ranked, scores)"""
+    return abi.call_rank(lib().oracle_rank_instance_types, cpu_milli, memory_bytes, price, arch, want_arch,
+                         min_cpu, min_memory_gb, max_price)
