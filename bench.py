@@ -296,6 +296,42 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
     return out
 
 
+def bench_ranking(args):
+    """Autoplacement ranking (FilterInstanceTypes + rankInstanceTypes,
+    instancetype.go:259-379) over a C5-sized catalog of 2,000 instance types
+    with all filters off (RankInstanceTypes).  One call = host buffers in,
+    ranked indices out, so the time is PCIe- and allocation-inclusive; rank 0
+    at N=1 only (replicas: the call does not shard)."""
+    import numpy as np
+    from gpusched import lib
+    rng = np.random.default_rng(5)
+    n = 2000
+    vcpu = rng.choice([2, 4, 8, 16, 32, 48, 64, 96], size=n)
+    ratio = rng.choice([2, 4, 8], size=n)
+    cpu = (vcpu * 1000).astype(np.int64)
+    mem = (vcpu * ratio * (1 << 30)).astype(np.int64)
+    price = np.round(vcpu * ratio * rng.choice([0.01, 0.0125, 0.02], size=n), 4)
+    arch = np.zeros(n, dtype=np.uint32)
+    for _ in range(max(args.warmup, 1)):
+        lib.rank_instance_types(cpu, mem, price, arch)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        order, score = lib.rank_instance_types(cpu, mem, price, arch)
+    ms = (time.perf_counter() - t0) * 1000 / args.steps
+    out = {"workload": f"RankInstanceTypes over {n} instance types (C5 catalog size), exact score ties",
+           "types": n, "ms_per_call_pcie_inclusive": round(ms, 4), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        from oracle import pyoracle
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            st, want, _ = pyoracle.rank_instance_types(cpu, mem, price, arch)
+        cms = (time.perf_counter() - t0) * 1000 / reps
+        out["cpu_baseline"] = {"ms_per_call": round(cms, 4), "cores": 1, "kind": "port",
+                               "sample": f"same {n} types, {reps} calls; GPU order identical: {want == order}"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -430,6 +466,8 @@ def main():
         line["consolidation"] = bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks)
     if not args.no_stress:
         line["stress"] = bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks)
+    if rank == 0 and world == 1:
+        line["ranking"] = bench_ranking(args)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

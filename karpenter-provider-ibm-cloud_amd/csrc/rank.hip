@@ -15,6 +15,10 @@
 // type in, 12 B out); there is nothing here for MFMA or the HBM roofline.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
 
 #include "../../include/gpusched.h"
 
@@ -317,45 +321,56 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GS_E_NO_DEVICE;
   if (n == 0) return GS_OK;
-  // one device buffer: inputs (8+8+8+4 B per type), outputs (4+8 B), count
+  // one grow-once device buffer (serialized by a mutex): inputs packed as
+  // cpu | mem | price (8 B each) | arch (4 B), outputs score (8 B) | order
+  // (4 B) | count; one H2D copy in, one D2H copy out
+  static std::mutex mu;
+  static char* dbuf = nullptr;
+  static size_t dcap = 0;
+  static std::vector<char> hin, hout;
+  std::lock_guard<std::mutex> lock(mu);
   const size_t nn = n;
-  const size_t bytes = nn * (8 + 8 + 8 + 8) + nn * 4 + nn * 4 + 64;
-  char* d = nullptr;
-  if (hipMalloc(&d, bytes) != hipSuccess) return GS_E_HIP;
-  gs_status st = GS_OK;
+  const size_t in_bytes = nn * 28, out_bytes = nn * 12 + 8;
+  const size_t bytes = ((in_bytes + 255) & ~(size_t)255) + out_bytes;
+  if (bytes > dcap) {
+    if (dbuf) (void)hipFree(dbuf);
+    dbuf = nullptr;
+    dcap = 0;
+    if (hipMalloc(&dbuf, bytes) != hipSuccess) return GS_E_HIP;
+    dcap = bytes;
+  }
+  char* d = dbuf;
+  char* dout = d + ((in_bytes + 255) & ~(size_t)255);
+  hin.resize(in_bytes);
+  hout.resize(out_bytes);
+  memcpy(hin.data(), cpu_milli, nn * 8);
+  memcpy(hin.data() + nn * 8, memory_bytes, nn * 8);
+  memcpy(hin.data() + nn * 16, price, nn * 8);
+  memcpy(hin.data() + nn * 24, arch, nn * 4);
   RankArgs a{};
   a.cpu_milli = (const int64_t*)d;
   a.memory_bytes = (const int64_t*)(d + nn * 8);
   a.price = (const double*)(d + nn * 16);
-  a.out_score = (double*)(d + nn * 24);
-  a.arch = (const uint32_t*)(d + nn * 32);
-  a.out_order = (uint32_t*)(d + nn * 36);
-  a.out_n = (uint32_t*)(d + nn * 40);
+  a.arch = (const uint32_t*)(d + nn * 24);
+  a.out_score = (double*)dout;
+  a.out_order = (uint32_t*)(dout + nn * 8);
+  a.out_n = (uint32_t*)(dout + nn * 12);
   a.min_cpu = min_cpu;
   a.min_memory_gb = min_memory_gb;
   a.max_price = max_price;
   a.n = n;
   a.want_arch = want_arch;
   const size_t lds = nn * (sizeof(double) + sizeof(uint32_t));
-  uint32_t kept = 0;
-  do {
-    if (hipMemcpy((void*)a.cpu_milli, cpu_milli, nn * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy((void*)a.memory_bytes, memory_bytes, nn * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy((void*)a.price, price, nn * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy((void*)a.arch, arch, nn * 4, hipMemcpyHostToDevice) != hipSuccess) {
-      st = GS_E_HIP;
-      break;
-    }
-    hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(RK_NT), lds, 0, a);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(&kept, a.out_n, 4, hipMemcpyDeviceToHost) != hipSuccess || kept > n ||
-        hipMemcpy(out_order, a.out_order, (size_t)kept * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(out_score, a.out_score, (size_t)kept * 8, hipMemcpyDeviceToHost) != hipSuccess) {
-      st = GS_E_HIP;
-      break;
-    }
-    *out_n = kept;
-  } while (0);
-  (void)hipFree(d);
-  return st;
+  if (hipMemcpy(d, hin.data(), in_bytes, hipMemcpyHostToDevice) != hipSuccess) return GS_E_HIP;
+  hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(RK_NT), lds, 0, a);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpy(hout.data(), dout, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)  // null stream: after the kernel
+    return GS_E_HIP;
+  uint32_t kept;
+  memcpy(&kept, hout.data() + nn * 12, 4);
+  if (kept > n) return GS_E_HIP;
+  memcpy(out_score, hout.data(), (size_t)kept * 8);
+  memcpy(out_order, hout.data() + nn * 8, (size_t)kept * 4);
+  *out_n = kept;
+  return GS_OK;
 }
