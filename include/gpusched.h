@@ -411,7 +411,7 @@ gs_status gs_feasibility_shard_device(gs_ctx* ctx, uint32_t word_begin, uint32_t
  * ties come out exactly as the reference's.  Writes out_order[0..*out_n)
  * (List indices, ranked) and out_score (same order).  One workgroup on the
  * current device; n <= GS_RANK_MAX (GS_E_CAPACITY above), negative
- * quantities GS_E_INVALID. */
+ * quantities and NaN prices GS_E_INVALID. */
 #define GS_ARCH_ANY 0xFFFFFFFFu
 #define GS_RANK_MAX 4096u
 gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,

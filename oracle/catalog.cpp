@@ -164,7 +164,7 @@ extern "C" gs_status oracle_rank_instance_types(uint32_t n, const int64_t* cpu_m
     return GS_E_INVALID;
   if (n > GS_RANK_MAX) return GS_E_CAPACITY;
   for (uint32_t i = 0; i < n; i++)
-    if (cpu_milli[i] < 0 || memory_bytes[i] < 0) return GS_E_INVALID;
+    if (cpu_milli[i] < 0 || memory_bytes[i] < 0 || std::isnan(price[i])) return GS_E_INVALID;
   struct Rankings {
     std::vector<double> score;
     std::vector<uint32_t> idx;

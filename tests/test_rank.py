@@ -45,6 +45,7 @@ def test_filters():
 
 def test_refusals():
     assert pyoracle.rank_instance_types([-1], [GI], [0.1], [0])[0] == abi.GS_E_INVALID
+    assert pyoracle.rank_instance_types([1000], [GI], [float('nan')], [0])[0] == abi.GS_E_INVALID
     n = abi.GS_RANK_MAX + 1
     assert pyoracle.rank_instance_types([1000] * n, [GI] * n, [0.1] * n, [0] * n)[0] == abi.GS_E_CAPACITY
     assert pyoracle.rank_instance_types([], [], [], []) == (abi.GS_OK, [], [])
@@ -107,6 +108,8 @@ def test_gpu_rank_kats_and_refusals():
     assert score == [0.0763888888888889, 0.0769927536231884, 11.0]
     with pytest.raises(lib.GpuSchedError):
         lib.rank_instance_types([-1], [GI], [0.1], [0])
+    with pytest.raises(lib.GpuSchedError):
+        lib.rank_instance_types([1000], [GI], [float('nan')], [0])
     n = abi.GS_RANK_MAX + 1
     with pytest.raises(lib.GpuSchedError):
         lib.rank_instance_types([1000] * n, [GI] * n, [0.1] * n, [0] * n)
