@@ -8,8 +8,9 @@
 //   1. per type, the four filters and calculateInstanceTypeScore (:90-110) in
 //      float64; kept types are compacted IN LIST ORDER into LDS with a ballot
 //      prefix per 256-type chunk (sort.Slice's input order decides tie order);
-//      each kept score gets a u16 key = how many kept scores are strictly
-//      below it (ties share a key, so every Less outcome is the float64 one);
+//      rank_key_kernel (grid-wide) gives each kept score a u16 key = how many
+//      kept scores are strictly below it (ties share a key, so every Less
+//      outcome is the float64 one);
 //   2. rank_sort_kernel (ffd.hip) runs the block-parallel restatement of Go's
 //      sort.Slice (pdqsort_func) that orders in-flight NodeClaims, on
 //      (key, position) pairs in LDS;
@@ -92,18 +93,35 @@ __global__ __launch_bounds__(RK_NT) void rank_kernel(RankArgs a) {
     kept += total;
     __syncthreads();  // wcnt reuse, and the compacted arrays before the sort
   }
-  // sort keys: how many kept scores are strictly below (ties share a key;
-  // key order == float64 order), payload the compacted position
   for (uint32_t k = tid; k < kept; k += RK_NT) {
-    const double x = sc[k];
-    uint32_t below = 0;
-    for (uint32_t j = 0; j < kept; j++) below += sc[j] < x;
-    a.keys[k] = (uint16_t)below;
-    a.pos[k] = (uint16_t)k;
-    a.cscore[k] = x;
+    a.cscore[k] = sc[k];
     a.cidx[k] = ix[k];
   }
   if (tid == 0) *a.out_n = kept;
+}
+
+// sort keys: key[k] = how many kept scores are strictly below score k (ties
+// share a key; key order == float64 order), payload the compacted position.
+// Workgroup b owns k in [64b, 64b + 64) (lane = k); its 4 waves split the j
+// range and add their partial counts in LDS.  The score read is wave-uniform.
+__global__ __launch_bounds__(RK_NT) void rank_key_kernel(RankArgs a) {
+  __shared__ uint32_t part[RK_NWAVE][64];
+  const uint32_t kept = *a.out_n;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t k = blockIdx.x * 64u + lane;
+  const double x = k < kept ? a.cscore[k] : 0.0;
+  const uint32_t per = (kept + RK_NWAVE - 1) / RK_NWAVE;
+  const uint32_t j0 = wave * per, j1 = j0 + per < kept ? j0 + per : kept;
+  uint32_t below = 0;
+  for (uint32_t j = j0; j < j1; j++) below += a.cscore[j] < x;
+  part[wave][lane] = below;
+  __syncthreads();
+  if (wave == 0 && k < kept) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < RK_NWAVE; w++) t += part[w][lane];
+    a.keys[k] = (uint16_t)t;
+    a.pos[k] = (uint16_t)k;
+  }
 }
 
 // after rank_sort_kernel: ranked List indices and scores
@@ -181,6 +199,7 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   const size_t lds = nn * (sizeof(double) + sizeof(uint32_t));
   if (hipMemcpy(d, hin.data(), in_bytes, hipMemcpyHostToDevice) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(RK_NT), lds, 0, a);
+  hipLaunchKernelGGL(rank_key_kernel, dim3((n + 63) / 64), dim3(RK_NT), 0, 0, a);
   if (hipGetLastError() != hipSuccess || gsk_rank_sort(a.keys, a.pos, a.out_n, n, 0) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_gather_kernel, dim3((n + RK_NT - 1) / RK_NT), dim3(RK_NT), 0, 0, a);
   if (hipGetLastError() != hipSuccess ||
