@@ -433,7 +433,9 @@ struct Wg {
 };
 
 // ------------------------------------------------------------ block-parallel
-template <uint32_t NT>
+// SEQ: subranges up to this length run on thread 0 (any SEQ >= 12 gives the
+// same permutation: both paths restate pdqsort_func)
+template <uint32_t NT, int SEQ = SEQ_SORT>
 struct Blk {
   static constexpr int FB = (int)NT;
   static constexpr int NWAVE = (int)NT / 64;
@@ -711,7 +713,7 @@ struct Blk {
   }
   __device__ void pdqsort(int n) {
     SeqSort seq{sc, ord};
-    if (n <= SEQ_SORT) {
+    if (n <= SEQ) {
       if (tid == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
       sync();
       return;
@@ -721,7 +723,7 @@ struct Blk {
     for (;;) {
       for (;;) {
         const int length = f.b - f.a;
-        if (length <= SEQ_SORT) {
+        if (length <= SEQ) {
           if (tid == 0) seq.pdq_frame(f);
           sync();
           break;
@@ -2252,6 +2254,10 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
 // compare (NaN refused on the host), so the permutation is the reference's.
 // pos[k] = compacted position; both sorted in place.  *np = the kept count
 // (written by rank_kernel on the same stream); cap bounds it (<= GS_RANK_MAX).
+#ifndef GS_RANK_SEQ
+#define GS_RANK_SEQ 32
+#endif
+constexpr int RANK_SEQ = GS_RANK_SEQ;
 extern "C" __global__ __launch_bounds__(FB_MAX) void rank_sort_kernel(uint16_t* keys, uint16_t* pos,
                                                                       const uint32_t* np, uint32_t cap) {
   __shared__ Shared S;
@@ -2266,7 +2272,7 @@ extern "C" __global__ __launch_bounds__(FB_MAX) void rank_sort_kernel(uint16_t* 
     ord[k] = pos[k];
   }
   __syncthreads();
-  Blk<FB_MAX> blk{sc, ord, scr, S, tid, tid & 63, tid >> 6, 0, (n + 1) / 2};
+  Blk<FB_MAX, RANK_SEQ> blk{sc, ord, scr, S, tid, tid & 63, tid >> 6, 0, (n + 1) / 2};
   blk.pdqsort((int)n);
   __syncthreads();
   for (uint32_t k = tid; k < n; k += FB_MAX) {
