@@ -49,7 +49,10 @@ namespace {
 constexpr int FB_MAX = GS_FB_MAX;  // workgroup size of the provisioning Solve (512: 256 VGPRs, no spills)
 constexpr int FB_SIM = 256;   // workgroup size of one consolidation simulation
 constexpr int NWAVE_MAX = FB_MAX / 64;
-constexpr int SEQ_SORT = 128;  // subranges up to this length sort on thread 0
+#ifndef GS_SEQ_SORT
+#define GS_SEQ_SORT 32  // measured on CM: 32 -> 789 ms, 64 -> 815, 128 -> 819 (same box)
+#endif
+constexpr int SEQ_SORT = GS_SEQ_SORT;  // subranges up to this length sort on thread 0
 
 constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
 enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
