@@ -255,10 +255,17 @@ typedef struct gs_feas_result {
 
 typedef struct gs_ctx gs_ctx;
 
+/* gs_config.flags */
+enum {
+  /* run the provisioning Solve on the multi-wave block kernel even when the
+   * single-wave kernel applies (both are bit-identical; tests compare them) */
+  GS_CFG_BLOCK_SOLVE = 1u << 0
+};
+
 typedef struct gs_config {
   int32_t device;        /* HIP device ordinal */
   uint32_t max_claims;   /* 0 = default */
-  uint32_t flags;        /* reserved */
+  uint32_t flags;        /* GS_CFG_* */
 } gs_config;
 
 /* ------------------------------------------------------------------------

@@ -35,7 +35,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   } else {
     // NodeClaims the LDS holds next to the thresholds and topology state
     const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, e.TG) + 8;
-    const uint32_t dyn = gsk_ffd_dyn_lds_max();
+    const uint32_t dyn = std::min(gsk_ffd_dyn_lds_max(), gsk_ffdw_dyn_lds_max());
     const uint32_t fit = dyn > other ? (dyn - other) / 23 : 0;
     d.max_claims = std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
     if (!d.max_claims) throw HipError{"topology / threshold state leaves no LDS for NodeClaims"};
@@ -234,6 +234,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GS_E_NO_DEVICE;
   auto* c = new gs_ctx();
   c->device = cfg ? cfg->device : 0;
+  c->cfg_flags = cfg ? cfg->flags : 0;
   try {
     HIPCHK(hipSetDevice(c->device));
     hipDeviceProp_t prop;
@@ -245,6 +246,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(gsk_init_ffd(kLdsBytes));
+    HIPCHK(gsk_init_ffdw(kLdsBytes));
     HIPCHK(gsk_init_trunc(65536));
   } catch (const HipError& e) {
     delete c;
@@ -295,7 +297,10 @@ gs_status gs_run(gs_ctx* c) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_feas(c, 0);
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    HIPCHK(gsk_ffd(&d, 1, c->stream));
+    if (!(c->cfg_flags & GS_CFG_BLOCK_SOLVE) && d.NN <= kWaveSolveMaxNodes)
+      HIPCHK(gsk_ffdw(&d, c->stream));
+    else
+      HIPCHK(gsk_ffd(&d, 1, c->stream));
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));

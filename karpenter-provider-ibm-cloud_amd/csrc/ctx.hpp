@@ -23,12 +23,18 @@ extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
                                hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);
+extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total);
+extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
+extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
 
 namespace gsc {
 
 constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: 4x u16 slack + room, ord/sc/scratch u16, tmpl u8, thresholds
 constexpr uint32_t kLdsBytes = 160 * 1024; // gfx950 LDS per workgroup
+// the single-wave Solve (ffd_wave.hip) scans existing nodes 64 at a time;
+// problems with more state nodes run the block kernel (ffd.hip)
+constexpr uint32_t kWaveSolveMaxNodes = 512;
 
 using Clock = std::chrono::steady_clock;
 inline double ms_since(Clock::time_point t0) {
@@ -59,6 +65,7 @@ struct SimPlan {
 
 struct gs_ctx {
   int device = 0;
+  uint32_t cfg_flags = 0;  // gs_config.flags
   std::string err;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "devutil.hpp"
+#include "ffd_common.hpp"
 #include "layout.hpp"
 
 using namespace gsd;
@@ -57,10 +58,6 @@ constexpr int SEQ_SORT = GS_SEQ_SORT;  // subranges up to this length sort on th
 constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
 enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 
-struct Frame {
-  int a, b, limit;
-  int wb, wp;  // wasBalanced, wasPartitioned
-};
 
 // Block-uniform state of the pod loop.  Every wave reads it once per pod
 // right after the loop-top barrier and then keeps its own register copy,
@@ -104,246 +101,6 @@ struct Shared {
 constexpr uint32_t VR_DW = sizeof(VarRec) / 4;
 static_assert(VR_DW <= 32, "VarRec prefetch uses one lane per dword");
 
-__device__ __forceinline__ int bits_len(uint64_t x) { return x ? 64 - __clzll((long long)x) : 0; }
-
-// ---------------------------------------------------------------- sequential
-// Go sort.Slice (src/sort/zsortfunc.go) over u16 keys with u16 payload, one
-// thread; pdq_frame() resumes a pdqsort_func loop from a given frame state.
-struct SeqSort {
-  uint16_t* sc;
-  uint16_t* ord;
-  __device__ bool less(int i, int j) const { return sc[i] < sc[j]; }
-  __device__ void swap(int i, int j) const {
-    uint16_t a = sc[i];
-    sc[i] = sc[j];
-    sc[j] = a;
-    a = ord[i];
-    ord[i] = ord[j];
-    ord[j] = a;
-  }
-  __device__ void insertion_sort(int a, int b) const {
-    for (int i = a + 1; i < b; i++)
-      for (int j = i; j > a && less(j, j - 1); j--) swap(j, j - 1);
-  }
-  __device__ void sift_down(int lo, int hi, int first) const {
-    int root = lo;
-    for (;;) {
-      int child = 2 * root + 1;
-      if (child >= hi) return;
-      if (child + 1 < hi && less(first + child, first + child + 1)) child++;
-      if (!less(first + root, first + child)) return;
-      swap(first + root, first + child);
-      root = child;
-    }
-  }
-  __device__ void heap_sort(int a, int b) const {
-    int first = a, lo = 0, hi = b - a;
-    for (int i = (hi - 1) / 2; i >= 0; i--) sift_down(i, hi, first);
-    for (int i = hi - 1; i >= 0; i--) {
-      swap(first, first + i);
-      sift_down(lo, i, first);
-    }
-  }
-  __device__ int partition(int a, int b, int pivot, bool* already) const {
-    swap(a, pivot);
-    int i = a + 1, j = b - 1;
-    while (i <= j && less(i, a)) i++;
-    while (i <= j && !less(j, a)) j--;
-    if (i > j) {
-      swap(j, a);
-      *already = true;
-      return j;
-    }
-    swap(i, j);
-    i++;
-    j--;
-    for (;;) {
-      while (i <= j && less(i, a)) i++;
-      while (i <= j && !less(j, a)) j--;
-      if (i > j) break;
-      swap(i, j);
-      i++;
-      j--;
-    }
-    swap(j, a);
-    *already = false;
-    return j;
-  }
-  __device__ int partition_equal(int a, int b, int pivot) const {
-    swap(a, pivot);
-    int i = a + 1, j = b - 1;
-    for (;;) {
-      while (i <= j && !less(a, i)) i++;
-      while (i <= j && less(a, j)) j--;
-      if (i > j) break;
-      swap(i, j);
-      i++;
-      j--;
-    }
-    return i;
-  }
-  __device__ bool partial_insertion_sort(int a, int b) const {
-    int i = a + 1;
-    for (int j = 0; j < 5; j++) {
-      while (i < b && !less(i, i - 1)) i++;
-      if (i == b) return true;
-      if (b - a < 50) return false;
-      swap(i, i - 1);
-      if (i - a >= 2)
-        for (int k = i - 1; k >= 1; k--) {
-          if (!less(k, k - 1)) break;
-          swap(k, k - 1);
-        }
-      if (b - i >= 2)
-        for (int k = i + 1; k < b; k++) {
-          if (!less(k, k - 1)) break;
-          swap(k, k - 1);
-        }
-    }
-    return false;
-  }
-  __device__ void break_patterns(int a, int b) const {
-    int length = b - a;
-    if (length >= 8) {
-      uint64_t r = (uint64_t)length;
-      uint64_t modulus = 1ull << bits_len((uint64_t)length);
-      int idx = a + (length / 4) * 2 - 1;
-      for (int i = 0; i < 3; i++) {
-        r ^= r << 13;
-        r ^= r >> 7;
-        r ^= r << 17;
-        int other = (int)(r & (modulus - 1));
-        if (other >= length) other -= length;
-        swap(idx - 1 + i, a + other);
-      }
-    }
-  }
-  __device__ void order2(int& a, int& b, int* swaps) const {
-    if (less(b, a)) {
-      (*swaps)++;
-      int t = a;
-      a = b;
-      b = t;
-    }
-  }
-  __device__ int median(int a, int b, int c, int* swaps) const {
-    order2(a, b, swaps);
-    order2(b, c, swaps);
-    order2(a, b, swaps);
-    return b;
-  }
-  // choosePivot with the (up to) 9 sampled keys loaded in one round trip;
-  // same comparisons, same swaps count, same result as choose_pivot()
-  __device__ int choose_pivot_fast(int a, int b, int* hint) const {
-    const int l = b - a;
-    int swaps = 0;
-    const int i0 = a + l / 4 * 1, j0 = a + l / 4 * 2, k0 = a + l / 4 * 3;
-    if (l < 8) {
-      *hint = 1;
-      return j0;
-    }
-    int idx[9] = {i0 - 1, i0, i0 + 1, j0 - 1, j0, j0 + 1, k0 - 1, k0, k0 + 1};
-    uint16_t key[9];
-#pragma unroll
-    for (int t = 0; t < 9; t++) key[t] = (l >= 50 || t % 3 == 1) ? sc[idx[t]] : 0;
-    auto med = [&](int x, int y, int z, uint16_t kx, uint16_t ky, uint16_t kz, uint16_t* km) {
-      // order2(x,y); order2(y,z); order2(x,y); return y
-      if (ky < kx) { swaps++; int t = x; x = y; y = t; uint16_t u = kx; kx = ky; ky = u; }
-      if (kz < ky) { swaps++; int t = y; y = z; z = t; uint16_t u = ky; ky = kz; kz = u; }
-      if (ky < kx) { swaps++; int t = x; x = y; y = t; uint16_t u = kx; kx = ky; ky = u; }
-      *km = ky;
-      return y;
-    };
-    int i = i0, j = j0, k = k0;
-    uint16_t ki = key[1], kj = key[4], kk = key[7];
-    if (l >= 50) {
-      i = med(idx[0], idx[1], idx[2], key[0], key[1], key[2], &ki);
-      j = med(idx[3], idx[4], idx[5], key[3], key[4], key[5], &kj);
-      k = med(idx[6], idx[7], idx[8], key[6], key[7], key[8], &kk);
-    }
-    uint16_t km;
-    j = med(i, j, k, ki, kj, kk, &km);
-    *hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
-    return j;
-  }
-  // hint: 0 unknown, 1 increasing, 2 decreasing
-  __device__ int choose_pivot(int a, int b, int* hint) const {
-    int l = b - a, swaps = 0;
-    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
-    if (l >= 8) {
-      if (l >= 50) {
-        i = median(i - 1, i, i + 1, &swaps);
-        j = median(j - 1, j, j + 1, &swaps);
-        k = median(k - 1, k, k + 1, &swaps);
-      }
-      j = median(i, j, k, &swaps);
-    }
-    *hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
-    return j;
-  }
-  __device__ void reverse_range(int a, int b) const {
-    int i = a, j = b - 1;
-    while (i < j) {
-      swap(i, j);
-      i++;
-      j--;
-    }
-  }
-  __device__ void pdq_frame(Frame f0) const {
-    Frame st[32];
-    int sp = 0;
-    st[sp++] = f0;
-    while (sp > 0) {
-      Frame f = st[--sp];
-      for (;;) {
-        int length = f.b - f.a;
-        if (length <= 12) {
-          insertion_sort(f.a, f.b);
-          break;
-        }
-        if (f.limit == 0) {
-          heap_sort(f.a, f.b);
-          break;
-        }
-        if (!f.wb) {
-          break_patterns(f.a, f.b);
-          f.limit--;
-        }
-        int hint;
-        int pivot = choose_pivot(f.a, f.b, &hint);
-        if (hint == 2) {
-          reverse_range(f.a, f.b);
-          pivot = (f.b - 1) - (pivot - f.a);
-          hint = 1;
-        }
-        if (f.wb && f.wp && hint == 1) {
-          if (partial_insertion_sort(f.a, f.b)) break;
-        }
-        if (f.a > 0 && !less(f.a - 1, pivot)) {
-          f.a = partition_equal(f.a, f.b, pivot);
-          continue;
-        }
-        bool already;
-        int mid = partition(f.a, f.b, pivot, &already);
-        f.wp = already;
-        int leftLen = mid - f.a, rightLen = f.b - mid;
-        int bal = length / 8;
-        Frame child;
-        if (leftLen < rightLen) {
-          f.wb = leftLen >= bal;
-          child = Frame{f.a, mid, f.limit, 1, 1};
-          f.a = mid + 1;
-        } else {
-          f.wb = rightLen >= bal;
-          child = Frame{mid + 1, f.b, f.limit, 1, 1};
-          f.b = mid;
-        }
-        st[sp++] = f;
-        f = child;
-      }
-    }
-  }
-};
 
 // ------------------------------------------------------- hot block helpers
 // The per-pod reductions and the one-step rotation.  Only force-inlined
@@ -440,6 +197,7 @@ struct Wg {
 // same permutation: both paths restate pdqsort_func)
 template <uint32_t NT, int SEQ = SEQ_SORT>
 struct Blk {
+  static_assert(SEQ >= 12, "block pdqsort must hand ranges <= 12 (Go's insertion-sort cutoff) to SeqSort");
   static constexpr int FB = (int)NT;
   static constexpr int NWAVE = (int)NT / 64;
   uint16_t* sc;
@@ -715,7 +473,7 @@ struct Blk {
     sync();
   }
   __device__ void pdqsort(int n) {
-    SeqSort seq{sc, ord};
+    SeqSort seq{{sc, ord}};
     if (n <= SEQ) {
       if (tid == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
       sync();
@@ -789,156 +547,6 @@ struct Blk {
   }
 };
 
-// first m in [m0, n) with thr[m] >= x (thresholds ascending); n if none
-// Cursor advance over one resource's ascending thresholds: the first m >= m0
-// with thr[m] >= x.  A 4-wide window read in one LDS round trip covers the
-// common case; thr has 4 readable entries past every range.
-__device__ __forceinline__ uint32_t thr_window(const int64_t* thr, uint32_t n, uint32_t m0, int64_t x) {
-  uint32_t m = m0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) {
-    const int64_t vk = thr[m0 + k];  // unconditional: the padded LDS copy covers m0 + 3
-    m += (m0 + k < n && vk < x) ? 1u : 0u;
-  }
-  return m;
-}
-
-__device__ __forceinline__ uint32_t thr_search(const int64_t* thr, uint32_t n, uint32_t lo, int64_t x) {
-  uint32_t hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (thr[mid] < x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// choosePivot's hint for sort.Slice over sc[0, M), M > 12: the (up to) nine
-// sampled keys read by nine lanes in one LDS round trip, the median-of-three
-// comparisons on scalars (same swap count as SeqSort::choose_pivot)
-__device__ __forceinline__ int pivot_hint_wave(const uint16_t* sc, int l, uint32_t lane) {
-  const int i0 = l / 4 * 1, j0 = l / 4 * 2, k0 = l / 4 * 3;
-  const int idx[9] = {i0 - 1, i0, i0 + 1, j0 - 1, j0, j0 + 1, k0 - 1, k0, k0 + 1};
-  int mine = 0;
-#pragma unroll
-  for (int t = 0; t < 9; t++)
-    if ((int)lane == t) mine = idx[t];
-  const uint32_t kl = lane < 9 && (l >= 50 || lane % 3 == 1) ? sc[mine] : 0u;
-  uint32_t key[9];
-#pragma unroll
-  for (int t = 0; t < 9; t++) key[t] = __builtin_amdgcn_readlane(kl, t);
-  int swaps = 0;
-  auto med = [&](uint32_t kx, uint32_t ky, uint32_t kz) {
-    // order2(x,y); order2(y,z); order2(x,y); the middle key
-    if (ky < kx) { swaps++; const uint32_t u = kx; kx = ky; ky = u; }
-    if (kz < ky) { swaps++; const uint32_t u = ky; ky = kz; kz = u; }
-    if (ky < kx) { swaps++; const uint32_t u = kx; kx = ky; ky = u; }
-    return ky;
-  };
-  uint32_t ki = key[1], kj = key[4], kk = key[7];
-  if (l >= 50) {
-    ki = med(key[0], key[1], key[2]);
-    kj = med(key[3], key[4], key[5]);
-    kk = med(key[6], key[7], key[8]);
-  }
-  med(ki, kj, kk);
-  return swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
-}
-
-// first k in [lo, hi) with pred(k) for a monotone pred (false...true), hi if
-// none: a 64-ary search, one LDS round trip per level (two up to 4096)
-template <class Pred>
-__device__ __forceinline__ uint32_t wave_first(uint32_t lo, uint32_t hi, uint32_t lane, Pred pred) {
-  while (hi - lo > 64) {
-    const uint32_t step = (hi - lo + 63) / 64;
-    const uint32_t k = lo + lane * step + step - 1;  // last index of this lane's segment
-    const uint64_t b = __ballot(k >= hi || pred(k));
-    if (!b) return hi;
-    const uint32_t i = (uint32_t)__ffsll((long long)b) - 1;
-    lo = lo + i * step;
-    hi = lo + step < hi ? lo + step : hi;
-  }
-  const uint32_t k = lo + lane;
-  const uint64_t b = __ballot(k < hi && pred(k));
-  return b ? lo + (uint32_t)__ffsll((long long)b) - 1 : hi;
-}
-
-// phase timers (t_sort / t_scan / t_tmpl, Ctrl.dbg): s_memrealtime costs
-// hundreds of cycles on the pod loop's critical path, so only GS_FFD_PHASES
-// builds read the clock
-__device__ __forceinline__ uint64_t phase_clock() {
-#ifdef GS_FFD_PHASES
-  return wall_clock64();
-#else
-  return 0;
-#endif
-}
-
-// the kernel argument block, addressed in the constant (kernarg) space
-typedef const __attribute__((address_space(4))) DevProblem* KArg;
-
-// wave-uniform 64-bit value into SGPRs (readfirstlane is 32-bit)
-__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
-// Monotone 16-bit code of a non-negative quantity: exact below 1024, then a
-// 9-bit mantissa per binade (relative step <= 2^-9).  codes are consecutive
-// in value order, so floor/ceil differ by at most one.
-__device__ __forceinline__ uint32_t qcode_floor(int64_t v) {
-  if (v <= 0) return 0;
-  const uint64_t x = (uint64_t)v;
-  const uint32_t b = 64u - (uint32_t)__clzll((long long)x);
-  if (b <= 10) return (uint32_t)x;
-  const uint32_t s = b - 10;
-  return 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
-}
-__device__ __forceinline__ uint32_t qcode_ceil(int64_t v) {
-  if (v <= 0) return 0;
-  const uint64_t x = (uint64_t)v;
-  const uint32_t b = 64u - (uint32_t)__clzll((long long)x);
-  if (b <= 10) return (uint32_t)x;
-  const uint32_t s = b - 10;
-  const uint32_t c = 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
-  return c + ((x & ((1ull << s) - 1)) ? 1u : 0u);
-}
-
-// the value a code stands for: qcode_floor(v) <= v's code <= qcode_ceil(v)
-// and qcode_value(qcode_floor(v)) <= v <= qcode_value(qcode_ceil(v))
-__device__ __forceinline__ int64_t qcode_value(uint32_t c) {
-  if (c < 1024u) return (int64_t)c;
-  const uint32_t s = (c - 1024u) / 512u + 1u, m = (c - 1024u) % 512u + 512u;
-  return (int64_t)((uint64_t)m << s);
-}
-
-// LDS room of a NodeClaim: qcode_floor(thr[cursor] - tot) per resource (<= 4),
-// a lower bound of what a pod may add before any threshold cursor moves
-__device__ __forceinline__ uint64_t pack_room(const int64_t* thr, const uint32_t* thoff, const uint32_t* cur,
-                                              const int64_t* tot, uint32_t RQ) {
-  uint64_t s = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < 4; r++) {
-    if (r >= RQ) break;
-    const uint32_t o = thoff[r], n = thoff[r + 1] - o;
-    const int64_t room = cur[r] < n ? thr[o + cur[r]] - tot[r] : 0;
-    s |= (uint64_t)qcode_floor(room) << (16 * r);
-  }
-  return s;
-}
-
-// LDS slack of a NodeClaim: qcode_ceil(maxa - tot) per resource (<= 4)
-template <class DP>
-__device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa, const int64_t* tot) {
-  uint64_t s = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < 4; r++) {
-    if (r >= d.RQ) break;
-    s |= (uint64_t)qcode_ceil(maxa[r] - tot[r]) << (16 * r);
-  }
-  return s;
-}
 
 }  // namespace
 
@@ -1407,7 +1015,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           // sorted input: pdqsort_func / insertionSort leave it untouched
         } else if (M <= 12) {
           fp = FP_SMALL;
-        } else if (pivot_hint_wave(s_sc, (int)M, lane) == 1 && M >= 50) {
+        } else if (pivot_hint_wave(SplitAcc{s_sc, s_ord}, (int)M, lane) == 1 && M >= 50) {
           // partialInsertionSort fixes the single inversion: one
           // rotation; its far end by a 64-ary search over the sorted remainder
           // (INC: first k > q with count >= x; APPEND: first k < M-1 with
@@ -1438,7 +1046,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
         if (fp == FP_SMALL || fp == FP_GENERIC) __syncthreads();  // every wave has decided before the order changes
         if (fp == FP_SMALL) {
           if (tid == 0) {
-            SeqSort ss{s_sc, s_ord};
+            SeqSort ss{{s_sc, s_ord}};
             ss.insertion_sort(0, (int)M);
           }
         } else if ((fp == MOD_INC || fp == MOD_APPEND) && wg.rotate1((int)rlo, (int)rhi, fp == MOD_INC)) {

@@ -1,0 +1,1290 @@
+// ffd_wave.hip — K4 provisioning Solve as ONE wave (64 lanes, no barriers).
+//
+// The <U> Scheduler.Solve queue loop is sequential in pod order; its cost
+// per pod is a chain of dependent steps (pop, sort.Slice emulation, first-fit
+// scan of the in-flight NodeClaims, NodeClaim.Add).  A multi-wave workgroup
+// pays a workgroup barrier and an LDS round trip of shared loop state for
+// every step of that chain; one wave pays neither:
+//  * the loop state (queue head/length, epoch, claim count, pending sort
+//    modification) lives in scalar registers;
+//  * the sorted NodeClaim order is one packed u32 per position (count in the
+//    low 16 bits, claim id in the high 16): one LDS access reads or moves
+//    both, and the scan reads a position's claim id and count together;
+//  * every cross-lane LDS hand-off is ordered by the wave's in-order LDS
+//    queue (wsync() only stops the compiler from reordering);
+//  * the next pod's variant record and requests are prefetched into lanes
+//    during the current pod (first pass: records laid out in queue order);
+//  * a fast-accepted NodeClaim.Add (requests only) is LDS updates plus
+//    no-return atomic adds of the requests at L2: no round trip.
+// Results are bit-identical to ffd.hip's block kernel (same restatement of
+// Go's sort.Slice, same candidate order, same Add), which still serves the
+// consolidation simulations and Solves with many existing nodes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "devutil.hpp"
+#include "ffd_common.hpp"
+#include "layout.hpp"
+
+using namespace gsd;
+
+namespace {
+
+constexpr uint32_t VR_DW = sizeof(VarRec) / 4;
+static_assert(VR_DW == 32, "VarRec is one dword per lane of a half wave");
+static_assert(offsetof(VarRec, fk_begin) == 4 && offsetof(VarRec, fk_count) == 8 && offsetof(VarRec, ctb) == 12 &&
+                  offsetof(VarRec, itmask_off) == 16 && offsetof(VarRec, zfull_off) == 48 &&
+                  offsetof(VarRec, cfull_off) == 52 && offsetof(VarRec, zm) == 56 && offsetof(VarRec, cm) == 64 &&
+                  offsetof(VarRec, tol) == 72 && offsetof(VarRec, tolt) == 80 && offsetof(VarRec, t_own) == 88 &&
+                  offsetof(VarRec, t_sel) == 96 && offsetof(VarRec, zs) == 104 && offsetof(VarRec, zn) == 112 &&
+                  offsetof(VarRec, zflags) == 120 && offsetof(VarRec, vix) == 124,
+              "VarRec dword map used by ffdw_kernel");
+static_assert(offsetof(ClaimRec, maxa) == 128, "ClaimRec maxa after two 64-B lines");
+
+constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
+constexpr uint64_t SWAR_HI = 0x8000800080008000ull;  // top bit of each 16-bit code field
+enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
+#ifndef GS_WAVE_SEQ
+#define GS_WAVE_SEQ 32
+#endif
+
+// compiler barrier for LDS hand-offs between lanes of the one wave: the
+// hardware keeps a wave's LDS accesses in order, the compiler must too
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// readlane as an unsigned dword (the builtin returns int: widening it
+// directly would sign-extend a low dword with bit 31 set)
+__device__ __forceinline__ uint32_t rlane(uint32_t x, uint32_t i) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)i);
+}
+
+// GS_FFD_TL (diagnostic build): shader cycles per pod-loop segment into Ctrl.dbg
+#ifdef GS_FFD_TL
+#define TLW(k)                                         \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
+    tl[k] += t_ - tl_last;                             \
+    tl_last = t_;                                      \
+  } while (0)
+#else
+#define TLW(k) \
+  do {         \
+  } while (0)
+#endif
+
+__device__ __forceinline__ uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((long long)m) - 1u; }
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t x, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t y = shfl_xor_u64(x, m);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+// -------------------------------------------------------- wave-parallel sort
+// sort.Slice(newNodeClaims, len(Pods) asc) over the packed order: the block
+// restatement of pdqsort_func (ffd.hip Blk) with one wave, so every block
+// reduction is a ballot and every barrier an in-order LDS queue.  Ranges up
+// to SEQ elements run the sequential port on lane 0.
+template <int SEQ>
+struct WaveSort {
+  static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
+  uint32_t* so;
+  uint16_t* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
+  Frame* stk;
+  uint32_t lane, half;
+
+  __device__ __forceinline__ uint32_t key(int i) const { return so[i] & 0xFFFFu; }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    const uint32_t a = so[i];
+    so[i] = so[j];
+    so[j] = a;
+  }
+  template <class Pred>
+  __device__ uint32_t count(int lo, int hi, Pred pred) const {
+    uint32_t c = 0;
+    for (int base = lo; base < hi; base += 64) {
+      const int k = base + (int)lane;
+      c += (uint32_t)__popcll(__ballot(k < hi && pred(k)));
+    }
+    return c;
+  }
+  // positions k in [lo,hi) with pred(k), ascending or descending, to out[]
+  template <class Pred>
+  __device__ uint32_t compact(int lo, int hi, bool desc, uint16_t* out, Pred pred) const {
+    uint32_t total = 0;
+    const int n = hi - lo;
+    for (int base = 0; base < n; base += 64) {
+      const int idx = base + (int)lane;
+      const int k = desc ? hi - 1 - idx : lo + idx;
+      const bool in = idx < n && pred(k);
+      const uint64_t m = __ballot(in);
+      if (in) out[total + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)k;
+      total += (uint32_t)__popcll(m);
+    }
+    wsync();
+    return total;
+  }
+  // swap the k-th left-list position with the k-th right-list position
+  __device__ void swap_lists(uint32_t s) const {
+    for (uint32_t k = lane; k < s; k += 64) {
+      const int x = scr[k], y = scr[half + k];
+      const uint32_t a = so[x], b = so[y];
+      wsync();
+      so[x] = b;
+      so[y] = a;
+    }
+    wsync();
+  }
+  __device__ int partition(int a, int b, int pivot, bool* already) const {
+    if (lane == 0) swap(a, pivot);
+    wsync();
+    const uint32_t p = key(a);
+    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) < p; });
+    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
+    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
+    swap_lists(s);
+    if (lane == 0) swap(mid, a);
+    wsync();
+    *already = s == 0;
+    return mid;
+  }
+  __device__ int partition_equal(int a, int b, int pivot) const {
+    if (lane == 0) swap(a, pivot);
+    wsync();
+    const uint32_t p = key(a);
+    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) <= p; });
+    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
+    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) <= p; });
+    swap_lists(s);
+    return mid + 1;
+  }
+  // one rotation: left = the element at lo lands at hi, (lo, hi] shift left;
+  // otherwise the element at hi lands at lo, [lo, hi) shift right.  Passes of
+  // 8 values per lane read before they write, in the order that never
+  // overwrites a position a later pass still reads.
+  static constexpr int KR = 8;
+  __device__ void rotate(int lo, int hi, bool left) const {
+    if (hi <= lo) return;
+    const uint32_t x = so[left ? lo : hi];
+    wsync();
+    if (left) {
+      for (int base = lo; base < hi; base += 64 * KR) {
+        uint32_t v[KR];
+#pragma unroll
+        for (int i = 0; i < KR; i++) {
+          const int k = base + (int)lane + 64 * i;
+          v[i] = k < hi ? so[k + 1] : 0u;
+        }
+        wsync();
+#pragma unroll
+        for (int i = 0; i < KR; i++) {
+          const int k = base + (int)lane + 64 * i;
+          if (k < hi) so[k] = v[i];
+        }
+        wsync();
+      }
+      if (lane == 0) so[hi] = x;
+    } else {
+      for (int top = hi - 1; top >= lo; top -= 64 * KR) {
+        uint32_t v[KR];
+#pragma unroll
+        for (int i = 0; i < KR; i++) {
+          const int k = top - (int)lane - 64 * i;
+          v[i] = k >= lo ? so[k] : 0u;
+        }
+        wsync();
+#pragma unroll
+        for (int i = 0; i < KR; i++) {
+          const int k = top - (int)lane - 64 * i;
+          if (k >= lo) so[k + 1] = v[i];
+        }
+        wsync();
+      }
+      if (lane == 0) so[lo] = x;
+    }
+    wsync();
+  }
+  // first k in [from, b) with key(k) < key(k-1); b if none
+  __device__ int first_inversion(int from, int b) const {
+    for (int base = from; base < b; base += 64) {
+      const int k = base + (int)lane;
+      const uint64_t m = __ballot(k < b && key(k) < key(k - 1));
+      if (m) return base + (int)ffs64(m);
+    }
+    return b;
+  }
+  __device__ bool partial_insertion_sort(int a, int b) const {
+    int i = a + 1;
+    for (int j = 0; j < 5; j++) {
+      i = first_inversion(i, b);
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      if (lane == 0) swap(i, i - 1);
+      wsync();
+      if (i - a >= 2) {
+        // the smaller element (now at i-1) moves left past larger elements,
+        // down to absolute index 0 (Go's loop runs to j >= 1)
+        const uint32_t x = key(i - 1);
+        int q = -1;
+        for (int top = i - 2; top >= 0; top -= 64) {
+          const int k = top - (int)lane;
+          const uint64_t m = __ballot(k >= 0 && key(k) <= x);
+          if (m) {
+            q = top - (int)ffs64(m);  // lowest lane = highest position
+            break;
+          }
+        }
+        rotate(q + 1, i - 1, false);
+      }
+      if (b - i >= 2) {
+        const uint32_t y = key(i);
+        int q = b;
+        for (int base = i + 1; base < b; base += 64) {
+          const int k = base + (int)lane;
+          const uint64_t m = __ballot(k < b && key(k) >= y);
+          if (m) {
+            q = base + (int)ffs64(m);
+            break;
+          }
+        }
+        rotate(i, q - 1, true);
+      }
+    }
+    return false;
+  }
+  __device__ void reverse_range(int a, int b) const {
+    const int n = (b - a) / 2;
+    for (int k = (int)lane; k < n; k += 64) {
+      const uint32_t x = so[a + k], y = so[b - 1 - k];
+      wsync();
+      so[a + k] = y;
+      so[b - 1 - k] = x;
+    }
+    wsync();
+  }
+  __device__ void pdqsort(int n) const {
+    const SeqSortP seq{{so}};
+    if (n <= SEQ) {
+      if (lane == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
+      wsync();
+      return;
+    }
+    int sp = 0;
+    Frame f{0, n, bits_len((uint64_t)n), 1, 1};
+    for (;;) {
+      for (;;) {
+        const int length = f.b - f.a;
+        if (length <= SEQ) {
+          if (lane == 0) seq.pdq_frame(f);
+          wsync();
+          break;
+        }
+        if (f.limit == 0) {
+          if (lane == 0) seq.heap_sort(f.a, f.b);
+          wsync();
+          break;
+        }
+        if (!f.wb) {
+          if (lane == 0) seq.break_patterns(f.a, f.b);
+          wsync();
+          f.limit--;
+        }
+        int hint = 0;
+        int pivot = seq.choose_pivot_fast(f.a, f.b, &hint);  // every lane, same keys
+        pivot = __builtin_amdgcn_readfirstlane(pivot);
+        hint = __builtin_amdgcn_readfirstlane(hint);
+        if (hint == 2) {
+          reverse_range(f.a, f.b);
+          pivot = (f.b - 1) - (pivot - f.a);
+          hint = 1;
+        }
+        if (f.wb && f.wp && hint == 1) {
+          if (partial_insertion_sort(f.a, f.b)) break;
+        }
+        if (f.a > 0 && !(key(f.a - 1) < key(pivot))) {
+          f.a = partition_equal(f.a, f.b, pivot);
+          continue;
+        }
+        bool already;
+        const int mid = partition(f.a, f.b, pivot, &already);
+        f.wp = already;
+        const int leftLen = mid - f.a, rightLen = f.b - mid;
+        const int bal = length / 8;
+        Frame child;
+        if (leftLen < rightLen) {
+          f.wb = leftLen >= bal;
+          child = Frame{f.a, mid, f.limit, 1, 1};
+          f.a = mid + 1;
+        } else {
+          f.wb = rightLen >= bal;
+          child = Frame{mid + 1, f.b, f.limit, 1, 1};
+          f.b = mid;
+        }
+        if (lane == 0) stk[sp] = f;
+        wsync();
+        sp++;
+        f = child;
+      }
+      if (sp == 0) break;
+      sp--;
+      f.a = __builtin_amdgcn_readfirstlane(stk[sp].a);
+      f.b = __builtin_amdgcn_readfirstlane(stk[sp].b);
+      f.limit = __builtin_amdgcn_readfirstlane(stk[sp].limit);
+      f.wb = __builtin_amdgcn_readfirstlane(stk[sp].wb);
+      f.wp = __builtin_amdgcn_readfirstlane(stk[sp].wp);
+    }
+    wsync();
+  }
+};
+
+// <U> Requirements.Compatible over the variant's free-key entries
+__device__ __forceinline__ bool fk_ok_range(const DevProblem& d, uint32_t fb, uint32_t fc, const FK* cfk, bool strict) {
+  for (uint32_t k = 0; k < fc; k++) {
+    const FKEntry& e = d.fk_entries[fb + k];
+    if (!fk_compatible(cfk[e.slot], e.st, strict ? false : ((d.wk_slots >> e.slot) & 1))) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+// Grid-wide reset of the Solve's working state (queue, per-pod counters,
+// NodePool remaining limits, existing-node copies, hostname counts): the
+// single-wave kernel starts from it.
+extern "C" __global__ __launch_bounds__(256) void ffd_init_kernel(DevProblem d) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t i = i0; i < d.P; i += stride) {
+    d.queue[i] = d.queue0[i];
+    d.last_epoch[i] = 0;
+    d.last_len[i] = 0;
+    d.cur_var[i] = d.var_begin[i];
+  }
+  for (uint32_t i = i0; i < d.T * d.R; i += stride) d.t_rem[i] = d.tmpl[i / d.R].limits[i % d.R];
+  for (uint32_t i = i0; i < d.NN; i += stride) d.nodes[i] = d.nodes0[i];
+  for (uint32_t i = i0; i < d.NN * d.F; i += stride) d.n_fk[i] = d.n_fk0[i];
+  for (uint32_t i = i0; i < d.TGH * d.NN; i += stride) d.hn[i] = d.hn0[i];
+}
+
+template <uint32_t RR, bool TOPO>
+__global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
+  extern __shared__ uint64_t lds64[];
+  __shared__ Frame s_stk[64];
+  __shared__ uint64_t s_slot[SLOT_LDS_MAX];
+  __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
+  __shared__ uint32_t s_thoff[RMAX + 1];
+  __shared__ uint32_t s_exl[64];  // exact-check batch: position | claim << 16
+  constexpr uint32_t R = RR;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t MC = d.max_claims;
+  // dynamic LDS, per claim 23 B (the block kernel's layout, ffd.hip):
+  // slack u64 | room u64 | packed order u32 | sort scratch u16 | template u8
+  uint64_t* s_slk = lds64;
+  uint64_t* s_rm = s_slk + MC;
+  uint32_t* s_so = (uint32_t*)(s_rm + MC);
+  uint16_t* s_scr = (uint16_t*)(s_so + MC);
+  uint8_t* s_tmpl = (uint8_t*)(s_scr + MC);
+  const uint32_t thr_base = (23u * MC + 7u) & ~7u;
+  int64_t* s_thr = (int64_t*)((char*)lds64 + thr_base);
+  const uint32_t W = d.W, F = d.F, T = d.T, OW = d.OW, P = d.P;
+  const uint32_t nthr = d.thr_off[R];
+  const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
+  uint64_t* s_known = (uint64_t*)((char*)lds64 + tg_off);
+  int64_t* s_tmin = (int64_t*)(s_known + d.TG);
+  int32_t* s_zcnt = (int32_t*)(s_tmin + d.TG);
+  const int64_t* thr = s_thr;
+  const uint64_t* slot = s_slot;
+
+  for (uint32_t i = lane; i < nthr + 4; i += 64) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
+  for (uint32_t i = lane; i < d.Z * d.C * W; i += 64) s_slot[i] = d.slot_set[i];
+  if (lane <= R) s_thoff[lane] = d.thr_off[lane];
+  for (uint32_t t = lane; t < T; t += 64) {
+    s_tzm[t] = d.tmpl[t].zm;
+    s_tcm[t] = d.tmpl[t].cm;
+  }
+  if (TOPO) {
+    for (uint32_t i = lane; i < d.TG * ZVMAX; i += 64) s_zcnt[i] = d.tg_cnt0[i];
+    for (uint32_t g = lane; g < d.TG; g += 64) s_known[g] = d.tgroups[g].known0;
+  }
+  wsync();
+  const WaveSort<GS_WAVE_SEQ> ws{s_so, s_scr, s_stk, lane, MC / 2};
+  const PackedAcc acc{s_so};
+
+  // first-pass records (queue order): the next pod's variant record (lanes
+  // 0..31, one dword each) and requests (lanes 32.., two dwords each)
+  const uint32_t* qv_dw = (const uint32_t*)d.qvars;
+  const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
+  uint32_t nx_vr = 0, nx_rq = 0;
+  if (P) {
+    if (lane < VR_DW) nx_vr = qv_dw[lane];
+    if (lane >= 32 && lane < 32 + 2 * R) nx_rq = qr_dw[lane - 32];
+  }
+
+  // uniform loop state (scalar registers)
+  uint32_t qhead = 0, qlen = P, epoch = 1, M = 0, modkind = MOD_NONE, modpos = 0, nlog = 0, status = 0;
+  bool wrapped = false;
+  uint64_t pops = 0, n_generic = 0, n_fast = 0, n_cand = 0, n_full = 0, n_nev = 0, n_npre = 0, n_fa = 0;
+  const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
+
+#ifdef GS_FFD_TL
+  uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
+  uint64_t n_fsum = 0;
+#endif
+  for (;;) {
+    // ---------------------------------------------------------- Queue.Pop
+    TLW(7);  // previous pod's tail (continue paths)
+    if (status) break;
+    if (pops > max_pops) {
+      status = 2;
+      break;
+    }
+    if (qlen == 0) break;
+    uint32_t vrd, rqd, p, v;
+    if (!wrapped) {
+      // first pass: the pod at qhead is queue0[qhead] with its first
+      // variant and was never pushed (no staleness stop)
+      vrd = nx_vr;
+      rqd = nx_rq;
+      p = rlane(vrd, 0);
+      v = rlane(vrd, VR_DW - 1);
+    } else {
+      p = __builtin_amdgcn_readfirstlane(d.queue[qhead]);
+      const uint32_t le = __builtin_amdgcn_readfirstlane(d.last_epoch[p]);
+      const uint32_t ll = __builtin_amdgcn_readfirstlane(d.last_len[p]);
+      v = __builtin_amdgcn_readfirstlane(d.cur_var[p]);
+      if (le == epoch && ll == qlen) break;
+      vrd = lane < VR_DW ? ((const uint32_t*)(d.vars + v))[lane] : 0u;
+      rqd = lane >= 32 && lane < 32 + 2 * R ? ((const uint32_t*)(d.pod_req + (size_t)p * R))[lane - 32] : 0u;
+    }
+    if (qhead + 1 == P) wrapped = true;
+    qhead = qhead + 1 == P ? 0 : qhead + 1;
+    qlen--;
+    pops++;
+    if (!wrapped && qlen > 0) {
+      if (lane < VR_DW) nx_vr = qv_dw[(size_t)qhead * VR_DW + lane];
+      if (lane >= 32 && lane < 32 + 2 * R) nx_rq = qr_dw[(size_t)qhead * 2 * R + (lane - 32)];
+    }
+    const uint32_t gp = p;
+    auto VD = [&](uint32_t i) -> uint32_t { return rlane(vrd, i); };
+    auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
+    const uint32_t fk_begin = VD(1), fk_count = VD(2), vctb = VD(3);
+    const uint32_t zfull_off = VD(12), cfull_off = VD(13);
+    const uint64_t vzm = VD64(14), vcm = VD64(16), vtol = VD64(18), vtolt = VD64(20);
+    const uint64_t own = TOPO ? VD64(22) : 0, vtsel = TOPO ? VD64(24) : 0;
+    const uint64_t vzs = TOPO ? VD64(26) : 0, vzn = VD64(28);
+    const uint32_t vzflags = VD(30);
+    uint32_t itoff[KMAX_IT];
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX_IT; k++) itoff[k] = VD(4 + k);
+    int64_t rq[RR];
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++)
+      rq[r] = (int64_t)((uint64_t)rlane(rqd, 32 + 2 * r) | ((uint64_t)rlane(rqd, 33 + 2 * r) << 32));
+    int64_t rq_lane = 0;  // lane r < R: resource r's request
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++)
+      if (lane == r) rq_lane = rq[r];
+
+    TLW(0);  // pop + record
+    // <U> Topology.AddRequirements: each owned zone group's minimum domain
+    // count over the pod's strict zone domains (domainMinCount)
+    if (TOPO && own) {
+      if (((own & d.tg_zone) >> lane) & 1) {
+        const uint64_t cand = s_known[lane] & vzs;
+        int64_t mn = INT32_MAX;
+        int32_t n = 0;
+        for (uint64_t m = cand; m; m &= m - 1) {
+          n++;
+          const int64_t c = s_zcnt[lane * ZVMAX + ffs64(m)];
+          mn = c < mn ? c : mn;
+        }
+        if (d.tgroups[lane].mind && n < d.tgroups[lane].mind) mn = 0;
+        s_tmin[lane] = mn;
+      }
+      wsync();
+    }
+    const uint64_t tself = own & vtsel;
+
+    // ----------------- existing nodes in order: first ExistingNode.CanAdd wins
+    if (d.NN) {
+      uint32_t fn = INF;
+      for (uint32_t base = 0; base < d.NN; base += 64) {
+        const uint32_t n = base + lane;
+        bool feas = false;
+        if (n < d.NN) {
+          const NodeRec& nr = d.nodes[n];
+          const FK* nfk = d.n_fk + (size_t)n * F;
+          feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
+#pragma unroll
+          for (uint32_t k = 0; k < KMAX_IT; k++) {
+            const uint32_t off = itoff[k];
+            if (k >= d.K || !feas || off == NONE) continue;
+            const uint32_t vid = nr.vid[k];
+            feas = vid != NONE && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+          }
+          if (feas && zfull_off != NONE)
+            feas = nr.zvid != NONE && ((d.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+          if (feas && cfull_off != NONE)
+            feas = nr.cvid != NONE && ((d.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+          if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
+          if (TOPO && feas && own) {
+            for (uint64_t m = own & d.tg_zone; m && feas; m &= m - 1) {
+              const uint32_t g = ffs64(m), z = nr.zvid;
+              feas = z < (uint32_t)ZVMAX && ((s_known[g] >> z) & 1) &&
+                     (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= d.tgroups[g].skew;
+            }
+            for (uint64_t m = own & d.tg_host; m && feas; m &= m - 1) {
+              const uint32_t g = ffs64(m);
+              feas = (int64_t)d.hn[(size_t)d.tgroups[g].hslot * d.NN + n] + (int64_t)((tself >> g) & 1) <=
+                     d.tgroups[g].skew;
+            }
+          }
+        }
+        const uint64_t b = __ballot(feas);
+        n_nev += d.NN - base < 64 ? d.NN - base : 64;
+        if (b) {
+          fn = base + ffs64(b);
+          break;
+        }
+      }
+      n_npre += fn != INF ? fn + 1 : d.NN;
+      if (fn != INF) {
+        // ExistingNode.Add: requests and requirements
+        int64_t* areq = d.nodes[fn].req;
+        FK* afk = d.n_fk + (size_t)fn * F;
+        if (lane < R) areq[lane] += rq_lane;
+        if (lane < fk_count) {
+          const FKEntry& e = d.fk_entries[fk_begin + lane];
+          FK* nf = afk + e.slot;
+          const FK cur = *nf;
+          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                                         : e.st;
+        }
+        if (lane == 0) {
+          d.log[nlog] = LogRec{gp, v, fn | 0x80000000u, 0};
+          // <U> Topology.Record: the node's labels are single domains
+          for (uint64_t m = TOPO ? vtsel : 0; m; m &= m - 1) {
+            const uint32_t g = ffs64(m);
+            if ((d.tg_host >> g) & 1) {
+              d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
+            } else {
+              const uint32_t z = d.nodes0[fn].zvid;
+              if (z < (uint32_t)ZVMAX) {
+                s_zcnt[g * ZVMAX + z]++;
+                s_known[g] |= 1ull << z;
+              }
+            }
+          }
+        }
+        wsync();
+        nlog++;
+        continue;
+      }
+    }
+
+    TLW(1);  // topology minimum + existing nodes
+    // ------------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
+    if (M > 1) {
+      // at most one NodeClaim changed since the last sort: one pod added at
+      // modpos (INC) or one NodeClaim appended (APPEND)
+      bool inversion = false;
+      if (modkind == MOD_INC) inversion = modpos + 1 < M && acc.key(modpos + 1) < acc.key(modpos);
+      else if (modkind == MOD_APPEND) inversion = acc.key(M - 2) > acc.key(M - 1);
+      inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
+      if (inversion) {
+        if (M <= 12) {
+          if (lane == 0) SeqSortP{{s_so}}.insertion_sort(0, (int)M);
+          wsync();
+        } else if (M >= 50 && pivot_hint_wave(acc, (int)M, lane) == 1) {
+          // partialInsertionSort fixes the single inversion: one rotation
+          n_fast++;
+          if (modkind == MOD_INC) {
+            const uint32_t x = acc.key(modpos);
+            const uint32_t e = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
+            ws.rotate((int)modpos, (int)e - 1, true);
+          } else {
+            const uint32_t x = acc.key(M - 1);
+            const uint32_t lo = wave_first(0, M - 1, lane, [&](uint32_t k) { return acc.key(k) > x; });
+            ws.rotate((int)lo, (int)M - 1, false);
+          }
+        } else {
+          n_generic++;
+          ws.pdqsort((int)M);
+        }
+      }
+      modkind = MOD_NONE;
+    }
+
+    TLW(2);  // sort
+    // request codes for the LDS slack / room tests, packed 16 bits per
+    // resource (codes < 2^15, so a SWAR subtract compares all four at once)
+    uint64_t rqq_p = 0, rqc_p = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      if (r < d.RQ) {
+        rqq_p |= (uint64_t)qcode_floor(rq[r]) << (16 * r);
+        rqc_p |= (uint64_t)qcode_ceil(rq[r]) << (16 * r);
+      }
+    }
+#ifdef GS_NO_FAST
+    bool simple = false;
+#else
+    bool simple = !TOPO && (vctb & VF_SIMPLE);
+#endif
+#pragma unroll
+    for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
+
+    // --------------------------- in-flight NodeClaims, first that CanAdd wins
+    // Phase A walks the sorted positions in LDS, four 64-position chunks per
+    // step, with the necessary test (template tolerated, request code <=
+    // slack code per resource) and, for simple pods, the sufficient test
+    // (request code <= room code: CanAdd holds without reading the claim).
+    // It stops at the first fast accept, collecting every candidate before it
+    // that needs the exact check (at most 64 per batch).  Phase B runs the
+    // exact NodeClaim.CanAdd on the batch, one lane per candidate: the first
+    // feasible candidate wins, else the fast accept, else the scan resumes.
+    uint32_t f = INF;
+    bool ovf = false;  // the winner lane's u16 pod count overflowed
+    uint32_t scan_from = 0;
+    for (;;) {
+      uint32_t nex = 0, fa_pos = INF, fa_j = 0, resume = INF;
+      for (uint32_t base = scan_from; base < M && fa_pos == INF && resume == INF; base += 256) {
+        uint32_t je[4];
+        uint64_t sq[4], rmv[4];
+        uint32_t tt[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+          const uint32_t pos = base + 64 * k + lane;
+          je[k] = s_so[pos < M ? pos : M - 1] >> 16;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+          sq[k] = s_slk[je[k]];
+          rmv[k] = s_rm[je[k]];
+          tt[k] = s_tmpl[je[k]];
+        }
+        uint64_t fab[4], exb[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+          // bitwise (not short-circuit) predicates: no branches
+          const bool valid = base + 64 * k + lane < M;
+          const bool tol = (vtolt >> tt[k]) & 1;
+          const bool sok = (((sq[k] | SWAR_HI) - rqq_p) & SWAR_HI) == SWAR_HI;
+          const bool rok = (((rmv[k] | SWAR_HI) - rqc_p) & SWAR_HI) == SWAR_HI;
+          const bool lp = valid & tol & sok;
+          const bool fa = lp & simple & rok;
+          fab[k] = __ballot(fa);
+          exb[k] = __ballot(lp & !fa);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+          const uint32_t cb = base + 64 * k;
+          if (cb >= M) break;
+          const uint32_t mfl = fab[k] ? ffs64(fab[k]) : 64u;
+          const uint64_t ex = exb[k] & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));
+          const uint32_t cnt = (uint32_t)__popcll(ex);
+          if (nex + cnt > 64) {
+            resume = cb;  // batch full: check it, then rescan from this chunk
+            break;
+          }
+          n_cand += M - cb < 64 ? M - cb : 64;
+          if (ex) {
+            if ((ex >> lane) & 1)
+              s_exl[nex + (uint32_t)__popcll(ex & ((1ull << lane) - 1ull))] = ((cb + lane) & 0xFFFFu) | (je[k] << 16);
+            nex += cnt;
+          }
+          if (fab[k]) {
+            fa_pos = cb + mfl;
+            fa_j = rlane(je[k], mfl);
+            break;
+          }
+        }
+      }
+      wsync();
+      TLW(5);  // phase A: LDS prefilter
+      if (nex) {
+        // --- exact NodeClaim.CanAdd, lane i = i-th candidate (ascending
+        // positions): one 64-B header read, option words and the (variant,
+        // template) row, threshold cursors, offering grid
+        n_full += nex;
+        const uint32_t xe = lane < nex ? s_exl[lane] : 0u;
+        const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
+        const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
+      bool feas = false;
+      uint32_t tz = NONE;
+      uint64_t zm = 0, cm = 0, czf = 0;
+      uint32_t czfl = 0;
+      uint32_t mrow[RR];
+      int64_t tot[RR];
+      uint64_t nx[WREG] = {0, 0, 0, 0};
+      uint64_t G = 0, Gt = 0;
+      if (lane < nex) {
+        const ClaimRec* cr = d.c_rec + j;
+        uint32_t cur[RR];
+        {
+          const uint4* q = (const uint4*)cr;
+          const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+          const int64_t lo[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                 (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+          const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+          zm = ((uint64_t)h2.w << 32) | h2.z;
+          cm = ((uint64_t)h3.y << 32) | h3.x;
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            tot[r] = r < 4 ? lo[r] : cr->tot_hi[r - 4];
+            cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+          }
+        }
+        const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+        const uint64_t* opts = d.c_opts + (size_t)j * OW;
+        if (W <= WREG) {
+          const uint4* oq = (const uint4*)opts;
+          const uint4* rq4 = (const uint4*)row;
+          const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+          const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                 (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                 (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                 (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+          for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
+        }
+        bool pre = true;
+        if (fk_count) pre = fk_ok_range(d, fk_begin, fk_count, d.c_fk + (size_t)j * F, false);
+        if (TOPO && pre && own) {
+          // <U> Topology.AddRequirements on the NodeClaim: every owned zone
+          // group picks the minimum-count known domain within maxSkew among
+          // the NodeClaim's (claim AND pod) zone domains, ties by name; the
+          // picks must agree.  Hostname groups: this NodeClaim's count.
+          czf = cr->zfull;
+          czfl = cr->zflags;
+          const uint64_t D = czf & vzn;
+          for (uint64_t m = own & d.tg_zone; m && pre; m &= m - 1) {
+            const uint32_t g = ffs64(m);
+            const uint64_t cand = D & s_known[g];
+            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
+            uint32_t best = NONE;
+            int64_t bc = INT32_MAX;
+            for (uint32_t k = 0; k < d.NZV && cand; k++) {
+              const uint32_t z = d.zone_order[k];
+              if (!((cand >> z) & 1)) continue;
+              const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
+              if (c - mn <= skew && c < bc) {
+                best = z;
+                bc = c;
+              }
+            }
+            if (best == NONE || (tz != NONE && tz != best)) pre = false;
+            tz = best;
+          }
+          for (uint64_t m = own & d.tg_host; m && pre; m &= m - 1) {
+            const uint32_t g = ffs64(m);
+            pre = (int64_t)d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j] + (int64_t)((tself >> g) & 1) <=
+                  d.tgroups[g].skew;
+          }
+          if (pre && tz != NONE) {
+            const uint32_t zc = d.zone_cat[tz];
+            zm = zc < 64 ? (zm & (1ull << zc)) : 0;
+          }
+        }
+        if (pre) {
+          G = grid_of(zm & vzm, cm & vcm, d.Z, d.C);
+          Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, d.Z, d.C);
+          uint32_t mm[RR];
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+            mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
+          }
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+            if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
+            mrow[r] = o + r + mm[r];
+          }
+          uint64_t accw = 0;
+          if (W <= WREG) {
+            // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
+            // whose cursor moves narrows the options further
+#pragma unroll
+            for (uint32_t r = 0; r < RR; r++) {
+              if (mm[r] != cur[r]) {
+                const uint4* tq = (const uint4*)(d.thr_set + (size_t)mrow[r] * OW);
+                const uint4 t0 = tq[0], t1 = tq[1];
+                nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
+              }
+            }
+            if (G != Gt) {
+              uint64_t off[WREG] = {};
+              for (uint64_t gm = G; gm; gm &= gm - 1) {
+                const uint32_t g = ffs64(gm);
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++)
+                  if (w < W) off[w] |= slot[g * W + w];
+              }
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++) nx[w] &= off[w];
+            }
+#pragma unroll
+            for (uint32_t w = 0; w < WREG; w++) accw |= nx[w];
+          } else {
+            // 4 words per round trip, stop at the first batch with a survivor
+            for (uint32_t w0 = 0; w0 < W && !accw; w0 += 4) {
+              const uint4* oq = (const uint4*)(opts + w0);
+              const uint4* rq4 = (const uint4*)(row + w0);
+              const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+              uint64_t x[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                               (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                               (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                               (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                if (mm[r] == cur[r]) continue;
+                const uint4* tq = (const uint4*)(d.thr_set + (size_t)mrow[r] * OW + w0);
+                const uint4 t0 = tq[0], t1 = tq[1];
+                x[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                x[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                x[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                x[3] &= ((uint64_t)t1.w << 32) | t1.z;
+              }
+#pragma unroll
+              for (uint32_t w = 0; w < 4; w++) {
+                if (w0 + w >= W) x[w] = 0;
+                if (x[w] && G != Gt) {
+                  uint64_t off = 0;
+                  for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w0 + w];
+                  x[w] &= off;
+                }
+                accw |= x[w];
+              }
+            }
+          }
+          feas = accw != 0;
+        }
+      }
+        const uint64_t fm = __ballot(feas);
+        TLW(6);  // phase B: exact checks
+        if (fm) {
+          const uint32_t wl = ffs64(fm);
+          f = rlane(xpos, wl);
+        if (lane == wl) {
+          // NodeClaim.Add by the winning lane: options, requests, requirements
+          ClaimRec* cr = d.c_rec + j;
+          uint64_t* opts = d.c_opts + (size_t)j * OW;
+          if (W <= WREG) {
+  #pragma unroll
+            for (uint32_t w = 0; w < WREG; w++)
+              if (w < W) opts[w] = nx[w];  // already narrowed to the grid
+          } else {
+            const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+            for (uint32_t w = 0; w < W; w++) {
+              uint64_t x = opts[w] & row[w];
+  #pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x &= d.thr_set[(size_t)mrow[r] * OW + w];
+              if (G != Gt) {
+                uint64_t off = 0;
+                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                x &= off;
+              }
+              opts[w] = x;
+            }
+          }
+          int64_t nt[RR], ma[RR];
+          uint32_t cu[RR];
+  #pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            nt[r] = tot[r] + rq[r];
+            ma[r] = cr->maxa[r];
+            cu[r] = mrow[r] - s_thoff[r] - r;
+            cr->tot(r) = nt[r];
+            cr->thr(r) = (uint16_t)cu[r];
+          }
+          s_slk[j] = pack_slack(d, ma, nt);  // exact re-quantization: no drift
+          s_rm[j] = pack_room(thr, s_thoff, cu, nt, d.RQ);
+          cr->zm = zm & vzm;  // zm carries the topology narrowing
+          cr->cm &= vcm;
+          cr->ctb &= vctb;
+          if (TOPO) {
+            // zone requirement after Add (+ the topology domain), then
+            // <U> Topology.Record for every group selecting the pod
+            if (!own) {
+              czf = cr->zfull;
+              czfl = cr->zflags;
+            }
+            const uint64_t zf = czf & vzn & (tz != NONE ? 1ull << tz : ~0ull);
+            const uint32_t zl = tz != NONE ? 0u : (czfl & vzflags);
+            cr->zfull = zf;
+            cr->zflags = zl;
+            for (uint64_t m = vtsel; m; m &= m - 1) {
+              const uint32_t g = ffs64(m);
+              if ((d.tg_host >> g) & 1) {
+                d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j]++;
+              } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
+                const uint32_t z = ffs64(zf);
+                s_zcnt[g * ZVMAX + z]++;
+                s_known[g] |= 1ull << z;
+              }
+            }
+          }
+          FK* cf = d.c_fk + (size_t)j * F;
+          for (uint32_t k = 0; k < fk_count; k++) {
+            const FKEntry& e = d.fk_entries[fk_begin + k];
+            const FK cur = cf[e.slot];
+            cf[e.slot] = (cur.flags & FK_PRESENT)
+                             ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                             : e.st;
+          }
+          const uint32_t e = s_so[f];
+          if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+          s_so[f] = e + 1u;
+          d.log[nlog] = LogRec{gp, v, j, 0};
+        }
+          break;
+        }
+      }
+      if (fa_pos != INF) {
+        // --- fast accept (simple pod): NodeClaim.Add changes the requests
+        // only; options, cursors and requirements stay.  The totals take
+        // no-return atomic adds at L2 (no round trip on the pod's path; a
+        // later exact check of this claim reads them after the adds, same
+        // wave, same addresses); LDS room and slack shrink by the request
+        // (still a lower / upper bound).
+        f = fa_pos;
+        const uint32_t j = fa_j;
+        if (lane < R && lane < 4 && rq_lane != 0)
+          atomicAdd((unsigned long long*)&d.c_rec[j].tot_lo[lane], (unsigned long long)rq_lane);
+        if (lane == 0) {
+          const uint64_t rm = s_rm[j], sl = s_slk[j];
+          uint64_t rm2 = 0, sl2 = 0;
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) {
+            if (r >= d.RQ) break;
+            rm2 |= (uint64_t)qcode_floor(qcode_value((uint32_t)(rm >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
+            sl2 |= (uint64_t)qcode_ceil(qcode_value((uint32_t)(sl >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
+          }
+          s_rm[j] = rm2;
+          s_slk[j] = sl2;
+          const uint32_t e = s_so[f];
+          if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+          s_so[f] = e + 1u;
+          d.log[nlog] = LogRec{gp, v, j, 0};
+        }
+        n_fa++;
+        break;
+      }
+      if (resume == INF) break;
+      scan_from = resume;
+    }
+    if (__ballot(ovf)) status = 3;
+    TLW(3);  // scan + Add
+#ifdef GS_FFD_TL
+    n_fsum += f != INF ? f : 0;
+#endif
+    if (f != INF) {
+      wsync();
+      modkind = MOD_INC;
+      modpos = f;
+      nlog++;
+      continue;
+    }
+
+    // ------------------------------- new NodeClaim from templates, in order
+    bool opened = false;
+    for (uint32_t t = 0; t < T; t++) {
+      const TmplRec& tr = d.tmpl[t];
+      const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+      // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
+      // a new hostname domain has count 0, always within maxSkew >= 1):
+      // the picked zone narrows the K1 row to that zone's offerings
+      uint32_t ttz = NONE, tzc = NONE;
+      if (TOPO && own) {
+        const uint64_t D = tr.zfull & vzn;
+        bool ok = true;
+        for (uint64_t m = own & d.tg_zone; m && ok; m &= m - 1) {
+          const uint32_t g = ffs64(m);
+          const uint64_t cand = D & s_known[g];
+          const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
+          uint32_t best = NONE;
+          int64_t bc = INT32_MAX;
+          for (uint32_t k = 0; k < d.NZV && cand; k++) {
+            const uint32_t z = d.zone_order[k];
+            if (!((cand >> z) & 1)) continue;
+            const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
+            if (c - mn <= skew && c < bc) {
+              best = z;
+              bc = c;
+            }
+          }
+          if (best == NONE || (ttz != NONE && ttz != best)) ok = false;
+          ttz = best;
+        }
+        if (ok && ttz != NONE) {
+          tzc = d.zone_cat[ttz];
+          ok = tzc < 64;
+        }
+        ttz = __builtin_amdgcn_readfirstlane(ttz);
+        tzc = __builtin_amdgcn_readfirstlane(tzc);
+        if (!__builtin_amdgcn_readfirstlane(ok ? 1u : 0u)) continue;
+      }
+      const uint64_t tcm = tr.cm & vcm;
+      auto rowx = [&](uint32_t w) -> uint64_t {
+        uint64_t x = row[w];
+        if (ttz != NONE) {
+          uint64_t off = 0;
+          for (uint32_t c = 0; c < d.C; c++)
+            if ((tcm >> c) & 1) off |= slot[(tzc * d.C + c) * W + w];
+          x &= off;
+        }
+        return x;
+      };
+      bool anyl = false;
+      if (d.fk_ok[(size_t)v * T + t])
+        for (uint32_t w = lane; w < W; w += 64) anyl = anyl || rowx(w) != 0;
+      if (!__ballot(anyl)) continue;
+      if (tr.has_limits) {
+        // <U> filterByRemainingResources on the template's options
+        bool hit = false;
+        for (uint32_t i = lane; i < d.N; i += 64) {
+          if (!((rowx(i >> 6) >> (i & 63)) & 1)) continue;
+          bool ok = true;
+          for (uint32_t r = 0; r < R; r++)
+            if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
+          hit = hit || ok;
+        }
+        if (!__ballot(hit)) continue;
+      }
+      if (M >= MC) {
+        status = 1;
+        break;
+      }
+      const uint32_t j = M;
+      ClaimRec* cr = d.c_rec + j;
+      // threshold cursors of the fresh claim: lane r < R
+      int64_t tot_l = 0;
+      uint32_t c0_l = 0;
+      if (lane < R) {
+        tot_l = tr.daemon[lane] + rq_lane;
+        const uint32_t o = s_thoff[lane], n = s_thoff[lane + 1] - o;
+        c0_l = thr_search(thr + o, n, 0, tot_l);
+      }
+      uint32_t c0[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) c0[r] = (uint32_t)__shfl((int)c0_l, (int)r);
+      // option words (lane w holds word w, and w + 64)
+      uint64_t xw[2] = {0, 0};
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t w = lane + 64 * h;
+        if (w >= W) continue;
+        uint64_t x = rowx(w);
+        // establish opts ⊆ thr_set[cursor] for the candidate scan
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + c0[r]) * OW + w];
+        if (tr.has_limits) {
+          uint64_t y = 0;
+          for (uint64_t m = x; m; m &= m - 1) {
+            const uint32_t b = ffs64(m);
+            const uint32_t i = w * 64 + b;
+            bool ok = true;
+            for (uint32_t r = 0; r < R; r++)
+              if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
+            if (ok) y |= 1ull << b;
+          }
+          x = y;
+        }
+        d.c_opts[(size_t)j * OW + w] = x;
+        xw[h] = x;
+      }
+      if (lane < RR) {
+        cr->tot(lane) = tot_l;
+        cr->thr(lane) = (uint16_t)c0_l;
+      }
+      // max allocatable over the new claim's options (the slack bound), and
+      // (limits) the max capacity for subtractMax: lane = instance type
+      uint64_t mxa[RR], mxc[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) mxa[r] = mxc[r] = 0;
+      for (uint32_t w = 0; w < W; w++) {
+        const uint64_t word = shfl_u64(xw[w >> 6], w & 63);
+        if (!((word >> lane) & 1)) continue;
+        const uint32_t i = w * 64 + lane;
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) {
+          const uint64_t a = (uint64_t)d.it_alloc[(size_t)r * d.N + i];
+          mxa[r] = a > mxa[r] ? a : mxa[r];
+          if (tr.has_limits && ((tr.limit_rmask >> r) & 1)) {
+            const uint64_t c = (uint64_t)(d.it_cap[(size_t)r * d.N + i] + (1ll << 62));
+            mxc[r] = c > mxc[r] ? c : mxc[r];
+          }
+        }
+      }
+      int64_t ma[RR], nt[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) {
+        ma[r] = (int64_t)wave_max_u64(mxa[r]);
+        if (tr.has_limits) mxc[r] = wave_max_u64(mxc[r]);
+        nt[r] = tr.daemon[r] + rq[r];
+      }
+      if (lane == 0) {
+        cr->tmpl = t;
+        cr->count = 1;
+        cr->zm = tr.zm & vzm & (ttz != NONE ? 1ull << tzc : ~0ull);
+        cr->cm = tr.cm & vcm;
+        cr->ctb = tr.ctb & vctb;
+        cr->zfull = tr.zfull & vzn & (ttz != NONE ? 1ull << ttz : ~0ull);
+        cr->zflags = ttz != NONE ? 0u : (tr.zflags & vzflags);
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) cr->maxa[r] = ma[r];
+        if (TOPO) {
+          // <U> Topology.Register(hostname placeholder) + Record
+          for (uint32_t h = 0; h < d.TGH; h++) d.hc[(size_t)h * d.max_claims + j] = 0;
+          for (uint64_t m = vtsel; m; m &= m - 1) {
+            const uint32_t g = ffs64(m);
+            if ((d.tg_host >> g) & 1) {
+              d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j]++;
+            } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
+              const uint32_t z = ffs64(cr->zfull);
+              s_zcnt[g * ZVMAX + z]++;
+              s_known[g] |= 1ull << z;
+            }
+          }
+        }
+        FK* cf = d.c_fk + (size_t)j * F;
+        for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
+        for (uint32_t k = 0; k < fk_count; k++) {
+          const FKEntry& e = d.fk_entries[fk_begin + k];
+          const FK cur = cf[e.slot];
+          cf[e.slot] = (cur.flags & FK_PRESENT)
+                           ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                           : e.st;
+        }
+        s_so[M] = 1u | (M << 16);
+        s_tmpl[M] = (uint8_t)t;
+        s_slk[j] = pack_slack(d, ma, nt);
+        s_rm[j] = pack_room(thr, s_thoff, c0, nt, d.RQ);
+        d.log[nlog] = LogRec{gp, v, j, 0};
+        if (tr.has_limits) {
+          // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+          for (uint32_t r = 0; r < R; r++)
+            if (((tr.limit_rmask >> r) & 1) && mxc[r] != 0) d.t_rem[(size_t)t * R + r] -= (int64_t)(mxc[r] - (1ull << 62));
+        }
+      }
+      wsync();
+      M++;
+      modkind = MOD_APPEND;
+      nlog++;
+      opened = true;
+      break;
+    }
+    TLW(4);  // new NodeClaim
+    if (status) break;
+    if (opened) continue;
+
+    // -------------------------------------- failed: Relax, then Queue.Push
+    {
+      const uint32_t vb = __builtin_amdgcn_readfirstlane(d.var_begin[gp]);
+      const uint32_t vc = __builtin_amdgcn_readfirstlane(d.var_count[gp]);
+      const bool relaxed = v + 1 < vb + vc;
+      uint32_t tail = qhead + qlen;
+      if (tail >= P) tail -= P;
+      qlen++;
+      if (lane == 0) {
+        if (relaxed) d.cur_var[p] = v + 1;
+        d.queue[tail] = p;
+        if (!relaxed) {
+          d.last_epoch[p] = epoch;
+          d.last_len[p] = qlen;
+        }
+      }
+      if (relaxed) epoch++;
+    }
+  }
+  wsync();
+  for (uint32_t i = lane; i < M; i += 64) {
+    const uint32_t e = s_so[i];
+    d.c_sorted[i] = e >> 16;
+    d.c_rec[e >> 16].count = e & 0xFFFFu;
+  }
+  if (lane == 0) {
+    Ctrl c = {};
+    c.status = status;
+    c.n_claims = M;
+    c.n_log = nlog;
+    c.qhead = qhead;
+    c.qlen = qlen;
+    c.epoch = epoch;
+    c.pops = pops;
+    c.generic_sorts = n_generic;
+    c.fast_sorts = n_fast;
+    c.cand_evals = n_cand;
+    c.cand_full = n_full;
+    c.node_evals = n_nev;
+    c.node_prefix = n_npre;
+    c.dbg[15] = n_fa;
+#ifdef GS_FFD_TL
+    for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
+    c.dbg[8] = n_fsum;
+#endif
+    *d.ctrl = c;
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+                                      uint32_t TG);
+static uint32_t g_ffdw_dyn_max = 0;
+
+template <uint32_t RR, bool TOPO>
+static hipError_t ffdw_attr(uint32_t lds_total) {
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffdw_kernel<RR, TOPO>);
+  if (e != hipSuccess) return e;
+  const uint32_t dyn = lds_total > a.sharedSizeBytes ? lds_total - (uint32_t)a.sharedSizeBytes : 0;
+  if (!g_ffdw_dyn_max || dyn < g_ffdw_dyn_max) g_ffdw_dyn_max = dyn;
+  return hipFuncSetAttribute((const void*)ffdw_kernel<RR, TOPO>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+}
+
+extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total) {
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {ffdw_attr<1, false>(lds_total), ffdw_attr<2, false>(lds_total), ffdw_attr<3, false>(lds_total),
+                       ffdw_attr<4, false>(lds_total), ffdw_attr<5, false>(lds_total), ffdw_attr<6, false>(lds_total),
+                       ffdw_attr<7, false>(lds_total), ffdw_attr<8, false>(lds_total), ffdw_attr<1, true>(lds_total),
+                       ffdw_attr<2, true>(lds_total), ffdw_attr<3, true>(lds_total), ffdw_attr<4, true>(lds_total),
+                       ffdw_attr<5, true>(lds_total), ffdw_attr<6, true>(lds_total), ffdw_attr<7, true>(lds_total),
+                       ffdw_attr<8, true>(lds_total)})
+    if (x != hipSuccess) e = x;
+  return e;
+}
+
+extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
+
+// the single-wave provisioning Solve: grid-wide state reset, then one wave
+extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, 0, 0, d->TG);
+  if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
+  if (d->n_sims) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
+  switch (d->R * 2 + (d->TG ? 1 : 0)) {
+#define GSK_CASE(n)                                                                                      \
+  case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(64), lds, s, *d); break;      \
+  case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(64), lds, s, *d); break;
+    GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
+#undef GSK_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

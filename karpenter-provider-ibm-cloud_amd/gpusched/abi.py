@@ -134,6 +134,9 @@ class GsFeasResult(C.Structure):
     ]
 
 
+GS_CFG_BLOCK_SOLVE = 1  # gs_config.flags: run the Solve on the block kernel
+
+
 class GsConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_claims", _U32), ("flags", _U32)]
 

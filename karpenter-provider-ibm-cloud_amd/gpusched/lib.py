@@ -10,7 +10,9 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgpusched.so")
+# GPUSCHED_LIB selects an in-tree diagnostic build of the same library
+# (csrc/Makefile targets tl / diag / phases write libgpusched_<variant>.so)
+LIB_PATH = os.path.join(HERE, os.environ.get("GPUSCHED_LIB", "libgpusched.so"))
 
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
@@ -129,10 +131,10 @@ class Solver:
     """One gs_ctx on one device (karpenter-core drives one provisioning
     Solve and one consolidation simulation at a time per context)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, flags=0):
         self.L = load()
         self.ctx = C.c_void_p()
-        cfg = abi.GsConfig(device, 0, 0)
+        cfg = abi.GsConfig(device, 0, flags)
         st = self.L.gs_create(C.byref(cfg), C.byref(self.ctx))
         if st != abi.GS_OK:
             raise GpuSchedError(st, "gs_create failed (no gfx950 device?)")

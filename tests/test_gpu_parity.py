@@ -13,10 +13,12 @@ from oracle import pyoracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def solver():
+@pytest.fixture(scope="module", params=["wave", "block"])
+def solver(request):
+    """both provisioning Solve kernels: the single-wave one (default) and the
+    block kernel (GS_CFG_BLOCK_SOLVE), bit-identical by construction"""
     from gpusched.lib import Solver
-    s = Solver(0)
+    s = Solver(0, abi.GS_CFG_BLOCK_SOLVE if request.param == "block" else 0)
     yield s
     s.close()
 

@@ -100,10 +100,10 @@ def test_oracle_and_encoder_accept_random_topology(seed):
 
 
 # ------------------------------------------------------------------ GPU parity
-@pytest.fixture(scope="module")
-def solver():
+@pytest.fixture(scope="module", params=["wave", "block"])
+def solver(request):
     from gpusched.lib import Solver
-    s = Solver(0)
+    s = Solver(0, abi.GS_CFG_BLOCK_SOLVE if request.param == "block" else 0)
     yield s
     s.close()
 

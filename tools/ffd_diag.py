@@ -13,7 +13,7 @@ from gpusched.lib import Solver  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 p = synth.make_cm(n_pods=int(args[0]) if args else 100000)
-s = Solver(0)
+s = Solver(0, 1 if "--block" in sys.argv else 0)
 s.prepare(p)
 s.run()
 out = (C.c_uint64 * 16)()
@@ -22,7 +22,13 @@ s.L.gs_debug_ctrl(s.ctx, out, 16)
 d, res = s.fetch()
 base = {"ffd_ms": res.t_ffd_ms, "pops": res.pops, "claims": len(d['claims']), "cand_evals": res.cand_evals,
         "cand_full": res.cand_full}
-if "--tl" in sys.argv:
+if "--tl" in sys.argv and "--block" not in sys.argv:
+    names = ["pop_record", "nodes", "sort", "scan_add", "new_claim", "scanA_lds", "scanB_exact", "tail"]
+    base["cycles_per_pop"] = {n: round(out[i] / max(res.pops, 1), 1) for i, n in enumerate(names) if n != "-"}
+    base["cycles_per_pop_total"] = round(sum(out[i] for i in range(8)) / max(res.pops, 1), 1)
+    base["mean_winner_pos"] = round(out[8] / max(res.pops, 1), 1)
+    base["fast_accepts"] = out[15]
+elif "--tl" in sys.argv:
     names = ["to_top", "publish", "pop", "stage_nodes", "sort_decide", "rotate", "chunk_lds", "reduce2", "exact",
              "winner_end", "new_claim"]
     base["cycles_per_pop"] = {n: round(out[i] / max(res.pops, 1), 1) for i, n in enumerate(names)}
