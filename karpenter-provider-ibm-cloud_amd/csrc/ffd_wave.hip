@@ -42,6 +42,13 @@ static_assert(offsetof(VarRec, fk_begin) == 4 && offsetof(VarRec, fk_count) == 8
 static_assert(offsetof(ClaimRec, maxa) == 128, "ClaimRec maxa after two 64-B lines");
 
 constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
+// solver <-> memory-agent wave channels (LDS)
+constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the solver
+constexpr uint32_t RING_DW = 48; // VarRec (32 dwords) + requests (<= 16 dwords)
+constexpr uint32_t WQ = 32;      // global-memory write requests in flight
+constexpr uint32_t WQ_DW = 16;
+enum : uint32_t { WQ_LOG = 1, WQ_FA = 2, WQ_STOP = 3 };
+constexpr uint32_t SPIN_MAX = 1u << 26;  // bounded waits: a stuck partner ends the kernel, not the GPU
 constexpr uint64_t SWAR_HI = 0x8000800080008000ull;  // top bit of each 16-bit code field
 enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 #ifndef GS_WAVE_SEQ
@@ -75,6 +82,30 @@ __device__ __forceinline__ uint32_t rlane(uint32_t x, uint32_t i) {
   } while (0)
 #endif
 
+// channel words are polled: volatile LDS accesses.  The pointer is cast to
+// the LDS address space explicitly (a volatile access through a generic
+// pointer compiles to a flat, system-coherent load that also waits on every
+// outstanding global memory operation).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t vld(const uint32_t* p) { return *(const volatile lds_u32*)(const lds_u32*)p; }
+__device__ __forceinline__ void vst(uint32_t* p, uint32_t x) { *(volatile lds_u32*)(lds_u32*)p = x; }
+
+// The Solve loop keeps only its own state in scalar registers; its cold
+// paths re-read the kernel arguments through the kernarg pointer (scalar
+// loads from the constant cache) and the pod's variant fields from the
+// record lane (readlane) where they use them, instead of holding ~100
+// scalar values across the loop (which spills them into VGPR lanes).
+__device__ __forceinline__ KArg karg() {
+  KArg p = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// an opaque copy: readlanes of it are not merged with earlier ones
+__device__ __forceinline__ uint32_t fresh(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((long long)m) - 1u; }
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t x, uint32_t src) {
@@ -86,6 +117,21 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
     const uint64_t y = shfl_xor_u64(x, m);
     x = y > x ? y : x;
   }
+  return x;
+}
+
+// ------------------------------------------------ 16-bit code fields (SWAR)
+// a request / slack / room is four 15-bit codes in one u64 (layout.hpp
+// qcode); SWAR_HI keeps the borrow of each field inside the field
+__device__ __forceinline__ bool swar_ge(uint64_t a, uint64_t b) {  // every field a >= b
+  return (((a | SWAR_HI) - b) & SWAR_HI) == SWAR_HI;
+}
+__device__ __forceinline__ uint64_t swar_max(uint64_t a, uint64_t b) {  // field-wise max
+  const uint64_t m = ((((a | SWAR_HI) - b) & SWAR_HI) >> 15) * 0xFFFFull;
+  return (a & m) | (b & ~m);
+}
+__device__ __forceinline__ uint64_t wave_swar_max(uint64_t x) {
+  for (int m = 32; m >= 1; m >>= 1) x = swar_max(x, shfl_xor_u64(x, m));
   return x;
 }
 
@@ -169,44 +215,27 @@ struct WaveSort {
   }
   // one rotation: left = the element at lo lands at hi, (lo, hi] shift left;
   // otherwise the element at hi lands at lo, [lo, hi) shift right.  Passes of
-  // 8 values per lane read before they write, in the order that never
-  // overwrites a position a later pass still reads.
-  static constexpr int KR = 8;
+  // 64 positions read before they write, in the order that never overwrites
+  // a position a later pass still reads.
   __device__ void rotate(int lo, int hi, bool left) const {
     if (hi <= lo) return;
     const uint32_t x = so[left ? lo : hi];
     wsync();
     if (left) {
-      for (int base = lo; base < hi; base += 64 * KR) {
-        uint32_t v[KR];
-#pragma unroll
-        for (int i = 0; i < KR; i++) {
-          const int k = base + (int)lane + 64 * i;
-          v[i] = k < hi ? so[k + 1] : 0u;
-        }
+      for (int base = lo; base < hi; base += 64) {
+        const int k = base + (int)lane;
+        const uint32_t v = k < hi ? so[k + 1] : 0u;
         wsync();
-#pragma unroll
-        for (int i = 0; i < KR; i++) {
-          const int k = base + (int)lane + 64 * i;
-          if (k < hi) so[k] = v[i];
-        }
+        if (k < hi) so[k] = v;
         wsync();
       }
       if (lane == 0) so[hi] = x;
     } else {
-      for (int top = hi - 1; top >= lo; top -= 64 * KR) {
-        uint32_t v[KR];
-#pragma unroll
-        for (int i = 0; i < KR; i++) {
-          const int k = top - (int)lane - 64 * i;
-          v[i] = k >= lo ? so[k] : 0u;
-        }
+      for (int top = hi - 1; top >= lo; top -= 64) {
+        const int k = top - (int)lane;
+        const uint32_t v = k >= lo ? so[k] : 0u;
         wsync();
-#pragma unroll
-        for (int i = 0; i < KR; i++) {
-          const int k = top - (int)lane - 64 * i;
-          if (k >= lo) so[k + 1] = v[i];
-        }
+        if (k >= lo) so[k + 1] = v;
         wsync();
       }
       if (lane == 0) so[lo] = x;
@@ -376,15 +405,21 @@ extern "C" __global__ __launch_bounds__(256) void ffd_init_kernel(DevProblem d) 
 }
 
 template <uint32_t RR, bool TOPO>
-__global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
+__global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
   __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
   __shared__ uint32_t s_thoff[RMAX + 1];
   __shared__ uint32_t s_exl[64];  // exact-check batch: position | claim << 16
+  __shared__ int64_t s_hint_rq[4];  // requests of the pod that set the infeasible-prefix hint
+  // channels between the solver (wave 0) and the memory agent (wave 1)
+  __shared__ uint32_t s_ring[RING][RING_DW];  // first-pass pod records
+  __shared__ uint32_t s_ring_seq[RING];       // queue position + 1 held by each slot
+  __shared__ uint32_t s_wq[WQ][WQ_DW];        // write requests
+  __shared__ uint32_t s_ctl[4];               // [0] first-pass pops, [1] requests posted, [2] requests completed
   constexpr uint32_t R = RR;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t MC = d.max_claims;
   // dynamic LDS, per claim 23 B (the block kernel's layout, ffd.hip):
   // slack u64 | room u64 | packed order u32 | sort scratch u16 | template u8
@@ -404,40 +439,151 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
   const int64_t* thr = s_thr;
   const uint64_t* slot = s_slot;
 
-  for (uint32_t i = lane; i < nthr + 4; i += 64) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
-  for (uint32_t i = lane; i < d.Z * d.C * W; i += 64) s_slot[i] = d.slot_set[i];
-  if (lane <= R) s_thoff[lane] = d.thr_off[lane];
-  for (uint32_t t = lane; t < T; t += 64) {
+  for (uint32_t i = tid; i < nthr + 4; i += 128) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
+  for (uint32_t i = tid; i < d.Z * d.C * W; i += 128) s_slot[i] = d.slot_set[i];
+  if (tid <= R) s_thoff[tid] = d.thr_off[tid];
+  for (uint32_t t = tid; t < T; t += 128) {
     s_tzm[t] = d.tmpl[t].zm;
     s_tcm[t] = d.tmpl[t].cm;
   }
   if (TOPO) {
-    for (uint32_t i = lane; i < d.TG * ZVMAX; i += 64) s_zcnt[i] = d.tg_cnt0[i];
-    for (uint32_t g = lane; g < d.TG; g += 64) s_known[g] = d.tgroups[g].known0;
+    for (uint32_t i = tid; i < d.TG * ZVMAX; i += 128) s_zcnt[i] = d.tg_cnt0[i];
+    for (uint32_t g = tid; g < d.TG; g += 128) s_known[g] = d.tgroups[g].known0;
   }
-  wsync();
+  if (tid < RING) s_ring_seq[tid] = 0;
+  if (tid < 4) s_ctl[tid] = 0;
+  __syncthreads();  // the only workgroup barrier: the waves split here
+
+  if (wave == 1) {
+    // ================================================== memory agent wave
+    // (1) stages the next first-pass pod records (queue order) into the LDS
+    //     ring ahead of the solver; (2) performs the solver's global writes
+    //     (add log, fast-accept request totals) and reports their completion.
+    //     The solver wave thus issues no global memory operation on its
+    //     common path, and never waits on one it did not need.
+    const uint32_t* qv_dw = (const uint32_t*)d.qvars;
+    const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
+    uint32_t k_fill = 0, head = 0, idle = 0;
+    for (;;) {
+      bool busy = false, stop = false;
+      const uint32_t tail = __builtin_amdgcn_readfirstlane(vld(&s_ctl[1]));
+      while (head != tail) {
+        const uint32_t x = lane < WQ_DW ? vld(&s_wq[head % WQ][lane]) : 0u;
+        const uint32_t type = rlane(x, 0), idx = rlane(x, 1), tgt = rlane(x, 4);
+        const uint32_t rlo = (uint32_t)__shfl((int)x, (int)(5 + 2 * (lane & 3))),
+                       rhi = (uint32_t)__shfl((int)x, (int)(6 + 2 * (lane & 3)));
+        if (type == WQ_STOP) {
+          stop = true;
+        } else {
+          if (lane == 0) d.log[idx] = LogRec{rlane(x, 2), rlane(x, 3), tgt, 0};
+          const uint64_t a = (uint64_t)rlo | ((uint64_t)rhi << 32);
+          if (type == WQ_FA && lane < R && lane < 4 && a)
+            atomicAdd((unsigned long long*)&d.c_rec[tgt].tot_lo[lane], (unsigned long long)a);
+        }
+        head++;
+        busy = true;
+      }
+      if (busy) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the writes are done
+        wsync();
+        if (lane == 0) vst(&s_ctl[2], head);
+      }
+      if (stop) break;
+      const uint32_t sq = __builtin_amdgcn_readfirstlane(vld(&s_ctl[0]));
+      const uint32_t lim = P < sq + RING ? P : sq + RING;
+      if (k_fill < lim) {
+        constexpr uint32_t KB = 8;
+        const uint32_t n = lim - k_fill < KB ? lim - k_fill : KB;
+        uint32_t val[KB];
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++) {
+          const size_t k = k_fill + i;
+          val[i] = 0;
+          if (i < n) {
+            if (lane < VR_DW) val[i] = qv_dw[k * VR_DW + lane];
+            else if (lane < 32 + 2 * R) val[i] = qr_dw[k * 2 * R + (lane - 32)];
+          }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++)
+          if (i < n && lane < RING_DW) s_ring[(k_fill + i) % RING][lane] = val[i];
+        wsync();
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++)
+          if (i < n && lane == 0) vst(&s_ring_seq[(k_fill + i) % RING], k_fill + i + 1);
+        k_fill += n;
+        busy = true;
+      }
+      if (busy) {
+        idle = 0;
+      } else {
+#ifdef GS_AGENT_SLEEP
+        __builtin_amdgcn_s_sleep(GS_AGENT_SLEEP);
+#else
+        __builtin_amdgcn_s_sleep(1);
+#endif
+        if (++idle > SPIN_MAX) break;
+      }
+    }
+    return;
+  }
+
+  // ======================================================== solver wave
   const WaveSort<GS_WAVE_SEQ> ws{s_so, s_scr, s_stk, lane, MC / 2};
   const PackedAcc acc{s_so};
-
-  // first-pass records (queue order): the next pod's variant record (lanes
-  // 0..31, one dword each) and requests (lanes 32.., two dwords each)
-  const uint32_t* qv_dw = (const uint32_t*)d.qvars;
-  const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
-  uint32_t nx_vr = 0, nx_rq = 0;
-  if (P) {
-    if (lane < VR_DW) nx_vr = qv_dw[lane];
-    if (lane >= 32 && lane < 32 + 2 * R) nx_rq = qr_dw[lane - 32];
-  }
+  uint32_t wq_tail = 0;  // write requests posted
+  // Infeasible-prefix hint: sorted positions [0, hint) hold NodeClaims that
+  // cannot take a pod with requests >= s_hint_rq (resources 0..3) that
+  // tolerates no template outside hint_tolt.  NodeClaims only fill up
+  // (requests grow, options shrink), so the prefix stays infeasible; every
+  // reorder of the sorted order moves the bound exactly (or drops it).
+  // Pods come sorted by cpu, then memory, descending: runs of equal
+  // requests skip the prefix their predecessors already ruled out.
+  uint32_t hint = 0;
+  bool hint_ok = false;
+  uint64_t hint_tolt = 0;
+  bool chan_err = false;  // a channel wait exceeded SPIN_MAX
+  // post one write request (uniform control flow: every lane takes part)
+  auto post = [&](uint32_t type, uint32_t idx, uint32_t pod, uint32_t var, uint32_t tgt, uint32_t rqd_) {
+    for (uint32_t spin = 0; wq_tail - __builtin_amdgcn_readfirstlane(vld(&s_ctl[2])) >= WQ; spin++) {
+      __builtin_amdgcn_s_sleep(1);
+      if (spin > SPIN_MAX) {
+        chan_err = true;
+        break;
+      }
+    }
+    const uint32_t rqx = (uint32_t)__shfl((int)rqd_, (int)(32 + (lane - 5) % 8));
+    uint32_t x = lane == 0 ? type : lane == 1 ? idx : lane == 2 ? pod : lane == 3 ? var : lane == 4 ? tgt : 0u;
+    if (type == WQ_FA && lane >= 5 && lane < 13) x = rqx;
+    if (lane < WQ_DW) s_wq[wq_tail % WQ][lane] = x;
+    wsync();
+    if (lane == 0) vst(&s_ctl[1], wq_tail + 1);
+    wq_tail++;
+  };
+  // wait until every posted write has completed (before reading claim state)
+  auto drain = [&]() {
+    for (uint32_t spin = 0; __builtin_amdgcn_readfirstlane(vld(&s_ctl[2])) != wq_tail; spin++) {
+      __builtin_amdgcn_s_sleep(1);
+      if (spin > SPIN_MAX) {
+        chan_err = true;
+        break;
+      }
+    }
+  };
 
   // uniform loop state (scalar registers)
   uint32_t qhead = 0, qlen = P, epoch = 1, M = 0, modkind = MOD_NONE, modpos = 0, nlog = 0, status = 0;
   bool wrapped = false;
-  uint64_t pops = 0, n_generic = 0, n_fast = 0, n_cand = 0, n_full = 0, n_nev = 0, n_npre = 0, n_fa = 0;
+  uint64_t pops = 0;
+  // instrumentation counters, lane k = counter k (no scalar registers)
+  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA };
+  uint64_t ctr = 0;
+#define CTR(k, x) (ctr += lane == (k) ? (uint64_t)(x) : 0ull)
   const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
 
 #ifdef GS_FFD_TL
   uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
-  uint64_t n_fsum = 0;
+  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0;
 #endif
   for (;;) {
     // ---------------------------------------------------------- Queue.Pop
@@ -451,9 +597,25 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
     uint32_t vrd, rqd, p, v;
     if (!wrapped) {
       // first pass: the pod at qhead is queue0[qhead] with its first
-      // variant and was never pushed (no staleness stop)
-      vrd = nx_vr;
-      rqd = nx_rq;
+      // variant and was never pushed (no staleness stop); the agent staged
+      // its record in ring slot qhead % RING
+      const uint32_t rs = qhead % RING;
+      for (uint32_t spin = 0; __builtin_amdgcn_readfirstlane(vld(&s_ring_seq[rs])) != qhead + 1; spin++) {
+        __builtin_amdgcn_s_sleep(0);
+        if (spin > SPIN_MAX) {
+          chan_err = true;
+          break;
+        }
+      }
+      if (chan_err) {
+        status = 2;
+        break;
+      }
+      const uint32_t x = lane < RING_DW ? vld(&s_ring[rs][lane]) : 0u;
+      wsync();
+      if (lane == 0) vst(&s_ctl[0], qhead + 1);  // the slot may be refilled
+      vrd = x;
+      rqd = x;
       p = rlane(vrd, 0);
       v = rlane(vrd, VR_DW - 1);
     } else {
@@ -469,22 +631,12 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     pops++;
-    if (!wrapped && qlen > 0) {
-      if (lane < VR_DW) nx_vr = qv_dw[(size_t)qhead * VR_DW + lane];
-      if (lane >= 32 && lane < 32 + 2 * R) nx_rq = qr_dw[(size_t)qhead * 2 * R + (lane - 32)];
-    }
     const uint32_t gp = p;
     auto VD = [&](uint32_t i) -> uint32_t { return rlane(vrd, i); };
     auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
-    const uint32_t fk_begin = VD(1), fk_count = VD(2), vctb = VD(3);
-    const uint32_t zfull_off = VD(12), cfull_off = VD(13);
-    const uint64_t vzm = VD64(14), vcm = VD64(16), vtol = VD64(18), vtolt = VD64(20);
+    const uint32_t vctb = VD(3);
+    const uint64_t vtolt = VD64(20);
     const uint64_t own = TOPO ? VD64(22) : 0, vtsel = TOPO ? VD64(24) : 0;
-    const uint64_t vzs = TOPO ? VD64(26) : 0, vzn = VD64(28);
-    const uint32_t vzflags = VD(30);
-    uint32_t itoff[KMAX_IT];
-#pragma unroll
-    for (uint32_t k = 0; k < KMAX_IT; k++) itoff[k] = VD(4 + k);
     int64_t rq[RR];
 #pragma unroll
     for (uint32_t r = 0; r < RR; r++)
@@ -498,7 +650,9 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
     // <U> Topology.AddRequirements: each owned zone group's minimum domain
     // count over the pod's strict zone domains (domainMinCount)
     if (TOPO && own) {
-      if (((own & d.tg_zone) >> lane) & 1) {
+      const auto& KD = *karg();
+      const uint64_t vzs = rlane(vrd, 26) | ((uint64_t)rlane(vrd, 27) << 32);
+      if (((own & KD.tg_zone) >> lane) & 1) {
         const uint64_t cand = s_known[lane] & vzs;
         int64_t mn = INT32_MAX;
         int32_t n = 0;
@@ -507,7 +661,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
           const int64_t c = s_zcnt[lane * ZVMAX + ffs64(m)];
           mn = c < mn ? c : mn;
         }
-        if (d.tgroups[lane].mind && n < d.tgroups[lane].mind) mn = 0;
+        if (KD.tgroups[lane].mind && n < KD.tgroups[lane].mind) mn = 0;
         s_tmin[lane] = mn;
       }
       wsync();
@@ -516,70 +670,75 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 
     // ----------------- existing nodes in order: first ExistingNode.CanAdd wins
     if (d.NN) {
+      const auto& KD = *karg();
+      const uint32_t vx = fresh(vrd);
+      auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+      auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+      const uint32_t fk_begin = VX(1), fk_count = VX(2), zfull_off = VX(12), cfull_off = VX(13);
+      const uint64_t vtol = VX64(18);
       uint32_t fn = INF;
-      for (uint32_t base = 0; base < d.NN; base += 64) {
+      for (uint32_t base = 0; base < KD.NN; base += 64) {
         const uint32_t n = base + lane;
         bool feas = false;
-        if (n < d.NN) {
-          const NodeRec& nr = d.nodes[n];
-          const FK* nfk = d.n_fk + (size_t)n * F;
+        if (n < KD.NN) {
+          const NodeRec& nr = KD.nodes[n];
+          const FK* nfk = KD.n_fk + (size_t)n * F;
           feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
 #pragma unroll
           for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
 #pragma unroll
           for (uint32_t k = 0; k < KMAX_IT; k++) {
-            const uint32_t off = itoff[k];
-            if (k >= d.K || !feas || off == NONE) continue;
+            const uint32_t off = VX(4 + k);
+            if (k >= KD.K || !feas || off == NONE) continue;
             const uint32_t vid = nr.vid[k];
-            feas = vid != NONE && ((d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+            feas = vid != NONE && ((KD.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
           }
           if (feas && zfull_off != NONE)
-            feas = nr.zvid != NONE && ((d.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+            feas = nr.zvid != NONE && ((KD.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
           if (feas && cfull_off != NONE)
-            feas = nr.cvid != NONE && ((d.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+            feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
           if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
           if (TOPO && feas && own) {
-            for (uint64_t m = own & d.tg_zone; m && feas; m &= m - 1) {
+            for (uint64_t m = own & KD.tg_zone; m && feas; m &= m - 1) {
               const uint32_t g = ffs64(m), z = nr.zvid;
               feas = z < (uint32_t)ZVMAX && ((s_known[g] >> z) & 1) &&
-                     (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= d.tgroups[g].skew;
+                     (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= KD.tgroups[g].skew;
             }
-            for (uint64_t m = own & d.tg_host; m && feas; m &= m - 1) {
+            for (uint64_t m = own & KD.tg_host; m && feas; m &= m - 1) {
               const uint32_t g = ffs64(m);
-              feas = (int64_t)d.hn[(size_t)d.tgroups[g].hslot * d.NN + n] + (int64_t)((tself >> g) & 1) <=
-                     d.tgroups[g].skew;
+              feas = (int64_t)KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + n] + (int64_t)((tself >> g) & 1) <=
+                     KD.tgroups[g].skew;
             }
           }
         }
         const uint64_t b = __ballot(feas);
-        n_nev += d.NN - base < 64 ? d.NN - base : 64;
+        CTR(C_NEV, KD.NN - base < 64 ? KD.NN - base : 64);
         if (b) {
           fn = base + ffs64(b);
           break;
         }
       }
-      n_npre += fn != INF ? fn + 1 : d.NN;
+      CTR(C_NPRE, fn != INF ? fn + 1 : KD.NN);
       if (fn != INF) {
         // ExistingNode.Add: requests and requirements
-        int64_t* areq = d.nodes[fn].req;
-        FK* afk = d.n_fk + (size_t)fn * F;
+        int64_t* areq = KD.nodes[fn].req;
+        FK* afk = KD.n_fk + (size_t)fn * F;
         if (lane < R) areq[lane] += rq_lane;
         if (lane < fk_count) {
-          const FKEntry& e = d.fk_entries[fk_begin + lane];
+          const FKEntry& e = KD.fk_entries[fk_begin + lane];
           FK* nf = afk + e.slot;
           const FK cur = *nf;
-          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
                                          : e.st;
         }
         if (lane == 0) {
-          d.log[nlog] = LogRec{gp, v, fn | 0x80000000u, 0};
           // <U> Topology.Record: the node's labels are single domains
           for (uint64_t m = TOPO ? vtsel : 0; m; m &= m - 1) {
             const uint32_t g = ffs64(m);
-            if ((d.tg_host >> g) & 1) {
-              d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
+            if ((KD.tg_host >> g) & 1) {
+              KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + fn]++;
             } else {
-              const uint32_t z = d.nodes0[fn].zvid;
+              const uint32_t z = KD.nodes0[fn].zvid;
               if (z < (uint32_t)ZVMAX) {
                 s_zcnt[g * ZVMAX + z]++;
                 s_known[g] |= 1ull << z;
@@ -588,6 +747,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
           }
         }
         wsync();
+        post(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0);
         nlog++;
         continue;
       }
@@ -606,21 +766,26 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         if (M <= 12) {
           if (lane == 0) SeqSortP{{s_so}}.insertion_sort(0, (int)M);
           wsync();
+          hint_ok = false;
         } else if (M >= 50 && pivot_hint_wave(acc, (int)M, lane) == 1) {
           // partialInsertionSort fixes the single inversion: one rotation
-          n_fast++;
+          CTR(C_FAST, 1);
           if (modkind == MOD_INC) {
             const uint32_t x = acc.key(modpos);
             const uint32_t e = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
             ws.rotate((int)modpos, (int)e - 1, true);
+            // (modpos, e-1] shift left, the changed claim lands at e-1
+            if (modpos < hint && e - 1 >= hint) hint--;
           } else {
             const uint32_t x = acc.key(M - 1);
             const uint32_t lo = wave_first(0, M - 1, lane, [&](uint32_t k) { return acc.key(k) > x; });
             ws.rotate((int)lo, (int)M - 1, false);
+            if (lo < hint) hint = lo;  // the new claim lands at lo
           }
         } else {
-          n_generic++;
+          CTR(C_GEN, 1);
           ws.pdqsort((int)M);
+          hint_ok = false;
         }
       }
       modkind = MOD_NONE;
@@ -644,6 +809,9 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 #endif
 #pragma unroll
     for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
+#ifdef GS_FFD_TL
+    n_nonsimple += simple ? 0u : 1u;
+#endif
 
     // --------------------------- in-flight NodeClaims, first that CanAdd wins
     // Phase A walks the sorted positions in LDS, four 64-position chunks per
@@ -656,68 +824,59 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
     // feasible candidate wins, else the fast accept, else the scan resumes.
     uint32_t f = INF;
     bool ovf = false;  // the winner lane's u16 pod count overflowed
-    uint32_t scan_from = 0;
+    uint32_t lo_bound = 0;
+    if (hint_ok && (vtolt & ~hint_tolt) == 0) {
+      const bool ge = lane >= 4 || lane >= R || rq_lane >= s_hint_rq[lane];
+      if (__ballot(!ge) == 0) lo_bound = hint;
+    }
+    uint32_t scan_from = lo_bound & ~63u;
     for (;;) {
       uint32_t nex = 0, fa_pos = INF, fa_j = 0, resume = INF;
-      for (uint32_t base = scan_from; base < M && fa_pos == INF && resume == INF; base += 256) {
-        uint32_t je[4];
-        uint64_t sq[4], rmv[4];
-        uint32_t tt[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-          const uint32_t pos = base + 64 * k + lane;
-          je[k] = s_so[pos < M ? pos : M - 1] >> 16;
+      for (uint32_t cb = scan_from; cb < M; cb += 64) {
+        const uint32_t pos = cb + lane;
+        const uint32_t je = s_so[pos < M ? pos : M - 1] >> 16;
+        const uint64_t sq = s_slk[je], rmv = s_rm[je];
+        const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
+        // bitwise (not short-circuit) predicates: no branches
+        const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
+        const bool fa = lp & simple & swar_ge(rmv, rqc_p);
+        const uint64_t fab = __ballot(fa), exb = __ballot(lp & !fa);
+        const uint32_t mfl = fab ? ffs64(fab) : 64u;
+        const uint64_t ex = exb & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));
+        const uint32_t cnt = (uint32_t)__popcll(ex);
+        if (nex + cnt > 64) {
+          resume = cb;  // batch full: check it, then rescan from this chunk
+          break;
         }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-          sq[k] = s_slk[je[k]];
-          rmv[k] = s_rm[je[k]];
-          tt[k] = s_tmpl[je[k]];
+        CTR(C_CAND, M - cb < 64 ? M - cb : 64);
+        if (ex) {
+          if ((ex >> lane) & 1) s_exl[nex + (uint32_t)__popcll(ex & ((1ull << lane) - 1ull))] = (pos & 0xFFFFu) | (je << 16);
+          nex += cnt;
         }
-        uint64_t fab[4], exb[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-          // bitwise (not short-circuit) predicates: no branches
-          const bool valid = base + 64 * k + lane < M;
-          const bool tol = (vtolt >> tt[k]) & 1;
-          const bool sok = (((sq[k] | SWAR_HI) - rqq_p) & SWAR_HI) == SWAR_HI;
-          const bool rok = (((rmv[k] | SWAR_HI) - rqc_p) & SWAR_HI) == SWAR_HI;
-          const bool lp = valid & tol & sok;
-          const bool fa = lp & simple & rok;
-          fab[k] = __ballot(fa);
-          exb[k] = __ballot(lp & !fa);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-          const uint32_t cb = base + 64 * k;
-          if (cb >= M) break;
-          const uint32_t mfl = fab[k] ? ffs64(fab[k]) : 64u;
-          const uint64_t ex = exb[k] & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));
-          const uint32_t cnt = (uint32_t)__popcll(ex);
-          if (nex + cnt > 64) {
-            resume = cb;  // batch full: check it, then rescan from this chunk
-            break;
-          }
-          n_cand += M - cb < 64 ? M - cb : 64;
-          if (ex) {
-            if ((ex >> lane) & 1)
-              s_exl[nex + (uint32_t)__popcll(ex & ((1ull << lane) - 1ull))] = ((cb + lane) & 0xFFFFu) | (je[k] << 16);
-            nex += cnt;
-          }
-          if (fab[k]) {
-            fa_pos = cb + mfl;
-            fa_j = rlane(je[k], mfl);
-            break;
-          }
+        if (fab) {
+          fa_pos = cb + mfl;
+          fa_j = rlane(je, mfl);
+          break;
         }
       }
       wsync();
       TLW(5);  // phase A: LDS prefilter
       if (nex) {
+        drain();  // the agent's request totals must be in the claim records
+        const auto& KD = *karg();
+        const uint32_t vx = fresh(vrd);
+        auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+        auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+        const uint32_t fk_begin = VX(1), fk_count = VX(2), vzflags = VX(30);
+        const uint64_t vzm = VX64(14), vcm = VX64(16), vzn = VX64(28);
         // --- exact NodeClaim.CanAdd, lane i = i-th candidate (ascending
         // positions): one 64-B header read, option words and the (variant,
         // template) row, threshold cursors, offering grid
-        n_full += nex;
+        CTR(C_FULL, nex);
+#ifdef GS_FFD_TL
+        n_xns += simple ? 0u : nex;
+        n_xb++;
+#endif
         const uint32_t xe = lane < nex ? s_exl[lane] : 0u;
         const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
         const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
@@ -730,7 +889,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
       uint64_t nx[WREG] = {0, 0, 0, 0};
       uint64_t G = 0, Gt = 0;
       if (lane < nex) {
-        const ClaimRec* cr = d.c_rec + j;
+        const ClaimRec* cr = KD.c_rec + j;
         uint32_t cur[RR];
         {
           const uint4* q = (const uint4*)cr;
@@ -746,8 +905,8 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
           }
         }
-        const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
-        const uint64_t* opts = d.c_opts + (size_t)j * OW;
+        const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
+        const uint64_t* opts = KD.c_opts + (size_t)j * OW;
         if (W <= WREG) {
           const uint4* oq = (const uint4*)opts;
           const uint4* rq4 = (const uint4*)row;
@@ -760,7 +919,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
           for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
         }
         bool pre = true;
-        if (fk_count) pre = fk_ok_range(d, fk_begin, fk_count, d.c_fk + (size_t)j * F, false);
+        if (fk_count) pre = fk_ok_range(d, fk_begin, fk_count, KD.c_fk + (size_t)j * F, false);
         if (TOPO && pre && own) {
           // <U> Topology.AddRequirements on the NodeClaim: every owned zone
           // group picks the minimum-count known domain within maxSkew among
@@ -769,14 +928,14 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
           czf = cr->zfull;
           czfl = cr->zflags;
           const uint64_t D = czf & vzn;
-          for (uint64_t m = own & d.tg_zone; m && pre; m &= m - 1) {
+          for (uint64_t m = own & KD.tg_zone; m && pre; m &= m - 1) {
             const uint32_t g = ffs64(m);
             const uint64_t cand = D & s_known[g];
-            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
+            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = KD.tgroups[g].skew;
             uint32_t best = NONE;
             int64_t bc = INT32_MAX;
-            for (uint32_t k = 0; k < d.NZV && cand; k++) {
-              const uint32_t z = d.zone_order[k];
+            for (uint32_t k = 0; k < KD.NZV && cand; k++) {
+              const uint32_t z = KD.zone_order[k];
               if (!((cand >> z) & 1)) continue;
               const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
               if (c - mn <= skew && c < bc) {
@@ -787,19 +946,19 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             if (best == NONE || (tz != NONE && tz != best)) pre = false;
             tz = best;
           }
-          for (uint64_t m = own & d.tg_host; m && pre; m &= m - 1) {
+          for (uint64_t m = own & KD.tg_host; m && pre; m &= m - 1) {
             const uint32_t g = ffs64(m);
-            pre = (int64_t)d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j] + (int64_t)((tself >> g) & 1) <=
-                  d.tgroups[g].skew;
+            pre = (int64_t)KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j] + (int64_t)((tself >> g) & 1) <=
+                  KD.tgroups[g].skew;
           }
           if (pre && tz != NONE) {
-            const uint32_t zc = d.zone_cat[tz];
+            const uint32_t zc = KD.zone_cat[tz];
             zm = zc < 64 ? (zm & (1ull << zc)) : 0;
           }
         }
         if (pre) {
-          G = grid_of(zm & vzm, cm & vcm, d.Z, d.C);
-          Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, d.Z, d.C);
+          G = grid_of(zm & vzm, cm & vcm, KD.Z, KD.C);
+          Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, KD.Z, KD.C);
           uint32_t mm[RR];
 #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
@@ -819,7 +978,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
             for (uint32_t r = 0; r < RR; r++) {
               if (mm[r] != cur[r]) {
-                const uint4* tq = (const uint4*)(d.thr_set + (size_t)mrow[r] * OW);
+                const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW);
                 const uint4 t0 = tq[0], t1 = tq[1];
                 nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
                 nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
@@ -853,7 +1012,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
               for (uint32_t r = 0; r < RR; r++) {
                 if (mm[r] == cur[r]) continue;
-                const uint4* tq = (const uint4*)(d.thr_set + (size_t)mrow[r] * OW + w0);
+                const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW + w0);
                 const uint4 t0 = tq[0], t1 = tq[1];
                 x[0] &= ((uint64_t)t0.y << 32) | t0.x;
                 x[1] &= ((uint64_t)t0.w << 32) | t0.z;
@@ -880,20 +1039,23 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         if (fm) {
           const uint32_t wl = ffs64(fm);
           f = rlane(xpos, wl);
+#ifdef GS_FFD_TL
+          n_xwin++;
+#endif
         if (lane == wl) {
           // NodeClaim.Add by the winning lane: options, requests, requirements
-          ClaimRec* cr = d.c_rec + j;
-          uint64_t* opts = d.c_opts + (size_t)j * OW;
+          ClaimRec* cr = KD.c_rec + j;
+          uint64_t* opts = KD.c_opts + (size_t)j * OW;
           if (W <= WREG) {
   #pragma unroll
             for (uint32_t w = 0; w < WREG; w++)
               if (w < W) opts[w] = nx[w];  // already narrowed to the grid
           } else {
-            const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+            const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
             for (uint32_t w = 0; w < W; w++) {
               uint64_t x = opts[w] & row[w];
   #pragma unroll
-              for (uint32_t r = 0; r < RR; r++) x &= d.thr_set[(size_t)mrow[r] * OW + w];
+              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
               if (G != Gt) {
                 uint64_t off = 0;
                 for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
@@ -913,7 +1075,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             cr->thr(r) = (uint16_t)cu[r];
           }
           s_slk[j] = pack_slack(d, ma, nt);  // exact re-quantization: no drift
-          s_rm[j] = pack_room(thr, s_thoff, cu, nt, d.RQ);
+          s_rm[j] = pack_room(thr, s_thoff, cu, nt, KD.RQ);
           cr->zm = zm & vzm;  // zm carries the topology narrowing
           cr->cm &= vcm;
           cr->ctb &= vctb;
@@ -930,8 +1092,8 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             cr->zflags = zl;
             for (uint64_t m = vtsel; m; m &= m - 1) {
               const uint32_t g = ffs64(m);
-              if ((d.tg_host >> g) & 1) {
-                d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j]++;
+              if ((KD.tg_host >> g) & 1) {
+                KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
               } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
                 const uint32_t z = ffs64(zf);
                 s_zcnt[g * ZVMAX + z]++;
@@ -939,50 +1101,60 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
               }
             }
           }
-          FK* cf = d.c_fk + (size_t)j * F;
+          FK* cf = KD.c_fk + (size_t)j * F;
           for (uint32_t k = 0; k < fk_count; k++) {
-            const FKEntry& e = d.fk_entries[fk_begin + k];
+            const FKEntry& e = KD.fk_entries[fk_begin + k];
             const FK cur = cf[e.slot];
             cf[e.slot] = (cur.flags & FK_PRESENT)
-                             ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                             ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
                              : e.st;
           }
           const uint32_t e = s_so[f];
           if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
           s_so[f] = e + 1u;
-          d.log[nlog] = LogRec{gp, v, j, 0};
         }
+          wsync();
+          post(WQ_LOG, nlog, gp, v, rlane(j, wl), 0);
           break;
         }
       }
       if (fa_pos != INF) {
         // --- fast accept (simple pod): NodeClaim.Add changes the requests
-        // only; options, cursors and requirements stay.  The totals take
-        // no-return atomic adds at L2 (no round trip on the pod's path; a
-        // later exact check of this claim reads them after the adds, same
-        // wave, same addresses); LDS room and slack shrink by the request
-        // (still a lower / upper bound).
+        // only; options, cursors and requirements stay.  LDS room and slack
+        // shrink by the request (still a lower / upper bound); the agent wave
+        // adds the requests to the claim's totals (an exact check drains the
+        // channel before it reads them).
         f = fa_pos;
         const uint32_t j = fa_j;
-        if (lane < R && lane < 4 && rq_lane != 0)
-          atomicAdd((unsigned long long*)&d.c_rec[j].tot_lo[lane], (unsigned long long)rq_lane);
-        if (lane == 0) {
+        {
+          // lane r < RQ re-quantizes resource r: room (lower bound) and
+          // slack (upper bound) shrink by the request
           const uint64_t rm = s_rm[j], sl = s_slk[j];
+          uint32_t c_rm = 0, c_sl = 0;
+          if (lane < d.RQ) {
+            const uint32_t sh = 16 * lane;
+            c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - rq_lane);
+            c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - rq_lane);
+          }
           uint64_t rm2 = 0, sl2 = 0;
 #pragma unroll
           for (uint32_t r = 0; r < 4; r++) {
-            if (r >= d.RQ) break;
-            rm2 |= (uint64_t)qcode_floor(qcode_value((uint32_t)(rm >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
-            sl2 |= (uint64_t)qcode_ceil(qcode_value((uint32_t)(sl >> (16 * r)) & 0xFFFFu) - rq[r]) << (16 * r);
+            if (r < d.RQ) {
+              rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+              sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            }
           }
-          s_rm[j] = rm2;
-          s_slk[j] = sl2;
-          const uint32_t e = s_so[f];
-          if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
-          s_so[f] = e + 1u;
-          d.log[nlog] = LogRec{gp, v, j, 0};
+          if (lane == 0) {
+            s_rm[j] = rm2;
+            s_slk[j] = sl2;
+            const uint32_t e = s_so[f];
+            if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+            s_so[f] = e + 1u;
+          }
         }
-        n_fa++;
+        wsync();
+        post(WQ_FA, nlog, gp, v, j, rqd);  // the agent adds the requests and logs
+        CTR(C_FA, 1);
         break;
       }
       if (resume == INF) break;
@@ -993,6 +1165,13 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
     n_fsum += f != INF ? f : 0;
 #endif
+    if (simple) {
+      // [0, f) (or all positions) are infeasible for these requests
+      hint = f != INF ? f : M;
+      hint_ok = true;
+      hint_tolt = vtolt;
+      if (lane < 4) s_hint_rq[lane] = rq_lane;
+    }
     if (f != INF) {
       wsync();
       modkind = MOD_INC;
@@ -1003,9 +1182,16 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 
     // ------------------------------- new NodeClaim from templates, in order
     bool opened = false;
+    {
+      const auto& KD = *karg();
+      const uint32_t vx = fresh(vrd);
+      auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+      auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+      const uint32_t fk_begin = VX(1), fk_count = VX(2), vzflags = VX(30);
+      const uint64_t vzm = VX64(14), vcm = VX64(16), vzn = VX64(28);
     for (uint32_t t = 0; t < T; t++) {
-      const TmplRec& tr = d.tmpl[t];
-      const uint64_t* row = d.rows + ((size_t)v * T + t) * OW;
+      const TmplRec& tr = KD.tmpl[t];
+      const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
       // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
       // a new hostname domain has count 0, always within maxSkew >= 1):
       // the picked zone narrows the K1 row to that zone's offerings
@@ -1013,14 +1199,14 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
       if (TOPO && own) {
         const uint64_t D = tr.zfull & vzn;
         bool ok = true;
-        for (uint64_t m = own & d.tg_zone; m && ok; m &= m - 1) {
+        for (uint64_t m = own & KD.tg_zone; m && ok; m &= m - 1) {
           const uint32_t g = ffs64(m);
           const uint64_t cand = D & s_known[g];
-          const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
+          const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = KD.tgroups[g].skew;
           uint32_t best = NONE;
           int64_t bc = INT32_MAX;
-          for (uint32_t k = 0; k < d.NZV && cand; k++) {
-            const uint32_t z = d.zone_order[k];
+          for (uint32_t k = 0; k < KD.NZV && cand; k++) {
+            const uint32_t z = KD.zone_order[k];
             if (!((cand >> z) & 1)) continue;
             const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
             if (c - mn <= skew && c < bc) {
@@ -1032,7 +1218,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
           ttz = best;
         }
         if (ok && ttz != NONE) {
-          tzc = d.zone_cat[ttz];
+          tzc = KD.zone_cat[ttz];
           ok = tzc < 64;
         }
         ttz = __builtin_amdgcn_readfirstlane(ttz);
@@ -1044,24 +1230,24 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         uint64_t x = row[w];
         if (ttz != NONE) {
           uint64_t off = 0;
-          for (uint32_t c = 0; c < d.C; c++)
-            if ((tcm >> c) & 1) off |= slot[(tzc * d.C + c) * W + w];
+          for (uint32_t c = 0; c < KD.C; c++)
+            if ((tcm >> c) & 1) off |= slot[(tzc * KD.C + c) * W + w];
           x &= off;
         }
         return x;
       };
       bool anyl = false;
-      if (d.fk_ok[(size_t)v * T + t])
+      if (KD.fk_ok[(size_t)v * T + t])
         for (uint32_t w = lane; w < W; w += 64) anyl = anyl || rowx(w) != 0;
       if (!__ballot(anyl)) continue;
       if (tr.has_limits) {
         // <U> filterByRemainingResources on the template's options
         bool hit = false;
-        for (uint32_t i = lane; i < d.N; i += 64) {
+        for (uint32_t i = lane; i < KD.N; i += 64) {
           if (!((rowx(i >> 6) >> (i & 63)) & 1)) continue;
           bool ok = true;
           for (uint32_t r = 0; r < R; r++)
-            if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
+            if ((tr.limit_rmask >> r) & 1) ok = ok && KD.it_cap[(size_t)r * KD.N + i] <= KD.t_rem[(size_t)t * R + r];
           hit = hit || ok;
         }
         if (!__ballot(hit)) continue;
@@ -1071,7 +1257,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         break;
       }
       const uint32_t j = M;
-      ClaimRec* cr = d.c_rec + j;
+      ClaimRec* cr = KD.c_rec + j;
       // threshold cursors of the fresh claim: lane r < R
       int64_t tot_l = 0;
       uint32_t c0_l = 0;
@@ -1092,7 +1278,7 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         uint64_t x = rowx(w);
         // establish opts ⊆ thr_set[cursor] for the candidate scan
 #pragma unroll
-        for (uint32_t r = 0; r < RR; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + c0[r]) * OW + w];
+        for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)(s_thoff[r] + r + c0[r]) * OW + w];
         if (tr.has_limits) {
           uint64_t y = 0;
           for (uint64_t m = x; m; m &= m - 1) {
@@ -1100,12 +1286,12 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             const uint32_t i = w * 64 + b;
             bool ok = true;
             for (uint32_t r = 0; r < R; r++)
-              if ((tr.limit_rmask >> r) & 1) ok = ok && d.it_cap[(size_t)r * d.N + i] <= d.t_rem[(size_t)t * R + r];
+              if ((tr.limit_rmask >> r) & 1) ok = ok && KD.it_cap[(size_t)r * KD.N + i] <= KD.t_rem[(size_t)t * R + r];
             if (ok) y |= 1ull << b;
           }
           x = y;
         }
-        d.c_opts[(size_t)j * OW + w] = x;
+        KD.c_opts[(size_t)j * OW + w] = x;
         xw[h] = x;
       }
       if (lane < RR) {
@@ -1123,10 +1309,10 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         const uint32_t i = w * 64 + lane;
 #pragma unroll
         for (uint32_t r = 0; r < RR; r++) {
-          const uint64_t a = (uint64_t)d.it_alloc[(size_t)r * d.N + i];
+          const uint64_t a = (uint64_t)KD.it_alloc[(size_t)r * KD.N + i];
           mxa[r] = a > mxa[r] ? a : mxa[r];
           if (tr.has_limits && ((tr.limit_rmask >> r) & 1)) {
-            const uint64_t c = (uint64_t)(d.it_cap[(size_t)r * d.N + i] + (1ll << 62));
+            const uint64_t c = (uint64_t)(KD.it_cap[(size_t)r * KD.N + i] + (1ll << 62));
             mxc[r] = c > mxc[r] ? c : mxc[r];
           }
         }
@@ -1150,11 +1336,11 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
         for (uint32_t r = 0; r < RR; r++) cr->maxa[r] = ma[r];
         if (TOPO) {
           // <U> Topology.Register(hostname placeholder) + Record
-          for (uint32_t h = 0; h < d.TGH; h++) d.hc[(size_t)h * d.max_claims + j] = 0;
+          for (uint32_t h = 0; h < KD.TGH; h++) KD.hc[(size_t)h * KD.max_claims + j] = 0;
           for (uint64_t m = vtsel; m; m &= m - 1) {
             const uint32_t g = ffs64(m);
-            if ((d.tg_host >> g) & 1) {
-              d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + j]++;
+            if ((KD.tg_host >> g) & 1) {
+              KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
             } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
               const uint32_t z = ffs64(cr->zfull);
               s_zcnt[g * ZVMAX + z]++;
@@ -1162,32 +1348,33 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
             }
           }
         }
-        FK* cf = d.c_fk + (size_t)j * F;
-        for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
+        FK* cf = KD.c_fk + (size_t)j * F;
+        for (uint32_t s = 0; s < F; s++) cf[s] = KD.t_fk[(size_t)t * F + s];
         for (uint32_t k = 0; k < fk_count; k++) {
-          const FKEntry& e = d.fk_entries[fk_begin + k];
+          const FKEntry& e = KD.fk_entries[fk_begin + k];
           const FK cur = cf[e.slot];
           cf[e.slot] = (cur.flags & FK_PRESENT)
-                           ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                           ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
                            : e.st;
         }
         s_so[M] = 1u | (M << 16);
         s_tmpl[M] = (uint8_t)t;
         s_slk[j] = pack_slack(d, ma, nt);
-        s_rm[j] = pack_room(thr, s_thoff, c0, nt, d.RQ);
-        d.log[nlog] = LogRec{gp, v, j, 0};
+        s_rm[j] = pack_room(thr, s_thoff, c0, nt, KD.RQ);
         if (tr.has_limits) {
           // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
           for (uint32_t r = 0; r < R; r++)
-            if (((tr.limit_rmask >> r) & 1) && mxc[r] != 0) d.t_rem[(size_t)t * R + r] -= (int64_t)(mxc[r] - (1ull << 62));
+            if (((tr.limit_rmask >> r) & 1) && mxc[r] != 0) KD.t_rem[(size_t)t * R + r] -= (int64_t)(mxc[r] - (1ull << 62));
         }
       }
       wsync();
+      post(WQ_LOG, nlog, gp, v, j, 0);
       M++;
       modkind = MOD_APPEND;
       nlog++;
       opened = true;
       break;
+    }
     }
     TLW(4);  // new NodeClaim
     if (status) break;
@@ -1195,29 +1382,37 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
 
     // -------------------------------------- failed: Relax, then Queue.Push
     {
-      const uint32_t vb = __builtin_amdgcn_readfirstlane(d.var_begin[gp]);
-      const uint32_t vc = __builtin_amdgcn_readfirstlane(d.var_count[gp]);
+      const auto& KD = *karg();
+      const uint32_t vb = __builtin_amdgcn_readfirstlane(KD.var_begin[gp]);
+      const uint32_t vc = __builtin_amdgcn_readfirstlane(KD.var_count[gp]);
       const bool relaxed = v + 1 < vb + vc;
       uint32_t tail = qhead + qlen;
       if (tail >= P) tail -= P;
       qlen++;
       if (lane == 0) {
-        if (relaxed) d.cur_var[p] = v + 1;
-        d.queue[tail] = p;
+        if (relaxed) KD.cur_var[p] = v + 1;
+        KD.queue[tail] = p;
         if (!relaxed) {
-          d.last_epoch[p] = epoch;
-          d.last_len[p] = qlen;
+          KD.last_epoch[p] = epoch;
+          KD.last_len[p] = qlen;
         }
       }
       if (relaxed) epoch++;
     }
   }
+  // stop the agent once every posted write is done
+  post(WQ_STOP, 0, 0, 0, 0, 0);
+  drain();
+  if (chan_err) status = 2;
   wsync();
   for (uint32_t i = lane; i < M; i += 64) {
     const uint32_t e = s_so[i];
     d.c_sorted[i] = e >> 16;
     d.c_rec[e >> 16].count = e & 0xFFFFu;
   }
+  auto ctr_at = [&](uint32_t k) -> uint64_t { return (uint64_t)rlane((uint32_t)ctr, k) | ((uint64_t)rlane((uint32_t)(ctr >> 32), k) << 32); };
+  const uint64_t ctr_gen = ctr_at(C_GEN), ctr_fast = ctr_at(C_FAST), ctr_cand = ctr_at(C_CAND), ctr_full = ctr_at(C_FULL),
+                 ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA);
   if (lane == 0) {
     Ctrl c = {};
     c.status = status;
@@ -1227,16 +1422,20 @@ __global__ __launch_bounds__(64, 1) void ffdw_kernel(DevProblem d) {
     c.qlen = qlen;
     c.epoch = epoch;
     c.pops = pops;
-    c.generic_sorts = n_generic;
-    c.fast_sorts = n_fast;
-    c.cand_evals = n_cand;
-    c.cand_full = n_full;
-    c.node_evals = n_nev;
-    c.node_prefix = n_npre;
-    c.dbg[15] = n_fa;
+    c.generic_sorts = ctr_gen;
+    c.fast_sorts = ctr_fast;
+    c.cand_evals = ctr_cand;
+    c.cand_full = ctr_full;
+    c.node_evals = ctr_nev;
+    c.node_prefix = ctr_npre;
+    c.dbg[15] = ctr_fa;
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
     c.dbg[8] = n_fsum;
+    c.dbg[9] = n_xns;
+    c.dbg[10] = n_xb;
+    c.dbg[11] = n_xwin;
+    c.dbg[12] = n_nonsimple;
 #endif
     *d.ctrl = c;
   }
@@ -1279,8 +1478,8 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
   switch (d->R * 2 + (d->TG ? 1 : 0)) {
 #define GSK_CASE(n)                                                                                      \
-  case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(64), lds, s, *d); break;      \
-  case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(64), lds, s, *d); break;
+  case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(128), lds, s, *d); break;      \
+  case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(128), lds, s, *d); break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

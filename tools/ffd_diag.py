@@ -28,6 +28,10 @@ if "--tl" in sys.argv and "--block" not in sys.argv:
     base["cycles_per_pop_total"] = round(sum(out[i] for i in range(8)) / max(res.pops, 1), 1)
     base["mean_winner_pos"] = round(out[8] / max(res.pops, 1), 1)
     base["fast_accepts"] = out[15]
+    base["exact_cands_nonsimple"] = out[9]
+    base["exact_batches"] = out[10]
+    base["exact_wins"] = out[11]
+    base["nonsimple_pops"] = out[12]
 elif "--tl" in sys.argv:
     names = ["to_top", "publish", "pop", "stage_nodes", "sort_decide", "rotate", "chunk_lds", "reduce2", "exact",
              "winner_end", "new_claim"]
