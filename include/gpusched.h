@@ -418,7 +418,9 @@ gs_status gs_feasibility_shard_device(gs_ctx* ctx, uint32_t word_begin, uint32_t
  * ties come out exactly as the reference's.  Writes out_order[0..*out_n)
  * (List indices, ranked) and out_score (same order).  One workgroup on the
  * current device; n <= GS_RANK_MAX (GS_E_CAPACITY above), negative
- * quantities and NaN prices GS_E_INVALID. */
+ * quantities and NaN prices GS_E_INVALID.  Runs on the calling thread's
+ * current HIP device (hipSetDevice, or the device of the last gs_* call on
+ * this thread); device buffers are kept per device. */
 #define GS_ARCH_ANY 0xFFFFFFFFu
 #define GS_RANK_MAX 4096u
 gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,

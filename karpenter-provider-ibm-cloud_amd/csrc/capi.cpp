@@ -276,7 +276,7 @@ gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
   er = capacity_check(c->enc);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
-  c->problem = p;
+  c->n_nodepools = p->n_nodepools;
   try {
     HIPCHK(hipSetDevice(c->device));
     auto t1 = Clock::now();
@@ -470,7 +470,7 @@ gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
 gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
   auto& e = c->enc;
-  const uint32_t P = e.P, NP = c->problem->n_nodepools, W = e.W;
+  const uint32_t P = e.P, NP = c->n_nodepools, W = e.W;
   word_end = std::min(word_end, W);
   if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
   float ms = 0;

@@ -37,14 +37,6 @@ std::string norm_key(const std::string& k) {
 
 const char* str(const gs_problem* p, uint32_t id) { return id < p->n_strings && p->strings[id] ? p->strings[id] : ""; }
 
-// one disruption candidate: <U> Candidate.instanceType / capacityType and
-// getCandidatePrices' c.instanceType.Offerings.Compatible(labels).Cheapest()
-struct CandInfo {
-  bool priced = false;
-  double price = 0;
-  std::string it_name;
-  bool spot = false;
-};
 
 CandInfo candidate_info(const gs_problem* p, uint32_t node) {
   CandInfo ci;
@@ -94,6 +86,22 @@ CandInfo candidate_info(const gs_problem* p, uint32_t node) {
   return ci;
 }
 
+}  // namespace
+
+// What the decisions read from the caller's cluster, copied at
+// gs_consolidate time (gs_consolidate_rerun must not touch caller memory:
+// the ABI only borrows it for the duration of a call)
+CandTable build_cand_table(const gs_problem* p, const uint32_t* cands, uint32_t n) {
+  CandTable t;
+  for (uint32_t i = 0; i < n; i++)
+    if (cands[i] < p->n_nodes && !t.node.count(cands[i])) t.node.emplace(cands[i], candidate_info(p, cands[i]));
+  t.it_name.reserve(p->n_instance_types);
+  for (uint32_t i = 0; i < p->n_instance_types; i++) t.it_name.push_back(str(p, p->instance_types[i].name));
+  return t;
+}
+
+namespace {
+
 // the simulations a mode evaluates (candidate node indices per simulation)
 gs_status build_sets(const gs_consolidation* in, SimPlan& sp, std::string* err) {
   sp.sets.clear();
@@ -135,12 +143,12 @@ uint64_t grid_of(uint64_t zm, uint64_t cm, uint32_t Z, uint32_t C) {
 }
 
 // <U> filterOutSameInstanceType: indices of the options that survive
-std::vector<uint32_t> filter_out_same_type(const gs_problem* p, const std::vector<uint32_t>& cands,
+std::vector<uint32_t> filter_out_same_type(const CandTable& t, const std::vector<uint32_t>& cands,
                                            const uint32_t* opts, const double* prices, uint32_t n) {
   std::set<std::string> existing;
   std::map<std::string, double> price_by_type;
   for (uint32_t c : cands) {
-    const CandInfo ci = candidate_info(p, c);
+    const CandInfo& ci = t.node.at(c);
     existing.insert(ci.it_name);
     if (!ci.priced) continue;
     auto f = price_by_type.find(ci.it_name);
@@ -149,7 +157,7 @@ std::vector<uint32_t> filter_out_same_type(const gs_problem* p, const std::vecto
   }
   double max_price = __DBL_MAX__;
   for (uint32_t i = 0; i < n; i++) {
-    const std::string nm = str(p, p->instance_types[opts[i]].name);
+    const std::string& nm = t.it_name[opts[i]];
     if (!existing.count(nm)) continue;
     auto f = price_by_type.find(nm);
     const double pr = f == price_by_type.end() ? 0.0 : f->second;  // Go map zero value
@@ -162,7 +170,7 @@ std::vector<uint32_t> filter_out_same_type(const gs_problem* p, const std::vecto
 }
 
 // policy replay over a complete command table
-int32_t choose(const gs_problem* p, uint32_t mode, const std::vector<std::vector<uint32_t>>& sets, uint32_t multi_max,
+int32_t choose(const CandTable& t, uint32_t mode, const std::vector<std::vector<uint32_t>>& sets, uint32_t multi_max,
                const gs_command* cmds, const uint32_t* opts, const double* prices, std::vector<uint32_t>* multi_opts) {
   multi_opts->clear();
   if (mode == GS_CONSOLIDATE_SINGLE) {
@@ -179,7 +187,7 @@ int32_t choose(const gs_problem* p, uint32_t mode, const std::vector<std::vector
     bool valid = false;
     std::vector<uint32_t> keep;
     if (c.decision == GS_DECISION_REPLACE) {
-      for (uint32_t i : filter_out_same_type(p, sets[mid - 1], opts + c.options.begin, prices + c.options.begin,
+      for (uint32_t i : filter_out_same_type(t, sets[mid - 1], opts + c.options.begin, prices + c.options.begin,
                                              c.options.count))
         keep.push_back(opts[c.options.begin + i]);
       valid = !keep.empty();
@@ -345,7 +353,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     double cp = 0;
     bool all_spot = true, priced = true;
     for (uint32_t n : sp.sets[s]) {
-      const CandInfo ci = candidate_info(cl, n);
+      const CandInfo& ci = c->cand_table.node.at(n);
       priced = priced && ci.priced;
       cp += ci.price;
       all_spot = all_spot && ci.spot;
@@ -394,7 +402,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   int32_t chosen = -1;
   c->multi_opts.clear();
   if (NS == sp.sets.size())
-    chosen = choose(cl, in->mode, sp.sets, sp.multi_max, c->commands.data(), c->cmd_options.data(),
+    chosen = choose(c->cand_table, in->mode, sp.sets, sp.multi_max, c->commands.data(), c->cmd_options.data(),
                     c->cmd_prices.data(), &c->multi_opts);
   c->t_fetch = ms_since(t0);
   std::memset(out, 0, sizeof(*out));
@@ -465,6 +473,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   c->cons_in = *in;
   c->cons_in.candidates = c->cons_cands.data();
   c->cons_in.sets = c->cons_sets.data();
+  c->cand_table = build_cand_table(in->cluster, in->candidates, in->n_candidates);
   // the combined pod list: pending pods, then every bound pod
   const gs_problem* cl = in->cluster;
   c->n_pending = cl->n_pods;
@@ -477,7 +486,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   c->cons_problem.n_bound_pods = 0;
   c->cons_problem.bound_pod_node = nullptr;
   if (cl->n_spreads) return fail(c, GS_E_UNSUPPORTED, "topology spread constraints in consolidation simulations");
-  c->problem = &c->cons_problem;
+  c->n_nodepools = c->cons_problem.n_nodepools;
   auto t0 = Clock::now();
   gsh::Err er = gsh::encode(&c->cons_problem, c->enc);
   c->t_encode = ms_since(t0);
@@ -514,7 +523,8 @@ gs_status gs_consolidation_choose(const gs_consolidation* in, const gs_command* 
   for (uint32_t s = 0; s < n_commands; s++)
     if (commands[s].decision == GS_DECISION_SKIPPED) return GS_E_INVALID;
   std::vector<uint32_t> mo;
-  *chosen = choose(in->cluster, in->mode, sp.sets, sp.multi_max, commands, options, option_prices, &mo);
+  const CandTable t = build_cand_table(in->cluster, in->candidates, in->n_candidates);
+  *chosen = choose(t, in->mode, sp.sets, sp.multi_max, commands, options, option_prices, &mo);
   if (multi_options && n_multi_options) {
     const uint32_t n = (uint32_t)std::min<size_t>(mo.size(), 60);
     std::copy(mo.begin(), mo.begin() + n, multi_options);

@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/gpusched.h"
@@ -50,6 +51,19 @@ struct HipError {
     if (e_ != hipSuccess) throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)}; \
   } while (0)
 
+// one disruption candidate: <U> Candidate.instanceType / capacityType and
+// getCandidatePrices' c.instanceType.Offerings.Compatible(labels).Cheapest()
+struct CandInfo {
+  bool priced = false;
+  double price = 0;
+  std::string it_name;
+  bool spot = false;
+};
+struct CandTable {
+  std::unordered_map<uint32_t, CandInfo> node;  // candidate node index -> info
+  std::vector<std::string> it_name;              // catalog index -> instance-type name
+};
+
 // The simulations of one gs_consolidate call (device-side layout: layout.hpp
 // DevProblem consolidation fields).
 struct SimPlan {
@@ -73,8 +87,8 @@ struct gs_ctx {
   gsh::Encoded enc;
   gsd::DevProblem dp{};
   bool prepared = false, ran = false;
+  uint32_t n_nodepools = 0;  // of the prepared problem (the caller's arrays are not kept)
   double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
-  const gs_problem* problem = nullptr;
   // result storage
   std::vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
   std::vector<std::string> req_text;
@@ -96,6 +110,7 @@ struct gs_ctx {
   std::vector<gs_range> cons_sets;
   uint32_t n_pending = 0;
   gsc::SimPlan sims;
+  gsc::CandTable cand_table;
   std::vector<gs_command> commands;
   std::vector<uint32_t> cmd_options;
   std::vector<double> cmd_prices;

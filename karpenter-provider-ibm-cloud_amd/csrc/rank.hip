@@ -151,14 +151,21 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GS_E_NO_DEVICE;
   if (n == 0) return GS_OK;
-  // one grow-once device buffer (serialized by a mutex): inputs packed as
-  // cpu | mem | price (8 B each) | arch (4 B), outputs score (8 B) | order
+  // one grow-once buffer per device (the call runs on the calling thread's
+  // current device; cgo may move a goroutine between OS threads, so a buffer
+  // is never reused on another device), serialized by a mutex: inputs packed
+  // as cpu | mem | price (8 B each) | arch (4 B), outputs score (8 B) | order
   // (4 B) | count; one H2D copy in, one D2H copy out
+  constexpr int kMaxDev = 64;
   static std::mutex mu;
-  static char* dbuf = nullptr;
-  static size_t dcap = 0;
+  static char* dbufs[kMaxDev] = {};
+  static size_t dcaps[kMaxDev] = {};
   static std::vector<char> hin, hout;
   std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return GS_E_NO_DEVICE;
+  char*& dbuf = dbufs[dev];
+  size_t& dcap = dcaps[dev];
   const size_t nn = n;
   const size_t in_bytes = nn * 28, out_bytes = nn * 12 + 8;
   const size_t out_off = (in_bytes + 255) & ~(size_t)255;

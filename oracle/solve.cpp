@@ -930,6 +930,18 @@ struct Scheduler {
   bool claim_can_add(const NodeClaim& n, const Pod& pod, Reqs* reqs_out, vector<const InstanceType*>* its_out,
                      Res* req_out) {
     if (!tolerates_all(n.tmpl->taints, pod.tolerations)) return false;
+    Res requests = merge(n.requests, pod.requests);
+    // Evaluation order only (same result): filterInstanceTypesByRequirements
+    // keeps an instance type only if Fits(requests, allocatable), and every
+    // step before it is side-effect free, so when no option fits the merged
+    // requests CanAdd is false whatever the requirement checks would say.
+    bool any_fit = false;
+    for (auto* it : n.options)
+      if (fits(requests, it->allocatable)) {
+        any_fit = true;
+        break;
+      }
+    if (!any_fit) return false;
     Reqs nr = n.reqs;  // NewRequirements(n.Requirements.Values()...)
     if (!nr.compatible(pod.reqs, true)) return false;
     nr.add_all(pod.reqs);
@@ -937,7 +949,6 @@ struct Scheduler {
     if (!topo_requirements(pod, nr, &topo)) return false;
     if (!nr.compatible(topo, true)) return false;
     nr.add_all(topo);
-    Res requests = merge(n.requests, pod.requests);
     auto remaining = filter_its(n.options, nr, requests);
     if (remaining.empty()) return false;
     *reqs_out = std::move(nr);

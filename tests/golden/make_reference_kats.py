@@ -88,6 +88,67 @@ KATS = {
             [{"name": "test-profile", "vcpu": 2, "memory_gib": 16}, False, "IBM client not initialized"],
         ],
     },
+    "rank_orders": {  # pkg/providers/common/instancetype/instancetype_mock_test.go:221-361
+        # makeInstanceType(name, cpu milli, memory bytes, arch) + the price the
+        # ranking sees (RankInstanceTypes with a nil pricing provider or nil
+        # client prices every type at 0.0, :300-353)
+        "source": "instancetype_mock_test.go:221-361",
+        "cases": [
+            {"name": "ByPrice", "types": [["expensive", 4000, 16 * 2**30, 1.00], ["cheap", 4000, 16 * 2**30, 0.10],
+                                          ["mid", 4000, 16 * 2**30, 0.50]],
+             "want": ["cheap", "mid", "expensive"]},
+            {"name": "NoPricing_FallsBackToResourceSize",
+             "types": [["large", 8000, 32 * 2**30, 0.0], ["small", 2000, 8 * 2**30, 0.0]], "want": ["small", "large"]},
+            {"name": "MixedPricingAndNoPricing",
+             "types": [["no-price", 4000, 8 * 2**30, 0.0], ["has-price", 4000, 8 * 2**30, 0.10]],
+             "want_first": "has-price"},
+            {"name": "NilPricingProvider",
+             "types": [["bx2-8x32", 8000, 32 * 2**30, 0.0], ["bx2-2x8", 2000, 8 * 2**30, 0.0]],
+             "want": ["bx2-2x8", "bx2-8x32"]},
+            {"name": "EmptyInput", "types": [], "want": []},
+            {"name": "SingleInstance", "types": [["bx2-4x16", 4000, 16 * 2**30, 0.0]], "want": ["bx2-4x16"]},
+            {"name": "ClientNilWithPricingProvider",
+             "types": [["bx2-4x16", 4000, 16 * 2**30, 0.0], ["bx2-2x8", 2000, 8 * 2**30, 0.0]],
+             "want": ["bx2-2x8", "bx2-4x16"]},
+            {"name": "EqualScores_PreservesAll",
+             "types": [["bx2-2x8", 2000, 8 * 2**30, 0.0], ["cx2-2x8", 2000, 8 * 2**30, 0.0]],
+             "want_set": ["bx2-2x8", "cx2-2x8"]},
+        ],
+    },
+    "score_zero_resources": {  # instancetype_mock_test.go:372-383
+        "source": "instancetype_mock_test.go:372-383",
+        "cpu_milli": 0, "memory_bytes": 0, "price": 0.0, "want": 0.0,
+    },
+    "resolve_capacity_type": {  # pkg/providers/common/capacitytype/capacitytype_test.go:30-169
+        # nodeClaim requirements (None = nil Requirements), instance types as
+        # lists of offerings [capacity type, zone, price, available]
+        "source": "capacitytype_test.go:30-169",
+        "cases": [
+            {"name": "nil requirements defaults to on-demand", "requirements": None, "types": [], "want": "on-demand"},
+            {"name": "empty requirements defaults to on-demand", "requirements": [], "types": [],
+             "want": "on-demand"},
+            {"name": "on-demand only requirement returns on-demand",
+             "requirements": [["karpenter.sh/capacity-type", "In", ["on-demand"]]], "types": [], "want": "on-demand"},
+            {"name": "spot allowed but no available spot offering returns on-demand",
+             "requirements": [["karpenter.sh/capacity-type", "In", ["spot", "on-demand"]]],
+             "types": [[["on-demand", "us-south-1", 0.1, True]]], "want": "on-demand"},
+            {"name": "spot allowed with available spot offering returns spot",
+             "requirements": [["karpenter.sh/capacity-type", "In", ["spot", "on-demand"]]],
+             "types": [[["spot", "us-south-1", 0.06, True]]], "want": "spot"},
+            {"name": "spot allowed but spot offering unavailable returns on-demand",
+             "requirements": [["karpenter.sh/capacity-type", "In", ["spot"]]],
+             "types": [[["spot", "us-south-1", 0.06, False]]], "want": "on-demand"},
+        ],
+    },
+    "get_instance_types_counts": {  # pkg/cloudprovider/cloudprovider_test.go:686-798 (+ getTestInstanceType)
+        # a NodePool without requirements keeps every listed type, whatever its
+        # offerings (GetInstanceTypes filters on Compatible only, cloudprovider.go:574-577)
+        "source": "cloudprovider_test.go:686-798",
+        "cases": [
+            {"name": "successful get instance types", "n_types": 2, "second_has_offerings": False, "want": 2},
+            {"name": "empty instance types", "n_types": 0, "want": 0},
+        ],
+    },
     "fake_profiles": {  # pkg/fake/zz_generated_ibm_test_data.go:27-243 (C1 catalog)
         "source": "pkg/fake/zz_generated_ibm_test_data.go:27-243,286-314",
         "profiles": [["bx2-2x8", 2, 8, None], ["bx2-4x16", 4, 16, None], ["bx2-8x32", 8, 32, None],
