@@ -428,6 +428,47 @@ gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int
                                  int64_t min_memory_gb, double max_price, uint32_t* out_order, uint32_t* out_n,
                                  double* out_score);
 
+/* ------------------------------------------------ launch-time re-filter
+ * One NodeClaim as CloudProvider.Create sees it (reference
+ * pkg/cloudprovider/cloudprovider.go:284-346): spec.requirements and
+ * spec.resources.requests, as ranges into the catalog gs_problem's reqs /
+ * quantities arrays (append the claims' requirements to the same pools). */
+typedef struct gs_claim_query {
+  gs_range requirements; /* NodeClaim spec.requirements (NewNodeSelectorRequirementsWithMinValues) */
+  gs_range requests;     /* spec.resources.requests */
+} gs_claim_query;
+
+enum { GS_CAPACITY_ON_DEMAND = 0, GS_CAPACITY_SPOT = 1 };
+
+/* Results of gs_create_filter, owned by the ctx (valid until the next
+ * gs_create_filter or gs_destroy).  Bitsets are [n_queries][words], bit i of
+ * word w = catalog instance type 64*w + i (List order). */
+typedef struct gs_claim_filter_result {
+  uint32_t n_queries;
+  uint32_t words;               /* ceil(n_instance_types / 64) */
+  const uint64_t* compatible;   /* Create's filter: reqs.Compatible(it.Requirements, AllowUndefinedWellKnownLabels)
+                                   && len(it.Offerings.Compatible(reqs).Available()) > 0
+                                   && resources.Fits(requests, it.Allocatable())   cloudprovider.go:322-329 */
+  const uint64_t* requirements; /* GetInstanceTypes' filter: reqs.Compatible(it.Requirements, ...) only
+                                   (cloudprovider.go:574-577), the claim's requirements standing for the
+                                   NodePool template's */
+  const uint32_t* n_compatible; /* popcount of `compatible` (0: Create returns InsufficientCapacityError, :345) */
+  const int32_t* selected;      /* instanceTypes[0] of the compatible list (vpc/instance/provider.go:215-221),
+                                   -1 when empty */
+  const uint32_t* capacity_type; /* GS_CAPACITY_*: capacitytype.ResolveCapacityType(nodeClaim, compatible)
+                                   (pkg/providers/common/capacitytype/capacitytype.go:27-42) */
+} gs_claim_filter_result;
+
+/* Batched CloudProvider.Create re-filter + instance selection + capacity type
+ * for n_queries NodeClaims against the catalog's instance types (only the
+ * catalog fields of `catalog` are read: strings, value_ids, reqs, quantities,
+ * offerings, instance_types).  Requirements use the full scheduling.Requirement
+ * algebra (In/NotIn/Exists/DoesNotExist/Gt/Lt, any key, label-key
+ * normalisation); Gte/Lte and minValues are GS_E_UNSUPPORTED.  One device
+ * pass over all (claim, instance type) pairs on the ctx's device. */
+gs_status gs_create_filter(gs_ctx* ctx, const gs_problem* catalog, const gs_claim_query* queries,
+                           uint32_t n_queries, gs_claim_filter_result* out);
+
 /* host-only: run the encoder (no device needed) and report whether this
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.
  * A Go caller uses it to choose between this library and upstream Solve. */
@@ -437,8 +478,9 @@ gs_status gs_validate(const gs_problem* problem, char* err, size_t err_len);
  * gs_quantity, gs_label, gs_taint, gs_toleration, gs_term, gs_offering,
  * gs_instance_type, gs_nodepool, gs_pod, gs_node, gs_problem, gs_result,
  * gs_feas_result, gs_config, gs_consolidation, gs_command,
- * gs_consolidation_result.  Bindings check their layouts against it.
- * Returns the number of entries (19); writes min(n, 19). */
+ * gs_consolidation_result, gs_claim_query, gs_claim_filter_result.
+ * Bindings check their layouts against it.
+ * Returns the number of entries (21); writes min(n, 21). */
 uint32_t gs_abi_sizes(uint32_t* out, uint32_t n);
 
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);

@@ -270,7 +270,6 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   const gsh::Encoded& e = c->enc;
   const SimPlan& sp = c->sims;
   const gs_consolidation* in = &c->cons_in;
-  const gs_problem* cl = in->cluster;
   auto& d = c->dp;
   const size_t NS = sp.evaluated.size();
   const gsd::Ctrl* ctrl = c->h_ctrl;

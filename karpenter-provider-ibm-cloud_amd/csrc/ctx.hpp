@@ -123,6 +123,14 @@ struct gs_ctx {
   uint32_t* h_nits = nullptr;
   double t_sim = 0;
 
+  // gs_create_filter: grow-once device arena and result storage
+  void* cf_dev = nullptr;
+  size_t cf_bytes = 0;
+  std::vector<uint64_t> cf_create, cf_reqs, cf_spot;
+  std::vector<uint32_t> cf_n, cf_ct;
+  std::vector<int32_t> cf_sel;
+  double t_filter = 0;
+
   std::vector<void*> host_allocs;  // pinned staging buffers (consolidation results)
   void free_all() {
     for (void* p : allocs) (void)hipFree(p);

@@ -1242,4 +1242,9 @@ Err encode(const gs_problem* p, Encoded& e) {
   return Err{};
 }
 
+// label helpers shared with the launch-time re-filter (filter.hip)
+bool label_is_wellknown(const std::string& k) { return is_wellknown(k); }
+std::string label_normalize(const std::string& k) { return normalize(k); }
+bool go_atoi64(const std::string& s, int64_t* out) { return atoi64(s, out); }
+
 }  // namespace gsh

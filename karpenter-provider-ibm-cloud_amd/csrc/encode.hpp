@@ -138,6 +138,11 @@ struct Err {
 
 Err encode(const gs_problem* p, Encoded& e);
 
+// <U> v1.WellKnownLabels (+ IBM keys), v1.NormalizedLabels, strconv.Atoi
+bool label_is_wellknown(const std::string& k);
+std::string label_normalize(const std::string& k);
+bool go_atoi64(const std::string& s, int64_t* out);
+
 // algebra (exposed for decode)
 KReq kreq_intersect(const Vocab& v, const KReq& a, const KReq& b);
 void reqs_add(const Encoded& e, Reqs& r, uint32_t key, const KReq& q);

@@ -237,6 +237,41 @@ class GsConsolidationResult(C.Structure):
     ]
 
 
+class GsClaimQuery(C.Structure):
+    _fields_ = [("requirements", GsRange), ("requests", GsRange)]
+
+
+GS_CAPACITY_ON_DEMAND, GS_CAPACITY_SPOT = 0, 1
+
+
+class GsClaimFilterResult(C.Structure):
+    _fields_ = [
+        ("n_queries", _U32), ("words", _U32),
+        ("compatible", C.POINTER(C.c_uint64)),
+        ("requirements", C.POINTER(C.c_uint64)),
+        ("n_compatible", C.POINTER(C.c_uint32)),
+        ("selected", C.POINTER(C.c_int32)),
+        ("capacity_type", C.POINTER(C.c_uint32)),
+    ]
+
+
+def _bits(ptr, q, words, n):
+    return [64 * w + i for w in range(words) for i in range(64)
+            if (ptr[q * words + w] >> i) & 1 and 64 * w + i < n]
+
+
+def claim_filter_to_list(res: GsClaimFilterResult, n_types: int) -> list:
+    """per query: {compatible: [catalog indices], requirements: [...],
+    selected, capacity_type} (List order)"""
+    out = []
+    for q in range(res.n_queries):
+        out.append(dict(compatible=_bits(res.compatible, q, res.words, n_types),
+                        requirements=_bits(res.requirements, q, res.words, n_types),
+                        n_compatible=int(res.n_compatible[q]), selected=int(res.selected[q]),
+                        capacity_type=int(res.capacity_type[q])))
+    return out
+
+
 def commands_to_list(res: GsConsolidationResult) -> list:
     """Canonical, comparable form of the commands (copied out of library memory)."""
     out = []

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, os.environ.get("GPUSCHED_LIB", "libgpusched.so"))
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
            "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard",
-           "gs_feasibility_shard_device", "gs_rank_instance_types"]
+           "gs_feasibility_shard_device", "gs_rank_instance_types", "gs_create_filter"]
 
 
 class GpuSchedError(RuntimeError):
@@ -54,6 +54,9 @@ def load():
         L.gs_feasibility_shard.restype = C.c_int
         L.gs_feasibility_shard_device.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(abi.GsFeasDevice)]
         L.gs_feasibility_shard_device.restype = C.c_int
+        L.gs_create_filter.argtypes = [vp, C.POINTER(abi.GsProblem), C.POINTER(abi.GsClaimQuery), C.c_uint32,
+                                       C.POINTER(abi.GsClaimFilterResult)]
+        L.gs_create_filter.restype = C.c_int
         L.gs_rank_instance_types.argtypes = abi.RANK_ARGTYPES
         L.gs_rank_instance_types.restype = C.c_int
         L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
@@ -197,6 +200,16 @@ class Solver:
         if raw:
             return res
         return abi.commands_to_list(res), int(res.chosen), _multi(res), res
+
+    def create_filter(self, problem, raw=False):
+        """gs_create_filter over problem.claim_queries: per claim
+        {compatible, requirements, n_compatible, selected, capacity_type}"""
+        res = abi.GsClaimFilterResult()
+        self._check(self.L.gs_create_filter(self.ctx, C.byref(problem.struct), problem.claim_queries,
+                                            problem.n_claim_queries, C.byref(res)))
+        if raw:
+            return res
+        return abi.claim_filter_to_list(res, len(problem.instance_types))
 
     def feasibility(self):
         res = abi.GsFeasResult()

@@ -36,6 +36,7 @@ class ProblemBuilder:
         self.bound_pods = []  # pods bound to state nodes (topology counts; consolidation moves them)
         self.bound_node = []
         self.spreads = []
+        self.claim_queries = []  # gs_claim_query (launch-time re-filter)
 
     # ------------------------------------------------------------ primitives
     def s(self, x: str) -> int:
@@ -154,6 +155,12 @@ class ProblemBuilder:
         self.bound_node.append(int(node))
         return len(self.bound_pods) - 1
 
+    def add_claim_query(self, requirements=(), requests=None):
+        """a NodeClaim for gs_create_filter: spec.requirements (key, op,
+        values) and spec.resources.requests"""
+        self.claim_queries.append((self._reqs(requirements), self._qty(requests or {})))
+        return len(self.claim_queries) - 1
+
     def add_node(self, name, labels, available, requests=None, taints=(), initialized=True):
         self.nodes.append((self.s(name), 1 if initialized else 0, self._labels(labels), self._taints(taints),
                            self._qty(available), self._qty(requests or {})))
@@ -174,6 +181,7 @@ class Problem:
     """Owns the numpy arrays backing a gs_problem struct."""
 
     def __init__(self, b: ProblemBuilder):
+        self._builder = b
         self.strings = list(b.strings)
         self._bytes = [x.encode() for x in self.strings]
         self._cstrs = (C.c_char_p * len(self._bytes))(*self._bytes)
@@ -193,6 +201,11 @@ class Problem:
         self.bound_pods = _np(b.bound_pods, abi.DT_POD)
         self.bound_node = np.asarray(b.bound_node, dtype=np.uint32)
         self.spreads = _np(b.spreads, abi.DT_SPREAD)
+        self.claim_queries = (abi.GsClaimQuery * max(1, len(b.claim_queries)))()
+        self.n_claim_queries = len(b.claim_queries)
+        for i, (rq, qt) in enumerate(b.claim_queries):
+            self.claim_queries[i].requirements.begin, self.claim_queries[i].requirements.count = rq
+            self.claim_queries[i].requests.begin, self.claim_queries[i].requests.count = qt
         self.struct = abi.GsProblem()
         st = self.struct
         st.strings = self._cstrs
@@ -203,6 +216,25 @@ class Problem:
             setattr(st, name, arr.ctypes.data if len(arr) else None)
             setattr(st, "n_" + name, len(arr))
         st.bound_pod_node = self.bound_node.ctypes.data if len(self.bound_node) else None
+
+    def with_pods(self, idx):
+        """a view with pending pods pods[idx] (same pools: requirement, label
+        and quantity ranges stay valid) — e.g. an oracle check on a sample of
+        a problem too large for the oracle"""
+        import copy
+        q = copy.copy(self)
+        q.pods = self.pods[np.asarray(idx, dtype=np.int64)].copy()
+        q.struct = abi.GsProblem()
+        C.memmove(C.byref(q.struct), C.byref(self.struct), C.sizeof(abi.GsProblem))
+        q.struct.pods = q.pods.ctypes.data if len(q.pods) else None
+        q.struct.n_pods = len(q.pods)
+        return q
+
+    def extended(self, fn):
+        """a new Problem: this one's builder after fn(builder) appends to it
+        (string / value / requirement ids of this problem stay valid)"""
+        fn(self._builder)
+        return Problem(self._builder)
 
     @property
     def n_pods(self):

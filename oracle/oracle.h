@@ -89,6 +89,17 @@ gs_status oracle_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const
 gs_status oracle_consolidate(const gs_consolidation* in, gs_consolidation_result* out, int32_t* chosen,
                              uint32_t* multi_opts, uint32_t* n_multi_opts);
 
+/* CloudProvider.Create's filter + instanceTypes[0] + ResolveCapacityType and
+ * GetInstanceTypes' requirement filter, per claim: the CPU restatement of
+ * gs_create_filter.  Bitsets [n][ceil(n_instance_types/64)], caller-owned. */
+gs_status oracle_create_filter(const gs_problem* catalog, const gs_claim_query* queries, uint32_t n,
+                               uint64_t* compatible, uint64_t* requirements, int32_t* selected,
+                               uint32_t* capacity_type);
+/* capacitytype.ResolveCapacityType(nodeClaim, instanceTypes) over an explicit
+ * list of catalog indices (capacitytype.go:27-42) */
+gs_status oracle_resolve_capacity_type(const gs_problem* catalog, const gs_claim_query* query, const uint32_t* its,
+                                       uint32_t n, uint32_t* out);
+
 /* Go sort.Slice (pdqsort_func) applied to an int array with Less = a[i] < a[j];
  * perm receives the resulting permutation of original indices. */
 void oracle_go_sort_ints(int64_t* keys, uint32_t* perm, uint32_t n);

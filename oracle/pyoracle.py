@@ -68,6 +68,13 @@ def lib():
         L.oracle_consolidate.argtypes = [C.POINTER(abi.GsConsolidation), C.POINTER(abi.GsConsolidationResult),
                                          C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_consolidate.restype = C.c_int
+        L.oracle_create_filter.argtypes = [C.POINTER(abi.GsProblem), C.POINTER(abi.GsClaimQuery), C.c_uint32,
+                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_uint32)]
+        L.oracle_create_filter.restype = C.c_int
+        L.oracle_resolve_capacity_type.argtypes = [C.POINTER(abi.GsProblem), C.POINTER(abi.GsClaimQuery),
+                                                   C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.oracle_resolve_capacity_type.restype = C.c_int
         L.oracle_go_sort_ints.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_uint32), C.c_uint32]
         _lib = L
     return _lib
@@ -180,3 +187,32 @@ def rank_instance_types(cpu_milli, memory_bytes, price, arch, want_arch=abi.GS_A
     """oracle_rank_instance_types -> (status, List indices ranked, scores)"""
     return abi.call_rank(lib().oracle_rank_instance_types, cpu_milli, memory_bytes, price, arch, want_arch,
                          min_cpu, min_memory_gb, max_price)
+
+
+def create_filter(problem):
+    """oracle_create_filter over problem.claim_queries -> (status, list like
+    gpusched.lib.Solver.create_filter)"""
+    nq, n = problem.n_claim_queries, len(problem.instance_types)
+    W = (n + 63) // 64
+    comp = (C.c_uint64 * max(1, nq * W))()
+    reqs = (C.c_uint64 * max(1, nq * W))()
+    sel = (C.c_int32 * max(1, nq))()
+    ct = (C.c_uint32 * max(1, nq))()
+    st = lib().oracle_create_filter(C.byref(problem.struct), problem.claim_queries, nq, comp, reqs, sel, ct)
+    if st != abi.GS_OK:
+        return st, None
+    out = []
+    for q in range(nq):
+        c = abi._bits(comp, q, W, n)
+        out.append(dict(compatible=c, requirements=abi._bits(reqs, q, W, n), n_compatible=len(c),
+                        selected=int(sel[q]), capacity_type=int(ct[q])))
+    return st, out
+
+
+def resolve_capacity_type(problem, query_index, its):
+    """ResolveCapacityType(claim, [catalog[i] for i in its]) -> (status, GS_CAPACITY_*)"""
+    arr = (C.c_uint32 * max(1, len(its)))(*its)
+    out = C.c_uint32(0)
+    st = lib().oracle_resolve_capacity_type(C.byref(problem.struct), C.byref(problem.claim_queries[query_index]),
+                                            arr, len(its), C.byref(out))
+    return st, int(out.value)

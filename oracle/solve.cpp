@@ -540,9 +540,10 @@ struct Builder {
   void check_range(gs_range r, uint32_t n, const char* what) {
     if ((uint64_t)r.begin + r.count > n) throw Unsupported{GS_E_INVALID, string("range out of bounds: ") + what};
   }
+  bool allow_placeholder = false;  // launch-time filter: hostname values are plain labels
   Req req_of(const gs_requirement& q) {
     if (q.op > GS_OP_LT) throw Unsupported{GS_E_UNSUPPORTED, "Gte/Lte operators"};
-    if (normalize_key(str(q.key)) == kHostname)
+    if (!allow_placeholder && normalize_key(str(q.key)) == kHostname)
       for (uint32_t i = 0; i < q.values.count && q.values.begin + i < p->n_value_ids; i++)
         if (str(p->value_ids[q.values.begin + i]).rfind("hostname-placeholder-", 0) == 0)
           throw Unsupported{GS_E_UNSUPPORTED, "requirement names a hostname placeholder"};
@@ -1559,5 +1560,105 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
   out->options = r.opts.data();
   out->option_prices = r.prices.data();
   out->chosen = chosen;
+  return GS_OK;
+}
+
+// ===================================================================== launch-time re-filter
+// CloudProvider.Create (reference pkg/cloudprovider/cloudprovider.go:320-346):
+//   reqs := NewNodeSelectorRequirementsWithMinValues(nodeClaim.Spec.Requirements...)
+//   compatible := lo.Filter(instanceTypes, reqs.Compatible(i.Requirements, AllowUndefinedWellKnownLabels) == nil
+//       && len(i.Offerings.Compatible(reqs).Available()) > 0 && resources.Fits(requests, i.Allocatable()))
+// GetInstanceTypes (:574-577): the requirement clause alone.
+// instance provider (vpc/instance/provider.go:215-221): instanceTypes[0].
+// ResolveCapacityType (common/capacitytype/capacitytype.go:27-42).
+namespace {
+
+struct CatalogOracle {
+  OracleState st;
+  Builder b;
+  explicit CatalogOracle(const gs_problem* p) : b{p, st} {
+    b.allow_placeholder = true;
+    for (uint32_t i = 0; i < p->n_strings; i++) st.strings.push_back(p->strings[i] ? p->strings[i] : "");
+    st.its.resize(p->n_instance_types);
+    for (uint32_t i = 0; i < p->n_instance_types; i++) {
+      auto& g = p->instance_types[i];
+      auto& it = st.its[i];
+      it.index = i;
+      it.name = b.str(g.name);
+      it.reqs = b.reqs_of(g.requirements);
+      it.capacity = b.res_of(g.capacity);
+      it.overhead = b.res_of(g.overhead);
+      it.allocatable = subtract(it.capacity, it.overhead);
+      b.check_range(g.offerings, p->n_offerings, "offerings");
+      for (uint32_t k = 0; k < g.offerings.count; k++) {
+        auto& o = p->offerings[g.offerings.begin + k];
+        it.offerings.push_back({b.reqs_of(o.requirements), o.price, o.available != 0});
+      }
+    }
+  }
+  // Offerings.Compatible(reqs).Available(), in offering order
+  static vector<const Offering*> available(const InstanceType& it, const Reqs& reqs) {
+    vector<const Offering*> out;
+    for (auto& o : it.offerings)
+      if (reqs.compatible(o.reqs, true) && o.available) out.push_back(&o);
+    return out;
+  }
+  static bool create_ok(const InstanceType& it, const Reqs& reqs, const Res& requests) {
+    const bool req_ok = reqs.compatible(it.reqs, true);
+    const bool off_ok = !available(it, reqs).empty();
+    const bool fit = fits(requests, it.allocatable);
+    return req_ok && off_ok && fit;
+  }
+  static uint32_t resolve_capacity_type(const Reqs& reqs, const vector<const InstanceType*>& its) {
+    const Req allowed = reqs.get(kCapacityType);
+    if (allowed.has("spot"))
+      for (auto* it : its)
+        for (auto* o : available(*it, reqs))
+          if (o->reqs.get(kCapacityType).has("spot")) return GS_CAPACITY_SPOT;
+    return GS_CAPACITY_ON_DEMAND;
+  }
+};
+
+}  // namespace
+
+extern "C" gs_status oracle_create_filter(const gs_problem* catalog, const gs_claim_query* qs, uint32_t nq,
+                                          uint64_t* compatible, uint64_t* requirements, int32_t* selected,
+                                          uint32_t* capacity_type) {
+  try {
+    CatalogOracle co(catalog);
+    const uint32_t N = catalog->n_instance_types, W = (N + 63) / 64;
+    for (uint32_t q = 0; q < nq; q++) {
+      const Reqs reqs = co.b.reqs_of(qs[q].requirements);
+      const Res requests = co.b.res_of(qs[q].requests);
+      vector<const InstanceType*> list;
+      for (uint32_t w = 0; w < W; w++) compatible[(size_t)q * W + w] = requirements[(size_t)q * W + w] = 0;
+      for (auto& it : co.st.its) {
+        if (reqs.compatible(it.reqs, true)) requirements[(size_t)q * W + it.index / 64] |= 1ull << (it.index % 64);
+        if (!CatalogOracle::create_ok(it, reqs, requests)) continue;
+        compatible[(size_t)q * W + it.index / 64] |= 1ull << (it.index % 64);
+        list.push_back(&it);
+      }
+      selected[q] = list.empty() ? -1 : (int32_t)list[0]->index;
+      capacity_type[q] = CatalogOracle::resolve_capacity_type(reqs, list);
+    }
+  } catch (const Unsupported& u) {
+    return u.code;
+  }
+  return GS_OK;
+}
+
+extern "C" gs_status oracle_resolve_capacity_type(const gs_problem* catalog, const gs_claim_query* q,
+                                                  const uint32_t* its, uint32_t n, uint32_t* out) {
+  try {
+    CatalogOracle co(catalog);
+    vector<const InstanceType*> list;
+    for (uint32_t i = 0; i < n; i++) {
+      if (its[i] >= co.st.its.size()) return GS_E_INVALID;
+      list.push_back(&co.st.its[its[i]]);
+    }
+    *out = CatalogOracle::resolve_capacity_type(co.b.reqs_of(q->requirements), list);
+  } catch (const Unsupported& u) {
+    return u.code;
+  }
   return GS_OK;
 }

@@ -152,3 +152,22 @@ def test_gpu_consolidation_c4_scale_invariants(solver):
     st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, sub, mode=abi.CONSOLIDATE_SINGLE))
     assert st == abi.GS_OK
     assert [cmds[i] for i in sub] == want
+
+
+@pytest.mark.gpu
+def test_gpu_consolidation_rerun_after_input_overwritten(solver):
+    """gs_consolidate copies what the reruns need (no borrowed
+    cluster / candidate pointers survive the call): scribbling over every
+    caller array afterwards leaves the rerun's commands unchanged"""
+    import numpy as np
+    p = _problem("c4", 3)
+    cin = ConsolidationInput(p, list(range(len(p.nodes))), mode=abi.CONSOLIDATE_SINGLE)
+    a = solver.consolidate(cin)[:3]
+    rng = np.random.default_rng(0)
+    for arr in (p.quantities, p.reqs, p.labels, p.offerings, p.instance_types, p.nodes, p.pods, p.bound_pods,
+                p.value_ids, p.bound_node, cin.candidates):
+        if len(arr):
+            raw = arr.view(np.uint8)
+            raw[:] = rng.integers(0, 256, size=raw.shape, dtype=np.uint8)
+    b = solver.consolidate_rerun()[:3]
+    assert a == b

@@ -113,3 +113,75 @@ def test_gpu_rank_kats_and_refusals():
     n = abi.GS_RANK_MAX + 1
     with pytest.raises(lib.GpuSchedError):
         lib.rank_instance_types([1000] * n, [GI] * n, [0.1] * n, [0] * n)
+
+
+def _kats():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")) as f:
+        return json.load(f)
+
+
+RANK_ORDER_CASES = _kats()["rank_orders"]["cases"]
+
+
+def _check_rank_order(case, order):
+    names = [t[0] for t in case["types"]]
+    got = [names[i] for i in order]
+    if "want" in case:
+        assert got == case["want"], case["name"]
+    if "want_first" in case:
+        assert got[0] == case["want_first"], case["name"]
+    if "want_set" in case:
+        assert sorted(got) == sorted(case["want_set"]), case["name"]
+
+
+def _rank_cols(case):
+    t = case["types"]
+    return [x[1] for x in t], [x[2] for x in t], [x[3] for x in t], [0] * len(t)
+
+
+@pytest.mark.parametrize("case", RANK_ORDER_CASES, ids=[c["name"] for c in RANK_ORDER_CASES])
+def test_rank_order_kats(case):
+    """rankInstanceTypes orders (instancetype_mock_test.go:221-361) through the oracle"""
+    st, order, _ = pyoracle.rank_instance_types(*_rank_cols(case))
+    assert st == abi.GS_OK
+    _check_rank_order(case, order)
+
+
+def test_score_zero_resources_kat():
+    k = _kats()["score_zero_resources"]  # instancetype_mock_test.go:372-383
+    assert pyoracle.lib().oracle_instance_score(k["cpu_milli"], k["memory_bytes"], k["price"]) == k["want"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", RANK_ORDER_CASES, ids=[c["name"] for c in RANK_ORDER_CASES])
+def test_gpu_rank_order_kats(case):
+    from gpusched import lib
+    order, score = lib.rank_instance_types(*_rank_cols(case))
+    _check_rank_order(case, order)
+    assert order == pyoracle.rank_instance_types(*_rank_cols(case))[1]
+
+
+@pytest.mark.gpu
+def test_gpu_rank_zero_resources_kat():
+    from gpusched import lib
+    _, score = lib.rank_instance_types([0], [0], [0.0], [0])
+    assert score == [_kats()["score_zero_resources"]["want"]]
+
+
+@pytest.mark.gpu
+def test_gpu_rank_runs_on_current_device():
+    """gs_rank_instance_types keeps one buffer per device and launches on the
+    calling thread's current device (ADVICE r1: rank.hip per-device buffers);
+    a gs_create on the last visible device makes it current."""
+    import torch
+    from gpusched import lib
+    n = torch.cuda.device_count()
+    cpu, mem, price, arch = catalog(3, 300)
+    want = pyoracle.rank_instance_types(cpu, mem, price, arch)[1]
+    for dev in sorted({0, n - 1}):
+        s = lib.Solver(device=dev)
+        assert lib.rank_instance_types(cpu, mem, price, arch)[0] == want
+        s.close()
+    assert lib.rank_instance_types(cpu, mem, price, arch)[0] == want
