@@ -261,12 +261,27 @@ def test_gpu_create_filter_after_solve(solver, seed):
     keeps at least one (the Solve only opens claims some option can launch)"""
     from gpusched import synth
     p = synth.random_problem(seed, n_pods=300, with_nodes=False, with_limits=False)
-    _, res = solver.solve(p)
+    res, _ = solver.solve(p)
     if not res["claims"]:
         pytest.skip("no claims")
     p2 = p.extended(lambda b: claim_queries_from_solve(p, res, b))
     got = solver.create_filter(p2)
     _same(got, pyoracle.create_filter(p2)[1])
     for c, g in zip(res["claims"], got):
+        assert set(g["compatible"]) <= set(c["its"])
+        assert g["n_compatible"] >= 1 and g["selected"] in c["its"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_create_filter_after_oracle_solve(seed):
+    """the same chain through the oracle alone (CPU)"""
+    from gpusched import synth
+    p = synth.random_problem(seed, n_pods=300, with_nodes=False, with_limits=False)
+    st, res, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK and res["claims"]
+    p2 = p.extended(lambda b: claim_queries_from_solve(p, res, b))
+    st, out = pyoracle.create_filter(p2)
+    assert st == abi.GS_OK
+    for c, g in zip(res["claims"], out):
         assert set(g["compatible"]) <= set(c["its"])
         assert g["n_compatible"] >= 1 and g["selected"] in c["its"]
