@@ -230,6 +230,9 @@ typedef struct gs_result {
   uint32_t words, n_templates, n_variants; /* encoded sizes: IT words, templates, pod variants */
   double t_encode_ms, t_upload_ms, t_feas_ms, t_ffd_ms, t_truncate_ms, t_fetch_ms, t_total_ms;
   double t_ffd_sort_ms, t_ffd_scan_ms, t_ffd_template_ms; /* in-kernel phase split of t_ffd_ms */
+  uint64_t claim_prefix;             /* in-flight NodeClaims a sequential first-fit visits (first feasible
+                                        position + 1, or all): the reference's NodeClaim.CanAdd calls */
+  uint64_t node_prefix;              /* ... and existing nodes (ExistingNode.CanAdd calls) */
 } gs_result;
 
 /* Static pod x offering feasibility (K1/K2): for every (pod, nodepool) the

@@ -443,6 +443,8 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->pops = c->ctrl.pops;
   out->cand_evals = c->ctrl.cand_evals;
   out->cand_full = c->ctrl.cand_full;
+  out->claim_prefix = c->ctrl.claim_prefix;
+  out->node_prefix = c->ctrl.node_prefix;
   out->t_ffd_sort_ms = c->ctrl.t_sort * 1e-5;  // wall_clock64 runs at 100 MHz
   out->t_ffd_scan_ms = c->ctrl.t_scan * 1e-5;
   out->t_ffd_template_ms = c->ctrl.t_tmpl * 1e-5;

@@ -17,6 +17,7 @@
 #include <numeric>
 #include <set>
 #include <stdexcept>
+#include <string_view>
 
 namespace gsh {
 namespace {
@@ -213,6 +214,20 @@ struct Ctx {
   }
   void chk(gs_range r, uint32_t n, const char* what) const {
     if ((uint64_t)r.begin + r.count > n) throw Fail{GS_E_INVALID, std::string("range out of bounds: ") + what};
+  }
+
+  // canonical string ids: the first id carrying each distinct text (callers
+  // may repeat a string under several ids)
+  std::vector<uint32_t> canon;
+  void build_canon() {
+    canon.resize(strs.size());
+    std::unordered_map<std::string_view, uint32_t> first;
+    first.reserve(strs.size() * 2);
+    for (uint32_t i = 0; i < strs.size(); i++) canon[i] = first.emplace(std::string_view(strs[i]), i).first->second;
+  }
+  uint32_t C(uint32_t id) const {
+    if (id >= canon.size()) throw Fail{GS_E_INVALID, "string id out of range"};
+    return canon[id];
   }
 
   // ---------------------------------------------------------- vocabulary
@@ -445,7 +460,16 @@ struct Ctx {
     if (e.Z * e.C > 64) throw Fail{GS_E_UNSUPPORTED, "zones x capacity types > 64"};
     // resources
     std::set<std::string> rn;
-    for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(S(p->quantities[i].resource));
+    {
+      std::vector<uint8_t> seen(strs.size(), 0);
+      for (uint32_t i = 0; i < p->n_quantities; i++) {
+        const uint32_t c = C(p->quantities[i].resource);
+        if (!seen[c]) {
+          seen[c] = 1;
+          rn.insert(strs[c]);
+        }
+      }
+    }
     e.res_names.assign(rn.begin(), rn.end());
     e.R = (uint32_t)e.res_names.size();
     if (e.R > (uint32_t)gsd::RMAX) throw Fail{GS_E_UNSUPPORTED, "more than 8 distinct resources"};
@@ -461,6 +485,11 @@ struct Ctx {
       e.res_name_ids.push_back(sid);
     }
     rid_map = rid;
+    rid_of_sid.assign(strs.size(), gsd::NONE);
+    for (uint32_t i = 0; i < strs.size(); i++) {
+      auto f = rid.find(strs[canon[i]]);
+      if (f != rid.end()) rid_of_sid[i] = f->second;
+    }
     auto resvec = [this](gs_range r, int64_t* out, bool* present) { resvec_fn(r, out, present); };
     // per IT arrays
     e.it_vid.assign((size_t)e.K * e.N, 0);
@@ -562,11 +591,14 @@ struct Ctx {
   }
   std::vector<uint64_t> it_ok;
   std::unordered_map<std::string, uint32_t> rid_map;
+  std::vector<uint32_t> rid_of_sid;  // string id -> resource index (NONE: not a resource)
   void resvec_fn(gs_range r, int64_t* out, bool* present) const {
     chk(r, p->n_quantities, "quantities");
     for (uint32_t k = 0; k < r.count; k++) {
       auto& q = p->quantities[r.begin + k];
-      uint32_t x = rid_map.at(S(q.resource));
+      if (q.resource >= rid_of_sid.size() || rid_of_sid[q.resource] == gsd::NONE)
+        throw Fail{GS_E_INVALID, "unknown resource"};
+      const uint32_t x = rid_of_sid[q.resource];
       out[x] += q.milli;
       if (present) present[x] = true;
     }
@@ -642,7 +674,6 @@ struct Ctx {
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
   std::vector<std::string> pod_ns;
-  std::vector<std::map<std::string, std::string>> pod_labels;
   std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
 
   std::map<std::string, std::string> label_map(gs_range r) const {
@@ -752,10 +783,11 @@ struct Ctx {
         }
       }
     }
-    for (uint32_t i = 0; i < e.P; i++) {
+    for (uint32_t i = 0; i < e.P && e.TG; i++) {
+      const auto labels_i = label_map(p->pods[i].labels);
       uint64_t sel = 0;
       for (uint32_t g = 0; g < e.TG; g++)
-        if (group_selects(groups[g], pod_ns[i], pod_labels[i])) sel |= 1ull << g;
+        if (group_selects(groups[g], pod_ns[i], labels_i)) sel |= 1ull << g;
       for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) e.vars[v].t_sel = sel;
     }
   }
@@ -966,14 +998,17 @@ struct Ctx {
 
   void build_pods() {
     e.P = p->n_pods;
-    std::unordered_map<std::string, uint32_t> uid_seen;
+    std::vector<uint8_t> uid_seen(strs.size(), 0);
+    e.variants.reserve((size_t)e.P + (e.P >> 2));
     e.pod_req.assign((size_t)e.P * e.R, 0);
     std::vector<int64_t> cpu(e.P, 0), mem(e.P, 0);
     auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
     for (uint32_t i = 0; i < e.P; i++) {
       auto& pd = p->pods[i];
       if (pd.flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
-      if (!uid_seen.emplace(S(pd.uid), i).second) throw Fail{GS_E_INVALID, "duplicate pod uid"};
+      const uint32_t cu = C(pd.uid);
+      if (uid_seen[cu]) throw Fail{GS_E_INVALID, "duplicate pod uid"};
+      uid_seen[cu] = 1;
       resvec_fn(pd.requests, &e.pod_req[(size_t)i * e.R], nullptr);
       if (rc != rid_map.end()) cpu[i] = e.pod_req[(size_t)i * e.R + rc->second];
       if (rmm != rid_map.end()) mem[i] = e.pod_req[(size_t)i * e.R + rmm->second];
@@ -992,7 +1027,7 @@ struct Ctx {
       std::stable_sort(pref.begin(), pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
       // topology spread constraints -> groups (owners); namespace / labels for selectors
       pod_ns.push_back(S(pd.ns));
-      pod_labels.push_back(label_map(pd.labels));
+      chk(pd.labels, p->n_labels, "labels");
       const std::vector<SpreadEnc> sps = spreads_of(pd);
       if (!sps.empty() && (pd.node_selector.count || pd.required_terms.count))
         for (auto& sp : sps)
@@ -1112,15 +1147,29 @@ struct Ctx {
     if (e.itmask.empty()) e.itmask.push_back(0);
     if (e.fk_entries.empty()) e.fk_entries.push_back(gsd::FKEntry{});
     // <U> NewQueue: cpu desc, memory desc, creationTimestamp asc, UID asc (total order)
-    e.queue0.resize(e.P);
-    std::iota(e.queue0.begin(), e.queue0.end(), 0);
-    std::sort(e.queue0.begin(), e.queue0.end(), [&](uint32_t a, uint32_t b) {
-      if (cpu[a] != cpu[b]) return cpu[a] > cpu[b];
-      if (mem[a] != mem[b]) return mem[a] > mem[b];
-      int64_t ta = p->pods[a].creation_ns, tb = p->pods[b].creation_ns;
-      if (ta != tb) return ta < tb;
-      return S(p->pods[a].uid) < S(p->pods[b].uid);
+    // sorted on packed keys: the UID's first 8 bytes (big-endian, so integer
+    // order is byte order) decide most ties without touching the strings
+    struct QK {
+      int64_t cpu, mem, ts;
+      uint64_t u8;
+      uint32_t i;
+    };
+    std::vector<QK> qk(e.P);
+    for (uint32_t i = 0; i < e.P; i++) {
+      const std::string& u = S(p->pods[i].uid);
+      uint64_t x = 0;
+      for (size_t b = 0; b < 8; b++) x = (x << 8) | (b < u.size() ? (uint8_t)u[b] : 0u);
+      qk[i] = QK{cpu[i], mem[i], p->pods[i].creation_ns, x, i};
+    }
+    std::sort(qk.begin(), qk.end(), [&](const QK& a, const QK& b) {
+      if (a.cpu != b.cpu) return a.cpu > b.cpu;
+      if (a.mem != b.mem) return a.mem > b.mem;
+      if (a.ts != b.ts) return a.ts < b.ts;
+      if (a.u8 != b.u8) return a.u8 < b.u8;
+      return strs[p->pods[a.i].uid] < strs[p->pods[b.i].uid];
     });
+    e.queue0.resize(e.P);
+    for (uint32_t k = 0; k < e.P; k++) e.queue0[k] = qk[k].i;
     e.checks = (uint64_t)e.P * e.checks_per_pod;
   }
 
@@ -1227,6 +1276,7 @@ Err encode(const gs_problem* p, Encoded& e) {
   try {
     c.strs.reserve(p->n_strings);
     for (uint32_t i = 0; i < p->n_strings; i++) c.strs.push_back(p->strings[i] ? p->strings[i] : "");
+    c.build_canon();
     c.build_vocab();
     c.build_catalog();
     c.build_templates();

@@ -79,7 +79,7 @@ struct Shared {
   uint32_t fast_path, modpos_sorted;
   uint32_t rot_lo, rot_hi;  // fast path: the one rotation partialInsertionSort performs
   int piv, hint;
-  uint64_t generic, fast, cand, cand_full, node_evals, node_prefix;
+  uint64_t generic, fast, cand, cand_full, node_evals, node_prefix, claim_prefix;
   uint32_t failed;
   uint64_t t_sort, t_scan, t_tmpl, t0;
   uint64_t dbg[16];
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       S.hb[0].nlog = 0;
       S.nov = ncand;
       S.qoff = qoff;
-      S.hb[0].pops = S.generic = S.fast = S.cand = S.cand_full = S.node_evals = S.node_prefix = 0;
+      S.hb[0].pops = S.generic = S.fast = S.cand = S.cand_full = S.node_evals = S.node_prefix = S.claim_prefix = 0;
       S.failed = 0;
       S.t_sort = S.t_scan = S.t_tmpl = 0;
       for (int q = 0; q < 16; q++) S.dbg[q] = S.tl[q] = 0;
@@ -1494,6 +1494,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       pf_stage3();
       TL(9);  // reduction + winner update
       if (tid == 0) {
+        S.claim_prefix += f != INF ? f + 1 : M;
         const uint64_t tB = phase_clock();
         S.t_scan += tB - tA;
         S.dbg[14] = tB;
@@ -1760,6 +1761,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       c.cand_full = S.cand_full;
       c.node_evals = S.node_evals;
       c.node_prefix = S.node_prefix;
+      c.claim_prefix = S.claim_prefix;
       c.failed = S.failed;
       c.pad = 0;
       c.t_sort = S.t_sort;

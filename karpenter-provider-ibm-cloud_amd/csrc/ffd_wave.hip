@@ -576,7 +576,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   bool wrapped = false;
   uint64_t pops = 0;
   // instrumentation counters, lane k = counter k (no scalar registers)
-  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA };
+  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG };
   uint64_t ctr = 0;
 #define CTR(k, x) (ctr += lane == (k) ? (uint64_t)(x) : 0ull)
   const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
@@ -1161,6 +1161,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       scan_from = resume;
     }
     if (__ballot(ovf)) status = 3;
+    CTR(C_ALG, f != INF ? f + 1 : M);  // the reference's NodeClaim.CanAdd calls
     TLW(3);  // scan + Add
 #ifdef GS_FFD_TL
     n_fsum += f != INF ? f : 0;
@@ -1412,7 +1413,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   }
   auto ctr_at = [&](uint32_t k) -> uint64_t { return (uint64_t)rlane((uint32_t)ctr, k) | ((uint64_t)rlane((uint32_t)(ctr >> 32), k) << 32); };
   const uint64_t ctr_gen = ctr_at(C_GEN), ctr_fast = ctr_at(C_FAST), ctr_cand = ctr_at(C_CAND), ctr_full = ctr_at(C_FULL),
-                 ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA);
+                 ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA), ctr_alg = ctr_at(C_ALG);
   if (lane == 0) {
     Ctrl c = {};
     c.status = status;
@@ -1428,6 +1429,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.cand_full = ctr_full;
     c.node_evals = ctr_nev;
     c.node_prefix = ctr_npre;
+    c.claim_prefix = ctr_alg;
     c.dbg[15] = ctr_fa;
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];

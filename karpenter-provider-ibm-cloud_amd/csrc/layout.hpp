@@ -13,6 +13,17 @@
 #include <stdint.h>
 #include <stddef.h>
 
+// host-only builds of the encoder (g++ with sanitizers, tools/encode_harness.cpp)
+// see the shared records without the HIP function attributes
+#ifndef __HIPCC__
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
 namespace gsd {
 
 constexpr int RMAX = 8;        // resource dimensions per vector
@@ -147,6 +158,7 @@ struct Ctrl {
   uint64_t cand_full;    // candidates that passed the slack prefilter
   uint64_t node_evals;   // existing-node ExistingNode.CanAdd evaluations (whole scan chunks)
   uint64_t node_prefix;  // node positions a sequential first-fit visits (found index + 1, or all)
+  uint64_t claim_prefix; // in-flight NodeClaims a sequential first-fit visits (the reference's CanAdd calls)
   uint32_t failed;       // simulations: non-pending pods unplaced or placed on uninitialized nodes
   uint32_t pad;
   uint64_t t_sort, t_scan, t_tmpl, t_total;  // wall_clock64 ticks (100 MHz) per phase

@@ -103,6 +103,7 @@ class GsResult(C.Structure):
         ("t_ffd_ms", C.c_double), ("t_truncate_ms", C.c_double), ("t_fetch_ms", C.c_double),
         ("t_total_ms", C.c_double),
         ("t_ffd_sort_ms", C.c_double), ("t_ffd_scan_ms", C.c_double), ("t_ffd_template_ms", C.c_double),
+        ("claim_prefix", C.c_uint64), ("node_prefix", C.c_uint64),
     ]
 
 

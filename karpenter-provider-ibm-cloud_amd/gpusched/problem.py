@@ -217,6 +217,22 @@ class Problem:
             setattr(st, "n_" + name, len(arr))
         st.bound_pod_node = self.bound_node.ctypes.data if len(self.bound_node) else None
 
+    _DUMP_ARRAYS = ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
+                    "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods", "bound_node")
+
+    def dump(self, path):
+        """binary dump read by tools/encode_harness.cpp (host-only encoder
+        runs: sanitizers, profiling)"""
+        import struct
+        with open(path, "wb") as f:
+            f.write(b"GSPD" + struct.pack("<II", 1, len(self._bytes)))
+            for s in self._bytes:
+                f.write(struct.pack("<I", len(s)) + s)
+            for name in self._DUMP_ARRAYS:
+                a = np.ascontiguousarray(getattr(self, name))
+                f.write(struct.pack("<QQ", len(a), a.dtype.itemsize))
+                f.write(a.tobytes())
+
     def with_pods(self, idx):
         """a view with pending pods pods[idx] (same pools: requirement, label
         and quantity ranges stay valid) — e.g. an oracle check on a sample of

@@ -975,11 +975,13 @@ struct Scheduler {
     return true;
   }
 
+  uint64_t claim_calls = 0, node_calls = 0;  // CanAdd calls (instrumentation)
   bool add(Pod& pod) {
     for (uint32_t ni : st.node_order) {
       auto& n = st.nodes[ni];
       Reqs r;
       Res q;
+      node_calls++;
       if (node_can_add(n, pod, &r, &q)) {
         n.reqs = std::move(r);
         n.requests = std::move(q);
@@ -999,6 +1001,7 @@ struct Scheduler {
       Reqs r;
       vector<const InstanceType*> its;
       Res q;
+      claim_calls++;
       if (claim_can_add(*nc, pod, &r, &its, &q)) {
         nc->reqs = std::move(r);
         nc->options = std::move(its);
@@ -1178,6 +1181,8 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   out->n_errors = (uint32_t)r.error_pods.size();
   out->error_pods = r.error_pods.data();
   out->pops = s.pops;
+  out->claim_prefix = s.claim_calls;
+  out->node_prefix = s.node_calls;
   out->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GS_OK;
 }

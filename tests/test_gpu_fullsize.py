@@ -54,8 +54,9 @@ def _case(name):
     if name not in _cache:
         p = {"cm_100k": synth.make_cm, "c3_50k": synth.make_c3,
              "c5_50k": lambda: synth.make_c5(n_pods=50_000)}[name]()
-        st, want, _ = pyoracle.solve(p)
+        st, want, raw = pyoracle.solve(p)
         assert st == abi.GS_OK
+        want["_calls"] = (int(raw.claim_prefix), int(raw.node_prefix))
         _cache.clear()  # one full-size problem resident at a time
         _cache[name] = (p, want)
     return _cache[name]
@@ -72,8 +73,11 @@ def _compare(got, want):
 @pytest.mark.parametrize("name", ["cm_100k", "c3_50k", "c5_50k"])
 def test_fullsize_solve_matches_live_oracle(solver, name):
     p, want = _case(name)
-    got, _ = solver.solve(p)
+    got, raw = solver.solve(p)
     _compare(got, want)
+    # the kernels' first-fit counters equal the reference's CanAdd calls
+    # (the roofline's algorithmic bytes are priced on them)
+    assert (int(raw.claim_prefix), int(raw.node_prefix)) == want["_calls"]
     if name in gold():
         assert digest(got) == gold()[name]["sha256"]
 
