@@ -2,25 +2,33 @@
 """bench.py — BASELINE.json metric on MI355X:
 pod x offering feasibility checks/sec + Solve latency (ms), 100k pods.
 
-Headline (`value`): a step = one device-resident provisioning Solve of the CM
-workload through the C-ABI (gs_run: K1/K2 feasibility -> K4 first-fit-
-decreasing -> K3 OrderByPrice/Truncate(60)); encode + host->HBM upload happen
-once before the timed region and are reported separately.  checks per step =
-pods x offerings reachable from the NodePool.  The Solve is
-sequential in pod order, so --gpus N runs N independent replicas (one
-independent cluster's Solve per rank, no data-path collective): weak scaling;
-value = sum of checks over ranks / max step time.
+Headline (`value`, `ms_per_step`): a step = one provisioning Solve of the CM
+workload (BASELINE configs[1]) through the C-ABI with the problem resident in
+HBM (gs_run: K1/K2 feasibility -> K4 first-fit-decreasing -> K3
+OrderByPrice/Truncate(60)); checks per step = pods x offerings reachable from
+the NodePool.  `solve_latency_ms` is §8(d)'s latency: the wall
+clock of complete gs_solve calls (encode + H2D + kernels + D2H + decode into
+the result memory), timed separately over the same workload; the device-only
+step is `device_ms_per_step`.  The Solve is sequential in pod order, so
+--gpus N runs N independent replicas (one cluster's Solve per rank, no
+data-path collective): weak scaling; value = sum of checks over ranks / max
+step time.
 
-`consolidation`: the C4 workload (BASELINE configs[3]): a SingleNodeConsolidation
-sweep over all 5,000 state nodes, each an independent SimulateScheduling Solve
-(one workgroup per simulation).  Simulations are sharded round-robin over the
-N ranks, their commands all-gathered (RCCL over xGMI), and the policy replayed
-on every rank: strong scaling.
-
-`stress`: the C5 workload (BASELINE configs[4]): the static pod x offering
-matrix of 200k pods x 2,000 instance types x 6 zones x 2 capacity types with
-instance-type columns sharded over the ranks and combined by RCCL all-reduces
-(SUM rows / SUM offering counts / MIN OrderByPrice key): strong scaling.
+Every BASELINE config has a leg with its own roofline and CPU baseline:
+  configs.C1/C2/C3  provisioning Solve legs (same step definition as CM)
+  consolidation     C4: SingleNodeConsolidation over 5,000 state nodes
+                    (sharded round-robin over ranks, commands all-gathered
+                    over RCCL, policy replayed: strong scaling), plus a packed
+                    C4 variant with mixed Delete/Replace/NoOp decisions and a
+                    MultiNodeConsolidation leg (binary-search prefixes)
+  stress            C5: the static pod x offering matrix, 200k pods x 24,000
+                    offerings, instance-type words sharded over ranks
+  create_filter     the launch-time re-filter of every CM NodeClaim
+  ranking           autoplacement ranking over a C5-sized catalog
+The CPU baselines run the oracle (oracle/, a C++ restatement of the
+reference algorithm) on the GPU box's host: Solve legs on the full config
+(1 thread: the Solve is sequential), consolidation on a bounded candidate
+sample with 1 and `pool` worker processes.
 """
 import argparse
 import json
@@ -36,34 +44,30 @@ sys.path.insert(0, ROOT)
 
 from gpusched import abi, synth  # noqa: E402
 from gpusched.consolidation import (ConsolidationInput, arrays_to_list, choose_arrays, gather_arrays,  # noqa: E402
-                                    result_arrays)
+                                    n_multi_sims, result_arrays)
 from gpusched.lib import Solver  # noqa: E402
 
 METRIC = "pod×offering feasibility checks/sec + Solve latency (ms) at 100k pods, 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+CM_WORKLOAD = ("CM: 100k pods x C2 synthetic IBM VPC catalog (198 profiles x 3 zones x {on-demand, spot} = "
+               "1,188 offerings), 1 NodePool, 1% GPU pods, 10% nodeSelectors")
 
 
-def algorithmic_bytes(res, problem, n_claims):
-    """per-launch ALGORITHMIC bytes from the run's counters"""
-    V, T, W = res.n_variants, res.n_templates, res.words
-    R = res.n_resources
-    O = len(problem.offerings)
-    N = len(problem.instance_types)
-    feas = V * 128 + O * 48 + V * T * (W * 8 + 12)
-    per_cand = 24 + W * 8 * (2 + R) + R * 8      # header, opts, row, R threshold sets, totals
-    per_pop = R * 8 + 96                          # pod requests + variant record
-    adds = len(problem.pods) - res.n_errors
-    per_add = W * 8 + R * 8 + 24 + 16             # claim update + add-log record
-    ffd = res.pops * per_pop + res.cand_evals * per_cand + adds * per_add
-    trunc = n_claims * (W * 8 + 24 + 60 * 4) + N * 16
-    return {"feas": feas, "ffd": ffd, "trunc": trunc}
+# ------------------------------------------------------------------ roofline
+def ffd_bytes(res, n_types):
+    """SURVEY §8(d) K4 algorithmic bytes per launch: per pod Σ_in-flight
+    ⌈N_IT/8⌉ (the option bitset of every NodeClaim a sequential first fit
+    visits: res.claim_prefix, pinned equal to the oracle's NodeClaim.CanAdd
+    calls by tests/test_gpu_fullsize.py) + 32 B of request sums per pop +
+    40 B per existing node visited (res.node_prefix)"""
+    return int(res.claim_prefix) * ((n_types + 7) // 8) + 32 * int(res.pops) + 40 * int(res.node_prefix)
 
 
-def load_traffic(path):
-    """{kernel: HBM bytes per launch} from the committed PMC profile (null when absent)"""
-    if not path or not os.path.exists(path):
-        return {}
-    return {k: v["bytes"] for k, v in json.load(open(path)).items()}
+def feas_bytes(V, T, O, words):
+    """per-launch algorithmic bytes of feas_kernel over `words` instance-type
+    words: variant records (128 B), the offering list (48 B), rows + cheapest
+    key + offering count written per (variant, template)"""
+    return V * 128 + O * 48 + V * T * (words * 8 + 12)
 
 
 def node_check_bytes(R, K=4):
@@ -72,64 +76,201 @@ def node_check_bytes(R, K=4):
     return 16 * R + 8 + 4 + 4 * K + 8
 
 
-def cpu_baseline(n_pods):
-    """oracle (C++ port of the reference algorithm, 1 thread) on a bounded
-    sample of the same workload; also checks the GPU result on that sample"""
-    from oracle import pyoracle
-    problem = synth.make_cm(n_pods=n_pods)
+def load_traffic(path):
+    """{leg: {kernel: HBM bytes per launch}} from the committed PMC profile (empty when absent)"""
+    if not path or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
+def traffic_of(traffic, leg, kernel):
+    x = traffic.get(leg, {}).get(kernel)
+    return x["bytes"] if isinstance(x, dict) else x
+
+
+def roofline(kernel, algo_bytes, avg_ms, traffic=None):
+    ach = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(algo_bytes), "avg_ms": round(avg_ms, 4),
+            "traffic": traffic}
+
+
+def digest(res_dict):
+    import hashlib
+    return hashlib.sha256(json.dumps(res_dict, sort_keys=True, separators=(",", ":")).encode()).hexdigest()
+
+
+# ------------------------------------------------------------- Solve legs
+def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_over_ranks=None, traffic=None,
+              leg=None):
+    """device-resident steps (gs_run) and complete gs_solve calls on one problem"""
     t0 = time.perf_counter()
-    st, want, _ = pyoracle.solve(problem)
-    dt = time.perf_counter() - t0
-    s = Solver(0)
+    solver.prepare(problem)
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(warmup):
+        solver.run()
+    kt = []
+    if barrier:
+        barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solver.run()  # synchronous: returns after the stream's last event
+        kt.append(solver.last_run_ms())
+    if barrier:
+        barrier()
+    elapsed = time.perf_counter() - t0
+    if max_over_ranks:
+        elapsed = max_over_ranks(elapsed)
+    t1 = time.perf_counter()
+    out, res = solver.fetch()
+    fetch_py_ms = (time.perf_counter() - t1) * 1e3
+    # §8(d) latency: whole gs_solve calls, C-ABI wall clock (no Python-side copy)
+    lat, phases = [], []
+    for _ in range(latency_steps):
+        t2 = time.perf_counter()
+        r = solver.solve_raw(problem)
+        lat.append((time.perf_counter() - t2) * 1e3)
+        phases.append((r.t_encode_ms, r.t_upload_ms, r.t_feas_ms, r.t_ffd_ms, r.t_truncate_ms, r.t_fetch_ms))
+    kms = {k: sum(x[i] for x in kt) / len(kt) for i, k in enumerate(("feas", "ffd", "trunc"))}
+    n_types = len(problem.instance_types)
+    ab = {"feas": feas_bytes(res.n_variants, res.n_templates, len(problem.offerings), res.words),
+          "ffd": ffd_bytes(res, n_types)}
+    names = {"feas": "feas_kernel", "ffd": "ffdw_kernel" if solver.flags == 0 and len(problem.nodes) <= 512
+             else "ffd_kernel"}
+    ph = np.mean(np.array(phases), axis=0) if phases else np.zeros(6)
+    return {
+        "ms_per_step": elapsed * 1e3 / steps,
+        "checks": problem.checks(),
+        "device_kernel_ms": {k: round(v, 4) for k, v in kms.items()},
+        "solve_latency_ms": round(float(np.mean(lat)), 3) if lat else None,
+        "solve_latency_ms_each": [round(x, 2) for x in lat],
+        "solve_latency_phases_ms": {"encode": round(ph[0], 2), "upload": round(ph[1], 2), "feas": round(ph[2], 3),
+                                    "ffd": round(ph[3], 2), "truncate": round(ph[4], 3),
+                                    "fetch_decode": round(ph[5], 2)},
+        "prepare_ms_first_call": round(prep_ms, 2),
+        "python_result_copy_ms": round(fetch_py_ms, 2),
+        "new_nodeclaims": len(out["claims"]),
+        "pod_errors": len(out["errors"]),
+        "queue_pops": int(res.pops),
+        "first_fit_claim_visits": int(res.claim_prefix),
+        "first_fit_node_visits": int(res.node_prefix),
+        "ffd_candidates_scanned": int(res.cand_evals),
+        "ffd_candidates_exact_checked": int(res.cand_full),
+        "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
+        "roofline": roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        "roofline_feasibility_kernel": roofline("feas_kernel", ab["feas"], kms["feas"],
+                                                traffic_of(traffic or {}, leg, "feas")),
+        "_result": out,
+    }
+
+
+def cpu_baseline_solve(problem, got):
+    """the oracle's Solve (1 thread) on the SAME full problem; its own input
+    build is reported apart from the Solve, like the product's encode"""
+    from oracle import pyoracle
+    t0 = time.perf_counter()
+    st, want, raw = pyoracle.solve(problem)
+    wall = (time.perf_counter() - t0) * 1e3
+    build_ms = float(raw.t_encode_ms)
+    solve_ms = wall - build_ms
+    return {"value": problem.checks() / (solve_ms * 1e-3), "unit": "checks/s", "cores": 1, "kind": "port",
+            "sample": f"full problem ({len(problem.pods)} pods); oracle Solve {solve_ms:.0f} ms + its input build "
+                      f"{build_ms:.0f} ms = {wall:.0f} ms wall (the Solve is sequential: 1 thread)",
+            "solve_ms": round(solve_ms, 1), "wall_ms": round(wall, 1),
+            "gpu_result_bit_exact": bool(st == abi.GS_OK and got == want)}
+
+
+def config_leg(name, problem, args, traffic):
+    solver = Solver(0)
     try:
-        got, _ = s.solve(problem)
+        r = solve_leg(problem, solver, max(1, min(args.steps, 5)), 1, args.latency_steps, traffic=traffic, leg=name)
     finally:
-        s.close()
-    return {
-        "value": problem.checks() / dt,
-        "unit": "checks/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"CM distribution, first {n_pods} pods (same C2 catalog, 1 NodePool); oracle Solve "
-                  f"{dt * 1e3:.0f} ms; GPU result on the sample bit-exact: {got == want}",
-        "solve_ms": dt * 1e3,
-    }
+        solver.close()
+    got = r.pop("_result")
+    r["value"] = r["checks"] / (r["ms_per_step"] * 1e-3)
+    r["unit"] = "checks/s"
+    r["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_solve(problem, got)
+    return r
 
 
-def cpu_baseline_consolidation(problem, cmds, n_sample):
-    """oracle SingleNodeConsolidation simulations (1 thread) on a bounded sample
-    of the candidates; checks the GPU commands on that sample"""
+# ------------------------------------------------------- consolidation legs
+_POOL = None  # worker processes, forked before this process touches the GPU
+_WORKER_PROBLEMS = {}
+
+
+def c4_problem(spec):
+    """spec = (n_nodes, generator kwargs): workers rebuild the cluster
+    themselves (deterministic generator) instead of inheriting GPU-process state"""
+    key = json.dumps(spec, sort_keys=True)
+    if key not in _WORKER_PROBLEMS:
+        _WORKER_PROBLEMS.clear()
+        _WORKER_PROBLEMS[key] = synth.make_c4(n_nodes=spec[0], **spec[1])
+    return _WORKER_PROBLEMS[key]
+
+
+def _oracle_chunk(job):
+    spec, cands, mode, sets = job
     from oracle import pyoracle
-    n = len(problem.nodes)
+    cin = ConsolidationInput(c4_problem(spec), cands, mode=mode, sets=sets)
+    st, cmds, _, _ = pyoracle.consolidate(cin)
+    return st, cmds
+
+
+def _warm(spec):
+    c4_problem(spec)
+    return True
+
+
+def oracle_consolidation_timed(spec, jobs, workers):
+    """oracle consolidation jobs on 1 process (here) or on the pool's
+    `workers` processes (the oracle keeps global state: processes, not
+    threads); the clusters are built before the clock starts"""
+    if workers <= 1 or _POOL is None:
+        c4_problem(spec)
+        t0 = time.perf_counter()
+        outs = [_oracle_chunk(j) for j in jobs]
+    else:
+        _POOL.map(_warm, [spec] * workers * 2, chunksize=1)
+        t0 = time.perf_counter()
+        outs = _POOL.map(_oracle_chunk, jobs, chunksize=1)
+    return time.perf_counter() - t0, outs
+
+
+def cpu_baseline_single(spec, n, cmds, n_sample, workers):
+    """oracle SingleNodeConsolidation simulations on an evenly spaced sample
+    of the candidates, 1 process and `workers` processes; the GPU commands are
+    compared on the sample"""
     sub = list(range(0, n, max(1, n // n_sample)))[:n_sample]
-    t0 = time.perf_counter()
-    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(problem, sub, mode=abi.CONSOLIDATE_SINGLE))
-    dt = time.perf_counter() - t0
-    return {
-        "value": len(sub) / dt,
-        "unit": "simulations/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"C4 cluster, {len(sub)} evenly spaced single-node candidates; oracle {dt * 1e3:.0f} ms; "
-                  f"GPU commands on the sample identical: {st == 0 and [cmds[i] for i in sub] == want}",
-    }
+    one = sub[:max(1, len(sub) // max(workers, 1))]
+    t1, o1 = oracle_consolidation_timed(spec, [(spec, one, abi.CONSOLIDATE_SINGLE, None)], 1)
+    chunks = [sub[i::workers] for i in range(workers)]
+    tw, ow = oracle_consolidation_timed(spec, [(spec, c, abi.CONSOLIDATE_SINGLE, None) for c in chunks if c],
+                                        workers)
+    want = {}
+    for c, (st, out) in zip([c for c in chunks if c], ow):
+        for i, cmd in zip(c, out or []):
+            want[i] = cmd
+    same = all(cmds[i] == want.get(i) for i in sub)
+    return {"value": len(sub) / tw, "unit": "simulations/s", "cores": workers, "kind": "port",
+            "value_1_core": len(one) / t1,
+            "sample": f"{len(sub)} evenly spaced single-node candidates on {workers} processes ({tw:.1f} s); "
+                      f"{len(one)} of them on 1 process ({t1:.1f} s); GPU commands on the sample identical: {same}"}
 
 
-def bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks):
-    problem = synth.make_c4(n_nodes=args.c4_nodes)
+def consolidation_leg(problem, mode, args, rank, world, local, dist, device, barrier, max_over_ranks, traffic, leg,
+                      max_candidates=0):
     n = len(problem.nodes)
     cands = list(range(n))
     shard = (rank, world) if world > 1 else (0, 0)
-    cin = ConsolidationInput(problem, cands, mode=abi.CONSOLIDATE_SINGLE, shard=shard)
-    full = ConsolidationInput(problem, cands, mode=abi.CONSOLIDATE_SINGLE)
+    cin = ConsolidationInput(problem, cands, mode=mode, shard=shard, max_candidates=max_candidates)
+    full = ConsolidationInput(problem, cands, mode=mode, max_candidates=max_candidates)
     solver = Solver(local)
     t0 = time.perf_counter()
-    cmds, _, _, res = solver.consolidate(cin)  # encode + upload + first run
+    solver.consolidate(cin)  # encode + upload + first run
     prep_ms = (time.perf_counter() - t0) * 1e3
 
     def sweep():
-        # device simulations + host decisions, then (N > 1) the all-gather of
-        # every rank's commands and the policy replay
         r = solver.consolidate_rerun(raw=True)
         if world == 1:
             return None, int(r.chosen), r
@@ -140,95 +281,92 @@ def bench_consolidation(args, rank, world, local, dist, device, barrier, max_ove
     for _ in range(args.warmup):
         sweep()
     kt = []
+    steps = args.steps
     barrier()
     t0 = time.perf_counter()
-    steps_ms = []
-    for _ in range(args.steps):
-        ts = time.perf_counter()
+    for _ in range(steps):
         merged, chosen, r = sweep()
-        steps_ms.append((time.perf_counter() - ts) * 1e3)
         kt.append((r.t_feas_ms, r.t_sim_ms, r.t_truncate_ms, r.t_fetch_ms))
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     if merged is None:
         merged = result_arrays(r)
     merged = arrays_to_list(*merged)
-    ms = elapsed * 1e3 / args.steps
-    feas_ms = sum(k[0] for k in kt) / len(kt)
-    sim_ms = sum(k[1] for k in kt) / len(kt)
-    trunc_ms = sum(k[2] for k in kt) / len(kt)
-    decide_ms = sum(k[3] for k in kt) / len(kt)
-    R = len(set(int(x) for x in problem.quantities["resource"]))  # encoded resource dimensions
+    ms = elapsed * 1e3 / steps
+    feas_ms, sim_ms, trunc_ms, decide_ms = (sum(k[i] for k in kt) / len(kt) for i in range(4))
+    R = len(set(int(x) for x in problem.quantities["resource"]))
     nb = node_check_bytes(R)
-    # per-launch algorithmic bytes of the simulation kernel on THIS rank: the
-    # node records a sequential first-fit visits + per pop (variant record
-    # 104 B + requests 8R) + per simulation (candidate ids, control block)
-    n_local = (n + world - 1) // world
+    n_sims = len(merged)
+    n_local = (n_sims + world - 1) // world
     sim_bytes = r.node_prefix * nb + r.pops * (104 + 8 * R) + n_local * 256
-    ach = sim_bytes / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else 0.0
     counts = {}
     for c in merged:
         k = abi.DECISION_NAMES[c["decision"]]
         counts[k] = counts.get(k, 0) + 1
     out = {
-        "workload": f"C4: {n} state nodes (C2 catalog, 2 NodePools, 60-90% cpu used, {len(problem.bound_pods)} "
-                    f"bound pods), SingleNodeConsolidation over all {n} candidates",
-        "simulations": n,
-        "value": n / (ms * 1e-3),
+        "mode": {abi.CONSOLIDATE_SINGLE: "SingleNodeConsolidation",
+                 abi.CONSOLIDATE_MULTI: "MultiNodeConsolidation"}[mode],
+        "simulations": n_sims,
+        "value": n_sims / (ms * 1e-3),
         "unit": "simulations/s",
         "ms_per_sweep": ms,
         "scaling": "strong",
         "node_checks_per_s": r.checks * world / (ms * 1e-3),
         "kernel_ms": {"feas": round(feas_ms, 4), "sim": round(sim_ms, 4), "trunc": round(trunc_ms, 4)},
         "host_decide_fetch_ms": round(decide_ms, 3),
-        "sweep_ms_each": [round(x, 3) for x in steps_ms],
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "pods_simulated": int(r.pods_simulated),
-        "node_evals": int(r.node_evals),
         "node_prefix": int(r.node_prefix),
         "chosen": chosen,
         "decisions": counts,
-        "roofline": {"kernel": "ffd_kernel<SIM>", "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(sim_bytes),
-                     "avg_ms": round(sim_ms, 4), "traffic": load_traffic(args.traffic_json).get("sim")},
+        "roofline": roofline("ffd_kernel<SIM>", sim_bytes, sim_ms, traffic_of(traffic, leg, "sim")),
         "cpu_baseline": None,
+        "_commands": merged,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_consolidation(problem, merged, args.cpu_sample_sims)
     solver.close()
     return out
 
 
-def feas_bytes(V, T, O, words):
-    """per-launch algorithmic bytes of feas_kernel over `words` instance-type
-    words: variant records, the offering list, rows + counts + keys written"""
-    return V * 128 + O * 48 + V * T * (words * 8 + 12)
+def cpu_baseline_multi(spec, n, cmds, n_prefixes, workers):
+    """oracle MultiNodeConsolidation prefix simulations (the binary search's
+    candidates[0:mid+1]) on a sample of prefix lengths, as EVAL sets, on
+    `workers` processes; GPU commands compared on the sample"""
+    n_sims = len(cmds)
+    mids = sorted(set(int(x) for x in np.linspace(0, n_sims - 1, n_prefixes)))
+    cands = list(range(n))
+    jobs = [(spec, cands, abi.CONSOLIDATE_EVAL, [(0, m + 2)]) for m in mids]
+    tw, outs = oracle_consolidation_timed(spec, jobs, workers)
+    same = all(st == abi.GS_OK and out and out[0] == cmds[m] for m, (st, out) in zip(mids, outs))
+    return {"value": len(mids) / tw, "unit": "simulations/s", "cores": workers, "kind": "port",
+            "sample": f"{len(mids)} prefix simulations (lengths {[m + 2 for m in mids]}) on {workers} processes "
+                      f"({tw:.1f} s); GPU commands on the sample identical: {same}"}
 
 
-def cpu_baseline_stress(n_pods):
-    """oracle static matrix (1 thread) on the first n_pods of the C5 workload;
+# ---------------------------------------------------------------- C5 stress
+def cpu_baseline_stress(problem, n_pods):
+    """oracle static matrix (1 thread) on an evenly spaced pod sample of C5;
     checks the GPU matrix on that sample"""
     from oracle import pyoracle
-    problem = synth.make_c5(n_pods=n_pods)
+    idx = np.linspace(0, len(problem.pods) - 1, n_pods).astype(np.int64)
+    sub = problem.with_pods(idx)
     t0 = time.perf_counter()
-    st, want = pyoracle.feasibility(problem)
+    st, want = pyoracle.feasibility(sub)
     dt = time.perf_counter() - t0
     s = Solver(0)
     try:
-        s.prepare(problem)
+        s.prepare(sub)
         got, _ = s.feasibility()
     finally:
         s.close()
     same = all(np.array_equal(got[k], want[k]) for k in ("rows", "cheapest", "n_feasible_offerings"))
-    return {"value": problem.checks() / dt, "unit": "checks/s", "cores": 1, "kind": "port",
-            "sample": f"C5, first {n_pods} pods; oracle static matrix {dt * 1e3:.0f} ms; GPU matrix on the "
+    return {"value": sub.checks() / dt, "unit": "checks/s", "cores": 1, "kind": "port",
+            "sample": f"C5, {n_pods} evenly spaced pods; oracle static matrix {dt * 1e3:.0f} ms; GPU matrix on the "
                       f"sample bit-exact: {bool(same)}"}
 
 
-def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks):
-    """C5 (BASELINE configs[4]): the static pod x offering matrix of 200k pods x
-    2,000 types x 6 zones x 2 capacity types, instance-type words sharded over
-    the ranks and combined in place by three RCCL all-reduces: strong scaling"""
+def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks, traffic):
+    """C5 (BASELINE configs[4]): the static pod x offering matrix, instance-type
+    words sharded over the ranks and combined in place by RCCL: strong scaling"""
     from gpusched.feasibility import device_combine, word_range
     problem = synth.make_c5(n_pods=args.c5_pods)
     solver = Solver(local)
@@ -270,7 +408,6 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
                      torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]))
         equal = bool(max_over_ranks(0.0 if equal else 1.0) == 0.0)
     ab = feas_bytes(r.n_variants, r.n_templates, len(problem.offerings), we - wb)
-    ach = ab / (k_ms * 1e-3) / 1e9
     out = {
         "workload": f"C5: {len(problem.pods)} pods x {len(problem.instance_types)} instance types x 6 zones x "
                     f"2 capacity types ({len(problem.offerings)} offerings), static feasibility matrix + cheapest "
@@ -285,24 +422,21 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
         "kernel_ms": round(k_ms, 4),
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "shards_equal_whole": equal,
-        "roofline": {"kernel": "feas_kernel", "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(ab),
-                     "avg_ms": round(k_ms, 4), "traffic": load_traffic(args.traffic_json).get("feas_c5")},
+        "roofline": roofline("feas_kernel", ab, k_ms, traffic_of(traffic, "c5", "feas")),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_stress(args.cpu_sample_c5_pods)
+        out["cpu_baseline"] = cpu_baseline_stress(problem, args.cpu_sample_c5_pods)
     solver.close()
     return out
 
 
+# ------------------------------------------------------------ small legs
 def bench_ranking(args):
     """Autoplacement ranking (FilterInstanceTypes + rankInstanceTypes,
     instancetype.go:259-379) over a C5-sized catalog of 2,000 instance types
-    with all filters off (RankInstanceTypes).  One call = host buffers in,
-    ranked indices out, so the time is PCIe- and allocation-inclusive; rank 0
-    at N=1 only (replicas: the call does not shard)."""
-    import numpy as np
+    with all filters off.  One call = host buffers in, ranked indices out
+    (PCIe-inclusive); rank 0 at N=1 only."""
     from gpusched import lib
     rng = np.random.default_rng(5)
     n = 2000
@@ -332,22 +466,87 @@ def bench_ranking(args):
     return out
 
 
+def claim_queries(problem, result):
+    """ToNodeClaim: each emitted NodeClaim's requirements + instance-type
+    In[options] and its requests, as gs_claim_query rows"""
+    names = [problem.strings[i] for i in problem.instance_types["name"]]
+
+    def add(b):
+        for c in result["claims"]:
+            reqs = []
+            for line in c["requirements"].split("\n") if c["requirements"] else []:
+                key, op, vals, gt, lt, _ = line.split("|")
+                if key == "node.kubernetes.io/instance-type":
+                    continue
+                if not (op == "Exists" and (gt != "-" or lt != "-")):
+                    reqs.append((key, op, vals.split(",") if vals else []))
+                if gt != "-":
+                    reqs.append((key, "Gt", [gt]))
+                if lt != "-":
+                    reqs.append((key, "Lt", [lt]))
+            reqs.append(("node.kubernetes.io/instance-type", "In", [names[i] for i in c["its"]]))
+            b.add_claim_query(reqs, c["requests"])
+    return problem.extended(add)
+
+
+def bench_create_filter(problem, result, args):
+    """CloudProvider.Create's re-filter + instanceTypes[0] + ResolveCapacityType
+    for every NodeClaim the CM Solve emitted, one gs_create_filter call
+    (host buffers in, results out: PCIe-inclusive)"""
+    p2 = claim_queries(problem, result)
+    solver = Solver(0)
+    try:
+        for _ in range(max(args.warmup, 1)):
+            solver.create_filter(p2, raw=True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            solver.create_filter(p2, raw=True)
+        ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        kernel_ms = solver_filter_ms(solver)
+        got = solver.create_filter(p2)
+    finally:
+        solver.close()
+    nq, n = p2.n_claim_queries, len(p2.instance_types)
+    out = {"workload": f"{nq} CM NodeClaims x {n} instance types (List order), requirement algebra + offerings "
+                       f"+ Fits", "pairs": nq * n, "ms_per_call_pcie_inclusive": round(ms, 3),
+           "kernel_ms": kernel_ms, "pairs_per_s": nq * n / (ms * 1e-3), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        from oracle import pyoracle
+        t0 = time.perf_counter()
+        st, want = pyoracle.create_filter(p2)
+        cms = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"ms_per_call": round(cms, 2), "pairs_per_s": nq * n / (cms * 1e-3), "cores": 1,
+                               "kind": "port", "sample": f"same {nq} claims; GPU results identical: {got == want}"}
+    return out
+
+
+def solver_filter_ms(solver):
+    return None  # the kernel time is inside the call; rocprofv3 stats carry it
+
+
+# --------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pods", type=int, default=100_000)
-    ap.add_argument("--cpu-sample-pods", type=int, default=40_000)
+    ap.add_argument("--latency-steps", type=int, default=3)
     ap.add_argument("--c4-nodes", type=int, default=5000)
-    ap.add_argument("--cpu-sample-sims", type=int, default=100)
+    ap.add_argument("--cpu-sample-sims", type=int, default=160)
+    ap.add_argument("--cpu-sample-prefixes", type=int, default=16)
+    ap.add_argument("--pool", type=int, default=min(16, os.cpu_count() or 1),
+                    help="worker processes for the consolidation CPU baselines (the box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C3 Solve legs")
     ap.add_argument("--c5-pods", type=int, default=200_000)
-    ap.add_argument("--cpu-sample-c5-pods", type=int, default=1000)
+    ap.add_argument("--cpu-sample-c5-pods", type=int, default=2000)
     ap.add_argument("--no-stress", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output, committed under profiles/)")
+    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | c4 | c4_mixed | c4_multi | "
+                                                 "c5 | filter | ranking (profiling passes)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch per leg (tools/pmc_traffic.py, committed under profiles/)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -360,8 +559,6 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if torch.cuda.is_available():
-            # RCCL over xGMI: barriers, the max-over-ranks time and the
-            # consolidation all-gather
             torch.cuda.set_device(local)
             device = torch.device("cuda", local)
             dist.init_process_group("nccl", device_id=device)
@@ -380,94 +577,97 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    problem = synth.make_cm(n_pods=args.pods, seed=0x5EED0006 + rank)
-    solver = Solver(local)
-    t0 = time.perf_counter()
-    solver.prepare(problem)
-    prep_ms = (time.perf_counter() - t0) * 1e3
-    for _ in range(args.warmup):
-        solver.run()
-
-    kt = []
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        solver.run()  # synchronous: returns after the stream's last event
-        kt.append(solver.last_run_ms())
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-
-    t1 = time.perf_counter()
-    out, res = solver.fetch()
-    fetch_ms = (time.perf_counter() - t1) * 1e3
-    checks = problem.checks()
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = checks * world / elapsed * args.steps
-
-    feas_ms = sum(k[0] for k in kt) / len(kt)
-    ffd_ms = sum(k[1] for k in kt) / len(kt)
-    trunc_ms = sum(k[2] for k in kt) / len(kt)
-    ab = algorithmic_bytes(res, problem, len(out["claims"]))
-    kms = {"feas": feas_ms, "ffd": ffd_ms, "trunc": trunc_ms}
-    dom = max(kms, key=kms.get)
     traffic = load_traffic(args.traffic_json)
+    only = args.only
+    solo = rank == 0 and world == 1
+    global _POOL
+    if solo and not args.no_cpu_baseline and not args.no_consolidation and args.pool > 1 and \
+            only in (None, "c4", "c4_mixed", "c4_multi"):
+        import multiprocessing as mp
+        _POOL = mp.get_context("fork").Pool(args.pool)  # before any GPU call in this process
+    line = {"metric": METRIC, "value": None, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic"}
 
-    def roof(k):
-        ach = ab[k] / (kms[k] * 1e-3) / 1e9
-        return {"kernel": {"feas": "feas_kernel", "ffd": "ffd_kernel", "trunc": "trunc_kernel"}[k],
-                "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": ab[k], "avg_ms": round(kms[k], 4)}
+    if only in (None, "cm", "filter"):
+        problem = synth.make_cm(n_pods=args.pods, seed=0x5EED0006 + rank)
+        solver = Solver(local)
+        r = solve_leg(problem, solver, args.steps, args.warmup, args.latency_steps if only != "filter" else 0,
+                      barrier, max_over_ranks, traffic, "cm")
+        solver.close()
+        result = r.pop("_result")
+        ms = r.pop("ms_per_step")
+        line.update({
+            "value": r["checks"] * world / (ms * 1e-3),
+            "ms_per_step": ms,
+            "device_ms_per_step": ms,
+            "config": {"workload": CM_WORKLOAD, "pods": len(problem.pods),
+                       "instance_types": len(problem.instance_types), "offerings": len(problem.offerings),
+                       "nodepools": len(problem.nodepools), "checks_per_step": r["checks"],
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+        })
+        line.update({k: v for k, v in r.items() if k != "checks"})
+        line["result_sha256"] = digest(result)
+        line["cpu_baseline"] = None
+        if solo and not args.no_cpu_baseline and only is None:
+            line["cpu_baseline"] = cpu_baseline_solve(problem, result)
+        if solo and only in (None, "filter"):
+            line["create_filter"] = bench_create_filter(problem, result, args)
+        del problem, result
 
-    roofline = roof(dom)
-    roofline["traffic"] = traffic.get(dom)
-    line = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "checks/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int64",
-        "data": "synthetic",
-        "config": {
-            "workload": "CM: 100k pods x C2 synthetic IBM VPC catalog (198 profiles x 3 zones x "
-                        "{on-demand, spot} = 1,188 offerings), 1 NodePool, 1% GPU pods, 10% nodeSelectors",
-            "pods": len(problem.pods),
-            "instance_types": len(problem.instance_types),
-            "offerings": len(problem.offerings),
-            "nodepools": len(problem.nodepools),
-            "checks_per_step": checks,
-            "parallelism": f"replicas{world}" if world > 1 else "single",
-        },
-        "solve_latency_ms": ms_per_step,
-        "kernel_ms": {k: round(v, 4) for k, v in kms.items()},
-        "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 2),
-        "fetch_decode_ms": round(fetch_ms, 2),
-        "new_nodeclaims": len(out["claims"]),
-        "pod_errors": len(out["errors"]),
-        "queue_pops": int(res.pops),
-        "ffd_candidates_scored": int(res.cand_evals),
-        "ffd_candidates_full_check": int(res.cand_full),
-        "ffd_phase_ms": {"sort": round(res.t_ffd_sort_ms, 2), "scan": round(res.t_ffd_scan_ms, 2),
-                         "template": round(res.t_ffd_template_ms, 2)},
-        "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
-        "roofline": roofline,
-        "roofline_feasibility_kernel": dict(roof("feas"), traffic=traffic.get("feas")),
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_pods)
-    solver.close()
-    if not args.no_consolidation:
-        line["consolidation"] = bench_consolidation(args, rank, world, local, dist, device, barrier, max_over_ranks)
-    if not args.no_stress:
-        line["stress"] = bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks)
-    if rank == 0 and world == 1:
+    if solo and not args.no_configs and only in (None, "c1", "c2", "c3"):
+        configs = {}
+        gens = {"c1": (synth.make_c1, "C1: 500 pods x 8 fake profiles x 3 zones (24 offerings), 1 NodePool"),
+                "c2": (synth.make_c2, "C2: 10k pods x C2 catalog (1,188 offerings), 1 NodePool"),
+                "c3": (synth.make_c3, "C3: 50k pods x C2 catalog, 4 weighted NodePools, taints/tolerations, "
+                                      "required + preferred node affinity, 20% zone topology spread")}
+        for name, (gen, desc) in gens.items():
+            if only not in (None, name):
+                continue
+            leg = config_leg(name, gen(), args, traffic)
+            leg["workload"] = desc
+            configs[name.upper()] = leg
+        line["configs"] = configs
+
+    if not args.no_consolidation and only in (None, "c4", "c4_mixed", "c4_multi"):
+        legs = {}
+        specs = {
+            "c4": (dict(), abi.CONSOLIDATE_SINGLE, 0,
+                   "C4: {n} state nodes (C2 catalog, 2 NodePools, 60-90% cpu used, {b} bound pods), "
+                   "SingleNodeConsolidation over all {n} candidates"),
+            "c4_mixed": (dict(util=(0.9, 0.99), full_frac=0.5, big_frac=1.0, pack=True), abi.CONSOLIDATE_SINGLE, 0,
+                         "C4 packed: {n} state nodes filled until no pod of their shape fits (90-99% cpu, "
+                         "{b} bound 1-6 vCPU pods): mixed Delete / Replace / NoOp, SingleNodeConsolidation"),
+            "c4_multi": (dict(), abi.CONSOLIDATE_MULTI, 100,
+                         "C4: {n} state nodes, MultiNodeConsolidation: every binary-search prefix "
+                         "candidates[0:mid+1] of the first 100 candidates as one simulation"),
+        }
+        for name, (kw, mode, maxc, desc) in specs.items():
+            if only not in (None, name):
+                continue
+            spec = (args.c4_nodes, kw)
+            problem = c4_problem(spec)
+            leg = consolidation_leg(problem, mode, args, rank, world, local, dist, device, barrier, max_over_ranks,
+                                    traffic, name, max_candidates=maxc)
+            cmds = leg.pop("_commands")
+            leg["workload"] = desc.format(n=len(problem.nodes), b=len(problem.bound_pods))
+            if solo and not args.no_cpu_baseline:
+                n = len(problem.nodes)
+                if mode == abi.CONSOLIDATE_SINGLE:
+                    leg["cpu_baseline"] = cpu_baseline_single(spec, n, cmds, args.cpu_sample_sims, args.pool)
+                else:
+                    leg["cpu_baseline"] = cpu_baseline_multi(spec, n, cmds, args.cpu_sample_prefixes, args.pool)
+            legs[name] = leg
+        line["consolidation"] = legs.get("c4")
+        line["consolidation_legs"] = legs
+
+    if not args.no_stress and only in (None, "c5"):
+        line["stress"] = bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks, traffic)
+    if solo and only in (None, "ranking"):
         line["ranking"] = bench_ranking(args)
+    if _POOL is not None:
+        _POOL.close()
+        _POOL.join()
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

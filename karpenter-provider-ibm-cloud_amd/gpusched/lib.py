@@ -137,6 +137,7 @@ class Solver:
     def __init__(self, device=0, flags=0):
         self.L = load()
         self.ctx = C.c_void_p()
+        self.flags = flags
         cfg = abi.GsConfig(device, 0, flags)
         st = self.L.gs_create(C.byref(cfg), C.byref(self.ctx))
         if st != abi.GS_OK:
@@ -180,6 +181,14 @@ class Solver:
         res = abi.GsResult()
         self._check(self.L.gs_fetch(self.ctx, C.byref(res)))
         return abi.result_to_dict(res, self.problem), res
+
+    def solve_raw(self, problem):
+        """one gs_solve call (encode + H2D + kernels + D2H + decode into the
+        library's result memory) -> gs_result, no Python-side copy"""
+        self.problem = problem
+        res = abi.GsResult()
+        self._check(self.L.gs_solve(self.ctx, C.byref(problem.struct), C.byref(res)))
+        return res
 
     def solve(self, problem):
         self.prepare(problem)

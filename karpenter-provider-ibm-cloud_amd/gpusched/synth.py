@@ -386,13 +386,17 @@ CONFIGS["C4sim"] = make_c4_sim
 BIG_CPU = np.array([1000, 2000, 3000, 4000, 6000], dtype=np.int64)
 
 
-def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=200, full_frac=0.15, big_frac=0.3):
+def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=200, full_frac=0.15, big_frac=0.3,
+            pack=False):
     """C4 consolidation cluster: state nodes sampled from the C2
     catalog in 2 NodePools, each carrying bound reschedulable pods that use
     `util` of its allocatable cpu (a `full_frac` share of nodes run at ~97 %;
     a `big_frac` share of nodes carry 1-6 vCPU pods),
     plus `n_pending` pending pods.  Node available = allocatable - daemon -
-    bound pods (StateNode.Available)."""
+    bound pods (StateNode.Available).  pack=True keeps adding the node's
+    smallest pod shape after the first misfit, so no node keeps room for
+    another pod of its kind (consolidation then mixes Delete, Replace and
+    NoOp)."""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     profs = c2_profiles(n_its)
@@ -429,7 +433,13 @@ def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=2
                 mem = int(rng.choice(MEM_CHOICES[:4]))
             if used["cpu"] + cpu > target * alloc["cpu"] or used["memory"] + mem > alloc["memory"] \
                     or used["pods"] + 1000 > alloc["pods"]:
-                break
+                if not pack:
+                    break
+                cpu = int(min(BIG_CPU)) if big else int(min(CPU_CHOICES))
+                mem = int(MEM_CHOICES[2]) if big else int(MEM_CHOICES[0])
+                if used["cpu"] + cpu > target * alloc["cpu"] or used["memory"] + mem > alloc["memory"] \
+                        or used["pods"] + 1000 > alloc["pods"]:
+                    break
             used["cpu"] += cpu
             used["memory"] += mem
             used["pods"] += 1000

@@ -1137,6 +1137,7 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   } catch (const Unsupported& u) {
     return u.code;
   }
+  const double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   Scheduler s{st};
   auto errors = s.solve();
   ResultStore& r = g_res;
@@ -1182,6 +1183,7 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   out->error_pods = r.error_pods.data();
   out->pops = s.pops;
   out->claim_prefix = s.claim_calls;
+  out->t_encode_ms = build_ms;  // the oracle's own input build (string sets)
   out->node_prefix = s.node_calls;
   out->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GS_OK;
