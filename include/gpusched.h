@@ -472,6 +472,79 @@ typedef struct gs_claim_filter_result {
 gs_status gs_create_filter(gs_ctx* ctx, const gs_problem* catalog, const gs_claim_query* queries,
                            uint32_t n_queries, gs_claim_filter_result* out);
 
+/* ------------------------------------------------------ catalog ingest
+ * IBMInstanceTypeProvider.List over the VPC wire data (reference
+ * pkg/providers/common/instancetype/instancetype.go:221-246,433-537,659-858;
+ * profiles as ListInstanceProfiles returns them, pkg/cloudprovider/ibm/vpc.go:489-495). */
+
+/* the vpcv1.InstanceProfile fields convertVPCProfileToInstanceType reads */
+enum { GS_VPC_NIL = 0, GS_VPC_VALUE = 1, GS_VPC_OTHER = 2 };          /* *_kind: nil / the Value variant / another variant */
+enum { GS_AVAIL_NIL = 0, GS_AVAIL_ENUM = 1, GS_AVAIL_FIXED = 2 };     /* AvailabilityClass variants */
+typedef struct gs_vpc_profile {
+  const char* name;                 /* NULL: nil */
+  int32_t vcpu_kind; int64_t vcpu;  /* VcpuCount (InstanceProfileVcpu{Value}) */
+  int32_t memory_kind; int64_t memory_gib; /* Memory (InstanceProfileMemory{Value}, GiB) */
+  const char* arch;                 /* VcpuArchitecture.Value, NULL: nil ("amd64") */
+  int32_t gpu_kind; int64_t gpu;    /* GpuCount (InstanceProfileGpu{Value}; other variants count 0) */
+  int32_t avail_kind;               /* GS_AVAIL_* */
+  const char* const* avail_values; uint32_t n_avail_values; /* Enum values / Fixed value (0 or 1 entries) */
+} gs_vpc_profile;
+
+/* PricingProvider.GetPrice(name, zone): the last entry matching name and
+ * (zone == NULL or zone); no entry -> 0.0 (instancetype.go:753 drops the error) */
+typedef struct gs_price {
+  const char* name;
+  const char* zone;
+  double price;
+} gs_price;
+
+/* UnavailableOfferings entries ("<profile>:<zone>:<capacity type>", reference
+ * pkg/cache/unavailable_offerings.go:36-77): unavailable while now <= expiry */
+typedef struct gs_unavailable {
+  const char* key;
+  int64_t expiry_unix_ns;
+} gs_unavailable;
+
+typedef struct gs_catalog_env {
+  const char* const* zones; uint32_t n_zones; /* getZonesForRegion, in order (0: every profile fails) */
+  int32_t spot_discount_percent;              /* options.SpotDiscountPercent (0 -> 60) */
+  const gs_price* prices; uint32_t n_prices;
+  const gs_unavailable* unavailable; uint32_t n_unavailable;
+  int64_t now_unix_ns;
+  int32_t has_kubelet;                        /* nodeClass != nil && nodeClass.Spec.Kubelet != nil */
+  const char* kube_reserved_cpu;              /* NULL: key absent; unparsable: the default (calculateOverhead) */
+  const char* kube_reserved_memory;
+  const char* system_reserved_cpu;
+  const char* system_reserved_memory;
+  const char* eviction_memory_available;      /* evictionHard["memory.available"] */
+} gs_catalog_env;
+
+/* The converted catalog in gs_problem form (its own string table): splice
+ * strings / value_ids / reqs / quantities / offerings / instance_types into a
+ * gs_problem, offsetting the ids, or use them as they are.  Owned by the ctx,
+ * valid until the next gs_build_catalog or gs_destroy. */
+typedef struct gs_catalog {
+  const char* const* strings; uint32_t n_strings;
+  const uint32_t* value_ids; uint32_t n_value_ids;
+  const gs_requirement* reqs; uint32_t n_reqs;
+  const gs_quantity* quantities; uint32_t n_quantities;
+  const gs_offering* offerings; uint32_t n_offerings;
+  const gs_instance_type* instance_types; uint32_t n_instance_types;
+  uint32_t n_skipped;                 /* profiles the conversion refused (List logs and skips them) */
+  const uint32_t* skipped;            /* their indices */
+  const char* const* skip_reasons;    /* the conversion error text, per skipped profile */
+} gs_catalog;
+
+/* List: convert every profile in VPC order, skipping the ones the conversion
+ * refuses; GS_E_INVALID when none converts ("no instance types found").
+ * Capacity {cpu, memory, pods, nvidia.com/gpu}, requirements {instance-type,
+ * arch, instance-family, instance-size}, Overhead.Total() from
+ * calculateOverhead, offerings zones x GetSupportedCapacityTypes with the
+ * spot discount and the UnavailableOfferings overlay (the price / overlay
+ * expansion of all profiles x zones x capacity types runs on the device). */
+gs_status gs_build_catalog(gs_ctx* ctx, const gs_vpc_profile* profiles, uint32_t n_profiles,
+                           const gs_catalog_env* env, gs_catalog* out);
+
 /* host-only: run the encoder (no device needed) and report whether this
  * build can solve the problem exactly; GS_E_UNSUPPORTED names the feature.
  * A Go caller uses it to choose between this library and upstream Solve. */
@@ -481,9 +554,10 @@ gs_status gs_validate(const gs_problem* problem, char* err, size_t err_len);
  * gs_quantity, gs_label, gs_taint, gs_toleration, gs_term, gs_offering,
  * gs_instance_type, gs_nodepool, gs_pod, gs_node, gs_problem, gs_result,
  * gs_feas_result, gs_config, gs_consolidation, gs_command,
- * gs_consolidation_result, gs_claim_query, gs_claim_filter_result.
+ * gs_consolidation_result, gs_claim_query, gs_claim_filter_result,
+ * gs_vpc_profile, gs_price, gs_unavailable, gs_catalog_env, gs_catalog.
  * Bindings check their layouts against it.
- * Returns the number of entries (21); writes min(n, 21). */
+ * Returns the number of entries (26); writes min(n, 26). */
 uint32_t gs_abi_sizes(uint32_t* out, uint32_t n);
 
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);

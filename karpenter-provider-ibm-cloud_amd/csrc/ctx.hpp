@@ -130,6 +130,14 @@ struct gs_ctx {
   std::vector<uint32_t> cf_n, cf_ct;
   std::vector<int32_t> cf_sel;
   double t_filter = 0;
+  // gs_build_catalog result storage
+  std::vector<std::string> cat_strs, cat_reasons;
+  std::vector<const char*> cat_ptrs, cat_reason_ptrs;
+  std::vector<uint32_t> cat_vals, cat_skipped;
+  std::vector<gs_requirement> cat_reqs;
+  std::vector<gs_quantity> cat_qty;
+  std::vector<gs_offering> cat_offs;
+  std::vector<gs_instance_type> cat_its;
 
   std::vector<void*> host_allocs;  // pinned staging buffers (consolidation results)
   void free_all() {

@@ -273,6 +273,99 @@ def claim_filter_to_list(res: GsClaimFilterResult, n_types: int) -> list:
     return out
 
 
+GS_VPC_NIL, GS_VPC_VALUE, GS_VPC_OTHER = 0, 1, 2
+GS_AVAIL_NIL, GS_AVAIL_ENUM, GS_AVAIL_FIXED = 0, 1, 2
+
+
+class GsVpcProfile(C.Structure):
+    _fields_ = [
+        ("name", C.c_char_p), ("vcpu_kind", C.c_int32), ("vcpu", C.c_int64),
+        ("memory_kind", C.c_int32), ("memory_gib", C.c_int64), ("arch", C.c_char_p),
+        ("gpu_kind", C.c_int32), ("gpu", C.c_int64), ("avail_kind", C.c_int32),
+        ("avail_values", C.POINTER(C.c_char_p)), ("n_avail_values", _U32),
+    ]
+
+
+class GsPrice(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("zone", C.c_char_p), ("price", C.c_double)]
+
+
+class GsUnavailable(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("expiry_unix_ns", C.c_int64)]
+
+
+class GsCatalogEnv(C.Structure):
+    _fields_ = [
+        ("zones", C.POINTER(C.c_char_p)), ("n_zones", _U32),
+        ("spot_discount_percent", C.c_int32),
+        ("prices", C.POINTER(GsPrice)), ("n_prices", _U32),
+        ("unavailable", C.POINTER(GsUnavailable)), ("n_unavailable", _U32),
+        ("now_unix_ns", C.c_int64),
+        ("has_kubelet", C.c_int32),
+        ("kube_reserved_cpu", C.c_char_p), ("kube_reserved_memory", C.c_char_p),
+        ("system_reserved_cpu", C.c_char_p), ("system_reserved_memory", C.c_char_p),
+        ("eviction_memory_available", C.c_char_p),
+    ]
+
+
+class GsCatalog(C.Structure):
+    _fields_ = [
+        ("strings", C.POINTER(C.c_char_p)), ("n_strings", _U32),
+        ("value_ids", C.POINTER(C.c_uint32)), ("n_value_ids", _U32),
+        ("reqs", _P), ("n_reqs", _U32),
+        ("quantities", _P), ("n_quantities", _U32),
+        ("offerings", _P), ("n_offerings", _U32),
+        ("instance_types", _P), ("n_instance_types", _U32),
+        ("n_skipped", _U32), ("skipped", C.POINTER(C.c_uint32)),
+        ("skip_reasons", C.POINTER(C.c_char_p)),
+    ]
+
+
+def _np_view(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n * np.dtype(dtype).itemsize,))
+    return raw.view(dtype).copy()
+
+
+def catalog_to_list(cat: GsCatalog) -> list:
+    """gs_catalog -> [{name, requirements [(key, op, [values])], capacity {res: milli},
+    overhead {res: milli}, offerings [(zone, ct, price, available)]}] in List order"""
+    strs = [cat.strings[i].decode() for i in range(cat.n_strings)]
+    vals = [int(cat.value_ids[i]) for i in range(cat.n_value_ids)]
+    reqs = _np_view(cat.reqs, cat.n_reqs, DT_REQ)
+    qty = _np_view(cat.quantities, cat.n_quantities, DT_QTY)
+    offs = _np_view(cat.offerings, cat.n_offerings, DT_OFFERING)
+    its = _np_view(cat.instance_types, cat.n_instance_types, DT_IT)
+    ops = {v: k for k, v in OPS.items()}
+
+    def rl(b, n):
+        out = []
+        for r in reqs[b:b + n]:
+            vb, vn = r["values"]
+            out.append((strs[r["key"]], ops[int(r["op"])], [strs[v] for v in vals[vb:vb + vn]]))
+        return out
+
+    def ql(b, n):
+        d = {}
+        for q in qty[b:b + n]:
+            d[strs[q["resource"]]] = d.get(strs[q["resource"]], 0) + int(q["milli"])
+        return d
+
+    out = []
+    for it in its:
+        ob, on = it["offerings"]
+        ol = []
+        for o in offs[ob:ob + on]:
+            rb, rn = o["requirements"]
+            d = {k: v[0] for k, _, v in rl(rb, rn)}
+            ol.append((d["topology.kubernetes.io/zone"], d["karpenter.sh/capacity-type"], float(o["price"]),
+                       bool(o["available"])))
+        out.append({"name": strs[it["name"]], "requirements": rl(*it["requirements"]),
+                    "capacity": ql(*it["capacity"]), "overhead": ql(*it["overhead"]), "offerings": ol})
+    return out
+
+
 def commands_to_list(res: GsConsolidationResult) -> list:
     """Canonical, comparable form of the commands (copied out of library memory)."""
     out = []

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, os.environ.get("GPUSCHED_LIB", "libgpusched.so"))
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
            "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard",
-           "gs_feasibility_shard_device", "gs_rank_instance_types", "gs_create_filter"]
+           "gs_feasibility_shard_device", "gs_rank_instance_types", "gs_create_filter", "gs_build_catalog"]
 
 
 class GpuSchedError(RuntimeError):
@@ -57,6 +57,9 @@ def load():
         L.gs_create_filter.argtypes = [vp, C.POINTER(abi.GsProblem), C.POINTER(abi.GsClaimQuery), C.c_uint32,
                                        C.POINTER(abi.GsClaimFilterResult)]
         L.gs_create_filter.restype = C.c_int
+        L.gs_build_catalog.argtypes = [vp, C.POINTER(abi.GsVpcProfile), C.c_uint32, C.POINTER(abi.GsCatalogEnv),
+                                       C.POINTER(abi.GsCatalog)]
+        L.gs_build_catalog.restype = C.c_int
         L.gs_rank_instance_types.argtypes = abi.RANK_ARGTYPES
         L.gs_rank_instance_types.restype = C.c_int
         L.gs_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
@@ -219,6 +222,59 @@ class Solver:
         if raw:
             return res
         return abi.claim_filter_to_list(res, len(problem.instance_types))
+
+    def build_catalog(self, profiles, zones, price_rows=(), unavailable=(), now_ns=0, spot_discount_percent=0,
+                      kubelet=None, raw=False):
+        """gs_build_catalog.  profiles: dicts with name, vcpu, memory_gib, arch,
+        gpu, availability_class (None | ("enum", [..]) | ("fixed", v)) and
+        optional vcpu_kind / memory_kind / gpu_kind; price_rows: (name, zone
+        or None, price); unavailable: (key, expiry_ns).  -> (types, skipped
+        [(index, reason)], raw gs_catalog)"""
+        keep = []
+        arr = (abi.GsVpcProfile * max(1, len(profiles)))()
+        enc = lambda x: None if x is None else x.encode()  # noqa: E731
+        for i, p in enumerate(profiles):
+            a = arr[i]
+            a.name = enc(p.get("name"))
+            a.vcpu_kind = p.get("vcpu_kind", abi.GS_VPC_NIL if p.get("vcpu") is None else abi.GS_VPC_VALUE)
+            a.vcpu = p.get("vcpu") or 0
+            a.memory_kind = p.get("memory_kind", abi.GS_VPC_NIL if p.get("memory_gib") is None else abi.GS_VPC_VALUE)
+            a.memory_gib = p.get("memory_gib") or 0
+            a.arch = enc(p.get("arch"))
+            a.gpu_kind = p.get("gpu_kind", abi.GS_VPC_NIL if p.get("gpu") is None else abi.GS_VPC_VALUE)
+            a.gpu = p.get("gpu") or 0
+            ac = p.get("availability_class")
+            if ac is None:
+                a.avail_kind = abi.GS_AVAIL_NIL
+            else:
+                kind, val = ac
+                vals = list(val) if kind == "enum" else ([] if val is None else [val])
+                va = (C.c_char_p * max(1, len(vals)))(*[v.encode() for v in vals])
+                keep.append(va)
+                a.avail_kind = abi.GS_AVAIL_ENUM if kind == "enum" else abi.GS_AVAIL_FIXED
+                a.avail_values, a.n_avail_values = va, len(vals)
+        e = abi.GsCatalogEnv()
+        za = (C.c_char_p * max(1, len(zones)))(*[z.encode() for z in zones])
+        pr = (abi.GsPrice * max(1, len(price_rows)))(*[abi.GsPrice(enc(n), enc(z), float(v)) for n, z, v in price_rows])
+        ua = (abi.GsUnavailable * max(1, len(unavailable)))(*[abi.GsUnavailable(enc(k), int(x)) for k, x in unavailable])
+        keep += [za, pr, ua]
+        e.zones, e.n_zones = za, len(zones)
+        e.spot_discount_percent = spot_discount_percent
+        e.prices, e.n_prices = pr, len(price_rows)
+        e.unavailable, e.n_unavailable = ua, len(unavailable)
+        e.now_unix_ns = now_ns
+        if kubelet is not None:
+            e.has_kubelet = 1
+            kr, sr, eh = kubelet.get("kubeReserved", {}), kubelet.get("systemReserved", {}), kubelet.get("evictionHard", {})
+            e.kube_reserved_cpu = enc(kr.get("cpu"))
+            e.kube_reserved_memory = enc(kr.get("memory"))
+            e.system_reserved_cpu = enc(sr.get("cpu"))
+            e.system_reserved_memory = enc(sr.get("memory"))
+            e.eviction_memory_available = enc(eh.get("memory.available"))
+        out = abi.GsCatalog()
+        self._check(self.L.gs_build_catalog(self.ctx, arr, len(profiles), C.byref(e), C.byref(out)))
+        skipped = [(int(out.skipped[i]), out.skip_reasons[i].decode()) for i in range(out.n_skipped)]
+        return abi.catalog_to_list(out), skipped, out
 
     def feasibility(self):
         res = abi.GsFeasResult()

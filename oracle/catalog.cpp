@@ -10,6 +10,7 @@
 #include "oracle.h"
 #include "gosort.h"
 
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -225,8 +226,11 @@ extern "C" gs_status oracle_convert_profile(const oracle_profile* pr, const orac
   if (cts.empty()) cts.push_back("on-demand");
   int pct = env->spot_discount_percent;
   if (pct == 0) pct = 60;
-  std::set<string> unavailable;
-  for (uint32_t i = 0; i < env->n_unavailable; i++) unavailable.insert(env->unavailable[i]);
+  // UnavailableOfferings (pkg/cache/unavailable_offerings.go:36-77): Add is a
+  // map assignment; IsUnavailable = present && !now.After(expiry)
+  std::map<string, int64_t> unavailable;
+  for (uint32_t i = 0; i < env->n_unavailable; i++)
+    unavailable[env->unavailable[i]] = env->unavailable_expiry ? env->unavailable_expiry[i] : INT64_MAX;
   // calculateOverhead
   int64_t kc = 100, km = 1073741824000LL, sc = 100, sm = 1073741824000LL, ev = 524288000000LL;
   if (env->has_nodeclass && env->has_kubelet) {
@@ -252,9 +256,12 @@ extern "C" gs_status oracle_convert_profile(const oracle_profile* pr, const orac
     for (auto& ct : cts) {
       double price = 0.0;  // GetPrice error -> 0 (instancetype.go:753 discards the error)
       for (uint32_t k = 0; k < env->n_prices; k++)
-        if (name == env->price_names[k]) price = env->prices[k];
+        if (name == env->price_names[k] &&
+            (!env->price_zones || !env->price_zones[k] || zone == env->price_zones[k]))
+          price = env->prices[k];
       if (ct == "spot") price = price * (double)pct / 100.0;
-      bool avail = !unavailable.count(name + ":" + zone + ":" + ct);
+      auto uf = unavailable.find(name + ":" + zone + ":" + ct);
+      bool avail = !(uf != unavailable.end() && !(env->now_ns > uf->second));
       char pbuf[64];
       std::snprintf(pbuf, sizeof pbuf, "%.17g", price);
       t += "offering=" + zone + "|" + ct + "|" + hexbits(price) + "|" + pbuf + "|" + (avail ? "1" : "0") + "\n";

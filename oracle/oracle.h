@@ -56,6 +56,9 @@ typedef struct oracle_catalog_env {
   const char* system_reserved_cpu;
   const char* system_reserved_memory;
   const char* eviction_memory_available;
+  const char* const* price_zones;      /* NULL, or per price entry its zone (NULL entry: every zone) */
+  const int64_t* unavailable_expiry;   /* NULL: entries never expire; else unavailable while now <= expiry */
+  int64_t now_ns;
 } oracle_catalog_env;
 
 /* convertVPCProfileToInstanceType.  On success returns GS_OK and a

@@ -33,6 +33,9 @@ class OracleEnv(C.Structure):
         ("kube_reserved_cpu", C.c_char_p), ("kube_reserved_memory", C.c_char_p),
         ("system_reserved_cpu", C.c_char_p), ("system_reserved_memory", C.c_char_p),
         ("eviction_memory_available", C.c_char_p),
+        ("price_zones", C.POINTER(C.c_char_p)),
+        ("unavailable_expiry", C.POINTER(C.c_int64)),
+        ("now_ns", C.c_int64),
     ]
 
 
@@ -115,8 +118,10 @@ def _cstrs(xs):
 
 def convert_profile(name, vcpu=None, memory_gib=None, arch=None, gpu=None, availability_class=None,
                     zones=(), prices=None, spot_discount_percent=0, unavailable=(), has_client=True,
-                    kubelet=None, vcpu_kind=None, memory_kind=None):
-    """returns (status, text)"""
+                    kubelet=None, vcpu_kind=None, memory_kind=None, price_rows=None, unavailable_expiry=None,
+                    now_ns=0, gpu_kind=None):
+    """returns (status, text).  price_rows: [(name, zone or None, price)]
+    instead of the name-keyed `prices`; unavailable_expiry: per key expiry (ns)"""
     keep = []
     p = OracleProfile()
     p.name = name.encode() if name is not None else None
@@ -125,7 +130,7 @@ def convert_profile(name, vcpu=None, memory_gib=None, arch=None, gpu=None, avail
     p.memory_kind = memory_kind if memory_kind is not None else (0 if memory_gib is None else 1)
     p.memory_gib = memory_gib or 0
     p.arch = arch.encode() if arch else None
-    p.gpu_kind = 0 if gpu is None else 1
+    p.gpu_kind = gpu_kind if gpu_kind is not None else (0 if gpu is None else 1)
     p.gpu = gpu or 0
     if availability_class is None:
         p.avail_kind = 0
@@ -142,14 +147,22 @@ def convert_profile(name, vcpu=None, memory_gib=None, arch=None, gpu=None, avail
     keep.append(za)
     e.zones, e.n_zones = za, zn
     e.spot_discount_percent = spot_discount_percent
-    prices = prices or {}
-    pn, n = _cstrs(list(prices))
-    pv = (C.c_double * max(1, n))(*prices.values())
-    keep += [pn, pv]
+    if price_rows is None:
+        price_rows = [(k, None, v) for k, v in (prices or {}).items()]
+    pn, n = _cstrs([r[0] for r in price_rows])
+    pz = (C.c_char_p * max(1, n))(*[None if r[1] is None else r[1].encode() for r in price_rows])
+    pv = (C.c_double * max(1, n))(*[r[2] for r in price_rows])
+    keep += [pn, pv, pz]
     e.price_names, e.prices, e.n_prices = pn, pv, n
+    e.price_zones = pz
     ua, un = _cstrs(list(unavailable))
     keep.append(ua)
     e.unavailable, e.n_unavailable = ua, un
+    if unavailable_expiry is not None:
+        ux = (C.c_int64 * max(1, un))(*unavailable_expiry)
+        keep.append(ux)
+        e.unavailable_expiry = ux
+    e.now_ns = now_ns
     if kubelet is not None:
         e.has_nodeclass = 1
         e.has_kubelet = 1
