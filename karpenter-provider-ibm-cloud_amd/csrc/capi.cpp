@@ -76,6 +76,8 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.var_count, e.var_count);
   c->upload(d.vars, e.vars);
   c->upload(d.itmask, e.itmask);
+  c->upload(d.var_itclass, e.var_itclass);
+  c->upload(d.itclass_mask, e.itclass_mask);
   c->upload(d.fk_entries, e.fk_entries);
   c->upload(d.queue0, e.queue0);
   if (!sims) {

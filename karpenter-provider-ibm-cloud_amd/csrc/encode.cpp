@@ -1100,8 +1100,20 @@ struct Ctx {
       e.var_count.push_back((uint32_t)e.variants.size() - e.var_begin.back());
     }
     e.V = (uint32_t)e.variants.size();
-    // device variant records
+    // device variant records; identical has-bitsets share one arena slot and
+    // identical IT-key requirement sets one class
     e.vars.resize(e.V);
+    e.var_itclass.assign(e.V, gsd::NONE);
+    std::map<std::vector<uint64_t>, uint32_t> arena_slot, itclass_of;
+    std::vector<std::vector<uint32_t>> class_offs;  // per class: arena offset per IT key (NONE: unconstrained)
+    auto arena = [&](const std::vector<uint64_t>& words) {
+      auto f = arena_slot.find(words);
+      if (f != arena_slot.end()) return f->second;
+      const uint32_t off = (uint32_t)e.itmask.size();
+      e.itmask.insert(e.itmask.end(), words.begin(), words.end());
+      arena_slot.emplace(words, off);
+      return off;
+    };
     for (uint32_t i = 0; i < e.P; i++)
       for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
         auto& pv = e.variants[v];
@@ -1109,18 +1121,28 @@ struct Ctx {
         std::memset(&vr, 0, sizeof vr);
         vr.pod = i;
         for (int k = 0; k < gsd::KMAX_IT; k++) vr.itmask_off[k] = gsd::NONE;
+        bool itk = false;
         for (uint32_t k = 0; k < e.K; k++) {
           auto f = pv.reqs.find(e.it_keys[k]);
           if (f == pv.reqs.end()) continue;
-          vr.itmask_off[k] = (uint32_t)e.itmask.size();
-          e.itmask.insert(e.itmask.end(), f->second.has.w.begin(), f->second.has.w.end());
+          vr.itmask_off[k] = arena(f->second.has.w);
+          itk = true;
+        }
+        if (itk) {
+          // the class key: the arena slots of the constrained keys
+          std::vector<uint64_t> sig(vr.itmask_off, vr.itmask_off + e.K);
+          auto f = itclass_of.find(sig);
+          if (f == itclass_of.end()) {
+            f = itclass_of.emplace(sig, (uint32_t)class_offs.size()).first;
+            class_offs.emplace_back(vr.itmask_off, vr.itmask_off + e.K);
+          }
+          e.var_itclass[v] = f->second;
         }
         vr.zfull_off = vr.cfull_off = gsd::NONE;
         for (int kk = 0; kk < 2; kk++) {
           auto f = pv.reqs.find(kk ? e.k_ct : e.k_zone);
           if (f == pv.reqs.end()) continue;
-          (kk ? vr.cfull_off : vr.zfull_off) = (uint32_t)e.itmask.size();
-          e.itmask.insert(e.itmask.end(), f->second.has.w.begin(), f->second.has.w.end());
+          (kk ? vr.cfull_off : vr.zfull_off) = arena(f->second.has.w);
         }
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
@@ -1145,6 +1167,18 @@ struct Ctx {
         vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
       }
     if (e.itmask.empty()) e.itmask.push_back(0);
+    e.itclass_mask.assign(std::max<size_t>(class_offs.size(), 1) * e.W, 0);
+    for (size_t c = 0; c < class_offs.size(); c++)
+      for (uint32_t it = 0; it < e.N; it++) {
+        bool ok = true;
+        for (uint32_t k = 0; k < e.K && ok; k++) {
+          const uint32_t off = class_offs[c][k];
+          if (off == gsd::NONE) continue;
+          const uint32_t vid = e.it_vid[(size_t)k * e.N + it];
+          ok = (e.itmask[off + (vid >> 6)] >> (vid & 63)) & 1;
+        }
+        if (ok) e.itclass_mask[c * e.W + it / 64] |= 1ull << (it % 64);
+      }
     if (e.fk_entries.empty()) e.fk_entries.push_back(gsd::FKEntry{});
     // <U> NewQueue: cpu desc, memory desc, creationTimestamp asc, UID asc (total order)
     // sorted on packed keys: the UID's first 8 bytes (big-endian, so integer

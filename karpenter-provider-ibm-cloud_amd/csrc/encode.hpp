@@ -112,6 +112,11 @@ struct Encoded {
   std::vector<uint32_t> var_begin, var_count, queue0;
   std::vector<gsd::VarRec> vars;
   std::vector<uint64_t> itmask;
+  // variants with IT-key requirements, deduplicated by those requirements:
+  // class c allows instance type i iff every constrained key's Has covers
+  // i's value (<U> it.Requirements.Intersects on IT keys)
+  std::vector<uint32_t> var_itclass;
+  std::vector<uint64_t> itclass_mask;
   std::vector<gsd::FKEntry> fk_entries;
   uint32_t NN = 0;
   std::vector<uint32_t> node_order;  // device position -> gs_problem node index

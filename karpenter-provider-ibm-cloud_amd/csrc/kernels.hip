@@ -26,97 +26,105 @@ constexpr int BLOCK = 256;
 }  // namespace
 
 // ===================================================================== K1/K2
-// One wave per (variant v, template t).  The row is word-parallel bitset
-// algebra over instance types (lane w holds IT word w):
+// A wave evaluates PP = 64/LP (variant v, template t) pairs at once: lane
+// group s (LP lanes, LP = the row's word count rounded up to a power of two,
+// at most 64) holds pair s's row, lane wl of the group row word wl (+64 per
+// extra pass when W > 64).  The row is word-parallel bitset algebra over
+// instance types:
 //   row = template options (static: within NodePool limits)
 //       AND_r  thr_set[r][lower_bound(thr_val_r, daemon_r + pod_r)]   (Fits)
 //       AND    OR_{pair g in grid(template, pod)} slot_set[g]          (offering)
-//       AND    IT-key requirement bits (only for variants that have IT-key
-//              requirements: lane = IT, __ballot per word)
-// nfo = sum_g popcount(row AND slot_set[g]); the cheapest instance type is
-// the first entry of the (price rank, name rank)-sorted offering list whose
-// IT is in the row and whose pair is in the grid (= OrderByPrice(...)[0]).
+//       AND    the IT-key requirement class mask (variants with IT-key
+//              requirements; one mask per distinct requirement set)
+// The threshold searches of all PP pairs run first, one lane per (pair,
+// resource), so the dependent binary-search chains overlap instead of
+// serialising per pair.  nfo = sum_g popcount(row AND slot_set[g]); the
+// cheapest instance type is the first entry of the (price rank, name
+// rank)-sorted offering list whose IT is in the row and whose pair is in the
+// grid (= OrderByPrice(...)[0]).
 // static_mode = 1 (gs_feasibility): a NodeClaim opened for the pod alone, with
 // the free-key Compatible check and the NodePool limits folded into the row.
 // static_mode = 0 (FFD): rows carry only the monotone predicates; the
 // free-key check against the fresh template goes to fk_ok[] because an
 // in-flight NodeClaim can gain keys that make a later pod compatible.
-extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode, uint32_t w_lo,
-                                                                uint32_t w_hi) {
-  __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's row (N <= 8192)
+namespace {
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace
+
+template <uint32_t LP>
+__global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode, uint32_t w_lo,
+                                                     uint32_t w_hi) {
+  constexpr uint32_t PP = 64 / LP;
+  __shared__ uint32_t s_cur[BLOCK / 64][PP][RMAX];
+  __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's rows (PP x LP words, or 128 when LP = 64)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // wave-uniform in SGPRs: the variant record is read in place
-  const uint32_t pair = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + wv);
-  if (pair >= d.V * d.T) return;  // wave-uniform
-  const uint32_t v = pair / d.T, t = pair % d.T;
+  const uint32_t sub = lane / LP, wl = lane % LP;
+  const uint32_t VT = d.V * d.T;
+  const uint32_t pair0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (BLOCK / 64) + wv) * PP);
+  if (pair0 >= VT) return;  // wave-uniform
+  const uint32_t W = d.W, OW = d.OW, R = d.R, T = d.T;
+
+  // <U> resources.Fits(Merge(daemon, pod), allocatable): one lane per
+  // (pair, resource) finds the first threshold >= the demand
+  for (uint32_t id = lane; id < PP * R; id += 64) {
+    const uint32_t s = id / R, r = id % R, p = pair0 + s;
+    uint32_t cur = 0;
+    if (p < VT) {
+      const uint32_t v = p / T, t = p % T;
+      const int64_t dem = d.tmpl[t].daemon[r] + d.pod_req[(size_t)d.vars[v].pod * R + r];
+      const uint32_t o = d.thr_off[r];
+      cur = o + r + lower_bound_i64(d.thr_val + o, d.thr_off[r + 1] - o, dem);
+    }
+    s_cur[wv][s][r] = cur;
+  }
+  wave_lds_sync();
+
+  const uint32_t pair = pair0 + sub;
+  const bool valid = pair < VT;
+  const uint32_t v = valid ? pair / T : 0, t = valid ? pair % T : 0;
   const VarRec& vr = d.vars[v];
   const TmplRec& tr = d.tmpl[t];
-  const uint32_t W = d.W, OW = d.OW, R = d.R;
-  uint64_t* rowout = d.rows + (size_t)pair * OW;
-
-  // wave-uniform parts of NodeClaim.CanAdd on a fresh NodeClaim
-  bool ok_all = (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
-  const bool fk_ok = var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
+  // per-pair parts of NodeClaim.CanAdd on a fresh NodeClaim (uniform in the group)
+  bool ok_all = valid && (tr.taints & ~vr.tol) == 0;  // <U> Taints.ToleratesPod
+  const bool fk_ok = valid && var_fk_ok(d, vr, d.t_fk + (size_t)t * d.F);
   if (static_mode) ok_all = ok_all && fk_ok;
   const uint64_t G = grid_of(tr.zm & vr.zm, tr.cm & vr.cm, d.Z, d.C), Gt = grid_of(tr.zm, tr.cm, d.Z, d.C);
   if (!G) ok_all = false;
-  // <U> resources.Fits(Merge(daemon, pod), allocatable): lane r finds the
-  // first threshold >= the demand of resource r (a two-level ballot search
-  // issuing all resources' loads together measured slower on C5: more
-  // memory instructions for the same latency)
-  uint32_t curs[RMAX];
-  {
-    uint32_t cur = 0;
-    if (lane < R) {
-      const int64_t dem = tr.daemon[lane] + d.pod_req[(size_t)vr.pod * R + lane];
-      const uint32_t o = d.thr_off[lane];
-      cur = o + lane + lower_bound_i64(d.thr_val + o, d.thr_off[lane + 1] - o, dem);
-    }
-    // every lane gets every cursor (shuffles in wave-uniform control flow)
-#pragma unroll
-    for (uint32_t r = 0; r < RMAX; r++) curs[r] = (uint32_t)__shfl((int)cur, (int)r);
-  }
-  bool itkeys = false;
-  for (uint32_t k = 0; k < d.K; k++) itkeys = itkeys || vr.itmask_off[k] != NONE;
+  // <U> compatible(it, reqs): it.Requirements.Intersects(reqs) on IT keys,
+  // precomputed per distinct IT-key requirement set (encoder classes)
+  const uint32_t itc = valid ? d.var_itclass[v] : NONE;
+  const uint64_t* itmask = itc != NONE ? d.itclass_mask + (size_t)itc * W : nullptr;
   const uint64_t* topts = (static_mode && tr.has_limits ? d.t_limopts : d.t_opts) + (size_t)t * W;
+  uint64_t* rowout = d.rows + (size_t)pair * OW;
+  const uint32_t* cur = s_cur[wv][sub];
 
   uint32_t nf = 0;
   uint64_t any = 0;
-  for (uint32_t w0 = 0; w0 < W; w0 += 64) {
-    const uint32_t w = w0 + lane;
+  for (uint32_t w0 = 0; w0 < W; w0 += LP) {
+    const uint32_t w = w0 + wl;
     uint64_t x = 0;
-    if (ok_all && w >= w_lo && w < w_hi) {  // this instance-type column shard
+    if (ok_all && w < W && w >= w_lo && w < w_hi) {  // this instance-type column shard
       x = topts[w];
 #pragma unroll
       for (uint32_t r = 0; r < RMAX; r++)
-        if (r < R) x &= d.thr_set[(size_t)curs[r] * OW + w];
+        if (r < R) x &= d.thr_set[(size_t)cur[r] * OW + w];
       if (G != Gt) {  // template options already have an offering on the template's grid
         uint64_t off = 0;
         for (uint64_t m = G; m; m &= m - 1) off |= d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w];
         x &= off;
       }
+      if (itmask) x &= itmask[w];
     }
-    if (itkeys && ok_all) {
-      // <U> compatible(it, reqs): it.Requirements.Intersects(reqs) on IT keys
-      const uint32_t wend = W - w0 < 64 ? W - w0 : 64;
-      for (uint32_t q = 0; q < wend; q++) {
-        const uint64_t wx = (uint64_t)__shfl((long long)x, q);
-        if (!wx) continue;  // wave-uniform
-        const uint32_t i = (w0 + q) * 64 + lane;
-        bool ok = (wx >> lane) & 1;
-        for (uint32_t k = 0; k < d.K && ok; k++) {
-          const uint32_t off = vr.itmask_off[k];
-          if (off == NONE) continue;
-          const uint32_t vid = d.it_vid[(size_t)k * d.N + i];
-          ok = (d.itmask[off + (vid >> 6)] >> (vid & 63)) & 1;
-        }
-        const uint64_t bits = __ballot(ok);
-        if (lane == q) x = bits;
-      }
-    }
-    if (w < W) {
+    if (valid && w < W) {
       rowout[w] = x;
-      if (w < 128) s_row[wv][w] = x;
+      if (LP < 64) s_row[wv][lane] = x;
+      else if (w < 128) s_row[wv][w] = x;
       // offerings: sum over grid pairs of row AND slot_set[g]
       // (the Solve's rows need neither the offering count nor the cheapest type)
       if (static_mode)
@@ -124,48 +132,65 @@ extern "C" __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, ui
     }
     any |= x;
   }
-  nf = wave_sum_u32(nf);
+  // group reductions (LP lanes, xor partners stay inside the group)
+#pragma unroll
+  for (uint32_t m = LP / 2; m >= 1; m >>= 1) nf += (uint32_t)__shfl_xor((int)nf, (int)m);
+  const uint64_t nonempty = __ballot(any != 0);
+  wave_lds_sync();
   uint32_t cheapest = NONE;
   uint64_t ckey = 0x7FFFFFFFFFFFFFFFull;  // INT64_MAX: none
-  if (static_mode && __ballot(any != 0)) {
+  if (static_mode) {
     // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
-    // IT is in the row and whose (zone, capacity type) pair is in the grid
-    // four 64-entry chunks in flight per step (deep scans are latency-bound)
+    // IT is in the row and whose (zone, capacity type) pair is in the grid;
+    // the whole wave scans for one pair at a time, four 64-entry chunks in
+    // flight per step (deep scans are latency-bound)
     constexpr uint32_t KS = 4;
-    for (uint32_t base = 0; base < d.n_off; base += 64 * KS) {
-      uint32_t e[KS];
+    for (uint32_t s = 0; s < PP; s++) {
+      const uint64_t gmask = (LP == 64 ? ~0ull : ((1ull << LP) - 1)) << (s * LP);
+      if (!(nonempty & gmask)) continue;  // wave-uniform
+      const uint64_t Gs = (uint64_t)__shfl((long long)G, (int)(s * LP));
+      const uint64_t* srow = s_row[wv] + (LP < 64 ? s * LP : 0);
+      uint32_t found = NONE;
+      uint64_t fkey = 0x7FFFFFFFFFFFFFFFull;
+      for (uint32_t base = 0; base < d.n_off; base += 64 * KS) {
+        uint32_t e[KS];
 #pragma unroll
-      for (uint32_t k = 0; k < KS; k++) {
-        const uint32_t j = base + k * 64 + lane;
-        e[k] = j < d.n_off ? d.off_sorted[j] : NONE;
-      }
-      uint64_t b = 0;
-      uint32_t kk = 0;
+        for (uint32_t k = 0; k < KS; k++) {
+          const uint32_t j = base + k * 64 + lane;
+          e[k] = j < d.n_off ? d.off_sorted[j] : NONE;
+        }
+        uint64_t b = 0;
+        uint32_t kk = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < KS; k++) {
-        const uint32_t i = e[k] & 0xFFFFu, g = e[k] >> 16;
-        const bool hit = e[k] != NONE && ((G >> g) & 1) && ((s_row[wv][i >> 6] >> (i & 63)) & 1);
-        const uint64_t bk = __ballot(hit);
-        if (!b && bk) {
-          b = bk;
-          kk = k;
+        for (uint32_t k = 0; k < KS; k++) {
+          const uint32_t i = e[k] & 0xFFFFu, g = e[k] >> 16;
+          const bool hit = e[k] != NONE && ((Gs >> g) & 1) && ((srow[i >> 6] >> (i & 63)) & 1);
+          const uint64_t bk = __ballot(hit);
+          if (!b && bk) {
+            b = bk;
+            kk = k;
+          }
+        }
+        if (b) {
+          const int src = (int)(__ffsll((long long)b) - 1);
+          uint32_t ek = e[0];
+#pragma unroll
+          for (uint32_t k = 1; k < KS; k++)
+            if (kk == k) ek = e[k];
+          const uint32_t esrc = (uint32_t)__shfl((int)ek, src);
+          found = esrc & 0xFFFFu;
+          const uint32_t gg = esrc >> 16;
+          fkey = ((uint64_t)d.it_prank[(size_t)found * 64 + gg] << 32) | d.it_namerank[found];
+          break;
         }
       }
-      if (b) {
-        const int src = (int)(__ffsll((long long)b) - 1);
-        uint32_t ek = e[0];
-#pragma unroll
-        for (uint32_t k = 1; k < KS; k++)
-          if (kk == k) ek = e[k];
-        const uint32_t esrc = (uint32_t)__shfl((int)ek, src);
-        cheapest = esrc & 0xFFFFu;
-        const uint32_t gg = esrc >> 16;
-        ckey = ((uint64_t)d.it_prank[(size_t)cheapest * 64 + gg] << 32) | d.it_namerank[cheapest];
-        break;
+      if (sub == s) {
+        cheapest = found;
+        ckey = fkey;
       }
     }
   }
-  if (lane == 0) {
+  if (valid && wl == 0) {
     d.fk_ok[pair] = fk_ok ? 1u : 0u;
     d.nfo[pair] = nf;
     d.cheapest[pair] = cheapest;
@@ -243,12 +268,26 @@ extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes) {
                              (int)trunc_lds_bytes);
 }
 
+template <uint32_t LP>
+static void launch_feas_lp(const DevProblem* d, uint32_t static_mode, uint32_t w_lo, uint32_t w_hi, hipStream_t s) {
+  const uint64_t pairs = (uint64_t)d->V * d->T;
+  const uint64_t per_block = (BLOCK / 64) * (64 / LP);
+  const uint32_t blocks = (uint32_t)((pairs + per_block - 1) / per_block);
+  hipLaunchKernelGGL(feas_kernel<LP>, dim3(blocks), dim3(BLOCK), 0, s, *d, static_mode, w_lo, w_hi);
+}
+
 extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, uint32_t w_lo, uint32_t w_hi,
                                hipStream_t s) {
-  const uint64_t pairs = (uint64_t)d->V * d->T;
-  if (!pairs) return hipSuccess;
-  const uint32_t blocks = (uint32_t)((pairs + (BLOCK / 64) - 1) / (BLOCK / 64));
-  hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(BLOCK), 0, s, *d, static_mode, w_lo, w_hi);
+  if (!d->V || !d->T) return hipSuccess;
+  // lanes per pair: the row's word count rounded up to a power of two
+  const uint32_t W = d->W;
+  if (W <= 1) launch_feas_lp<1>(d, static_mode, w_lo, w_hi, s);
+  else if (W <= 2) launch_feas_lp<2>(d, static_mode, w_lo, w_hi, s);
+  else if (W <= 4) launch_feas_lp<4>(d, static_mode, w_lo, w_hi, s);
+  else if (W <= 8) launch_feas_lp<8>(d, static_mode, w_lo, w_hi, s);
+  else if (W <= 16) launch_feas_lp<16>(d, static_mode, w_lo, w_hi, s);
+  else if (W <= 32) launch_feas_lp<32>(d, static_mode, w_lo, w_hi, s);
+  else launch_feas_lp<64>(d, static_mode, w_lo, w_hi, s);
   return hipGetLastError();
 }
 

@@ -201,6 +201,8 @@ struct DevProblem {
   const uint32_t* var_count;   // [P]
   const VarRec* vars;          // [V]
   const uint64_t* itmask;      // arena
+  const uint32_t* var_itclass; // [V] IT-key requirement class of each variant (NONE: no IT keys)
+  const uint64_t* itclass_mask;// [classes][W] instance types each class's IT-key requirements allow
   const FKEntry* fk_entries;
   const uint32_t* queue0;      // [P] initial queue order
   const VarRec* qvars;         // [P] first variant of queue0[k], in queue order (first-pass prefetch)
