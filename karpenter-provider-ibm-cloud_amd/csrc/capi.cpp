@@ -2,6 +2,8 @@
 // buffers, kernel launches on one HIP stream, result decode.
 #include "ctx.hpp"
 
+#include <set>
+
 namespace gsc {
 
 gs_status fail(gs_ctx* c, gs_status s, const std::string& m) {
@@ -48,8 +50,6 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.it_namerank, e.it_namerank);
   c->upload(d.rank_to_it, e.rank_to_it);
   c->upload(d.slot_set, e.slot_set);
-  c->upload(d.off_sorted, e.off_sorted);
-  d.n_off = (uint32_t)e.off_sorted.size();
   {
     std::vector<int64_t> tv = e.thr_val;  // 4 sentinels: the device reads a 4-wide window past each range
     tv.insert(tv.end(), 4, INT64_MAX);
@@ -173,7 +173,59 @@ uint32_t trunc_lds_bytes(uint32_t N) {
   return np2 * 8;
 }
 
+// <U> OrderByPrice(...)[0] tables for the static matrix: for every distinct
+// offering grid G = grid(template AND pod zones, template AND pod capacity
+// types), the instance types with an available offering in G, keyed and
+// sorted by (min price rank over G, name rank).  Built once per prepared
+// problem, on the first gs_feasibility.
+uint64_t host_grid_of(uint64_t zm, uint64_t cm, uint32_t Z, uint32_t C) {
+  const uint64_t cmask = C >= 64 ? ~0ull : ((1ull << C) - 1);
+  uint64_t g = 0;
+  for (uint32_t z = 0; z < Z; z++)
+    if ((zm >> z) & 1) g |= (cm & cmask) << (z * C);
+  return g;
+}
+
+void build_grid_orders(gs_ctx* c) {
+  auto& e = c->enc;
+  auto& d = c->dp;
+  if (d.grid_list) return;
+  std::set<std::pair<uint64_t, uint64_t>> zc;
+  for (uint32_t v = 0; v < e.V; v++) zc.insert({e.vars[v].zm, e.vars[v].cm});
+  std::set<uint64_t> gs;
+  for (uint32_t t = 0; t < e.T; t++)
+    for (auto& m : zc) gs.insert(host_grid_of(e.tmpl[t].zm & m.first, e.tmpl[t].cm & m.second, e.Z, e.C));
+  std::vector<uint64_t> list(gs.begin(), gs.end()), keys;
+  std::vector<uint32_t> off{0};
+  for (uint64_t G : list) {
+    const size_t b = keys.size();
+    for (uint32_t i = 0; i < e.N; i++) {
+      uint32_t mp = gsd::NONE;
+      for (uint64_t m = e.it_pair[i] & G; m; m &= m - 1) mp = std::min(mp, e.it_prank[(size_t)i * 64 + __builtin_ctzll(m)]);
+      if (mp != gsd::NONE) keys.push_back(((uint64_t)mp << 32) | e.it_namerank[i]);
+    }
+    std::sort(keys.begin() + b, keys.end());
+    off.push_back((uint32_t)keys.size());
+  }
+  if (keys.empty()) keys.push_back(0);
+  const size_t bl = list.size() * 8, bo = off.size() * 4, bk = keys.size() * 8;
+  char* p = nullptr;
+  HIPCHK(hipMalloc((void**)&p, bl + bo + bk + 512));
+  c->allocs.push_back(p);
+  char* po = p + ((bl + 255) & ~(size_t)255);
+  char* pk = po + ((bo + 255) & ~(size_t)255);
+  HIPCHK(hipMemcpyAsync(p, list.data(), bl, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(po, off.data(), bo, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(pk, keys.data(), bk, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  d.grid_list = (const uint64_t*)p;
+  d.grid_off = (const uint32_t*)po;
+  d.grid_keys = (const uint64_t*)pk;
+  d.n_grids = (uint32_t)list.size();
+}
+
 void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u) {
+  if (apply_limits) build_grid_orders(c);
   HIPCHK(gsk_feas(&c->dp, apply_limits, w_lo, w_hi, c->stream));
 }
 

@@ -557,17 +557,6 @@ struct Ctx {
     for (uint32_t i = 0; i < e.N; i++)
       for (uint32_t g = 0; g < 64; g++)
         if (e.it_pair[i] >> g & 1) e.slot_set[(size_t)g * e.W + i / 64] |= 1ull << (i % 64);
-    // available offerings in OrderByPrice key order: (price rank, name rank)
-    e.off_sorted.clear();
-    for (uint32_t i = 0; i < e.N; i++)
-      for (uint32_t g = 0; g < 64; g++)
-        if (e.it_pair[i] >> g & 1) e.off_sorted.push_back(i | (g << 16));
-    std::sort(e.off_sorted.begin(), e.off_sorted.end(), [&](uint32_t a, uint32_t b) {
-      const uint32_t ia = a & 0xFFFFu, ib = b & 0xFFFFu;
-      const uint64_t ka = ((uint64_t)e.it_prank[(size_t)ia * 64 + (a >> 16)] << 32) | e.it_namerank[ia];
-      const uint64_t kb = ((uint64_t)e.it_prank[(size_t)ib * 64 + (b >> 16)] << 32) | e.it_namerank[ib];
-      return ka != kb ? ka < kb : a < b;
-    });
     // fit thresholds per resource over selectable ITs
     e.thr_off.assign(e.R + 1, 0);
     std::vector<std::vector<int64_t>> vals(e.R);

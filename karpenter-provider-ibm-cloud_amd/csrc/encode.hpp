@@ -103,7 +103,6 @@ struct Encoded {
   std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
   std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
   std::vector<double> prices;  // distinct offering prices ascending: price rank -> price
-  std::vector<uint32_t> off_sorted;  // available offerings (it | pair << 16) by (price rank, name rank)
   std::vector<uint64_t> t_limopts;   // [T][W] template options within the NodePool limits (static matrix)
   std::vector<gsd::TmplRec> tmpl;
   std::vector<uint64_t> t_opts;

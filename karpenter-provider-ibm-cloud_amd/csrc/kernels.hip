@@ -39,9 +39,8 @@ constexpr int BLOCK = 256;
 // The threshold searches of all PP pairs run first, one lane per (pair,
 // resource), so the dependent binary-search chains overlap instead of
 // serialising per pair.  nfo = sum_g popcount(row AND slot_set[g]); the
-// cheapest instance type is the first entry of the (price rank, name
-// rank)-sorted offering list whose IT is in the row and whose pair is in the
-// grid (= OrderByPrice(...)[0]).
+// cheapest instance type (= OrderByPrice(...)[0]) is the first instance type
+// of the pair's grid order (capi.cpp build_grid_orders) that is in the row.
 // static_mode = 1 (gs_feasibility): a NodeClaim opened for the pod alone, with
 // the free-key Compatible check and the NodePool limits folded into the row.
 // static_mode = 0 (FFD): rows carry only the monotone predicates; the
@@ -140,47 +139,37 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
   uint32_t cheapest = NONE;
   uint64_t ckey = 0x7FFFFFFFFFFFFFFFull;  // INT64_MAX: none
   if (static_mode) {
-    // <U> OrderByPrice(...)[0]: first (price rank, name rank) offering whose
-    // IT is in the row and whose (zone, capacity type) pair is in the grid;
-    // the whole wave scans for one pair at a time, four 64-entry chunks in
-    // flight per step (deep scans are latency-bound)
-    constexpr uint32_t KS = 4;
+    // <U> OrderByPrice(...)[0]: the pair's grid G indexes a list of the
+    // instance types with an available offering in G, sorted by (min price
+    // rank over G, name rank); the first one in the row is the cheapest.  The
+    // whole wave scans for one pair at a time, 64 keys per step.
+    uint32_t gi = 0;
+    {
+      uint32_t lo = 0, hi = d.n_grids;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (d.grid_list[m] < G) lo = m + 1;
+        else hi = m;
+      }
+      gi = lo;
+    }
     for (uint32_t s = 0; s < PP; s++) {
       const uint64_t gmask = (LP == 64 ? ~0ull : ((1ull << LP) - 1)) << (s * LP);
       if (!(nonempty & gmask)) continue;  // wave-uniform
-      const uint64_t Gs = (uint64_t)__shfl((long long)G, (int)(s * LP));
+      const uint32_t g = (uint32_t)__shfl((int)gi, (int)(s * LP));
+      const uint32_t kb = d.grid_off[g], ke = d.grid_off[g + 1];
       const uint64_t* srow = s_row[wv] + (LP < 64 ? s * LP : 0);
       uint32_t found = NONE;
       uint64_t fkey = 0x7FFFFFFFFFFFFFFFull;
-      for (uint32_t base = 0; base < d.n_off; base += 64 * KS) {
-        uint32_t e[KS];
-#pragma unroll
-        for (uint32_t k = 0; k < KS; k++) {
-          const uint32_t j = base + k * 64 + lane;
-          e[k] = j < d.n_off ? d.off_sorted[j] : NONE;
-        }
-        uint64_t b = 0;
-        uint32_t kk = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < KS; k++) {
-          const uint32_t i = e[k] & 0xFFFFu, g = e[k] >> 16;
-          const bool hit = e[k] != NONE && ((Gs >> g) & 1) && ((srow[i >> 6] >> (i & 63)) & 1);
-          const uint64_t bk = __ballot(hit);
-          if (!b && bk) {
-            b = bk;
-            kk = k;
-          }
-        }
+      for (uint32_t base = kb; base < ke; base += 64) {
+        const uint32_t j = base + lane;
+        const uint64_t key = j < ke ? d.grid_keys[j] : ~0ull;
+        const uint32_t i = j < ke ? d.rank_to_it[(uint32_t)key] : 0u;
+        const uint64_t b = __ballot(j < ke && ((srow[i >> 6] >> (i & 63)) & 1));
         if (b) {
           const int src = (int)(__ffsll((long long)b) - 1);
-          uint32_t ek = e[0];
-#pragma unroll
-          for (uint32_t k = 1; k < KS; k++)
-            if (kk == k) ek = e[k];
-          const uint32_t esrc = (uint32_t)__shfl((int)ek, src);
-          found = esrc & 0xFFFFu;
-          const uint32_t gg = esrc >> 16;
-          fkey = ((uint64_t)d.it_prank[(size_t)found * 64 + gg] << 32) | d.it_namerank[found];
+          fkey = (uint64_t)__shfl((long long)key, src);
+          found = (uint32_t)__shfl((int)i, src);
           break;
         }
       }

@@ -183,8 +183,14 @@ struct DevProblem {
   const uint32_t* it_namerank; // [N]
   const uint32_t* rank_to_it;  // [N]
   const uint64_t* slot_set;    // [64][W] ITs with an available offering on pair g
-  const uint32_t* off_sorted;  // [n_off] available offerings (it | pair << 16) in (price rank, name rank) order
-  uint32_t n_off, pad_off;
+  // OrderByPrice per distinct offering grid G (gs_feasibility only, built
+  // on first use): grid_list sorted; the instance types with an available
+  // offering in G as keys (min price rank over G << 32 | name rank), ascending,
+  // at grid_keys[grid_off[g] .. grid_off[g+1])
+  const uint64_t* grid_list;
+  const uint32_t* grid_off;
+  const uint64_t* grid_keys;
+  uint32_t n_grids, pad_grid;
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
   const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
