@@ -265,10 +265,27 @@ enum {
   GS_CFG_BLOCK_SOLVE = 1u << 0
 };
 
+/* One Go process, several devices: with n_shards > 1 the context owns one
+ * child context per shard (HIP device shard_devices[k], a device may repeat)
+ * and, from ONE calling thread, runs
+ *  - gs_consolidate / gs_consolidate_rerun: simulation s on shard s % n, in
+ *    parallel (one host thread per shard), then merges the command tables and
+ *    replays SingleNode/MultiNode selection (gs_consolidation_choose) on the
+ *    host: the result is identical to the single-device call;
+ *  - gs_feasibility / gs_feasibility_shard: the requested instance-type words
+ *    split evenly over the shards; rows are disjoint (copied), offering counts
+ *    added, the cheapest taken as the minimum OrderByPrice key;
+ *  - the provisioning Solve (gs_prepare/gs_run/gs_fetch) on `device` only: it
+ *    is sequential in pod order and does not shard.
+ * gs_prepare also encodes and uploads the problem on every shard (in parallel).
+ * gs_feasibility_shard_device refuses a sharded context (its results live in
+ * one device's memory: use one context per device there). */
 typedef struct gs_config {
-  int32_t device;        /* HIP device ordinal */
+  int32_t device;        /* HIP device ordinal (the Solve's device) */
   uint32_t max_claims;   /* 0 = default */
   uint32_t flags;        /* GS_CFG_* */
+  uint32_t n_shards;     /* 0 or 1: single device */
+  const int32_t* shard_devices; /* [n_shards] device per shard; NULL: `device` for every shard */
 } gs_config;
 
 /* ------------------------------------------------------------------------

@@ -125,6 +125,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->alloc(d.cheapest_key, VT);
   c->alloc(d.nfo, VT);
   c->alloc(d.fk_ok, VT);
+  c->alloc(d.pair_cur, VT * R1);
   c->alloc(d.queue, PA);
   c->alloc(d.last_len, PA);
   c->alloc(d.last_epoch, PA);
@@ -196,32 +197,59 @@ void build_grid_orders(gs_ctx* c) {
   for (uint32_t t = 0; t < e.T; t++)
     for (auto& m : zc) gs.insert(host_grid_of(e.tmpl[t].zm & m.first, e.tmpl[t].cm & m.second, e.Z, e.C));
   std::vector<uint64_t> list(gs.begin(), gs.end()), keys;
-  std::vector<uint32_t> off{0};
-  for (uint64_t G : list) {
+  std::vector<uint32_t> off{0}, its;
+  uint32_t max_cnt = 0;
+  for (uint64_t G : list) max_cnt = std::max<uint32_t>(max_cnt, (uint32_t)__builtin_popcountll(G));
+  uint32_t NPL = 1;
+  while ((1u << NPL) <= max_cnt) NPL++;
+  std::vector<uint64_t> planes(std::max<size_t>(list.size(), 1) * NPL * e.W, 0);
+  for (size_t g = 0; g < list.size(); g++) {
+    const uint64_t G = list[g];
     const size_t b = keys.size();
+    std::vector<std::pair<uint64_t, uint32_t>> ki;
     for (uint32_t i = 0; i < e.N; i++) {
       uint32_t mp = gsd::NONE;
       for (uint64_t m = e.it_pair[i] & G; m; m &= m - 1) mp = std::min(mp, e.it_prank[(size_t)i * 64 + __builtin_ctzll(m)]);
-      if (mp != gsd::NONE) keys.push_back(((uint64_t)mp << 32) | e.it_namerank[i]);
+      if (mp != gsd::NONE) ki.push_back({((uint64_t)mp << 32) | e.it_namerank[i], i});
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(e.it_pair[i] & G);
+      for (uint32_t pb = 0; pb < NPL; pb++)
+        if ((cnt >> pb) & 1) planes[(g * NPL + pb) * e.W + i / 64] |= 1ull << (i % 64);
     }
-    std::sort(keys.begin() + b, keys.end());
+    std::sort(ki.begin(), ki.end());
+    for (auto& x : ki) {
+      keys.push_back(x.first);
+      its.push_back(x.second);
+    }
+    (void)b;
     off.push_back((uint32_t)keys.size());
   }
-  if (keys.empty()) keys.push_back(0);
-  const size_t bl = list.size() * 8, bo = off.size() * 4, bk = keys.size() * 8;
+  if (keys.empty()) {
+    keys.push_back(0);
+    its.push_back(0);
+  }
+  const size_t bl = list.size() * 8, bo = off.size() * 4, bk = keys.size() * 8, bi = its.size() * 4,
+               bp = planes.size() * 8;
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   char* p = nullptr;
-  HIPCHK(hipMalloc((void**)&p, bl + bo + bk + 512));
+  HIPCHK(hipMalloc((void**)&p, up(bl) + up(bo) + up(bk) + up(bi) + up(bp)));
   c->allocs.push_back(p);
-  char* po = p + ((bl + 255) & ~(size_t)255);
-  char* pk = po + ((bo + 255) & ~(size_t)255);
+  char* po = p + up(bl);
+  char* pk = po + up(bo);
+  char* pi = pk + up(bk);
+  char* pp = pi + up(bi);
   HIPCHK(hipMemcpyAsync(p, list.data(), bl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(po, off.data(), bo, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(pk, keys.data(), bk, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(pi, its.data(), bi, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(pp, planes.data(), bp, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   d.grid_list = (const uint64_t*)p;
   d.grid_off = (const uint32_t*)po;
   d.grid_keys = (const uint64_t*)pk;
+  d.grid_its = (const uint32_t*)pi;
+  d.grid_planes = (const uint64_t*)pp;
   d.n_grids = (uint32_t)list.size();
+  d.n_planes = NPL;
 }
 
 void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u) {
@@ -237,6 +265,28 @@ gsh::Err capacity_check(const gsh::Encoded& e) {
   if ((size_t)e.Z * e.C * e.W > gsd::SLOT_LDS_MAX)
     return gsh::Err{GS_E_CAPACITY, "zones x capacity types x instance-type words exceeds 1024"};
   return gsh::Err{GS_OK, ""};
+}
+
+gs_status prepare_one(gs_ctx* c, const gs_problem* p) {
+  c->prepared = c->ran = false;
+  c->cons_ready = false;
+  auto t0 = Clock::now();
+  gsh::Err er = gsh::encode(p, c->enc);
+  c->t_encode = ms_since(t0);
+  if (er.code != GS_OK) return fail(c, er.code, er.msg);
+  er = capacity_check(c->enc);
+  if (er.code != GS_OK) return fail(c, er.code, er.msg);
+  c->n_nodepools = p->n_nodepools;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    auto t1 = Clock::now();
+    upload_problem(c, nullptr);
+    c->t_upload = ms_since(t1);
+  } catch (const HipError& e) {
+    return fail(c, GS_E_HIP, e.msg);
+  }
+  c->prepared = true;
+  return GS_OK;
 }
 
 }  // namespace gsc
@@ -308,12 +358,29 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     delete c;
     return GS_E_HIP;
   }
+  if (cfg && cfg->n_shards > 1) {
+    for (uint32_t k = 0; k < cfg->n_shards; k++) {
+      gs_config sc = *cfg;
+      sc.device = cfg->shard_devices ? cfg->shard_devices[k] : cfg->device;
+      sc.n_shards = 0;
+      sc.shard_devices = nullptr;
+      gs_ctx* child = nullptr;
+      const gs_status st = gs_create(&sc, &child);
+      if (st != GS_OK) {
+        gs_destroy(c);
+        return st;
+      }
+      c->shards.push_back(child);
+    }
+  }
   *out = c;
   return GS_OK;
 }
 
 void gs_destroy(gs_ctx* c) {
   if (!c) return;
+  for (gs_ctx* s : c->shards) gs_destroy(s);
+  c->shards.clear();
   (void)hipSetDevice(c->device);
   c->free_all();
   if (c->cf_dev) (void)hipFree(c->cf_dev);
@@ -325,25 +392,8 @@ void gs_destroy(gs_ctx* c) {
 
 gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   if (!c || !p) return GS_E_INVALID;
-  c->prepared = c->ran = false;
-  c->cons_ready = false;
-  auto t0 = Clock::now();
-  gsh::Err er = gsh::encode(p, c->enc);
-  c->t_encode = ms_since(t0);
-  if (er.code != GS_OK) return fail(c, er.code, er.msg);
-  er = capacity_check(c->enc);
-  if (er.code != GS_OK) return fail(c, er.code, er.msg);
-  c->n_nodepools = p->n_nodepools;
-  try {
-    HIPCHK(hipSetDevice(c->device));
-    auto t1 = Clock::now();
-    upload_problem(c, nullptr);
-    c->t_upload = ms_since(t1);
-  } catch (const HipError& e) {
-    return fail(c, GS_E_HIP, e.msg);
-  }
-  c->prepared = true;
-  return GS_OK;
+  if (!c->shards.empty()) return sharded_prepare(c, p);
+  return prepare_one(c, p);
 }
 
 gs_status gs_run(gs_ctx* c) {
@@ -528,6 +578,7 @@ gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
 
 gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
+  if (!c->shards.empty()) return sharded_feasibility(c, word_begin, word_end, out);
   auto& e = c->enc;
   const uint32_t P = e.P, NP = c->n_nodepools, W = e.W;
   word_end = std::min(word_end, W);
@@ -588,6 +639,8 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) { return gs_feasibility
 
 gs_status gs_feasibility_shard_device(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_device* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
+  if (!c->shards.empty())
+    return fail(c, GS_E_UNSUPPORTED, "device-resident shard results on a sharded context (use one context per device)");
   auto& e = c->enc;
   word_end = std::min(word_end, e.W);
   if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");

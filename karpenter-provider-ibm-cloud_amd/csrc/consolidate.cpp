@@ -454,6 +454,16 @@ gs_status check_input(const gs_consolidation* in, std::string* err) {
 }
 
 }  // namespace
+
+// the host policy replay over a complete command table (gs_consolidation_choose
+// and the sharded context's merge)
+int32_t choose_commands(const CandTable& t, const gs_consolidation* in, const gs_command* commands,
+                        const uint32_t* options, const double* prices, std::vector<uint32_t>* multi) {
+  SimPlan sp;
+  std::string err;
+  if (build_sets(in, sp, &err) != GS_OK) return -1;
+  return choose(t, in->mode, sp.sets, sp.multi_max, commands, options, prices, multi);
+}
 }  // namespace gsc
 
 using namespace gsc;
@@ -465,6 +475,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   std::string err;
   gs_status st = check_input(in, &err);
   if (st != GS_OK) return fail(c, st, err);
+  if (!c->shards.empty()) return sharded_consolidate(c, in, out);
   c->prepared = c->ran = false;
   // own copies of the caller's candidate arrays (gs_consolidate_rerun)
   c->cons_cands.assign(in->candidates, in->candidates + in->n_candidates);
@@ -508,6 +519,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
 
 gs_status gs_consolidate_rerun(gs_ctx* c, gs_consolidation_result* out) {
   if (!c || !out || !c->cons_ready) return GS_E_INVALID;
+  if (!c->shards.empty()) return sharded_consolidate(c, nullptr, out);
   return run_and_decide(c, out);
 }
 

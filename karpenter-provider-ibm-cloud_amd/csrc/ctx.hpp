@@ -80,6 +80,7 @@ struct SimPlan {
 struct gs_ctx {
   int device = 0;
   uint32_t cfg_flags = 0;  // gs_config.flags
+  std::vector<gs_ctx*> shards;  // gs_config.n_shards > 1: one child context per shard (multi.cpp)
   std::string err;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
@@ -174,6 +175,14 @@ struct gs_ctx {
 namespace gsc {
 
 gs_status fail(gs_ctx* c, gs_status s, const std::string& m);
+gs_status prepare_one(gs_ctx* c, const gs_problem* p);  // gs_prepare on one device
+// multi.cpp: contexts with shards
+gs_status sharded_prepare(gs_ctx* c, const gs_problem* p);
+gs_status sharded_feasibility(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out);
+gs_status sharded_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation_result* out);
+CandTable build_cand_table(const gs_problem* p, const uint32_t* cands, uint32_t n);
+int32_t choose_commands(const CandTable& t, const gs_consolidation* in, const gs_command* commands,
+                        const uint32_t* options, const double* prices, std::vector<uint32_t>* multi);
 gsh::Err capacity_check(const gsh::Encoded& e);
 uint32_t trunc_lds_bytes(uint32_t N);
 // encode output -> device arena; `sims` non-null: consolidation arenas

@@ -56,11 +56,25 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 }  // namespace
 
+// <U> resources.Fits(Merge(daemon, pod), allocatable) cursors, one lane per
+// (variant, template, resource): the first threshold >= the demand.  A pass of
+// its own so that the dependent binary-search loads of all pairs overlap.
+__global__ __launch_bounds__(BLOCK) void feas_cursor_kernel(DevProblem d) {
+  const uint32_t R = d.R, T = d.T;
+  const uint64_t id = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (id >= (uint64_t)d.V * T * R) return;
+  const uint32_t r = (uint32_t)(id % R);
+  const uint64_t pair = id / R;
+  const uint32_t v = (uint32_t)(pair / T), t = (uint32_t)(pair % T);
+  const int64_t dem = d.tmpl[t].daemon[r] + d.pod_req[(size_t)d.vars[v].pod * R + r];
+  const uint32_t o = d.thr_off[r];
+  d.pair_cur[id] = o + r + lower_bound_i64(d.thr_val + o, d.thr_off[r + 1] - o, dem);
+}
+
 template <uint32_t LP>
 __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode, uint32_t w_lo,
                                                      uint32_t w_hi) {
   constexpr uint32_t PP = 64 / LP;
-  __shared__ uint32_t s_cur[BLOCK / 64][PP][RMAX];
   __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's rows (PP x LP words, or 128 when LP = 64)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t sub = lane / LP, wl = lane % LP;
@@ -68,21 +82,6 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
   const uint32_t pair0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (BLOCK / 64) + wv) * PP);
   if (pair0 >= VT) return;  // wave-uniform
   const uint32_t W = d.W, OW = d.OW, R = d.R, T = d.T;
-
-  // <U> resources.Fits(Merge(daemon, pod), allocatable): one lane per
-  // (pair, resource) finds the first threshold >= the demand
-  for (uint32_t id = lane; id < PP * R; id += 64) {
-    const uint32_t s = id / R, r = id % R, p = pair0 + s;
-    uint32_t cur = 0;
-    if (p < VT) {
-      const uint32_t v = p / T, t = p % T;
-      const int64_t dem = d.tmpl[t].daemon[r] + d.pod_req[(size_t)d.vars[v].pod * R + r];
-      const uint32_t o = d.thr_off[r];
-      cur = o + r + lower_bound_i64(d.thr_val + o, d.thr_off[r + 1] - o, dem);
-    }
-    s_cur[wv][s][r] = cur;
-  }
-  wave_lds_sync();
 
   const uint32_t pair = pair0 + sub;
   const bool valid = pair < VT;
@@ -101,7 +100,21 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
   const uint64_t* itmask = itc != NONE ? d.itclass_mask + (size_t)itc * W : nullptr;
   const uint64_t* topts = (static_mode && tr.has_limits ? d.t_limopts : d.t_opts) + (size_t)t * W;
   uint64_t* rowout = d.rows + (size_t)pair * OW;
-  const uint32_t* cur = s_cur[wv][sub];
+  uint32_t cur[RMAX];
+#pragma unroll
+  for (uint32_t r = 0; r < RMAX; r++) cur[r] = valid && r < R ? d.pair_cur[(size_t)pair * R + r] : 0u;
+  // static matrix: the pair's grid in the OrderByPrice tables (capi.cpp build_grid_orders)
+  uint32_t gi = 0;
+  if (static_mode) {
+    uint32_t lo = 0, hi = d.n_grids;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (d.grid_list[m] < G) lo = m + 1;
+      else hi = m;
+    }
+    gi = lo;
+  }
+  const uint64_t* planes = d.grid_planes + (size_t)gi * d.n_planes * W;
 
   uint32_t nf = 0;
   uint64_t any = 0;
@@ -126,8 +139,8 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
       else if (w < 128) s_row[wv][w] = x;
       // offerings: sum over grid pairs of row AND slot_set[g]
       // (the Solve's rows need neither the offering count nor the cheapest type)
-      if (static_mode)
-        for (uint64_t m = G; m; m &= m - 1) nf += __popcll(x & d.slot_set[(size_t)(__ffsll((long long)m) - 1) * W + w]);
+      if (static_mode && G)
+        for (uint32_t b = 0; b < d.n_planes; b++) nf += (uint32_t)__popcll(x & planes[(size_t)b * W + w]) << b;
     }
     any |= x;
   }
@@ -141,42 +154,36 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
   if (static_mode) {
     // <U> OrderByPrice(...)[0]: the pair's grid G indexes a list of the
     // instance types with an available offering in G, sorted by (min price
-    // rank over G, name rank); the first one in the row is the cheapest.  The
-    // whole wave scans for one pair at a time, 64 keys per step.
-    uint32_t gi = 0;
-    {
-      uint32_t lo = 0, hi = d.n_grids;
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (d.grid_list[m] < G) lo = m + 1;
-        else hi = m;
+    // rank over G, name rank); the first one in the row is the cheapest.
+    // Every lane group scans its own pair's list, KS x LP keys per step.
+    constexpr uint32_t KS = LP >= 16 ? 2 : (64 / LP > 8 ? 8 : 64 / LP);
+    const uint64_t gmask = (LP == 64 ? ~0ull : ((1ull << LP) - 1)) << (sub * LP);
+    const uint32_t kb = d.grid_off[gi], ke = d.grid_off[gi + 1];
+    const uint64_t* srow = s_row[wv] + (LP < 64 ? sub * LP : 0);
+    bool active = valid && ((nonempty & gmask) != 0);
+    for (uint32_t base = kb; __ballot(active); base += KS * LP) {
+      uint32_t it[KS];
+      bool hit[KS];
+#pragma unroll
+      for (uint32_t k = 0; k < KS; k++) {
+        const uint32_t j = base + k * LP + wl;
+        it[k] = active && j < ke ? d.grid_its[j] : NONE;
       }
-      gi = lo;
-    }
-    for (uint32_t s = 0; s < PP; s++) {
-      const uint64_t gmask = (LP == 64 ? ~0ull : ((1ull << LP) - 1)) << (s * LP);
-      if (!(nonempty & gmask)) continue;  // wave-uniform
-      const uint32_t g = (uint32_t)__shfl((int)gi, (int)(s * LP));
-      const uint32_t kb = d.grid_off[g], ke = d.grid_off[g + 1];
-      const uint64_t* srow = s_row[wv] + (LP < 64 ? s * LP : 0);
-      uint32_t found = NONE;
-      uint64_t fkey = 0x7FFFFFFFFFFFFFFFull;
-      for (uint32_t base = kb; base < ke; base += 64) {
-        const uint32_t j = base + lane;
-        const uint64_t key = j < ke ? d.grid_keys[j] : ~0ull;
-        const uint32_t i = j < ke ? d.rank_to_it[(uint32_t)key] : 0u;
-        const uint64_t b = __ballot(j < ke && ((srow[i >> 6] >> (i & 63)) & 1));
-        if (b) {
-          const int src = (int)(__ffsll((long long)b) - 1);
-          fkey = (uint64_t)__shfl((long long)key, src);
-          found = (uint32_t)__shfl((int)i, src);
-          break;
-        }
+#pragma unroll
+      for (uint32_t k = 0; k < KS; k++) hit[k] = it[k] != NONE && ((srow[it[k] >> 6] >> (it[k] & 63)) & 1);
+      uint32_t first = NONE;
+#pragma unroll
+      for (uint32_t k = 0; k < KS; k++) {
+        const uint64_t bk = __ballot(hit[k]) & gmask;
+        if (first == NONE && bk) first = k * LP + ((uint32_t)__ffsll((long long)bk) - 1 - sub * LP);
       }
-      if (sub == s) {
-        cheapest = found;
-        ckey = fkey;
+      if (active && first != NONE) {
+        const uint32_t j = base + first;
+        cheapest = d.grid_its[j];
+        ckey = d.grid_keys[j];
+        active = false;
       }
+      if (base + KS * LP >= ke) active = false;
     }
   }
   if (valid && wl == 0) {
@@ -268,6 +275,8 @@ static void launch_feas_lp(const DevProblem* d, uint32_t static_mode, uint32_t w
 extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, uint32_t w_lo, uint32_t w_hi,
                                hipStream_t s) {
   if (!d->V || !d->T) return hipSuccess;
+  const uint64_t nc = (uint64_t)d->V * d->T * d->R;
+  if (nc) hipLaunchKernelGGL(feas_cursor_kernel, dim3((uint32_t)((nc + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, *d);
   // lanes per pair: the row's word count rounded up to a power of two
   const uint32_t W = d->W;
   if (W <= 1) launch_feas_lp<1>(d, static_mode, w_lo, w_hi, s);

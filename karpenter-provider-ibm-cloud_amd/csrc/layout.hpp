@@ -187,10 +187,15 @@ struct DevProblem {
   // on first use): grid_list sorted; the instance types with an available
   // offering in G as keys (min price rank over G << 32 | name rank), ascending,
   // at grid_keys[grid_off[g] .. grid_off[g+1])
+  // grid_its: the same instance types' indices; grid_planes[g][b][W]: bit b
+  // of |available offerings of i in G| for every instance type i (the
+  // offering count of a row is sum_b popcount(row AND plane b) << b)
   const uint64_t* grid_list;
   const uint32_t* grid_off;
   const uint64_t* grid_keys;
-  uint32_t n_grids, pad_grid;
+  const uint32_t* grid_its;
+  const uint64_t* grid_planes;
+  uint32_t n_grids, n_planes;
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
   const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
@@ -223,6 +228,7 @@ struct DevProblem {
   uint64_t* cheapest_key;      // [V][T] (price_rank << 32 | name_rank), INT64_MAX = none
   uint32_t* nfo;               // [V][T]
   uint32_t* fk_ok;             // [V][T] free-key Compatible vs the fresh template
+  uint32_t* pair_cur;          // [V][T][R] Fits threshold cursors (feas_cursor_kernel)
   // FFD state
   uint32_t* queue;             // [P]
   uint32_t* last_len;          // [P]

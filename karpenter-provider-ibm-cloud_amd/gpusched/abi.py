@@ -139,7 +139,8 @@ GS_CFG_BLOCK_SOLVE = 1  # gs_config.flags: run the Solve on the block kernel
 
 
 class GsConfig(C.Structure):
-    _fields_ = [("device", C.c_int32), ("max_claims", _U32), ("flags", _U32)]
+    _fields_ = [("device", C.c_int32), ("max_claims", _U32), ("flags", _U32), ("n_shards", _U32),
+                ("shard_devices", C.POINTER(C.c_int32))]
 
 
 def _arr(ptr, n, dtype):

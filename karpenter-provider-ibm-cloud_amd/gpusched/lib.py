@@ -137,11 +137,15 @@ class Solver:
     """One gs_ctx on one device (karpenter-core drives one provisioning
     Solve and one consolidation simulation at a time per context)."""
 
-    def __init__(self, device=0, flags=0):
+    def __init__(self, device=0, flags=0, shard_devices=None):
         self.L = load()
         self.ctx = C.c_void_p()
         self.flags = flags
         cfg = abi.GsConfig(device, 0, flags)
+        if shard_devices:
+            self._shards = (C.c_int32 * len(shard_devices))(*shard_devices)
+            cfg.n_shards = len(shard_devices)
+            cfg.shard_devices = self._shards
         st = self.L.gs_create(C.byref(cfg), C.byref(self.ctx))
         if st != abi.GS_OK:
             raise GpuSchedError(st, "gs_create failed (no gfx950 device?)")

@@ -1,0 +1,103 @@
+"""Library-owned multi-GPU (gs_config.n_shards, csrc/multi.cpp): one context
+drives several shard contexts from one calling thread — the single-process
+flow a Go controller uses.  Shards may share a device, so a
+one-GPU box exercises the whole path (child contexts, per-shard host threads,
+merge, host policy replay).
+
+Every sharded result must equal the single-device result bit for bit:
+consolidation commands / chosen / multi options (SINGLE, MULTI, EVAL, and the
+reruns), the static feasibility matrix (rows, cheapest, offering counts,
+OrderByPrice keys, sub-ranges of words), and the Solve (parent device).
+"""
+import numpy as np
+import pytest
+
+from gpusched import abi, synth
+from gpusched.consolidation import ConsolidationInput
+
+pytestmark = pytest.mark.gpu
+
+SHARDS = [[0, 0], [0, 0, 0]]
+
+
+@pytest.fixture(scope="module")
+def single():
+    from gpusched import lib
+    s = lib.Solver()
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="module", params=SHARDS, ids=["2shards", "3shards"])
+def sharded(request):
+    from gpusched import lib
+    s = lib.Solver(shard_devices=request.param)
+    yield s
+    s.close()
+
+
+def _cons(kind, seed):
+    if kind == "rand":
+        return synth.random_consolidation(seed)
+    return synth.make_c4(n_nodes=60, n_pending=4, seed=seed, util=(0.9, 0.99), full_frac=0.5, big_frac=1.0, pack=True)
+
+
+@pytest.mark.parametrize("kind,seed", [("rand", s) for s in range(6)] + [("c4", 0), ("c4", 1)])
+@pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
+def test_sharded_consolidation_equals_single(single, sharded, kind, seed, mode):
+    p = _cons(kind, seed)
+    cands = list(range(len(p.nodes)))
+    want = single.consolidate(ConsolidationInput(p, cands, mode=mode))[:3]
+    got = sharded.consolidate(ConsolidationInput(p, cands, mode=mode))[:3]
+    assert got == want
+    assert sharded.consolidate_rerun()[:3] == want
+
+
+def test_sharded_eval_sets(single, sharded):
+    p = synth.random_consolidation(7, n_nodes=12, n_pending=2)
+    sets = [(0, 1), (1, 3), (0, 0), (4, 8), (2, 10)]
+    want = single.consolidate(ConsolidationInput(p, list(range(12)), mode=abi.CONSOLIDATE_EVAL, sets=sets))[:3]
+    got = sharded.consolidate(ConsolidationInput(p, list(range(12)), mode=abi.CONSOLIDATE_EVAL, sets=sets))[:3]
+    assert got == want
+
+
+def test_sharded_refuses_caller_sharding(sharded):
+    from gpusched import lib
+    p = synth.random_consolidation(1)
+    with pytest.raises(lib.GpuSchedError):
+        sharded.consolidate(ConsolidationInput(p, list(range(len(p.nodes))), shard=(0, 2)))
+
+
+def _feas_equal(a, b):
+    for k in ("rows", "cheapest", "n_feasible_offerings", "cheapest_key"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("make", [lambda: synth.make_c2(n_pods=3000), lambda: synth.make_c3(n_pods=2000),
+                                  lambda: synth.random_problem(4), lambda: synth.make_c5(n_pods=5000)],
+                         ids=["c2", "c3", "random", "c5"])
+def test_sharded_feasibility_equals_single(single, sharded, make):
+    p = make()
+    single.prepare(p)
+    want, _ = single.feasibility()
+    sharded.prepare(p)
+    got, _ = sharded.feasibility()
+    _feas_equal(got, want)
+    W = want["rows"].shape[2]
+    lo, hi = W // 3, max(W // 3 + 1, W - 1)
+    want_part, _ = single.feasibility_shard(lo, hi)
+    got_part, _ = sharded.feasibility_shard(lo, hi)
+    _feas_equal(got_part, want_part)
+
+
+def test_sharded_solve_runs_on_parent(single, sharded):
+    p = synth.random_problem(11)
+    assert sharded.solve(p)[0] == single.solve(p)[0]
+
+
+def test_sharded_device_results_refused(sharded):
+    from gpusched import lib
+    sharded.prepare(synth.random_problem(2))
+    with pytest.raises(lib.GpuSchedError) as e:
+        sharded.feasibility_shard_device(0, 1)
+    assert e.value.status == abi.GS_E_UNSUPPORTED
