@@ -4,15 +4,17 @@ GPU with an RCCL all-reduce (min-price/index) over xGMI").
 
 Rank r evaluates instance-type words [W*r/N, W*(r+1)/N) with
 gs_feasibility_shard(_device); the shards combine exactly:
-  rows        integer SUM all-reduce (each word is non-zero on one rank only,
-              so the sum is the bitwise OR),
+  rows        ALL-GATHER of each rank's own word slice (disjoint columns,
+              padded to ceil(W/N) words), written into place,
   offerings   SUM all-reduce,
   cheapest    MIN all-reduce of the OrderByPrice key (price_rank << 32 |
               name_rank; INT64_MAX = none), mapped back to the type through
               its name rank.
-`device_combine` runs the three collectives in place on the library's HBM
-buffers (RCCL over xGMI, no host round trip); `combine` is the same algebra on
-host arrays (gloo on CPU ranks, and the pod-level result of gs_feasibility_shard).
+`device_combine` runs the collectives on the library's HBM buffers (RCCL over
+xGMI, no host round trip); `combine` is the same algebra on host arrays (gloo
+on CPU ranks, and the pod-level result of gs_feasibility_shard).  One process
+driving several GPUs uses the library's own sharded context instead
+(gs_config.n_shards, csrc/multi.cpp).
 """
 import numpy as np
 
@@ -31,20 +33,36 @@ def cheapest_from_keys(keys, name_rank):
     return np.where(keys == NONE_KEY, -1, it_of_rank[low]).astype(np.int32)
 
 
+def _gather_slices(rows2d, words, rank, world, dist):
+    """rows2d: torch int64 [n, >= words]; every rank's word slice all-gathered
+    into place (each rank sends only its own columns)"""
+    import torch
+    S = -(-words // world)  # widest slice
+    wb, we = word_range(words, rank, world)
+    mine = torch.zeros((rows2d.shape[0], S), dtype=torch.int64, device=rows2d.device)
+    mine[:, :we - wb] = rows2d[:, wb:we]
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    for r in range(world):
+        b, e = word_range(words, r, world)
+        rows2d[:, b:e] = parts[r][:, :e - b]
+
+
 def combine(rows, nfo, keys, name_rank, rank, world, dist, device=None):
-    """all-reduce one rank's shard result into the full matrix (every rank)"""
+    """combine one rank's shard result into the full matrix (every rank)"""
     keys = np.asarray(keys).astype(np.int64)
     if world > 1:
         import torch
-        t_rows = torch.from_numpy(rows.view(np.int64).copy())
+        P, T, W = rows.shape
+        t_rows = torch.from_numpy(rows.view(np.int64).reshape(P * T, W).copy())
         t_nfo = torch.from_numpy(nfo.astype(np.int64))
         t_key = torch.from_numpy(keys.copy())
         if device is not None:
             t_rows, t_nfo, t_key = t_rows.to(device), t_nfo.to(device), t_key.to(device)
-        dist.all_reduce(t_rows, op=dist.ReduceOp.SUM)
+        _gather_slices(t_rows, W, rank, world, dist)
         dist.all_reduce(t_nfo, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_key, op=dist.ReduceOp.MIN)
-        rows = t_rows.cpu().numpy().view(np.uint64)
+        rows = t_rows.cpu().numpy().view(np.uint64).reshape(P, T, W)
         nfo = t_nfo.cpu().numpy().astype(np.uint32)
         keys = t_key.cpu().numpy()
     return {"rows": rows, "n_feasible_offerings": nfo, "cheapest": cheapest_from_keys(keys, name_rank),
@@ -70,9 +88,12 @@ def device_views(res, device):
 
 
 def device_combine(res, dist, device):
-    """the three in-place all-reduces on the library's buffers (RCCL)"""
+    """the collectives in place on the library's buffers (RCCL): all-gather
+    of the disjoint word slices, SUM of offering counts, MIN of keys"""
     rows, nfo, key = device_views(res, device)
-    dist.all_reduce(rows, op=dist.ReduceOp.SUM)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    VT, S = res.n_variants * res.n_templates, res.row_stride
+    _gather_slices(rows.view(VT, S), res.words, rank, world, dist)
     dist.all_reduce(nfo, op=dist.ReduceOp.SUM)
     dist.all_reduce(key, op=dist.ReduceOp.MIN)
     return rows, nfo, key

@@ -1,5 +1,5 @@
-"""IT-column sharding of the static matrix on CPU ranks (gloo, world size 2):
-the SUM / MIN all-reduce combination of gpusched.feasibility.combine over
+"""IT-column sharding of the static matrix on CPU ranks (gloo, world size 2
+and 3, uneven word slices): the all-gather / SUM / MIN combination of gpusched.feasibility.combine over
 synthetic shard results equals the unsharded matrix (the GPU side is
 tests/test_gpu_parity.py::test_feasibility_shards_combine_to_whole)."""
 import os
@@ -52,23 +52,27 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_feasibility_gloo_world2():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_feasibility_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p_ in procs:
         p_.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = dict(q.get(timeout=120) for _ in range(world))
     for p_ in procs:
         p_.join(timeout=60)
         assert p_.exitcode == 0
     rows, name_rank, price, _, _ = _whole()
     full, nfo, keys = _shard(rows, name_rank, price, 0, 1)
     want = combine(full, nfo, keys, name_rank, 0, 1, None)
-    for r in range(2):
+    for r in range(world):
         for k in ("rows", "n_feasible_offerings", "cheapest", "cheapest_key"):
             assert np.array_equal(np.asarray(res[r][k], dtype=want[k].dtype), want[k]), (r, k)
