@@ -470,8 +470,13 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   } catch (const HipError& ex) {
     return fail(c, GS_E_HIP, ex.msg);
   }
-  if (c->ctrl.status == 1) return fail(c, GS_E_CAPACITY, "NodeClaim count exceeded the device capacity");
-  if (c->ctrl.status != 0) return fail(c, GS_E_HIP, "ffd kernel reported an internal error");
+  if (c->ctrl.status == gsd::ST_CLAIMS)
+    return fail(c, GS_E_CAPACITY, "NodeClaim count exceeded the device capacity (" +
+                                      std::to_string(c->dp.max_claims) + " in-flight NodeClaims)");
+  if (c->ctrl.status == gsd::ST_POD_COUNT)
+    return fail(c, GS_E_CAPACITY, "a NodeClaim would hold more than 65535 pods (16-bit pod count in LDS)");
+  if (c->ctrl.status == gsd::ST_INTERNAL) return fail(c, GS_E_HIP, "ffd kernel reported an internal error (queue / channel bound)");
+  if (c->ctrl.status != 0) return fail(c, GS_E_HIP, "ffd kernel reported an unknown status");
   const uint32_t M = c->ctrl.n_claims;
   // pods per claim in add order, and each claim's requirement set
   std::vector<std::vector<uint32_t>> cp(M);

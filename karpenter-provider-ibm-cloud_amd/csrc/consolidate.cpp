@@ -324,6 +324,8 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   for (size_t k = 0; k < NS; k++) {
     const uint32_t s = sp.evaluated[k];
     const gsd::Ctrl& ct = ctrl[k];
+    if (ct.status == gsd::ST_POD_COUNT)
+      return fail(c, GS_E_CAPACITY, "a simulated NodeClaim would hold more than 65535 pods (16-bit pod count)");
     if (ct.status != 0) return fail(c, GS_E_HIP, "simulation kernel reported an internal error");
     const uint32_t q0 = sp.pod_off[k], P = sp.pod_off[k + 1] - q0;
     checks += (uint64_t)P * (e.NN - sp.sets[s].size() + e.checks_per_pod);

@@ -146,8 +146,11 @@ struct LogRec {
 };
 
 // FFD kernel control block (device <-> host)
+// Ctrl.status values
+enum : uint32_t { ST_OK = 0, ST_CLAIMS = 1, ST_INTERNAL = 2, ST_POD_COUNT = 3 };
+
 struct Ctrl {
-  uint32_t status;       // 0 ok, 1 claim capacity exceeded, 2 internal error
+  uint32_t status;       // ST_*: 0 ok, 1 claim capacity exceeded, 2 internal error, 3 u16 pod count overflow
   uint32_t n_claims;
   uint32_t n_log;
   uint32_t qhead, qlen;
