@@ -221,21 +221,40 @@ struct WaveSort {
     if (hi <= lo) return;
     const uint32_t x = so[left ? lo : hi];
     wsync();
+    // RU x 64 positions per pass: every lane loads its RU values (one LDS
+    // round trip), then stores them one position over
+    constexpr int RU = 4;
     if (left) {
-      for (int base = lo; base < hi; base += 64) {
-        const int k = base + (int)lane;
-        const uint32_t v = k < hi ? so[k + 1] : 0u;
+      for (int base = lo; base < hi; base += 64 * RU) {
+        uint32_t v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = base + u * 64 + (int)lane;
+          v[u] = k < hi ? so[k + 1] : 0u;
+        }
         wsync();
-        if (k < hi) so[k] = v;
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = base + u * 64 + (int)lane;
+          if (k < hi) so[k] = v[u];
+        }
         wsync();
       }
       if (lane == 0) so[hi] = x;
     } else {
-      for (int top = hi - 1; top >= lo; top -= 64) {
-        const int k = top - (int)lane;
-        const uint32_t v = k >= lo ? so[k] : 0u;
+      for (int top = hi - 1; top >= lo; top -= 64 * RU) {
+        uint32_t v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = top - u * 64 - (int)lane;
+          v[u] = k >= lo ? so[k] : 0u;
+        }
         wsync();
-        if (k >= lo) so[k + 1] = v;
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = top - u * 64 - (int)lane;
+          if (k >= lo) so[k + 1] = v[u];
+        }
         wsync();
       }
       if (lane == 0) so[lo] = x;
