@@ -423,6 +423,24 @@ extern "C" __global__ __launch_bounds__(256) void ffd_init_kernel(DevProblem d) 
   for (uint32_t i = i0; i < d.TGH * d.NN; i += stride) d.hn[i] = d.hn0[i];
 }
 
+// Go's choosePivot on n >= 50 elements samples the adjacent triples around
+// n/4, n/2 and 3n/4 (medianAdjacent) and reports "increasing" iff no
+// comparison swaps.  The array was sorted before this pod's Add, which
+// changed one key: INC raised key(modpos), so the only inversion is
+// (modpos, modpos + 1) and a swap needs both inside one triple (t-1, t, t+1),
+// i.e. modpos in {t-1, t}; otherwise the triple medians stay ordered.  APPEND
+// put the only out-of-order key at n-1, past every sampled position.  Only a
+// touched sample needs the LDS reads of pivot_hint_wave.
+__device__ __forceinline__ bool pivot_touched(uint32_t modkind, uint32_t modpos, uint32_t n) {
+  if (modkind != MOD_INC) return false;
+  const uint32_t q = n / 4;
+  const uint32_t t[3] = {q, 2 * q, 3 * q};
+  bool hit = false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) hit = hit || modpos + 1 == t[k] || modpos == t[k];
+  return hit;
+}
+
 template <uint32_t RR, bool TOPO>
 __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
@@ -602,7 +620,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
 #ifdef GS_FFD_TL
   uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
-  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0;
+  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0;
 #endif
   for (;;) {
     // ---------------------------------------------------------- Queue.Pop
@@ -786,19 +804,27 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if (lane == 0) SeqSortP{{s_so}}.insertion_sort(0, (int)M);
           wsync();
           hint_ok = false;
-        } else if (M >= 50 && pivot_hint_wave(acc, (int)M, lane) == 1) {
+        } else if (M >= 50 && (!pivot_touched(modkind, modpos, M) || pivot_hint_wave(acc, (int)M, lane) == 1)) {
           // partialInsertionSort fixes the single inversion: one rotation
           CTR(C_FAST, 1);
           if (modkind == MOD_INC) {
             const uint32_t x = acc.key(modpos);
             const uint32_t e = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
             ws.rotate((int)modpos, (int)e - 1, true);
+#ifdef GS_FFD_TL
+            n_rot++;
+            n_rotlen += e - 1 - modpos;
+#endif
             // (modpos, e-1] shift left, the changed claim lands at e-1
             if (modpos < hint && e - 1 >= hint) hint--;
           } else {
             const uint32_t x = acc.key(M - 1);
             const uint32_t lo = wave_first(0, M - 1, lane, [&](uint32_t k) { return acc.key(k) > x; });
             ws.rotate((int)lo, (int)M - 1, false);
+#ifdef GS_FFD_TL
+            n_rot++;
+            n_rotlen += M - 1 - lo;
+#endif
             if (lo < hint) hint = lo;  // the new claim lands at lo
           }
         } else {
@@ -1457,6 +1483,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.dbg[10] = n_xb;
     c.dbg[11] = n_xwin;
     c.dbg[12] = n_nonsimple;
+    c.dbg[13] = n_rot;
+    c.dbg[14] = n_rotlen;
 #endif
     *d.ctrl = c;
   }

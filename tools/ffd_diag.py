@@ -32,6 +32,8 @@ if "--tl" in sys.argv and "--block" not in sys.argv:
     base["exact_batches"] = out[10]
     base["exact_wins"] = out[11]
     base["nonsimple_pops"] = out[12]
+    base["rotations"] = out[13]
+    base["mean_rotation_len"] = round(out[14] / max(out[13], 1), 1)
 elif "--tl" in sys.argv:
     names = ["to_top", "publish", "pop", "stage_nodes", "sort_decide", "rotate", "chunk_lds", "reduce2", "exact",
              "winner_end", "new_claim"]
