@@ -43,9 +43,10 @@ typedef enum gs_status {
   GS_E_NO_DEVICE = 6    /* no gfx950 device visible */
 } gs_status;
 
-/* k8s NodeSelectorOperator (+ karpenter Gt/Lt).  Gte/Lte of the v1.13 CRD
- * (charts/crds/karpenter.sh_nodepools.yaml:292-300) are rejected with
- * GS_E_UNSUPPORTED until their upstream semantics are pinned. */
+/* k8s NodeSelectorOperator (+ Gt/Lt and the v1.13 CRD's Gte/Lte,
+ * charts/crds/karpenter.sh_nodepools.yaml:292-300).  Gte x / Lte x are
+ * integer bounds, evaluated as Gt x-1 / Lt x+1 (<U>: parity unpinned);
+ * their value must parse as an integer (GS_E_INVALID otherwise). */
 enum {
   GS_OP_IN = 0,
   GS_OP_NOTIN = 1,

@@ -239,7 +239,7 @@ struct Ctx {
     chk(r, p->n_reqs, "reqs");
     for (uint32_t i = 0; i < r.count; i++) {
       auto& q = p->reqs[r.begin + i];
-      if (q.op > GS_OP_LT) throw Fail{GS_E_UNSUPPORTED, "Gte/Lte requirement operators"};
+      if (q.op > GS_OP_LTE) throw Fail{GS_E_INVALID, "unknown requirement operator"};
       if (q.min_values >= 0) throw Fail{GS_E_UNSUPPORTED, "minValues"};
       chk(q.values, p->n_value_ids, "values");
       mention_key(S(q.key));
@@ -250,10 +250,12 @@ struct Ctx {
             throw Fail{GS_E_UNSUPPORTED, "requirement names a hostname placeholder"};
           mention(S(q.key), v);
         }
-      if (q.op == GS_OP_GT || q.op == GS_OP_LT) {
+      if (q.op >= GS_OP_GT) {
         int64_t x;
         if (q.values.count < 1 || !atoi64(S(p->value_ids[q.values.begin]), &x))
-          throw Fail{GS_E_INVALID, "Gt/Lt value is not an integer"};
+          throw Fail{GS_E_INVALID, "Gt/Lt/Gte/Lte value is not an integer"};
+        if ((q.op == GS_OP_GTE && x == INT64_MIN) || (q.op == GS_OP_LTE && x == INT64_MAX))
+          throw Fail{GS_E_INVALID, "Gte/Lte bound out of range"};
       }
     }
   }
@@ -290,7 +292,7 @@ struct Ctx {
         label_keys.insert(normalize(S(p->reqs[it0.requirements.begin + k].key)));
     }
     for (uint32_t i = 0; i < p->n_reqs; i++)
-      if (p->reqs[i].op == GS_OP_GT || p->reqs[i].op == GS_OP_LT) bounded.insert(normalize(S(p->reqs[i].key)));
+      if (p->reqs[i].op >= GS_OP_GT && p->reqs[i].op <= GS_OP_LTE) bounded.insert(normalize(S(p->reqs[i].key)));
     auto node_mention = [&](const std::string& key, const std::string& val) {
       const std::string k = normalize(key);
       int64_t x;
@@ -346,8 +348,17 @@ struct Ctx {
     int64_t bound = 0;
     if (q.op == GS_OP_IN || q.op == GS_OP_NOTIN)
       for (uint32_t i = 0; i < q.values.count; i++) vals.push_back(v.id.at(S(p->value_ids[q.values.begin + i])));
-    if (q.op == GS_OP_GT || q.op == GS_OP_LT) atoi64(S(p->value_ids[q.values.begin]), &bound);
-    return make_kreq(v, (int)q.op, vals, bound);
+    int op = (int)q.op;
+    if (op >= GS_OP_GT) atoi64(S(p->value_ids[q.values.begin]), &bound);
+    // over integer label values Gte x is Gt x-1 and Lte x is Lt x+1
+    if (op == GS_OP_GTE) {
+      op = GS_OP_GT;
+      bound -= 1;
+    } else if (op == GS_OP_LTE) {
+      op = GS_OP_LT;
+      bound += 1;
+    }
+    return make_kreq(v, op, vals, bound);
   }
   Reqs reqs_of(gs_range r) const {
     Reqs out;

@@ -227,7 +227,7 @@ struct Enc {
   }
   // <U> NewRequirement (keys normalised, In/NotIn values, Gt/Lt bounds)
   HReq make(const gs_requirement& q) {
-    if (q.op > GS_OP_LT) throw Fail{GS_E_UNSUPPORTED, "Gte/Lte requirement operators"};
+    if (q.op > GS_OP_LTE) throw Fail{GS_E_INVALID, "unknown requirement operator"};
     if (q.min_values >= 0) throw Fail{GS_E_UNSUPPORTED, "minValues"};
     chk(q.values, p->n_value_ids, "values");
     const std::string k = gsh::label_normalize(S(q.key));
@@ -246,12 +246,17 @@ struct Enc {
       std::sort(r.vals.begin(), r.vals.end());
       r.vals.erase(std::unique(r.vals.begin(), r.vals.end()), r.vals.end());
     }
-    if (q.op == GS_OP_GT || q.op == GS_OP_LT) {
+    if (q.op >= GS_OP_GT) {
       int64_t x = 0;
       if (q.values.count < 1 || !gsh::go_atoi64(S(p->value_ids[q.values.begin]), &x))
-        throw Fail{GS_E_INVALID, "Gt/Lt value is not an integer"};
-      (q.op == GS_OP_GT ? r.hg : r.hl) = true;
-      (q.op == GS_OP_GT ? r.gt : r.lt) = x;
+        throw Fail{GS_E_INVALID, "Gt/Lt/Gte/Lte value is not an integer"};
+      if ((q.op == GS_OP_GTE && x == INT64_MIN) || (q.op == GS_OP_LTE && x == INT64_MAX))
+        throw Fail{GS_E_INVALID, "Gte/Lte bound out of range"};
+      // over integer label values Gte x is Gt x-1 and Lte x is Lt x+1
+      const bool lower = q.op == GS_OP_GT || q.op == GS_OP_GTE;
+      const int64_t b = q.op == GS_OP_GTE ? x - 1 : q.op == GS_OP_LTE ? x + 1 : x;
+      (lower ? r.hg : r.hl) = true;
+      (lower ? r.gt : r.lt) = b;
     }
     return r;
   }

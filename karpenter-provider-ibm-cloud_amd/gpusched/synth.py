@@ -293,6 +293,8 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
         op = rng.choice(["In", "In", "In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"],
                         p=[0.3, 0.1, 0.1, 0.2, 0.1, 0.05, 0.075, 0.075])
         if op in ("Gt", "Lt"):
+            if rng.random() < 0.4:
+                op = op + "e"  # Gte / Lte
             return (k, op, [str(int(rng.integers(0, 10)))])
         if op in ("Exists", "DoesNotExist"):
             return (k, op, [])

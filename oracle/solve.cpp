@@ -180,11 +180,16 @@ Req make_req(const string& key_in, int op, const vector<string>& values, optiona
   r.min_values = mv;
   if (op == GS_OP_IN || op == GS_OP_DOES_NOT_EXIST) r.complement = false;
   if (op == GS_OP_IN || op == GS_OP_NOTIN) r.values.insert(values.begin(), values.end());
-  if (op == GS_OP_GT || op == GS_OP_LT) {
+  if (op >= GS_OP_GT && op <= GS_OP_LTE) {
     int64_t v = 0;
     if (values.empty() || !go_atoi(values[0], &v)) throw Unsupported{GS_E_INVALID, "Gt/Lt value is not an integer"};
+    // <U> Gte x / Lte x over integer label values: greaterThan x-1 / lessThan x+1
+    if ((op == GS_OP_GTE && v == INT64_MIN) || (op == GS_OP_LTE && v == INT64_MAX))
+      throw Unsupported{GS_E_INVALID, "Gte/Lte bound out of range"};
     if (op == GS_OP_GT) r.gt = v;
-    else r.lt = v;
+    else if (op == GS_OP_LT) r.lt = v;
+    else if (op == GS_OP_GTE) r.gt = v - 1;
+    else r.lt = v + 1;
   }
   return r;
 }
@@ -542,7 +547,7 @@ struct Builder {
   }
   bool allow_placeholder = false;  // launch-time filter: hostname values are plain labels
   Req req_of(const gs_requirement& q) {
-    if (q.op > GS_OP_LT) throw Unsupported{GS_E_UNSUPPORTED, "Gte/Lte operators"};
+    if (q.op > GS_OP_LTE) throw Unsupported{GS_E_INVALID, "unknown requirement operator"};
     if (!allow_placeholder && normalize_key(str(q.key)) == kHostname)
       for (uint32_t i = 0; i < q.values.count && q.values.begin + i < p->n_value_ids; i++)
         if (str(p->value_ids[q.values.begin + i]).rfind("hostname-placeholder-", 0) == 0)

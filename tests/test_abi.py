@@ -53,9 +53,17 @@ def test_validate_refuses_min_values():
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
 
 
-def test_validate_refuses_gte():
-    b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", "Gte", ["4"])]])
-    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+def test_validate_accepts_gte_lte():
+    for op in ("Gte", "Lte"):
+        b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", op, ["4"])]])
+        assert lib.validate(b.build())[0] == abi.GS_OK
+
+
+def test_validate_gte_lte_bounds():
+    b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", "Gte", ["-9223372036854775808"])]])
+    assert lib.validate(b.build())[0] == abi.GS_E_INVALID
+    b = _one_pod_problem(required_terms=[[("karpenter-ibm.sh/instance-cpu", "Lte", ["x"])]])
+    assert lib.validate(b.build())[0] == abi.GS_E_INVALID
 
 
 def test_validate_invalid_gt_value():

@@ -129,7 +129,7 @@ def random_catalog(seed, n_types=150, n_claims=40):
             reqs.append((ZONE, str(rng.choice(["In", "NotIn"])), list(rng.choice(zones, size=int(rng.integers(1, 3)),
                                                                                    replace=False))))
         if rng.random() < 0.25:
-            reqs.append(("karpenter-ibm.sh/instance-cpu", str(rng.choice(["Gt", "Lt"])), [str(rng.choice([4, 8, 16]))]))
+            reqs.append(("karpenter-ibm.sh/instance-cpu", str(rng.choice(["Gt", "Lt", "Gte", "Lte"])), [str(rng.choice([4, 8, 16]))]))
         if rng.random() < 0.15:
             reqs.append(("karpenter-ibm.sh/instance-cpu", "Gt", ["2"]))
             reqs.append(("karpenter-ibm.sh/instance-cpu", "Lt", ["3"]))  # bounds cross: DoesNotExist
