@@ -14,6 +14,10 @@ if [ -z "${SKIP_KT:-}" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- \
     python3 $R/bench.py --steps 3 --warmup 1 --latency-steps 1 --no-cpu-baseline > $O/bench_kt.json 2> $O/kt.err
   echo "kernel trace done"
+  # CM alone: the ffdw average in its stats is the headline leg's kernel only
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_cm -o kt -- \
+    python3 $R/bench.py --only cm --steps 5 --warmup 1 --latency-steps 0 --no-cpu-baseline > $O/bench_kt_cm.json 2> $O/kt_cm.err
+  echo "cm kernel trace done"
 fi
 rm -f $O/traffic.json
 for leg in $LEGS; do
