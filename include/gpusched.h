@@ -62,7 +62,10 @@ enum {
 enum { GS_TOL_EQUAL = 0, GS_TOL_EXISTS = 1 };
 
 /* gs_pod.flags: scheduling features present on the pod that this build
- * refuses (GS_E_UNSUPPORTED) rather than silently ignoring. */
+ * refuses (GS_E_UNSUPPORTED) rather than silently ignoring.  Pod
+ * anti-affinity terms and host ports are passed in gs_pod.anti_affinity /
+ * gs_pod.host_ports; the ANTI_AFFINITY / HOST_PORTS flags remain for forms
+ * those cannot express (a namespaceSelector, a matchLabelKeys list). */
 enum {
   GS_POD_TOPOLOGY_SPREAD = 1u << 0,
   GS_POD_AFFINITY = 1u << 1,
@@ -158,6 +161,31 @@ typedef struct gs_spread {
   uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is refused */
 } gs_spread;
 
+/* corev1.PodAffinityTerm of spec.affinity.podAntiAffinity: a required term,
+ * or a preferred one with its weight (<U> karpenter Topology,
+ * TopologyTypePodAntiAffinity: required and not-yet-relaxed preferred terms
+ * both constrain the pod; a required term also constrains, through the
+ * inverse group, every pod its selector selects).  topologyKey must be
+ * kubernetes.io/hostname (other keys GS_E_UNSUPPORTED). */
+typedef struct gs_anti_affinity {
+  uint32_t topology_key;       /* string id */
+  uint32_t required;           /* 1: requiredDuringScheduling..., 0: preferred */
+  int32_t weight;              /* preferred terms: the term's weight */
+  uint32_t has_selector;       /* 0: nil labelSelector (selects no pod) */
+  gs_range match_labels;       /* into labels */
+  gs_range match_expressions;  /* into reqs: In / NotIn / Exists / DoesNotExist */
+  gs_range namespaces;         /* into value_ids (string ids); empty = the pod's namespace */
+} gs_anti_affinity;
+
+/* a containers[].ports[] entry with hostPort != 0 (<U> scheduling
+ * HostPortUsage: two entries conflict when protocol and port are equal and
+ * either hostIP is unspecified or both are equal) */
+typedef struct gs_host_port {
+  uint32_t protocol;  /* string id; "" = TCP */
+  uint32_t ip;        /* string id; "", "0.0.0.0" and "::" = unspecified */
+  int32_t port;       /* 1..65535 */
+} gs_host_port;
+
 /* a pod; requests = resources.RequestsForPods(pod) (incl. pods=1) */
 typedef struct gs_pod {
   uint32_t uid;             /* string id */
@@ -171,6 +199,8 @@ typedef struct gs_pod {
   uint32_t ns;              /* metadata.namespace (string id) */
   gs_range labels;          /* metadata.labels, into labels (topology selectors) */
   gs_range spreads;         /* spec.topologySpreadConstraints, into spreads */
+  gs_range anti_affinity;   /* spec.affinity.podAntiAffinity terms, into anti_affinities */
+  gs_range host_ports;      /* host ports of all containers, into host_ports */
 } gs_pod;
 
 /* an existing (state) node: ExistingNode inputs */
@@ -203,6 +233,8 @@ typedef struct gs_problem {
    * reschedulable ones are what consolidation simulations move */
   const gs_pod* bound_pods; uint32_t n_bound_pods;
   const uint32_t* bound_pod_node;             /* [n_bound_pods] index into nodes */
+  const gs_anti_affinity* anti_affinities; uint32_t n_anti_affinities;
+  const gs_host_port* host_ports; uint32_t n_host_ports;
 } gs_problem;
 
 /* Results.TruncateInstanceTypes(60) of Scheduler.Solve */

@@ -8,7 +8,10 @@
 // independent of the oracle's string-set restatement (oracle/solve.cpp).
 #include "encode.hpp"
 
+#include <arpa/inet.h>
+
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <functional>
 #include <tuple>
@@ -667,13 +670,71 @@ struct Ctx {
       return h;
     }
   };
+  // <U> corev1.PodAffinityTerm of podAntiAffinity (hostname key)
+  struct AntiEnc {
+    SpreadEnc sel;              // has_sel / ml / ex
+    std::set<std::string> nss;  // the term's namespaces, else the pod's
+    bool required = false;
+    int32_t weight = 0;
+    bool selects(const std::string& ns, const std::map<std::string, std::string>& labels) const {
+      return nss.count(ns) && sel.matches(labels);
+    }
+    std::string hash() const {
+      std::string h = "anti|" + std::string(sel.has_sel ? "1" : "0");
+      for (auto& n : nss) h += "|n:" + n;
+      for (auto& kv : sel.ml) h += "|l:" + kv.first + "=" + kv.second;
+      for (auto& x : sel.ex) {
+        h += "|e:" + std::get<0>(x) + ":" + std::to_string(std::get<1>(x));
+        for (auto& v : std::get<2>(x)) h += "," + v;
+      }
+      return h;
+    }
+  };
+  // <U> scheduling.HostPort: Matches = same protocol and port, and either IP
+  // unspecified or equal (net.ParseIP; unparsable -> 0.0.0.0)
+  struct PortEnc {
+    std::string proto;
+    bool unspec = true;
+    std::array<uint8_t, 16> ip{};
+    int32_t port = 0;
+    bool matches(const PortEnc& o) const {
+      return proto == o.proto && port == o.port && (unspec || o.unspec || ip == o.ip);
+    }
+    std::string key() const {
+      std::string k = proto + "|" + std::to_string(port) + "|";
+      if (!unspec) k.append((const char*)ip.data(), 16);
+      return k;
+    }
+  };
+  // what makes a pod counted by a group
+  struct PodSel {
+    std::string ns;
+    std::map<std::string, std::string> labels;
+    std::set<std::string> carried;  // hashes of its required anti-affinity terms
+    std::vector<PortEnc> ports;
+  };
+  // A topology group as the device sees it.  kind 0: a spread constraint
+  // (counts the pods its selector selects in the owner's namespace).  The
+  // anti-affinity and host-port constraints are hostname groups whose owner
+  // may join only a domain with count + self <= skew, self = the owner is
+  // counted itself; with skew = self that is "count == 0":
+  //  kind 1 TopologyTypePodAntiAffinity (counts the pods the term selects),
+  //  kind 2 its inverse for a required term (owners = the pods the term
+  //         selects; counts the pods carrying the term),
+  //  kind 3 HostPortUsage (owners = pods with port entry e; counts the pods
+  //         with an entry that Matches e).
   struct GroupEnc {
     SpreadEnc sp;
     std::string ns;
+    int kind = 0;
+    AntiEnc anti;
+    std::string inv_hash;
+    PortEnc port;
   };
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
   std::vector<std::string> pod_ns;
+  std::vector<PodSel> pod_sel;  // pending pods
   std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
 
   std::map<std::string, std::string> label_map(gs_range r) const {
@@ -714,8 +775,92 @@ struct Ctx {
     }
     return out;
   }
-  bool group_selects(const GroupEnc& g, const std::string& ns, const std::map<std::string, std::string>& labels) const {
-    return ns == g.ns && g.sp.matches(labels);
+  std::vector<AntiEnc> antis_of(const gs_pod& pd) const {
+    chk(pd.anti_affinity, p->n_anti_affinities, "anti_affinities");
+    std::vector<AntiEnc> out;
+    for (uint32_t k = 0; k < pd.anti_affinity.count; k++) {
+      const gs_anti_affinity& q = p->anti_affinities[pd.anti_affinity.begin + k];
+      if (normalize(S(q.topology_key)) != kHostname)
+        throw Fail{GS_E_UNSUPPORTED, "pod anti-affinity topologyKey other than hostname"};
+      AntiEnc a;
+      a.required = q.required != 0;
+      a.weight = q.weight;
+      a.sel.key = kHostname;
+      a.sel.has_sel = q.has_selector != 0;
+      a.sel.ml = label_map(q.match_labels);
+      chk(q.match_expressions, p->n_reqs, "reqs");
+      for (uint32_t x = 0; x < q.match_expressions.count; x++) {
+        const gs_requirement& r = p->reqs[q.match_expressions.begin + x];
+        if (r.op > GS_OP_DOES_NOT_EXIST) throw Fail{GS_E_INVALID, "label selector operator"};
+        chk(r.values, p->n_value_ids, "values");
+        std::set<std::string> vals;
+        for (uint32_t v = 0; v < r.values.count; v++) vals.insert(S(p->value_ids[r.values.begin + v]));
+        a.sel.ex.emplace_back(S(r.key), r.op, std::move(vals));
+      }
+      chk(q.namespaces, p->n_value_ids, "values");
+      for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(S(p->value_ids[q.namespaces.begin + v]));
+      if (a.nss.empty()) a.nss.insert(S(pd.ns));
+      out.push_back(std::move(a));
+    }
+    return out;
+  }
+  std::vector<PortEnc> ports_of(const gs_pod& pd) const {
+    chk(pd.host_ports, p->n_host_ports, "host_ports");
+    std::vector<PortEnc> out;
+    static const std::array<uint8_t, 16> z6{}, z4{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff, 0, 0, 0, 0};
+    for (uint32_t k = 0; k < pd.host_ports.count; k++) {
+      const gs_host_port& q = p->host_ports[pd.host_ports.begin + k];
+      if (q.port < 1 || q.port > 65535) throw Fail{GS_E_INVALID, "host port out of range"};
+      PortEnc e;
+      e.proto = S(q.protocol).empty() ? std::string("TCP") : S(q.protocol);
+      e.port = q.port;
+      const std::string& ip = S(q.ip);
+      in_addr b4;
+      std::array<uint8_t, 16> b6;
+      e.ip = z4;  // unparsable: 0.0.0.0
+      if (inet_pton(AF_INET, ip.c_str(), &b4) == 1) std::memcpy(e.ip.data() + 12, &b4, 4);
+      else if (inet_pton(AF_INET6, ip.c_str(), b6.data()) == 1) e.ip = b6;
+      e.unspec = e.ip == z6 || e.ip == z4;
+      out.push_back(e);
+    }
+    return out;
+  }
+  PodSel sel_of(const gs_pod& pd) const {
+    PodSel ps;
+    ps.ns = S(pd.ns);
+    ps.labels = label_map(pd.labels);
+    for (auto& a : antis_of(pd))
+      if (a.required) ps.carried.insert(a.hash());
+    ps.ports = ports_of(pd);
+    return ps;
+  }
+  bool group_counts(const GroupEnc& g, const PodSel& ps) const {
+    switch (g.kind) {
+      case 0: return ps.ns == g.ns && g.sp.matches(ps.labels);
+      case 1: return g.anti.selects(ps.ns, ps.labels);
+      case 2: return ps.carried.count(g.inv_hash) != 0;
+      default:
+        for (auto& e : ps.ports)
+          if (e.matches(g.port)) return true;
+        return false;
+    }
+  }
+  uint32_t group_id(const std::string& h, GroupEnc&& g) {
+    auto f = group_idx.find(h);
+    if (f == group_idx.end()) {
+      f = group_idx.emplace(h, (uint32_t)groups.size()).first;
+      groups.push_back(std::move(g));
+    }
+    if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology groups"};
+    return f->second;
+  }
+  // a hostname group admitting an owner only where the count is 0
+  GroupEnc host_group(int kind, bool self) const {
+    GroupEnc g;
+    g.kind = kind;
+    g.sp.key = kHostname;
+    g.sp.skew = self ? 1 : 0;
+    return g;
   }
 
   // <U> NewTopology: domain universe (In values of NodePool requirements of
@@ -768,10 +913,9 @@ struct Ctx {
       const gs_pod& bp = p->bound_pods[b];
       if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
       const uint32_t pos = pos_of[p->bound_pod_node[b]];
-      const std::string ns = S(bp.ns);
-      const auto labels = label_map(bp.labels);
+      const PodSel ps = sel_of(bp);
       for (uint32_t g = 0; g < e.TG; g++) {
-        if (!group_selects(groups[g], ns, labels)) continue;
+        if (!group_counts(groups[g], ps)) continue;
         gsd::TGroupRec& t = e.tgroups[g];
         if (t.host) {
           e.hn0[(size_t)t.hslot * e.NN + pos]++;
@@ -784,10 +928,9 @@ struct Ctx {
       }
     }
     for (uint32_t i = 0; i < e.P && e.TG; i++) {
-      const auto labels_i = label_map(p->pods[i].labels);
       uint64_t sel = 0;
       for (uint32_t g = 0; g < e.TG; g++)
-        if (group_selects(groups[g], pod_ns[i], labels_i)) sel |= 1ull << g;
+        if (group_counts(groups[g], pod_sel[i])) sel |= 1ull << g;
       for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) e.vars[v].t_sel = sel;
     }
   }
@@ -1003,6 +1146,19 @@ struct Ctx {
     e.pod_req.assign((size_t)e.P * e.R, 0);
     std::vector<int64_t> cpu(e.P, 0), mem(e.P, 0);
     auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
+    // <U> the inverse anti-affinity groups: required terms of pending and
+    // bound pods (Topology.updateInverseAntiAffinity / updateInverseAffinities)
+    std::map<std::string, AntiEnc> inv_terms;
+    pod_sel.reserve(e.P);
+    for (uint32_t i = 0; i < e.P; i++) {
+      pod_sel.push_back(sel_of(p->pods[i]));
+      for (auto& a : antis_of(p->pods[i]))
+        if (a.required) inv_terms.emplace(a.hash(), a);
+    }
+    chk(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
+    for (uint32_t b = 0; b < p->n_bound_pods; b++)
+      for (auto& a : antis_of(p->bound_pods[b]))
+        if (a.required) inv_terms.emplace(a.hash(), a);
     for (uint32_t i = 0; i < e.P; i++) {
       auto& pd = p->pods[i];
       if (pd.flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
@@ -1041,11 +1197,38 @@ struct Ctx {
           f = group_idx.emplace(h, (uint32_t)groups.size()).first;
           groups.push_back(GroupEnc{sp, pod_ns.back()});
         }
-        if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups"};
+        if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology groups"};
         sgid.push_back(f->second);
       }
       std::vector<uint32_t> cur(sps.size());  // current constraints (swap-remove order)
       std::iota(cur.begin(), cur.end(), 0);
+      // anti-affinity, inverse anti-affinity and host-port groups
+      const PodSel& me = pod_sel[i];
+      uint64_t own_static = 0;
+      std::vector<std::pair<int32_t, uint32_t>> anti_pref;  // (weight, group)
+      for (auto& a : antis_of(pd)) {
+        const bool self = a.selects(me.ns, me.labels);
+        GroupEnc g = host_group(1, self);
+        g.anti = a;
+        const uint32_t gid = group_id("A|" + a.hash() + (self ? "|s" : "|n"), std::move(g));
+        if (a.required) own_static |= 1ull << gid;
+        else anti_pref.push_back({a.weight, gid});
+      }
+      if (anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
+      // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
+      std::stable_sort(anti_pref.begin(), anti_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+      for (auto& kv : inv_terms) {
+        if (!kv.second.selects(me.ns, me.labels)) continue;
+        const bool self = me.carried.count(kv.first) != 0;
+        GroupEnc g = host_group(2, self);
+        g.inv_hash = kv.first;
+        own_static |= 1ull << group_id("I|" + kv.first + (self ? "|s" : "|n"), std::move(g));
+      }
+      for (auto& pe : me.ports) {
+        GroupEnc g = host_group(3, true);
+        g.port = pe;
+        own_static |= 1ull << group_id("P|" + pe.key(), std::move(g));
+      }
       chk(pd.tolerations, p->n_tolerations, "tolerations");
       std::vector<Tol> tols;
       for (uint32_t k = 0; k < pd.tolerations.count; k++) {
@@ -1053,7 +1236,7 @@ struct Ctx {
         tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
       }
       e.var_begin.push_back((uint32_t)e.variants.size());
-      size_t ri = 0, pi = 0;
+      size_t ri = 0, pi = 0, ai = 0;
       for (;;) {
         // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
         PodVariant v;
@@ -1066,11 +1249,18 @@ struct Ctx {
         }
         v.tol = tol_mask(tols);
         for (uint32_t k : cur) v.own |= 1ull << sgid[k];
+        v.own |= own_static;
+        for (size_t k = ai; k < anti_pref.size(); k++) v.own |= 1ull << anti_pref[k].second;
         e.variants.push_back(std::move(v));
         variant_tols.push_back(tols);
         // <U> Preferences.Relax
         if (req_terms.size() - ri > 1) {
           ri++;
+          continue;
+        }
+        // removePreferredPodAntiAffinityTerm (the heaviest)
+        if (ai < anti_pref.size()) {
+          ai++;
           continue;
         }
         if (pi < pref.size()) {

@@ -40,7 +40,11 @@ DT_NODEPOOL = np.dtype([("name", "<u4"), ("weight", "<i4"), ("requirements", RAN
                         ("daemon_requests", RANGE), ("instance_types", RANGE)], align=True)
 DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), ("node_selector", RANGE),
                    ("required_terms", RANGE), ("preferred_terms", RANGE), ("tolerations", RANGE),
-                   ("flags", "<u4"), ("ns", "<u4"), ("labels", RANGE), ("spreads", RANGE)], align=True)
+                   ("flags", "<u4"), ("ns", "<u4"), ("labels", RANGE), ("spreads", RANGE),
+                   ("anti_affinity", RANGE), ("host_ports", RANGE)], align=True)
+DT_ANTI = np.dtype([("topology_key", "<u4"), ("required", "<u4"), ("weight", "<i4"), ("has_selector", "<u4"),
+                    ("match_labels", RANGE), ("match_expressions", RANGE), ("namespaces", RANGE)], align=True)
+DT_HOSTPORT = np.dtype([("protocol", "<u4"), ("ip", "<u4"), ("port", "<i4")], align=True)
 SPREAD_DO_NOT_SCHEDULE, SPREAD_SCHEDULE_ANYWAY = 0, 1
 POLICY_HONOR, POLICY_IGNORE = 0, 1
 DT_SPREAD = np.dtype([("topology_key", "<u4"), ("max_skew", "<i4"), ("when_unsatisfiable", "<u4"),
@@ -73,6 +77,8 @@ class GsProblem(C.Structure):
         ("spreads", _P), ("n_spreads", _U32),
         ("bound_pods", _P), ("n_bound_pods", _U32),
         ("bound_pod_node", _P),
+        ("anti_affinities", _P), ("n_anti_affinities", _U32),
+        ("host_ports", _P), ("n_host_ports", _U32),
     ]
 
 

@@ -600,3 +600,127 @@ def random_topology(seed, n_pods=None):
                   node_selector=sel, required_terms=required, tolerations=tols, labels={"app": app},
                   namespace=str(rng.choice(["default", "default", "other"])), spreads=spreads)
     return b.build()
+
+
+def _selector(rng, tgt):
+    r = rng.random()
+    if r < 0.6:
+        return {"labels": {"app": tgt}}
+    if r < 0.8:
+        return {"exprs": [("app", str(rng.choice(["In", "NotIn"])), [tgt, "cache"])]}
+    if r < 0.9:
+        return {"exprs": [("app", "Exists", [])]}
+    return None
+
+
+def random_affinity(seed, n_pods=None):
+    """small adversarial problems for pod anti-affinity and host ports:
+    required and preferred hostname anti-affinity (self- and other-selecting,
+    namespace lists, nil selectors), inverse groups from pending and bound
+    carriers, host ports over protocols and specific / unspecified host IPs,
+    mixed with topology spread, existing nodes, NodePool limits (relaxation)
+    and taints"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
+    profs = []
+    for fam in ["bx2", "cx2", "mx2"]:
+        for v in [2, 4, 8]:
+            if rng.random() < 0.7:
+                profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    if not profs:
+        profs = [("bx2-4x16", 4, 16, None)]
+    prices = {p_[0]: round(0.05 * p_[1] + 0.01 * float(rng.random()), 4) for p_ in profs}
+    its = build_catalog(b, profs, zones, spot=bool(rng.random() < 0.5), prices=prices, rng=rng,
+                        unavailable_frac=0.1)
+    for j in range(int(rng.integers(1, 3))):
+        reqs = [("topology.kubernetes.io/zone", "In", zones)] if rng.random() < 0.7 else []
+        taints = [("dedicated", "x", "PreferNoSchedule")] if rng.random() < 0.2 else []
+        limits = {"cpu": int(rng.choice([8, 16, 32])) * 1000} if rng.random() < 0.35 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, taints=taints, limits=limits,
+                       daemon={"cpu": 100, "pods": 1000})
+    # palettes shared by pods (deployments share their terms)
+    anti_pal = []
+    for _ in range(int(rng.integers(1, 5))):
+        t = {"required": bool(rng.random() < 0.35), "weight": int(rng.choice([1, 10, 50, 100])),
+             "selector": _selector(rng, str(rng.choice(APPS[:3])))}
+        if rng.random() < 0.15:
+            t["namespaces"] = sorted(set(rng.choice(["default", "other", "kube"], size=2).tolist()))
+        anti_pal.append(t)
+    port_pal = [(int(rng.choice([80, 443, 8080])), str(rng.choice(["TCP", "TCP", "", "UDP"])),
+                 str(rng.choice(["", "", "10.0.0.1", "10.0.0.2", "0.0.0.0"]))) for _ in range(int(rng.integers(1, 6)))]
+    spread_pal = []
+    for _ in range(int(rng.integers(0, 3))):
+        spread_pal.append({"key": "topology.kubernetes.io/zone" if rng.random() < 0.5 else "kubernetes.io/hostname",
+                           "max_skew": int(rng.choice([1, 2])), "node_affinity_policy": "Ignore",
+                           "when": "ScheduleAnyway" if rng.random() < 0.5 else "DoNotSchedule",
+                           "selector": {"labels": {"app": str(rng.choice(APPS[:3]))}}})
+
+    def pick(pal, kmax):
+        if not pal:
+            return []
+        k = int(rng.integers(0, kmax + 1))
+        return [dict(pal[i]) if isinstance(pal[i], dict) else pal[i]
+                for i in sorted(set(rng.choice(len(pal), size=k).tolist()))] if k else []
+
+    for k in range(int(rng.integers(0, 5))):
+        it = its[rng.integers(0, len(its))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(zones))
+        labels["karpenter.sh/capacity-type"] = "on-demand"
+        labels["kubernetes.io/hostname"] = f"n{k}"
+        avail = {"cpu": int(rng.choice([1000, 3000, 6000])), "memory": 8 * GI * 1000, "pods": 20_000}
+        b.add_node(f"n{k}", labels, avail, initialized=True)
+        for q in range(int(rng.integers(0, 4))):
+            anti = [t for t in pick(anti_pal, 1) if t["required"]] if rng.random() < 0.3 else []
+            b.add_bound_pod(k, _uid(rng), 0, {"cpu": 100, "pods": 1000},
+                            labels={"app": str(rng.choice(APPS[:3]))},
+                            namespace=str(rng.choice(["default", "default", "other"])),
+                            anti_affinity=anti, host_ports=pick(port_pal, 1) if rng.random() < 0.3 else [])
+    n = int(n_pods if n_pods is not None else rng.integers(1, 40))
+    for i in range(n):
+        req = {"cpu": int(rng.choice([250, 500, 1000, 2000])), "memory": int(rng.choice([1, 2, 4])) * GI * 1000,
+               "pods": 1000}
+        tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000, req,
+                  tolerations=tols, labels={"app": str(rng.choice(APPS[:3]))},
+                  namespace=str(rng.choice(["default", "default", "other"])),
+                  anti_affinity=pick(anti_pal, 2) if rng.random() < 0.6 else [],
+                  host_ports=pick(port_pal, 2) if rng.random() < 0.3 else [],
+                  spreads=pick(spread_pal, 1) if rng.random() < 0.3 else [])
+    return b.build()
+
+
+def e2e_deployments(n_deployments=8, replicas=20, with_nodes=False, seed=0x5EED00E2):
+    """the reference e2e suite's deployments (test/e2e/config.go:455-490):
+    labels app/test/purpose, requests 100m-1 CPU, and a preferred (weight 100)
+    podAntiAffinity on kubernetes.io/hostname selecting its own app; over the
+    C2-family catalog in 3 zones x {on-demand, spot}"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = []
+    for fam in ["bx2", "cx2", "mx2"]:
+        for v in [2, 4, 8, 16]:
+            profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs))
+    b.add_nodepool("default", requirements=[("topology.kubernetes.io/zone", "In", FAKE_ZONES)],
+                   daemon={"cpu": 100, "pods": 1000})
+    if with_nodes:
+        for k in range(6):
+            it = its[k % len(its)]
+            labels = {r[0]: r[2][0] for r in it.requirements}
+            labels["topology.kubernetes.io/zone"] = FAKE_ZONES[k % 3]
+            labels["kubernetes.io/hostname"] = f"node-{k}"
+            b.add_node(f"node-{k}", labels, {"cpu": 4000, "memory": 16 * GI * 1000, "pods": 30_000})
+            b.add_bound_pod(k, f"bound-{k}", 0, {"cpu": 100, "pods": 1000},
+                            labels={"app": f"e2e-{k % max(1, n_deployments)}", "test": "e2e"})
+    for d in range(n_deployments):
+        name = f"e2e-{d}"
+        cpu = int(rng.choice([100, 250, 500, 1000]))
+        mem = int(rng.choice([128, 256, 512, 1024])) * MI * 1000
+        for r in range(replicas):
+            b.add_pod(f"{name}-{r:04d}", 1_700_000_000_000_000_000 + d * 1_000_000_000, {"cpu": cpu, "memory": mem,
+                                                                                          "pods": 1000},
+                      labels={"app": name, "test": "e2e", "purpose": "karpenter-test"},
+                      anti_affinity=[{"required": False, "weight": 100, "selector": {"labels": {"app": name}}}])
+    return b.build()

@@ -9,7 +9,10 @@
 #include "oracle.h"
 #include "gosort.h"
 
+#include <arpa/inet.h>
+
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -394,6 +397,45 @@ struct Spread {
   }
 };
 
+// corev1.PodAffinityTerm of podAntiAffinity (hostname key)
+struct Anti {
+  string key;
+  bool required = false;
+  int32_t weight = 0;
+  Spread sel;                // has_selector / match_labels / exprs only
+  std::set<string> nss;      // buildNamespaceList: the term's list, else the pod's namespace
+  string hash() const {      // TopologyGroup.Hash: type, key, namespaces, selector
+    string h = "anti|" + key + "|" + (sel.has_selector ? "1" : "0");
+    for (auto& n : nss) h += "|n:" + n;
+    for (auto& kv : sel.match_labels) h += "|l:" + kv.first + "=" + kv.second;
+    for (auto& e : sel.exprs) {
+      h += "|e:" + e.key + ":" + std::to_string(e.op);
+      for (auto& v : e.values) h += "," + v;
+    }
+    return h;
+  }
+};
+
+// <U> scheduling.HostPort (GetHostPorts: nil hostIP parse -> 0.0.0.0, "" protocol -> TCP)
+struct HostPort {
+  string proto;
+  bool unspecified = true;
+  std::array<uint8_t, 16> ip{};  // IPv4 as ::ffff:a.b.c.d (net.IP.Equal)
+  int32_t port = 0;
+  bool matches(const HostPort& o) const {
+    if (proto != o.proto || port != o.port) return false;
+    if (unspecified || o.unspecified) return true;
+    return ip == o.ip;
+  }
+};
+
+bool ports_conflict(const vector<HostPort>& used, const vector<HostPort>& want) {
+  for (auto& w : want)
+    for (auto& u : used)
+      if (w.matches(u)) return true;
+  return false;
+}
+
 struct Pod {
   uint32_t index;
   string uid;
@@ -408,6 +450,9 @@ struct Pod {
   string ns;
   std::map<string, string> labels;
   vector<Spread> spreads;  // mutable (relaxation)
+  vector<Anti> anti_required;
+  vector<Anti> anti_preferred;  // mutable (relaxation)
+  vector<HostPort> ports;
 };
 
 struct Template {
@@ -427,6 +472,7 @@ struct NodeClaim {
   vector<const InstanceType*> options;
   Res requests;
   vector<const Pod*> pods;
+  vector<HostPort> ports;  // hostPortUsage
 };
 
 struct ExistingNode {
@@ -437,6 +483,7 @@ struct ExistingNode {
   vector<Taint> taints;
   Res available, requests;
   vector<const Pod*> pods;
+  vector<HostPort> ports;  // hostPortUsage of the bound pods
 };
 
 // <U> NewPodRequirements: nodeSelector + heaviest preferred term (sort.Slice
@@ -508,16 +555,21 @@ vector<const InstanceType*> order_by_price(vector<const InstanceType*> its, cons
   return out;
 }
 
-// <U> scheduling.TopologyGroup (TopologyTypeSpread) with an empty node filter
+// <U> scheduling.TopologyGroup with an empty node filter:
+// TopologyTypeSpread or TopologyTypePodAntiAffinity
 struct TGroup {
+  bool anti = false;
   string key;
   int32_t max_skew;
   optional<int32_t> min_domains;
-  string ns;
+  string ns;                          // spread: the owner's namespace
+  std::set<string> nss;               // anti-affinity: the term's namespaces
   Spread sel;
   std::map<string, int64_t> domains;  // known domains and their counts
   std::set<uint32_t> owners;          // pod indices
-  bool selects(const Pod& p) const { return p.ns == ns && sel.matches(p.labels); }
+  bool selects(const Pod& p) const {
+    return (anti ? nss.count(p.ns) > 0 : p.ns == ns) && sel.matches(p.labels);
+  }
 };
 
 struct OracleState {
@@ -532,6 +584,8 @@ struct OracleState {
   vector<string> resource_names;
   vector<TGroup> groups;            // creation order
   std::map<string, size_t> group_index;
+  vector<TGroup> inverse;           // t.inverseTopologies (required anti-affinity)
+  std::map<string, size_t> inverse_index;
 };
 
 struct Builder {
@@ -595,11 +649,11 @@ struct Builder {
   }
 
   // namespace, labels and topology spread constraints of a pod
-  void pod_meta(const gs_pod& g, Pod& pd) {
+  void pod_meta(const gs_pod& g, Pod& pd, bool pending = true) {
     pd.ns = str(g.ns);
     pd.labels = labels_of(g.labels);
     check_range(g.spreads, p->n_spreads, "spreads");
-    for (uint32_t k = 0; k < g.spreads.count; k++) {
+    for (uint32_t k = 0; k < (pending ? g.spreads.count : 0); k++) {
       const gs_spread& q = p->spreads[g.spreads.begin + k];
       Spread sp;
       sp.key = normalize_key(str(q.topology_key));
@@ -626,6 +680,66 @@ struct Builder {
       sp.ignore_affinity = q.node_affinity_policy == GS_POLICY_IGNORE;
       pd.spreads.push_back(std::move(sp));
     }
+    check_range(g.anti_affinity, p->n_anti_affinities, "anti_affinities");
+    for (uint32_t k = 0; k < g.anti_affinity.count; k++) {
+      const gs_anti_affinity& q = p->anti_affinities[g.anti_affinity.begin + k];
+      Anti a;
+      a.key = normalize_key(str(q.topology_key));
+      if (a.key != kHostname) throw Unsupported{GS_E_UNSUPPORTED, "pod anti-affinity topologyKey other than hostname"};
+      a.required = q.required != 0;
+      a.weight = q.weight;
+      a.sel.has_selector = q.has_selector != 0;
+      a.sel.match_labels = labels_of(q.match_labels);
+      check_range(q.match_expressions, p->n_reqs, "reqs");
+      for (uint32_t e = 0; e < q.match_expressions.count; e++) {
+        const gs_requirement& r = p->reqs[q.match_expressions.begin + e];
+        if (r.op > GS_OP_DOES_NOT_EXIST) throw Unsupported{GS_E_INVALID, "label selector operator"};
+        check_range(r.values, p->n_value_ids, "values");
+        Spread::Expr x{str(r.key), (int)r.op, {}};
+        for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
+        a.sel.exprs.push_back(std::move(x));
+      }
+      check_range(q.namespaces, p->n_value_ids, "values");
+      for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(str(p->value_ids[q.namespaces.begin + v]));
+      if (a.nss.empty()) a.nss.insert(pd.ns);
+      (a.required ? pd.anti_required : pd.anti_preferred).push_back(std::move(a));
+    }
+    if (pd.anti_preferred.size() > 12) throw Unsupported{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
+    check_range(g.host_ports, p->n_host_ports, "host_ports");
+    for (uint32_t k = 0; k < g.host_ports.count; k++) {
+      const gs_host_port& q = p->host_ports[g.host_ports.begin + k];
+      if (q.port < 1 || q.port > 65535) throw Unsupported{GS_E_INVALID, "host port out of range"};
+      HostPort hp;
+      hp.proto = str(q.protocol).empty() ? "TCP" : str(q.protocol);
+      hp.port = q.port;
+      // net.ParseIP; nil -> 0.0.0.0
+      const string& ip = str(q.ip);
+      uint8_t b6[16];
+      in_addr b4;
+      if (inet_pton(AF_INET, ip.c_str(), &b4) == 1) {
+        std::memset(hp.ip.data(), 0, 10);
+        hp.ip[10] = hp.ip[11] = 0xff;
+        std::memcpy(hp.ip.data() + 12, &b4, 4);
+      } else if (inet_pton(AF_INET6, ip.c_str(), b6) == 1) {
+        std::memcpy(hp.ip.data(), b6, 16);
+      } else {
+        hp.ip.fill(0);
+        hp.ip[10] = hp.ip[11] = 0xff;  // 0.0.0.0
+      }
+      static const std::array<uint8_t, 16> z6{}, z4{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff, 0, 0, 0, 0};
+      hp.unspecified = hp.ip == z6 || hp.ip == z4;  // IsUnspecified
+      pd.ports.push_back(std::move(hp));
+    }
+  }
+
+  TGroup anti_group(const Anti& a) {
+    TGroup g;
+    g.anti = true;
+    g.key = a.key;
+    g.max_skew = INT32_MAX;
+    g.nss = a.nss;
+    g.sel = a.sel;
+    return g;
   }
 
   // <U> NewTopology: one group per distinct constraint of the pods being
@@ -653,8 +767,44 @@ struct Builder {
         }
         st.groups[gi].owners.insert(pd.index);
       }
-    if (st.groups.empty()) return;
-    for (auto& g : st.groups) {
+    // <U> newForTopologies: required and preferred anti-affinity terms
+    for (auto& pd : st.pods)
+      for (auto* terms : {&pd.anti_required, &pd.anti_preferred})
+        for (auto& a : *terms) {
+          const string h = a.hash();
+          auto f = st.group_index.find(h);
+          if (f == st.group_index.end()) {
+            f = st.group_index.emplace(h, st.groups.size()).first;
+            st.groups.push_back(anti_group(a));
+          }
+          st.groups[f->second].owners.insert(pd.index);
+        }
+    // <U> updateInverseAntiAffinity: one inverse group per required term,
+    // owned by the pods that carry it (pending pods here, bound pods below)
+    auto inverse_of = [&](const Anti& a) -> TGroup& {
+      const string h = a.hash();
+      auto f = st.inverse_index.find(h);
+      if (f == st.inverse_index.end()) {
+        f = st.inverse_index.emplace(h, st.inverse.size()).first;
+        st.inverse.push_back(anti_group(a));
+      }
+      return st.inverse[f->second];
+    };
+    for (auto& pd : st.pods)
+      for (auto& a : pd.anti_required) inverse_of(a).owners.insert(pd.index);
+    vector<Pod> bound(p->n_bound_pods);
+    for (uint32_t b = 0; b < p->n_bound_pods; b++) {
+      if (p->bound_pod_node[b] >= st.nodes.size()) throw Unsupported{GS_E_INVALID, "bound pod node out of range"};
+      bound[b].index = UINT32_MAX;
+      pod_meta(p->bound_pods[b], bound[b], false);
+      for (auto& a : bound[b].anti_required) inverse_of(a);
+      // ExistingNode hostPortUsage
+      auto& n = st.nodes[p->bound_pod_node[b]];
+      n.ports.insert(n.ports.end(), bound[b].ports.begin(), bound[b].ports.end());
+    }
+    if (st.groups.empty() && st.inverse.empty()) return;
+    for (auto* gs : {&st.groups, &st.inverse})
+    for (auto& g : *gs) {
       for (size_t i = 0; i < np_reqs.size(); i++) {
         if (!np_has_its[i] || !np_reqs[i].has_key(g.key)) continue;
         const Req q = np_reqs[i].get(g.key);
@@ -668,17 +818,26 @@ struct Builder {
           for (auto& v : q.values) g.domains.emplace(v, 0);
       }
     }
-    check_range(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
-      if (p->bound_pod_node[b] >= st.nodes.size()) throw Unsupported{GS_E_INVALID, "bound pod node out of range"};
-      Pod bp;
-      bp.index = UINT32_MAX;
-      pod_meta(p->bound_pods[b], bp);
+      const Pod& bp = bound[b];
       const ExistingNode& n = st.nodes[p->bound_pod_node[b]];
+      // countDomains: selected bound pods on their nodes' domains
       for (auto& g : st.groups) {
         if (!g.selects(bp) || !n.reqs.has_key(g.key)) continue;
         const Req q = n.reqs.get(g.key);
-        if (q.op() == GS_OP_IN && q.values.size() == 1) g.domains[*q.values.begin()]++;
+        if (q.op() != GS_OP_IN) continue;
+        if (g.anti)
+          for (auto& v : q.values) g.domains[v]++;
+        else if (q.values.size() == 1)
+          g.domains[*q.values.begin()]++;
+      }
+      // updateInverseAffinities: a bound carrier of a required term blocks its node
+      for (auto& a : bp.anti_required) {
+        TGroup& g = st.inverse[st.inverse_index.at(a.hash())];
+        if (!n.reqs.has_key(g.key)) continue;
+        const Req q = n.reqs.get(g.key);
+        if (q.op() == GS_OP_IN)
+          for (auto& v : q.values) g.domains[v]++;
       }
     }
   }
@@ -820,8 +979,19 @@ bool relax(Pod& p, bool tolerate_pns) {
     p.required.erase(p.required.begin());
     return true;
   }
-  // removePreferredPodAffinityTerm / AntiAffinity: pods with pod affinity are
-  // refused up front (GS_POD_AFFINITY), nothing to relax here
+  // removePreferredPodAffinityTerm: pods with pod affinity are refused up
+  // front (GS_POD_AFFINITY), nothing to relax here
+  // removePreferredPodAntiAffinityTerm: sort.Slice by weight desc, drop [0]
+  if (!p.anti_preferred.empty()) {
+    struct D {
+      vector<Anti>& t;
+      bool less(int i, int j) { return t[i].weight > t[j].weight; }
+      void swap(int i, int j) { std::swap(t[i], t[j]); }
+    } d{p.anti_preferred};
+    gosort::slice(d, (int)p.anti_preferred.size());
+    p.anti_preferred.erase(p.anti_preferred.begin());
+    return true;
+  }
   // removePreferredNodeAffinityTerm: sort.SliceStable by weight desc, drop [0]
   if (!p.preferred.empty()) {
     std::stable_sort(p.preferred.begin(), p.preferred.end(),
@@ -866,6 +1036,14 @@ struct Scheduler {
   // the node's domains within maxSkew.  Upstream iterates a Go map / an
   // unsorted set, so ties fall in random order; restated: smallest name.
   Req next_domain(const TGroup& g, const Pod& pod, const Req& pod_domains, const Req& node_domains) const {
+    if (g.anti) {
+      // nextDomainAntiAffinity: the empty domains both sides allow
+      vector<string> opts;
+      for (auto& kv : g.domains)
+        if (kv.second == 0 && node_domains.has(kv.first) && pod_domains.has(kv.first)) opts.push_back(kv.first);
+      if (opts.empty()) return make_req(g.key, GS_OP_DOES_NOT_EXIST, {}, std::nullopt);
+      return make_req(g.key, GS_OP_IN, opts, std::nullopt);
+    }
     const int64_t mn = domain_min_count(g, pod_domains);
     const int64_t self = g.selects(pod) ? 1 : 0;
     string best;
@@ -893,8 +1071,14 @@ struct Scheduler {
   bool topology = true;  // off for the static (fresh NodeClaim) feasibility matrix
   bool topo_requirements(const Pod& pod, const Reqs& node_reqs, Reqs* out) const {
     if (!topology) return true;
-    for (auto& g : st.groups) {
-      if (!g.owners.count(pod.index)) continue;
+    // getMatchingTopologies: owned groups, then inverse groups that select the pod
+    vector<const TGroup*> match;
+    for (auto& g : st.groups)
+      if (g.owners.count(pod.index)) match.push_back(&g);
+    for (auto& g : st.inverse)
+      if (g.selects(pod)) match.push_back(&g);
+    for (const TGroup* gp : match) {
+      const TGroup& g = *gp;
       const Req pd = pod.strict.has_key(g.key) ? pod.strict.get(g.key) : make_req(g.key, GS_OP_EXISTS, {}, std::nullopt);
       const Req nd = node_reqs.has_key(g.key) ? node_reqs.get(g.key) : make_req(g.key, GS_OP_EXISTS, {}, std::nullopt);
       const Req d = next_domain(g, pod, pd, nd);
@@ -909,13 +1093,26 @@ struct Scheduler {
     for (auto& g : st.groups) {
       if (!g.selects(pod) || !reqs.has_key(g.key)) continue;
       const Req d = reqs.get(g.key);
-      if (!d.complement && d.values.size() == 1) g.domains[*d.values.begin()]++;
+      if (d.complement) continue;
+      if (g.anti) {
+        for (auto& v : d.values) g.domains[v]++;  // every domain the pod could be in
+      } else if (d.values.size() == 1) {
+        g.domains[*d.values.begin()]++;
+      }
+    }
+    // inverse groups the pod owns record where it landed
+    for (auto& g : st.inverse) {
+      if (!g.owners.count(pod.index) || !reqs.has_key(g.key)) continue;
+      const Req d = reqs.get(g.key);
+      if (!d.complement)
+        for (auto& v : d.values) g.domains[v]++;
     }
   }
   // Topology.Register(hostname, placeholder)
   void topo_register_hostname(const string& h) {
-    for (auto& g : st.groups)
-      if (g.key == kHostname) g.domains.emplace(h, 0);
+    for (auto* gs : {&st.groups, &st.inverse})
+      for (auto& g : *gs)
+        if (g.key == kHostname) g.domains.emplace(h, 0);
   }
   // Topology.Update after a relaxation: ownership follows the remaining constraints
   void topo_update(const Pod& pod) {
@@ -924,6 +1121,11 @@ struct Scheduler {
       auto f = st.group_index.find(sp.hash(pod.ns));
       if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
     }
+    for (auto* terms : {&pod.anti_required, &pod.anti_preferred})
+      for (auto& a : *terms) {
+        auto f = st.group_index.find(a.hash());
+        if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
+      }
   }
 
   vector<NodeClaim*> claims;  // s.newNodeClaims (sorted in place per pod)
@@ -936,6 +1138,7 @@ struct Scheduler {
   bool claim_can_add(const NodeClaim& n, const Pod& pod, Reqs* reqs_out, vector<const InstanceType*>* its_out,
                      Res* req_out) {
     if (!tolerates_all(n.tmpl->taints, pod.tolerations)) return false;
+    if (ports_conflict(n.ports, pod.ports)) return false;  // hostPortUsage.Conflicts
     Res requests = merge(n.requests, pod.requests);
     // Evaluation order only (same result): filterInstanceTypesByRequirements
     // keeps an instance type only if Fits(requests, allocatable), and every
@@ -966,6 +1169,7 @@ struct Scheduler {
   // <U> ExistingNode.CanAdd (strict Compatible: no AllowUndefined)
   bool node_can_add(const ExistingNode& n, const Pod& pod, Reqs* reqs_out, Res* req_out) {
     if (!tolerates_all(n.taints, pod.tolerations)) return false;
+    if (ports_conflict(n.ports, pod.ports)) return false;  // hostPortUsage.Conflicts
     Res requests = merge(n.requests, pod.requests);
     if (!fits(requests, n.available)) return false;
     Reqs nr = n.reqs;
@@ -991,6 +1195,7 @@ struct Scheduler {
         n.reqs = std::move(r);
         n.requests = std::move(q);
         n.pods.push_back(&pod);
+        n.ports.insert(n.ports.end(), pod.ports.begin(), pod.ports.end());
         topo_record(pod, n.reqs);
         return true;
       }
@@ -1012,6 +1217,7 @@ struct Scheduler {
         nc->options = std::move(its);
         nc->requests = std::move(q);
         nc->pods.push_back(&pod);
+        nc->ports.insert(nc->ports.end(), pod.ports.begin(), pod.ports.end());
         topo_record(pod, nc->reqs);
         return true;
       }
@@ -1049,6 +1255,7 @@ struct Scheduler {
       nc->options = std::move(its2);
       nc->requests = std::move(q);
       nc->pods.push_back(&pod);
+      nc->ports.insert(nc->ports.end(), pod.ports.begin(), pod.ports.end());
       topo_record(pod, nc->reqs);
       if (rem != st.remaining.end()) {
         // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
@@ -1505,7 +1712,8 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
       if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
     for (uint32_t i = 0; i < in->cluster->n_bound_pods; i++)
       if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
-    if (in->cluster->n_spreads) return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
+    if (in->cluster->n_spreads || in->cluster->n_anti_affinities || in->cluster->n_host_ports)
+      return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
     if (in->mode == GS_CONSOLIDATE_EVAL) {
       for (uint32_t s = 0; s < in->n_sets; s++) {
         if ((uint64_t)in->sets[s].begin + in->sets[s].count > in->n_candidates) return GS_E_INVALID;

@@ -42,6 +42,8 @@ def _problems():
         out.append((f"topo{s}", synth.random_topology(s)))
     for s in range(8):
         out.append((f"cons{s}", synth.random_consolidation(s)))
+    for s in range(10):
+        out.append((f"anti{s}", synth.random_affinity(s)))
     out.append(("c1", synth.make_c1()))
     out.append(("c3_2k", synth.make_c3(n_pods=2000)))
     out.append(("c4_200", synth.make_c4(n_nodes=200, n_pending=5)))
@@ -67,11 +69,16 @@ def _corrupt(kind):
         p.quantities["resource"][0] = len(p.strings) + 7
     elif kind == "nodepool_it_refs":
         p.nodepools["instance_types"]["count"][0] = len(p.it_refs) + 1
+    elif kind == "anti_affinity_range":
+        p.pods["anti_affinity"]["begin"][0] = len(p.anti_affinities) + 2
+        p.pods["anti_affinity"]["count"][0] = 1
+    elif kind == "host_port_range":
+        p.pods["host_ports"]["count"][len(p.pods) - 1] = 1 << 31
     return p
 
 
 CORRUPT = ["pod_requests_range", "req_key_id", "value_range", "it_offerings_range", "node_labels_range",
-           "quantity_resource_id", "nodepool_it_refs"]
+           "quantity_resource_id", "nodepool_it_refs", "anti_affinity_range", "host_port_range"]
 
 
 def _run(harness, dumps):

@@ -25,15 +25,15 @@ struct Dump {
 
 bool read_exact(FILE* f, void* dst, size_t n) { return fread(dst, 1, n, f) == n; }
 
-// layout: magic "GSPD", u32 version 1, u32 n_strings, per string u32 len +
-// bytes, then 16 arrays in gs_problem order (value_ids .. bound_pod_node),
+// layout: magic "GSPD", u32 version 2, u32 n_strings, per string u32 len +
+// bytes, then 18 arrays in gs_problem order (value_ids .. host_ports),
 // each u64 count + u64 element size + raw bytes
 bool load(const char* path, Dump& d) {
   FILE* f = fopen(path, "rb");
   if (!f) return false;
   char magic[4];
   uint32_t ver = 0, ns = 0;
-  bool ok = read_exact(f, magic, 4) && memcmp(magic, "GSPD", 4) == 0 && read_exact(f, &ver, 4) && ver == 1 &&
+  bool ok = read_exact(f, magic, 4) && memcmp(magic, "GSPD", 4) == 0 && read_exact(f, &ver, 4) && ver == 2 &&
             read_exact(f, &ns, 4);
   for (uint32_t i = 0; ok && i < ns; i++) {
     uint32_t len = 0;
@@ -42,7 +42,7 @@ bool load(const char* path, Dump& d) {
     ok = ok && (len == 0 || read_exact(f, &s[0], len));
     d.strs.push_back(std::move(s));
   }
-  for (int a = 0; ok && a < 16; a++) {
+  for (int a = 0; ok && a < 18; a++) {
     uint64_t n = 0, es = 0;
     ok = read_exact(f, &n, 8) && read_exact(f, &es, 8);
     std::vector<char> buf(n * es);
@@ -73,6 +73,8 @@ bool load(const char* path, Dump& d) {
   p.spreads = (const gs_spread*)A(13), p.n_spreads = N(13, sizeof(gs_spread));
   p.bound_pods = (const gs_pod*)A(14), p.n_bound_pods = N(14, sizeof(gs_pod));
   p.bound_pod_node = (const uint32_t*)A(15);
+  p.anti_affinities = (const gs_anti_affinity*)A(16), p.n_anti_affinities = N(16, sizeof(gs_anti_affinity));
+  p.host_ports = (const gs_host_port*)A(17), p.n_host_ports = N(17, sizeof(gs_host_port));
   return true;
 }
 
