@@ -84,7 +84,11 @@ typedef struct gs_requirement {
   uint32_t key;          /* string id */
   uint32_t op;           /* GS_OP_* */
   gs_range values;       /* into gs_problem.value_ids (string ids) */
-  int32_t min_values;    /* -1 when unset */
+  int32_t min_values;    /* -1 when unset.  NodePool requirements: <U> Strict
+                            minValues (SatisfiesMinValues in CanAdd, at
+                            NewScheduler and after Truncate(60)); claim queries:
+                            ignored; pod terms: GS_E_UNSUPPORTED; consolidation
+                            and static-matrix column shards: GS_E_UNSUPPORTED */
 } gs_requirement;
 
 typedef struct gs_quantity {
@@ -516,8 +520,8 @@ typedef struct gs_claim_filter_result {
  * for n_queries NodeClaims against the catalog's instance types (only the
  * catalog fields of `catalog` are read: strings, value_ids, reqs, quantities,
  * offerings, instance_types).  Requirements use the full scheduling.Requirement
- * algebra (In/NotIn/Exists/DoesNotExist/Gt/Lt, any key, label-key
- * normalisation); Gte/Lte and minValues are GS_E_UNSUPPORTED.  One device
+ * algebra (In/NotIn/Exists/DoesNotExist/Gt/Lt/Gte/Lte, any key, label-key
+ * normalisation); minValues is ignored, as Compatible ignores it.  One device
  * pass over all (claim, instance type) pairs on the ctx's device. */
 gs_status gs_create_filter(gs_ctx* ctx, const gs_problem* catalog, const gs_claim_query* queries,
                            uint32_t n_queries, gs_claim_filter_result* out);

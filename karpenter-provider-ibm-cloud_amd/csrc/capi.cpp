@@ -43,6 +43,9 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     if (!d.max_claims) throw HipError{"topology / threshold state leaves no LDS for NodeClaims"};
   }
   c->upload(d.it_vid, e.it_vid);
+  c->upload(d.it_dvid, e.it_dvid);
+  d.it_key_unique = e.it_key_unique;
+  d.any_mv = e.any_mv ? 1u : 0u;
   c->upload(d.it_alloc, e.it_alloc);
   c->upload(d.it_cap, e.it_cap);
   c->upload(d.it_pair, e.it_pair);
@@ -255,6 +258,9 @@ void build_grid_orders(gs_ctx* c) {
 void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u) {
   if (apply_limits) build_grid_orders(c);
   HIPCHK(gsk_feas(&c->dp, apply_limits, w_lo, w_hi, c->stream));
+  // the static matrix's rows answer CanAdd on a fresh NodeClaim, minValues
+  // included (whole rows only: callers refuse column shards with minValues)
+  if (apply_limits && c->enc.any_mv) HIPCHK(gsk_mv_rows(&c->dp, c->stream));
 }
 
 // device capacity of the encoded problem (the FFD kernel keeps these in LDS)
@@ -504,8 +510,24 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   c->claim_its.clear();
   c->req_text.assign(M, "");
   c->claim_requests.assign((size_t)M * e.R, 0);
+  // <U> Results.TruncateInstanceTypes: a NodeClaim whose top 60 by price miss
+  // its template's minValues is dropped, its pods become pod errors
+  std::vector<uint32_t> dropped_pods;
+  uint32_t kept = 0;
   for (uint32_t j = 0; j < M; j++) {
-    c->claim_nodepool[j] = e.tmpl[hdr[j].tmpl].np_index;
+    const gsd::TmplRec& tr = e.tmpl[hdr[j].tmpl];
+    bool drop = false;
+    for (uint32_t mm = tr.mv_mask; mm && !drop; mm &= mm - 1) {
+      const uint32_t k = (uint32_t)__builtin_ctz(mm);
+      std::set<uint32_t> vals;
+      for (uint32_t q = 0; q < nits[j]; q++) vals.insert(e.it_vid[(size_t)k * e.N + its[(size_t)j * 60 + q]]);
+      drop = vals.size() < tr.mv[k];
+    }
+    if (drop) {
+      dropped_pods.insert(dropped_pods.end(), cp[j].begin(), cp[j].end());
+      continue;
+    }
+    c->claim_nodepool[kept] = tr.np_index;
     c->claim_pods.insert(c->claim_pods.end(), cp[j].begin(), cp[j].end());
     c->claim_pod_offsets.push_back((uint32_t)c->claim_pods.size());
     c->claim_its.insert(c->claim_its.end(), its.begin() + (size_t)j * 60, its.begin() + (size_t)j * 60 + nits[j]);
@@ -521,13 +543,18 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
       gsh::reqs_add(e, creq[j], e.k_zone, q);
     }
     creq[j].erase(e.k_hostname);  // FinalizeScheduling
-    c->req_text[j] = gsh::canonical(e, creq[j]);
-    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)j * e.R + r] = hdr[j].tot(r);
+    c->req_text[kept] = gsh::canonical(e, creq[j]);
+    for (uint32_t r = 0; r < e.R; r++) c->claim_requests[(size_t)kept * e.R + r] = hdr[j].tot(r);
+    kept++;
   }
+  c->claim_nodepool.resize(kept);
+  c->req_text.resize(kept);
+  c->claim_requests.resize((size_t)kept * e.R);
   c->req_ptrs.clear();
   for (auto& s : c->req_text) c->req_ptrs.push_back(s.c_str());
   c->error_pods.clear();
   for (uint32_t i = 0; i < c->ctrl.qlen; i++) c->error_pods.push_back(queue[(c->ctrl.qhead + i) % e.P]);
+  c->error_pods.insert(c->error_pods.end(), dropped_pods.begin(), dropped_pods.end());
   std::sort(c->error_pods.begin(), c->error_pods.end());
   for (auto& v : np_) {
     c->node_pods.insert(c->node_pods.end(), v.begin(), v.end());
@@ -535,7 +562,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   }
   c->t_fetch = ms_since(t0);
   std::memset(out, 0, sizeof(*out));
-  out->n_claims = M;
+  out->n_claims = kept;
   out->claim_nodepool = c->claim_nodepool.data();
   out->claim_pod_offsets = c->claim_pod_offsets.data();
   out->claim_pods = c->claim_pods.data();
@@ -584,6 +611,8 @@ gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
 
 gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
+  if (c->enc.any_mv && (!c->shards.empty() || word_begin > 0 || word_end < c->enc.W))
+    return fail(c, GS_E_UNSUPPORTED, "minValues needs whole static-matrix rows (no instance-type column shards)");
   if (!c->shards.empty()) return sharded_feasibility(c, word_begin, word_end, out);
   auto& e = c->enc;
   const uint32_t P = e.P, NP = c->n_nodepools, W = e.W;
@@ -649,6 +678,8 @@ gs_status gs_feasibility_shard_device(gs_ctx* c, uint32_t word_begin, uint32_t w
     return fail(c, GS_E_UNSUPPORTED, "device-resident shard results on a sharded context (use one context per device)");
   auto& e = c->enc;
   word_end = std::min(word_end, e.W);
+  if (e.any_mv && (word_begin > 0 || word_end < e.W))
+    return fail(c, GS_E_UNSUPPORTED, "minValues needs whole static-matrix rows (no instance-type column shards)");
   if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
   float ms = 0;
   try {

@@ -506,6 +506,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
   er = capacity_check(c->enc);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
+  if (c->enc.any_mv) return fail(c, GS_E_UNSUPPORTED, "minValues in consolidation simulations");
   st = plan_sims(c, &c->cons_in, &err);
   if (st != GS_OK) return fail(c, st, err);
   try {

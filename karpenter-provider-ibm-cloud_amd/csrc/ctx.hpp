@@ -28,6 +28,7 @@ extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total);
 extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
 extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t gsk_mv_rows(const gsd::DevProblem* d, hipStream_t s);
 
 namespace gsc {
 

@@ -104,11 +104,13 @@ KReq kreq_intersect(const Vocab& v, const KReq& a, const KReq& b) {
   r.gt = a.hg && b.hg ? std::max(a.gt, b.gt) : (a.hg ? a.gt : b.gt);
   r.hl = a.hl || b.hl;
   r.lt = a.hl && b.hl ? std::min(a.lt, b.lt) : (a.hl ? a.lt : b.lt);
+  r.mv = std::max(a.mv, b.mv);
   if (r.hg && r.hl && r.gt >= r.lt) {  // DoesNotExist
     KReq d;
     d.comp = false;
     d.has = Bits(v.words());
     d.excl = Bits(v.words());
+    d.mv = r.mv;
     return d;
   }
   r.has = a.has;
@@ -243,7 +245,6 @@ struct Ctx {
     for (uint32_t i = 0; i < r.count; i++) {
       auto& q = p->reqs[r.begin + i];
       if (q.op > GS_OP_LTE) throw Fail{GS_E_INVALID, "unknown requirement operator"};
-      if (q.min_values >= 0) throw Fail{GS_E_UNSUPPORTED, "minValues"};
       chk(q.values, p->n_value_ids, "values");
       mention_key(S(q.key));
       if (q.op == GS_OP_IN || q.op == GS_OP_NOTIN)
@@ -361,7 +362,16 @@ struct Ctx {
       op = GS_OP_LT;
       bound += 1;
     }
-    return make_kreq(v, op, vals, bound);
+    KReq r = make_kreq(v, op, vals, bound);
+    r.mv = q.min_values >= 0 ? q.min_values : -1;
+    return r;
+  }
+  // a pod's NodeSelectorRequirement carries no minValues
+  void no_min_values(gs_range r) const {
+    chk(r, p->n_reqs, "reqs");
+    for (uint32_t i = 0; i < r.count; i++)
+      if (p->reqs[r.begin + i].min_values >= 0)
+        throw Fail{GS_E_UNSUPPORTED, "minValues outside NodePool / NodeClaim requirements"};
   }
   Reqs reqs_of(gs_range r) const {
     Reqs out;
@@ -1026,6 +1036,18 @@ struct Ctx {
   bool tolerate_pns = false;
   std::vector<std::vector<Tol>> variant_tols;
   void build_templates() {
+    // dense per-key value ids of the catalog (minValues counting)
+    e.it_dvid.assign((size_t)e.K * e.N, 0);
+    e.it_ndv.assign(e.K, 0);
+    for (uint32_t k = 0; k < e.K; k++) {
+      std::map<uint32_t, uint16_t> dense;
+      for (uint32_t i = 0; i < e.N; i++) {
+        auto f = dense.emplace(e.it_vid[(size_t)k * e.N + i], (uint16_t)std::min<size_t>(dense.size(), 65535)).first;
+        e.it_dvid[(size_t)k * e.N + i] = f->second;
+      }
+      e.it_ndv[k] = (uint32_t)dense.size();
+      if (dense.size() == e.N) e.it_key_unique |= 1u << k;
+    }
     std::vector<uint32_t> order(p->n_nodepools);
     std::iota(order.begin(), order.end(), 0);
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
@@ -1072,6 +1094,27 @@ struct Ctx {
       }
       uint64_t tm = taint_mask(np.taints);
       np_universe.emplace_back(tr, has_its);
+      // <U> minValues (Strict): NewScheduler's filterInstanceTypesByRequirements
+      // drops the NodePool when its options miss a minimum.  Instance types
+      // carry no value for a key outside the IT keys (Values() is empty).
+      uint32_t mv_mask = 0;
+      uint16_t mvk[gsd::KMAX_IT] = {0};
+      for (auto& kv : tr) {
+        if (kv.second.mv <= 0) continue;
+        if (e.keys[kv.first].cls != KEY_IT) {
+          any = false;
+          continue;
+        }
+        const int ks = e.keys[kv.first].slot;
+        if (!((e.it_key_unique >> ks) & 1) && e.it_ndv[ks] > 256)
+          throw Fail{GS_E_UNSUPPORTED, "minValues on a key with more than 256 instance-type values"};
+        mv_mask |= 1u << ks;
+        mvk[ks] = (uint16_t)std::min<int64_t>(kv.second.mv, 65535);
+        std::set<uint32_t> vals;
+        for (uint32_t i = 0; i < e.N; i++)
+          if ((opts[i / 64] >> (i % 64)) & 1) vals.insert(e.it_vid[(size_t)ks * e.N + i]);
+        if ((int64_t)vals.size() < kv.second.mv) any = false;
+      }
       if (!any) continue;
       if (e.T >= (uint32_t)gsd::TMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 NodePools"};
       gsd::TmplRec t{};
@@ -1105,6 +1148,9 @@ struct Ctx {
       }
       t.zfull = zone_full(tr);
       t.zflags = zone_flags(tr);
+      t.mv_mask = mv_mask;
+      for (int k = 0; k < gsd::KMAX_IT; k++) t.mv[k] = mvk[k];
+      if (mv_mask) e.any_mv = true;
       e.tmpl.push_back(t);
       e.t_opts.insert(e.t_opts.end(), opts.begin(), opts.end());
       e.tmpl_reqs.push_back(tr);
@@ -1171,11 +1217,14 @@ struct Ctx {
       // spec pieces
       Reqs ns = labels_reqs(pd.node_selector);
       std::vector<Reqs> req_terms;
-      for (uint32_t k = 0; k < pd.required_terms.count; k++)
+      for (uint32_t k = 0; k < pd.required_terms.count; k++) {
+        no_min_values(p->terms[pd.required_terms.begin + k].requirements);
         req_terms.push_back(reqs_of(p->terms[pd.required_terms.begin + k].requirements));
+      }
       std::vector<std::pair<int32_t, Reqs>> pref;
       for (uint32_t k = 0; k < pd.preferred_terms.count; k++) {
         auto& tm = p->terms[pd.preferred_terms.begin + k];
+        no_min_values(tm.requirements);
         pref.push_back({tm.weight, reqs_of(tm.requirements)});
       }
       if (pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred node-affinity terms"};
@@ -1489,7 +1538,8 @@ std::string canonical(const Encoded& e, const Reqs& r) {
     s += q.comp && q.hg ? std::to_string(q.gt) : "-";
     s += '|';
     s += q.comp && q.hl ? std::to_string(q.lt) : "-";
-    s += "|-";
+    s += '|';
+    s += q.mv >= 0 ? std::to_string(q.mv) : "-";
   }
   return s;
 }

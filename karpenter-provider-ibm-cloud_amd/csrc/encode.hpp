@@ -61,6 +61,7 @@ struct KReq {
   Bits excl;  // complement sets: excluded values (after bound filtering)
   bool hg = false, hl = false;
   int64_t gt = 0, lt = 0;
+  int64_t mv = -1;  // minValues (-1: unset); Add keeps the larger
 };
 
 enum KeyClass : uint8_t { KEY_IT = 0, KEY_ZONE = 1, KEY_CT = 2, KEY_FREE = 3 };
@@ -100,6 +101,10 @@ struct Encoded {
   uint64_t checks_per_pod = 0;
   // device arrays (host copies)
   std::vector<uint32_t> it_vid, it_prank, it_namerank, rank_to_it, thr_off;
+  std::vector<uint16_t> it_dvid;    // [K][N] dense value ids for minValues counting
+  uint32_t it_key_unique = 0;       // IT keys with a distinct value per type
+  std::vector<uint32_t> it_ndv;     // [K] distinct values per IT key
+  bool any_mv = false;              // some template carries minValues
   std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
   std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
   std::vector<double> prices;  // distinct offering prices ascending: price rank -> price

@@ -86,6 +86,7 @@ struct Shared {
   uint64_t tl[16], tl_last;  // GS_FFD_TL: shader cycles per loop segment (tid 0)
   uint64_t tl_arr[NWAVE_MAX];  // GS_FFD_TL: per-wave arrival at the loop-top barrier
   uint32_t c0[RMAX];  // threshold cursors of a NodeClaim being opened
+  uint32_t mvok;      // minValues verdict on the NodeClaim being opened
   uint32_t red[2][NWAVE_MAX];
   alignas(16) uint32_t red2[2][NWAVE_MAX];  // Wg reductions (own double buffer: never adjacent to a Blk one)
   unsigned long long red64[RMAX];
@@ -1343,6 +1344,21 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                 }
               }
               feas = acc != 0;
+              if (TOPO && feas && dd.tmpl[t].mv_mask) {
+                // minValues over the NodeClaim's options after Add (per thread)
+                feas = mv_ok(dd, dd.tmpl[t], [&](uint32_t w) -> uint64_t {
+                  if (W <= WREG) return w == 0 ? nx[0] : w == 1 ? nx[1] : w == 2 ? nx[2] : nx[3];
+                  uint64_t x = opts[w] & row[w];
+#pragma unroll
+                  for (uint32_t r = 0; r < RR; r++) x &= dd.thr_set[(size_t)mrow[r] * OW + w];
+                  if (G != Gt) {
+                    uint64_t off = 0;
+                    for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)(__ffsll((long long)gm) - 1) * W + w];
+                    x &= off;
+                  }
+                  return x;
+                });
+              }
 #ifdef GS_FFD_DIAG
               c3 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1577,20 +1593,14 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           }
           if (wg.first(hit == 0, 0) == INF) continue;
         }
-        if (M >= MCs) {
-          if (tid == 0) HN.status = 1;
-          __syncthreads();
-          break;
-        }
-        const uint32_t j = M;
-        ClaimRec* cr = d.c_rec + cbase + j;
         if (tid < R) {
           const int64_t tot = tr.daemon[tid] + preq[tid];
           const uint32_t o = s_thoff[tid], n = s_thoff[tid + 1] - o;
           S.c0[tid] = thr_search(thr + o, n, 0, tot);
         }
         __syncthreads();
-        for (uint32_t w = tid; w < W; w += FB) {
+        // the fresh NodeClaim's option word w
+        auto fresh = [&](uint32_t w) -> uint64_t {
           uint64_t x = rowx(w);
           // establish opts ⊆ thr_set[cursor] for the candidate scan
           for (uint32_t r = 0; r < R; r++) x &= d.thr_set[(size_t)(s_thoff[r] + r + S.c0[r]) * OW + w];
@@ -1607,8 +1617,22 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
             }
             x = y;
           }
-          d.c_opts[(size_t)(cbase + j) * OW + w] = x;
+          return x;
+        };
+        if (TOPO && tr.mv_mask) {
+          // minValues over the fresh NodeClaim's options (one thread)
+          if (tid == 0) S.mvok = mv_ok(d, tr, fresh) ? 1u : 0u;
+          __syncthreads();
+          if (!S.mvok) continue;
         }
+        if (M >= MCs) {
+          if (tid == 0) HN.status = 1;
+          __syncthreads();
+          break;
+        }
+        const uint32_t j = M;
+        ClaimRec* cr = d.c_rec + cbase + j;
+        for (uint32_t w = tid; w < W; w += FB) d.c_opts[(size_t)(cbase + j) * OW + w] = fresh(w);
         if (tid < RR) {
           int64_t tot = 0;
           uint32_t c0 = 0;
@@ -1847,7 +1871,7 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   const bool sim = d->n_sims > 0;
   if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread
   // shape: 0 provisioning, 1 provisioning with topology spread, 2 simulations
-  switch (d->R * 4 + (sim ? 2 : (d->TG ? 1 : 0))) {
+  switch (d->R * 4 + (sim ? 2 : (d->TG || d->any_mv ? 1 : 0))) {
 #define GSK_CASE(n)                                                                                          \
   case 4 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
   case 4 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \

@@ -434,5 +434,42 @@ __device__ __forceinline__ uint64_t pack_slack(const DP& d, const int64_t* maxa,
   return s;
 }
 
+// <U> InstanceTypes.SatisfiesMinValues (Strict policy) on the template's IT
+// keys: the distinct values of key k over an option set reach tr.mv[k].
+// word(w) yields the set's w-th word; the caller keeps word() uniform when
+// it evaluates per wave.  Keys with a distinct value per type count types;
+// the others OR dense value ids (< 256, checked by the encoder) into a
+// 256-bit set.  Every loop stops once the minimum is reached.
+template <class DP, class WordFn>
+__device__ inline bool mv_ok(const DP& d, const TmplRec& tr, WordFn word) {
+  for (uint32_t mm = tr.mv_mask; mm; mm &= mm - 1) {
+    const uint32_t k = (uint32_t)__builtin_ctz(mm);
+    const uint32_t need = tr.mv[k];
+    uint32_t n = 0;
+    if ((d.it_key_unique >> k) & 1) {
+      for (uint32_t w = 0; w < d.W && n < need; w++) n += (uint32_t)__popcll(word(w));
+    } else {
+      const uint16_t* dv = d.it_dvid + (size_t)k * d.N;
+      uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+      for (uint32_t w = 0; w < d.W && n < need; w++)
+        for (uint64_t m = word(w); m && n < need; m &= m - 1) {
+          const uint32_t x = dv[w * 64 + (uint32_t)__builtin_ctzll(m)];
+          const uint32_t q = x >> 6;
+          const uint64_t bit = 1ull << (x & 63);
+          const uint64_t cur = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
+          if (!(cur & bit)) {
+            n++;
+            s0 |= q == 0 ? bit : 0;
+            s1 |= q == 1 ? bit : 0;
+            s2 |= q == 2 ? bit : 0;
+            s3 |= q == 3 ? bit : 0;
+          }
+        }
+    }
+    if (n < need) return false;
+  }
+  return true;
+}
+
 }  // namespace
 }  // namespace gsd

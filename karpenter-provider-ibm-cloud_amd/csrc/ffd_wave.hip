@@ -1077,6 +1077,21 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             }
           }
           feas = accw != 0;
+          if (TOPO && feas && KD.tmpl[t].mv_mask) {
+            // minValues over the NodeClaim's options after Add (per lane)
+            feas = mv_ok(KD, KD.tmpl[t], [&](uint32_t w) -> uint64_t {
+              if (W <= WREG) return w == 0 ? nx[0] : w == 1 ? nx[1] : w == 2 ? nx[2] : nx[3];
+              uint64_t x = opts[w] & row[w];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
+              if (G != Gt) {
+                uint64_t off = 0;
+                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                x &= off;
+              }
+              return x;
+            });
+          }
         }
       }
         const uint64_t fm = __ballot(feas);
@@ -1298,12 +1313,6 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         }
         if (!__ballot(hit)) continue;
       }
-      if (M >= MC) {
-        status = 1;
-        break;
-      }
-      const uint32_t j = M;
-      ClaimRec* cr = KD.c_rec + j;
       // threshold cursors of the fresh claim: lane r < R
       int64_t tot_l = 0;
       uint32_t c0_l = 0;
@@ -1337,9 +1346,20 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
           x = y;
         }
-        KD.c_opts[(size_t)j * OW + w] = x;
         xw[h] = x;
       }
+      // minValues over the fresh NodeClaim's options (uniform: every lane
+      // evaluates the same words)
+      if (TOPO && tr.mv_mask && !mv_ok(KD, tr, [&](uint32_t w) { return shfl_u64(xw[w >> 6], w & 63); })) continue;
+      if (M >= MC) {
+        status = 1;
+        break;
+      }
+      const uint32_t j = M;
+      ClaimRec* cr = KD.c_rec + j;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++)
+        if (lane + 64 * h < W) KD.c_opts[(size_t)j * OW + lane + 64 * h] = xw[h];
       if (lane < RR) {
         cr->tot(lane) = tot_l;
         cr->thr(lane) = (uint16_t)c0_l;
@@ -1525,7 +1545,7 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
-  switch (d->R * 2 + (d->TG ? 1 : 0)) {
+  switch (d->R * 2 + (d->TG || d->any_mv ? 1 : 0)) {
 #define GSK_CASE(n)                                                                                      \
   case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(128), lds, s, *d); break;      \
   case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(128), lds, s, *d); break;

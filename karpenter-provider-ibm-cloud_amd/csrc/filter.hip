@@ -228,7 +228,7 @@ struct Enc {
   // <U> NewRequirement (keys normalised, In/NotIn values, Gt/Lt bounds)
   HReq make(const gs_requirement& q) {
     if (q.op > GS_OP_LTE) throw Fail{GS_E_INVALID, "unknown requirement operator"};
-    if (q.min_values >= 0) throw Fail{GS_E_UNSUPPORTED, "minValues"};
+    // minValues: Compatible ignores it (reference cloudprovider.go:321-325)
     chk(q.values, p->n_value_ids, "values");
     const std::string k = gsh::label_normalize(S(q.key));
     auto f = key_id.find(k);

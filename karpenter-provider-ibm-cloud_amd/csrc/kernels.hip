@@ -289,6 +289,56 @@ extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, uint32
   return hipGetLastError();
 }
 
+// <U> minValues (Strict) on the static matrix: a fresh NodeClaim whose
+// options miss a template minimum is not addable, so its row is empty (no
+// cheapest type, no offering).  One wave per (variant, template) pair whose
+// template carries minValues; lane w holds words w, w + 64, ...
+__global__ __launch_bounds__(BLOCK) void mv_rows_kernel(DevProblem d) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t pair = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+  if (pair >= d.V * d.T) return;  // wave-uniform
+  const TmplRec& tr = d.tmpl[pair % d.T];
+  if (!tr.mv_mask) return;
+  uint64_t* row = d.rows + (size_t)pair * d.OW;
+  bool ok = true;
+  for (uint32_t mm = tr.mv_mask; mm && ok; mm &= mm - 1) {
+    const uint32_t k = (uint32_t)__builtin_ctz(mm);
+    uint32_t n = 0;
+    if ((d.it_key_unique >> k) & 1) {
+      for (uint32_t w = lane; w < d.W; w += 64) n += (uint32_t)__popcll(row[w]);
+      n = wave_sum_u32(n);
+    } else {
+      const uint16_t* dv = d.it_dvid + (size_t)k * d.N;
+      uint64_t sv[4] = {0, 0, 0, 0};
+      for (uint32_t w = lane; w < d.W; w += 64)
+        for (uint64_t m = row[w]; m; m &= m - 1) {
+          const uint32_t x = dv[w * 64 + (uint32_t)__builtin_ctzll(m)];
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) sv[q] |= (x >> 6) == q ? 1ull << (x & 63) : 0ull;
+        }
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        for (int o = 32; o >= 1; o >>= 1) sv[q] |= shfl_xor_u64(sv[q], o);
+        n += (uint32_t)__popcll(sv[q]);
+      }
+    }
+    ok = n >= tr.mv[k];
+  }
+  if (ok) return;
+  for (uint32_t w = lane; w < d.W; w += 64) row[w] = 0;
+  if (lane == 0) {
+    d.nfo[pair] = 0;
+    d.cheapest[pair] = NONE;
+    d.cheapest_key[pair] = 0x7FFFFFFFFFFFFFFFull;
+  }
+}
+
+extern "C" hipError_t gsk_mv_rows(const DevProblem* d, hipStream_t s) {
+  const uint64_t pairs = (uint64_t)d->V * d->T;
+  if (!pairs) return hipSuccess;
+  hipLaunchKernelGGL(mv_rows_kernel, dim3((uint32_t)((pairs + BLOCK / 64 - 1) / (BLOCK / 64))), dim3(BLOCK), 0, s, *d);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t gsk_trunc(const DevProblem* d, uint32_t lds_bytes, hipStream_t s) {
   const uint32_t grid = d->n_sims ? d->n_sims : d->max_claims;

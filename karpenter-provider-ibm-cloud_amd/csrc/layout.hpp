@@ -92,7 +92,8 @@ struct TmplRec {
   int64_t limits[RMAX];  // initial remaining limits
   uint64_t zfull;        // zone Has over the zone vocabulary
   uint32_t zflags;       // ZF_COMP
-  uint32_t pad2;
+  uint32_t mv_mask;      // IT keys with a minValues requirement (Strict policy)
+  uint16_t mv[KMAX_IT];  // minValues per IT key
 };
 
 // one topology spread group (<U> TopologyGroup, type spread, empty node filter)
@@ -179,6 +180,9 @@ struct DevProblem {
   uint64_t wk_slots;  // free slots whose key is well-known
   // catalog
   const uint32_t* it_vid;      // [K][N]
+  const uint16_t* it_dvid;     // [K][N] dense id of the type's value among the catalog's (minValues)
+  uint32_t it_key_unique;      // IT keys whose value differs for every type (minValues counts types)
+  uint32_t any_mv;             // a template carries minValues: the Solve runs the general (TOPO) variant
   const int64_t* it_alloc;     // [R][N]
   const int64_t* it_cap;       // [R][N]
   const uint64_t* it_pair;     // [N] available (zone,ct) pairs

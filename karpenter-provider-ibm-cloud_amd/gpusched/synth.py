@@ -724,3 +724,82 @@ def e2e_deployments(n_deployments=8, replicas=20, with_nodes=False, seed=0x5EED0
                       labels={"app": name, "test": "e2e", "purpose": "karpenter-test"},
                       anti_affinity=[{"required": False, "weight": 100, "selector": {"labels": {"app": name}}}])
     return b.build()
+
+
+IT_KEY = "node.kubernetes.io/instance-type"
+FAMILY_KEY = "karpenter-ibm.sh/instance-family"
+SIZE_KEY = "karpenter-ibm.sh/instance-size"
+
+
+def random_min_values(seed, n_pods=None):
+    """small adversarial problems for NodePool minValues (Strict): minimums on
+    the instance-type, family and size keys (and, rarely, on a key instance
+    types do not carry), pods whose selectors and requests narrow the options
+    below the minimum, NodePool limits, several NodePools, existing nodes"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
+    profs = []
+    for fam in ["bx2", "cx2", "mx2", "ox2"]:
+        for v in [2, 4, 8, 16, 32]:
+            if rng.random() < 0.75:
+                profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    if len(profs) < 2:
+        profs = [("bx2-4x16", 4, 16, None), ("cx2-4x8", 4, 8, None)]
+    prices = {p_[0]: round(0.05 * p_[1] + 0.01 * float(rng.random()), 4) for p_ in profs}
+    its = build_catalog(b, profs, zones, spot=bool(rng.random() < 0.5), prices=prices, rng=rng,
+                        unavailable_frac=0.1)
+    fams = sorted({it.name.split("-")[0] for it in its})
+    for j in range(int(rng.integers(1, 3))):
+        reqs = []
+        r = rng.random()
+        if r < 0.35:
+            reqs.append((FAMILY_KEY, "In", fams, int(rng.integers(1, len(fams) + 2))))
+        elif r < 0.6:
+            reqs.append((IT_KEY, "Exists", [], int(rng.choice([1, 2, 3, 5, 8]))))
+        elif r < 0.8:
+            reqs.append((SIZE_KEY, "Exists", [], int(rng.integers(1, 5))))
+            if rng.random() < 0.5:
+                reqs.append((FAMILY_KEY, "Exists", [], int(rng.integers(1, 3))))
+        elif r < 0.85:
+            reqs.append(("topology.kubernetes.io/zone", "In", zones, 1))  # instance types carry no zone value
+        limits = {"cpu": int(rng.choice([16, 64])) * 1000} if rng.random() < 0.25 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
+                       daemon={"cpu": 100, "pods": 1000})
+    for k in range(int(rng.integers(0, 3))):
+        it = its[rng.integers(0, len(its))]
+        labels = {r_[0]: r_[2][0] for r_ in it.requirements}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(zones))
+        labels["kubernetes.io/hostname"] = f"n{k}"
+        b.add_node(f"n{k}", labels, {"cpu": int(rng.choice([1000, 4000])), "memory": 8 * GI * 1000, "pods": 20_000})
+    n = int(n_pods if n_pods is not None else rng.integers(1, 50))
+    for i in range(n):
+        req = {"cpu": int(rng.choice([250, 500, 1000, 2000, 6000, 14000])),
+               "memory": int(rng.choice([1, 2, 4, 16])) * GI * 1000, "pods": 1000}
+        sel, required = {}, []
+        r = rng.random()
+        if r < 0.15:
+            sel[FAMILY_KEY] = str(rng.choice(fams))
+        elif r < 0.25:
+            sel[IT_KEY] = its[rng.integers(0, len(its))].name
+        elif r < 0.35:
+            required.append([(FAMILY_KEY, "In", sorted(set(rng.choice(fams, size=2).tolist())))])
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000, req,
+                  node_selector=sel, required_terms=required)
+    return b.build()
+
+
+def min_values_truncation(n_cheap=70):
+    """a NodePool with minValues 2 on the family whose 60 cheapest options are
+    all one family: the NodeClaim passes CanAdd but Truncate(60) drops it"""
+    b = ProblemBuilder()
+    profs = [(f"cx2-{v}x{2 * v}", v, 2 * v, None) for v in range(2, 2 + n_cheap)]
+    profs += [("mx2-2x16", 2, 16, None), ("mx2-4x32", 4, 32, None)]
+    prices = {p_[0]: round(0.01 * p_[1], 4) for p_ in profs}
+    prices["mx2-2x16"] = 50.0
+    prices["mx2-4x32"] = 60.0
+    build_catalog(b, profs, FAKE_ZONES, spot=False, prices=prices)
+    b.add_nodepool("default", requirements=[(FAMILY_KEY, "In", ["cx2", "mx2"], 2)])
+    for i in range(3):
+        b.add_pod(f"p{i}", 0, {"cpu": 500, "memory": GI * 1000, "pods": 1000})
+    return b.build()

@@ -510,7 +510,31 @@ void update_pod_reqs(Pod& p) {
   p.strict = std::move(strict);
 }
 
-// <U> filterInstanceTypesByRequirements (no short-circuit across ITs)
+// <U> Requirements.HasMinValues
+bool has_min_values(const Reqs& reqs) {
+  for (auto& kv : reqs.m)
+    if (kv.second.min_values) return true;
+  return false;
+}
+
+// <U> InstanceTypes.SatisfiesMinValues: for every requirement with minValues,
+// the union of the instance types' values for its key (it.Requirements.Get(
+// key).Values(): none when the type does not carry the key) is large enough
+bool satisfies_min_values(const vector<const InstanceType*>& its, const Reqs& reqs) {
+  for (auto& kv : reqs.m) {
+    if (!kv.second.min_values) continue;
+    std::set<string> vals;
+    for (auto* it : its) {
+      const Req r = it->reqs.get(kv.first);
+      vals.insert(r.values.begin(), r.values.end());
+    }
+    if ((int64_t)vals.size() < *kv.second.min_values) return false;
+  }
+  return true;
+}
+
+// <U> filterInstanceTypesByRequirements (no short-circuit across ITs); a
+// minValues miss (Strict policy) leaves nothing
 vector<const InstanceType*> filter_its(const vector<const InstanceType*>& its, const Reqs& reqs, const Res& requests) {
   vector<const InstanceType*> out;
   for (auto* it : its) {
@@ -525,6 +549,7 @@ vector<const InstanceType*> filter_its(const vector<const InstanceType*>& its, c
     }
     if (compat && f && has_off) out.push_back(it);
   }
+  if (has_min_values(reqs) && !satisfies_min_values(out, reqs)) out.clear();
   return out;
 }
 
@@ -600,17 +625,21 @@ struct Builder {
     if ((uint64_t)r.begin + r.count > n) throw Unsupported{GS_E_INVALID, string("range out of bounds: ") + what};
   }
   bool allow_placeholder = false;  // launch-time filter: hostname values are plain labels
+  // NodeSelectorRequirementWithMinValues appear in NodePool and NodeClaim
+  // requirements; a pod's NodeSelectorRequirement has no minValues
+  bool allow_min_values = false;
   Req req_of(const gs_requirement& q) {
     if (q.op > GS_OP_LTE) throw Unsupported{GS_E_INVALID, "unknown requirement operator"};
     if (!allow_placeholder && normalize_key(str(q.key)) == kHostname)
       for (uint32_t i = 0; i < q.values.count && q.values.begin + i < p->n_value_ids; i++)
         if (str(p->value_ids[q.values.begin + i]).rfind("hostname-placeholder-", 0) == 0)
           throw Unsupported{GS_E_UNSUPPORTED, "requirement names a hostname placeholder"};
-    if (q.min_values >= 0) throw Unsupported{GS_E_UNSUPPORTED, "minValues"};
+    if (q.min_values >= 0 && !allow_min_values) throw Unsupported{GS_E_UNSUPPORTED, "minValues outside NodePool / NodeClaim requirements"};
     check_range(q.values, p->n_value_ids, "values");
     vector<string> vals;
     for (uint32_t i = 0; i < q.values.count; i++) vals.push_back(str(p->value_ids[q.values.begin + i]));
-    return make_req(str(q.key), (int)q.op, vals, std::nullopt);
+    return make_req(str(q.key), (int)q.op, vals,
+                    q.min_values >= 0 ? optional<int64_t>(q.min_values) : std::nullopt);
   }
   vector<Req> raw_reqs(gs_range r) {
     check_range(r, p->n_reqs, "reqs");
@@ -879,7 +908,9 @@ struct Builder {
       t.np_index = npi;
       t.name = str(np.name);
       t.weight = np.weight;
+      allow_min_values = true;
       Reqs npreqs = reqs_of(np.requirements);
+      allow_min_values = false;
       t.reqs = npreqs;
       auto labels = labels_of(np.labels);
       labels[kNodePool] = t.name;
@@ -1362,10 +1393,17 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   for (auto* nc : s.creation_order) {
     // FinalizeScheduling: drop hostname requirement
     nc->reqs.m.erase(kHostname);
+    // <U> Results.TruncateInstanceTypes: a NodeClaim whose top 60 by price
+    // miss minValues is dropped and its pods become pod errors
+    auto top = order_by_price(nc->options, nc->reqs, 60);
+    if (has_min_values(nc->reqs) && !satisfies_min_values(top, nc->reqs)) {
+      for (auto* p : nc->pods) errors.insert(p->index);
+      continue;
+    }
     r.claim_nodepool.push_back(nc->tmpl->np_index);
     for (auto* p : nc->pods) r.claim_pods.push_back(p->index);
     r.claim_pod_offsets.push_back((uint32_t)r.claim_pods.size());
-    for (auto* it : order_by_price(nc->options, nc->reqs, 60)) r.claim_its.push_back(it->index);
+    for (auto* it : top) r.claim_its.push_back(it->index);
     r.claim_it_offsets.push_back((uint32_t)r.claim_its.size());
     r.req_text.push_back(canonical(nc->reqs));
     for (auto& rn : st.resource_names) r.claim_requests.push_back(res_get(nc->requests, rn));
@@ -1378,7 +1416,7 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   }
   r.error_pods.assign(errors.begin(), errors.end());
   std::memset(out, 0, sizeof(*out));
-  out->n_claims = (uint32_t)s.creation_order.size();
+  out->n_claims = (uint32_t)r.claim_nodepool.size();
   out->claim_nodepool = r.claim_nodepool.data();
   out->claim_pod_offsets = r.claim_pod_offsets.data();
   out->claim_pods = r.claim_pods.data();
@@ -1714,6 +1752,8 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
       if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
     if (in->cluster->n_spreads || in->cluster->n_anti_affinities || in->cluster->n_host_ports)
       return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
+    for (auto& t : base.templates)
+      if (has_min_values(t.reqs)) return GS_E_UNSUPPORTED;  // likewise
     if (in->mode == GS_CONSOLIDATE_EVAL) {
       for (uint32_t s = 0; s < in->n_sets; s++) {
         if ((uint64_t)in->sets[s].begin + in->sets[s].count > in->n_candidates) return GS_E_INVALID;
@@ -1798,6 +1838,7 @@ struct CatalogOracle {
   Builder b;
   explicit CatalogOracle(const gs_problem* p) : b{p, st} {
     b.allow_placeholder = true;
+    b.allow_min_values = true;  // Compatible ignores minValues (cloudprovider.go:321-325)
     for (uint32_t i = 0; i < p->n_strings; i++) st.strings.push_back(p->strings[i] ? p->strings[i] : "");
     st.its.resize(p->n_instance_types);
     for (uint32_t i = 0; i < p->n_instance_types; i++) {
