@@ -68,7 +68,7 @@ enum { GS_TOL_EQUAL = 0, GS_TOL_EXISTS = 1 };
  * those cannot express (a namespaceSelector, a matchLabelKeys list). */
 enum {
   GS_POD_TOPOLOGY_SPREAD = 1u << 0,
-  GS_POD_AFFINITY = 1u << 1,
+  GS_POD_AFFINITY = 1u << 1,   /* forms gs_pod.affinity cannot express */
   GS_POD_ANTI_AFFINITY = 1u << 2,
   GS_POD_HOST_PORTS = 1u << 3,
   GS_POD_VOLUMES = 1u << 4
@@ -165,13 +165,18 @@ typedef struct gs_spread {
   uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is refused */
 } gs_spread;
 
-/* corev1.PodAffinityTerm of spec.affinity.podAntiAffinity: a required term,
- * or a preferred one with its weight (<U> karpenter Topology,
- * TopologyTypePodAntiAffinity: required and not-yet-relaxed preferred terms
- * both constrain the pod; a required term also constrains, through the
- * inverse group, every pod its selector selects).  topologyKey must be
- * kubernetes.io/hostname (other keys GS_E_UNSUPPORTED). */
-typedef struct gs_anti_affinity {
+/* corev1.PodAffinityTerm of spec.affinity.podAffinity or .podAntiAffinity: a
+ * required term, or a preferred one with its weight (<U> karpenter Topology:
+ * required and not-yet-relaxed preferred terms both constrain the pod).
+ *  - anti-affinity (TopologyTypePodAntiAffinity): only domains where no
+ *    selected pod runs; a required term also constrains, through the inverse
+ *    group, every pod its selector selects;
+ *  - affinity (TopologyTypePodAffinity): only domains where a selected pod
+ *    runs, or, while none runs anywhere, the pod's own domain when the pod
+ *    is selected itself (nextDomainAffinity's bootstrap).
+ * topologyKey must be kubernetes.io/hostname (other keys GS_E_UNSUPPORTED:
+ * upstream picks a zone bootstrap domain in map order). */
+typedef struct gs_affinity_term {
   uint32_t topology_key;       /* string id */
   uint32_t required;           /* 1: requiredDuringScheduling..., 0: preferred */
   int32_t weight;              /* preferred terms: the term's weight */
@@ -179,7 +184,7 @@ typedef struct gs_anti_affinity {
   gs_range match_labels;       /* into labels */
   gs_range match_expressions;  /* into reqs: In / NotIn / Exists / DoesNotExist */
   gs_range namespaces;         /* into value_ids (string ids); empty = the pod's namespace */
-} gs_anti_affinity;
+} gs_affinity_term;
 
 /* a containers[].ports[] entry with hostPort != 0 (<U> scheduling
  * HostPortUsage: two entries conflict when protocol and port are equal and
@@ -203,8 +208,9 @@ typedef struct gs_pod {
   uint32_t ns;              /* metadata.namespace (string id) */
   gs_range labels;          /* metadata.labels, into labels (topology selectors) */
   gs_range spreads;         /* spec.topologySpreadConstraints, into spreads */
-  gs_range anti_affinity;   /* spec.affinity.podAntiAffinity terms, into anti_affinities */
+  gs_range anti_affinity;   /* spec.affinity.podAntiAffinity terms, into affinity_terms */
   gs_range host_ports;      /* host ports of all containers, into host_ports */
+  gs_range affinity;        /* spec.affinity.podAffinity terms, into affinity_terms */
 } gs_pod;
 
 /* an existing (state) node: ExistingNode inputs */
@@ -237,7 +243,7 @@ typedef struct gs_problem {
    * reschedulable ones are what consolidation simulations move */
   const gs_pod* bound_pods; uint32_t n_bound_pods;
   const uint32_t* bound_pod_node;             /* [n_bound_pods] index into nodes */
-  const gs_anti_affinity* anti_affinities; uint32_t n_anti_affinities;
+  const gs_affinity_term* affinity_terms; uint32_t n_affinity_terms;
   const gs_host_port* host_ports; uint32_t n_host_ports;
 } gs_problem;
 

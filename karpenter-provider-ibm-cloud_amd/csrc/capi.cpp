@@ -104,6 +104,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.NZV = e.NZV;
   d.tg_zone = e.tg_zone;
   d.tg_host = e.tg_host;
+  d.tg_aff = e.tg_aff;
   c->upload(d.tgroups, e.tgroups);
   c->upload(d.tg_cnt0, e.tg_cnt0);
   c->upload(d.zone_order, e.zone_order);
@@ -313,7 +314,7 @@ uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
                           sizeof(gs_consolidation_result), sizeof(gs_claim_query),
                           sizeof(gs_claim_filter_result), sizeof(gs_vpc_profile), sizeof(gs_price),
                           sizeof(gs_unavailable), sizeof(gs_catalog_env), sizeof(gs_catalog),
-                          sizeof(gs_anti_affinity), sizeof(gs_host_port)};
+                          sizeof(gs_affinity_term), sizeof(gs_host_port)};
   for (uint32_t i = 0; i < n && i < 28; i++) out[i] = s[i];
   return 28;
 }

@@ -733,6 +733,9 @@ struct Ctx {
   //         selects; counts the pods carrying the term),
   //  kind 3 HostPortUsage (owners = pods with port entry e; counts the pods
   //         with an entry that Matches e).
+  // kind 4 (TopologyTypePodAffinity) counts the pods its term selects and
+  // admits an owner where count > 0, or, while the total is 0, anywhere if
+  // the owner is counted itself (tg_aff; the kernel keeps the total).
   struct GroupEnc {
     SpreadEnc sp;
     std::string ns;
@@ -785,13 +788,14 @@ struct Ctx {
     }
     return out;
   }
-  std::vector<AntiEnc> antis_of(const gs_pod& pd) const {
-    chk(pd.anti_affinity, p->n_anti_affinities, "anti_affinities");
+  std::vector<AntiEnc> antis_of(const gs_pod& pd) const { return terms_of(pd, pd.anti_affinity); }
+  std::vector<AntiEnc> terms_of(const gs_pod& pd, gs_range rg) const {
+    chk(rg, p->n_affinity_terms, "affinity_terms");
     std::vector<AntiEnc> out;
-    for (uint32_t k = 0; k < pd.anti_affinity.count; k++) {
-      const gs_anti_affinity& q = p->anti_affinities[pd.anti_affinity.begin + k];
+    for (uint32_t k = 0; k < rg.count; k++) {
+      const gs_affinity_term& q = p->affinity_terms[rg.begin + k];
       if (normalize(S(q.topology_key)) != kHostname)
-        throw Fail{GS_E_UNSUPPORTED, "pod anti-affinity topologyKey other than hostname"};
+        throw Fail{GS_E_UNSUPPORTED, "pod (anti-)affinity topologyKey other than hostname"};
       AntiEnc a;
       a.required = q.required != 0;
       a.weight = q.weight;
@@ -847,7 +851,8 @@ struct Ctx {
   bool group_counts(const GroupEnc& g, const PodSel& ps) const {
     switch (g.kind) {
       case 0: return ps.ns == g.ns && g.sp.matches(ps.labels);
-      case 1: return g.anti.selects(ps.ns, ps.labels);
+      case 1:
+      case 4: return g.anti.selects(ps.ns, ps.labels);
       case 2: return ps.carried.count(g.inv_hash) != 0;
       default:
         for (auto& e : ps.ports)
@@ -910,6 +915,7 @@ struct Ctx {
       if (t.host) {
         t.hslot = e.TGH++;
         e.tg_host |= 1ull << g;
+        if (groups[g].kind == 4) e.tg_aff |= 1ull << g;
       } else {
         t.known0 = known_zone;
         e.tg_zone |= 1ull << g;
@@ -929,6 +935,7 @@ struct Ctx {
         gsd::TGroupRec& t = e.tgroups[g];
         if (t.host) {
           e.hn0[(size_t)t.hslot * e.NN + pos]++;
+          e.tg_cnt0[(size_t)g * gsd::ZVMAX]++;  // hostname groups: the total over domains (affinity bootstrap)
         } else {
           const uint32_t z = e.nodes[pos].zvid;
           if (z == gsd::NONE || z >= (uint32_t)gsd::ZVMAX) continue;
@@ -1264,6 +1271,16 @@ struct Ctx {
         else anti_pref.push_back({a.weight, gid});
       }
       if (anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
+      std::vector<std::pair<int32_t, uint32_t>> aff_pref;  // (weight, group)
+      for (auto& a : terms_of(pd, pd.affinity)) {
+        GroupEnc g = host_group(4, false);
+        g.anti = a;
+        const uint32_t gid = group_id("F|" + a.hash(), std::move(g));
+        if (a.required) own_static |= 1ull << gid;
+        else aff_pref.push_back({a.weight, gid});
+      }
+      if (aff_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
+      std::stable_sort(aff_pref.begin(), aff_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
       // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
       std::stable_sort(anti_pref.begin(), anti_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
       for (auto& kv : inv_terms) {
@@ -1285,7 +1302,7 @@ struct Ctx {
         tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
       }
       e.var_begin.push_back((uint32_t)e.variants.size());
-      size_t ri = 0, pi = 0, ai = 0;
+      size_t ri = 0, pi = 0, ai = 0, fi = 0;
       for (;;) {
         // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
         PodVariant v;
@@ -1300,6 +1317,7 @@ struct Ctx {
         for (uint32_t k : cur) v.own |= 1ull << sgid[k];
         v.own |= own_static;
         for (size_t k = ai; k < anti_pref.size(); k++) v.own |= 1ull << anti_pref[k].second;
+        for (size_t k = fi; k < aff_pref.size(); k++) v.own |= 1ull << aff_pref[k].second;
         e.variants.push_back(std::move(v));
         variant_tols.push_back(tols);
         // <U> Preferences.Relax
@@ -1307,7 +1325,11 @@ struct Ctx {
           ri++;
           continue;
         }
-        // removePreferredPodAntiAffinityTerm (the heaviest)
+        // removePreferredPodAffinityTerm, then ...AntiAffinityTerm (the heaviest)
+        if (fi < aff_pref.size()) {
+          fi++;
+          continue;
+        }
         if (ai < anti_pref.size()) {
           ai++;
           continue;

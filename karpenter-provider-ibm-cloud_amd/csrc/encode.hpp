@@ -128,7 +128,7 @@ struct Encoded {
   std::vector<gsd::FK> n_fk;
   // topology spread (layout.hpp DevProblem topology fields)
   uint32_t TG = 0, TGH = 0, NZV = 0;
-  uint64_t tg_zone = 0, tg_host = 0;
+  uint64_t tg_zone = 0, tg_host = 0, tg_aff = 0;  // tg_aff: hostname pod-affinity groups
   std::vector<gsd::TGroupRec> tgroups;
   std::vector<int32_t> tg_cnt0;      // [TG][64]
   std::vector<uint32_t> zone_order;  // zone vocabulary ids by name

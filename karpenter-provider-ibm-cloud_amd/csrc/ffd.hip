@@ -925,8 +925,8 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               // hostname groups: min count 0
               for (uint64_t m = own & d.tg_host; m && feas; m &= m - 1) {
                 const uint32_t g = __ffsll((long long)m) - 1;
-                feas = (int64_t)d.hn[(size_t)d.tgroups[g].hslot * d.NN + n] + (int64_t)((tself >> g) & 1) <=
-                       d.tgroups[g].skew;
+                const int64_t c = d.hn[(size_t)d.tgroups[g].hslot * d.NN + n], self = (int64_t)((tself >> g) & 1);
+                feas = ((d.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= d.tgroups[g].skew;
               }
             }
           }
@@ -984,6 +984,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               const uint32_t g = __ffsll((long long)m) - 1;
               if ((d.tg_host >> g) & 1) {
                 d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
+                s_zcnt[g * ZVMAX]++;  // hostname groups: the total
               } else {
                 const uint32_t z = d.nodes0[fn].zvid;
                 if (z < (uint32_t)ZVMAX) {
@@ -1248,8 +1249,10 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               }
               for (uint64_t m = own & dd.tg_host; m && pre; m &= m - 1) {
                 const uint32_t g = __ffsll((long long)m) - 1;
-                pre = (int64_t)dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j] + (int64_t)((tself >> g) & 1) <=
-                      dd.tgroups[g].skew;
+                const int64_t c = dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j],
+                              self = (int64_t)((tself >> g) & 1);
+                pre = ((dd.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self))
+                                             : c + self <= dd.tgroups[g].skew;
               }
               if (pre && tz != NONE) {
                 const uint32_t zc = dd.zone_cat[tz];
@@ -1485,6 +1488,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                 const uint32_t g = __ffsll((long long)m) - 1;
                 if ((dd.tg_host >> g) & 1) {
                   dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j]++;
+                  s_zcnt[g * ZVMAX]++;
                 } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
                   const uint32_t z = __ffsll((long long)zf) - 1;
                   s_zcnt[g * ZVMAX + z]++;
@@ -1562,6 +1566,12 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
           if (ok && ttz != NONE) {
             tzc = d.zone_cat[ttz];
             ok = tzc < 64;
+          }
+          // pod affinity on the fresh hostname domain (count 0): only the
+          // bootstrap of a self-selecting pod while no selected pod runs
+          for (uint64_t m = own & d.tg_aff; m && ok; m &= m - 1) {
+            const uint32_t g = __ffsll((long long)m) - 1;
+            ok = s_zcnt[g * ZVMAX] == 0 && ((tself >> g) & 1);
           }
           if (!ok) continue;
         }
@@ -1659,6 +1669,7 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
               const uint32_t g = __ffsll((long long)m) - 1;
               if ((d.tg_host >> g) & 1) {
                 d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + cbase + j]++;
+                s_zcnt[g * ZVMAX]++;
               } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
                 const uint32_t z = __ffsll((long long)cr->zfull) - 1;
                 s_zcnt[g * ZVMAX + z]++;

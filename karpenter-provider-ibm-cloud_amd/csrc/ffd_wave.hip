@@ -743,8 +743,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             }
             for (uint64_t m = own & KD.tg_host; m && feas; m &= m - 1) {
               const uint32_t g = ffs64(m);
-              feas = (int64_t)KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + n] + (int64_t)((tself >> g) & 1) <=
-                     KD.tgroups[g].skew;
+              const int64_t c = KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + n], self = (int64_t)((tself >> g) & 1);
+              feas = ((KD.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= KD.tgroups[g].skew;
             }
           }
         }
@@ -774,6 +774,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const uint32_t g = ffs64(m);
             if ((KD.tg_host >> g) & 1) {
               KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + fn]++;
+              s_zcnt[g * ZVMAX]++;  // hostname groups: the total
             } else {
               const uint32_t z = KD.nodes0[fn].zvid;
               if (z < (uint32_t)ZVMAX) {
@@ -993,8 +994,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
           for (uint64_t m = own & KD.tg_host; m && pre; m &= m - 1) {
             const uint32_t g = ffs64(m);
-            pre = (int64_t)KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j] + (int64_t)((tself >> g) & 1) <=
-                  KD.tgroups[g].skew;
+            const int64_t c = KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j], self = (int64_t)((tself >> g) & 1);
+            pre = ((KD.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= KD.tgroups[g].skew;
           }
           if (pre && tz != NONE) {
             const uint32_t zc = KD.zone_cat[tz];
@@ -1154,6 +1155,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               const uint32_t g = ffs64(m);
               if ((KD.tg_host >> g) & 1) {
                 KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
+                s_zcnt[g * ZVMAX]++;
               } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
                 const uint32_t z = ffs64(zf);
                 s_zcnt[g * ZVMAX + z]++;
@@ -1282,6 +1284,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           tzc = KD.zone_cat[ttz];
           ok = tzc < 64;
         }
+        // pod affinity on the fresh hostname domain (count 0): only the
+        // bootstrap of a self-selecting pod while no selected pod runs
+        for (uint64_t m = own & KD.tg_aff; m && ok; m &= m - 1) {
+          const uint32_t g = ffs64(m);
+          ok = s_zcnt[g * ZVMAX] == 0 && ((tself >> g) & 1);
+        }
         ttz = __builtin_amdgcn_readfirstlane(ttz);
         tzc = __builtin_amdgcn_readfirstlane(tzc);
         if (!__builtin_amdgcn_readfirstlane(ok ? 1u : 0u)) continue;
@@ -1407,6 +1415,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const uint32_t g = ffs64(m);
             if ((KD.tg_host >> g) & 1) {
               KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
+              s_zcnt[g * ZVMAX]++;
             } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
               const uint32_t z = ffs64(cr->zfull);
               s_zcnt[g * ZVMAX + z]++;

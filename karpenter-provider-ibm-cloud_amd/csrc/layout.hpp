@@ -252,6 +252,7 @@ struct DevProblem {
   uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size
   uint32_t pad_tg;
   uint64_t tg_zone, tg_host;   // group masks by key
+  uint64_t tg_aff;             // hostname groups with the pod-affinity rule (count > 0, or total 0 and self)
   const TGroupRec* tgroups;    // [TG]
   const int32_t* tg_cnt0;      // [TG][64] zone counts before the Solve
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)

@@ -41,8 +41,8 @@ DT_NODEPOOL = np.dtype([("name", "<u4"), ("weight", "<i4"), ("requirements", RAN
 DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), ("node_selector", RANGE),
                    ("required_terms", RANGE), ("preferred_terms", RANGE), ("tolerations", RANGE),
                    ("flags", "<u4"), ("ns", "<u4"), ("labels", RANGE), ("spreads", RANGE),
-                   ("anti_affinity", RANGE), ("host_ports", RANGE)], align=True)
-DT_ANTI = np.dtype([("topology_key", "<u4"), ("required", "<u4"), ("weight", "<i4"), ("has_selector", "<u4"),
+                   ("anti_affinity", RANGE), ("host_ports", RANGE), ("affinity", RANGE)], align=True)
+DT_AFFINITY = np.dtype([("topology_key", "<u4"), ("required", "<u4"), ("weight", "<i4"), ("has_selector", "<u4"),
                     ("match_labels", RANGE), ("match_expressions", RANGE), ("namespaces", RANGE)], align=True)
 DT_HOSTPORT = np.dtype([("protocol", "<u4"), ("ip", "<u4"), ("port", "<i4")], align=True)
 SPREAD_DO_NOT_SCHEDULE, SPREAD_SCHEDULE_ANYWAY = 0, 1
@@ -77,7 +77,7 @@ class GsProblem(C.Structure):
         ("spreads", _P), ("n_spreads", _U32),
         ("bound_pods", _P), ("n_bound_pods", _U32),
         ("bound_pod_node", _P),
-        ("anti_affinities", _P), ("n_anti_affinities", _U32),
+        ("affinity_terms", _P), ("n_affinity_terms", _U32),
         ("host_ports", _P), ("n_host_ports", _U32),
     ]
 

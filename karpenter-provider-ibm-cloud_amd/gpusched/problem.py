@@ -36,7 +36,7 @@ class ProblemBuilder:
         self.bound_pods = []  # pods bound to state nodes (topology counts; consolidation moves them)
         self.bound_node = []
         self.spreads = []
-        self.anti_affinities = []
+        self.affinity_terms = []
         self.host_ports = []
         self.claim_queries = []  # gs_claim_query (launch-time re-filter)
 
@@ -138,7 +138,7 @@ class ProblemBuilder:
         """terms: dicts with key (default kubernetes.io/hostname), required
         (bool), weight, selector (None = nil, else {"labels": {...},
         "exprs": [(key, op, values)]}), namespaces (list; empty = the pod's)"""
-        b = len(self.anti_affinities)
+        b = len(self.affinity_terms)
         for t in terms:
             sel = t.get("selector")
             ml = self._labels((sel or {}).get("labels", {}))
@@ -146,9 +146,9 @@ class ProblemBuilder:
             nss = list(t.get("namespaces", []))
             vb = len(self.value_ids)
             self.value_ids.extend(self.s(x) for x in nss)
-            self.anti_affinities.append((self.s(t.get("key", "kubernetes.io/hostname")), 1 if t.get("required") else 0,
+            self.affinity_terms.append((self.s(t.get("key", "kubernetes.io/hostname")), 1 if t.get("required") else 0,
                                          int(t.get("weight", 1)), 0 if sel is None else 1, ml, me, (vb, len(nss))))
-        return (b, len(self.anti_affinities) - b)
+        return (b, len(self.affinity_terms) - b)
 
     def _ports(self, ports):
         """ports: (port, protocol, ip) tuples (protocol "" = TCP, ip "" = unspecified)"""
@@ -159,27 +159,29 @@ class ProblemBuilder:
         return (b, len(self.host_ports) - b)
 
     def _pod(self, uid, creation_ns, requests, node_selector, required_terms, preferred_terms, tolerations, flags,
-             namespace, labels, spreads, anti_affinity=(), host_ports=()):
+             namespace, labels, spreads, anti_affinity=(), host_ports=(), affinity=()):
         return (self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
                 self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
                 self._tols(tolerations), int(flags), self.s(namespace), self._labels(labels or {}),
-                self._spreads(spreads), self._anti(anti_affinity), self._ports(host_ports))
+                self._spreads(spreads), self._anti(anti_affinity), self._ports(host_ports), self._anti(affinity))
 
     def add_pod(self, uid, creation_ns, requests, node_selector=None, required_terms=(), preferred_terms=(),
                 tolerations=(), flags=0, namespace="default", labels=None, spreads=(), anti_affinity=(),
-                host_ports=()):
-        """required_terms: list of reqs lists; preferred_terms: list of (weight, reqs)"""
+                host_ports=(), affinity=()):
+        """required_terms: list of reqs lists; preferred_terms: list of (weight, reqs);
+        anti_affinity / affinity: pod (anti-)affinity term dicts (see _anti)"""
         self.pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
-                                   tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports))
+                                   tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports, affinity))
         return len(self.pods) - 1
 
     def add_bound_pod(self, node, uid, creation_ns, requests, node_selector=None, required_terms=(),
                       preferred_terms=(), tolerations=(), flags=0, namespace="default", labels=None, spreads=(),
-                      anti_affinity=(), host_ports=()):
+                      anti_affinity=(), host_ports=(), affinity=()):
         """a pod bound to state node `node` (counted by topology selectors;
         consolidation reschedules the candidates' pods)"""
         self.bound_pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
-                                         tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports))
+                                         tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports,
+                                         affinity))
         self.bound_node.append(int(node))
         return len(self.bound_pods) - 1
 
@@ -229,7 +231,7 @@ class Problem:
         self.bound_pods = _np(b.bound_pods, abi.DT_POD)
         self.bound_node = np.asarray(b.bound_node, dtype=np.uint32)
         self.spreads = _np(b.spreads, abi.DT_SPREAD)
-        self.anti_affinities = _np(b.anti_affinities, abi.DT_ANTI)
+        self.affinity_terms = _np(b.affinity_terms, abi.DT_AFFINITY)
         self.host_ports = _np(b.host_ports, abi.DT_HOSTPORT)
         self.claim_queries = (abi.GsClaimQuery * max(1, len(b.claim_queries)))()
         self.n_claim_queries = len(b.claim_queries)
@@ -242,7 +244,7 @@ class Problem:
         st.n_strings = len(self._bytes)
         for name in ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                      "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods",
-                     "anti_affinities", "host_ports"):
+                     "affinity_terms", "host_ports"):
             arr = getattr(self, name)
             setattr(st, name, arr.ctypes.data if len(arr) else None)
             setattr(st, "n_" + name, len(arr))
@@ -250,7 +252,7 @@ class Problem:
 
     _DUMP_ARRAYS = ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                     "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods", "bound_node",
-                    "anti_affinities", "host_ports")
+                    "affinity_terms", "host_ports")
 
     def dump(self, path):
         """binary dump read by tools/encode_harness.cpp (host-only encoder

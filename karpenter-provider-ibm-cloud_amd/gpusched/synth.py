@@ -618,8 +618,9 @@ def random_affinity(seed, n_pods=None):
     required and preferred hostname anti-affinity (self- and other-selecting,
     namespace lists, nil selectors), inverse groups from pending and bound
     carriers, host ports over protocols and specific / unspecified host IPs,
-    mixed with topology spread, existing nodes, NodePool limits (relaxation)
-    and taints"""
+    hostname pod affinity (required and preferred, bootstrap by self-selecting
+    pods), mixed with topology spread, existing nodes, NodePool limits
+    (relaxation) and taints"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
@@ -647,6 +648,13 @@ def random_affinity(seed, n_pods=None):
         if rng.random() < 0.15:
             t["namespaces"] = sorted(set(rng.choice(["default", "other", "kube"], size=2).tolist()))
         anti_pal.append(t)
+    aff_pal = []
+    for _ in range(int(rng.integers(0, 3))):
+        t = {"required": bool(rng.random() < 0.4), "weight": int(rng.choice([1, 20, 80])),
+             "selector": _selector(rng, str(rng.choice(APPS[:3])))}
+        if rng.random() < 0.15:
+            t["namespaces"] = ["default", "other"]
+        aff_pal.append(t)
     port_pal = [(int(rng.choice([80, 443, 8080])), str(rng.choice(["TCP", "TCP", "", "UDP"])),
                  str(rng.choice(["", "", "10.0.0.1", "10.0.0.2", "0.0.0.0"]))) for _ in range(int(rng.integers(1, 6)))]
     spread_pal = []
@@ -687,7 +695,8 @@ def random_affinity(seed, n_pods=None):
                   namespace=str(rng.choice(["default", "default", "other"])),
                   anti_affinity=pick(anti_pal, 2) if rng.random() < 0.6 else [],
                   host_ports=pick(port_pal, 2) if rng.random() < 0.3 else [],
-                  spreads=pick(spread_pal, 1) if rng.random() < 0.3 else [])
+                  spreads=pick(spread_pal, 1) if rng.random() < 0.3 else [],
+                  affinity=pick(aff_pal, 1) if rng.random() < 0.3 else [])
     return b.build()
 
 

@@ -397,15 +397,16 @@ struct Spread {
   }
 };
 
-// corev1.PodAffinityTerm of podAntiAffinity (hostname key)
-struct Anti {
+// corev1.PodAffinityTerm of podAffinity / podAntiAffinity (hostname key)
+struct AffTerm {
+  bool affinity = false;     // podAffinity (else podAntiAffinity)
   string key;
   bool required = false;
   int32_t weight = 0;
   Spread sel;                // has_selector / match_labels / exprs only
   std::set<string> nss;      // buildNamespaceList: the term's list, else the pod's namespace
   string hash() const {      // TopologyGroup.Hash: type, key, namespaces, selector
-    string h = "anti|" + key + "|" + (sel.has_selector ? "1" : "0");
+    string h = string(affinity ? "aff|" : "anti|") + key + "|" + (sel.has_selector ? "1" : "0");
     for (auto& n : nss) h += "|n:" + n;
     for (auto& kv : sel.match_labels) h += "|l:" + kv.first + "=" + kv.second;
     for (auto& e : sel.exprs) {
@@ -450,8 +451,10 @@ struct Pod {
   string ns;
   std::map<string, string> labels;
   vector<Spread> spreads;  // mutable (relaxation)
-  vector<Anti> anti_required;
-  vector<Anti> anti_preferred;  // mutable (relaxation)
+  vector<AffTerm> anti_required;
+  vector<AffTerm> anti_preferred;  // mutable (relaxation)
+  vector<AffTerm> aff_required;
+  vector<AffTerm> aff_preferred;   // mutable (relaxation)
   vector<HostPort> ports;
 };
 
@@ -581,9 +584,10 @@ vector<const InstanceType*> order_by_price(vector<const InstanceType*> its, cons
 }
 
 // <U> scheduling.TopologyGroup with an empty node filter:
-// TopologyTypeSpread or TopologyTypePodAntiAffinity
+// TopologyTypeSpread, TopologyTypePodAntiAffinity or TopologyTypePodAffinity
 struct TGroup {
   bool anti = false;
+  bool aff = false;
   string key;
   int32_t max_skew;
   optional<int32_t> min_domains;
@@ -593,7 +597,7 @@ struct TGroup {
   std::map<string, int64_t> domains;  // known domains and their counts
   std::set<uint32_t> owners;          // pod indices
   bool selects(const Pod& p) const {
-    return (anti ? nss.count(p.ns) > 0 : p.ns == ns) && sel.matches(p.labels);
+    return (anti || aff ? nss.count(p.ns) > 0 : p.ns == ns) && sel.matches(p.labels);
   }
 };
 
@@ -709,30 +713,38 @@ struct Builder {
       sp.ignore_affinity = q.node_affinity_policy == GS_POLICY_IGNORE;
       pd.spreads.push_back(std::move(sp));
     }
-    check_range(g.anti_affinity, p->n_anti_affinities, "anti_affinities");
-    for (uint32_t k = 0; k < g.anti_affinity.count; k++) {
-      const gs_anti_affinity& q = p->anti_affinities[g.anti_affinity.begin + k];
-      Anti a;
-      a.key = normalize_key(str(q.topology_key));
-      if (a.key != kHostname) throw Unsupported{GS_E_UNSUPPORTED, "pod anti-affinity topologyKey other than hostname"};
-      a.required = q.required != 0;
-      a.weight = q.weight;
-      a.sel.has_selector = q.has_selector != 0;
-      a.sel.match_labels = labels_of(q.match_labels);
-      check_range(q.match_expressions, p->n_reqs, "reqs");
-      for (uint32_t e = 0; e < q.match_expressions.count; e++) {
-        const gs_requirement& r = p->reqs[q.match_expressions.begin + e];
-        if (r.op > GS_OP_DOES_NOT_EXIST) throw Unsupported{GS_E_INVALID, "label selector operator"};
-        check_range(r.values, p->n_value_ids, "values");
-        Spread::Expr x{str(r.key), (int)r.op, {}};
-        for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
-        a.sel.exprs.push_back(std::move(x));
+    auto terms = [&](gs_range rg, bool affinity) {
+      check_range(rg, p->n_affinity_terms, "affinity_terms");
+      for (uint32_t k = 0; k < rg.count; k++) {
+        const gs_affinity_term& q = p->affinity_terms[rg.begin + k];
+        AffTerm a;
+        a.affinity = affinity;
+        a.key = normalize_key(str(q.topology_key));
+        if (a.key != kHostname)
+          throw Unsupported{GS_E_UNSUPPORTED, "pod (anti-)affinity topologyKey other than hostname"};
+        a.required = q.required != 0;
+        a.weight = q.weight;
+        a.sel.has_selector = q.has_selector != 0;
+        a.sel.match_labels = labels_of(q.match_labels);
+        check_range(q.match_expressions, p->n_reqs, "reqs");
+        for (uint32_t e = 0; e < q.match_expressions.count; e++) {
+          const gs_requirement& r = p->reqs[q.match_expressions.begin + e];
+          if (r.op > GS_OP_DOES_NOT_EXIST) throw Unsupported{GS_E_INVALID, "label selector operator"};
+          check_range(r.values, p->n_value_ids, "values");
+          Spread::Expr x{str(r.key), (int)r.op, {}};
+          for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
+          a.sel.exprs.push_back(std::move(x));
+        }
+        check_range(q.namespaces, p->n_value_ids, "values");
+        for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(str(p->value_ids[q.namespaces.begin + v]));
+        if (a.nss.empty()) a.nss.insert(pd.ns);
+        if (affinity) (a.required ? pd.aff_required : pd.aff_preferred).push_back(std::move(a));
+        else (a.required ? pd.anti_required : pd.anti_preferred).push_back(std::move(a));
       }
-      check_range(q.namespaces, p->n_value_ids, "values");
-      for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(str(p->value_ids[q.namespaces.begin + v]));
-      if (a.nss.empty()) a.nss.insert(pd.ns);
-      (a.required ? pd.anti_required : pd.anti_preferred).push_back(std::move(a));
-    }
+    };
+    terms(g.anti_affinity, false);
+    if (pending) terms(g.affinity, true);  // pod affinity has no inverse: bound pods' terms do nothing
+    if (pd.aff_preferred.size() > 12) throw Unsupported{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
     if (pd.anti_preferred.size() > 12) throw Unsupported{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
     check_range(g.host_ports, p->n_host_ports, "host_ports");
     for (uint32_t k = 0; k < g.host_ports.count; k++) {
@@ -761,9 +773,10 @@ struct Builder {
     }
   }
 
-  TGroup anti_group(const Anti& a) {
+  TGroup anti_group(const AffTerm& a) {
     TGroup g;
-    g.anti = true;
+    g.anti = !a.affinity;
+    g.aff = a.affinity;
     g.key = a.key;
     g.max_skew = INT32_MAX;
     g.nss = a.nss;
@@ -798,7 +811,7 @@ struct Builder {
       }
     // <U> newForTopologies: required and preferred anti-affinity terms
     for (auto& pd : st.pods)
-      for (auto* terms : {&pd.anti_required, &pd.anti_preferred})
+      for (auto* terms : {&pd.anti_required, &pd.anti_preferred, &pd.aff_required, &pd.aff_preferred})
         for (auto& a : *terms) {
           const string h = a.hash();
           auto f = st.group_index.find(h);
@@ -810,7 +823,7 @@ struct Builder {
         }
     // <U> updateInverseAntiAffinity: one inverse group per required term,
     // owned by the pods that carry it (pending pods here, bound pods below)
-    auto inverse_of = [&](const Anti& a) -> TGroup& {
+    auto inverse_of = [&](const AffTerm& a) -> TGroup& {
       const string h = a.hash();
       auto f = st.inverse_index.find(h);
       if (f == st.inverse_index.end()) {
@@ -1010,12 +1023,21 @@ bool relax(Pod& p, bool tolerate_pns) {
     p.required.erase(p.required.begin());
     return true;
   }
-  // removePreferredPodAffinityTerm: pods with pod affinity are refused up
-  // front (GS_POD_AFFINITY), nothing to relax here
+  // removePreferredPodAffinityTerm: sort.Slice by weight desc, drop [0]
+  if (!p.aff_preferred.empty()) {
+    struct D {
+      vector<AffTerm>& t;
+      bool less(int i, int j) { return t[i].weight > t[j].weight; }
+      void swap(int i, int j) { std::swap(t[i], t[j]); }
+    } d{p.aff_preferred};
+    gosort::slice(d, (int)p.aff_preferred.size());
+    p.aff_preferred.erase(p.aff_preferred.begin());
+    return true;
+  }
   // removePreferredPodAntiAffinityTerm: sort.Slice by weight desc, drop [0]
   if (!p.anti_preferred.empty()) {
     struct D {
-      vector<Anti>& t;
+      vector<AffTerm>& t;
       bool less(int i, int j) { return t[i].weight > t[j].weight; }
       void swap(int i, int j) { std::swap(t[i], t[j]); }
     } d{p.anti_preferred};
@@ -1067,6 +1089,30 @@ struct Scheduler {
   // the node's domains within maxSkew.  Upstream iterates a Go map / an
   // unsorted set, so ties fall in random order; restated: smallest name.
   Req next_domain(const TGroup& g, const Pod& pod, const Req& pod_domains, const Req& node_domains) const {
+    if (g.aff) {
+      // nextDomainAffinity: the domains the pod allows that hold a selected
+      // pod; while none does, a self-selecting pod bootstraps on one domain
+      // both sides allow (upstream takes the first in map order: for the
+      // hostname key the node side allows exactly one, its own)
+      vector<string> opts;
+      for (auto& kv : g.domains)
+        if (kv.second > 0 && pod_domains.has(kv.first)) opts.push_back(kv.first);
+      if (opts.empty() && g.selects(pod)) {
+        for (auto& kv : g.domains)
+          if (pod_domains.has(kv.first) && node_domains.has(kv.first)) {
+            opts.push_back(kv.first);
+            break;
+          }
+        if (opts.empty())
+          for (auto& kv : g.domains)
+            if (pod_domains.has(kv.first)) {
+              opts.push_back(kv.first);
+              break;
+            }
+      }
+      if (opts.empty()) return make_req(g.key, GS_OP_DOES_NOT_EXIST, {}, std::nullopt);
+      return make_req(g.key, GS_OP_IN, opts, std::nullopt);
+    }
     if (g.anti) {
       // nextDomainAntiAffinity: the empty domains both sides allow
       vector<string> opts;
@@ -1152,7 +1198,7 @@ struct Scheduler {
       auto f = st.group_index.find(sp.hash(pod.ns));
       if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
     }
-    for (auto* terms : {&pod.anti_required, &pod.anti_preferred})
+    for (auto* terms : {&pod.anti_required, &pod.anti_preferred, &pod.aff_required, &pod.aff_preferred})
       for (auto& a : *terms) {
         auto f = st.group_index.find(a.hash());
         if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
@@ -1750,7 +1796,7 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
       if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
     for (uint32_t i = 0; i < in->cluster->n_bound_pods; i++)
       if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
-    if (in->cluster->n_spreads || in->cluster->n_anti_affinities || in->cluster->n_host_ports)
+    if (in->cluster->n_spreads || in->cluster->n_affinity_terms || in->cluster->n_host_ports)
       return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
     for (auto& t : base.templates)
       if (has_min_values(t.reqs)) return GS_E_UNSUPPORTED;  // likewise

@@ -94,5 +94,5 @@ def test_struct_layouts_match_library():
             C.sizeof(abi.GsConsolidation), C.sizeof(abi.GsCommand), C.sizeof(abi.GsConsolidationResult),
             C.sizeof(abi.GsClaimQuery), C.sizeof(abi.GsClaimFilterResult), C.sizeof(abi.GsVpcProfile),
             C.sizeof(abi.GsPrice), C.sizeof(abi.GsUnavailable), C.sizeof(abi.GsCatalogEnv), C.sizeof(abi.GsCatalog),
-            abi.DT_ANTI.itemsize, abi.DT_HOSTPORT.itemsize]
+            abi.DT_AFFINITY.itemsize, abi.DT_HOSTPORT.itemsize]
     assert list(out) == mine

@@ -1,5 +1,6 @@
-"""Pod anti-affinity and host ports (<U> karpenter
-Topology TopologyTypePodAntiAffinity + inverse groups, HostPortUsage).
+"""Pod (anti-)affinity and host ports (<U> karpenter
+Topology TopologyTypePodAntiAffinity + inverse groups, TopologyTypePodAffinity
+with nextDomainAffinity's bootstrap, HostPortUsage).
 
 The reference's own e2e workload sets a preferred hostname anti-affinity on
 its deployments (reference test/e2e/config.go:473-490); `e2e_deployments`
@@ -189,6 +190,57 @@ def test_host_ports_of_bound_pods():
     assert res["nodes"][0] == [] and res["nodes"][1] == [0] and _pods(res) == [[1]]
 
 
+def _big(n, aff):
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("default", requirements=[(Z, "In", synth.FAKE_ZONES)])
+    for i in range(n):
+        # 3 vCPU: two per NodeClaim on the largest (8-vCPU) type
+        b.add_pod(f"p{i}", 0, {"cpu": 3000, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  affinity=aff)
+    return b
+
+
+def test_self_affinity_bootstraps_then_follows():
+    # p0 bootstraps a NodeClaim, p1 joins it; p2 needs a domain with a web
+    # pod and none has room: required fails, preferred relaxes
+    res = _solve(_big(4, [{"required": True, "selector": WEB}]))
+    assert _pods(res) == [[0, 1]] and res["errors"] == [2, 3]
+    res = _solve(_big(4, [{"required": False, "weight": 5, "selector": WEB}]))
+    assert _pods(res) == [[0, 1], [2, 3]] and not res["errors"]
+    assert _pods(_solve(_big(4, []))) == [[0, 1], [2, 3]]
+
+
+def test_affinity_to_pods_that_do_not_run_fails():
+    res = _solve(_base(n_pods=2, labels={"app": "web"}))
+    b = _base(n_pods=0)
+    for i in range(2):
+        b.add_pod(f"w{i}", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  affinity=[{"required": True, "selector": {"labels": {"app": "db"}}}])
+    res = _solve(b)
+    assert res["errors"] == [0, 1] and not res["claims"]
+
+
+def test_affinity_follows_bound_and_pending_pods():
+    # a bound db pod on n1: web pods with affinity to db go to n1
+    b = _base(n_pods=0)
+    _nodes(b)
+    b.add_bound_pod(1, "db0", 0, {"cpu": 100}, labels={"app": "db"})
+    for i in range(2):
+        b.add_pod(f"w{i}", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  affinity=[{"required": True, "selector": {"labels": {"app": "db"}}}])
+    res = _solve(b)
+    assert res["nodes"][0] == [] and res["nodes"][1] == [0, 1]
+    # a pending db pod (scheduled first: larger) opens a NodeClaim, the web pods follow it
+    b = _base(n_pods=0)
+    b.add_pod("db", 0, {"cpu": 2000, "memory": 1 << 30, "pods": 1000}, labels={"app": "db"})
+    for i in range(2):
+        b.add_pod(f"w{i}", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  affinity=[{"required": True, "selector": {"labels": {"app": "db"}}}])
+    assert _pods(_solve(b)) == [[0, 1, 2]]
+
+
 def test_refusals():
     b = _base(n_pods=1, anti=[{"key": Z, "required": True, "selector": WEB}])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
@@ -198,6 +250,10 @@ def test_refusals():
     assert lib.validate(b.build())[0] == abi.GS_E_INVALID
     b = _base(n_pods=1, ports=[(70000, "TCP", "")])
     assert lib.validate(b.build())[0] == abi.GS_E_INVALID
+    b = _base(n_pods=0)
+    b.add_pod("x", 0, {"cpu": 1}, affinity=[{"key": Z, "required": True, "selector": WEB}])
+    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
     b = _base(n_pods=1)
     b.add_pod("x", 0, {"cpu": 1}, flags=abi.POD_ANTI_AFFINITY)
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
@@ -251,6 +307,8 @@ _KATS = [
     lambda: _one_type_limit(False),
     lambda: _one_type_limit(True),
     lambda: _base(n_pods=3, ports=[(8080, "TCP", "")]),
+    lambda: _big(4, [{"required": True, "selector": WEB}]),
+    lambda: _big(4, [{"required": False, "weight": 5, "selector": WEB}]),
 ]
 
 

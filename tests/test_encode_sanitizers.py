@@ -72,7 +72,7 @@ def _corrupt(kind):
     elif kind == "nodepool_it_refs":
         p.nodepools["instance_types"]["count"][0] = len(p.it_refs) + 1
     elif kind == "anti_affinity_range":
-        p.pods["anti_affinity"]["begin"][0] = len(p.anti_affinities) + 2
+        p.pods["anti_affinity"]["begin"][0] = len(p.affinity_terms) + 2
         p.pods["anti_affinity"]["count"][0] = 1
     elif kind == "host_port_range":
         p.pods["host_ports"]["count"][len(p.pods) - 1] = 1 << 31

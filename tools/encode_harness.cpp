@@ -73,7 +73,7 @@ bool load(const char* path, Dump& d) {
   p.spreads = (const gs_spread*)A(13), p.n_spreads = N(13, sizeof(gs_spread));
   p.bound_pods = (const gs_pod*)A(14), p.n_bound_pods = N(14, sizeof(gs_pod));
   p.bound_pod_node = (const uint32_t*)A(15);
-  p.anti_affinities = (const gs_anti_affinity*)A(16), p.n_anti_affinities = N(16, sizeof(gs_anti_affinity));
+  p.affinity_terms = (const gs_affinity_term*)A(16), p.n_affinity_terms = N(16, sizeof(gs_affinity_term));
   p.host_ports = (const gs_host_port*)A(17), p.n_host_ports = N(17, sizeof(gs_host_port));
   return true;
 }
