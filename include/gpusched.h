@@ -71,7 +71,7 @@ enum {
   GS_POD_AFFINITY = 1u << 1,   /* forms gs_pod.affinity cannot express */
   GS_POD_ANTI_AFFINITY = 1u << 2,
   GS_POD_HOST_PORTS = 1u << 3,
-  GS_POD_VOLUMES = 1u << 4
+  GS_POD_VOLUMES = 1u << 4      /* forms gs_pod.volumes cannot express */
 };
 
 typedef struct gs_range {
@@ -195,6 +195,20 @@ typedef struct gs_host_port {
   int32_t port;       /* 1..65535 */
 } gs_host_port;
 
+/* a pod volume that counts toward a node's CSI attach limit (<U>
+ * scheduling.Volumes from GetVolumes: the CSI driver and the volume's
+ * identity, e.g. the bound PV name; two pods naming the same volume share it) */
+typedef struct gs_volume {
+  uint32_t driver;  /* string id */
+  uint32_t id;      /* string id */
+} gs_volume;
+
+/* CSINode allocatable attach count of one driver on an existing node */
+typedef struct gs_volume_limit {
+  uint32_t driver;  /* string id */
+  int32_t limit;
+} gs_volume_limit;
+
 /* a pod; requests = resources.RequestsForPods(pod) (incl. pods=1) */
 typedef struct gs_pod {
   uint32_t uid;             /* string id */
@@ -211,6 +225,7 @@ typedef struct gs_pod {
   gs_range anti_affinity;   /* spec.affinity.podAntiAffinity terms, into affinity_terms */
   gs_range host_ports;      /* host ports of all containers, into host_ports */
   gs_range affinity;        /* spec.affinity.podAffinity terms, into affinity_terms */
+  gs_range volumes;         /* CSI volumes, into volumes (<U> ExistingNode.CanAdd VolumeUsage) */
 } gs_pod;
 
 /* an existing (state) node: ExistingNode inputs */
@@ -221,6 +236,7 @@ typedef struct gs_node {
   gs_range taints;
   gs_range available;   /* StateNode.Available() */
   gs_range requests;    /* remaining daemonset requests already owed */
+  gs_range volume_limits; /* into volume_limits; a driver without an entry has no limit */
 } gs_node;
 
 typedef struct gs_problem {
@@ -245,6 +261,8 @@ typedef struct gs_problem {
   const uint32_t* bound_pod_node;             /* [n_bound_pods] index into nodes */
   const gs_affinity_term* affinity_terms; uint32_t n_affinity_terms;
   const gs_host_port* host_ports; uint32_t n_host_ports;
+  const gs_volume* volumes; uint32_t n_volumes;
+  const gs_volume_limit* volume_limits; uint32_t n_volume_limits;
 } gs_problem;
 
 /* Results.TruncateInstanceTypes(60) of Scheduler.Solve */

@@ -46,6 +46,10 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.it_dvid, e.it_dvid);
   d.it_key_unique = e.it_key_unique;
   d.any_mv = e.any_mv ? 1u : 0u;
+  d.any_vol = e.any_vol ? 1u : 0u;
+  c->upload(d.n_vol0, e.n_vol);
+  c->alloc(d.n_vol, e.n_vol.size());
+  c->upload(d.pod_vol, e.pod_vol);
   c->upload(d.it_alloc, e.it_alloc);
   c->upload(d.it_cap, e.it_cap);
   c->upload(d.it_pair, e.it_pair);
@@ -305,7 +309,7 @@ extern "C" {
 const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
 
 uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
-  const uint32_t s[28] = {sizeof(gs_range),        sizeof(gs_requirement),         sizeof(gs_quantity),
+  const uint32_t s[30] = {sizeof(gs_range),        sizeof(gs_requirement),         sizeof(gs_quantity),
                           sizeof(gs_label),        sizeof(gs_taint),               sizeof(gs_toleration),
                           sizeof(gs_term),         sizeof(gs_offering),            sizeof(gs_instance_type),
                           sizeof(gs_nodepool),     sizeof(gs_pod),                 sizeof(gs_node),
@@ -314,9 +318,10 @@ uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
                           sizeof(gs_consolidation_result), sizeof(gs_claim_query),
                           sizeof(gs_claim_filter_result), sizeof(gs_vpc_profile), sizeof(gs_price),
                           sizeof(gs_unavailable), sizeof(gs_catalog_env), sizeof(gs_catalog),
-                          sizeof(gs_affinity_term), sizeof(gs_host_port)};
-  for (uint32_t i = 0; i < n && i < 28; i++) out[i] = s[i];
-  return 28;
+                          sizeof(gs_affinity_term), sizeof(gs_host_port), sizeof(gs_volume),
+                          sizeof(gs_volume_limit)};
+  for (uint32_t i = 0; i < n && i < 30; i++) out[i] = s[i];
+  return 30;
 }
 
 gs_status gs_validate(const gs_problem* p, char* err, size_t len) {

@@ -497,7 +497,7 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   c->cons_problem.bound_pods = nullptr;  // every bound pod is in the combined pod list
   c->cons_problem.n_bound_pods = 0;
   c->cons_problem.bound_pod_node = nullptr;
-  if (cl->n_spreads || cl->n_affinity_terms || cl->n_host_ports)
+  if (cl->n_spreads || cl->n_affinity_terms || cl->n_host_ports || cl->n_volumes)
     return fail(c, GS_E_UNSUPPORTED, "topology spread / anti-affinity / host ports in consolidation simulations");
   c->n_nodepools = c->cons_problem.n_nodepools;
   auto t0 = Clock::now();

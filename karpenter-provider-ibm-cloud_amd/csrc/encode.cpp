@@ -878,6 +878,66 @@ struct Ctx {
     return g;
   }
 
+  // <U> VolumeUsage (ExistingNode.CanAdd's ExceedsLimits): per node the
+  // distinct volumes of its bound pods per driver and the CSINode limits; a
+  // node already over a limit takes no pod at all (the union check fails
+  // whatever the pod mounts)
+  void build_volumes() {
+    std::map<std::string, uint32_t> drv;
+    std::map<std::pair<std::string, std::string>, uint32_t> vol;
+    e.pod_vol.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
+    for (uint32_t i = 0; i < e.P; i++) {
+      const gs_pod& pd = p->pods[i];
+      chk(pd.volumes, p->n_volumes, "volumes");
+      for (uint32_t k = 0; k < pd.volumes.count; k++) {
+        const gs_volume& v = p->volumes[pd.volumes.begin + k];
+        const uint32_t d = drv.emplace(S(v.driver), (uint32_t)drv.size()).first->second;
+        const uint32_t b = vol.emplace(std::make_pair(S(v.driver), S(v.id)), (uint32_t)vol.size()).first->second;
+        if (d >= (uint32_t)gsd::VDMAX) throw Fail{GS_E_UNSUPPORTED, "pending pods mount volumes of more than 4 CSI drivers"};
+        if (b >= 64) throw Fail{GS_E_UNSUPPORTED, "pending pods mount more than 64 distinct volumes"};
+        e.pod_vol[(size_t)i * gsd::VDMAX + d] |= 1ull << b;
+      }
+    }
+    std::vector<uint32_t> pos_of(e.NN);
+    for (uint32_t i = 0; i < e.NN; i++) pos_of[e.node_order[i]] = i;
+    std::vector<std::map<std::string, std::set<std::string>>> used(e.NN);
+    if (p->n_bound_pods && !p->bound_pod_node) throw Fail{GS_E_INVALID, "bound pods without their nodes"};
+    for (uint32_t b = 0; b < p->n_bound_pods; b++) {
+      const gs_pod& bp = p->bound_pods[b];
+      if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
+      chk(bp.volumes, p->n_volumes, "volumes");
+      for (uint32_t k = 0; k < bp.volumes.count; k++) {
+        const gs_volume& v = p->volumes[bp.volumes.begin + k];
+        used[pos_of[p->bound_pod_node[b]]][S(v.driver)].insert(S(v.id));
+      }
+    }
+    e.n_vol.assign(std::max<uint32_t>(e.NN, 1), gsd::NodeVol{});
+    for (uint32_t pos = 0; pos < e.NN; pos++) {
+      const gs_node& g = p->nodes[e.node_order[pos]];
+      chk(g.volume_limits, p->n_volume_limits, "volume_limits");
+      std::map<std::string, int64_t> lim;
+      for (uint32_t k = 0; k < g.volume_limits.count; k++)
+        lim[S(p->volume_limits[g.volume_limits.begin + k].driver)] = p->volume_limits[g.volume_limits.begin + k].limit;
+      gsd::NodeVol& nv = e.n_vol[pos];
+      for (int d = 0; d < gsd::VDMAX; d++) nv.lim[d] = INT32_MAX;
+      for (auto& kv : used[pos]) {
+        auto f = lim.find(kv.first);
+        if (f != lim.end() && (int64_t)kv.second.size() > f->second) e.nodes[pos].ok = 0;  // already over
+      }
+      for (auto& dv : drv) {
+        auto f = lim.find(dv.first);
+        if (f != lim.end()) nv.lim[dv.second] = (int32_t)std::max<int64_t>(f->second, -1);
+        auto u = used[pos].find(dv.first);
+        nv.cnt[dv.second] = u == used[pos].end() ? 0 : (int32_t)u->second.size();
+      }
+      for (auto& vv : vol) {
+        auto u = used[pos].find(vv.first.first);
+        if (u != used[pos].end() && u->second.count(vv.first.second)) nv.present |= 1ull << vv.second;
+      }
+    }
+    e.any_vol = !drv.empty() && e.NN > 0;
+  }
+
   // <U> NewTopology: domain universe (In values of NodePool requirements of
   // NodePools that have instance types, existing nodes' labels) and the
   // counts of the selected bound pods; selection masks per pod
@@ -1580,6 +1640,7 @@ Err encode(const gs_problem* p, Encoded& e) {
     c.build_pods();
     c.build_nodes();
     c.build_topology();
+    c.build_volumes();
   } catch (const Fail& f) {
     return Err{f.code, f.msg};
   } catch (const std::out_of_range& ex) {

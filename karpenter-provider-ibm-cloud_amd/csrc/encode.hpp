@@ -105,6 +105,9 @@ struct Encoded {
   uint32_t it_key_unique = 0;       // IT keys with a distinct value per type
   std::vector<uint32_t> it_ndv;     // [K] distinct values per IT key
   bool any_mv = false;              // some template carries minValues
+  bool any_vol = false;             // pending pods mount CSI volumes and nodes exist
+  std::vector<gsd::NodeVol> n_vol;  // [NN] in node order
+  std::vector<uint64_t> pod_vol;    // [P][VDMAX]
   std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
   std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
   std::vector<double> prices;  // distinct offering prices ascending: price rank -> price

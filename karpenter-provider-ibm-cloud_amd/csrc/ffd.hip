@@ -602,6 +602,8 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
   if (!SIM) {
     for (uint32_t i = tid; i < d.NN; i += FB) d.nodes[i] = d.nodes0[i];
     for (uint32_t i = tid; i < d.NN * F; i += FB) d.n_fk[i] = d.n_fk0[i];
+    if (d.any_vol)
+      for (uint32_t i = tid; i < d.NN; i += FB) d.n_vol[i] = d.n_vol0[i];
   }
   if (tid <= R) s_thoff[tid] = d.thr_off[tid];
   for (uint32_t t = tid; t < T; t += FB) {
@@ -878,6 +880,11 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
       if (d.NN) {
         // first-fit: a 64-node window first (the common hit), then full-width
         // chunks; every chunk ends in one block min over node positions
+        // <U> VolumeUsage: the pod's pending-volume bits per CSI driver
+        uint64_t pvol[VDMAX] = {0, 0, 0, 0};
+        if (TOPO && d.any_vol)
+#pragma unroll
+          for (uint32_t q = 0; q < VDMAX; q++) pvol[q] = d.pod_vol[(size_t)gp * VDMAX + q];
         uint32_t fn = INF;
         for (uint32_t base = 0, width = 64; base < d.NN; base += width, width = FB) {
           const uint32_t n = base + tid;
@@ -929,6 +936,13 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                 feas = ((d.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= d.tgroups[g].skew;
               }
             }
+            if (TOPO && feas && d.any_vol) {
+              // ExceedsLimits: distinct volumes per driver after the union
+              const NodeVol& nv = d.n_vol[n];
+#pragma unroll
+              for (uint32_t q = 0; q < VDMAX; q++)
+                if (pvol[q]) feas = feas && nv.cnt[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+            }
           }
           fn = wg.first(feas, base);
           if (tid == 0) S.node_evals += d.NN - base < width ? d.NN - base : width;
@@ -977,6 +991,17 @@ __global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
                                            : e.st;
           }
           if (tid == 0) {
+            if (TOPO && d.any_vol) {
+              // VolumeUsage.Add
+              NodeVol& nv = d.n_vol[fn];
+              uint64_t all = 0;
+#pragma unroll
+              for (uint32_t q = 0; q < VDMAX; q++) {
+                nv.cnt[q] += __popcll(pvol[q] & ~nv.present);
+                all |= pvol[q];
+              }
+              nv.present |= all;
+            }
             logp[HN.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
             S.found = 1;
             // <U> Topology.Record: the node's labels are single domains
@@ -1882,7 +1907,7 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   const bool sim = d->n_sims > 0;
   if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread
   // shape: 0 provisioning, 1 provisioning with topology spread, 2 simulations
-  switch (d->R * 4 + (sim ? 2 : (d->TG || d->any_mv ? 1 : 0))) {
+  switch (d->R * 4 + (sim ? 2 : (d->TG || d->any_mv || d->any_vol ? 1 : 0))) {
 #define GSK_CASE(n)                                                                                          \
   case 4 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
   case 4 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \

@@ -421,6 +421,8 @@ extern "C" __global__ __launch_bounds__(256) void ffd_init_kernel(DevProblem d) 
   for (uint32_t i = i0; i < d.NN; i += stride) d.nodes[i] = d.nodes0[i];
   for (uint32_t i = i0; i < d.NN * d.F; i += stride) d.n_fk[i] = d.n_fk0[i];
   for (uint32_t i = i0; i < d.TGH * d.NN; i += stride) d.hn[i] = d.hn0[i];
+  if (d.any_vol)
+    for (uint32_t i = i0; i < d.NN; i += stride) d.n_vol[i] = d.n_vol0[i];
 }
 
 // Go's choosePivot on n >= 50 elements samples the adjacent triples around
@@ -713,6 +715,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
       const uint32_t fk_begin = VX(1), fk_count = VX(2), zfull_off = VX(12), cfull_off = VX(13);
       const uint64_t vtol = VX64(18);
+      // <U> VolumeUsage: the pod's pending-volume bits per CSI driver
+      uint64_t pvol[VDMAX] = {0, 0, 0, 0};
+      if (TOPO && KD.any_vol)
+#pragma unroll
+        for (uint32_t q = 0; q < VDMAX; q++) pvol[q] = KD.pod_vol[(size_t)gp * VDMAX + q];
       uint32_t fn = INF;
       for (uint32_t base = 0; base < KD.NN; base += 64) {
         const uint32_t n = base + lane;
@@ -747,6 +754,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               feas = ((KD.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= KD.tgroups[g].skew;
             }
           }
+          if (TOPO && feas && KD.any_vol) {
+            // ExceedsLimits: distinct volumes per driver after the union
+            const NodeVol& nv = KD.n_vol[n];
+#pragma unroll
+            for (uint32_t q = 0; q < VDMAX; q++)
+              if (pvol[q]) feas = feas && nv.cnt[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+          }
         }
         const uint64_t b = __ballot(feas);
         CTR(C_NEV, KD.NN - base < 64 ? KD.NN - base : 64);
@@ -769,6 +783,17 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
                                          : e.st;
         }
         if (lane == 0) {
+          if (TOPO && KD.any_vol) {
+            // VolumeUsage.Add
+            NodeVol& nv = KD.n_vol[fn];
+            uint64_t all = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < VDMAX; q++) {
+              nv.cnt[q] += __popcll(pvol[q] & ~nv.present);
+              all |= pvol[q];
+            }
+            nv.present |= all;
+          }
           // <U> Topology.Record: the node's labels are single domains
           for (uint64_t m = TOPO ? vtsel : 0; m; m &= m - 1) {
             const uint32_t g = ffs64(m);
@@ -1554,7 +1579,7 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
-  switch (d->R * 2 + (d->TG || d->any_mv ? 1 : 0)) {
+  switch (d->R * 2 + (d->TG || d->any_mv || d->any_vol ? 1 : 0)) {
 #define GSK_CASE(n)                                                                                      \
   case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(128), lds, s, *d); break;      \
   case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(128), lds, s, *d); break;

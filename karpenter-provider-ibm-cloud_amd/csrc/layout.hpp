@@ -141,6 +141,16 @@ struct NodeRec {
   uint32_t init;         // StateNode.Initialized()
 };
 
+// <U> VolumeUsage of an existing node over the CSI drivers that pending pods
+// use (<= VDMAX): which of the pending pods' volumes (<= 64) it already
+// mounts, its distinct volume count and its limit per driver
+constexpr int VDMAX = 4;
+struct NodeVol {
+  uint64_t present;
+  int32_t cnt[VDMAX];
+  int32_t lim[VDMAX];  // INT32_MAX: no limit
+};
+
 // add-log entry: pod popped & placed, in order
 struct LogRec {
   uint32_t pod, var, target, pad;  // target: claim id, or (node id | 0x80000000)
@@ -228,6 +238,10 @@ struct DevProblem {
   const NodeRec* nodes0;       // [NN] in <U> order: initialized first, then name
   const FK* n_fk0;             // [NN][F] free-key requirement state per node
   NodeRec* nodes;              // working copies (reset at every run)
+  const NodeVol* n_vol0;       // [NN] volume usage before the Solve (any_vol)
+  NodeVol* n_vol;              // [NN] working copies
+  const uint64_t* pod_vol;     // [P][VDMAX] the pod's pending-volume bits per driver
+  uint32_t any_vol;            // pending pods mount CSI volumes: the general (TOPO) variant checks limits
   FK* n_fk;
   // feasibility outputs
   uint64_t* rows;              // [V][T][OW]

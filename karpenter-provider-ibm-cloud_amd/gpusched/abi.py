@@ -41,7 +41,10 @@ DT_NODEPOOL = np.dtype([("name", "<u4"), ("weight", "<i4"), ("requirements", RAN
 DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), ("node_selector", RANGE),
                    ("required_terms", RANGE), ("preferred_terms", RANGE), ("tolerations", RANGE),
                    ("flags", "<u4"), ("ns", "<u4"), ("labels", RANGE), ("spreads", RANGE),
-                   ("anti_affinity", RANGE), ("host_ports", RANGE), ("affinity", RANGE)], align=True)
+                   ("anti_affinity", RANGE), ("host_ports", RANGE), ("affinity", RANGE), ("volumes", RANGE)],
+                  align=True)
+DT_VOLUME = np.dtype([("driver", "<u4"), ("id", "<u4")], align=True)
+DT_VOLUME_LIMIT = np.dtype([("driver", "<u4"), ("limit", "<i4")], align=True)
 DT_AFFINITY = np.dtype([("topology_key", "<u4"), ("required", "<u4"), ("weight", "<i4"), ("has_selector", "<u4"),
                     ("match_labels", RANGE), ("match_expressions", RANGE), ("namespaces", RANGE)], align=True)
 DT_HOSTPORT = np.dtype([("protocol", "<u4"), ("ip", "<u4"), ("port", "<i4")], align=True)
@@ -52,7 +55,7 @@ DT_SPREAD = np.dtype([("topology_key", "<u4"), ("max_skew", "<i4"), ("when_unsat
                       ("match_expressions", RANGE), ("node_affinity_policy", "<u4"),
                       ("node_taints_policy", "<u4")], align=True)
 DT_NODE = np.dtype([("name", "<u4"), ("initialized", "<u4"), ("labels", RANGE), ("taints", RANGE),
-                    ("available", RANGE), ("requests", RANGE)], align=True)
+                    ("available", RANGE), ("requests", RANGE), ("volume_limits", RANGE)], align=True)
 
 _P = C.c_void_p
 _U32 = C.c_uint32
@@ -79,6 +82,8 @@ class GsProblem(C.Structure):
         ("bound_pod_node", _P),
         ("affinity_terms", _P), ("n_affinity_terms", _U32),
         ("host_ports", _P), ("n_host_ports", _U32),
+        ("volumes", _P), ("n_volumes", _U32),
+        ("volume_limits", _P), ("n_volume_limits", _U32),
     ]
 
 

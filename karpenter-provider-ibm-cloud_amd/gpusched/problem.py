@@ -38,6 +38,8 @@ class ProblemBuilder:
         self.spreads = []
         self.affinity_terms = []
         self.host_ports = []
+        self.volumes = []
+        self.volume_limits = []
         self.claim_queries = []  # gs_claim_query (launch-time re-filter)
 
     # ------------------------------------------------------------ primitives
@@ -159,29 +161,34 @@ class ProblemBuilder:
         return (b, len(self.host_ports) - b)
 
     def _pod(self, uid, creation_ns, requests, node_selector, required_terms, preferred_terms, tolerations, flags,
-             namespace, labels, spreads, anti_affinity=(), host_ports=(), affinity=()):
+             namespace, labels, spreads, anti_affinity=(), host_ports=(), affinity=(), volumes=()):
+        vb = len(self.volumes)
+        self.volumes.extend((self.s(drv), self.s(vid)) for drv, vid in volumes)
         return (self.s(uid), int(creation_ns), self._qty(requests), self._labels(node_selector or {}),
                 self._terms([(0, t) for t in required_terms]), self._terms(preferred_terms),
                 self._tols(tolerations), int(flags), self.s(namespace), self._labels(labels or {}),
-                self._spreads(spreads), self._anti(anti_affinity), self._ports(host_ports), self._anti(affinity))
+                self._spreads(spreads), self._anti(anti_affinity), self._ports(host_ports), self._anti(affinity),
+                (vb, len(self.volumes) - vb))
 
     def add_pod(self, uid, creation_ns, requests, node_selector=None, required_terms=(), preferred_terms=(),
                 tolerations=(), flags=0, namespace="default", labels=None, spreads=(), anti_affinity=(),
-                host_ports=(), affinity=()):
+                host_ports=(), affinity=(), volumes=()):
         """required_terms: list of reqs lists; preferred_terms: list of (weight, reqs);
-        anti_affinity / affinity: pod (anti-)affinity term dicts (see _anti)"""
+        anti_affinity / affinity: pod (anti-)affinity term dicts (see _anti);
+        volumes: (csi driver, volume id) pairs"""
         self.pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
-                                   tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports, affinity))
+                                   tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports, affinity,
+                                   volumes))
         return len(self.pods) - 1
 
     def add_bound_pod(self, node, uid, creation_ns, requests, node_selector=None, required_terms=(),
                       preferred_terms=(), tolerations=(), flags=0, namespace="default", labels=None, spreads=(),
-                      anti_affinity=(), host_ports=(), affinity=()):
+                      anti_affinity=(), host_ports=(), affinity=(), volumes=()):
         """a pod bound to state node `node` (counted by topology selectors;
         consolidation reschedules the candidates' pods)"""
         self.bound_pods.append(self._pod(uid, creation_ns, requests, node_selector, required_terms, preferred_terms,
                                          tolerations, flags, namespace, labels, spreads, anti_affinity, host_ports,
-                                         affinity))
+                                         affinity, volumes))
         self.bound_node.append(int(node))
         return len(self.bound_pods) - 1
 
@@ -191,9 +198,12 @@ class ProblemBuilder:
         self.claim_queries.append((self._reqs(requirements), self._qty(requests or {})))
         return len(self.claim_queries) - 1
 
-    def add_node(self, name, labels, available, requests=None, taints=(), initialized=True):
+    def add_node(self, name, labels, available, requests=None, taints=(), initialized=True, volume_limits=None):
+        """volume_limits: {csi driver: CSINode allocatable count}"""
+        lb = len(self.volume_limits)
+        self.volume_limits.extend((self.s(k), int(v)) for k, v in (volume_limits or {}).items())
         self.nodes.append((self.s(name), 1 if initialized else 0, self._labels(labels), self._taints(taints),
-                           self._qty(available), self._qty(requests or {})))
+                           self._qty(available), self._qty(requests or {}), (lb, len(self.volume_limits) - lb)))
         return len(self.nodes) - 1
 
     def build(self):
@@ -233,6 +243,8 @@ class Problem:
         self.spreads = _np(b.spreads, abi.DT_SPREAD)
         self.affinity_terms = _np(b.affinity_terms, abi.DT_AFFINITY)
         self.host_ports = _np(b.host_ports, abi.DT_HOSTPORT)
+        self.volumes = _np(b.volumes, abi.DT_VOLUME)
+        self.volume_limits = _np(b.volume_limits, abi.DT_VOLUME_LIMIT)
         self.claim_queries = (abi.GsClaimQuery * max(1, len(b.claim_queries)))()
         self.n_claim_queries = len(b.claim_queries)
         for i, (rq, qt) in enumerate(b.claim_queries):
@@ -244,7 +256,7 @@ class Problem:
         st.n_strings = len(self._bytes)
         for name in ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                      "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods",
-                     "affinity_terms", "host_ports"):
+                     "affinity_terms", "host_ports", "volumes", "volume_limits"):
             arr = getattr(self, name)
             setattr(st, name, arr.ctypes.data if len(arr) else None)
             setattr(st, "n_" + name, len(arr))
@@ -252,14 +264,14 @@ class Problem:
 
     _DUMP_ARRAYS = ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                     "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods", "bound_node",
-                    "affinity_terms", "host_ports")
+                    "affinity_terms", "host_ports", "volumes", "volume_limits")
 
     def dump(self, path):
         """binary dump read by tools/encode_harness.cpp (host-only encoder
         runs: sanitizers, profiling)"""
         import struct
         with open(path, "wb") as f:
-            f.write(b"GSPD" + struct.pack("<II", 2, len(self._bytes)))
+            f.write(b"GSPD" + struct.pack("<II", 3, len(self._bytes)))
             for s in self._bytes:
                 f.write(struct.pack("<I", len(s)) + s)
             for name in self._DUMP_ARRAYS:

@@ -812,3 +812,35 @@ def min_values_truncation(n_cheap=70):
     for i in range(3):
         b.add_pod(f"p{i}", 0, {"cpu": 500, "memory": GI * 1000, "pods": 1000})
     return b.build()
+
+
+def random_volumes(seed, n_pods=None):
+    """small adversarial problems for CSI attach limits on existing nodes
+    (<U> VolumeUsage): 1-3 drivers, per-node limits (some nodes unlimited or
+    already at / over their limit), bound pods holding volumes, pending pods
+    with new and shared volumes, NodeClaims (no limits) as the overflow"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2"]
+    profs = [("bx2-4x16", 4, 16, None), ("bx2-8x32", 8, 32, None), ("cx2-4x8", 4, 8, None)]
+    its = build_catalog(b, profs, zones, spot=False, prices=price_table(profs))
+    b.add_nodepool("np0", daemon={"cpu": 100, "pods": 1000})
+    drivers = ["ebs.csi", "vpc.block.csi.ibm.io", "nfs.csi"][: int(rng.integers(1, 4))]
+    vols = [(str(rng.choice(drivers)), f"pv-{k}") for k in range(int(rng.integers(2, 24)))]
+    for k in range(int(rng.integers(1, 6))):
+        it = its[rng.integers(0, len(its))]
+        labels = {r_[0]: r_[2][0] for r_ in it.requirements}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(zones))
+        labels["kubernetes.io/hostname"] = f"n{k}"
+        lim = {d: int(rng.integers(0, 5)) for d in drivers if rng.random() < 0.7}
+        b.add_node(f"n{k}", labels, {"cpu": 16000, "memory": 64 * GI * 1000, "pods": 110_000}, volume_limits=lim)
+        for q in range(int(rng.integers(0, 4))):
+            mine = [vols[i] for i in sorted(set(rng.integers(0, len(vols), size=int(rng.integers(0, 3))).tolist()))]
+            b.add_bound_pod(k, _uid(rng), 0, {"cpu": 100, "pods": 1000}, volumes=mine)
+    n = int(n_pods if n_pods is not None else rng.integers(1, 30))
+    for i in range(n):
+        mine = [vols[j] for j in sorted(set(rng.integers(0, len(vols), size=int(rng.integers(0, 3))).tolist()))]
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000,
+                  {"cpu": int(rng.choice([250, 500, 1000])), "memory": GI * 1000, "pods": 1000},
+                  volumes=mine if rng.random() < 0.7 else [])
+    return b.build()

@@ -455,6 +455,7 @@ struct Pod {
   vector<AffTerm> anti_preferred;  // mutable (relaxation)
   vector<AffTerm> aff_required;
   vector<AffTerm> aff_preferred;   // mutable (relaxation)
+  vector<std::pair<string, string>> volumes;  // (CSI driver, volume id)
   vector<HostPort> ports;
 };
 
@@ -487,6 +488,8 @@ struct ExistingNode {
   Res available, requests;
   vector<const Pod*> pods;
   vector<HostPort> ports;  // hostPortUsage of the bound pods
+  std::map<string, std::set<string>> vols;  // VolumeUsage: driver -> volume ids
+  std::map<string, int64_t> vol_limits;     // CSINode allocatable counts
 };
 
 // <U> NewPodRequirements: nodeSelector + heaviest preferred term (sort.Slice
@@ -746,6 +749,9 @@ struct Builder {
     if (pending) terms(g.affinity, true);  // pod affinity has no inverse: bound pods' terms do nothing
     if (pd.aff_preferred.size() > 12) throw Unsupported{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
     if (pd.anti_preferred.size() > 12) throw Unsupported{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
+    check_range(g.volumes, p->n_volumes, "volumes");
+    for (uint32_t k = 0; k < g.volumes.count; k++)
+      pd.volumes.push_back({str(p->volumes[g.volumes.begin + k].driver), str(p->volumes[g.volumes.begin + k].id)});
     check_range(g.host_ports, p->n_host_ports, "host_ports");
     for (uint32_t k = 0; k < g.host_ports.count; k++) {
       const gs_host_port& q = p->host_ports[g.host_ports.begin + k];
@@ -840,9 +846,10 @@ struct Builder {
       bound[b].index = UINT32_MAX;
       pod_meta(p->bound_pods[b], bound[b], false);
       for (auto& a : bound[b].anti_required) inverse_of(a);
-      // ExistingNode hostPortUsage
+      // ExistingNode hostPortUsage and VolumeUsage
       auto& n = st.nodes[p->bound_pod_node[b]];
       n.ports.insert(n.ports.end(), bound[b].ports.begin(), bound[b].ports.end());
+      for (auto& v : bound[b].volumes) n.vols[v.first].insert(v.second);
     }
     if (st.groups.empty() && st.inverse.empty()) return;
     for (auto* gs : {&st.groups, &st.inverse})
@@ -999,6 +1006,11 @@ struct Builder {
       n.taints = taints_of(g.taints);
       n.available = res_of(g.available);
       n.requests = res_of(g.requests);
+      check_range(g.volume_limits, p->n_volume_limits, "volume_limits");
+      for (uint32_t k = 0; k < g.volume_limits.count; k++) {
+        const gs_volume_limit& l = p->volume_limits[g.volume_limits.begin + k];
+        n.vol_limits[str(l.driver)] = l.limit;
+      }
     }
     st.node_order.resize(p->n_nodes);
     for (uint32_t i = 0; i < p->n_nodes; i++) st.node_order[i] = i;
@@ -1247,6 +1259,15 @@ struct Scheduler {
   bool node_can_add(const ExistingNode& n, const Pod& pod, Reqs* reqs_out, Res* req_out) {
     if (!tolerates_all(n.taints, pod.tolerations)) return false;
     if (ports_conflict(n.ports, pod.ports)) return false;  // hostPortUsage.Conflicts
+    {
+      // <U> VolumeUsage.ExceedsLimits: every driver of the union within its limit
+      auto u = n.vols;
+      for (auto& v : pod.volumes) u[v.first].insert(v.second);
+      for (auto& kv : u) {
+        auto f = n.vol_limits.find(kv.first);
+        if (f != n.vol_limits.end() && (int64_t)kv.second.size() > f->second) return false;
+      }
+    }
     Res requests = merge(n.requests, pod.requests);
     if (!fits(requests, n.available)) return false;
     Reqs nr = n.reqs;
@@ -1273,6 +1294,7 @@ struct Scheduler {
         n.requests = std::move(q);
         n.pods.push_back(&pod);
         n.ports.insert(n.ports.end(), pod.ports.begin(), pod.ports.end());
+        for (auto& v : pod.volumes) n.vols[v.first].insert(v.second);
         topo_record(pod, n.reqs);
         return true;
       }
@@ -1796,7 +1818,7 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
       if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
     for (uint32_t i = 0; i < in->cluster->n_bound_pods; i++)
       if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
-    if (in->cluster->n_spreads || in->cluster->n_affinity_terms || in->cluster->n_host_ports)
+    if (in->cluster->n_spreads || in->cluster->n_affinity_terms || in->cluster->n_host_ports || in->cluster->n_volumes)
       return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
     for (auto& t : base.templates)
       if (has_min_values(t.reqs)) return GS_E_UNSUPPORTED;  // likewise

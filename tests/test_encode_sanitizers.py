@@ -46,6 +46,8 @@ def _problems():
         out.append((f"anti{s}", synth.random_affinity(s)))
     for s in range(8):
         out.append((f"minv{s}", synth.random_min_values(s)))
+    for s in range(8):
+        out.append((f"vol{s}", synth.random_volumes(s)))
     out.append(("c1", synth.make_c1()))
     out.append(("c3_2k", synth.make_c3(n_pods=2000)))
     out.append(("c4_200", synth.make_c4(n_nodes=200, n_pending=5)))
