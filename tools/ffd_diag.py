@@ -1,4 +1,4 @@
-"""Diagnostic: FFD kernel phase breakdown on the CM workload.
+"""Diagnostic: FFD kernel phase breakdown on the CM workload (--c1 / --c2: those configs).
 
 default build: barrier-to-barrier wall-clock timers (Ctrl.dbg);
 `make tl` build + --tl: shader cycles per pod-loop segment (GS_FFD_TL)."""
@@ -12,7 +12,12 @@ from gpusched import synth  # noqa: E402
 from gpusched.lib import Solver  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
-p = synth.make_cm(n_pods=int(args[0]) if args else 100000)
+if "--c1" in sys.argv:
+    p = synth.make_c1()
+elif "--c2" in sys.argv:
+    p = synth.make_c2()
+else:
+    p = synth.make_cm(n_pods=int(args[0]) if args else 100000)
 s = Solver(0, 1 if "--block" in sys.argv else 0)
 s.prepare(p)
 s.run()
