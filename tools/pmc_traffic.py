@@ -20,7 +20,9 @@ def kernel_key(name):
         return "ffd"
     if name.startswith("void ffd_kernel"):
         return "sim" if ", true," in name else "ffd"
-    if name.startswith("feas_kernel"):
+    if name.startswith("feas_cursor_kernel"):
+        return "feas_cursor"
+    if name.startswith("feas_kernel") or name.startswith("void feas_kernel"):
         return "feas"
     if name.startswith("trunc_kernel"):
         return "trunc"
