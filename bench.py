@@ -543,8 +543,8 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=200_000)
     ap.add_argument("--cpu-sample-c5-pods", type=int, default=2000)
     ap.add_argument("--no-stress", action="store_true")
-    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | c4 | c4_mixed | c4_multi | "
-                                                 "c5 | filter | ranking (profiling passes)")
+    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | c4 | c4_mixed | "
+                                                 "c4_multi | c5 | filter | ranking (profiling passes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per leg (tools/pmc_traffic.py, committed under profiles/)")
     args = ap.parse_args()
@@ -615,12 +615,17 @@ def main():
             line["create_filter"] = bench_create_filter(problem, result, args)
         del problem, result
 
-    if solo and not args.no_configs and only in (None, "c1", "c2", "c3"):
+    if solo and not args.no_configs and only in (None, "c1", "c2", "c3", "e2e"):
         configs = {}
         gens = {"c1": (synth.make_c1, "C1: 500 pods x 8 fake profiles x 3 zones (24 offerings), 1 NodePool"),
                 "c2": (synth.make_c2, "C2: 10k pods x C2 catalog (1,188 offerings), 1 NodePool"),
                 "c3": (synth.make_c3, "C3: 50k pods x C2 catalog, 4 weighted NodePools, taints/tolerations, "
-                                      "required + preferred node affinity, 20% zone topology spread")}
+                                      "required + preferred node affinity, 20% zone topology spread"),
+                # the reference e2e suite's deployment shape at scale (test/e2e/config.go:455-490)
+                "e2e": (lambda: synth.e2e_deployments(n_deployments=60, replicas=500),
+                        "e2e: 30k pods in 60 deployments x 500 replicas, each with a preferred (weight 100) "
+                        "kubernetes.io/hostname podAntiAffinity on its own app label, 16-type catalog x 3 zones x "
+                        "{on-demand, spot}")}
         for name, (gen, desc) in gens.items():
             if only not in (None, name):
                 continue
