@@ -1,4 +1,4 @@
-"""Diagnostic: FFD kernel phase breakdown on the CM workload (--c1 / --c2: those configs).
+"""Diagnostic: FFD kernel phase breakdown on the CM workload (--c1 / --c2 / --c3 / --e2e: those workloads).
 
 default build: barrier-to-barrier wall-clock timers (Ctrl.dbg);
 `make tl` build + --tl: shader cycles per pod-loop segment (GS_FFD_TL)."""
@@ -14,6 +14,10 @@ from gpusched.lib import Solver  # noqa: E402
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 if "--c1" in sys.argv:
     p = synth.make_c1()
+elif "--c3" in sys.argv:
+    p = synth.make_c3()
+elif "--e2e" in sys.argv:
+    p = synth.e2e_deployments(n_deployments=60, replicas=500)
 elif "--c2" in sys.argv:
     p = synth.make_c2()
 else:
@@ -26,7 +30,7 @@ s.L.gs_debug_ctrl.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
 s.L.gs_debug_ctrl(s.ctx, out, 16)
 d, res = s.fetch()
 base = {"ffd_ms": res.t_ffd_ms, "pops": res.pops, "claims": len(d['claims']), "cand_evals": res.cand_evals,
-        "cand_full": res.cand_full}
+        "cand_full": res.cand_full, "sorts_fast": res.sorts_fast, "sorts_generic": res.sorts_generic}
 if "--tl" in sys.argv and "--block" not in sys.argv:
     names = ["pop_record", "nodes", "sort", "scan_add", "new_claim", "scanA_lds", "scanB_exact", "tail"]
     base["cycles_per_pop"] = {n: round(out[i] / max(res.pops, 1), 1) for i, n in enumerate(names) if n != "-"}
