@@ -876,7 +876,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_NO_FAST
     bool simple = false;
 #else
-    bool simple = !TOPO && (vctb & VF_SIMPLE);
+    // a pod with no requirements and no owned topology group (VF_SIMPLE):
+    // its CanAdd is resources and taints only, in either variant
+    bool simple = (vctb & VF_SIMPLE) != 0;
 #endif
 #pragma unroll
     for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
@@ -1237,6 +1239,25 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const uint32_t e = s_so[f];
             if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
             s_so[f] = e + 1u;
+            if (TOPO && vtsel) {
+              // <U> Topology.Record in the groups that select the pod: the
+              // NodeClaim's requirements are unchanged by this Add
+              const auto& KD = *karg();
+              const ClaimRec* cr = KD.c_rec + j;
+              const uint64_t zf = cr->zfull;
+              const uint32_t zl = cr->zflags;
+              for (uint64_t m = vtsel; m; m &= m - 1) {
+                const uint32_t g = ffs64(m);
+                if ((KD.tg_host >> g) & 1) {
+                  KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
+                  s_zcnt[g * ZVMAX]++;
+                } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
+                  const uint32_t z = ffs64(zf);
+                  s_zcnt[g * ZVMAX + z]++;
+                  s_known[g] |= 1ull << z;
+                }
+              }
+            }
           }
         }
         wsync();
