@@ -154,12 +154,21 @@ struct WaveSort {
     so[i] = so[j];
     so[j] = a;
   }
+  // the passes below test RW x 64 positions per step: every lane issues its
+  // RW LDS reads before the first ballot (one round trip per step)
+  static constexpr int RW = 4;
   template <class Pred>
   __device__ uint32_t count(int lo, int hi, Pred pred) const {
     uint32_t c = 0;
-    for (int base = lo; base < hi; base += 64) {
-      const int k = base + (int)lane;
-      c += (uint32_t)__popcll(__ballot(k < hi && pred(k)));
+    for (int base = lo; base < hi; base += 64 * RW) {
+      bool in[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        in[u] = k < hi && pred(k);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) c += (uint32_t)__popcll(__ballot(in[u]));
     }
     return c;
   }
@@ -168,13 +177,20 @@ struct WaveSort {
   __device__ uint32_t compact(int lo, int hi, bool desc, uint16_t* out, Pred pred) const {
     uint32_t total = 0;
     const int n = hi - lo;
-    for (int base = 0; base < n; base += 64) {
-      const int idx = base + (int)lane;
-      const int k = desc ? hi - 1 - idx : lo + idx;
-      const bool in = idx < n && pred(k);
-      const uint64_t m = __ballot(in);
-      if (in) out[total + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)k;
-      total += (uint32_t)__popcll(m);
+    for (int base = 0; base < n; base += 64 * RW) {
+      bool in[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int idx = base + u * 64 + (int)lane;
+        in[u] = idx < n && pred(desc ? hi - 1 - idx : lo + idx);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int idx = base + u * 64 + (int)lane;
+        const uint64_t m = __ballot(in[u]);
+        if (in[u]) out[total + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(desc ? hi - 1 - idx : lo + idx);
+        total += (uint32_t)__popcll(m);
+      }
     }
     wsync();
     return total;
@@ -263,10 +279,18 @@ struct WaveSort {
   }
   // first k in [from, b) with key(k) < key(k-1); b if none
   __device__ int first_inversion(int from, int b) const {
-    for (int base = from; base < b; base += 64) {
-      const int k = base + (int)lane;
-      const uint64_t m = __ballot(k < b && key(k) < key(k - 1));
-      if (m) return base + (int)ffs64(m);
+    for (int base = from; base < b; base += 64 * RW) {
+      bool hit[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        hit[u] = k < b && key(k) < key(k - 1);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const uint64_t m = __ballot(hit[u]);
+        if (m) return base + u * 64 + (int)ffs64(m);
+      }
     }
     return b;
   }
