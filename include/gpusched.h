@@ -62,10 +62,10 @@ enum {
 enum { GS_TOL_EQUAL = 0, GS_TOL_EXISTS = 1 };
 
 /* gs_pod.flags: scheduling features present on the pod that this build
- * refuses (GS_E_UNSUPPORTED) rather than silently ignoring.  Pod
- * anti-affinity terms and host ports are passed in gs_pod.anti_affinity /
- * gs_pod.host_ports; the ANTI_AFFINITY / HOST_PORTS flags remain for forms
- * those cannot express (a namespaceSelector, a matchLabelKeys list). */
+ * refuses (GS_E_UNSUPPORTED) rather than silently ignoring.  Pod (anti-)
+ * affinity terms, host ports and volumes are passed in their gs_pod ranges;
+ * the flags remain for forms those cannot express (for example an affinity
+ * term's matchLabelKeys / mismatchLabelKeys). */
 enum {
   GS_POD_TOPOLOGY_SPREAD = 1u << 0,
   GS_POD_AFFINITY = 1u << 1,   /* forms gs_pod.affinity cannot express */
@@ -149,8 +149,9 @@ typedef struct gs_nodepool {
 } gs_nodepool;
 
 /* corev1.TopologySpreadConstraint (<U> karpenter Topology: spread groups on
- * topology.kubernetes.io/zone or kubernetes.io/hostname; other keys, a
- * Honor nodeTaintsPolicy and matchLabelKeys are refused) */
+ * topology.kubernetes.io/zone or kubernetes.io/hostname; other keys and a
+ * Honor nodeTaintsPolicy are refused).  matchLabelKeys: for every listed key
+ * the pod carries, the selector also requires key In [the pod's value]. */
 enum { GS_SPREAD_DO_NOT_SCHEDULE = 0, GS_SPREAD_SCHEDULE_ANYWAY = 1 };
 enum { GS_POLICY_HONOR = 0, GS_POLICY_IGNORE = 1 };
 typedef struct gs_spread {
@@ -163,6 +164,7 @@ typedef struct gs_spread {
   gs_range match_expressions;    /* into reqs: In / NotIn / Exists / DoesNotExist over pod labels */
   uint32_t node_affinity_policy; /* GS_POLICY_HONOR (default) or GS_POLICY_IGNORE */
   uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is refused */
+  gs_range match_label_keys;     /* into value_ids: label keys (string ids) */
 } gs_spread;
 
 /* corev1.PodAffinityTerm of spec.affinity.podAffinity or .podAntiAffinity: a
@@ -183,8 +185,19 @@ typedef struct gs_affinity_term {
   uint32_t has_selector;       /* 0: nil labelSelector (selects no pod) */
   gs_range match_labels;       /* into labels */
   gs_range match_expressions;  /* into reqs: In / NotIn / Exists / DoesNotExist */
-  gs_range namespaces;         /* into value_ids (string ids); empty = the pod's namespace */
+  gs_range namespaces;         /* into value_ids (string ids) */
+  uint32_t has_ns_selector;    /* namespaceSelector set ({} selects every namespace) */
+  gs_range ns_match_labels;    /* into labels: over gs_problem.namespaces' labels */
+  gs_range ns_match_expressions; /* into reqs */
+  /* <U> buildNamespaceList: no namespaces and no selector = the pod's
+   * namespace; else the listed ones plus those the selector matches */
 } gs_affinity_term;
+
+/* a namespace and its labels (namespaceSelector of pod (anti-)affinity terms) */
+typedef struct gs_namespace {
+  uint32_t name;    /* string id */
+  gs_range labels;  /* into labels */
+} gs_namespace;
 
 /* a containers[].ports[] entry with hostPort != 0 (<U> scheduling
  * HostPortUsage: two entries conflict when protocol and port are equal and
@@ -263,6 +276,7 @@ typedef struct gs_problem {
   const gs_host_port* host_ports; uint32_t n_host_ports;
   const gs_volume* volumes; uint32_t n_volumes;
   const gs_volume_limit* volume_limits; uint32_t n_volume_limits;
+  const gs_namespace* namespaces; uint32_t n_namespaces;
 } gs_problem;
 
 /* Results.TruncateInstanceTypes(60) of Scheduler.Solve */

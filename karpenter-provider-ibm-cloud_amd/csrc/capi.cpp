@@ -309,7 +309,7 @@ extern "C" {
 const char* gs_version(void) { return "gpusched 0.1 (gfx950)"; }
 
 uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
-  const uint32_t s[30] = {sizeof(gs_range),        sizeof(gs_requirement),         sizeof(gs_quantity),
+  const uint32_t s[31] = {sizeof(gs_range),        sizeof(gs_requirement),         sizeof(gs_quantity),
                           sizeof(gs_label),        sizeof(gs_taint),               sizeof(gs_toleration),
                           sizeof(gs_term),         sizeof(gs_offering),            sizeof(gs_instance_type),
                           sizeof(gs_nodepool),     sizeof(gs_pod),                 sizeof(gs_node),
@@ -319,9 +319,9 @@ uint32_t gs_abi_sizes(uint32_t* out, uint32_t n) {
                           sizeof(gs_claim_filter_result), sizeof(gs_vpc_profile), sizeof(gs_price),
                           sizeof(gs_unavailable), sizeof(gs_catalog_env), sizeof(gs_catalog),
                           sizeof(gs_affinity_term), sizeof(gs_host_port), sizeof(gs_volume),
-                          sizeof(gs_volume_limit)};
-  for (uint32_t i = 0; i < n && i < 30; i++) out[i] = s[i];
-  return 30;
+                          sizeof(gs_volume_limit), sizeof(gs_namespace)};
+  for (uint32_t i = 0; i < n && i < 31; i++) out[i] = s[i];
+  return 31;
 }
 
 gs_status gs_validate(const gs_problem* p, char* err, size_t len) {

@@ -784,6 +784,16 @@ struct Ctx {
         for (uint32_t v = 0; v < r.values.count; v++) vals.insert(S(p->value_ids[r.values.begin + v]));
         sp.ex.emplace_back(S(r.key), r.op, std::move(vals));
       }
+      // matchLabelKeys: key In [the pod's value] for every key the pod carries
+      chk(q.match_label_keys, p->n_value_ids, "values");
+      if (q.match_label_keys.count) {
+        const auto labels = label_map(pd.labels);
+        for (uint32_t m = 0; m < q.match_label_keys.count; m++) {
+          const std::string& k = S(p->value_ids[q.match_label_keys.begin + m]);
+          auto f = labels.find(k);
+          if (f != labels.end()) sp.ex.emplace_back(k, (uint32_t)GS_OP_IN, std::set<std::string>{f->second});
+        }
+      }
       out.push_back(std::move(sp));
     }
     return out;
@@ -811,9 +821,29 @@ struct Ctx {
         for (uint32_t v = 0; v < r.values.count; v++) vals.insert(S(p->value_ids[r.values.begin + v]));
         a.sel.ex.emplace_back(S(r.key), r.op, std::move(vals));
       }
+      // <U> buildNamespaceList: the listed namespaces plus those the
+      // namespaceSelector matches; neither = the pod's namespace
       chk(q.namespaces, p->n_value_ids, "values");
       for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(S(p->value_ids[q.namespaces.begin + v]));
-      if (a.nss.empty()) a.nss.insert(S(pd.ns));
+      if (q.has_ns_selector) {
+        SpreadEnc nsel;
+        nsel.has_sel = true;
+        nsel.ml = label_map(q.ns_match_labels);
+        chk(q.ns_match_expressions, p->n_reqs, "reqs");
+        for (uint32_t x = 0; x < q.ns_match_expressions.count; x++) {
+          const gs_requirement& r = p->reqs[q.ns_match_expressions.begin + x];
+          if (r.op > GS_OP_DOES_NOT_EXIST) throw Fail{GS_E_INVALID, "label selector operator"};
+          chk(r.values, p->n_value_ids, "values");
+          std::set<std::string> vals;
+          for (uint32_t v = 0; v < r.values.count; v++) vals.insert(S(p->value_ids[r.values.begin + v]));
+          nsel.ex.emplace_back(S(r.key), r.op, std::move(vals));
+        }
+        chk(gs_range{0, p->n_namespaces}, p->n_namespaces, "namespaces");
+        for (uint32_t n = 0; n < p->n_namespaces; n++)
+          if (nsel.matches(label_map(p->namespaces[n].labels))) a.nss.insert(S(p->namespaces[n].name));
+      } else if (a.nss.empty()) {
+        a.nss.insert(S(pd.ns));
+      }
       out.push_back(std::move(a));
     }
     return out;

@@ -46,14 +46,17 @@ DT_POD = np.dtype([("uid", "<u4"), ("creation_ns", "<i8"), ("requests", RANGE), 
 DT_VOLUME = np.dtype([("driver", "<u4"), ("id", "<u4")], align=True)
 DT_VOLUME_LIMIT = np.dtype([("driver", "<u4"), ("limit", "<i4")], align=True)
 DT_AFFINITY = np.dtype([("topology_key", "<u4"), ("required", "<u4"), ("weight", "<i4"), ("has_selector", "<u4"),
-                    ("match_labels", RANGE), ("match_expressions", RANGE), ("namespaces", RANGE)], align=True)
+                    ("match_labels", RANGE), ("match_expressions", RANGE), ("namespaces", RANGE),
+                    ("has_ns_selector", "<u4"), ("ns_match_labels", RANGE), ("ns_match_expressions", RANGE)],
+                   align=True)
+DT_NAMESPACE = np.dtype([("name", "<u4"), ("labels", RANGE)], align=True)
 DT_HOSTPORT = np.dtype([("protocol", "<u4"), ("ip", "<u4"), ("port", "<i4")], align=True)
 SPREAD_DO_NOT_SCHEDULE, SPREAD_SCHEDULE_ANYWAY = 0, 1
 POLICY_HONOR, POLICY_IGNORE = 0, 1
 DT_SPREAD = np.dtype([("topology_key", "<u4"), ("max_skew", "<i4"), ("when_unsatisfiable", "<u4"),
                       ("min_domains", "<i4"), ("has_selector", "<u4"), ("match_labels", RANGE),
                       ("match_expressions", RANGE), ("node_affinity_policy", "<u4"),
-                      ("node_taints_policy", "<u4")], align=True)
+                      ("node_taints_policy", "<u4"), ("match_label_keys", RANGE)], align=True)
 DT_NODE = np.dtype([("name", "<u4"), ("initialized", "<u4"), ("labels", RANGE), ("taints", RANGE),
                     ("available", RANGE), ("requests", RANGE), ("volume_limits", RANGE)], align=True)
 
@@ -84,6 +87,7 @@ class GsProblem(C.Structure):
         ("host_ports", _P), ("n_host_ports", _U32),
         ("volumes", _P), ("n_volumes", _U32),
         ("volume_limits", _P), ("n_volume_limits", _U32),
+        ("namespaces", _P), ("n_namespaces", _U32),
     ]
 
 

@@ -40,6 +40,7 @@ class ProblemBuilder:
         self.host_ports = []
         self.volumes = []
         self.volume_limits = []
+        self.namespaces = []
         self.claim_queries = []  # gs_claim_query (launch-time re-filter)
 
     # ------------------------------------------------------------ primitives
@@ -128,12 +129,16 @@ class ProblemBuilder:
             sel = sp.get("selector")
             ml = self._labels((sel or {}).get("labels", {}))
             me = self._reqs((sel or {}).get("exprs", []))
+            mk = list(sp.get("match_label_keys", []))
+            kb = len(self.value_ids)
+            self.value_ids.extend(self.s(k) for k in mk)
             self.spreads.append((self.s(sp["key"]), int(sp.get("max_skew", 1)),
                                  abi.SPREAD_SCHEDULE_ANYWAY if sp.get("when") == "ScheduleAnyway"
                                  else abi.SPREAD_DO_NOT_SCHEDULE,
                                  int(sp.get("min_domains", 0)), 0 if sel is None else 1, ml, me,
                                  abi.POLICY_IGNORE if sp.get("node_affinity_policy") == "Ignore" else abi.POLICY_HONOR,
-                                 abi.POLICY_HONOR if sp.get("node_taints_policy") == "Honor" else abi.POLICY_IGNORE))
+                                 abi.POLICY_HONOR if sp.get("node_taints_policy") == "Honor" else abi.POLICY_IGNORE,
+                                 (kb, len(mk))))
         return (b, len(self.spreads) - b)
 
     def _anti(self, terms):
@@ -148,8 +153,12 @@ class ProblemBuilder:
             nss = list(t.get("namespaces", []))
             vb = len(self.value_ids)
             self.value_ids.extend(self.s(x) for x in nss)
+            nsel = t.get("namespace_selector")  # None = unset, else {"labels": {...}, "exprs": [...]}
+            nml = self._labels((nsel or {}).get("labels", {}))
+            nme = self._reqs((nsel or {}).get("exprs", []))
             self.affinity_terms.append((self.s(t.get("key", "kubernetes.io/hostname")), 1 if t.get("required") else 0,
-                                         int(t.get("weight", 1)), 0 if sel is None else 1, ml, me, (vb, len(nss))))
+                                        int(t.get("weight", 1)), 0 if sel is None else 1, ml, me, (vb, len(nss)),
+                                        0 if nsel is None else 1, nml, nme))
         return (b, len(self.affinity_terms) - b)
 
     def _ports(self, ports):
@@ -191,6 +200,11 @@ class ProblemBuilder:
                                          affinity, volumes))
         self.bound_node.append(int(node))
         return len(self.bound_pods) - 1
+
+    def add_namespace(self, name, labels=None):
+        """a namespace and its labels (namespaceSelector of pod affinity terms)"""
+        self.namespaces.append((self.s(name), self._labels(labels or {})))
+        return len(self.namespaces) - 1
 
     def add_claim_query(self, requirements=(), requests=None):
         """a NodeClaim for gs_create_filter: spec.requirements (key, op,
@@ -245,6 +259,7 @@ class Problem:
         self.host_ports = _np(b.host_ports, abi.DT_HOSTPORT)
         self.volumes = _np(b.volumes, abi.DT_VOLUME)
         self.volume_limits = _np(b.volume_limits, abi.DT_VOLUME_LIMIT)
+        self.namespaces = _np(b.namespaces, abi.DT_NAMESPACE)
         self.claim_queries = (abi.GsClaimQuery * max(1, len(b.claim_queries)))()
         self.n_claim_queries = len(b.claim_queries)
         for i, (rq, qt) in enumerate(b.claim_queries):
@@ -256,7 +271,7 @@ class Problem:
         st.n_strings = len(self._bytes)
         for name in ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                      "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods",
-                     "affinity_terms", "host_ports", "volumes", "volume_limits"):
+                     "affinity_terms", "host_ports", "volumes", "volume_limits", "namespaces"):
             arr = getattr(self, name)
             setattr(st, name, arr.ctypes.data if len(arr) else None)
             setattr(st, "n_" + name, len(arr))
@@ -264,14 +279,14 @@ class Problem:
 
     _DUMP_ARRAYS = ("value_ids", "reqs", "quantities", "labels", "taints", "tolerations", "terms", "it_refs",
                     "offerings", "instance_types", "nodepools", "pods", "nodes", "spreads", "bound_pods", "bound_node",
-                    "affinity_terms", "host_ports", "volumes", "volume_limits")
+                    "affinity_terms", "host_ports", "volumes", "volume_limits", "namespaces")
 
     def dump(self, path):
         """binary dump read by tools/encode_harness.cpp (host-only encoder
         runs: sanitizers, profiling)"""
         import struct
         with open(path, "wb") as f:
-            f.write(b"GSPD" + struct.pack("<II", 3, len(self._bytes)))
+            f.write(b"GSPD" + struct.pack("<II", 4, len(self._bytes)))
             for s in self._bytes:
                 f.write(struct.pack("<I", len(s)) + s)
             for name in self._DUMP_ARRAYS:

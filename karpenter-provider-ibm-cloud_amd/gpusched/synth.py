@@ -580,6 +580,8 @@ def random_topology(seed, n_pods=None):
               "when": "ScheduleAnyway" if rng.random() < 0.4 else "DoNotSchedule", "selector": selector}
         if rng.random() < 0.15:
             sp["min_domains"] = int(rng.integers(2, 6))
+        if selector is not None and rng.random() < 0.25:
+            sp["match_label_keys"] = ["pod-template-hash"] + (["absent-key"] if rng.random() < 0.3 else [])
         palette.append(sp)
     n = int(n_pods if n_pods is not None else rng.integers(1, 40))
     for i in range(n):
@@ -596,8 +598,11 @@ def random_topology(seed, n_pods=None):
         if rng.random() < 0.1 and not spreads:
             sel["topology.kubernetes.io/zone"] = str(rng.choice(zones))
         tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+        labels = {"app": app}
+        if rng.random() < 0.6:
+            labels["pod-template-hash"] = str(rng.choice(["h1", "h2"]))
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000, req,
-                  node_selector=sel, required_terms=required, tolerations=tols, labels={"app": app},
+                  node_selector=sel, required_terms=required, tolerations=tols, labels=labels,
                   namespace=str(rng.choice(["default", "default", "other"])), spreads=spreads)
     return b.build()
 
@@ -641,12 +646,22 @@ def random_affinity(seed, n_pods=None):
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, taints=taints, limits=limits,
                        daemon={"cpu": 100, "pods": 1000})
     # palettes shared by pods (deployments share their terms)
+    b.add_namespace("default", {"team": "a"})
+    b.add_namespace("other", {"team": "b", "tier": "web"})
+    b.add_namespace("kube", {})
     anti_pal = []
     for _ in range(int(rng.integers(1, 5))):
         t = {"required": bool(rng.random() < 0.35), "weight": int(rng.choice([1, 10, 50, 100])),
              "selector": _selector(rng, str(rng.choice(APPS[:3])))}
         if rng.random() < 0.15:
             t["namespaces"] = sorted(set(rng.choice(["default", "other", "kube"], size=2).tolist()))
+        r = rng.random()
+        if r < 0.1:
+            t["namespace_selector"] = {}  # every namespace
+        elif r < 0.25:
+            t["namespace_selector"] = {"labels": {"team": str(rng.choice(["a", "b"]))}}
+        elif r < 0.3:
+            t["namespace_selector"] = {"exprs": [("tier", "Exists", [])]}
         anti_pal.append(t)
     aff_pal = []
     for _ in range(int(rng.integers(0, 3))):

@@ -713,6 +713,13 @@ struct Builder {
         for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
         sp.exprs.push_back(std::move(x));
       }
+      // matchLabelKeys: key In [the pod's value] for every key the pod carries
+      check_range(q.match_label_keys, p->n_value_ids, "values");
+      for (uint32_t m = 0; m < q.match_label_keys.count; m++) {
+        const string& k = str(p->value_ids[q.match_label_keys.begin + m]);
+        auto f = pd.labels.find(k);
+        if (f != pd.labels.end()) sp.exprs.push_back(Spread::Expr{k, GS_OP_IN, {f->second}});
+      }
       sp.ignore_affinity = q.node_affinity_policy == GS_POLICY_IGNORE;
       pd.spreads.push_back(std::move(sp));
     }
@@ -738,9 +745,28 @@ struct Builder {
           for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
           a.sel.exprs.push_back(std::move(x));
         }
+        // <U> buildNamespaceList
         check_range(q.namespaces, p->n_value_ids, "values");
         for (uint32_t v = 0; v < q.namespaces.count; v++) a.nss.insert(str(p->value_ids[q.namespaces.begin + v]));
-        if (a.nss.empty()) a.nss.insert(pd.ns);
+        if (q.has_ns_selector) {
+          Spread nsel;
+          nsel.has_selector = true;
+          nsel.match_labels = labels_of(q.ns_match_labels);
+          check_range(q.ns_match_expressions, p->n_reqs, "reqs");
+          for (uint32_t e = 0; e < q.ns_match_expressions.count; e++) {
+            const gs_requirement& r = p->reqs[q.ns_match_expressions.begin + e];
+            if (r.op > GS_OP_DOES_NOT_EXIST) throw Unsupported{GS_E_INVALID, "label selector operator"};
+            check_range(r.values, p->n_value_ids, "values");
+            Spread::Expr x{str(r.key), (int)r.op, {}};
+            for (uint32_t v = 0; v < r.values.count; v++) x.values.insert(str(p->value_ids[r.values.begin + v]));
+            nsel.exprs.push_back(std::move(x));
+          }
+          check_range(gs_range{0, p->n_namespaces}, p->n_namespaces, "namespaces");
+          for (uint32_t n = 0; n < p->n_namespaces; n++)
+            if (nsel.matches(labels_of(p->namespaces[n].labels))) a.nss.insert(str(p->namespaces[n].name));
+        } else if (a.nss.empty()) {
+          a.nss.insert(pd.ns);
+        }
         if (affinity) (a.required ? pd.aff_required : pd.aff_preferred).push_back(std::move(a));
         else (a.required ? pd.anti_required : pd.anti_preferred).push_back(std::move(a));
       }

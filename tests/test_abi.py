@@ -85,8 +85,8 @@ def test_validate_random_accepts():
 
 def test_struct_layouts_match_library():
     import ctypes as C
-    out = (C.c_uint32 * 30)()
-    assert lib.load().gs_abi_sizes(out, 30) == 30
+    out = (C.c_uint32 * 31)()
+    assert lib.load().gs_abi_sizes(out, 31) == 31
     mine = [8, abi.DT_REQ.itemsize, abi.DT_QTY.itemsize, abi.DT_LABEL.itemsize, abi.DT_TAINT.itemsize,
             abi.DT_TOL.itemsize, abi.DT_TERM.itemsize, abi.DT_OFFERING.itemsize, abi.DT_IT.itemsize,
             abi.DT_NODEPOOL.itemsize, abi.DT_POD.itemsize, abi.DT_NODE.itemsize, C.sizeof(abi.GsProblem),
@@ -95,5 +95,5 @@ def test_struct_layouts_match_library():
             C.sizeof(abi.GsClaimQuery), C.sizeof(abi.GsClaimFilterResult), C.sizeof(abi.GsVpcProfile),
             C.sizeof(abi.GsPrice), C.sizeof(abi.GsUnavailable), C.sizeof(abi.GsCatalogEnv), C.sizeof(abi.GsCatalog),
             abi.DT_AFFINITY.itemsize, abi.DT_HOSTPORT.itemsize,
-            abi.DT_VOLUME.itemsize, abi.DT_VOLUME_LIMIT.itemsize]
+            abi.DT_VOLUME.itemsize, abi.DT_VOLUME_LIMIT.itemsize, abi.DT_NAMESPACE.itemsize]
     assert list(out) == mine

@@ -241,6 +241,28 @@ def test_affinity_follows_bound_and_pending_pods():
     assert _pods(_solve(b)) == [[0, 1, 2]]
 
 
+def test_namespace_selector():
+    # a web pod in namespace team-b runs on n0; the pending pod (team-a) has a
+    # required anti-affinity on app=web: by default only its own namespace
+    # counts, with a namespaceSelector matching team-b the bound pod blocks n0
+    def build(nsel):
+        b = _base(n_pods=0)
+        b.add_namespace("team-a", {"team": "a"})
+        b.add_namespace("team-b", {"team": "b"})
+        _nodes(b)
+        b.add_bound_pod(0, "b0", 0, {"cpu": 100}, labels={"app": "web"}, namespace="team-b")
+        t = {"required": True, "selector": WEB}
+        if nsel is not None:
+            t["namespace_selector"] = nsel
+        b.add_pod("p0", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  namespace="team-a", anti_affinity=[t])
+        return b
+    assert _solve(build(None))["nodes"] == [[0], []]
+    assert _solve(build({"labels": {"team": "b"}}))["nodes"] == [[], [0]]
+    assert _solve(build({}))["nodes"] == [[], [0]]                      # {} selects every namespace
+    assert _solve(build({"labels": {"team": "c"}}))["nodes"] == [[0], []]  # selects none
+
+
 def test_refusals():
     b = _base(n_pods=1, anti=[{"key": Z, "required": True, "selector": WEB}])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED

@@ -79,6 +79,28 @@ def test_existing_pods_count_toward_domains():
     assert _zones(res) == [([0], "us-south-2"), ([1], "us-south-3")]
 
 
+def test_match_label_keys_split_the_group():
+    # two bound web pods of template hash h1 in us-south-1; pending pods of
+    # hash h2 spread over zones: counted with the h1 pods they avoid
+    # us-south-1, with matchLabelKeys [pod-template-hash] they start there
+    def build(mlk):
+        sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}
+        if mlk:
+            sp["match_label_keys"] = ["pod-template-hash"]
+        b = _base(n_pods=0)
+        b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0})
+        for q in range(2):
+            b.add_bound_pod(0, f"b{q}", 0, {"cpu": 1}, labels={"app": "web", "pod-template-hash": "h1"})
+        for i in range(2):
+            b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000},
+                      labels={"app": "web", "pod-template-hash": "h2"}, spreads=[sp])
+        return b
+    st, res, _ = pyoracle.solve(build(False).build())
+    assert _zones(res) == [([0], "us-south-2"), ([1], "us-south-3")]
+    st, res, _ = pyoracle.solve(build(True).build())
+    assert _zones(res) == [([0], "us-south-1"), ([1], "us-south-2")]
+
+
 def test_refusals():
     b = _base(n_pods=1, spread={"key": "karpenter.sh/capacity-type", "max_skew": 1, "selector": {}})
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
@@ -131,6 +153,18 @@ def test_gpu_topology_random_many_pods(solver, seed):
 
 @pytest.mark.gpu
 def test_gpu_topology_kats(solver):
+    for mlk in (False, True):
+        sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}
+        if mlk:
+            sp["match_label_keys"] = ["pod-template-hash"]
+        b = _base(n_pods=0)
+        b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0})
+        for q in range(2):
+            b.add_bound_pod(0, f"b{q}", 0, {"cpu": 1}, labels={"app": "web", "pod-template-hash": "h1"})
+        for i in range(2):
+            b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000},
+                      labels={"app": "web", "pod-template-hash": "h2"}, spreads=[sp])
+        _check(solver, b.build())
     _check(solver, _base(n_pods=7, spread={"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}).build())
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 

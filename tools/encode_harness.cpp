@@ -25,15 +25,15 @@ struct Dump {
 
 bool read_exact(FILE* f, void* dst, size_t n) { return fread(dst, 1, n, f) == n; }
 
-// layout: magic "GSPD", u32 version 3, u32 n_strings, per string u32 len +
-// bytes, then 20 arrays in gs_problem order (value_ids .. volume_limits),
+// layout: magic "GSPD", u32 version 4, u32 n_strings, per string u32 len +
+// bytes, then 21 arrays in gs_problem order (value_ids .. namespaces),
 // each u64 count + u64 element size + raw bytes
 bool load(const char* path, Dump& d) {
   FILE* f = fopen(path, "rb");
   if (!f) return false;
   char magic[4];
   uint32_t ver = 0, ns = 0;
-  bool ok = read_exact(f, magic, 4) && memcmp(magic, "GSPD", 4) == 0 && read_exact(f, &ver, 4) && ver == 3 &&
+  bool ok = read_exact(f, magic, 4) && memcmp(magic, "GSPD", 4) == 0 && read_exact(f, &ver, 4) && ver == 4 &&
             read_exact(f, &ns, 4);
   for (uint32_t i = 0; ok && i < ns; i++) {
     uint32_t len = 0;
@@ -42,7 +42,7 @@ bool load(const char* path, Dump& d) {
     ok = ok && (len == 0 || read_exact(f, &s[0], len));
     d.strs.push_back(std::move(s));
   }
-  for (int a = 0; ok && a < 20; a++) {
+  for (int a = 0; ok && a < 21; a++) {
     uint64_t n = 0, es = 0;
     ok = read_exact(f, &n, 8) && read_exact(f, &es, 8);
     std::vector<char> buf(n * es);
@@ -77,6 +77,7 @@ bool load(const char* path, Dump& d) {
   p.host_ports = (const gs_host_port*)A(17), p.n_host_ports = N(17, sizeof(gs_host_port));
   p.volumes = (const gs_volume*)A(18), p.n_volumes = N(18, sizeof(gs_volume));
   p.volume_limits = (const gs_volume_limit*)A(19), p.n_volume_limits = N(19, sizeof(gs_volume_limit));
+  p.namespaces = (const gs_namespace*)A(20), p.n_namespaces = N(20, sizeof(gs_namespace));
   return true;
 }
 
