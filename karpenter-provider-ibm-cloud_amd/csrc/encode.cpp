@@ -1291,17 +1291,28 @@ struct Ctx {
     auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
     // <U> the inverse anti-affinity groups: required terms of pending and
     // bound pods (Topology.updateInverseAntiAffinity / updateInverseAffinities)
+    // a problem without spreads, affinity terms or host ports builds no
+    // group: the per-pod selection state (labels, carried terms) is skipped
+    const bool topo_inputs = p->n_spreads || p->n_affinity_terms || p->n_host_ports;
     std::map<std::string, AntiEnc> inv_terms;
-    pod_sel.reserve(e.P);
-    for (uint32_t i = 0; i < e.P; i++) {
-      pod_sel.push_back(sel_of(p->pods[i]));
-      for (auto& a : antis_of(p->pods[i]))
-        if (a.required) inv_terms.emplace(a.hash(), a);
+    if (topo_inputs) {
+      pod_sel.reserve(e.P);
+      for (uint32_t i = 0; i < e.P; i++) {
+        pod_sel.push_back(sel_of(p->pods[i]));
+        for (auto& a : antis_of(p->pods[i]))
+          if (a.required) inv_terms.emplace(a.hash(), a);
+      }
+      chk(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
+      for (uint32_t b = 0; b < p->n_bound_pods; b++)
+        for (auto& a : antis_of(p->bound_pods[b]))
+          if (a.required) inv_terms.emplace(a.hash(), a);
+    } else {
+      for (uint32_t i = 0; i < e.P; i++) {
+        chk(p->pods[i].anti_affinity, p->n_affinity_terms, "affinity_terms");
+        chk(p->pods[i].affinity, p->n_affinity_terms, "affinity_terms");
+        chk(p->pods[i].host_ports, p->n_host_ports, "host_ports");
+      }
     }
-    chk(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
-    for (uint32_t b = 0; b < p->n_bound_pods; b++)
-      for (auto& a : antis_of(p->bound_pods[b]))
-        if (a.required) inv_terms.emplace(a.hash(), a);
     for (uint32_t i = 0; i < e.P; i++) {
       auto& pd = p->pods[i];
       if (pd.flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
@@ -1349,9 +1360,10 @@ struct Ctx {
       std::vector<uint32_t> cur(sps.size());  // current constraints (swap-remove order)
       std::iota(cur.begin(), cur.end(), 0);
       // anti-affinity, inverse anti-affinity and host-port groups
-      const PodSel& me = pod_sel[i];
       uint64_t own_static = 0;
-      std::vector<std::pair<int32_t, uint32_t>> anti_pref;  // (weight, group)
+      std::vector<std::pair<int32_t, uint32_t>> anti_pref, aff_pref;  // (weight, group)
+      if (topo_inputs) {
+      const PodSel& me = pod_sel[i];
       for (auto& a : antis_of(pd)) {
         const bool self = a.selects(me.ns, me.labels);
         GroupEnc g = host_group(1, self);
@@ -1361,7 +1373,6 @@ struct Ctx {
         else anti_pref.push_back({a.weight, gid});
       }
       if (anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
-      std::vector<std::pair<int32_t, uint32_t>> aff_pref;  // (weight, group)
       for (auto& a : terms_of(pd, pd.affinity)) {
         GroupEnc g = host_group(4, false);
         g.anti = a;
@@ -1384,6 +1395,7 @@ struct Ctx {
         GroupEnc g = host_group(3, true);
         g.port = pe;
         own_static |= 1ull << group_id("P|" + pe.key(), std::move(g));
+      }
       }
       chk(pd.tolerations, p->n_tolerations, "tolerations");
       std::vector<Tol> tols;
