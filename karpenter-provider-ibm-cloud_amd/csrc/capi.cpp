@@ -150,6 +150,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->alloc(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
   if (sims) {
     d.n_sims = (uint32_t)NS;
+    d.sim_nt = sims->nt;
     d.ov_cap = std::max<uint32_t>(sims->ov_cap, 1);
     d.nb_words = (e.NN + 31) / 32;
     c->upload(d.sim_pod_off, sims->pod_off);

@@ -260,7 +260,10 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   // persistent workgroups draining the simulation counter: as many as stay
   // resident (occupancy of the simulation kernel at this LDS size)
-  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds);
+  // many simulations: the narrow workgroup (throughput); few: the wide one
+  // (each simulation's latency) -- ffd.hip FB_SIM / FB_SIM_NARROW
+  sp.nt = sp.evaluated.size() >= 4 * (size_t)std::max(cus, 1) ? 128u : 256u;
+  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt);
   sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
   return GS_OK;
 }

@@ -18,7 +18,7 @@
 extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
-extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds);
+extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt);
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
                                       uint32_t TG);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
@@ -72,7 +72,7 @@ struct SimPlan {
   std::vector<uint32_t> evaluated;          // simulations of this shard, in order
   std::vector<uint32_t> pod_off, pods;      // per evaluated simulation: pod ids in queue order
   std::vector<uint32_t> cand_off, cands;    // per evaluated simulation: device node positions removed
-  uint32_t max_pods = 0, ov_cap = 0, blocks = 0;
+  uint32_t max_pods = 0, ov_cap = 0, blocks = 0, nt = 256;
   uint32_t multi_max = 0;                   // MULTI: firstNConsolidationOption's max
 };
 

@@ -48,7 +48,13 @@ namespace {
 #define GS_FB_MAX 512
 #endif
 constexpr int FB_MAX = GS_FB_MAX;  // workgroup size of the provisioning Solve (512: 256 VGPRs, no spills)
-constexpr int FB_SIM = 256;   // workgroup size of one consolidation simulation
+// Workgroup sizes of one consolidation simulation.  Many small simulations
+// (SingleNode: thousands, ~20 pods each) are throughput-bound: 128 threads at
+// 3 waves per SIMD compile spill-free and keep 6 workgroups per CU resident.
+// Few large ones (MultiNode prefixes: up to 100 nodes' pods) are latency-bound
+// and use 256 threads (gs_consolidate picks, DevProblem::sim_nt).
+constexpr int FB_SIM = 256;
+constexpr int FB_SIM_NARROW = 128;
 constexpr int NWAVE_MAX = FB_MAX / 64;
 #ifndef GS_SEQ_SORT
 #define GS_SEQ_SORT 32  // measured on CM: 32 -> 789 ms, 64 -> 815, 128 -> 819 (same box)
@@ -560,10 +566,16 @@ struct Blk {
 //    the existing nodes minus its candidates: the shared read-only base
 //    nodes0 / n_fk0 plus an overlay of the nodes this simulation touched (LDS
 //    bitmap + overlay ids, global req/FK copies per block).
+// Waves per SIMD the SIM shapes are compiled for.  At 4 the register budget
+// is 128 and the simulation loop spills (scratch traffic was 2/3 of the
+// kernel's HBM bytes on C4); at 3 (168 registers) the narrow shape is
+// spill-free.  The wide shape keeps 4: its few long simulations gain more
+// from residency than they lose to the spills.
+constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? 3 : 4; }
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
 
 template <uint32_t RR, bool SIM, uint32_t NT, bool TOPO>
-__global__ __launch_bounds__(NT, SIM ? 4 : 1) void ffd_kernel(DevProblem d) {
+__global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel(DevProblem d) {
   constexpr uint32_t FB = NT;  // threads of this workgroup
   extern __shared__ uint64_t lds64[];
   __shared__ Shared S;
@@ -1853,9 +1865,8 @@ extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32
 // every instantiation may use all LDS its static footprint leaves free
 static uint32_t g_ffd_dyn_max = 0;
 
-template <uint32_t RR, bool SIM, bool TOPO = false>
+template <uint32_t RR, bool SIM, bool TOPO = false, uint32_t NT = SIM ? FB_SIM : FB_MAX>
 static hipError_t ffd_attr(uint32_t lds_total) {
-  constexpr uint32_t NT = SIM ? FB_SIM : FB_MAX;
   hipFuncAttributes a;
   hipError_t e = hipFuncGetAttributes(&a, (const void*)ffd_kernel<RR, SIM, NT, TOPO>);
   if (e != hipSuccess) return e;
@@ -1876,7 +1887,11 @@ extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
                        ffd_attr<2, false, true>(lds_total), ffd_attr<3, false, true>(lds_total),
                        ffd_attr<4, false, true>(lds_total), ffd_attr<5, false, true>(lds_total),
                        ffd_attr<6, false, true>(lds_total), ffd_attr<7, false, true>(lds_total),
-                       ffd_attr<8, false, true>(lds_total)})
+                       ffd_attr<8, false, true>(lds_total), ffd_attr<1, true, false, FB_SIM_NARROW>(lds_total),
+                       ffd_attr<2, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<3, true, false, FB_SIM_NARROW>(lds_total),
+                       ffd_attr<4, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<5, true, false, FB_SIM_NARROW>(lds_total),
+                       ffd_attr<6, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<7, true, false, FB_SIM_NARROW>(lds_total),
+                       ffd_attr<8, true, false, FB_SIM_NARROW>(lds_total)})
     if (x != hipSuccess) e = x;
   return e;
 }
@@ -1885,13 +1900,17 @@ extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void) { return g_ffd_dyn_max; }
 
 // resident simulation workgroups per CU for a given dynamic LDS size
-extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds) {
+extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
+  const bool narrow = nt == (uint32_t)FB_SIM_NARROW;
   switch (R) {
-#define GSK_OCC(k) \
-  case k:                                                                                                    \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM, false>, FB_SIM, lds); \
+#define GSK_OCC(k)                                                                                              \
+  case k:                                                                                                       \
+    e = narrow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                  \
+                     &n, (const void*)ffd_kernel<k, true, FB_SIM_NARROW, false>, FB_SIM_NARROW, lds)            \
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM, false>, \
+                                                              FB_SIM, lds);                                     \
     break;
     GSK_OCC(1) GSK_OCC(2) GSK_OCC(3) GSK_OCC(4) GSK_OCC(5) GSK_OCC(6) GSK_OCC(7) GSK_OCC(8)
 #undef GSK_OCC
@@ -1906,12 +1925,17 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread
-  // shape: 0 provisioning, 1 provisioning with topology spread, 2 simulations
-  switch (d->R * 4 + (sim ? 2 : (d->TG || d->any_mv || d->any_vol ? 1 : 0))) {
+  // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations
+  if (sim && d->sim_nt != (uint32_t)FB_SIM && d->sim_nt != (uint32_t)FB_SIM_NARROW) return hipErrorInvalidValue;
+  const uint32_t shape = sim ? (d->sim_nt == (uint32_t)FB_SIM_NARROW ? 3u : 2u) : (d->TG || d->any_mv || d->any_vol ? 1u : 0u);
+  switch (d->R * 4 + shape) {
 #define GSK_CASE(n)                                                                                          \
   case 4 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
   case 4 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
-  case 4 * n + 2: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, false>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break;
+  case 4 * n + 2: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, false>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break; \
+  case 4 * n + 3:                                                                                            \
+    hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM_NARROW, false>), dim3(blocks), dim3(FB_SIM_NARROW), lds, s, *d); \
+    break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

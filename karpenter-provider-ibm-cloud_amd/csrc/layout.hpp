@@ -284,6 +284,7 @@ struct DevProblem {
   // NodeClaim per pod).  Existing nodes are the shared read-only nodes0/n_fk0
   // plus a per-block overlay of the nodes the simulation touched.
   uint32_t n_sims;
+  uint32_t sim_nt;             // threads per simulation workgroup (128 or 256)
   uint32_t ov_cap;             // overlay entries per block (candidates + pods of a simulation)
   uint32_t nb_words;           // ceil(NN / 32): LDS touched-node bitmap
   uint32_t n_pending;          // pod ids < n_pending are pending (their errors do not count)

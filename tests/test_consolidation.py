@@ -155,6 +155,26 @@ def test_gpu_consolidation_c4_scale_invariants(solver):
 
 
 @pytest.mark.gpu
+def test_gpu_consolidation_narrow_equals_wide(solver):
+    """5,000 simulations run in the 128-thread shape; each of 5 shards holds
+    1,000 (< 4 per CU) and runs the 256-thread shape (ffd.hip FB_SIM_NARROW,
+    consolidate.cpp plan_sims).  Mixed Delete / Replace / NoOp (bench c4_mixed)."""
+    p = synth.make_c4(n_nodes=5000, n_pending=0, util=(0.9, 0.99), full_frac=0.5, big_frac=1.0, pack=True)
+    cands = list(range(5000))
+    cin = ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_SINGLE)
+    whole, chosen, _, _ = solver.consolidate(cin)
+    assert {c["decision"] for c in whole} == {abi.DECISION_DELETE, abi.DECISION_REPLACE, abi.DECISION_NOOP}
+    for r in range(5):
+        part = solver.consolidate(ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_SINGLE, shard=(r, 5)))[0]
+        for i in range(r, 5000, 5):
+            assert part[i] == whole[i], i
+    sub = list(range(3, 5000, 500))
+    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, sub, mode=abi.CONSOLIDATE_SINGLE))
+    assert st == abi.GS_OK
+    assert [whole[i] for i in sub] == want
+
+
+@pytest.mark.gpu
 def test_gpu_consolidation_rerun_after_input_overwritten(solver):
     """gs_consolidate copies what the reruns need (no borrowed
     cluster / candidate pointers survive the call): scribbling over every
