@@ -17,6 +17,14 @@ struct Frame {
   int wb, wp;  // wasBalanced, wasPartitioned
 };
 
+// LDS-qualified element types: a pointer of these types keeps ds_* addressing
+// inside functions the compiler does not inline (WaveSort::pdqsort is one
+// out-of-line body shared by every wave-kernel instantiation; through a
+// generic pointer its LDS accesses become flat_* loads and stores)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) Frame lds_frame;
+
 __device__ __forceinline__ int bits_len(uint64_t x) { return x ? 64 - __clzll((long long)x) : 0; }
 
 // ---------------------------------------------------------------- sequential
@@ -39,7 +47,7 @@ struct SplitAcc {
   }
 };
 struct PackedAcc {
-  uint32_t* so;
+  lds_u32* so;
   __device__ __forceinline__ uint32_t key(int i) const { return so[i] & 0xFFFFu; }
   __device__ __forceinline__ void swap(int i, int j) const {
     const uint32_t a = so[i];

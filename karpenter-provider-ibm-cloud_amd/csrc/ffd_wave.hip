@@ -143,9 +143,9 @@ __device__ __forceinline__ uint64_t wave_swar_max(uint64_t x) {
 template <int SEQ>
 struct WaveSort {
   static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
-  uint32_t* so;
-  uint16_t* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
-  Frame* stk;
+  lds_u32* so;
+  lds_u16* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
+  lds_frame* stk;
   uint32_t lane, half;
 
   __device__ __forceinline__ uint32_t key(int i) const { return so[i] & 0xFFFFu; }
@@ -174,7 +174,7 @@ struct WaveSort {
   }
   // positions k in [lo,hi) with pred(k), ascending or descending, to out[]
   template <class Pred>
-  __device__ uint32_t compact(int lo, int hi, bool desc, uint16_t* out, Pred pred) const {
+  __device__ uint32_t compact(int lo, int hi, bool desc, lds_u16* out, Pred pred) const {
     uint32_t total = 0;
     const int n = hi - lo;
     for (int base = 0; base < n; base += 64 * RW) {
@@ -343,7 +343,7 @@ struct WaveSort {
     }
     wsync();
   }
-  __device__ void pdqsort(int n) const {
+  __device__ __forceinline__ void pdqsort_body(int n) const {
     const SeqSortP seq{{so}};
     if (n <= SEQ) {
       if (lane == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
@@ -401,7 +401,13 @@ struct WaveSort {
           child = Frame{mid + 1, f.b, f.limit, 1, 1};
           f.b = mid;
         }
-        if (lane == 0) stk[sp] = f;
+        if (lane == 0) {
+          stk[sp].a = f.a;
+          stk[sp].b = f.b;
+          stk[sp].limit = f.limit;
+          stk[sp].wb = f.wb;
+          stk[sp].wp = f.wp;
+        }
         wsync();
         sp++;
         f = child;
@@ -417,6 +423,16 @@ struct WaveSort {
     wsync();
   }
 };
+
+// The generic sort's one out-of-line body: the members arrive as scalar
+// arguments and the sorter is rebuilt locally, so they stay in registers (a
+// member function would reload them through a `this` pointer in scratch
+// after every LDS store)
+template <int SEQ>
+__device__ __noinline__ void wave_pdqsort(lds_u32* so, lds_u16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n) {
+  const WaveSort<SEQ> w{so, scr, stk, lane, half};
+  w.pdqsort_body(n);
+}
 
 // <U> Requirements.Compatible over the variant's free-key entries
 __device__ __forceinline__ bool fk_ok_range(const DevProblem& d, uint32_t fb, uint32_t fc, const FK* cfk, bool strict) {
@@ -592,8 +608,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   }
 
   // ======================================================== solver wave
-  const WaveSort<GS_WAVE_SEQ> ws{s_so, s_scr, s_stk, lane, MC / 2};
-  const PackedAcc acc{s_so};
+  const WaveSort<GS_WAVE_SEQ> ws{(lds_u32*)s_so, (lds_u16*)s_scr, (lds_frame*)s_stk, lane, MC / 2};
+  const PackedAcc acc{(lds_u32*)s_so};
   uint32_t wq_tail = 0;  // write requests posted
   // Infeasible-prefix hint: sorted positions [0, hint) hold NodeClaims that
   // cannot take a pod with requests >= s_hint_rq (resources 0..3) that
@@ -851,7 +867,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
       if (inversion) {
         if (M <= 12) {
-          if (lane == 0) SeqSortP{{s_so}}.insertion_sort(0, (int)M);
+          if (lane == 0) SeqSortP{{(lds_u32*)s_so}}.insertion_sort(0, (int)M);
           wsync();
           hint_ok = false;
         } else if (M >= 50 && (!pivot_touched(modkind, modpos, M) || pivot_hint_wave(acc, (int)M, lane) == 1)) {
@@ -879,7 +895,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         } else {
           CTR(C_GEN, 1);
-          ws.pdqsort((int)M);
+          wave_pdqsort<GS_WAVE_SEQ>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
           hint_ok = false;
         }
       }
