@@ -1943,43 +1943,3 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   }
   return hipGetLastError();
 }
-
-// ------------------------------------------------ autoplacement ranking sort
-// gs_rank_instance_types (rank.hip) sorts its kept instance types with the
-// block-parallel sort.Slice restatement above.  keys[k] = how many kept
-// scores are strictly below score k: the same Less outcomes as the float64
-// compare (NaN refused on the host), so the permutation is the reference's.
-// pos[k] = compacted position; both sorted in place.  *np = the kept count
-// (written by rank_kernel on the same stream); cap bounds it (<= GS_RANK_MAX).
-#ifndef GS_RANK_SEQ
-#define GS_RANK_SEQ 32
-#endif
-constexpr int RANK_SEQ = GS_RANK_SEQ;
-extern "C" __global__ __launch_bounds__(FB_MAX) void rank_sort_kernel(uint16_t* keys, uint16_t* pos,
-                                                                      const uint32_t* np, uint32_t cap) {
-  __shared__ Shared S;
-  extern __shared__ uint16_t rs_lds[];  // sc[cap] | ord[cap] | scr[cap + 2]
-  const uint32_t n = __builtin_amdgcn_readfirstlane(*np <= cap ? *np : 0u);
-  uint16_t* sc = rs_lds;
-  uint16_t* ord = rs_lds + cap;
-  uint16_t* scr = rs_lds + 2 * cap;
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t k = tid; k < n; k += FB_MAX) {
-    sc[k] = keys[k];
-    ord[k] = pos[k];
-  }
-  __syncthreads();
-  Blk<FB_MAX, RANK_SEQ> blk{sc, ord, scr, S, tid, tid & 63, tid >> 6, 0, (n + 1) / 2};
-  blk.pdqsort((int)n);
-  __syncthreads();
-  for (uint32_t k = tid; k < n; k += FB_MAX) {
-    keys[k] = sc[k];
-    pos[k] = ord[k];
-  }
-}
-
-extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, hipStream_t s) {
-  const size_t lds = (size_t)(3 * cap + 2) * sizeof(uint16_t);
-  hipLaunchKernelGGL(rank_sort_kernel, dim3(1), dim3(FB_MAX), lds, s, keys, pos, np, cap);
-  return hipGetLastError();
-}

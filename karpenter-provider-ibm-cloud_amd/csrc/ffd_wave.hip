@@ -1651,3 +1651,35 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
   }
   return hipGetLastError();
 }
+
+// ------------------------------------------------ autoplacement ranking sort
+// gs_rank_instance_types (rank.hip) sorts its kept instance types with the
+// single-wave sort.Slice restatement above (WaveSort: every partition step a
+// ballot, no workgroup barrier).  keys[k] = how many kept scores are strictly
+// below score k: the same Less outcomes as the float64 compare (NaN refused
+// on the host), so the permutation is the reference's.  pos[k] = compacted
+// position; both sorted in place.  *np = the kept count (written by
+// rank_kernel on the same stream); cap bounds it (<= GS_RANK_MAX).
+extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys, uint16_t* pos, const uint32_t* np,
+                                                                  uint32_t cap) {
+  extern __shared__ uint32_t rs_lds[];  // so[cap] (key | position << 16) | scr u16[cap + 2]
+  __shared__ Frame rs_stk[64];
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*np <= cap ? *np : 0u);
+  const uint32_t lane = threadIdx.x;
+  lds_u32* so = (lds_u32*)rs_lds;
+  lds_u16* scr = (lds_u16*)(rs_lds + cap);
+  for (uint32_t k = lane; k < n; k += 64) so[k] = (uint32_t)keys[k] | ((uint32_t)pos[k] << 16);
+  wsync();
+  wave_pdqsort<GS_WAVE_SEQ>(so, scr, (lds_frame*)rs_stk, lane, (n + 1) / 2, (int)n);
+  for (uint32_t k = lane; k < n; k += 64) {
+    const uint32_t x = so[k];
+    keys[k] = (uint16_t)(x & 0xFFFFu);
+    pos[k] = (uint16_t)(x >> 16);
+  }
+}
+
+extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, hipStream_t s) {
+  const size_t lds = (size_t)cap * sizeof(uint32_t) + (size_t)(cap + 2) * sizeof(uint16_t);
+  hipLaunchKernelGGL(rank_sort_kernel, dim3(1), dim3(64), lds, s, keys, pos, np, cap);
+  return hipGetLastError();
+}

@@ -11,9 +11,9 @@
 //      rank_key_kernel (grid-wide) gives each kept score a u16 key = how many
 //      kept scores are strictly below it (ties share a key, so every Less
 //      outcome is the float64 one);
-//   2. rank_sort_kernel (ffd.hip) runs the block-parallel restatement of Go's
-//      sort.Slice (pdqsort_func) that orders in-flight NodeClaims, on
-//      (key, position) pairs in LDS;
+//   2. rank_sort_kernel (ffd_wave.hip) runs the single-wave restatement of
+//      Go's sort.Slice (pdqsort_func) that orders in-flight NodeClaims, on
+//      (key, position) pairs packed in LDS;
 //   3. rank_gather_kernel writes the ranked List indices and scores.
 // The work is latency-bound (a single launch over <= 4096 types: 12 B per
 // type in, 12 B out); there is nothing here for MFMA or the HBM roofline.
@@ -102,18 +102,23 @@ __global__ __launch_bounds__(RK_NT) void rank_kernel(RankArgs a) {
 
 // sort keys: key[k] = how many kept scores are strictly below score k (ties
 // share a key; key order == float64 order), payload the compacted position.
-// Workgroup b owns k in [64b, 64b + 64) (lane = k); its 4 waves split the j
-// range and add their partial counts in LDS.  The score read is wave-uniform.
+// Workgroup b owns k in [64b, 64b + 64) (lane = k); it stages every kept
+// score in LDS with one coalesced pass, its 4 waves split the j range (a
+// broadcast LDS read per j) and add their partial counts in LDS.
 __global__ __launch_bounds__(RK_NT) void rank_key_kernel(RankArgs a) {
+  extern __shared__ double rk_all[];  // [kept] scores
   __shared__ uint32_t part[RK_NWAVE][64];
   const uint32_t kept = *a.out_n;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t k = blockIdx.x * 64u + lane;
-  const double x = k < kept ? a.cscore[k] : 0.0;
+  for (uint32_t j = threadIdx.x; j < kept; j += RK_NT) rk_all[j] = a.cscore[j];
+  __syncthreads();
+  const double x = k < kept ? rk_all[k] : 0.0;
   const uint32_t per = (kept + RK_NWAVE - 1) / RK_NWAVE;
   const uint32_t j0 = wave * per, j1 = j0 + per < kept ? j0 + per : kept;
   uint32_t below = 0;
-  for (uint32_t j = j0; j < j1; j++) below += a.cscore[j] < x;
+#pragma unroll 8
+  for (uint32_t j = j0; j < j1; j++) below += rk_all[j] < x;
   part[wave][lane] = below;
   __syncthreads();
   if (wave == 0 && k < kept) {
@@ -206,7 +211,7 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   const size_t lds = nn * (sizeof(double) + sizeof(uint32_t));
   if (hipMemcpy(d, hin.data(), in_bytes, hipMemcpyHostToDevice) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(RK_NT), lds, 0, a);
-  hipLaunchKernelGGL(rank_key_kernel, dim3((n + 63) / 64), dim3(RK_NT), 0, 0, a);
+  hipLaunchKernelGGL(rank_key_kernel, dim3((n + 63) / 64), dim3(RK_NT), nn * sizeof(double), 0, a);
   if (hipGetLastError() != hipSuccess || gsk_rank_sort(a.keys, a.pos, a.out_n, n, 0) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_gather_kernel, dim3((n + RK_NT - 1) / RK_NT), dim3(RK_NT), 0, 0, a);
   if (hipGetLastError() != hipSuccess ||
