@@ -927,9 +927,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #endif
 
     // --------------------------- in-flight NodeClaims, first that CanAdd wins
-    // Phase A walks the sorted positions in LDS, four 64-position chunks per
-    // step, with the necessary test (template tolerated, request code <=
-    // slack code per resource) and, for simple pods, the sufficient test
+    // Phase A walks the sorted positions in LDS, one 64-position chunk per
+    // step (2 or 4 chunks per step measured slower:
+    // profiles/r2/ffd_scan_width_ab.txt), with the necessary test (template
+    // tolerated, request code <= slack code per resource) and, for simple
+    // pods, the sufficient test
     // (request code <= room code: CanAdd holds without reading the claim).
     // It stops at the first fast accept, collecting every candidate before it
     // that needs the exact check (at most 64 per batch).  Phase B runs the
