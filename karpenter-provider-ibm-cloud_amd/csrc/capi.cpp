@@ -36,7 +36,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     d.max_claims = std::max<uint32_t>(sims->max_pods, 1);
   } else {
     // NodeClaims the LDS holds next to the thresholds and topology state
-    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, e.TG) + 8;
+    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) + 8;
     const uint32_t dyn = std::min(gsk_ffd_dyn_lds_max(), gsk_ffdw_dyn_lds_max());
     const uint32_t fit = dyn > other ? (dyn - other) / 23 : 0;
     d.max_claims = std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
@@ -105,12 +105,14 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   // topology spread groups
   d.TG = e.TG;
   d.TGH = e.TGH;
+  d.TGZ = e.TGZ;
+  d.ZS = e.ZS;
   d.NZV = e.NZV;
-  d.tg_zone = e.tg_zone;
-  d.tg_host = e.tg_host;
-  d.tg_aff = e.tg_aff;
+  d.zknown0 = e.zknown0;
   c->upload(d.tgroups, e.tgroups);
-  c->upload(d.tg_cnt0, e.tg_cnt0);
+  c->upload(d.tg_list, e.tg_list);
+  c->upload(d.zcnt0, e.zcnt0);
+  c->upload(d.htot0, e.htot0);
   c->upload(d.zone_order, e.zone_order);
   c->upload(d.zone_cat, e.zone_cat);
   c->upload(d.hn0, e.hn0);

@@ -20,7 +20,7 @@ extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
 extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt);
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
-                                      uint32_t TG);
+                                      uint32_t topo_bytes);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
                                hipStream_t s);
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);

@@ -680,9 +680,9 @@ struct Ctx {
       return h;
     }
   };
-  // <U> corev1.PodAffinityTerm of podAntiAffinity (hostname key)
+  // <U> corev1.PodAffinityTerm of pod (anti-)affinity (hostname or zone key)
   struct AntiEnc {
-    SpreadEnc sel;              // has_sel / ml / ex
+    SpreadEnc sel;              // key / has_sel / ml / ex
     std::set<std::string> nss;  // the term's namespaces, else the pod's
     bool required = false;
     int32_t weight = 0;
@@ -690,7 +690,7 @@ struct Ctx {
       return nss.count(ns) && sel.matches(labels);
     }
     std::string hash() const {
-      std::string h = "anti|" + std::string(sel.has_sel ? "1" : "0");
+      std::string h = "anti|" + sel.key + "|" + std::string(sel.has_sel ? "1" : "0");
       for (auto& n : nss) h += "|n:" + n;
       for (auto& kv : sel.ml) h += "|l:" + kv.first + "=" + kv.second;
       for (auto& x : sel.ex) {
@@ -798,18 +798,22 @@ struct Ctx {
     }
     return out;
   }
-  std::vector<AntiEnc> antis_of(const gs_pod& pd) const { return terms_of(pd, pd.anti_affinity); }
-  std::vector<AntiEnc> terms_of(const gs_pod& pd, gs_range rg) const {
+  std::vector<AntiEnc> antis_of(const gs_pod& pd) const { return terms_of(pd, pd.anti_affinity, false); }
+  // zone-key anti-affinity is deterministic (every empty zone both sides
+  // allow); zone-key pod affinity bootstraps on a zone picked in Go map order
+  std::vector<AntiEnc> terms_of(const gs_pod& pd, gs_range rg, bool affinity) const {
     chk(rg, p->n_affinity_terms, "affinity_terms");
     std::vector<AntiEnc> out;
     for (uint32_t k = 0; k < rg.count; k++) {
       const gs_affinity_term& q = p->affinity_terms[rg.begin + k];
-      if (normalize(S(q.topology_key)) != kHostname)
-        throw Fail{GS_E_UNSUPPORTED, "pod (anti-)affinity topologyKey other than hostname"};
+      const std::string tk = normalize(S(q.topology_key));
+      if (tk != kHostname && !(tk == kZone && !affinity))
+        throw Fail{GS_E_UNSUPPORTED, affinity ? "pod affinity topologyKey other than hostname"
+                                              : "pod anti-affinity topologyKey other than hostname / zone"};
       AntiEnc a;
       a.required = q.required != 0;
       a.weight = q.weight;
-      a.sel.key = kHostname;
+      a.sel.key = tk;
       a.sel.has_sel = q.has_selector != 0;
       a.sel.ml = label_map(q.match_labels);
       chk(q.match_expressions, p->n_reqs, "reqs");
@@ -893,20 +897,60 @@ struct Ctx {
   uint32_t group_id(const std::string& h, GroupEnc&& g) {
     auto f = group_idx.find(h);
     if (f == group_idx.end()) {
+      if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
       f = group_idx.emplace(h, (uint32_t)groups.size()).first;
       groups.push_back(std::move(g));
     }
-    if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology groups"};
     return f->second;
   }
-  // a hostname group admitting an owner only where the count is 0
-  GroupEnc host_group(int kind, bool self) const {
+  // a group admitting an owner only where the count is 0: on the hostname key
+  // through count + self <= skew = self; on the zone key (anti-affinity and
+  // its inverse) the domains with count 0 (TK_ANTI)
+  GroupEnc host_group(int kind, bool self, const std::string& key = kHostname) const {
     GroupEnc g;
     g.kind = kind;
-    g.sp.key = kHostname;
+    g.sp.key = key;
     g.sp.skew = self ? 1 : 0;
     return g;
   }
+
+  // Candidate groups of a pod for group_counts: each group is filed under
+  // one thing a counted pod must carry (a matchLabels pair, a carried term,
+  // a host port's protocol and number); groups with no such anchor are
+  // checked for every pod, and nil selectors select nothing
+  struct SelIndex {
+    std::unordered_map<std::string, std::vector<uint32_t>> by;
+    std::vector<uint32_t> generic;
+    explicit SelIndex(const std::vector<GroupEnc>& gs) {
+      for (uint32_t g = 0; g < gs.size(); g++) {
+        const GroupEnc& x = gs[g];
+        if (x.kind == 2) {
+          by["C" + x.inv_hash].push_back(g);
+        } else if (x.kind == 3) {
+          by["P" + x.port.proto + "|" + std::to_string(x.port.port)].push_back(g);
+        } else {
+          const SpreadEnc& sel = x.kind == 0 ? x.sp : x.anti.sel;
+          if (!sel.has_sel) continue;
+          if (!sel.ml.empty()) by["L" + sel.ml.begin()->first + "=" + sel.ml.begin()->second].push_back(g);
+          else generic.push_back(g);
+        }
+      }
+    }
+    void candidates(const PodSel& ps, std::vector<uint32_t>* out) const {
+      *out = generic;
+      auto add = [&](const std::string& k) {
+        auto f = by.find(k);
+        if (f != by.end()) out->insert(out->end(), f->second.begin(), f->second.end());
+      };
+      if (!by.empty()) {
+        for (auto& kv : ps.labels) add("L" + kv.first + "=" + kv.second);
+        for (auto& h : ps.carried) add("C" + h);
+        for (auto& pe : ps.ports) add("P" + pe.proto + "|" + std::to_string(pe.port));
+      }
+      std::sort(out->begin(), out->end());
+      out->erase(std::unique(out->begin(), out->end()), out->end());
+    }
+  };
 
   // <U> VolumeUsage (ExistingNode.CanAdd's ExceedsLimits): per node the
   // distinct volumes of its bound pods per driver and the CSINode limits; a
@@ -970,17 +1014,18 @@ struct Ctx {
 
   // <U> NewTopology: domain universe (In values of NodePool requirements of
   // NodePools that have instance types, existing nodes' labels) and the
-  // counts of the selected bound pods; selection masks per pod
+  // counts of the selected bound pods; per variant the owned-group list, per
+  // pod the selection list (layout.hpp VarRec own_off / sel_off)
   void build_topology() {
     e.TG = (uint32_t)groups.size();
     if (!e.TG) return;
-    if (e.TG > (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups"};
     const Vocab& zv = e.keys[e.k_zone].vocab;
     bool any_zone = false;
     for (auto& g : groups) any_zone = any_zone || g.sp.key == kZone;
     if (any_zone && zv.size() > (size_t)gsd::ZVMAX)
-      throw Fail{GS_E_UNSUPPORTED, "zone topology spread over more than 63 zone values"};
+      throw Fail{GS_E_UNSUPPORTED, "zone topology groups over more than 63 zone values"};
     e.NZV = (uint32_t)std::min<size_t>(zv.size() - 1, gsd::ZVMAX);
+    e.ZS = std::max<uint32_t>(e.NZV, 1);
     e.zone_order.resize(e.NZV);
     std::iota(e.zone_order.begin(), e.zone_order.end(), 0);
     std::sort(e.zone_order.begin(), e.zone_order.end(), [&](uint32_t a, uint32_t b) { return zv.vals[a] < zv.vals[b]; });
@@ -993,53 +1038,87 @@ struct Ctx {
       auto f = u.first.find(e.k_zone);
       if (f != u.first.end() && !f->second.comp) known_zone |= f->second.has.w[0];  // operator In
     }
+    e.known_np = known_zone;
+    e.zone_nodes.assign(gsd::ZVMAX, 0);
     for (auto& nr : e.nodes)
-      if (nr.zvid != gsd::NONE && nr.zvid < (uint32_t)gsd::ZVMAX) known_zone |= 1ull << nr.zvid;
+      if (nr.zvid != gsd::NONE && nr.zvid < e.ZS) {
+        known_zone |= 1ull << nr.zvid;
+        e.zone_nodes[nr.zvid]++;
+      }
+    e.zknown0 = known_zone;
     e.tgroups.assign(e.TG, gsd::TGroupRec{});
-    e.tg_cnt0.assign((size_t)e.TG * gsd::ZVMAX, 0);
     for (uint32_t g = 0; g < e.TG; g++) {
       gsd::TGroupRec& t = e.tgroups[g];
       t.skew = groups[g].sp.skew;
       t.mind = groups[g].sp.mind;
-      t.host = groups[g].sp.key == kHostname ? 1u : 0u;
-      if (t.host) {
-        t.hslot = e.TGH++;
-        e.tg_host |= 1ull << g;
-        if (groups[g].kind == 4) e.tg_aff |= 1ull << g;
+      const int kind = groups[g].kind;
+      if (groups[g].sp.key == kHostname) {
+        t.kind = gsd::TK_HOST | (kind == 4 ? gsd::TK_AFF : 0u);
+        t.slot = e.TGH++;
       } else {
+        t.kind = kind == 1 || kind == 2 ? gsd::TK_ANTI : 0u;
+        t.slot = e.TGZ++;
         t.known0 = known_zone;
-        e.tg_zone |= 1ull << g;
       }
     }
+    if (gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH) > 64u * 1024u)
+      throw Fail{GS_E_UNSUPPORTED, "topology group state exceeds 64 KiB of LDS (zone groups x zones)"};
+    e.zcnt0.assign((size_t)std::max<uint32_t>(e.TGZ, 1) * e.ZS, 0);
+    e.htot0.assign(std::max<uint32_t>(e.TGH, 1), 0);
     e.hn0.assign((size_t)std::max<uint32_t>(e.TGH, 1) * std::max<uint32_t>(e.NN, 1), 0);
+    e.zn_cnt.assign((size_t)std::max<uint32_t>(e.TGZ, 1) * std::max<uint32_t>(e.NN, 1), 0);
     std::vector<uint32_t> pos_of(e.NN);
     for (uint32_t i = 0; i < e.NN; i++) pos_of[e.node_order[i]] = i;
     if (p->n_bound_pods && !p->bound_pod_node) throw Fail{GS_E_INVALID, "bound pods without their nodes"};
+    SelIndex six(groups);
+    std::vector<uint32_t> cand;
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
       const gs_pod& bp = p->bound_pods[b];
       if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
       const uint32_t pos = pos_of[p->bound_pod_node[b]];
       const PodSel ps = sel_of(bp);
-      for (uint32_t g = 0; g < e.TG; g++) {
+      six.candidates(ps, &cand);
+      for (uint32_t g : cand) {
         if (!group_counts(groups[g], ps)) continue;
         gsd::TGroupRec& t = e.tgroups[g];
-        if (t.host) {
-          e.hn0[(size_t)t.hslot * e.NN + pos]++;
-          e.tg_cnt0[(size_t)g * gsd::ZVMAX]++;  // hostname groups: the total over domains (affinity bootstrap)
+        if (t.kind & gsd::TK_HOST) {
+          e.hn0[(size_t)t.slot * e.NN + pos]++;
+          e.htot0[t.slot]++;  // the total over domains (affinity bootstrap)
         } else {
           const uint32_t z = e.nodes[pos].zvid;
-          if (z == gsd::NONE || z >= (uint32_t)gsd::ZVMAX) continue;
-          e.tg_cnt0[(size_t)g * gsd::ZVMAX + z]++;
+          if (z == gsd::NONE || z >= e.ZS) continue;
+          e.zcnt0[(size_t)t.slot * e.ZS + z]++;
+          e.zn_cnt[(size_t)t.slot * e.NN + pos]++;
           t.known0 |= 1ull << z;
         }
       }
     }
-    for (uint32_t i = 0; i < e.P && e.TG; i++) {
-      uint64_t sel = 0;
-      for (uint32_t g = 0; g < e.TG; g++)
-        if (group_counts(groups[g], pod_sel[i])) sel |= 1ull << g;
-      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) e.vars[v].t_sel = sel;
+    // per pod: the selection list (shared by its variants), then each
+    // variant's own list with the self flag
+    e.tg_list.clear();
+    std::vector<uint8_t> selected(e.TG, 0);
+    std::vector<uint32_t> mine;
+    for (uint32_t i = 0; i < e.P; i++) {
+      six.candidates(pod_sel[i], &cand);
+      mine.clear();
+      for (uint32_t g : cand)
+        if (group_counts(groups[g], pod_sel[i])) mine.push_back(g);
+      const uint32_t so = (uint32_t)e.tg_list.size();
+      for (uint32_t g : mine) {
+        selected[g] = 1;
+        e.tg_list.push_back(e.tgroups[g].slot | (e.tgroups[g].kind << 24));
+      }
+      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
+        gsd::VarRec& vr = e.vars[v];
+        vr.sel_off = so;
+        vr.sel_n = (uint32_t)mine.size();
+        vr.own_off = (uint32_t)e.tg_list.size();
+        for (uint32_t g : e.variants[v].own) e.tg_list.push_back(g | (selected[g] ? gsd::TL_SELF : 0u));
+        vr.own_n = (uint32_t)e.variants[v].own.size();
+      }
+      for (uint32_t g : mine) selected[g] = 0;
     }
+    if (e.tg_list.empty()) e.tg_list.push_back(0);
   }
 
   // CT_SPOT | CT_OD: Requirement.Has("spot") / Has("on-demand") of the
@@ -1351,33 +1430,33 @@ struct Ctx {
         const std::string h = sp.hash(pod_ns.back());
         auto f = group_idx.find(h);
         if (f == group_idx.end()) {
+          if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
           f = group_idx.emplace(h, (uint32_t)groups.size()).first;
           groups.push_back(GroupEnc{sp, pod_ns.back()});
         }
-        if (f->second >= (uint32_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology groups"};
         sgid.push_back(f->second);
       }
       std::vector<uint32_t> cur(sps.size());  // current constraints (swap-remove order)
       std::iota(cur.begin(), cur.end(), 0);
       // anti-affinity, inverse anti-affinity and host-port groups
-      uint64_t own_static = 0;
+      std::vector<uint32_t> own_static;
       std::vector<std::pair<int32_t, uint32_t>> anti_pref, aff_pref;  // (weight, group)
       if (topo_inputs) {
       const PodSel& me = pod_sel[i];
       for (auto& a : antis_of(pd)) {
         const bool self = a.selects(me.ns, me.labels);
-        GroupEnc g = host_group(1, self);
+        GroupEnc g = host_group(1, self, a.sel.key);
         g.anti = a;
         const uint32_t gid = group_id("A|" + a.hash() + (self ? "|s" : "|n"), std::move(g));
-        if (a.required) own_static |= 1ull << gid;
+        if (a.required) own_static.push_back(gid);
         else anti_pref.push_back({a.weight, gid});
       }
       if (anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
-      for (auto& a : terms_of(pd, pd.affinity)) {
+      for (auto& a : terms_of(pd, pd.affinity, true)) {
         GroupEnc g = host_group(4, false);
         g.anti = a;
         const uint32_t gid = group_id("F|" + a.hash(), std::move(g));
-        if (a.required) own_static |= 1ull << gid;
+        if (a.required) own_static.push_back(gid);
         else aff_pref.push_back({a.weight, gid});
       }
       if (aff_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
@@ -1387,14 +1466,14 @@ struct Ctx {
       for (auto& kv : inv_terms) {
         if (!kv.second.selects(me.ns, me.labels)) continue;
         const bool self = me.carried.count(kv.first) != 0;
-        GroupEnc g = host_group(2, self);
+        GroupEnc g = host_group(2, self, kv.second.sel.key);
         g.inv_hash = kv.first;
-        own_static |= 1ull << group_id("I|" + kv.first + (self ? "|s" : "|n"), std::move(g));
+        own_static.push_back(group_id("I|" + kv.first + (self ? "|s" : "|n"), std::move(g)));
       }
       for (auto& pe : me.ports) {
         GroupEnc g = host_group(3, true);
         g.port = pe;
-        own_static |= 1ull << group_id("P|" + pe.key(), std::move(g));
+        own_static.push_back(group_id("P|" + pe.key(), std::move(g)));
       }
       }
       chk(pd.tolerations, p->n_tolerations, "tolerations");
@@ -1416,10 +1495,13 @@ struct Ctx {
           reqs_add_all(e, v.strict, req_terms[ri]);
         }
         v.tol = tol_mask(tols);
-        for (uint32_t k : cur) v.own |= 1ull << sgid[k];
-        v.own |= own_static;
-        for (size_t k = ai; k < anti_pref.size(); k++) v.own |= 1ull << anti_pref[k].second;
-        for (size_t k = fi; k < aff_pref.size(); k++) v.own |= 1ull << aff_pref[k].second;
+        for (uint32_t k : cur) v.own.push_back(sgid[k]);
+        v.own.insert(v.own.end(), own_static.begin(), own_static.end());
+        for (size_t k = ai; k < anti_pref.size(); k++) v.own.push_back(anti_pref[k].second);
+        for (size_t k = fi; k < aff_pref.size(); k++) v.own.push_back(aff_pref[k].second);
+        std::sort(v.own.begin(), v.own.end());
+        v.own.erase(std::unique(v.own.begin(), v.own.end()), v.own.end());
+        if (v.own.size() > (size_t)gsd::OWNMAX) throw Fail{GS_E_UNSUPPORTED, "a pod owns more than 64 topology groups"};
         e.variants.push_back(std::move(v));
         variant_tols.push_back(tols);
         // <U> Preferences.Relax
@@ -1509,8 +1591,7 @@ struct Ctx {
         }
         vr.zm = zone_has(pv.reqs);
         vr.cm = ct_has(pv.reqs);
-        vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && !pv.own ? gsd::VF_SIMPLE : 0u);
-        vr.t_own = pv.own;
+        vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && pv.own.empty() ? gsd::VF_SIMPLE : 0u);
         vr.zs = zone_full(pv.strict);
         vr.zn = zone_full(pv.reqs);
         vr.zflags = zone_flags(pv.reqs);

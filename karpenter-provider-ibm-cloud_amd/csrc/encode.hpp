@@ -80,7 +80,7 @@ struct PodVariant {
   Reqs reqs;
   Reqs strict;      // PodData.StrictRequirements: no preferred term (topology podDomains)
   uint64_t tol = 0;
-  uint64_t own = 0; // topology spread groups owned (after relaxations)
+  std::vector<uint32_t> own;  // topology groups owned (after relaxations), ascending ids
 };
 
 struct Encoded {
@@ -129,14 +129,22 @@ struct Encoded {
   std::vector<uint32_t> node_order;  // device position -> gs_problem node index
   std::vector<gsd::NodeRec> nodes;
   std::vector<gsd::FK> n_fk;
-  // topology spread (layout.hpp DevProblem topology fields)
-  uint32_t TG = 0, TGH = 0, NZV = 0;
-  uint64_t tg_zone = 0, tg_host = 0, tg_aff = 0;  // tg_aff: hostname pod-affinity groups
+  // topology groups (layout.hpp DevProblem topology fields)
+  uint32_t TG = 0, TGH = 0, TGZ = 0, NZV = 0, ZS = 1;
   std::vector<gsd::TGroupRec> tgroups;
-  std::vector<int32_t> tg_cnt0;      // [TG][64]
+  std::vector<uint32_t> tg_list;     // own / selection list arena
+  std::vector<int32_t> zcnt0;        // [TGZ][ZS]
+  std::vector<int32_t> htot0;        // [TGH]
   std::vector<uint32_t> zone_order;  // zone vocabulary ids by name
   std::vector<uint32_t> zone_cat;    // [64]
   std::vector<int32_t> hn0;          // [TGH][NN]
+  // consolidation: per zone group, the counted bound pods on each node
+  // [TGZ][NN] (a simulation subtracts its candidates' pods), the domains the
+  // NodePools contribute, and the number of nodes per zone value
+  std::vector<int32_t> zn_cnt;
+  uint64_t known_np = 0;
+  uint64_t zknown0 = 0;              // layout.hpp DevProblem::zknown0
+  std::vector<int32_t> zone_nodes;   // [64]
   // host-only, for decode
   std::vector<Reqs> tmpl_reqs;  // incl. hostname In[omega]
   std::vector<PodVariant> variants;

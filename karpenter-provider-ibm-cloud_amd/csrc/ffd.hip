@@ -598,11 +598,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
-  // topology spread: zone-domain counts [TG][64], known domains, per-pod minimum counts
+  // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + d.ov_cap * 4u + 7u) & ~7u;
-  uint64_t* s_known = (uint64_t*)((char*)lds64 + tg_off);
-  int64_t* s_tmin = (int64_t*)(s_known + d.TG);
-  int32_t* s_zcnt = (int32_t*)(s_tmin + d.TG);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
   Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
   Wg<NT> wg{&S.red2[0][0], s_sc, s_ord, tid, tid & 63, tid >> 6, 0};
 
@@ -650,8 +648,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
     for (uint32_t i = tid; i < T * R; i += FB) t_rem[i] = d.tmpl[i / R].limits[i % R];
     if (TOPO) {
       // <U> Topology: counts before the Solve (selected bound pods)
-      for (uint32_t i = tid; i < d.TG * ZVMAX; i += FB) s_zcnt[i] = d.tg_cnt0[i];
-      for (uint32_t g = tid; g < d.TG; g += FB) s_known[g] = d.tgroups[g].known0;
+      topo_init(d, ts, d.zknown0, tid, FB);
       for (uint32_t i = tid; i < d.TGH * d.NN; i += FB) d.hn[i] = d.hn0[i];
     }
     uint32_t ncand = 0;
@@ -870,23 +867,13 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
 
       // <U> Topology.AddRequirements, per pod: the minimum domain count of every
       // zone group the pod owns over its strict zone domains (domainMinCount)
-      const uint64_t own = TOPO ? vr.t_own : 0;  // topology spread groups the pod owns
-      if (TOPO && own) {
-        if (tid < 64 && ((own & d.tg_zone) >> tid) & 1) {
-          const uint64_t cand = s_known[tid] & vr.zs;
-          int64_t mn = INT32_MAX;
-          int32_t n = 0;
-          for (uint64_t m = cand; m; m &= m - 1) {
-            n++;
-            const int64_t c = s_zcnt[tid * ZVMAX + (uint32_t)__ffsll((long long)m) - 1];
-            mn = c < mn ? c : mn;
-          }
-          if (d.tgroups[tid].mind && n < d.tgroups[tid].mind) mn = 0;
-          s_tmin[tid] = mn;
-        }
+      // topology: the groups the pod owns (own list) and that count it (selection list)
+      const uint32_t own_n = TOPO ? vr.own_n : 0u, own_off = TOPO ? vr.own_off : 0u;
+      const uint32_t sel_n = TOPO ? vr.sel_n : 0u, sel_off = TOPO ? vr.sel_off : 0u;
+      if (TOPO && own_n) {
+        if (tid < 64) topo_tmin(d, ts, own_off, own_n, vr.zs, tid);
         __syncthreads();
       }
-      const uint64_t tself = own & vr.t_sel;  // self-selecting groups
 
       // --------------- existing nodes in order: first ExistingNode.CanAdd wins
       if (d.NN) {
@@ -933,21 +920,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (feas && vr.cfull_off != NONE)
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
-            if (TOPO && feas && own) {
-              // zone groups: the node's own zone is the only candidate domain
-              // (a node without the label fails the strict Compatible)
-              for (uint64_t m = own & d.tg_zone; m && feas; m &= m - 1) {
-                const uint32_t g = __ffsll((long long)m) - 1, z = nr.zvid;
-                feas = z < (uint32_t)ZVMAX && ((s_known[g] >> z) & 1) &&
-                       (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= d.tgroups[g].skew;
-              }
-              // hostname groups: min count 0
-              for (uint64_t m = own & d.tg_host; m && feas; m &= m - 1) {
-                const uint32_t g = __ffsll((long long)m) - 1;
-                const int64_t c = d.hn[(size_t)d.tgroups[g].hslot * d.NN + n], self = (int64_t)((tself >> g) & 1);
-                feas = ((d.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= d.tgroups[g].skew;
-              }
-            }
+            if (TOPO && feas && own_n)
+              feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid,
+                                  [&](uint32_t hs) -> int64_t { return d.hn[(size_t)hs * d.NN + n]; });
             if (TOPO && feas && d.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
               const NodeVol& nv = d.n_vol[n];
@@ -1017,18 +992,10 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             logp[HN.nlog++] = LogRec{gp, v, fn | 0x80000000u, 0};
             S.found = 1;
             // <U> Topology.Record: the node's labels are single domains
-            for (uint64_t m = TOPO ? vr.t_sel : 0; m; m &= m - 1) {
-              const uint32_t g = __ffsll((long long)m) - 1;
-              if ((d.tg_host >> g) & 1) {
-                d.hn[(size_t)d.tgroups[g].hslot * d.NN + fn]++;
-                s_zcnt[g * ZVMAX]++;  // hostname groups: the total
-              } else {
-                const uint32_t z = d.nodes0[fn].zvid;
-                if (z < (uint32_t)ZVMAX) {
-                  s_zcnt[g * ZVMAX + z]++;
-                  s_known[g] |= 1ull << z;
-                }
-              }
+            if (TOPO && sel_n) {
+              const uint32_t z = d.nodes0[fn].zvid;
+              topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
+                          [&](uint32_t hs) { d.hn[(size_t)hs * d.NN + fn]++; });
             }
           }
           pf_stage2();
@@ -1163,7 +1130,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         uint32_t j = 0, t = 0;
         uint64_t G = 0, Gt = 0;
         uint64_t zm = 0, cm = 0;  // the NodeClaim's catalog zone / capacity-type masks
-        uint32_t tz = NONE;  // zone domain topology spread picked for this NodeClaim
+        uint64_t zset = ~0ull;  // zone domains topology allows on this NodeClaim (~0: unconstrained)
         uint64_t czf = 0;    // the NodeClaim's zone Has / flags (read only under topology)
         uint32_t czfl = 0;
         uint32_t mrow[RR];
@@ -1258,43 +1225,15 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             c1 = __builtin_amdgcn_s_memtime();
 #endif
             if (pre && vr.fk_count) pre = var_fk_ok(dd, vr, dd.c_fk + (size_t)(cb + j) * F);
-            if (TOPO && pre && own) {
-              // <U> Topology.AddRequirements on the NodeClaim: every owned zone
-              // group picks the minimum-count known domain within maxSkew among
-              // the NodeClaim's (claim AND pod) zone domains, ties by name; the
-              // picks must agree.  Hostname groups: this NodeClaim's count.
+            if (TOPO && pre && own_n) {
+              // <U> Topology.AddRequirements on the NodeClaim over its (claim
+              // AND pod) zone domains; hostname groups: this NodeClaim's counts
               czf = cr->zfull;
               czfl = cr->zflags;
-              const uint64_t D = czf & vr.zn;
-              for (uint64_t m = own & dd.tg_zone; m && pre; m &= m - 1) {
-                const uint32_t g = __ffsll((long long)m) - 1;
-                const uint64_t cand = D & s_known[g];
-                const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = dd.tgroups[g].skew;
-                uint32_t best = NONE;
-                int64_t bc = INT32_MAX;
-                for (uint32_t k = 0; k < dd.NZV && cand; k++) {
-                  const uint32_t z = dd.zone_order[k];
-                  if (!((cand >> z) & 1)) continue;
-                  const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
-                  if (c - mn <= skew && c < bc) {
-                    best = z;
-                    bc = c;
-                  }
-                }
-                if (best == NONE || (tz != NONE && tz != best)) pre = false;
-                tz = best;
-              }
-              for (uint64_t m = own & dd.tg_host; m && pre; m &= m - 1) {
-                const uint32_t g = __ffsll((long long)m) - 1;
-                const int64_t c = dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j],
-                              self = (int64_t)((tself >> g) & 1);
-                pre = ((dd.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self))
-                                             : c + self <= dd.tgroups[g].skew;
-              }
-              if (pre && tz != NONE) {
-                const uint32_t zc = dd.zone_cat[tz];
-                zm = zc < 64 ? (zm & (1ull << zc)) : 0;
-              }
+              const int32_t* hrow = dd.hc + (size_t)(cb + j) * dd.TGH;
+              zset = topo_claim(dd, ts, own_off, own_n, czf & vr.zn, [&](uint32_t hs) -> int64_t { return hrow[hs]; });
+              pre = zset != 0;
+              if (pre && zset != ~0ull) zm &= topo_catmask(dd, zset);
             }
             if (pre) {
               G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
@@ -1513,25 +1452,16 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (TOPO) {
               // zone requirement after Add (+ the topology domain), then
               // <U> Topology.Record for every group selecting the pod
-              if (!own) {
+              if (!own_n) {
                 czf = cr->zfull;
                 czfl = cr->zflags;
               }
-              const uint64_t zf = czf & vr.zn & (tz != NONE ? 1ull << tz : ~0ull);
-              const uint32_t zl = tz != NONE ? 0u : (czfl & vr.zflags);
+              const uint64_t zf = czf & vr.zn & zset;
+              const uint32_t zl = zset != ~0ull ? 0u : (czfl & vr.zflags);
               cr->zfull = zf;
               cr->zflags = zl;
-              for (uint64_t m = vr.t_sel; m; m &= m - 1) {
-                const uint32_t g = __ffsll((long long)m) - 1;
-                if ((dd.tg_host >> g) & 1) {
-                  dd.hc[(size_t)dd.tgroups[g].hslot * dd.max_claims + cb + j]++;
-                  s_zcnt[g * ZVMAX]++;
-                } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
-                  const uint32_t z = __ffsll((long long)zf) - 1;
-                  s_zcnt[g * ZVMAX + z]++;
-                  s_known[g] |= 1ull << z;
-                }
-              }
+              int32_t* hrow = dd.hc + (size_t)(cb + j) * dd.TGH;
+              topo_record(dd, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs]++; });
             }
             FK* cf = dd.c_fk + (size_t)(cb + j) * F;
             for (uint32_t k = 0; k < vr.fk_count; k++) {
@@ -1578,47 +1508,24 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
         // a new hostname domain has count 0, always within maxSkew >= 1):
         // the picked zone narrows the K1 row to that zone's offerings
-        uint32_t ttz = NONE, tzc = NONE;
-        if (TOPO && own) {
-          const uint64_t D = tr.zfull & vr.zn;
-          bool ok = true;
-          for (uint64_t m = own & d.tg_zone; m && ok; m &= m - 1) {
-            const uint32_t g = __ffsll((long long)m) - 1;
-            const uint64_t cand = D & s_known[g];
-            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = d.tgroups[g].skew;
-            uint32_t best = NONE;
-            int64_t bc = INT32_MAX;
-            for (uint32_t k = 0; k < d.NZV && cand; k++) {
-              const uint32_t z = d.zone_order[k];
-              if (!((cand >> z) & 1)) continue;
-              const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
-              if (c - mn <= skew && c < bc) {
-                best = z;
-                bc = c;
-              }
-            }
-            if (best == NONE || (ttz != NONE && ttz != best)) ok = false;
-            ttz = best;
-          }
-          if (ok && ttz != NONE) {
-            tzc = d.zone_cat[ttz];
-            ok = tzc < 64;
-          }
-          // pod affinity on the fresh hostname domain (count 0): only the
-          // bootstrap of a self-selecting pod while no selected pod runs
-          for (uint64_t m = own & d.tg_aff; m && ok; m &= m - 1) {
-            const uint32_t g = __ffsll((long long)m) - 1;
-            ok = s_zcnt[g * ZVMAX] == 0 && ((tself >> g) & 1);
-          }
-          if (!ok) continue;
+        // (pod affinity on the fresh hostname domain, count 0: only the
+        // bootstrap of a self-selecting pod while no selected pod runs)
+        uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
+        if (TOPO && own_n) {
+          tzs = topo_claim(d, ts, own_off, own_n, tr.zfull & vr.zn, [](uint32_t) -> int64_t { return 0; });
+          if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(d, tzs);
+          if (tzs == 0 || tzcat == 0) continue;
         }
         const uint64_t tcm = tr.cm & vr.cm;
         auto rowx = [&](uint32_t w) -> uint64_t {
           uint64_t x = row[w];
-          if (ttz != NONE) {
+          if (tzs != ~0ull) {
             uint64_t off = 0;
-            for (uint32_t c = 0; c < d.C; c++)
-              if ((tcm >> c) & 1) off |= slot[(tzc * d.C + c) * W + w];
+            for (uint64_t zm_ = tzcat; zm_; zm_ &= zm_ - 1) {
+              const uint32_t zc = (uint32_t)__ffsll((long long)zm_) - 1u;
+              for (uint32_t c = 0; c < d.C; c++)
+                if ((tcm >> c) & 1) off |= slot[(zc * d.C + c) * W + w];
+            }
             x &= off;
           }
           return x;
@@ -1691,28 +1598,23 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           cr->thr(tid) = (uint16_t)c0;
           S.red64[tid] = 0;
         }
+        // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
+        if (TOPO) {
+          for (uint32_t h = tid; h < d.TGH; h += FB) d.hc[(size_t)(cbase + j) * d.TGH + h] = 0;
+          __syncthreads();
+        }
         if (tid == 0) {
           cr->tmpl = t;
           cr->count = 1;
-          cr->zm = tr.zm & vr.zm & (ttz != NONE ? 1ull << tzc : ~0ull);
+          cr->zm = tr.zm & vr.zm & tzcat;
           cr->cm = tr.cm & vr.cm;
           cr->ctb = tr.ctb & vr.ctb;
-          cr->zfull = tr.zfull & vr.zn & (ttz != NONE ? 1ull << ttz : ~0ull);
-          cr->zflags = ttz != NONE ? 0u : (tr.zflags & vr.zflags);
-          if (TOPO) {
-            // <U> Topology.Register(hostname placeholder) + Record
-            for (uint32_t h = 0; h < d.TGH; h++) d.hc[(size_t)h * d.max_claims + cbase + j] = 0;
-            for (uint64_t m = vr.t_sel; m; m &= m - 1) {
-              const uint32_t g = __ffsll((long long)m) - 1;
-              if ((d.tg_host >> g) & 1) {
-                d.hc[(size_t)d.tgroups[g].hslot * d.max_claims + cbase + j]++;
-                s_zcnt[g * ZVMAX]++;
-              } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
-                const uint32_t z = __ffsll((long long)cr->zfull) - 1;
-                s_zcnt[g * ZVMAX + z]++;
-                s_known[g] |= 1ull << z;
-              }
-            }
+          cr->zfull = tr.zfull & vr.zn & tzs;
+          cr->zflags = tzs != ~0ull ? 0u : (tr.zflags & vr.zflags);
+          if (TOPO && sel_n) {
+            // <U> Topology.Record
+            int32_t* hrow = d.hc + (size_t)(cbase + j) * d.TGH;
+            topo_record(d, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
           }
           FK* cf = d.c_fk + (size_t)(cbase + j) * F;
           for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
@@ -1856,10 +1758,10 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
 // (simulations) the touched-node bitmap + overlay ids, and the topology
 // spread state (known domains, per-pod minimum, zone counts) of TG groups
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
-                                      uint32_t TG) {
+                                      uint32_t topo_bytes) {
   const uint32_t thr = nthr + 4;
   const uint32_t base = (((23u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u + 7u) & ~7u;
-  return base + TG * 16u + TG * ZVMAX * 4u;
+  return base + topo_bytes;
 }
 
 // every instantiation may use all LDS its static footprint leaves free
@@ -1921,7 +1823,7 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, d->TG);
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread

@@ -479,5 +479,173 @@ __device__ inline bool mv_ok(const DP& d, const TmplRec& tr, WordFn word) {
   return true;
 }
 
+// ---------------------------------------------------------------- topology
+// <U> Topology state of one Solve in LDS (layout.hpp topo_lds_bytes): known
+// domains per zone group, the current pod's minimum count per owned group
+// (domainMinCount, by own-list index), zone counts per zone group, and per
+// hostname group the count over all domains (pod affinity's bootstrap rule).
+// Hostname counts per existing node / NodeClaim stay in global memory (hn,
+// hc); the callers pass them in as functors.
+struct TopoS {
+  uint64_t* known;  // [TGZ]
+  int64_t* tmin;    // [OWNMAX]
+  int32_t* zcnt;    // [TGZ][ZS]
+  int32_t* htot;    // [TGH]
+};
+__device__ __forceinline__ TopoS topo_lds(char* base, uint32_t tgz, uint32_t zs) {
+  TopoS t;
+  t.known = (uint64_t*)base;
+  t.tmin = (int64_t*)(base + tgz * 8u);
+  t.zcnt = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u);
+  t.htot = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u);
+  return t;
+}
+
+// the counts before the Solve; i/stride: this thread's share
+template <class DP>
+__device__ __forceinline__ void topo_init(const DP& d, const TopoS& ts, uint64_t known0, uint32_t i, uint32_t stride) {
+  for (uint32_t k = i; k < d.TGZ * d.ZS; k += stride) ts.zcnt[k] = d.zcnt0[k];
+  for (uint32_t k = i; k < d.TGZ; k += stride) ts.known[k] = known0;
+  for (uint32_t k = i; k < d.TGH; k += stride) ts.htot[k] = d.htot0[k];
+}
+
+// domainMinCount of every owned zone spread group over the pod's strict zone
+// domains vzs; lane k < own_n (<= OWNMAX) handles own-list entry k
+template <class DP>
+__device__ __forceinline__ void topo_tmin(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint64_t vzs,
+                                          uint32_t lane) {
+  if (lane >= own_n) return;
+  const TGroupRec& tr = d.tgroups[d.tg_list[own_off + lane] & TL_GID];
+  if (tr.kind & (TK_HOST | TK_ANTI)) return;
+  const uint64_t cand = ts.known[tr.slot] & vzs;
+  int64_t mn = INT32_MAX;
+  int32_t n = 0;
+  for (uint64_t m = cand; m; m &= m - 1) {
+    n++;
+    const int64_t c = ts.zcnt[tr.slot * d.ZS + (uint32_t)__ffsll((long long)m) - 1u];
+    mn = c < mn ? c : mn;
+  }
+  if (tr.mind && n < tr.mind) mn = 0;
+  ts.tmin[lane] = mn;
+}
+
+// <U> Topology.AddRequirements for an existing node: its zone label z is its
+// only zone domain (a node without one fails the strict Compatible), its
+// hostname count in group slot is hcount(slot)
+template <class DP, class HCount>
+__device__ __forceinline__ bool topo_node_ok(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint32_t z,
+                                             HCount hcount) {
+  for (uint32_t k = 0; k < own_n; k++) {
+    const uint32_t e = d.tg_list[own_off + k];
+    const TGroupRec& tr = d.tgroups[e & TL_GID];
+    const int64_t self = (e & TL_SELF) ? 1 : 0;
+    if (tr.kind & TK_HOST) {
+      const int64_t c = hcount(tr.slot);
+      if (tr.kind & TK_AFF) {
+        if (!(c > 0 || (ts.htot[tr.slot] == 0 && self))) return false;
+      } else if (c + self > tr.skew) {
+        return false;
+      }
+    } else {
+      if (z >= d.ZS || !((ts.known[tr.slot] >> z) & 1)) return false;
+      const int64_t c = ts.zcnt[tr.slot * d.ZS + z];
+      if (tr.kind & TK_ANTI) {
+        if (c != 0) return false;
+      } else if (c + self - ts.tmin[k] > tr.skew) {
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
+// <U> Topology.AddRequirements for a NodeClaim whose zone domains (claim AND
+// pod requirements) are D: every owned zone group's domains, intersected --
+// a spread group's minimum-count known domain within maxSkew (nextDomain-
+// TopologySpread, ties by name), an anti-affinity group's known domains with
+// count 0 (nextDomainAntiAffinity).  Hostname groups test the claim's count
+// hcount(slot) (0 on a fresh NodeClaim).  Returns the allowed zone set, ~0 when
+// no zone group applies, 0 when some group leaves no domain.
+template <class DP, class HCount>
+__device__ __forceinline__ uint64_t topo_claim(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint64_t D,
+                                               HCount hcount) {
+  uint64_t allow = ~0ull;
+  for (uint32_t k = 0; k < own_n; k++) {
+    const uint32_t e = d.tg_list[own_off + k];
+    const TGroupRec& tr = d.tgroups[e & TL_GID];
+    const int64_t self = (e & TL_SELF) ? 1 : 0;
+    if (tr.kind & TK_HOST) {
+      const int64_t c = hcount(tr.slot);
+      const bool ok = (tr.kind & TK_AFF) ? (c > 0 || (ts.htot[tr.slot] == 0 && self)) : c + self <= tr.skew;
+      if (!ok) return 0;
+      continue;
+    }
+    const uint64_t cand = D & ts.known[tr.slot];
+    uint64_t m = 0;
+    if (tr.kind & TK_ANTI) {
+      for (uint64_t x = cand; x; x &= x - 1) {
+        const uint32_t z = (uint32_t)__ffsll((long long)x) - 1u;
+        if (ts.zcnt[tr.slot * d.ZS + z] == 0) m |= 1ull << z;
+      }
+    } else if (cand) {
+      const int64_t mn = ts.tmin[k], skew = tr.skew;
+      uint32_t best = NONE;
+      int64_t bc = INT32_MAX;
+      for (uint32_t q = 0; q < d.NZV; q++) {
+        const uint32_t z = d.zone_order[q];
+        if (!((cand >> z) & 1)) continue;
+        const int64_t c = (int64_t)ts.zcnt[tr.slot * d.ZS + z] + self;
+        if (c - mn <= skew && c < bc) {
+          best = z;
+          bc = c;
+        }
+      }
+      m = best == NONE ? 0 : 1ull << best;
+    }
+    allow &= m;
+    if (!allow) return 0;
+  }
+  return allow;
+}
+
+// catalog zone mask of a zone-vocabulary set (zones outside the catalog have no offerings)
+template <class DP>
+__device__ __forceinline__ uint64_t topo_catmask(const DP& d, uint64_t zset) {
+  uint64_t c = 0;
+  for (uint64_t x = zset; x; x &= x - 1) {
+    const uint32_t zc = d.zone_cat[(uint32_t)__ffsll((long long)x) - 1u];
+    if (zc < 64) c |= 1ull << zc;
+  }
+  return c;
+}
+
+// <U> Topology.Record: every group selecting the pod counts the domain it
+// landed in -- a hostname group the target's own count (hinc(slot)), a zone
+// spread group a single non-complement zone, an anti-affinity group (or its
+// inverse) every zone of a non-complement requirement (zf, zl: the target's
+// zone Has and flags; an existing node: its label)
+template <class DP, class HInc>
+__device__ __forceinline__ void topo_record(const DP& d, const TopoS& ts, uint32_t sel_off, uint32_t sel_n, uint64_t zf,
+                                            uint32_t zl, HInc hinc) {
+  const uint64_t zmask = d.ZS >= 64 ? ~0ull : (1ull << d.ZS) - 1ull;
+  zf &= zmask;
+  for (uint32_t k = 0; k < sel_n; k++) {
+    const uint32_t e = d.tg_list[sel_off + k];
+    const uint32_t slot = e & 0xFFFFFFu, kind = e >> 24;
+    if (kind & TK_HOST) {
+      hinc(slot);
+      ts.htot[slot]++;
+    } else if (!(zl & ZF_COMP)) {
+      if (kind & TK_ANTI) {
+        for (uint64_t x = zf; x; x &= x - 1) ts.zcnt[slot * d.ZS + (uint32_t)__ffsll((long long)x) - 1u]++;
+        ts.known[slot] |= zf;
+      } else if (__popcll(zf) == 1) {
+        ts.zcnt[slot * d.ZS + (uint32_t)__ffsll((long long)zf) - 1u]++;
+        ts.known[slot] |= zf;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gsd

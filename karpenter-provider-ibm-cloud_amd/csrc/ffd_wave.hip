@@ -35,8 +35,9 @@ static_assert(VR_DW == 32, "VarRec is one dword per lane of a half wave");
 static_assert(offsetof(VarRec, fk_begin) == 4 && offsetof(VarRec, fk_count) == 8 && offsetof(VarRec, ctb) == 12 &&
                   offsetof(VarRec, itmask_off) == 16 && offsetof(VarRec, zfull_off) == 48 &&
                   offsetof(VarRec, cfull_off) == 52 && offsetof(VarRec, zm) == 56 && offsetof(VarRec, cm) == 64 &&
-                  offsetof(VarRec, tol) == 72 && offsetof(VarRec, tolt) == 80 && offsetof(VarRec, t_own) == 88 &&
-                  offsetof(VarRec, t_sel) == 96 && offsetof(VarRec, zs) == 104 && offsetof(VarRec, zn) == 112 &&
+                  offsetof(VarRec, tol) == 72 && offsetof(VarRec, tolt) == 80 && offsetof(VarRec, own_off) == 88 &&
+                  offsetof(VarRec, own_n) == 92 && offsetof(VarRec, sel_off) == 96 && offsetof(VarRec, sel_n) == 100 &&
+                  offsetof(VarRec, zs) == 104 && offsetof(VarRec, zn) == 112 &&
                   offsetof(VarRec, zflags) == 120 && offsetof(VarRec, vix) == 124,
               "VarRec dword map used by ffdw_kernel");
 static_assert(offsetof(ClaimRec, maxa) == 128, "ClaimRec maxa after two 64-B lines");
@@ -512,9 +513,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   const uint32_t W = d.W, F = d.F, T = d.T, OW = d.OW, P = d.P;
   const uint32_t nthr = d.thr_off[R];
   const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
-  uint64_t* s_known = (uint64_t*)((char*)lds64 + tg_off);
-  int64_t* s_tmin = (int64_t*)(s_known + d.TG);
-  int32_t* s_zcnt = (int32_t*)(s_tmin + d.TG);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
   const int64_t* thr = s_thr;
   const uint64_t* slot = s_slot;
 
@@ -525,10 +524,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     s_tzm[t] = d.tmpl[t].zm;
     s_tcm[t] = d.tmpl[t].cm;
   }
-  if (TOPO) {
-    for (uint32_t i = tid; i < d.TG * ZVMAX; i += 128) s_zcnt[i] = d.tg_cnt0[i];
-    for (uint32_t g = tid; g < d.TG; g += 128) s_known[g] = d.tgroups[g].known0;
-  }
+  if (TOPO) topo_init(d, ts, d.zknown0, tid, 128);
   if (tid < RING) s_ring_seq[tid] = 0;
   if (tid < 4) s_ctl[tid] = 0;
   __syncthreads();  // the only workgroup barrier: the waves split here
@@ -715,7 +711,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
     const uint32_t vctb = VD(3);
     const uint64_t vtolt = VD64(20);
-    const uint64_t own = TOPO ? VD64(22) : 0, vtsel = TOPO ? VD64(24) : 0;
+    // topology: own list (groups the variant owns), selection list (groups counting the pod)
+    const uint32_t own_off = TOPO ? VD(22) : 0u, own_n = TOPO ? VD(23) : 0u;
+    const uint32_t sel_off = TOPO ? VD(24) : 0u, sel_n = TOPO ? VD(25) : 0u;
     int64_t rq[RR];
 #pragma unroll
     for (uint32_t r = 0; r < RR; r++)
@@ -728,24 +726,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     TLW(0);  // pop + record
     // <U> Topology.AddRequirements: each owned zone group's minimum domain
     // count over the pod's strict zone domains (domainMinCount)
-    if (TOPO && own) {
+    if (TOPO && own_n) {
       const auto& KD = *karg();
       const uint64_t vzs = rlane(vrd, 26) | ((uint64_t)rlane(vrd, 27) << 32);
-      if (((own & KD.tg_zone) >> lane) & 1) {
-        const uint64_t cand = s_known[lane] & vzs;
-        int64_t mn = INT32_MAX;
-        int32_t n = 0;
-        for (uint64_t m = cand; m; m &= m - 1) {
-          n++;
-          const int64_t c = s_zcnt[lane * ZVMAX + ffs64(m)];
-          mn = c < mn ? c : mn;
-        }
-        if (KD.tgroups[lane].mind && n < KD.tgroups[lane].mind) mn = 0;
-        s_tmin[lane] = mn;
-      }
+      topo_tmin(KD, ts, own_off, own_n, vzs, lane);
       wsync();
     }
-    const uint64_t tself = own & vtsel;
 
     // ----------------- existing nodes in order: first ExistingNode.CanAdd wins
     if (d.NN) {
@@ -782,18 +768,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if (feas && cfull_off != NONE)
             feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
           if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
-          if (TOPO && feas && own) {
-            for (uint64_t m = own & KD.tg_zone; m && feas; m &= m - 1) {
-              const uint32_t g = ffs64(m), z = nr.zvid;
-              feas = z < (uint32_t)ZVMAX && ((s_known[g] >> z) & 1) &&
-                     (int64_t)s_zcnt[g * ZVMAX + z] + (int64_t)((tself >> g) & 1) - s_tmin[g] <= KD.tgroups[g].skew;
-            }
-            for (uint64_t m = own & KD.tg_host; m && feas; m &= m - 1) {
-              const uint32_t g = ffs64(m);
-              const int64_t c = KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + n], self = (int64_t)((tself >> g) & 1);
-              feas = ((KD.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= KD.tgroups[g].skew;
-            }
-          }
+          if (TOPO && feas && own_n)
+            feas = topo_node_ok(KD, ts, own_off, own_n, nr.zvid,
+                                [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; });
           if (TOPO && feas && KD.any_vol) {
             // ExceedsLimits: distinct volumes per driver after the union
             const NodeVol& nv = KD.n_vol[n];
@@ -835,18 +812,10 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             nv.present |= all;
           }
           // <U> Topology.Record: the node's labels are single domains
-          for (uint64_t m = TOPO ? vtsel : 0; m; m &= m - 1) {
-            const uint32_t g = ffs64(m);
-            if ((KD.tg_host >> g) & 1) {
-              KD.hn[(size_t)KD.tgroups[g].hslot * KD.NN + fn]++;
-              s_zcnt[g * ZVMAX]++;  // hostname groups: the total
-            } else {
-              const uint32_t z = KD.nodes0[fn].zvid;
-              if (z < (uint32_t)ZVMAX) {
-                s_zcnt[g * ZVMAX + z]++;
-                s_known[g] |= 1ull << z;
-              }
-            }
+          if (TOPO && sel_n) {
+            const uint32_t z = KD.nodes0[fn].zvid;
+            topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
+                        [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
           }
         }
         wsync();
@@ -996,7 +965,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
         const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
       bool feas = false;
-      uint32_t tz = NONE;
+      uint64_t zset = ~0ull;  // zone domains topology allows on this NodeClaim (~0: unconstrained)
       uint64_t zm = 0, cm = 0, czf = 0;
       uint32_t czfl = 0;
       uint32_t mrow[RR];
@@ -1035,41 +1004,15 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         }
         bool pre = true;
         if (fk_count) pre = fk_ok_range(d, fk_begin, fk_count, KD.c_fk + (size_t)j * F, false);
-        if (TOPO && pre && own) {
-          // <U> Topology.AddRequirements on the NodeClaim: every owned zone
-          // group picks the minimum-count known domain within maxSkew among
-          // the NodeClaim's (claim AND pod) zone domains, ties by name; the
-          // picks must agree.  Hostname groups: this NodeClaim's count.
+        if (TOPO && pre && own_n) {
+          // <U> Topology.AddRequirements on the NodeClaim over its (claim AND
+          // pod) zone domains; hostname groups: this NodeClaim's counts
           czf = cr->zfull;
           czfl = cr->zflags;
-          const uint64_t D = czf & vzn;
-          for (uint64_t m = own & KD.tg_zone; m && pre; m &= m - 1) {
-            const uint32_t g = ffs64(m);
-            const uint64_t cand = D & s_known[g];
-            const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = KD.tgroups[g].skew;
-            uint32_t best = NONE;
-            int64_t bc = INT32_MAX;
-            for (uint32_t k = 0; k < KD.NZV && cand; k++) {
-              const uint32_t z = KD.zone_order[k];
-              if (!((cand >> z) & 1)) continue;
-              const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
-              if (c - mn <= skew && c < bc) {
-                best = z;
-                bc = c;
-              }
-            }
-            if (best == NONE || (tz != NONE && tz != best)) pre = false;
-            tz = best;
-          }
-          for (uint64_t m = own & KD.tg_host; m && pre; m &= m - 1) {
-            const uint32_t g = ffs64(m);
-            const int64_t c = KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j], self = (int64_t)((tself >> g) & 1);
-            pre = ((KD.tg_aff >> g) & 1) ? (c > 0 || (s_zcnt[g * ZVMAX] == 0 && self)) : c + self <= KD.tgroups[g].skew;
-          }
-          if (pre && tz != NONE) {
-            const uint32_t zc = KD.zone_cat[tz];
-            zm = zc < 64 ? (zm & (1ull << zc)) : 0;
-          }
+          const int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+          zset = topo_claim(KD, ts, own_off, own_n, czf & vzn, [&](uint32_t hs) -> int64_t { return hrow[hs]; });
+          pre = zset != 0;
+          if (pre && zset != ~0ull) zm &= topo_catmask(KD, zset);
         }
         if (pre) {
           G = grid_of(zm & vzm, cm & vcm, KD.Z, KD.C);
@@ -1212,25 +1155,16 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if (TOPO) {
             // zone requirement after Add (+ the topology domain), then
             // <U> Topology.Record for every group selecting the pod
-            if (!own) {
+            if (!own_n) {
               czf = cr->zfull;
               czfl = cr->zflags;
             }
-            const uint64_t zf = czf & vzn & (tz != NONE ? 1ull << tz : ~0ull);
-            const uint32_t zl = tz != NONE ? 0u : (czfl & vzflags);
+            const uint64_t zf = czf & vzn & zset;
+            const uint32_t zl = zset != ~0ull ? 0u : (czfl & vzflags);
             cr->zfull = zf;
             cr->zflags = zl;
-            for (uint64_t m = vtsel; m; m &= m - 1) {
-              const uint32_t g = ffs64(m);
-              if ((KD.tg_host >> g) & 1) {
-                KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
-                s_zcnt[g * ZVMAX]++;
-              } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
-                const uint32_t z = ffs64(zf);
-                s_zcnt[g * ZVMAX + z]++;
-                s_known[g] |= 1ull << z;
-              }
-            }
+            int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+            topo_record(KD, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs]++; });
           }
           FK* cf = KD.c_fk + (size_t)j * F;
           for (uint32_t k = 0; k < fk_count; k++) {
@@ -1281,24 +1215,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const uint32_t e = s_so[f];
             if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
             s_so[f] = e + 1u;
-            if (TOPO && vtsel) {
+            if (TOPO && sel_n) {
               // <U> Topology.Record in the groups that select the pod: the
               // NodeClaim's requirements are unchanged by this Add
               const auto& KD = *karg();
               const ClaimRec* cr = KD.c_rec + j;
-              const uint64_t zf = cr->zfull;
-              const uint32_t zl = cr->zflags;
-              for (uint64_t m = vtsel; m; m &= m - 1) {
-                const uint32_t g = ffs64(m);
-                if ((KD.tg_host >> g) & 1) {
-                  KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
-                  s_zcnt[g * ZVMAX]++;
-                } else if (!(zl & ZF_COMP) && __popcll(zf) == 1) {
-                  const uint32_t z = ffs64(zf);
-                  s_zcnt[g * ZVMAX + z]++;
-                  s_known[g] |= 1ull << z;
-                }
-              }
+              int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+              topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
             }
           }
         }
@@ -1346,49 +1269,26 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
       // a new hostname domain has count 0, always within maxSkew >= 1):
       // the picked zone narrows the K1 row to that zone's offerings
-      uint32_t ttz = NONE, tzc = NONE;
-      if (TOPO && own) {
-        const uint64_t D = tr.zfull & vzn;
-        bool ok = true;
-        for (uint64_t m = own & KD.tg_zone; m && ok; m &= m - 1) {
-          const uint32_t g = ffs64(m);
-          const uint64_t cand = D & s_known[g];
-          const int64_t self = (int64_t)((tself >> g) & 1), mn = s_tmin[g], skew = KD.tgroups[g].skew;
-          uint32_t best = NONE;
-          int64_t bc = INT32_MAX;
-          for (uint32_t k = 0; k < KD.NZV && cand; k++) {
-            const uint32_t z = KD.zone_order[k];
-            if (!((cand >> z) & 1)) continue;
-            const int64_t c = (int64_t)s_zcnt[g * ZVMAX + z] + self;
-            if (c - mn <= skew && c < bc) {
-              best = z;
-              bc = c;
-            }
-          }
-          if (best == NONE || (ttz != NONE && ttz != best)) ok = false;
-          ttz = best;
-        }
-        if (ok && ttz != NONE) {
-          tzc = KD.zone_cat[ttz];
-          ok = tzc < 64;
-        }
-        // pod affinity on the fresh hostname domain (count 0): only the
-        // bootstrap of a self-selecting pod while no selected pod runs
-        for (uint64_t m = own & KD.tg_aff; m && ok; m &= m - 1) {
-          const uint32_t g = ffs64(m);
-          ok = s_zcnt[g * ZVMAX] == 0 && ((tself >> g) & 1);
-        }
-        ttz = __builtin_amdgcn_readfirstlane(ttz);
-        tzc = __builtin_amdgcn_readfirstlane(tzc);
-        if (!__builtin_amdgcn_readfirstlane(ok ? 1u : 0u)) continue;
+      // (pod affinity on the fresh hostname domain, count 0: only the
+      // bootstrap of a self-selecting pod while no selected pod runs)
+      uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
+      if (TOPO && own_n) {
+        tzs = topo_claim(KD, ts, own_off, own_n, tr.zfull & vzn, [](uint32_t) -> int64_t { return 0; });
+        if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(KD, tzs);
+        tzs = (uint64_t)uniform_i64((int64_t)tzs);
+        tzcat = (uint64_t)uniform_i64((int64_t)tzcat);
+        if (tzs == 0 || tzcat == 0) continue;
       }
       const uint64_t tcm = tr.cm & vcm;
       auto rowx = [&](uint32_t w) -> uint64_t {
         uint64_t x = row[w];
-        if (ttz != NONE) {
+        if (tzs != ~0ull) {
           uint64_t off = 0;
-          for (uint32_t c = 0; c < KD.C; c++)
-            if ((tcm >> c) & 1) off |= slot[(tzc * KD.C + c) * W + w];
+          for (uint64_t zm_ = tzcat; zm_; zm_ &= zm_ - 1) {
+            const uint32_t zc = ffs64(zm_);
+            for (uint32_t c = 0; c < KD.C; c++)
+              if ((tcm >> c) & 1) off |= slot[(zc * KD.C + c) * W + w];
+          }
           x &= off;
         }
         return x;
@@ -1486,30 +1386,24 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         if (tr.has_limits) mxc[r] = wave_max_u64(mxc[r]);
         nt[r] = tr.daemon[r] + rq[r];
       }
+      // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
+      if (TOPO)
+        for (uint32_t h = lane; h < KD.TGH; h += 64) KD.hc[(size_t)j * KD.TGH + h] = 0;
+      wsync();
       if (lane == 0) {
         cr->tmpl = t;
         cr->count = 1;
-        cr->zm = tr.zm & vzm & (ttz != NONE ? 1ull << tzc : ~0ull);
+        cr->zm = tr.zm & vzm & tzcat;
         cr->cm = tr.cm & vcm;
         cr->ctb = tr.ctb & vctb;
-        cr->zfull = tr.zfull & vzn & (ttz != NONE ? 1ull << ttz : ~0ull);
-        cr->zflags = ttz != NONE ? 0u : (tr.zflags & vzflags);
+        cr->zfull = tr.zfull & vzn & tzs;
+        cr->zflags = tzs != ~0ull ? 0u : (tr.zflags & vzflags);
 #pragma unroll
         for (uint32_t r = 0; r < RR; r++) cr->maxa[r] = ma[r];
-        if (TOPO) {
-          // <U> Topology.Register(hostname placeholder) + Record
-          for (uint32_t h = 0; h < KD.TGH; h++) KD.hc[(size_t)h * KD.max_claims + j] = 0;
-          for (uint64_t m = vtsel; m; m &= m - 1) {
-            const uint32_t g = ffs64(m);
-            if ((KD.tg_host >> g) & 1) {
-              KD.hc[(size_t)KD.tgroups[g].hslot * KD.max_claims + j]++;
-              s_zcnt[g * ZVMAX]++;
-            } else if (!(cr->zflags & ZF_COMP) && __popcll(cr->zfull) == 1) {
-              const uint32_t z = ffs64(cr->zfull);
-              s_zcnt[g * ZVMAX + z]++;
-              s_known[g] |= 1ull << z;
-            }
-          }
+        if (TOPO && sel_n) {
+          // <U> Topology.Record
+          int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+          topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
         }
         FK* cf = KD.c_fk + (size_t)j * F;
         for (uint32_t s = 0; s < F; s++) cf[s] = KD.t_fk[(size_t)t * F + s];
@@ -1609,7 +1503,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
 // ---------------------------------------------------------------- launchers
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
-                                      uint32_t TG);
+                                      uint32_t topo_bytes);
 static uint32_t g_ffdw_dyn_max = 0;
 
 template <uint32_t RR, bool TOPO>
@@ -1638,7 +1532,7 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
 
 // the single-wave provisioning Solve: grid-wide state reset, then one wave
 extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, 0, 0, d->TG);
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);

@@ -33,8 +33,14 @@ constexpr int TMAX = 64;       // NodeClaim templates (NodePools)
 constexpr uint32_t THR_LDS_MAX = 2048;   // fit thresholds staged in the FFD kernel's LDS
 constexpr uint32_t SLOT_LDS_MAX = 1024;  // (zone, capacity-type) pair type-set words in LDS
 constexpr int SMAX = 16;       // offerings per instance type
-constexpr int TGMAX = 64;      // topology spread groups
-constexpr int ZVMAX = 64;      // zone vocabulary (topology domains) when zone spread is used
+constexpr int TGMAX = 4096;    // topology groups (spread, pod (anti-)affinity, inverse, host ports)
+constexpr int OWNMAX = 64;     // topology groups one pod variant owns
+constexpr int ZVMAX = 64;      // zone vocabulary (topology domains) when zone groups are used
+// topology group kinds (TGroupRec.kind, and the top byte of a selection-list entry)
+enum : uint32_t { TK_HOST = 1u, TK_AFF = 2u, TK_ANTI = 4u };
+// own-list entry: group id | TL_SELF (the owner is counted by the group itself)
+constexpr uint32_t TL_SELF = 0x80000000u;
+constexpr uint32_t TL_GID = 0xFFFFu;
 enum : uint32_t { ZF_COMP = 1u };  // zone requirement is a complement (Exists / NotIn / absent)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 // capacity-type requirement bits (consolidation's spot-to-spot rule)
@@ -71,10 +77,12 @@ struct VarRec {
   uint64_t zm, cm;               // Has over catalog zones / capacity types
   uint64_t tol;                  // tolerated taint-vocabulary mask
   uint64_t tolt;                 // templates whose taints this variant tolerates
-  // topology spread (<U> Topology): groups the variant owns, groups that
-  // select the pod, zone Has over the zone vocabulary of the strict
-  // (podDomains) and full (nodeDomains) requirements
-  uint64_t t_own, t_sel;
+  // topology (<U> Topology): the groups the variant owns and the groups that
+  // select (count) the pod, as lists in DevProblem::tg_list (own entries:
+  // group id | TL_SELF; selection entries: slot | kind << 24), and the zone
+  // Has over the zone vocabulary of the strict (podDomains) and full
+  // (nodeDomains) requirements
+  uint32_t own_off, own_n, sel_off, sel_n;
   uint64_t zs, zn;
   uint32_t zflags;               // ZF_COMP of the full zone requirement
   uint32_t vix;                  // this record's own variant index
@@ -96,14 +104,23 @@ struct TmplRec {
   uint16_t mv[KMAX_IT];  // minValues per IT key
 };
 
-// one topology spread group (<U> TopologyGroup, type spread, empty node filter)
+// one topology group (<U> TopologyGroup, empty node filter)
 struct TGroupRec {
-  int32_t skew;          // maxSkew
+  int32_t skew;          // maxSkew (hostname anti-affinity / host ports: self, so the rule is count == 0)
   int32_t mind;          // minDomains (0 = unset)
-  uint32_t hslot;        // hostname groups: row in hn / hc
-  uint32_t host;         // 1: kubernetes.io/hostname, 0: topology.kubernetes.io/zone
+  uint32_t slot;         // TK_HOST: row in hn / column in hc; zone groups: row in the zone count table
+  uint32_t kind;         // TK_HOST (hostname key, else zone), TK_AFF (pod affinity), TK_ANTI (anti-affinity / inverse)
   uint64_t known0;       // zone groups: domains known before the Solve (universe + counted)
 };
+static_assert(sizeof(TGroupRec) == 24, "TGroupRec layout");
+
+// LDS bytes of the Solve kernels' topology state: known domains [TGZ] u64,
+// per-owned-group minimum counts [OWNMAX] i64, zone counts [TGZ][ZS] i32,
+// hostname totals [TGH] i32
+__host__ __device__ inline uint32_t topo_lds_bytes(uint32_t tgz, uint32_t zs, uint32_t tgh) {
+  if (!tgz && !tgh) return 0;
+  return (tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u;
+}
 
 // per-claim record (device-owned, AoS: one candidate = one 192-B record read
 // in a single round trip)
@@ -262,18 +279,20 @@ struct DevProblem {
   LogRec* log;                 // [P]
   uint32_t* c_sorted;          // [max_claims] final sort order (debug)
   Ctrl* ctrl;
-  // topology spread
+  // topology groups
   uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size
+  uint32_t TGZ, ZS;            // zone groups, zone-count stride (max(NZV, 1))
   uint32_t pad_tg;
-  uint64_t tg_zone, tg_host;   // group masks by key
-  uint64_t tg_aff;             // hostname groups with the pod-affinity rule (count > 0, or total 0 and self)
+  uint64_t zknown0;            // zone domains known before the Solve (universe + counted), every zone group
   const TGroupRec* tgroups;    // [TG]
-  const int32_t* tg_cnt0;      // [TG][64] zone counts before the Solve
+  const uint32_t* tg_list;     // own / selection list arena (VarRec own_off / sel_off)
+  const int32_t* zcnt0;        // [TGZ][ZS] zone counts before the Solve
+  const int32_t* htot0;        // [TGH] hostname groups: counted pods over all domains before the Solve
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)
   const uint32_t* zone_cat;    // [64] zone vocabulary id -> catalog zone index (NONE)
   const int32_t* hn0;          // [TGH][NN] hostname counts per existing node before the Solve
   int32_t* hn;                 // [TGH][NN] working copy
-  int32_t* hc;                 // [TGH][max_claims] per NodeClaim
+  int32_t* hc;                 // [max_claims][TGH] per NodeClaim (one row per claim)
   // truncation outputs
   uint32_t* c_its;             // [max_claims][60] (simulations: [n_sims][60])
   uint32_t* c_nits;            // [max_claims]     (simulations: [n_sims])

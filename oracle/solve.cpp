@@ -730,8 +730,11 @@ struct Builder {
         AffTerm a;
         a.affinity = affinity;
         a.key = normalize_key(str(q.topology_key));
-        if (a.key != kHostname)
-          throw Unsupported{GS_E_UNSUPPORTED, "pod (anti-)affinity topologyKey other than hostname"};
+        // zone-key anti-affinity is deterministic (nextDomainAntiAffinity: every
+        // empty domain); zone-key affinity bootstraps on a zone in Go map order
+        if (a.key != kHostname && !(a.key == kZone && !affinity))
+          throw Unsupported{GS_E_UNSUPPORTED, affinity ? "pod affinity topologyKey other than hostname"
+                                                       : "pod anti-affinity topologyKey other than hostname / zone"};
         a.required = q.required != 0;
         a.weight = q.weight;
         a.sel.has_selector = q.has_selector != 0;

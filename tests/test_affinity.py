@@ -264,9 +264,11 @@ def test_namespace_selector():
 
 
 def test_refusals():
+    # zone-key anti-affinity is supported (tests/test_zone_anti_affinity.py);
+    # zone-key pod affinity is refused (its bootstrap zone is Go map order)
     b = _base(n_pods=1, anti=[{"key": Z, "required": True, "selector": WEB}])
-    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
-    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+    assert pyoracle.solve(b.build())[0] == abi.GS_OK
+    assert lib.validate(b.build())[0] == abi.GS_OK
     b = _base(n_pods=1, ports=[(0, "TCP", "")])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_INVALID
     assert lib.validate(b.build())[0] == abi.GS_E_INVALID
@@ -279,10 +281,10 @@ def test_refusals():
     b = _base(n_pods=1)
     b.add_pod("x", 0, {"cpu": 1}, flags=abi.POD_ANTI_AFFINITY)
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
-    # a bound pod's anti-affinity on another key constrains pending pods: refused
+    # a bound pod's anti-affinity on a key other than hostname / zone: refused
     b = _base(n_pods=1)
     _nodes(b, 1)
-    b.add_bound_pod(0, "b0", 0, {"cpu": 100}, anti_affinity=[{"key": Z, "required": True, "selector": WEB}])
+    b.add_bound_pod(0, "b0", 0, {"cpu": 100}, anti_affinity=[{"key": "rack", "required": True, "selector": WEB}])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
 
