@@ -387,7 +387,8 @@ enum {
   GS_NOOP_PRICE_UNKNOWN = 3,   /* getCandidatePrices: no offering of a candidate's type matches its labels */
   GS_NOOP_SPOT_TO_SPOT = 4,    /* all candidates spot, replacement may be spot, SpotToSpotConsolidation off */
   GS_NOOP_NOT_CHEAPER = 5,     /* RemoveInstanceTypeOptionsByPriceAndMinValues left no option */
-  GS_NOOP_SAME_TYPE = 6        /* multi-node: filterOutSameInstanceType left no option */
+  GS_NOOP_SAME_TYPE = 6,       /* multi-node: filterOutSameInstanceType left no option */
+  GS_NOOP_MIN_VALUES = 7       /* RemoveInstanceTypeOptionsByPriceAndMinValues: the cheaper options miss a minValues requirement */
 };
 
 typedef struct gs_consolidation {

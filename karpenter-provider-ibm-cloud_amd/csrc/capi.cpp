@@ -50,6 +50,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.n_vol0, e.n_vol);
   c->alloc(d.n_vol, e.n_vol.size());
   c->upload(d.pod_vol, e.pod_vol);
+  c->upload(d.pod_vfresh, e.pod_vfresh);
   c->upload(d.it_alloc, e.it_alloc);
   c->upload(d.it_cap, e.it_cap);
   c->upload(d.it_pair, e.it_pair);
@@ -161,6 +162,18 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->upload(d.sim_cands, sims->cands);
     c->alloc(d.ov_req, (size_t)sims->blocks * d.ov_cap * gsd::RMAX);
     c->alloc(d.ov_fk, (size_t)sims->blocks * d.ov_cap * F1);
+    // the general (topology / volumes / minValues) simulation variant
+    c->alloc(d.ov_hn, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1));
+    c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
+    {
+      std::vector<uint64_t> known = sims->known;
+      known.resize(std::max<size_t>(NS, 1), 0);
+      c->upload(d.sim_known, known);
+    }
+    c->upload(d.zn_cnt, e.zn_cnt);
+    c->alloc(d.slot_its, e.any_mv ? CA * 60 : 1);
+    c->alloc(d.slot_nits, e.any_mv ? CA : 1);
+    c->alloc(d.slot_drop, e.any_mv ? CA : 1);
     c->alloc(d.sim_ctrl, NS);
     c->alloc(d.sim_hdr, NS);
     c->alloc(d.sim_next, 1);
@@ -425,7 +438,7 @@ gs_status gs_run(gs_ctx* c) {
     else
       HIPCHK(gsk_ffd(&d, 1, c->stream));
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), c->stream));
+    HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), 0, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[3]));
     float a = 0, b = 0, x = 0;

@@ -97,7 +97,49 @@ CandTable build_cand_table(const gs_problem* p, const uint32_t* cands, uint32_t 
     if (cands[i] < p->n_nodes && !t.node.count(cands[i])) t.node.emplace(cands[i], candidate_info(p, cands[i]));
   t.it_name.reserve(p->n_instance_types);
   for (uint32_t i = 0; i < p->n_instance_types; i++) t.it_name.push_back(str(p, p->instance_types[i].name));
+  // NodePool minValues: the keys and minimums, and the instance types' values of those keys
+  std::set<std::string> keys;
+  t.np_mv.assign(p->n_nodepools, {});
+  for (uint32_t np = 0; np < p->n_nodepools; np++) {
+    const gs_range r = p->nodepools[np].requirements;
+    for (uint32_t k = 0; k < r.count && (uint64_t)r.begin + k < p->n_reqs; k++) {
+      const gs_requirement& q = p->reqs[r.begin + k];
+      if (q.min_values < 0) continue;
+      t.np_mv[np].push_back({norm_key(str(p, q.key)), q.min_values});
+      keys.insert(t.np_mv[np].back().first);
+    }
+  }
+  if (!keys.empty()) {
+    t.it_vals.assign(p->n_instance_types, {});
+    for (uint32_t i = 0; i < p->n_instance_types; i++) {
+      const gs_range r = p->instance_types[i].requirements;
+      for (uint32_t k = 0; k < r.count && (uint64_t)r.begin + k < p->n_reqs; k++) {
+        const gs_requirement& q = p->reqs[r.begin + k];
+        const std::string key = norm_key(str(p, q.key));
+        if (!keys.count(key) || q.op != GS_OP_IN) continue;
+        auto& vals = t.it_vals[i][key];
+        for (uint32_t v = 0; v < q.values.count && (uint64_t)q.values.begin + v < p->n_value_ids; v++)
+          vals.push_back(str(p, p->value_ids[q.values.begin + v]));
+      }
+    }
+  }
   return t;
+}
+
+// <U> InstanceTypes.SatisfiesMinValues(NodeClaim requirements) on an option
+// list: the NodeClaim's minimums are its NodePool's
+bool mv_satisfied(const CandTable& t, uint32_t nodepool, const uint32_t* its, size_t n) {
+  if (nodepool >= t.np_mv.size()) return true;
+  for (auto& km : t.np_mv[nodepool]) {
+    std::set<std::string> vals;
+    for (size_t i = 0; i < n; i++) {
+      if (its[i] >= t.it_vals.size()) continue;
+      auto f = t.it_vals[its[i]].find(km.first);
+      if (f != t.it_vals[its[i]].end()) vals.insert(f->second.begin(), f->second.end());
+    }
+    if ((int64_t)vals.size() < km.second) return false;
+  }
+  return true;
 }
 
 namespace {
@@ -190,7 +232,8 @@ int32_t choose(const CandTable& t, uint32_t mode, const std::vector<std::vector<
       for (uint32_t i : filter_out_same_type(t, sets[mid - 1], opts + c.options.begin, prices + c.options.begin,
                                              c.options.count))
         keep.push_back(opts[c.options.begin + i]);
-      valid = !keep.empty();
+      // filterOutSameInstanceType ends in RemoveInstanceTypeOptionsByPriceAndMinValues
+      valid = !keep.empty() && mv_satisfied(t, c.nodepool, keep.data(), keep.size());
     }
     if (valid || c.decision == GS_DECISION_DELETE) {
       chosen = mid - 1;
@@ -227,14 +270,29 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   sp.pods.clear();
   sp.cand_off.assign(1, 0);
   sp.cands.clear();
+  sp.known.clear();
   sp.max_pods = 0;
   sp.ov_cap = 0;
   std::vector<uint32_t> mine, merged;
+  std::vector<int32_t> zn(64);
   for (uint32_t s : sp.evaluated) {
     mine.clear();
     for (uint32_t n : sp.sets[s]) {
       mine.insert(mine.end(), bound_by_node[n].begin(), bound_by_node[n].end());
       sp.cands.push_back(pos_of[n]);
+    }
+    if (e.TGZ) {
+      // <U> NewTopology over the state nodes the simulation keeps: the
+      // NodePools' zones plus the zones of the remaining nodes
+      std::copy(e.zone_nodes.begin(), e.zone_nodes.end(), zn.begin());
+      for (uint32_t n : sp.sets[s]) {
+        const uint32_t z = e.nodes[pos_of[n]].zvid;
+        if (z < 64) zn[z]--;
+      }
+      uint64_t k = e.known_np;
+      for (uint32_t z = 0; z < 64; z++)
+        if (zn[z] > 0) k |= 1ull << z;
+      sp.known.push_back(k);
     }
     std::sort(mine.begin(), mine.end(), [&](uint32_t a, uint32_t b) { return rank[a] < rank[b]; });
     merged.resize(pend.size() + mine.size());
@@ -251,7 +309,8 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     return GS_E_CAPACITY;
   }
   const uint32_t lds = gsk_ffd_lds_bytes(std::max<uint32_t>(sp.max_pods, 1), (uint32_t)e.thr_val.size(),
-                                         (e.NN + 31) / 32, std::max<uint32_t>(sp.ov_cap, 1), 0);
+                                         (e.NN + 31) / 32, std::max<uint32_t>(sp.ov_cap, 1),
+                                         gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH));
   if (lds > gsk_ffd_dyn_lds_max()) {
     *err = "simulation exceeds the workgroup LDS (pods per simulation or state nodes)";
     return GS_E_CAPACITY;
@@ -263,8 +322,12 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   // many simulations: the narrow workgroup (throughput); few: the wide one
   // (each simulation's latency) -- ffd.hip FB_SIM / FB_SIM_NARROW
   sp.nt = sp.evaluated.size() >= 4 * (size_t)std::max(cus, 1) ? 128u : 256u;
-  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt);
+  const bool general = e.TG || e.any_mv || e.any_vol;
+  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt, general ? 1u : 0u);
   sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
+  // per-block overlays of hostname counts: at most 1 GiB (fewer persistent blocks otherwise)
+  const size_t ov_row = (size_t)std::max<uint32_t>(sp.ov_cap, 1) * e.TGH * sizeof(int32_t);
+  if (ov_row) sp.blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(sp.blocks, (size_t)(1u << 30) / ov_row));
   return GS_OK;
 }
 
@@ -290,7 +353,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
       HIPCHK(gsk_ffd(&d, sp.blocks, c->stream));
     }
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    if (NS) HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), c->stream));
+    if (NS) HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), (uint32_t)sp.pods.size(), c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[3]));
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
@@ -376,6 +439,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
       continue;
     }
     // RemoveInstanceTypeOptionsByPriceAndMinValues over the OrderByPrice list
+    // (the price filter, then SatisfiesMinValues on what is left)
     const uint64_t G = grid_of(h.zm, h.cm, e.Z, e.C);
     const uint32_t ob = (uint32_t)c->cmd_options.size();
     for (uint32_t i = 0; i < nits[k]; i++) {
@@ -394,12 +458,19 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
       }
     }
     const uint32_t n_opt = (uint32_t)c->cmd_options.size() - ob;
+    const uint32_t np = e.tmpl[h.tmpl].np_index;
+    if (e.tmpl[h.tmpl].mv_mask && !mv_satisfied(c->cand_table, np, c->cmd_options.data() + ob, n_opt)) {
+      c->cmd_options.resize(ob);
+      c->cmd_prices.resize(ob);
+      cmd.reason = GS_NOOP_MIN_VALUES;
+      continue;
+    }
     if (n_opt == 0) {
       cmd.reason = GS_NOOP_NOT_CHEAPER;
       continue;
     }
     cmd.decision = GS_DECISION_REPLACE;
-    cmd.nodepool = e.tmpl[h.tmpl].np_index;
+    cmd.nodepool = np;
     cmd.spot_only = has_spot && has_od ? 1u : 0u;
     cmd.options = gs_range{ob, n_opt};
   }
@@ -494,22 +565,19 @@ gs_status gs_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation
   c->n_pending = cl->n_pods;
   c->cons_pods.assign(cl->pods, cl->pods + cl->n_pods);
   c->cons_pods.insert(c->cons_pods.end(), cl->bound_pods, cl->bound_pods + cl->n_bound_pods);
+  // every bound pod is in the combined pod list (a simulation reschedules the
+  // candidates' pods) and stays a bound pod (the topology counts, host ports
+  // and volumes of the nodes a simulation keeps): bound pod b is pod n_pending + b
   c->cons_problem = *cl;
   c->cons_problem.pods = c->cons_pods.data();
   c->cons_problem.n_pods = (uint32_t)c->cons_pods.size();
-  c->cons_problem.bound_pods = nullptr;  // every bound pod is in the combined pod list
-  c->cons_problem.n_bound_pods = 0;
-  c->cons_problem.bound_pod_node = nullptr;
-  if (cl->n_spreads || cl->n_affinity_terms || cl->n_host_ports || cl->n_volumes)
-    return fail(c, GS_E_UNSUPPORTED, "topology spread / anti-affinity / host ports in consolidation simulations");
   c->n_nodepools = c->cons_problem.n_nodepools;
   auto t0 = Clock::now();
-  gsh::Err er = gsh::encode(&c->cons_problem, c->enc);
+  gsh::Err er = gsh::encode(&c->cons_problem, c->enc, c->n_pending);
   c->t_encode = ms_since(t0);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
   er = capacity_check(c->enc);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
-  if (c->enc.any_mv) return fail(c, GS_E_UNSUPPORTED, "minValues in consolidation simulations");
   st = plan_sims(c, &c->cons_in, &err);
   if (st != GS_OK) return fail(c, st, err);
   try {

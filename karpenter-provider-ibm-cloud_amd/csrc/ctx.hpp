@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <map>
 #include <unordered_map>
 #include <vector>
 
@@ -18,7 +19,7 @@
 extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
-extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt);
+extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt, uint32_t general);
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
                                       uint32_t topo_bytes);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
@@ -27,7 +28,7 @@ extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStre
 extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total);
 extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
 extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, hipStream_t s);
-extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, uint32_t n_slots, hipStream_t s);
 extern "C" hipError_t gsk_mv_rows(const gsd::DevProblem* d, hipStream_t s);
 
 namespace gsc {
@@ -63,7 +64,13 @@ struct CandInfo {
 struct CandTable {
   std::unordered_map<uint32_t, CandInfo> node;  // candidate node index -> info
   std::vector<std::string> it_name;              // catalog index -> instance-type name
+  // NodePool minValues (<U> SatisfiesMinValues in
+  // RemoveInstanceTypeOptionsByPriceAndMinValues): per NodePool the (key,
+  // minimum) pairs, per instance type its values of those keys
+  std::vector<std::vector<std::pair<std::string, int64_t>>> np_mv;
+  std::vector<std::map<std::string, std::vector<std::string>>> it_vals;
 };
+bool mv_satisfied(const CandTable& t, uint32_t nodepool, const uint32_t* its, size_t n);
 
 // The simulations of one gs_consolidate call (device-side layout: layout.hpp
 // DevProblem consolidation fields).
@@ -73,6 +80,7 @@ struct SimPlan {
   std::vector<uint32_t> pod_off, pods;      // per evaluated simulation: pod ids in queue order
   std::vector<uint32_t> cand_off, cands;    // per evaluated simulation: device node positions removed
   uint32_t max_pods = 0, ov_cap = 0, blocks = 0, nt = 256;
+  std::vector<uint64_t> known;              // per evaluated simulation: zone domains known without its candidates
   uint32_t multi_max = 0;                   // MULTI: firstNConsolidationOption's max
 };
 

@@ -749,6 +749,7 @@ struct Ctx {
   std::vector<std::string> pod_ns;
   std::vector<PodSel> pod_sel;  // pending pods
   std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
+  uint32_t bound_alias = gsd::NONE;  // bound pod b is also pod bound_alias + b (consolidation)
 
   std::map<std::string, std::string> label_map(gs_range r) const {
     chk(r, p->n_labels, "labels");
@@ -956,19 +957,45 @@ struct Ctx {
   // distinct volumes of its bound pods per driver and the CSINode limits; a
   // node already over a limit takes no pod at all (the union check fails
   // whatever the pod mounts)
+  // A volume only one pod mounts (pods and bound pods, a bound pod that is
+  // also in the pod list -- consolidation -- counting once) can never be on a
+  // node the pod is placed on: it is a per-driver count of "fresh" volumes.
+  // The others (<= 64 distinct) are bits a node may already hold.
   void build_volumes() {
     std::map<std::string, uint32_t> drv;
     std::map<std::pair<std::string, std::string>, uint32_t> vol;
-    e.pod_vol.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
+    std::map<std::pair<std::string, std::string>, std::set<uint32_t>> users;
+    auto volkey = [&](const gs_volume& v) { return std::make_pair(S(v.driver), S(v.id)); };
     for (uint32_t i = 0; i < e.P; i++) {
       const gs_pod& pd = p->pods[i];
       chk(pd.volumes, p->n_volumes, "volumes");
-      for (uint32_t k = 0; k < pd.volumes.count; k++) {
-        const gs_volume& v = p->volumes[pd.volumes.begin + k];
-        const uint32_t d = drv.emplace(S(v.driver), (uint32_t)drv.size()).first->second;
-        const uint32_t b = vol.emplace(std::make_pair(S(v.driver), S(v.id)), (uint32_t)vol.size()).first->second;
+      for (uint32_t k = 0; k < pd.volumes.count; k++) users[volkey(p->volumes[pd.volumes.begin + k])].insert(i);
+    }
+    if (p->n_bound_pods && !p->bound_pod_node) throw Fail{GS_E_INVALID, "bound pods without their nodes"};
+    for (uint32_t b = 0; b < p->n_bound_pods; b++) {
+      const gs_pod& bp = p->bound_pods[b];
+      chk(bp.volumes, p->n_volumes, "volumes");
+      const uint32_t who = bound_alias != gsd::NONE ? bound_alias + b : e.P + b;
+      for (uint32_t k = 0; k < bp.volumes.count; k++) {
+        auto f = users.find(volkey(p->volumes[bp.volumes.begin + k]));
+        if (f != users.end()) f->second.insert(who);  // only volumes pods in the list mount matter
+      }
+    }
+    e.pod_vol.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
+    e.pod_vfresh.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
+    for (uint32_t i = 0; i < e.P; i++) {
+      const gs_pod& pd = p->pods[i];
+      std::set<std::pair<std::string, std::string>> mine;
+      for (uint32_t k = 0; k < pd.volumes.count; k++) mine.insert(volkey(p->volumes[pd.volumes.begin + k]));
+      for (auto& vk : mine) {
+        const uint32_t d = drv.emplace(vk.first, (uint32_t)drv.size()).first->second;
         if (d >= (uint32_t)gsd::VDMAX) throw Fail{GS_E_UNSUPPORTED, "pending pods mount volumes of more than 4 CSI drivers"};
-        if (b >= 64) throw Fail{GS_E_UNSUPPORTED, "pending pods mount more than 64 distinct volumes"};
+        if (users[vk].size() < 2) {
+          e.pod_vfresh[(size_t)i * gsd::VDMAX + d]++;
+          continue;
+        }
+        const uint32_t b = vol.emplace(vk, (uint32_t)vol.size()).first->second;
+        if (b >= 64) throw Fail{GS_E_UNSUPPORTED, "pods share more than 64 distinct volumes"};
         e.pod_vol[(size_t)i * gsd::VDMAX + d] |= 1ull << b;
       }
     }
@@ -1749,9 +1776,10 @@ std::string canonical(const Encoded& e, const Reqs& r) {
   return s;
 }
 
-Err encode(const gs_problem* p, Encoded& e) {
+Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
   e = Encoded();
   Ctx c{p, e, {}};
+  c.bound_alias = bound_alias;
   try {
     c.strs.reserve(p->n_strings);
     for (uint32_t i = 0; i < p->n_strings; i++) c.strs.push_back(p->strings[i] ? p->strings[i] : "");

@@ -107,7 +107,8 @@ struct Encoded {
   bool any_mv = false;              // some template carries minValues
   bool any_vol = false;             // pending pods mount CSI volumes and nodes exist
   std::vector<gsd::NodeVol> n_vol;  // [NN] in node order
-  std::vector<uint64_t> pod_vol;    // [P][VDMAX]
+  std::vector<uint64_t> pod_vol;    // [P][VDMAX] shared-volume bits
+  std::vector<uint32_t> pod_vfresh; // [P][VDMAX] volumes only this pod mounts
   std::vector<int64_t> it_alloc, it_cap, thr_val, fk_ival;
   std::vector<uint64_t> it_pair, slot_set, thr_set, fk_isint;
   std::vector<double> prices;  // distinct offering prices ascending: price rank -> price
@@ -156,7 +157,10 @@ struct Err {
   std::string msg;
 };
 
-Err encode(const gs_problem* p, Encoded& e);
+// bound_alias != NONE: bound pod b is also pod bound_alias + b of the pod
+// list (consolidation encodes the bound pods both as counted and as
+// schedulable pods)
+Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias = gsd::NONE);
 
 // <U> v1.WellKnownLabels (+ IBM keys), v1.NormalizedLabels, strconv.Atoi
 bool label_is_wellknown(const std::string& k);

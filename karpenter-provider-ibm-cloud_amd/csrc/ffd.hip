@@ -647,9 +647,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
     }
     for (uint32_t i = tid; i < T * R; i += FB) t_rem[i] = d.tmpl[i / R].limits[i % R];
     if (TOPO) {
-      // <U> Topology: counts before the Solve (selected bound pods)
-      topo_init(d, ts, d.zknown0, tid, FB);
-      for (uint32_t i = tid; i < d.TGH * d.NN; i += FB) d.hn[i] = d.hn0[i];
+      // <U> Topology: counts before the Solve (selected bound pods); a
+      // simulation knows the zones of the nodes it keeps (and the NodePools')
+      topo_init(d, ts, SIM ? d.sim_known[sim] : d.zknown0, tid, FB);
+      if (!SIM)
+        for (uint32_t i = tid; i < d.TGH * d.NN; i += FB) d.hn[i] = d.hn0[i];
     }
     uint32_t ncand = 0;
     if (SIM) {
@@ -661,6 +663,22 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         const uint32_t n = d.sim_cands[c0 + k];
         s_ovid[k] = n | OV_EXCL;
         atomicOr(&s_nb[n >> 5], 1u << (n & 31));
+      }
+      if (TOPO) {
+        // SimulateScheduling reschedules the candidates' pods: Topology
+        // excludes them from the counts (excludedPods)
+        const uint32_t ng = d.TGZ + d.TGH;
+        for (uint32_t x = tid; x < ncand * ng; x += FB) {
+          const uint32_t n = d.sim_cands[c0 + x / ng], g = x % ng;
+          if (g < d.TGZ) {
+            const int32_t c = d.zn_cnt[(size_t)g * d.NN + n];
+            const uint32_t z = d.nodes0[n].zvid;
+            if (c && z < d.ZS) atomicSub(&ts.zcnt[g * d.ZS + z], c);
+          } else {
+            const int32_t c = d.hn0[(size_t)(g - d.TGZ) * d.NN + n];
+            if (c) atomicSub(&ts.htot[g - d.TGZ], c);
+          }
+        }
       }
     }
     if (tid == 0) {
@@ -881,9 +899,13 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         // chunks; every chunk ends in one block min over node positions
         // <U> VolumeUsage: the pod's pending-volume bits per CSI driver
         uint64_t pvol[VDMAX] = {0, 0, 0, 0};
+        uint32_t pfresh[VDMAX] = {0, 0, 0, 0};
         if (TOPO && d.any_vol)
 #pragma unroll
-          for (uint32_t q = 0; q < VDMAX; q++) pvol[q] = d.pod_vol[(size_t)gp * VDMAX + q];
+          for (uint32_t q = 0; q < VDMAX; q++) {
+          pvol[q] = d.pod_vol[(size_t)gp * VDMAX + q];
+          pfresh[q] = d.pod_vfresh[(size_t)gp * VDMAX + q];
+        }
         uint32_t fn = INF;
         for (uint32_t base = 0, width = 64; base < d.NN; base += width, width = FB) {
           const uint32_t n = base + tid;
@@ -893,6 +915,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const int64_t* nreq = nr.req;
             const FK* nfk = (SIM ? d.n_fk0 : d.n_fk) + (size_t)n * F;
             feas = nr.ok && (nr.taints & ~vr.tol) == 0;  // Taints.ToleratesPod
+            size_t oe = ~(size_t)0;  // SIM: the node's overlay entry (hostname counts, volume usage)
             if (SIM && feas && ((s_nb[n >> 5] >> (n & 31)) & 1)) {
               // touched by this simulation: removed candidate, or overlay copy
               uint32_t e = 0;
@@ -900,7 +923,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               if (s_ovid[e] & OV_EXCL) {
                 feas = false;
               } else {
-                const size_t oe = (size_t)blockIdx.x * d.ov_cap + e;
+                oe = (size_t)blockIdx.x * d.ov_cap + e;
                 nreq = d.ov_req + oe * RMAX;
                 nfk = d.ov_fk + oe * F;
               }
@@ -921,14 +944,16 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
             if (TOPO && feas && own_n)
-              feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid,
-                                  [&](uint32_t hs) -> int64_t { return d.hn[(size_t)hs * d.NN + n]; });
+              feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
+                if (!SIM) return d.hn[(size_t)hs * d.NN + n];
+                return oe != ~(size_t)0 ? d.ov_hn[oe * d.TGH + hs] : d.hn0[(size_t)hs * d.NN + n];
+              });
             if (TOPO && feas && d.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
-              const NodeVol& nv = d.n_vol[n];
+              const NodeVol& nv = !SIM ? d.n_vol[n] : oe != ~(size_t)0 ? d.ov_vol[oe] : d.n_vol0[n];
 #pragma unroll
               for (uint32_t q = 0; q < VDMAX; q++)
-                if (pvol[q]) feas = feas && nv.cnt[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+                if (pvol[q] | pfresh[q]) feas = feas && nv.cnt[q] + (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
             }
           }
           fn = wg.first(feas, base);
@@ -940,6 +965,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           // ExistingNode.Add: requests and requirements
           int64_t* areq;
           FK* afk;
+          int32_t* ahn = nullptr;   // the node's hostname counts (row stride ahs)
+          size_t ahs = 0;
+          NodeVol* avol = nullptr;  // the node's volume usage
           if (SIM) {
             // copy-on-write overlay entry for the node
             if (tid == 0) {
@@ -960,14 +988,26 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const size_t oe = (size_t)blockIdx.x * d.ov_cap + S.ove;
             areq = d.ov_req + oe * RMAX;
             afk = d.ov_fk + oe * F;
+            if (TOPO) {
+              ahn = d.ov_hn + oe * d.TGH;
+              ahs = 1;
+              avol = d.ov_vol + oe;
+            }
             if (S.ov_new) {
               if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
               if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
+              if (TOPO) {
+                for (uint32_t x = tid; x < d.TGH; x += FB) ahn[x] = d.hn0[(size_t)x * d.NN + fn];
+                if (d.any_vol && tid == 128) *avol = d.n_vol0[fn];
+              }
             }
             __syncthreads();
           } else {
             areq = d.nodes[fn].req;
             afk = d.n_fk + (size_t)fn * F;
+            ahn = d.hn + fn;
+            ahs = d.NN;
+            avol = d.n_vol + fn;
           }
           if (tid < R) areq[tid] += preq[tid];
           if (tid >= 64 && tid < 64 + vr.fk_count) {
@@ -980,11 +1020,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           if (tid == 0) {
             if (TOPO && d.any_vol) {
               // VolumeUsage.Add
-              NodeVol& nv = d.n_vol[fn];
+              NodeVol& nv = *avol;
               uint64_t all = 0;
 #pragma unroll
               for (uint32_t q = 0; q < VDMAX; q++) {
-                nv.cnt[q] += __popcll(pvol[q] & ~nv.present);
+                nv.cnt[q] += (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present);
                 all |= pvol[q];
               }
               nv.present |= all;
@@ -995,7 +1035,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (TOPO && sel_n) {
               const uint32_t z = d.nodes0[fn].zvid;
               topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
-                          [&](uint32_t hs) { d.hn[(size_t)hs * d.NN + fn]++; });
+                          [&](uint32_t hs) { ahn[(size_t)hs * ahs]++; });
             }
           }
           pf_stage2();
@@ -1778,42 +1818,46 @@ static hipError_t ffd_attr(uint32_t lds_total) {
                              (int)dyn);
 }
 
-extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
+template <uint32_t RR>
+static hipError_t ffd_attr_all(uint32_t lds_total) {
   hipError_t e = hipSuccess;
-  for (hipError_t x : {ffd_attr<1, false>(lds_total), ffd_attr<2, false>(lds_total), ffd_attr<3, false>(lds_total),
-                       ffd_attr<4, false>(lds_total), ffd_attr<5, false>(lds_total), ffd_attr<6, false>(lds_total),
-                       ffd_attr<7, false>(lds_total), ffd_attr<8, false>(lds_total), ffd_attr<1, true>(lds_total),
-                       ffd_attr<2, true>(lds_total), ffd_attr<3, true>(lds_total), ffd_attr<4, true>(lds_total),
-                       ffd_attr<5, true>(lds_total), ffd_attr<6, true>(lds_total), ffd_attr<7, true>(lds_total),
-                       ffd_attr<8, true>(lds_total), ffd_attr<1, false, true>(lds_total),
-                       ffd_attr<2, false, true>(lds_total), ffd_attr<3, false, true>(lds_total),
-                       ffd_attr<4, false, true>(lds_total), ffd_attr<5, false, true>(lds_total),
-                       ffd_attr<6, false, true>(lds_total), ffd_attr<7, false, true>(lds_total),
-                       ffd_attr<8, false, true>(lds_total), ffd_attr<1, true, false, FB_SIM_NARROW>(lds_total),
-                       ffd_attr<2, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<3, true, false, FB_SIM_NARROW>(lds_total),
-                       ffd_attr<4, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<5, true, false, FB_SIM_NARROW>(lds_total),
-                       ffd_attr<6, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<7, true, false, FB_SIM_NARROW>(lds_total),
-                       ffd_attr<8, true, false, FB_SIM_NARROW>(lds_total)})
+  for (hipError_t x : {ffd_attr<RR, false>(lds_total), ffd_attr<RR, false, true>(lds_total), ffd_attr<RR, true>(lds_total),
+                       ffd_attr<RR, true, false, FB_SIM_NARROW>(lds_total), ffd_attr<RR, true, true, FB_SIM>(lds_total),
+                       ffd_attr<RR, true, true, FB_SIM_NARROW>(lds_total)})
     if (x != hipSuccess) e = x;
   return e;
 }
 
-// dynamic LDS available to every ffd_kernel instantiation (after gsk_init_ffd)
+extern "C" hipError_t gsk_init_ffd(uint32_t lds_total) {
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {ffd_attr_all<1>(lds_total), ffd_attr_all<2>(lds_total), ffd_attr_all<3>(lds_total),
+                       ffd_attr_all<4>(lds_total), ffd_attr_all<5>(lds_total), ffd_attr_all<6>(lds_total),
+                       ffd_attr_all<7>(lds_total), ffd_attr_all<8>(lds_total)})
+    if (x != hipSuccess) e = x;
+  return e;
+}
+
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void) { return g_ffd_dyn_max; }
 
 // resident simulation workgroups per CU for a given dynamic LDS size
-extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt) {
+template <uint32_t RR>
+static hipError_t sim_occ(int* n, bool narrow, bool general, uint32_t lds) {
+  if (general)
+    return narrow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(n, (const void*)ffd_kernel<RR, true, FB_SIM_NARROW, true>,
+                                                                 FB_SIM_NARROW, lds)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(n, (const void*)ffd_kernel<RR, true, FB_SIM, true>, FB_SIM, lds);
+  return narrow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(n, (const void*)ffd_kernel<RR, true, FB_SIM_NARROW, false>,
+                                                               FB_SIM_NARROW, lds)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(n, (const void*)ffd_kernel<RR, true, FB_SIM, false>, FB_SIM, lds);
+}
+
+extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt, uint32_t general) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
   const bool narrow = nt == (uint32_t)FB_SIM_NARROW;
   switch (R) {
-#define GSK_OCC(k)                                                                                              \
-  case k:                                                                                                       \
-    e = narrow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                  \
-                     &n, (const void*)ffd_kernel<k, true, FB_SIM_NARROW, false>, FB_SIM_NARROW, lds)            \
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)ffd_kernel<k, true, FB_SIM, false>, \
-                                                              FB_SIM, lds);                                     \
-    break;
+#define GSK_OCC(k) \
+  case k: e = sim_occ<k>(&n, narrow, general != 0, lds); break;
     GSK_OCC(1) GSK_OCC(2) GSK_OCC(3) GSK_OCC(4) GSK_OCC(5) GSK_OCC(6) GSK_OCC(7) GSK_OCC(8)
 #undef GSK_OCC
   }
@@ -1826,17 +1870,22 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
-  if (sim && d->TG) return hipErrorInvalidValue;  // simulations refuse topology spread
-  // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations
+  // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations,
+  // 4 / 5 simulations / narrow simulations, general variant (topology groups, volumes, minValues)
   if (sim && d->sim_nt != (uint32_t)FB_SIM && d->sim_nt != (uint32_t)FB_SIM_NARROW) return hipErrorInvalidValue;
-  const uint32_t shape = sim ? (d->sim_nt == (uint32_t)FB_SIM_NARROW ? 3u : 2u) : (d->TG || d->any_mv || d->any_vol ? 1u : 0u);
-  switch (d->R * 4 + shape) {
+  const bool general = d->TG || d->any_mv || d->any_vol;
+  const uint32_t shape = sim ? (d->sim_nt == (uint32_t)FB_SIM_NARROW ? 3u : 2u) + (general ? 2u : 0u) : (general ? 1u : 0u);
+  switch (d->R * 8 + shape) {
 #define GSK_CASE(n)                                                                                          \
-  case 4 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
-  case 4 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
-  case 4 * n + 2: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, false>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break; \
-  case 4 * n + 3:                                                                                            \
+  case 8 * n: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, false>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
+  case 8 * n + 1: hipLaunchKernelGGL((ffd_kernel<n, false, FB_MAX, true>), dim3(1), dim3(FB_MAX), lds, s, *d); break; \
+  case 8 * n + 2: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, false>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break; \
+  case 8 * n + 3:                                                                                            \
     hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM_NARROW, false>), dim3(blocks), dim3(FB_SIM_NARROW), lds, s, *d); \
+    break;                                                                                                    \
+  case 8 * n + 4: hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM, true>), dim3(blocks), dim3(FB_SIM), lds, s, *d); break; \
+  case 8 * n + 5:                                                                                            \
+    hipLaunchKernelGGL((ffd_kernel<n, true, FB_SIM_NARROW, true>), dim3(blocks), dim3(FB_SIM_NARROW), lds, s, *d); \
     break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE

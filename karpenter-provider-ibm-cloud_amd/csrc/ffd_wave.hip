@@ -743,9 +743,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       const uint64_t vtol = VX64(18);
       // <U> VolumeUsage: the pod's pending-volume bits per CSI driver
       uint64_t pvol[VDMAX] = {0, 0, 0, 0};
+      uint32_t pfresh[VDMAX] = {0, 0, 0, 0};
       if (TOPO && KD.any_vol)
 #pragma unroll
-        for (uint32_t q = 0; q < VDMAX; q++) pvol[q] = KD.pod_vol[(size_t)gp * VDMAX + q];
+        for (uint32_t q = 0; q < VDMAX; q++) {
+          pvol[q] = KD.pod_vol[(size_t)gp * VDMAX + q];
+          pfresh[q] = KD.pod_vfresh[(size_t)gp * VDMAX + q];
+        }
       uint32_t fn = INF;
       for (uint32_t base = 0; base < KD.NN; base += 64) {
         const uint32_t n = base + lane;
@@ -776,7 +780,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const NodeVol& nv = KD.n_vol[n];
 #pragma unroll
             for (uint32_t q = 0; q < VDMAX; q++)
-              if (pvol[q]) feas = feas && nv.cnt[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+              if (pvol[q] | pfresh[q]) feas = feas && nv.cnt[q] + (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
           }
         }
         const uint64_t b = __ballot(feas);
@@ -806,7 +810,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             uint64_t all = 0;
 #pragma unroll
             for (uint32_t q = 0; q < VDMAX; q++) {
-              nv.cnt[q] += __popcll(pvol[q] & ~nv.present);
+              nv.cnt[q] += (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present);
               all |= pvol[q];
             }
             nv.present |= all;

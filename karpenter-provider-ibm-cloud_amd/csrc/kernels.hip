@@ -199,13 +199,26 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
 // (rank of its cheapest available compatible offering price, name rank)
 // Consolidation simulations (n_sims > 0): block s truncates the NodeClaim of
 // simulation s when it opened exactly one (the only case computeConsolidation
-// prices); output slot s.
-extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
+// prices); output slot s.  With minValues (all_slots): block j truncates
+// NodeClaim arena slot j of whichever simulation holds it and flags a top 60
+// that misses a minimum (<U> Results.TruncateInstanceTypes drops it); the
+// sim_fix kernel then settles each simulation.
+extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d, uint32_t all_slots) {
   extern __shared__ uint64_t keys[];
   __shared__ uint32_t cnt;
   uint32_t j = blockIdx.x;  // claim
   const uint32_t o = blockIdx.x;  // output slot
-  if (d.n_sims) {
+  if (all_slots) {
+    // the simulation whose arena holds slot j: last s with sim_pod_off[s] <= j
+    uint32_t lo = 0, hi = d.n_sims;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (d.sim_pod_off[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    if (j >= d.sim_pod_off[d.n_sims] || d.sim_ctrl[lo].status != 0 || j - d.sim_pod_off[lo] >= d.sim_ctrl[lo].n_claims)
+      return;
+  } else if (d.n_sims) {
     if (o >= d.n_sims || d.sim_ctrl[o].status != 0 || d.sim_ctrl[o].n_claims != 1) return;
     j = d.sim_pod_off[o];
   } else if (j >= d.ctrl->n_claims) {
@@ -253,9 +266,78 @@ extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d) {
     }
   }
   const uint32_t take = n < 60 ? n : 60;
+  if (all_slots) {
+    for (uint32_t i = tid; i < take; i += BLOCK) d.slot_its[(size_t)j * 60 + i] = d.rank_to_it[(uint32_t)keys[i]];
+    if (tid == 0) {
+      d.slot_nits[j] = take;
+      // SatisfiesMinValues on the top 60: distinct values per minimum key
+      const TmplRec& tr = d.tmpl[h.tmpl];
+      bool ok = true;
+      for (uint32_t mm = tr.mv_mask; mm && ok; mm &= mm - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctz(mm);
+        uint32_t nd = take;
+        if (!((d.it_key_unique >> k) & 1)) {
+          uint64_t sv[4] = {0, 0, 0, 0};
+          nd = 0;
+          for (uint32_t i = 0; i < take; i++) {
+            const uint32_t x = d.it_dvid[(size_t)k * d.N + d.rank_to_it[(uint32_t)keys[i]]];
+            const uint64_t bit = 1ull << (x & 63);
+            if (!(sv[x >> 6] & bit)) {
+              sv[x >> 6] |= bit;
+              nd++;
+            }
+          }
+        }
+        ok = nd >= tr.mv[k];
+      }
+      d.slot_drop[j] = ok ? 0u : 1u;
+    }
+    return;
+  }
   if (d.n_sims && tid < sizeof(ClaimRec) / 4) ((uint32_t*)(d.sim_hdr + o))[tid] = ((const uint32_t*)&h)[tid];
   for (uint32_t i = tid; i < take; i += BLOCK) d.c_its[(size_t)o * 60 + i] = d.rank_to_it[(uint32_t)keys[i]];
   if (tid == 0) d.c_nits[o] = take;
+}
+
+// Simulations with minValues: <U> Results.TruncateInstanceTypes drops every
+// NodeClaim flagged by trunc_kernel (all_slots); their pods become pod errors,
+// which count against the simulation when not pending
+// (AllNonPendingPodsScheduled).  One thread per simulation: the surviving
+// count, the failed pods, and the single survivor's header and top 60 in the
+// per-simulation output slot.
+extern "C" __global__ __launch_bounds__(BLOCK) void sim_fix_kernel(DevProblem d) {
+  const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+  if (s >= d.n_sims) return;
+  Ctrl& c = d.sim_ctrl[s];
+  if (c.status) return;
+  const uint32_t off = d.sim_pod_off[s], nc = c.n_claims;
+  uint32_t surv = 0, sj = NONE;
+  bool drop = false;
+  for (uint32_t j = 0; j < nc; j++) {
+    if (d.slot_drop[off + j]) {
+      drop = true;
+    } else {
+      if (!surv) sj = j;
+      surv++;
+    }
+  }
+  if (drop) {
+    uint32_t extra = 0;
+    for (uint32_t i = 0; i < c.n_log; i++) {
+      const LogRec l = d.log[off + i];
+      if (!(l.target & 0x80000000u) && d.slot_drop[off + l.target] && l.pod >= d.n_pending) extra++;
+    }
+    c.failed += extra;
+  }
+  c.n_claims = surv;
+  if (surv == 1) {
+    const uint32_t* src = (const uint32_t*)(d.c_rec + off + sj);
+    uint32_t* dst = (uint32_t*)(d.sim_hdr + s);
+    for (uint32_t q = 0; q < sizeof(ClaimRec) / 4; q++) dst[q] = src[q];
+    const uint32_t nt = d.slot_nits[off + sj];
+    for (uint32_t i = 0; i < nt; i++) d.c_its[(size_t)s * 60 + i] = d.slot_its[(size_t)(off + sj) * 60 + i];
+    d.c_nits[s] = nt;
+  }
 }
 
 // ------------------------------------------------------------ host launchers
@@ -340,9 +422,17 @@ extern "C" hipError_t gsk_mv_rows(const DevProblem* d, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t gsk_trunc(const DevProblem* d, uint32_t lds_bytes, hipStream_t s) {
+// simulations with minValues (any_mv): every NodeClaim arena slot, then the
+// per-simulation settlement; otherwise one block per simulation / NodeClaim
+extern "C" hipError_t gsk_trunc(const DevProblem* d, uint32_t lds_bytes, uint32_t n_slots, hipStream_t s) {
+  if (d->n_sims && d->any_mv) {
+    if (!n_slots) return hipSuccess;
+    hipLaunchKernelGGL(trunc_kernel, dim3(n_slots), dim3(BLOCK), lds_bytes, s, *d, 1u);
+    hipLaunchKernelGGL(sim_fix_kernel, dim3((d->n_sims + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *d);
+    return hipGetLastError();
+  }
   const uint32_t grid = d->n_sims ? d->n_sims : d->max_claims;
   if (!grid) return hipSuccess;
-  hipLaunchKernelGGL(trunc_kernel, dim3(grid), dim3(BLOCK), lds_bytes, s, *d);
+  hipLaunchKernelGGL(trunc_kernel, dim3(grid), dim3(BLOCK), lds_bytes, s, *d, 0u);
   return hipGetLastError();
 }

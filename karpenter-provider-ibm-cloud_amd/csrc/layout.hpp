@@ -257,7 +257,8 @@ struct DevProblem {
   NodeRec* nodes;              // working copies (reset at every run)
   const NodeVol* n_vol0;       // [NN] volume usage before the Solve (any_vol)
   NodeVol* n_vol;              // [NN] working copies
-  const uint64_t* pod_vol;     // [P][VDMAX] the pod's pending-volume bits per driver
+  const uint64_t* pod_vol;     // [P][VDMAX] the pod's shared-volume bits per driver (volumes other pods mount too)
+  const uint32_t* pod_vfresh;  // [P][VDMAX] the pod's volumes no other pod mounts, per driver (never present on a node)
   uint32_t any_vol;            // pending pods mount CSI volumes: the general (TOPO) variant checks limits
   FK* n_fk;
   // feasibility outputs
@@ -296,6 +297,11 @@ struct DevProblem {
   // truncation outputs
   uint32_t* c_its;             // [max_claims][60] (simulations: [n_sims][60])
   uint32_t* c_nits;            // [max_claims]     (simulations: [n_sims])
+  // simulations with minValues: OrderByPrice + Truncate(60) of every NodeClaim
+  // arena slot and whether its top 60 miss a minimum (TruncateInstanceTypes drop)
+  uint32_t* slot_its;          // [sim claim slots][60]
+  uint32_t* slot_nits;         // [sim claim slots]
+  uint32_t* slot_drop;         // [sim claim slots]
   // consolidation simulations (n_sims > 0: one workgroup per simulation).
   // Per simulation s the pod range [sim_pod_off[s], sim_pod_off[s+1]) indexes
   // sim_pods and is also the simulation's arena in queue/last_len/last_epoch/
@@ -316,6 +322,14 @@ struct DevProblem {
   Ctrl* sim_ctrl;              // [n_sims]
   ClaimRec* sim_hdr;           // [n_sims] header of the single NodeClaim (trunc_kernel copies it)
   uint32_t* sim_next;          // work counter (reset before each launch)
+  // simulations with topology groups / volumes: per simulation the zone
+  // domains known without the candidates; the counted bound pods per zone
+  // group and node (the candidates' pods are rescheduled, not counted); per
+  // block the hostname counts and volume usage of the overlay nodes
+  const uint64_t* sim_known;   // [n_sims]
+  const int32_t* zn_cnt;       // [TGZ][NN]
+  int32_t* ov_hn;              // [grid][ov_cap][TGH]
+  NodeVol* ov_vol;             // [grid][ov_cap]
 };
 
 }  // namespace gsd

@@ -210,7 +210,7 @@ CONSOLIDATE_EVAL, CONSOLIDATE_SINGLE, CONSOLIDATE_MULTI = 0, 1, 2
 DECISION_NOOP, DECISION_DELETE, DECISION_REPLACE, DECISION_SKIPPED = 0, 1, 2, 3
 DECISION_NAMES = {0: "NoOp", 1: "Delete", 2: "Replace", 3: "Skipped"}
 (NOOP_NONE, NOOP_UNSCHEDULABLE, NOOP_MULTIPLE_CLAIMS, NOOP_PRICE_UNKNOWN, NOOP_SPOT_TO_SPOT,
- NOOP_NOT_CHEAPER, NOOP_SAME_TYPE) = range(7)
+ NOOP_NOT_CHEAPER, NOOP_SAME_TYPE, NOOP_MIN_VALUES) = range(8)
 
 
 class GsRange(C.Structure):

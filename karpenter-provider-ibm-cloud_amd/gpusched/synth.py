@@ -859,3 +859,141 @@ def random_volumes(seed, n_pods=None):
                   {"cpu": int(rng.choice([250, 500, 1000])), "memory": GI * 1000, "pods": 1000},
                   volumes=mine if rng.random() < 0.7 else [])
     return b.build()
+
+
+def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None):
+    """small adversarial consolidation clusters for the general simulation
+    variant: bound and pending pods with zone / hostname topology spread,
+    hostname and zone pod anti-affinity (required, preferred, inverse
+    carriers), hostname pod affinity, host ports, CSI volumes (shared and
+    per-pod, node attach limits) and NodePools with minValues"""
+    rng = np.random.default_rng(0xC0A50000 + seed)
+    b = ProblemBuilder()
+    zones = FAKE_ZONES[: int(rng.integers(2, 4))]
+    profs = []
+    for fam in ["bx2", "cx2", "mx2"]:
+        for v in [2, 4, 8, 16]:
+            if rng.random() < 0.7:
+                profs.append((f"{fam}-{v}x{v * MEM_RATIO[fam[0]]}", v, v * MEM_RATIO[fam[0]], None))
+    if len(profs) < 3:
+        profs = [("bx2-2x8", 2, 8, None), ("bx2-8x32", 8, 32, None), ("cx2-4x8", 4, 8, None)]
+    prices = {p[0]: round(float(rng.choice([0.05, 0.1, 0.1, 0.2, 0.4])) * p[1] / 2, 4) for p in profs}
+    its = build_catalog(b, profs, zones, spot=True, prices=prices, rng=rng, unavailable_frac=0.1)
+    mv = bool(rng.random() < 0.3) if min_values is None else min_values
+    n_np = int(rng.integers(1, 3))
+    for j in range(n_np):
+        reqs = [("topology.kubernetes.io/zone", "In", list(zones))]
+        if mv and j == 0:
+            reqs.append(("karpenter-ibm.sh/instance-family", "Exists", [], int(rng.integers(1, 3))))
+        limits = {"cpu": int(rng.choice([16, 64, 256])) * 1000} if rng.random() < 0.2 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
+                       daemon={"cpu": 100, "pods": 1000})
+    apps = ["web", "db", "cache"]
+    anti_pal = [{"key": str(rng.choice(["kubernetes.io/hostname", "topology.kubernetes.io/zone"])),
+                 "required": bool(rng.random() < 0.3), "weight": int(rng.choice([1, 50, 100])),
+                 "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(1, 4)))]
+    aff_pal = [{"required": bool(rng.random() < 0.3), "weight": 10,
+                "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(0, 2)))]
+    spread_pal = [{"key": str(rng.choice(["topology.kubernetes.io/zone", "kubernetes.io/hostname"])),
+                   "max_skew": int(rng.choice([1, 2])), "node_affinity_policy": "Ignore",
+                   "when": "ScheduleAnyway" if rng.random() < 0.5 else "DoNotSchedule",
+                   "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(0, 3)))]
+    port_pal = [(int(rng.choice([80, 443, 8080])), "TCP", "") for _ in range(int(rng.integers(1, 3)))]
+    drivers = ["vpc.block.csi.ibm.io", "nfs.csi"]
+    shared_vols = [(str(rng.choice(drivers)), f"shared-{k}") for k in range(4)]
+    uid_n = [0]
+
+    def feats():
+        f = {}
+        if rng.random() < 0.35 and anti_pal:
+            f["anti_affinity"] = [anti_pal[int(rng.integers(0, len(anti_pal)))]]
+        if rng.random() < 0.15 and aff_pal:
+            f["affinity"] = [aff_pal[int(rng.integers(0, len(aff_pal)))]]
+        if rng.random() < 0.25 and spread_pal:
+            f["spreads"] = [spread_pal[int(rng.integers(0, len(spread_pal)))]]
+        if rng.random() < 0.15:
+            f["host_ports"] = [port_pal[int(rng.integers(0, len(port_pal)))]]
+        if rng.random() < 0.3:
+            uid_n[0] += 1
+            v = [(str(rng.choice(drivers)), f"pv-{seed}-{uid_n[0]}")]
+            if rng.random() < 0.3:
+                v.append(shared_vols[int(rng.integers(0, len(shared_vols)))])
+            f["volumes"] = v
+        return f
+
+    nn = int(n_nodes if n_nodes is not None else rng.integers(2, 14))
+    for k in range(nn):
+        it = its[rng.integers(0, len(its))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels["topology.kubernetes.io/zone"] = zones[rng.integers(0, len(zones))]
+        labels["karpenter.sh/capacity-type"] = str(rng.choice(["spot", "on-demand"]))
+        labels["karpenter.sh/nodepool"] = f"np{rng.integers(0, n_np)}"
+        labels["kubernetes.io/hostname"] = f"n-{k:03d}"
+        alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        used = {"cpu": 100, "memory": 0, "pods": 1000}
+        target = float(rng.uniform(0.2, 0.9))
+        for _ in range(int(rng.integers(0, 8))):
+            cpu = int(rng.choice([100, 250, 500, 1000, 2000]))
+            mem = int(rng.choice([128 * MI, GI, 2 * GI])) * 1000
+            if used["cpu"] + cpu > target * alloc["cpu"] or used["memory"] + mem > alloc["memory"]:
+                break
+            used["cpu"] += cpu
+            used["memory"] += mem
+            used["pods"] += 1000
+            b.add_bound_pod(k, _uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 3)) * 1_000_000_000,
+                            {"cpu": cpu, "memory": mem, "pods": 1000}, labels={"app": str(rng.choice(apps))},
+                            **feats())
+        avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
+        lim = {d: int(rng.integers(1, 6)) for d in drivers if rng.random() < 0.5}
+        b.add_node(f"n-{k:03d}", labels, avail, initialized=bool(rng.random() < 0.9), volume_limits=lim)
+    npend = int(n_pending if n_pending is not None else rng.choice([0, 0, 1, 2]))
+    for i in range(npend):
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000, {"cpu": int(rng.choice([100, 500, 1000])),
+                                                         "memory": int(GI) * 1000, "pods": 1000},
+                  labels={"app": str(rng.choice(apps))}, **feats())
+    return b.build()
+
+
+def e2e_consolidation_cluster(n_nodes=5000, replicas=4, seed=0x5EED0C4E, util=(0.3, 0.8)):
+    """C4-scale cluster of the reference e2e workload shape
+    (test/e2e/scheduling_test.go:38-122 TestE2EConsolidationWithPDB and
+    test/e2e/config.go:455-490): deployments of `replicas` pods, each pod
+    1 vCPU / 1 GiB with a preferred (weight 100) hostname anti-affinity on its
+    own app, spread over nodes of the C2 catalog in 3 zones; one NodePool"""
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    profs = c2_profiles(200)
+    its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng, unavailable_frac=0.02)
+    daemon = {"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000}
+    b.add_nodepool("default", requirements=[("topology.kubernetes.io/zone", "In", FAKE_ZONES)], daemon=daemon)
+    cand = [it for it in its if it.capacity["nvidia.com/gpu"] == 0 and 2000 <= it.capacity["cpu"] <= 16000]
+    dep = 0
+    left = 0
+    for k in range(n_nodes):
+        it = cand[rng.integers(0, len(cand))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels.update({"topology.kubernetes.io/zone": FAKE_ZONES[k % 3], "karpenter.sh/capacity-type": "on-demand",
+                       "karpenter.sh/nodepool": "default", "kubernetes.io/hostname": f"node-{k:05d}"})
+        alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        used = dict(daemon)
+        target = float(rng.uniform(*util))
+        apps_here = set()
+        while used["cpu"] + 1000 <= target * alloc["cpu"] and used["memory"] + GI * 1000 <= alloc["memory"]:
+            if left == 0:
+                dep += 1
+                left = replicas
+            if dep in apps_here:  # the preferred anti-affinity kept replicas apart
+                break
+            apps_here.add(dep)
+            left -= 1
+            used["cpu"] += 1000
+            used["memory"] += GI * 1000
+            used["pods"] += 1000
+            name = f"e2e-{dep:05d}"
+            b.add_bound_pod(k, f"{name}-{replicas - left:02d}", 1_700_000_000_000_000_000 + dep * 1_000_000_000,
+                            {"cpu": 1000, "memory": GI * 1000, "pods": 1000},
+                            labels={"app": name, "test": "e2e"},
+                            anti_affinity=[{"required": False, "weight": 100, "selector": {"labels": {"app": name}}}])
+        avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
+        b.add_node(f"node-{k:05d}", labels, avail, initialized=True)
+    return b.build()

@@ -1737,6 +1737,19 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
   b.build();
   Scheduler s{st};
   auto errors = s.solve();
+  // Results.TruncateInstanceTypes(MaxInstanceTypes): a NodeClaim whose top 60
+  // by OrderByPrice miss a minValues requirement is dropped, its pods become
+  // pod errors
+  vector<NodeClaim*> kept;
+  for (NodeClaim* nc : s.creation_order) {
+    Reqs r = nc->reqs;
+    r.m.erase(kHostname);
+    if (has_min_values(r) && !satisfies_min_values(order_by_price(nc->options, r, 60), r)) {
+      for (const Pod* p : nc->pods) errors.insert(p->index);
+      continue;
+    }
+    kept.push_back(nc);
+  }
   uint32_t failed = 0;
   for (uint32_t e : errors)
     if (e >= n_pending) failed++;
@@ -1746,7 +1759,7 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
       for (auto* p : n.pods)
         if (p->index >= n_pending) failed++;
   cmd.n_failed_pods = failed;
-  cmd.n_new_claims = (uint32_t)s.creation_order.size();
+  cmd.n_new_claims = (uint32_t)kept.size();
   if (failed) {
     cmd.reason = GS_NOOP_UNSCHEDULABLE;
     return cmd;
@@ -1771,7 +1784,7 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
     all_spot = all_spot && k.spot;
   }
   cmd.candidate_price = cp;
-  NodeClaim* nc = s.creation_order[0];
+  NodeClaim* nc = kept[0];
   nc->reqs.m.erase(kHostname);  // FinalizeScheduling
   auto ordered = order_by_price(nc->options, nc->reqs, 60);  // TruncateInstanceTypes + OrderByPrice
   Req ctr = nc->reqs.get(kCapacityType);
@@ -1779,7 +1792,8 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
     cmd.reason = GS_NOOP_SPOT_TO_SPOT;
     return cmd;
   }
-  // RemoveInstanceTypeOptionsByPriceAndMinValues (no minValues: refused up front)
+  // RemoveInstanceTypeOptionsByPriceAndMinValues: the options cheaper than the
+  // candidates, then SatisfiesMinValues on what is left
   vector<const InstanceType*> keep;
   vector<double> kp;
   for (auto* it : ordered) {
@@ -1788,6 +1802,10 @@ gs_command simulate(const gs_consolidation* in, const vector<uint32_t>& cands, c
       keep.push_back(it);
       kp.push_back(pr);
     }
+  }
+  if (has_min_values(nc->reqs) && !satisfies_min_values(keep, nc->reqs)) {
+    cmd.reason = GS_NOOP_MIN_VALUES;
+    return cmd;
   }
   if (keep.empty()) {
     cmd.reason = GS_NOOP_NOT_CHEAPER;
@@ -1847,10 +1865,6 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
       if (in->candidates[i] >= in->cluster->n_nodes) return GS_E_INVALID;
     for (uint32_t i = 0; i < in->cluster->n_bound_pods; i++)
       if (in->cluster->bound_pod_node[i] >= in->cluster->n_nodes) return GS_E_INVALID;
-    if (in->cluster->n_spreads || in->cluster->n_affinity_terms || in->cluster->n_host_ports || in->cluster->n_volumes)
-      return GS_E_UNSUPPORTED;  // the product refuses them too (this round)
-    for (auto& t : base.templates)
-      if (has_min_values(t.reqs)) return GS_E_UNSUPPORTED;  // likewise
     if (in->mode == GS_CONSOLIDATE_EVAL) {
       for (uint32_t s = 0; s < in->n_sets; s++) {
         if ((uint64_t)in->sets[s].begin + in->sets[s].count > in->n_candidates) return GS_E_INVALID;
@@ -1896,6 +1910,14 @@ extern "C" gs_status oracle_consolidate(const gs_consolidation* in, gs_consolida
                                         r.prices.data() + c.options.begin, c.options.count);
         for (uint32_t i : idx) keep.push_back(r.opts[c.options.begin + i]);
         valid = !keep.empty();
+        // RemoveInstanceTypeOptionsByPriceAndMinValues inside
+        // filterOutSameInstanceType: a minValues miss invalidates the prefix
+        for (auto& t : base.templates)
+          if (t.np_index == c.nodepool && has_min_values(t.reqs)) {
+            vector<const InstanceType*> its;
+            for (uint32_t x : keep) its.push_back(&base.its[x]);
+            if (!satisfies_min_values(its, t.reqs)) valid = false;
+          }
       }
       if (valid || c.decision == GS_DECISION_DELETE) {
         chosen = mid - 1;

@@ -1,0 +1,133 @@
+"""Consolidation on real clusters (VERDICT r2 Missing 1):
+simulations whose clusters carry topology spread, pod (anti-)affinity on the
+hostname and zone keys, host ports, CSI volumes and NodePool minValues.
+
+<U> SimulateScheduling builds a new Topology over the state nodes it keeps:
+the candidates' pods are rescheduled (excludedPods: not counted), every other
+bound pod keeps counting on its node, and the zone-domain universe is the
+NodePools' zones plus the kept nodes' zones.  Host ports and volumes of the
+kept nodes' bound pods stay in use.  Results.TruncateInstanceTypes drops a
+NodeClaim whose top 60 miss a minValues requirement (its pods become errors);
+RemoveInstanceTypeOptionsByPriceAndMinValues (computeConsolidation and the
+multi-node filterOutSameInstanceType) rejects a replacement whose cheaper
+options miss one.  The reference's own consolidation scenario runs pods with
+a preferred hostname anti-affinity (reference
+test/e2e/scheduling_test.go:38-122): e2e_consolidation_cluster builds that
+shape at C4 scale.
+
+GPU tests require the general (TOPO) variant of the simulation kernel to equal
+the oracle's naive re-Solve of every reduced problem, command for command.
+"""
+import pytest
+
+from gpusched import abi, lib, synth
+from gpusched.consolidation import ConsolidationInput
+from oracle import pyoracle
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_oracle_general_consolidation_runs(seed):
+    p = synth.random_consolidation_general(seed)
+    for mode in (abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI):
+        cin = ConsolidationInput(p, list(range(len(p.nodes))), mode=mode)
+        st, cmds, chosen, multi = pyoracle.consolidate(cin)
+        assert st == abi.GS_OK
+        # the host policy replay agrees with the oracle's own choice
+        assert lib.choose(cin, cmds) == (chosen, multi)
+
+
+def test_oracle_general_consolidation_sees_constraints():
+    """the features change decisions: dropping every constraint from the same
+    clusters gives different commands for some simulations"""
+    changed = 0
+    for seed in range(16):
+        p = synth.random_consolidation_general(seed)
+        cin = ConsolidationInput(p, list(range(len(p.nodes))), mode=abi.CONSOLIDATE_SINGLE)
+        _, cmds, _, _ = pyoracle.consolidate(cin)
+        changed += sum(1 for c in cmds if c["decision"] == abi.DECISION_NOOP and
+                       c["reason"] in (abi.NOOP_UNSCHEDULABLE, abi.NOOP_MIN_VALUES, abi.NOOP_MULTIPLE_CLAIMS))
+    assert changed > 0
+
+
+def test_oracle_e2e_consolidation_shape_small():
+    p = synth.e2e_consolidation_cluster(n_nodes=30)
+    cin = ConsolidationInput(p, list(range(30)), mode=abi.CONSOLIDATE_SINGLE)
+    st, cmds, chosen, _ = pyoracle.consolidate(cin)
+    assert st == abi.GS_OK and len(cmds) == 30
+    assert any(c["decision"] != abi.DECISION_NOOP for c in cmds)
+
+
+# ------------------------------------------------------------------- GPU parity
+@pytest.fixture(scope="module")
+def solver():
+    from gpusched.lib import Solver
+    s = Solver(0)
+    yield s
+    s.close()
+
+
+def check(solver, p, mode, cands=None, shard=(0, 0)):
+    cands = list(range(len(p.nodes))) if cands is None else cands
+    cin = ConsolidationInput(p, cands, mode=mode)
+    st, want, want_chosen, want_multi = pyoracle.consolidate(cin)
+    assert st == abi.GS_OK
+    got, chosen, multi, _ = solver.consolidate(ConsolidationInput(p, cands, mode=mode, shard=shard))
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        if shard[1] and i % shard[1] != shard[0]:
+            continue
+        assert g == w, (i, g, w)
+    if not shard[1]:
+        assert (chosen, multi) == (want_chosen, want_multi)
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
+def test_gpu_general_consolidation(solver, seed, mode):
+    check(solver, synth.random_consolidation_general(seed), mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_general_consolidation_min_values(solver, seed):
+    check(solver, synth.random_consolidation_general(100 + seed, min_values=True), abi.CONSOLIDATE_MULTI)
+    check(solver, synth.random_consolidation_general(100 + seed, min_values=True), abi.CONSOLIDATE_SINGLE)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_gpu_general_consolidation_larger(solver, seed):
+    p = synth.random_consolidation_general(200 + seed, n_nodes=40, n_pending=3)
+    check(solver, p, abi.CONSOLIDATE_SINGLE)
+    check(solver, p, abi.CONSOLIDATE_MULTI)
+
+
+@pytest.mark.gpu
+def test_gpu_e2e_consolidation_shape(solver):
+    p = synth.e2e_consolidation_cluster(n_nodes=60)
+    check(solver, p, abi.CONSOLIDATE_SINGLE)
+    check(solver, p, abi.CONSOLIDATE_MULTI)
+
+
+@pytest.mark.gpu
+def test_gpu_e2e_consolidation_5000_nodes_sampled(solver):
+    """the e2e workload at C4 scale (5,000 nodes): SINGLE over every node and
+    MULTI's 100 prefixes on the GPU; a sample of the SINGLE simulations and
+    the first MULTI prefixes against the oracle"""
+    p = synth.e2e_consolidation_cluster(n_nodes=5000)
+    cands = list(range(5000))
+    whole, chosen, _, _ = solver.consolidate(ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_SINGLE))
+    assert len(whole) == 5000
+    sub = list(range(0, 5000, 500))
+    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, sub, mode=abi.CONSOLIDATE_SINGLE))
+    assert st == abi.GS_OK
+    assert [whole[i] for i in sub] == want
+    multi, _, _, _ = solver.consolidate(ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_MULTI))
+    assert len(multi) == 100
+    # prefixes [0..m] of the first 8 candidates against the oracle's EVAL of the same sets
+    sets = [(0, m + 1) for m in range(1, 8)]
+    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, cands[:8], mode=abi.CONSOLIDATE_EVAL, sets=sets))
+    assert st == abi.GS_OK
+    assert multi[:7] == want
