@@ -1,0 +1,251 @@
+"""The reference e2e suite's expectations as Solve-level known-answer scenarios
+(VERDICT r2 Missing 3 / next-round item 2): the only evidence the reference
+itself holds about what a Solve must produce.
+
+tests/golden/e2e_scenarios.json (written by tests/golden/make_e2e_scenarios.py)
+restates each test's NodePool, workloads, arrival order and assertion with
+its reference file:line:
+  * scheduling_test.go:246-344  3 replicas, required hostname anti-affinity
+                                -> 3 distinct NodeClaims
+  * scheduling_test.go:359-475  instance-type node affinity -> only that type
+  * multizone_test.go:188-289   zone spread maxSkew 1 -> skew <= 1, > 1 zone
+  * multizone_test.go:83-174    preferred zone anti-affinity -> > 1 zone
+  * scheduling_test.go:38-176   4 replicas, preferred hostname anti-affinity
+                                -> several nodes; scaled down, consolidation
+The CPU tests run every scenario through the oracle and assert the reference
+test's property; the GPU tests require both HIP Solve kernels (and the
+consolidation simulation kernel) to equal the oracle at every step, so the
+property holds for the product too.
+"""
+import json
+import os
+
+import pytest
+
+from gpusched import abi, synth
+from gpusched.consolidation import ConsolidationInput
+from gpusched.problem import ProblemBuilder
+from oracle import pyoracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "e2e_scenarios.json")) as f:
+    GOLD = json.load(f)
+ZONES = GOLD["zones"]
+IT = "node.kubernetes.io/instance-type"
+Z = "topology.kubernetes.io/zone"
+H = "kubernetes.io/hostname"
+NP = "e2e-nodepool"
+GI = 1 << 30
+MI = 1 << 20
+
+
+def zones_of(claim):
+    for line in claim["requirements"].split("\n"):
+        f = line.split("|")
+        if f[0] == Z and f[1] == "In":
+            return sorted(v for v in f[2].split(",") if v)
+    return list(ZONES)
+
+
+class Cluster:
+    """the e2e cluster between Solves: launched nodes with their bound pods"""
+
+    def __init__(self, sc):
+        self.sc = sc
+        self.nodes = []  # dict(name, it, zone, pods)
+        self.pods = []   # every pod spec created so far, in creation order
+        b = ProblemBuilder()
+        self.its = synth.build_catalog(b, synth.FAKE_PROFILES, ZONES, spot=False,
+                                       prices=synth.price_table(synth.FAKE_PROFILES))
+        self.first_type = None
+
+    def make_pods(self, w, first=0, count=None):
+        out = []
+        count = w["replicas"] if count is None else count
+        for r in range(first, first + count):
+            anti = [dict(a, selector={"labels": {"app": w["app"]}}) for a in w.get("anti_affinity", [])]
+            sp = w.get("spread")
+            spreads = [dict(sp, selector={"labels": {"app": w["app"]}}, node_affinity_policy="Ignore")] if sp else []
+            req_terms = []
+            if w.get("node_affinity_first_node_type"):
+                req_terms = [[(IT, "In", [self.first_type])]]
+            out.append(dict(uid=f"{w['app']}-{r:02d}", app=w["app"], cpu=w["cpu_m"], mem=w["memory_mi"] * MI * 1000,
+                            anti=anti, spreads=spreads, req_terms=req_terms, ts=len(self.pods) + len(out)))
+        return out
+
+    def _add(self, b, p, node=None):
+        kw = dict(node_selector={"karpenter.sh/nodepool": NP}, required_terms=p["req_terms"],
+                  labels={"app": p["app"], "test": "e2e"}, anti_affinity=p["anti"], spreads=p["spreads"])
+        req = {"cpu": p["cpu"], "memory": p["mem"], "pods": 1000}
+        ts = 1_700_000_000_000_000_000 + p["ts"] * 1_000_000_000
+        if node is None:
+            b.add_pod(p["uid"], ts, req, **kw)
+        else:
+            b.add_bound_pod(node, p["uid"], ts, req, **kw)
+
+    def problem(self, pending):
+        b = ProblemBuilder()
+        synth.build_catalog(b, synth.FAKE_PROFILES, ZONES, spot=False, prices=synth.price_table(synth.FAKE_PROFILES))
+        b.add_nodepool(NP, requirements=[tuple(r) for r in self.sc["nodepool"]["requirements"]])
+        for k, n in enumerate(self.nodes):
+            it = self.its[n["it"]]
+            labels = {r[0]: r[2][0] for r in it.requirements}
+            labels.update({Z: n["zone"], "karpenter.sh/capacity-type": "on-demand", "karpenter.sh/nodepool": NP,
+                           H: n["name"]})
+            alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+            used = {"cpu": sum(p["cpu"] for p in n["pods"]), "memory": sum(p["mem"] for p in n["pods"]),
+                    "pods": 1000 * len(n["pods"])}
+            b.add_node(n["name"], labels, {r: alloc[r] - used.get(r, 0) for r in alloc})
+        for k, n in enumerate(self.nodes):
+            for p in n["pods"]:
+                self._add(b, p, node=k)
+        for p in pending:
+            self._add(b, p)
+        return b.build()
+
+    def launch(self, res, pending):
+        """NodeClaims become nodes (Create: the first compatible type in
+        catalog order, the first allowed zone); placed pods become bound"""
+        for k, pods in enumerate(res["nodes"]):
+            self.nodes[k]["pods"].extend(pending[i] for i in pods)
+        for c in res["claims"]:
+            it = min(c["its"])
+            self.nodes.append(dict(name=f"launched-{len(self.nodes):02d}", it=it, zone=zones_of(c)[0],
+                                   pods=[pending[i] for i in c["pods"]]))
+            if self.first_type is None:
+                self.first_type = self.its[it].name
+        self.pods.extend(pending)
+        return [pending[i] for i in res["errors"]]
+
+
+def _solve_all(problem, solvers):
+    st, want, _ = pyoracle.solve(problem)
+    assert st == abi.GS_OK
+    if solvers:
+        from test_gpu_parity import _diff
+        for s in solvers:
+            got, _ = s.solve(problem)
+            d = _diff(got, want)
+            assert d is None, d
+    return want
+
+
+def run_scenario(sc, solvers=(), consolidator=None):
+    """replays the scenario; returns (cluster, last result, last pending)"""
+    cl = Cluster(sc)
+    arrival = sc["arrival"]
+    res, pending, errors = None, [], []
+    if arrival == "together":
+        pending = [p for w in sc["workloads"] for p in cl.make_pods(w)]
+        res = _solve_all(cl.problem(pending), solvers)
+    elif arrival == "one_by_one":
+        for w in sc["workloads"]:
+            for r in range(w["replicas"]):
+                pending = errors + cl.make_pods(w, first=r, count=1)
+                res = _solve_all(cl.problem(pending), solvers)
+                errors = cl.launch(res, pending)
+    else:  # by_workload: each deployment after the previous one launched
+        for w in sc["workloads"]:
+            pending = cl.make_pods(w)
+            res = _solve_all(cl.problem(pending), solvers)
+            errors = cl.launch(res, pending)
+    return cl, res, pending
+
+
+def _app_claims(res, pending, app):
+    return [c for c in res["claims"] if any(pending[i]["app"] == app for i in c["pods"])]
+
+
+def check_expectation(sc, cl, res, pending, consolidator=None):
+    e = sc["expect"]
+    app = e["app"]
+    if e["kind"] == "distinct_nodeclaims":
+        assert not res["errors"]
+        claims = _app_claims(res, pending, app)
+        assert len(claims) == e["n"]
+        assert all(sum(pending[i]["app"] == app for i in c["pods"]) == 1 for c in claims)
+    elif e["kind"] == "instance_type_is_first_node_type":
+        assert not res["errors"]
+        names = {k: cl.its[k].name for k in range(len(cl.its))}
+        for k, pods in enumerate(res["nodes"]):
+            if any(pending[i]["app"] == app for i in pods):
+                assert names[cl.nodes[k]["it"]] == cl.first_type
+        for c in _app_claims(res, pending, app):
+            assert [names[i] for i in c["its"]] == [cl.first_type]
+        placed = sum(len(c["pods"]) for c in res["claims"]) + sum(len(p) for p in res["nodes"])
+        assert placed == len(pending)
+    elif e["kind"] == "zone_skew":
+        assert not res["errors"]
+        count = {z: 0 for z in ZONES}
+        for c in _app_claims(res, pending, app):
+            zs = zones_of(c)
+            assert len(zs) == 1
+            count[zs[0]] += sum(pending[i]["app"] == app for i in c["pods"])
+        used = [v for v in count.values() if v]
+        assert len(used) >= e["min_zones"]
+        assert max(count.values()) - min(count.values()) <= e["max_skew"]
+    elif e["kind"] == "min_zones":
+        zones = {n["zone"] for n in cl.nodes if any(p["app"] == app for p in n["pods"])}
+        assert len(zones) >= e["min_zones"]
+    elif e["kind"] == "multi_node_then_consolidate":
+        assert not res["errors"]
+        assert len(_app_claims(res, pending, app)) >= e["min_nodes"]
+        cl.launch(res, pending)
+        # the Deployment scales down: the newest replicas go
+        keep = {p["uid"] for p in sorted(cl.pods, key=lambda p: p["ts"])[: e["scale_to"]]}
+        for n in cl.nodes:
+            n["pods"] = [p for p in n["pods"] if p["uid"] in keep]
+        p = cl.problem([])
+        cin = ConsolidationInput(p, list(range(len(cl.nodes))), mode=abi.CONSOLIDATE_SINGLE)
+        st, cmds, chosen, _ = pyoracle.consolidate(cin)
+        assert st == abi.GS_OK
+        empty = [k for k, n in enumerate(cl.nodes) if not n["pods"]]
+        assert empty and all(cmds[k]["decision"] == abi.DECISION_DELETE for k in empty)
+        assert chosen >= 0 and cmds[chosen]["decision"] == abi.DECISION_DELETE
+        if consolidator is not None:
+            got, gchosen, _, _ = consolidator.consolidate(cin)
+            assert (got, gchosen) == (cmds, chosen)
+            mcin = ConsolidationInput(p, list(range(len(cl.nodes))), mode=abi.CONSOLIDATE_MULTI)
+            st, mw, mc, mm = pyoracle.consolidate(mcin)
+            assert st == abi.GS_OK
+            g, gc, gm, _ = consolidator.consolidate(mcin)
+            assert (g, gc, gm) == (mw, mc, mm)
+    else:
+        raise AssertionError(e["kind"])
+
+
+IDS = [s["id"] for s in GOLD["scenarios"]]
+
+
+@pytest.mark.parametrize("k", range(len(IDS)), ids=IDS)
+def test_scenario_on_oracle(k):
+    sc = GOLD["scenarios"][k]
+    cl, res, pending = run_scenario(sc)
+    check_expectation(sc, cl, res, pending)
+
+
+def test_fixture_is_current():
+    """the committed JSON is what make_e2e_scenarios.py writes"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mk", os.path.join(HERE, "golden", "make_e2e_scenarios.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    assert json.loads(json.dumps({"zones": mk.ZONES, "scenarios": mk.SCENARIOS})) == GOLD
+
+
+# ------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def solvers():
+    from gpusched.lib import Solver
+    ss = [Solver(0), Solver(0, abi.GS_CFG_BLOCK_SOLVE)]
+    yield ss
+    for s in ss:
+        s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(len(IDS)), ids=IDS)
+def test_scenario_on_gpu(solvers, k):
+    sc = GOLD["scenarios"][k]
+    cl, res, pending = run_scenario(sc, solvers=solvers)
+    check_expectation(sc, cl, res, pending, consolidator=solvers[0])
