@@ -304,7 +304,9 @@ typedef struct gs_result {
   uint64_t sorts_fast, sorts_generic;/* Go sort.Slice emulations by path */
   uint32_t words, n_templates, n_variants; /* encoded sizes: IT words, templates, pod variants */
   double t_encode_ms, t_upload_ms, t_feas_ms, t_ffd_ms, t_truncate_ms, t_fetch_ms, t_total_ms;
-  double t_ffd_sort_ms, t_ffd_scan_ms, t_ffd_template_ms; /* in-kernel phase split of t_ffd_ms */
+  double t_ffd_sort_ms, t_ffd_scan_ms, t_ffd_template_ms; /* in-kernel phase split of t_ffd_ms; -1 = not
+                                        measured (the phase timers sit on the pod loop's critical path and
+                                        are built only into the GS_FFD_PHASES diagnostic library) */
   uint64_t claim_prefix;             /* in-flight NodeClaims a sequential first-fit visits (first feasible
                                         position + 1, or all): the reference's NodeClaim.CanAdd calls */
   uint64_t node_prefix;              /* ... and existing nodes (ExistingNode.CanAdd calls) */

@@ -605,9 +605,11 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->cand_full = c->ctrl.cand_full;
   out->claim_prefix = c->ctrl.claim_prefix;
   out->node_prefix = c->ctrl.node_prefix;
-  out->t_ffd_sort_ms = c->ctrl.t_sort * 1e-5;  // wall_clock64 runs at 100 MHz
-  out->t_ffd_scan_ms = c->ctrl.t_scan * 1e-5;
-  out->t_ffd_template_ms = c->ctrl.t_tmpl * 1e-5;
+  // wall_clock64 runs at 100 MHz; ~0: the phase timers are not built in (-1)
+  auto phase_ms = [](uint64_t t) { return t == ~0ull ? -1.0 : (double)t * 1e-5; };
+  out->t_ffd_sort_ms = phase_ms(c->ctrl.t_sort);
+  out->t_ffd_scan_ms = phase_ms(c->ctrl.t_scan);
+  out->t_ffd_template_ms = phase_ms(c->ctrl.t_tmpl);
   out->sorts_fast = c->ctrl.fast_sorts;
   out->sorts_generic = c->ctrl.generic_sorts;
   out->words = e.W;

@@ -1778,9 +1778,13 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       c.claim_prefix = S.claim_prefix;
       c.failed = S.failed;
       c.pad = 0;
+#ifdef GS_FFD_PHASES
       c.t_sort = S.t_sort;
       c.t_scan = S.t_scan;
       c.t_tmpl = S.t_tmpl;
+#else
+      c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
+#endif
       c.t_total = wall_clock64() - S.t0;
       S.dbg[7] = __builtin_amdgcn_s_memtime() - S.dbg[7];  // shader clock cycles over the solve
 #ifdef GS_FFD_TL

@@ -497,7 +497,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   __shared__ uint32_t s_ring[RING][RING_DW];  // first-pass pod records
   __shared__ uint32_t s_ring_seq[RING];       // queue position + 1 held by each slot
   __shared__ uint32_t s_wq[WQ][WQ_DW];        // write requests
-  __shared__ uint32_t s_ctl[4];               // [0] first-pass pops, [1] requests posted, [2] requests completed
+  __shared__ uint32_t s_ctl[4];               // [0] first-pass pops, [1] requests posted, [2] requests completed,
+                                              // [3] solver heartbeat (pops)
   constexpr uint32_t R = RR;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t MC = d.max_claims;
@@ -538,7 +539,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     //     common path, and never waits on one it did not need.
     const uint32_t* qv_dw = (const uint32_t*)d.qvars;
     const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
-    uint32_t k_fill = 0, head = 0, idle = 0;
+    uint32_t k_fill = 0, head = 0, idle = 0, beat = 0;
     for (;;) {
       bool busy = false, stop = false;
       const uint32_t tail = __builtin_amdgcn_readfirstlane(vld(&s_ctl[1]));
@@ -589,8 +590,14 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         k_fill += n;
         busy = true;
       }
-      if (busy) {
+      // the agent leaves on WQ_STOP only; its bounded wait (a stuck solver
+      // ends the kernel, not the GPU) restarts whenever the solver pops a pod,
+      // so a long tail of pods that post nothing (failures, relaxations)
+      // cannot outlast it
+      const uint32_t hb = __builtin_amdgcn_readfirstlane(vld(&s_ctl[3]));
+      if (busy || hb != beat) {
         idle = 0;
+        beat = hb;
       } else {
 #ifdef GS_AGENT_SLEEP
         __builtin_amdgcn_s_sleep(GS_AGENT_SLEEP);
@@ -706,6 +713,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     pops++;
+    if (lane == 0) vst(&s_ctl[3], (uint32_t)pops);  // heartbeat for the agent's bounded wait
     const uint32_t gp = p;
     auto VD = [&](uint32_t i) -> uint32_t { return rlane(vrd, i); };
     auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
@@ -1491,6 +1499,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.node_prefix = ctr_npre;
     c.claim_prefix = ctr_alg;
     c.dbg[15] = ctr_fa;
+    c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
     c.dbg[8] = n_fsum;

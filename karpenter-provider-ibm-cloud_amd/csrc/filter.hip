@@ -339,6 +339,13 @@ extern "C" gs_status gs_create_filter(gs_ctx* c, const gs_problem* p, const gs_c
                                       gs_claim_filter_result* out) {
   if (!c || !p || !out || (nq && !qs)) return GS_E_INVALID;
   std::memset(out, 0, sizeof(*out));
+  // reject before any allocation: the grid's y dimension, and every array the
+  // host pass reads that is null while its count is not
+  if (nq > 65535u) return fail(c, GS_E_INVALID, "more than 65535 claims in one gs_create_filter call");
+  if ((p->n_instance_types && !p->instance_types) || (p->n_offerings && !p->offerings) ||
+      (p->n_quantities && !p->quantities) || (p->n_reqs && !p->reqs) || (p->n_value_ids && !p->value_ids) ||
+      (p->n_strings && !p->strings))
+    return fail(c, GS_E_INVALID, "null array with a non-zero count");
   Enc e;
   e.p = p;
   std::vector<FIt> its;
@@ -470,7 +477,6 @@ extern "C" gs_status gs_create_filter(gs_ctx* c, const gs_problem* p, const gs_c
       d.out_create = (uint64_t*)(base + o_out);
       d.out_reqs = d.out_create + (size_t)nq * W;
       d.out_spot = d.out_reqs + (size_t)nq * W;
-      if (nq > 65535u) throw HipError{"more than 65535 claims in one gs_create_filter call"};
       HIPCHK(hipEventRecord(c->ev[6], c->stream));
       hipLaunchKernelGGL(claim_filter_kernel, dim3((N + 255) / 256, nq), dim3(256), 0, c->stream, d);
       HIPCHK(hipGetLastError());

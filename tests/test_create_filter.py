@@ -288,3 +288,22 @@ def test_oracle_create_filter_after_oracle_solve(seed):
     for c, g in zip(res["claims"], out):
         assert set(g["compatible"]) <= set(c["its"])
         assert g["n_compatible"] >= 1 and g["selected"] in c["its"]
+
+
+@pytest.mark.gpu
+def test_gpu_create_filter_rejects_bad_inputs_before_allocating(solver):
+    """nq > 65535 and null arrays with non-zero counts return
+    GS_E_INVALID (no dereference, no device allocation)"""
+    import ctypes as C
+    p = random_catalog(7, 20, 3)
+    res = abi.GsClaimFilterResult()
+    st = solver.L.gs_create_filter(solver.ctx, C.byref(p.struct), p.claim_queries, 70000, C.byref(res))
+    assert st == abi.GS_E_INVALID
+    for field in ("instance_types", "offerings", "quantities", "reqs", "value_ids"):
+        bad = abi.GsProblem()
+        C.memmove(C.byref(bad), C.byref(p.struct), C.sizeof(bad))
+        setattr(bad, field, None)
+        st = solver.L.gs_create_filter(solver.ctx, C.byref(bad), p.claim_queries, p.n_claim_queries, C.byref(res))
+        assert st == abi.GS_E_INVALID, field
+    # the context still works afterwards
+    assert solver.create_filter(p) == solver.create_filter(p)

@@ -170,3 +170,39 @@ def test_feasibility_device_shards(solver, name, world):
     assert np.array_equal(got["rows"], want["rows"])
     assert np.array_equal(got["n_feasible_offerings"], want["n_feasible_offerings"])
     assert np.array_equal(got["cheapest"], want["cheapest"])
+
+
+def failing_tail(n_pods=3000, seed=11):
+    """a long wrapped-phase tail of pods that never place (NodePool
+    limits) and relax through several preferred node-affinity variants -- pops
+    that post nothing to the single-wave kernel's memory agent"""
+    import numpy as np
+    from gpusched.problem import ProblemBuilder
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=True,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("limited", limits={"cpu": 16000}, daemon={"cpu": 100, "pods": 1000})
+    fams = ["bx2", "cx2", "mx2"]
+    for i in range(n_pods):
+        pref = [(int(w), [("karpenter-ibm.sh/instance-family", "In", [str(rng.choice(fams))])])
+                for w in rng.choice([1, 10, 50, 100], size=4, replace=False)]
+        b.add_pod(f"tail-{i:05d}", int(rng.integers(0, 4)), {"cpu": int(rng.choice([500, 1000, 2000])),
+                                                            "memory": 1 << 30, "pods": 1000}, preferred_terms=pref)
+    return b.build()
+
+
+@pytest.mark.gpu
+def test_gpu_failing_tail_both_kernels():
+    from gpusched.lib import Solver
+    p = failing_tail()
+    st, want, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK and len(want["errors"]) > 2000
+    for flags in (0, abi.GS_CFG_BLOCK_SOLVE):
+        s = Solver(0, flags)
+        try:
+            got, res = s.solve(p)
+        finally:
+            s.close()
+        d = _diff(got, want)
+        assert d is None, d
