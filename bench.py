@@ -49,6 +49,7 @@ from gpusched.lib import Solver  # noqa: E402
 
 METRIC = "pod×offering feasibility checks/sec + Solve latency (ms) at 100k pods, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: aggregate L2 bandwidth (8 XCDs)
 CM_WORKLOAD = ("CM: 100k pods x C2 synthetic IBM VPC catalog (198 profiles x 3 zones x {on-demand, spot} = "
                "1,188 offerings), 1 NodePool, 1% GPU pods, 10% nodeSelectors")
 
@@ -84,16 +85,25 @@ def load_traffic(path):
         return json.load(f)
 
 
-def traffic_of(traffic, leg, kernel):
-    x = traffic.get(leg, {}).get(kernel)
-    return x["bytes"] if isinstance(x, dict) else x
+def traffic_of(traffic, leg, *kernels):
+    """PMC HBM bytes per launch of a leg's kernel(s), summed (None when not profiled)"""
+    tot, seen = 0, False
+    for k in kernels:
+        x = traffic.get(leg, {}).get(k)
+        if x is not None:
+            tot += x["bytes"] if isinstance(x, dict) else x
+            seen = True
+    return tot if seen else None
 
 
-def roofline(kernel, algo_bytes, avg_ms, traffic=None):
+def roofline(kernel, algo_bytes, avg_ms, traffic=None, peak=HBM_PEAK_GBS, bound="hbm"):
     ach = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes": int(algo_bytes), "avg_ms": round(avg_ms, 4),
-            "traffic": traffic}
+    out = {"kernel": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": "GB/s",
+           "frac": ach / peak, "algorithmic_bytes": int(algo_bytes), "avg_ms": round(avg_ms, 4), "traffic": traffic}
+    if traffic and avg_ms > 0:
+        # the rate the PMC bytes imply: a frac above it by more than 1.2x is not HBM evidence
+        out["pmc_rate_gbs"] = round(traffic / (avg_ms * 1e-3) / 1e9, 3)
+    return out
 
 
 def digest(res_dict):
@@ -159,8 +169,8 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         "ffd_candidates_exact_checked": int(res.cand_full),
         "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
         "roofline": roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
-        "roofline_feasibility_kernel": roofline("feas_kernel", ab["feas"], kms["feas"],
-                                                traffic_of(traffic or {}, leg, "feas")),
+        "roofline_feasibility_kernel": roofline("feas_cursor_kernel + feas_kernel", ab["feas"], kms["feas"],
+                                                traffic_of(traffic or {}, leg, "feas", "feas_cursor")),
         "_result": out,
     }
 
@@ -190,7 +200,25 @@ def config_leg(name, problem, args, traffic):
     got = r.pop("_result")
     r["value"] = r["checks"] / (r["ms_per_step"] * 1e-3)
     r["unit"] = "checks/s"
-    r["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_solve(problem, got)
+    r["result_sha256"] = digest(got)
+    if args.no_cpu_baseline:
+        r["cpu_baseline"] = None
+    elif name == "c5_solve":
+        # the full C5 oracle Solve takes ~6.5 min: a bounded, evenly spaced pod
+        # sample (its own Solve) is timed instead; exactness at full size is the
+        # committed oracle digest
+        idx = np.linspace(0, len(problem.pods) - 1, args.cpu_sample_c5_solve_pods).astype(np.int64)
+        sub = problem.with_pods(idx)
+        solver = Solver(0)
+        try:
+            sgot, _ = solver.solve(sub)
+        finally:
+            solver.close()
+        cb = cpu_baseline_solve(sub, sgot)
+        cb["sample"] = f"C5, {len(idx)} evenly spaced pods as their own Solve: " + cb["sample"]
+        r["cpu_baseline"] = cb
+    else:
+        r["cpu_baseline"] = cpu_baseline_solve(problem, got)
     return r
 
 
@@ -199,13 +227,18 @@ _POOL = None  # worker processes, forked before this process touches the GPU
 _WORKER_PROBLEMS = {}
 
 
+C4_GENERATORS = {"c4": "make_c4", "e2e": "e2e_consolidation_cluster"}
+
+
 def c4_problem(spec):
-    """spec = (n_nodes, generator kwargs): workers rebuild the cluster
-    themselves (deterministic generator) instead of inheriting GPU-process state"""
+    """spec = (n_nodes, generator kwargs[, generator]): workers rebuild the
+    cluster themselves (deterministic generator) instead of inheriting
+    GPU-process state"""
     key = json.dumps(spec, sort_keys=True)
     if key not in _WORKER_PROBLEMS:
         _WORKER_PROBLEMS.clear()
-        _WORKER_PROBLEMS[key] = synth.make_c4(n_nodes=spec[0], **spec[1])
+        gen = getattr(synth, C4_GENERATORS[spec[2] if len(spec) > 2 else "c4"])
+        _WORKER_PROBLEMS[key] = gen(n_nodes=spec[0], **spec[1])
     return _WORKER_PROBLEMS[key]
 
 
@@ -298,7 +331,12 @@ def consolidation_leg(problem, mode, args, rank, world, local, dist, device, bar
     nb = node_check_bytes(R)
     n_sims = len(merged)
     n_local = (n_sims + world - 1) // world
-    sim_bytes = r.node_prefix * nb + r.pops * (104 + 8 * R) + n_local * 256
+    # HBM-unique algorithmic bytes of one launch: the shared node table once,
+    # every simulated pod's variant record + requests + add-log entry, the
+    # control block per simulation.  The node checks each simulation repeats
+    # (node_prefix visits) are served by L2 / MALL: priced against L2 apart.
+    uniq_bytes = n * nb + int(r.pods_simulated) * (128 + 8 * R + 16) + n_local * 256
+    visit_bytes = r.node_prefix * nb + r.pops * (104 + 8 * R) + n_local * 256
     counts = {}
     for c in merged:
         k = abi.DECISION_NAMES[c["decision"]]
@@ -319,7 +357,8 @@ def consolidation_leg(problem, mode, args, rank, world, local, dist, device, bar
         "node_prefix": int(r.node_prefix),
         "chosen": chosen,
         "decisions": counts,
-        "roofline": roofline("ffd_kernel<SIM>", sim_bytes, sim_ms, traffic_of(traffic, leg, "sim")),
+        "roofline": roofline("ffd_kernel<SIM>", uniq_bytes, sim_ms, traffic_of(traffic, leg, "sim")),
+        "roofline_l2_node_visits": roofline("ffd_kernel<SIM>", visit_bytes, sim_ms, None, L2_PEAK_GBS, "l2"),
         "cpu_baseline": None,
         "_commands": merged,
     }
@@ -422,7 +461,7 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
         "kernel_ms": round(k_ms, 4),
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "shards_equal_whole": equal,
-        "roofline": roofline("feas_kernel", ab, k_ms, traffic_of(traffic, "c5", "feas")),
+        "roofline": roofline("feas_cursor_kernel + feas_kernel", ab, k_ms, traffic_of(traffic, "c5", "feas", "feas_cursor")),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -542,9 +581,11 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C3 Solve legs")
     ap.add_argument("--c5-pods", type=int, default=200_000)
     ap.add_argument("--cpu-sample-c5-pods", type=int, default=2000)
+    ap.add_argument("--cpu-sample-c5-solve-pods", type=int, default=20000)
     ap.add_argument("--no-stress", action="store_true")
-    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | c4 | c4_mixed | "
-                                                 "c4_multi | c5 | filter | ranking (profiling passes)")
+    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | e2e200 | c5_solve | "
+                                                 "c4 | c4_mixed | c4_multi | c4_e2e | c4_e2e_multi | c5 | filter | "
+                                                 "ranking (profiling passes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per leg (tools/pmc_traffic.py, committed under profiles/)")
     args = ap.parse_args()
@@ -582,7 +623,7 @@ def main():
     solo = rank == 0 and world == 1
     global _POOL
     if solo and not args.no_cpu_baseline and not args.no_consolidation and args.pool > 1 and \
-            only in (None, "c4", "c4_mixed", "c4_multi"):
+            only in (None, "c4", "c4_mixed", "c4_multi", "c4_e2e", "c4_e2e_multi"):
         import multiprocessing as mp
         _POOL = mp.get_context("fork").Pool(args.pool)  # before any GPU call in this process
     line = {"metric": METRIC, "value": None, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
@@ -615,7 +656,7 @@ def main():
             line["create_filter"] = bench_create_filter(problem, result, args)
         del problem, result
 
-    if solo and not args.no_configs and only in (None, "c1", "c2", "c3", "e2e"):
+    if solo and not args.no_configs and only in (None, "c1", "c2", "c3", "e2e", "e2e200", "c5_solve"):
         configs = {}
         gens = {"c1": (synth.make_c1, "C1: 500 pods x 8 fake profiles x 3 zones (24 offerings), 1 NodePool"),
                 "c2": (synth.make_c2, "C2: 10k pods x C2 catalog (1,188 offerings), 1 NodePool"),
@@ -625,16 +666,26 @@ def main():
                 "e2e": (lambda: synth.e2e_deployments(n_deployments=60, replicas=500),
                         "e2e: 30k pods in 60 deployments x 500 replicas, each with a preferred (weight 100) "
                         "kubernetes.io/hostname podAntiAffinity on its own app label, 16-type catalog x 3 zones x "
-                        "{on-demand, spot}")}
+                        "{on-demand, spot}"),
+                "e2e200": (lambda: synth.e2e_deployments(n_deployments=200, replicas=150),
+                           "e2e200: 30k pods in 200 deployments x 150 replicas (200 topology groups), the e2e "
+                           "deployment shape above"),
+                # BASELINE configs[4] as a Solve: 200k pods x 2,000 types x 6 zones x 2 capacity types
+                "c5_solve": (synth.make_c5, "C5 Solve: 200k pods x 2,000 synthetic instance types x 6 zones x "
+                                            "{on-demand, spot} (24,000 offerings), 1 NodePool")}
         for name, (gen, desc) in gens.items():
             if only not in (None, name):
                 continue
             leg = config_leg(name, gen(), args, traffic)
             leg["workload"] = desc
             configs[name.upper()] = leg
+            if name == "c5_solve":
+                # the oracle's C5 200k result digest (tests/golden/fullsize.json, 6.5 min on one core)
+                with open(os.path.join(ROOT, "tests", "golden", "fullsize.json")) as f:
+                    leg["oracle_digest_equal"] = leg.pop("result_sha256") == json.load(f)["c5_200k"]["sha256"]
         line["configs"] = configs
 
-    if not args.no_consolidation and only in (None, "c4", "c4_mixed", "c4_multi"):
+    if not args.no_consolidation and only in (None, "c4", "c4_mixed", "c4_multi", "c4_e2e", "c4_e2e_multi"):
         legs = {}
         specs = {
             "c4": (dict(), abi.CONSOLIDATE_SINGLE, 0,
@@ -646,11 +697,21 @@ def main():
             "c4_multi": (dict(), abi.CONSOLIDATE_MULTI, 100,
                          "C4: {n} state nodes, MultiNodeConsolidation: every binary-search prefix "
                          "candidates[0:mid+1] of the first 100 candidates as one simulation"),
+            # the reference's consolidation e2e workload (test/e2e/scheduling_test.go:38-122) at C4 scale:
+            # every pod carries a preferred hostname anti-affinity (general simulation variant)
+            "c4_e2e": (dict(), abi.CONSOLIDATE_SINGLE, 0,
+                       "C4 e2e shape: {n} state nodes of the C2 catalog running {b} pods of 4-replica deployments, "
+                       "1 vCPU / 1 GiB each with a preferred (weight 100) kubernetes.io/hostname podAntiAffinity on "
+                       "its own app (reference test/e2e/scheduling_test.go:38-122), SingleNodeConsolidation over "
+                       "all {n} candidates (topology variant of the simulation kernel)"),
+            "c4_e2e_multi": (dict(), abi.CONSOLIDATE_MULTI, 100,
+                             "C4 e2e shape: {n} state nodes as c4_e2e, MultiNodeConsolidation prefixes of the first "
+                             "100 candidates (topology variant)"),
         }
         for name, (kw, mode, maxc, desc) in specs.items():
             if only not in (None, name):
                 continue
-            spec = (args.c4_nodes, kw)
+            spec = (args.c4_nodes, kw, "e2e" if name.startswith("c4_e2e") else "c4")
             problem = c4_problem(spec)
             leg = consolidation_leg(problem, mode, args, rank, world, local, dist, device, barrier, max_over_ranks,
                                     traffic, name, max_candidates=maxc)

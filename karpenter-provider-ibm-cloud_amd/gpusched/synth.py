@@ -954,21 +954,24 @@ def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=
     return b.build()
 
 
-def e2e_consolidation_cluster(n_nodes=5000, replicas=4, seed=0x5EED0C4E, util=(0.3, 0.8)):
+def e2e_consolidation_cluster(n_nodes=5000, replicas=4, seed=0x5EED0C4E, util=(0.5, 0.95)):
     """C4-scale cluster of the reference e2e workload shape
     (test/e2e/scheduling_test.go:38-122 TestE2EConsolidationWithPDB and
     test/e2e/config.go:455-490): deployments of `replicas` pods, each pod
     1 vCPU / 1 GiB with a preferred (weight 100) hostname anti-affinity on its
-    own app, spread over nodes of the C2 catalog in 3 zones; one NodePool"""
+    own app, spread over 2-8 vCPU nodes of the C2 catalog in 3 zones (a node
+    holds pods of distinct deployments, as the anti-affinity placed them);
+    one NodePool"""
+    import collections
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     profs = c2_profiles(200)
     its = build_catalog(b, profs, FAKE_ZONES, spot=True, prices=price_table(profs), rng=rng, unavailable_frac=0.02)
     daemon = {"cpu": 200, "memory": 256 * MI * 1000, "pods": 2000}
     b.add_nodepool("default", requirements=[("topology.kubernetes.io/zone", "In", FAKE_ZONES)], daemon=daemon)
-    cand = [it for it in its if it.capacity["nvidia.com/gpu"] == 0 and 2000 <= it.capacity["cpu"] <= 16000]
-    dep = 0
-    left = 0
+    cand = [it for it in its if it.capacity["nvidia.com/gpu"] == 0 and 2000 <= it.capacity["cpu"] <= 8000]
+    active = collections.deque()  # [deployment, replicas left]
+    n_dep = 0
     for k in range(n_nodes):
         it = cand[rng.integers(0, len(cand))]
         labels = {r[0]: r[2][0] for r in it.requirements}
@@ -977,20 +980,24 @@ def e2e_consolidation_cluster(n_nodes=5000, replicas=4, seed=0x5EED0C4E, util=(0
         alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
         used = dict(daemon)
         target = float(rng.uniform(*util))
-        apps_here = set()
+        here = []
         while used["cpu"] + 1000 <= target * alloc["cpu"] and used["memory"] + GI * 1000 <= alloc["memory"]:
-            if left == 0:
-                dep += 1
-                left = replicas
-            if dep in apps_here:  # the preferred anti-affinity kept replicas apart
+            while len(active) < 8:
+                active.append([n_dep, replicas])
+                n_dep += 1
+            d = active.popleft()
+            if d[0] in here:  # every active deployment already runs here
+                active.appendleft(d)
                 break
-            apps_here.add(dep)
-            left -= 1
+            here.append(d[0])
+            d[1] -= 1
+            if d[1]:
+                active.append(d)
             used["cpu"] += 1000
             used["memory"] += GI * 1000
             used["pods"] += 1000
-            name = f"e2e-{dep:05d}"
-            b.add_bound_pod(k, f"{name}-{replicas - left:02d}", 1_700_000_000_000_000_000 + dep * 1_000_000_000,
+            name = f"e2e-{d[0]:05d}"
+            b.add_bound_pod(k, f"{name}-{replicas - d[1]:02d}", 1_700_000_000_000_000_000 + d[0] * 1_000_000_000,
                             {"cpu": 1000, "memory": GI * 1000, "pods": 1000},
                             labels={"app": name, "test": "e2e"},
                             anti_affinity=[{"required": False, "weight": 100, "selector": {"labels": {"app": name}}}])
