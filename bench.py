@@ -146,7 +146,7 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
     n_types = len(problem.instance_types)
     ab = {"feas": feas_bytes(res.n_variants, res.n_templates, len(problem.offerings), res.words),
           "ffd": ffd_bytes(res, n_types)}
-    names = {"feas": "feas_kernel", "ffd": "ffdw_kernel" if solver.flags == 0 and len(problem.nodes) <= 512
+    names = {"feas": "feas_kernel", "ffd": "ffdw_kernel" if solver.flags == 0 and len(problem.nodes) <= 6144
              else "ffd_kernel"}
     ph = np.mean(np.array(phases), axis=0) if phases else np.zeros(6)
     return {
@@ -203,11 +203,12 @@ def config_leg(name, problem, args, traffic):
     r["result_sha256"] = digest(got)
     if args.no_cpu_baseline:
         r["cpu_baseline"] = None
-    elif name == "c5_solve":
-        # the full C5 oracle Solve takes ~6.5 min: a bounded, evenly spaced pod
-        # sample (its own Solve) is timed instead; exactness at full size is the
-        # committed oracle digest
-        idx = np.linspace(0, len(problem.pods) - 1, args.cpu_sample_c5_solve_pods).astype(np.int64)
+    elif name in ("c5_solve", "cm_c4"):
+        # the full oracle Solve takes minutes: a bounded, evenly spaced pod
+        # sample (its own Solve, same cluster) is timed instead; exactness at
+        # full size is the committed oracle digest (C5) or the sample itself
+        n_s = args.cpu_sample_c5_solve_pods if name == "c5_solve" else args.cpu_sample_cm_c4_pods
+        idx = np.linspace(0, len(problem.pods) - 1, n_s).astype(np.int64)
         sub = problem.with_pods(idx)
         solver = Solver(0)
         try:
@@ -215,7 +216,7 @@ def config_leg(name, problem, args, traffic):
         finally:
             solver.close()
         cb = cpu_baseline_solve(sub, sgot)
-        cb["sample"] = f"C5, {len(idx)} evenly spaced pods as their own Solve: " + cb["sample"]
+        cb["sample"] = f"{name}, {len(idx)} evenly spaced pods as their own Solve: " + cb["sample"]
         r["cpu_baseline"] = cb
     else:
         r["cpu_baseline"] = cpu_baseline_solve(problem, got)
@@ -582,8 +583,9 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=200_000)
     ap.add_argument("--cpu-sample-c5-pods", type=int, default=2000)
     ap.add_argument("--cpu-sample-c5-solve-pods", type=int, default=20000)
+    ap.add_argument("--cpu-sample-cm-c4-pods", type=int, default=10000)
     ap.add_argument("--no-stress", action="store_true")
-    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | e2e200 | c5_solve | "
+    ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | e2e200 | c5_solve | cm_c4 | "
                                                  "c4 | c4_mixed | c4_multi | c4_e2e | c4_e2e_multi | c5 | filter | "
                                                  "ranking (profiling passes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2", "traffic.json"),
@@ -656,7 +658,7 @@ def main():
             line["create_filter"] = bench_create_filter(problem, result, args)
         del problem, result
 
-    if solo and not args.no_configs and only in (None, "c1", "c2", "c3", "e2e", "e2e200", "c5_solve"):
+    if solo and not args.no_configs and only in (None, "c1", "c2", "c3", "e2e", "e2e200", "c5_solve", "cm_c4"):
         configs = {}
         gens = {"c1": (synth.make_c1, "C1: 500 pods x 8 fake profiles x 3 zones (24 offerings), 1 NodePool"),
                 "c2": (synth.make_c2, "C2: 10k pods x C2 catalog (1,188 offerings), 1 NodePool"),
@@ -672,7 +674,12 @@ def main():
                            "deployment shape above"),
                 # BASELINE configs[4] as a Solve: 200k pods x 2,000 types x 6 zones x 2 capacity types
                 "c5_solve": (synth.make_c5, "C5 Solve: 200k pods x 2,000 synthetic instance types x 6 zones x "
-                                            "{on-demand, spot} (24,000 offerings), 1 NodePool")}
+                                            "{on-demand, spot} (24,000 offerings), 1 NodePool"),
+                # CM's pods provisioned into C4's cluster: 5,000 state nodes first (single-wave kernel's LDS
+                # node codes, existing-node fast accept and infeasible-prefix hint)
+                "cm_c4": (lambda: synth.make_c4(n_nodes=5000, n_pending=100_000),
+                          "CM pods onto C4: 100k CM-distribution pending pods into a cluster of 5,000 state nodes "
+                          "(C2 catalog, 2 NodePools, 60-90% cpu used), then new NodeClaims")}
         for name, (gen, desc) in gens.items():
             if only not in (None, name):
                 continue

@@ -35,12 +35,21 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   if (sims) {
     d.max_claims = std::max<uint32_t>(sims->max_pods, 1);
   } else {
-    // NodeClaims the LDS holds next to the thresholds and topology state
+    // NodeClaims the LDS holds next to the thresholds, topology state and
+    // (single-wave kernel) the existing nodes' slack codes
+    // (the block kernel's capacity; the single-wave kernel's is smaller by the
+    // node codes -- a Solve that outgrows it reruns on the block kernel)
     const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) + 8;
     const uint32_t dyn = std::min(gsk_ffd_dyn_lds_max(), gsk_ffdw_dyn_lds_max());
-    const uint32_t fit = dyn > other ? (dyn - other) / 23 : 0;
-    d.max_claims = std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
+    auto claims_fit = [&](uint32_t extra) {
+      const uint32_t fit = dyn > other + extra ? (dyn - other - extra) / 23 : 0;
+      return std::min<uint32_t>(std::min<uint32_t>(std::max<uint32_t>(e.P, 1), kMaxClaimsLds), fit);
+    };
+    d.max_claims = claims_fit(0);
     if (!d.max_claims) throw HipError{"topology / threshold state leaves no LDS for NodeClaims"};
+    const bool wave_ok = !(c->cfg_flags & GS_CFG_BLOCK_SOLVE) && e.NN <= kWaveSolveMaxNodes;
+    d.max_claims_wave = wave_ok ? claims_fit(gsd::wave_node_lds_bytes(e.NN)) : 0u;
+    c->wave = d.max_claims_wave > 0;
   }
   c->upload(d.it_vid, e.it_vid);
   c->upload(d.it_dvid, e.it_dvid);
@@ -433,7 +442,7 @@ gs_status gs_run(gs_ctx* c) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_feas(c, 0);
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    if (!(c->cfg_flags & GS_CFG_BLOCK_SOLVE) && d.NN <= kWaveSolveMaxNodes)
+    if (c->wave)
       HIPCHK(gsk_ffdw(&d, c->stream));
     else
       HIPCHK(gsk_ffd(&d, 1, c->stream));
@@ -441,6 +450,20 @@ gs_status gs_run(gs_ctx* c) {
     HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), 0, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[3]));
+    if (c->wave && d.max_claims_wave < d.max_claims) {
+      // the single-wave kernel ran out of LDS NodeClaims: the block kernel
+      // holds more (no node codes beside them)
+      uint32_t st = 0;
+      HIPCHK(hipMemcpy(&st, &d.ctrl->status, sizeof st, hipMemcpyDeviceToHost));
+      if (st == gsd::ST_CLAIMS) {
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(gsk_ffd(&d, 1, c->stream));
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), 0, c->stream));
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[3]));
+      }
+    }
     float a = 0, b = 0, x = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
     HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));

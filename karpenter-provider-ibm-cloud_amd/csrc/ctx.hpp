@@ -35,9 +35,10 @@ namespace gsc {
 
 constexpr uint32_t kMaxClaimsLds = 8192;  // LDS: 4x u16 slack + room, ord/sc/scratch u16, tmpl u8, thresholds
 constexpr uint32_t kLdsBytes = 160 * 1024; // gfx950 LDS per workgroup
-// the single-wave Solve (ffd_wave.hip) scans existing nodes 64 at a time;
-// problems with more state nodes run the block kernel (ffd.hip)
-constexpr uint32_t kWaveSolveMaxNodes = 512;
+// the single-wave Solve (ffd_wave.hip) keeps 17 B of slack codes per existing
+// node in LDS (layout.hpp wave_node_lds_bytes) beside the NodeClaims; larger
+// clusters run the block kernel (ffd.hip)
+constexpr uint32_t kWaveSolveMaxNodes = 6144;
 
 using Clock = std::chrono::steady_clock;
 inline double ms_since(Clock::time_point t0) {
@@ -97,6 +98,7 @@ struct gs_ctx {
   gsh::Encoded enc;
   gsd::DevProblem dp{};
   bool prepared = false, ran = false;
+  bool wave = false;  // the prepared Solve runs the single-wave kernel
   uint32_t n_nodepools = 0;  // of the prepared problem (the caller's arrays are not kept)
   double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
   // result storage

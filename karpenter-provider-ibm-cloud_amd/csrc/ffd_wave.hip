@@ -48,7 +48,7 @@ constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the s
 constexpr uint32_t RING_DW = 48; // VarRec (32 dwords) + requests (<= 16 dwords)
 constexpr uint32_t WQ = 32;      // global-memory write requests in flight
 constexpr uint32_t WQ_DW = 16;
-enum : uint32_t { WQ_LOG = 1, WQ_FA = 2, WQ_STOP = 3 };
+enum : uint32_t { WQ_LOG = 1, WQ_FA = 2, WQ_STOP = 3, WQ_NFA = 4 };
 constexpr uint32_t SPIN_MAX = 1u << 26;  // bounded waits: a stuck partner ends the kernel, not the GPU
 constexpr uint64_t SWAR_HI = 0x8000800080008000ull;  // top bit of each 16-bit code field
 enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
@@ -493,6 +493,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   __shared__ uint32_t s_thoff[RMAX + 1];
   __shared__ uint32_t s_exl[64];  // exact-check batch: position | claim << 16
   __shared__ int64_t s_hint_rq[4];  // requests of the pod that set the infeasible-prefix hint
+  __shared__ int64_t s_hint_nrq[RMAX];  // ... of the pod that set the existing-node hint
   // channels between the solver (wave 0) and the memory agent (wave 1)
   __shared__ uint32_t s_ring[RING][RING_DW];  // first-pass pod records
   __shared__ uint32_t s_ring_seq[RING];       // queue position + 1 held by each slot
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
                                               // [3] solver heartbeat (pops)
   constexpr uint32_t R = RR;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t MC = d.max_claims;
+  const uint32_t MC = d.max_claims_wave;
   // dynamic LDS, per claim 23 B (the block kernel's layout, ffd.hip):
   // slack u64 | room u64 | packed order u32 | sort scratch u16 | template u8
   uint64_t* s_slk = lds64;
@@ -515,6 +516,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   const uint32_t nthr = d.thr_off[R];
   const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
+  // existing nodes (wave_node_lds_bytes): slack codes (upper bound), room
+  // codes (lower bound) of available - requests per resource 0..3, and a
+  // flag byte: bit 0 = plain (ok, no taints, resources 4.. not over)
+  const uint32_t nd_off = (tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u;
+  uint64_t* s_nslk = (uint64_t*)((char*)lds64 + nd_off);
+  uint64_t* s_nrm = (uint64_t*)((char*)lds64 + nd_off + d.NN * 8u);
+  uint8_t* s_nflag = (uint8_t*)((char*)lds64 + nd_off + d.NN * 16u);
   const int64_t* thr = s_thr;
   const uint64_t* slot = s_slot;
 
@@ -526,6 +534,25 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     s_tcm[t] = d.tmpl[t].cm;
   }
   if (TOPO) topo_init(d, ts, d.zknown0, tid, 128);
+  for (uint32_t n = tid; n < d.NN; n += 128) {
+    const NodeRec& nr = d.nodes0[n];
+    int64_t sl[RR];
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++) sl[r] = nr.avail[r] - nr.req[r];
+    uint64_t a = 0, b = 0;
+    bool plain = nr.ok && nr.taints == 0;
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++) {
+      if (r < 4 && r < d.RQ) {
+        a |= (uint64_t)qcode_ceil(sl[r]) << (16 * r);
+        b |= (uint64_t)qcode_floor(sl[r]) << (16 * r);
+      }
+      if (r >= 4) plain = plain && sl[r] >= 0;
+    }
+    s_nslk[n] = a;
+    s_nrm[n] = b;
+    s_nflag[n] = plain ? 1u : 0u;
+  }
   if (tid < RING) s_ring_seq[tid] = 0;
   if (tid < 4) s_ctl[tid] = 0;
   __syncthreads();  // the only workgroup barrier: the waves split here
@@ -551,10 +578,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         if (type == WQ_STOP) {
           stop = true;
         } else {
-          if (lane == 0) d.log[idx] = LogRec{rlane(x, 2), rlane(x, 3), tgt, 0};
+          if (lane == 0) d.log[idx] = LogRec{rlane(x, 2), rlane(x, 3), type == WQ_NFA ? tgt | 0x80000000u : tgt, 0};
           const uint64_t a = (uint64_t)rlo | ((uint64_t)rhi << 32);
           if (type == WQ_FA && lane < R && lane < 4 && a)
             atomicAdd((unsigned long long*)&d.c_rec[tgt].tot_lo[lane], (unsigned long long)a);
+          if (type == WQ_NFA && lane < R && lane < 4 && a)
+            atomicAdd((unsigned long long*)&d.nodes[tgt].req[lane], (unsigned long long)a);
         }
         head++;
         busy = true;
@@ -624,6 +653,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   uint32_t hint = 0;
   bool hint_ok = false;
   uint64_t hint_tolt = 0;
+  // Existing nodes: positions [0, nhint) cannot take a pod whose requests are
+  // all >= s_hint_nrq and that tolerates no taint outside nhint_tol (nodes
+  // only fill up; a pod with requirements, topology or volumes is only more
+  // constrained).  Set by plain pods (no requirements, topology, volumes).
+  uint32_t nhint = 0;
+  bool nhint_ok = false;
+  uint64_t nhint_tol = 0;
   bool chan_err = false;  // a channel wait exceeded SPIN_MAX
   // post one write request (uniform control flow: every lane takes part)
   auto post = [&](uint32_t type, uint32_t idx, uint32_t pod, uint32_t var, uint32_t tgt, uint32_t rqd_) {
@@ -636,7 +672,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     }
     const uint32_t rqx = (uint32_t)__shfl((int)rqd_, (int)(32 + (lane - 5) % 8));
     uint32_t x = lane == 0 ? type : lane == 1 ? idx : lane == 2 ? pod : lane == 3 ? var : lane == 4 ? tgt : 0u;
-    if (type == WQ_FA && lane >= 5 && lane < 13) x = rqx;
+    if ((type == WQ_FA || type == WQ_NFA) && lane >= 5 && lane < 13) x = rqx;
     if (lane < WQ_DW) s_wq[wq_tail % WQ][lane] = x;
     wsync();
     if (lane == 0) vst(&s_ctl[1], wq_tail + 1);
@@ -758,58 +794,160 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           pvol[q] = KD.pod_vol[(size_t)gp * VDMAX + q];
           pfresh[q] = KD.pod_vfresh[(size_t)gp * VDMAX + q];
         }
+      // LDS prefilter (per resource 0..3: request code <= slack code) and,
+      // for a plain pod (no requirements, topology or volumes) on a plain
+      // node, the sufficient test (request code <= room code: CanAdd holds
+      // without reading the node); the exact ExistingNode.CanAdd runs on the
+      // prefilter's survivors before the chunk's first fast accept
+      bool pvany = false;
+#pragma unroll
+      for (uint32_t q = 0; q < VDMAX; q++) pvany = pvany || pvol[q] || pfresh[q];
+      bool nplain = (vctb & VF_SIMPLE) && !pvany;
+#pragma unroll
+      for (uint32_t r = 4; r < RR; r++) nplain = nplain && rq[r] == 0;
+      uint64_t nrqq = 0, nrqc = 0;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++)
+        if (r < KD.RQ) {
+          nrqq |= (uint64_t)qcode_floor(rq[r]) << (16 * r);
+          nrqc |= (uint64_t)qcode_ceil(rq[r]) << (16 * r);
+        }
+      uint32_t nlo = 0;
+      if (nhint_ok && (vtol & ~nhint_tol) == 0) {
+        const bool ge = lane >= R || rq_lane >= s_hint_nrq[lane < RMAX ? lane : 0];
+        if (__ballot(!ge) == 0) nlo = nhint;
+      }
       uint32_t fn = INF;
-      for (uint32_t base = 0; base < KD.NN; base += 64) {
+      bool nfa_win = false;
+      for (uint32_t base = nlo & ~63u; base < KD.NN; base += 64) {
         const uint32_t n = base + lane;
-        bool feas = false;
-        if (n < KD.NN) {
-          const NodeRec& nr = KD.nodes[n];
-          const FK* nfk = KD.n_fk + (size_t)n * F;
-          feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
+        const bool in = (n < KD.NN) & (n >= nlo);
+        const uint32_t nc = in ? n : 0u;
+        const uint64_t nsl = s_nslk[nc], nrm = s_nrm[nc];
+        const uint32_t nfl = s_nflag[nc];
+        const bool lp = in & swar_ge(nsl, nrqq);
+        const bool fa = lp & nplain & (bool)(nfl & 1u) & swar_ge(nrm, nrqc);
+        const uint64_t lpb = __ballot(lp);
+        CTR(C_NEV, KD.NN - base < 64 ? KD.NN - base : 64);
+        if (!lpb) continue;
+        const uint64_t fab = __ballot(fa);
+        const uint32_t mfl = fab ? ffs64(fab) : 64u;
+        const bool need = lp & !fa & (lane < mfl);
+        bool feas = fa;
+        if (__ballot(need)) {
+          drain();  // node requests the agent still adds (fast accepts)
+          if (need) {
+            const NodeRec& nr = KD.nodes[n];
+            const FK* nfk = KD.n_fk + (size_t)n * F;
+            feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
 #pragma unroll
-          for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
+            for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
 #pragma unroll
-          for (uint32_t k = 0; k < KMAX_IT; k++) {
-            const uint32_t off = VX(4 + k);
-            if (k >= KD.K || !feas || off == NONE) continue;
-            const uint32_t vid = nr.vid[k];
-            feas = vid != NONE && ((KD.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
-          }
-          if (feas && zfull_off != NONE)
-            feas = nr.zvid != NONE && ((KD.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
-          if (feas && cfull_off != NONE)
-            feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
-          if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
-          if (TOPO && feas && own_n)
-            feas = topo_node_ok(KD, ts, own_off, own_n, nr.zvid,
-                                [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; });
-          if (TOPO && feas && KD.any_vol) {
-            // ExceedsLimits: distinct volumes per driver after the union
-            const NodeVol& nv = KD.n_vol[n];
+            for (uint32_t k = 0; k < KMAX_IT; k++) {
+              const uint32_t off = VX(4 + k);
+              if (k >= KD.K || !feas || off == NONE) continue;
+              const uint32_t vid = nr.vid[k];
+              feas = vid != NONE && ((KD.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+            }
+            if (feas && zfull_off != NONE)
+              feas = nr.zvid != NONE && ((KD.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+            if (feas && cfull_off != NONE)
+              feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+            if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
+            if (TOPO && feas && own_n)
+              feas = topo_node_ok(KD, ts, own_off, own_n, nr.zvid,
+                                  [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; });
+            if (TOPO && feas && KD.any_vol) {
+              // ExceedsLimits: distinct volumes per driver after the union
+              const NodeVol& nv = KD.n_vol[n];
 #pragma unroll
-            for (uint32_t q = 0; q < VDMAX; q++)
-              if (pvol[q] | pfresh[q]) feas = feas && nv.cnt[q] + (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+              for (uint32_t q = 0; q < VDMAX; q++)
+                if (pvol[q] | pfresh[q]) feas = feas && nv.cnt[q] + (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+            }
           }
         }
         const uint64_t b = __ballot(feas);
-        CTR(C_NEV, KD.NN - base < 64 ? KD.NN - base : 64);
         if (b) {
           fn = base + ffs64(b);
+          nfa_win = ((fab >> ffs64(b)) & 1) != 0;
           break;
         }
       }
       CTR(C_NPRE, fn != INF ? fn + 1 : KD.NN);
+      if (nplain) {
+        // [nlo, fn) (or all) cannot take these requests; nodes only fill up
+        nhint = fn != INF ? fn : KD.NN;
+        nhint_ok = true;
+        nhint_tol = vtol;
+        if (lane < R) s_hint_nrq[lane] = rq_lane;
+      }
+      if (fn != INF && nfa_win) {
+        // ExistingNode.Add of a plain pod: requests only.  The LDS codes
+        // shrink by the request (still an upper / lower bound); the agent adds
+        // the requests to the node (an exact check drains the channel first)
+        const uint64_t sl = s_nslk[fn], rm = s_nrm[fn];
+        uint32_t c_sl = 0, c_rm = 0;
+        if (lane < KD.RQ) {
+          const uint32_t sh = 16 * lane;
+          c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - rq_lane);
+          c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - rq_lane);
+        }
+        uint64_t sl2 = 0, rm2 = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++)
+          if (r < KD.RQ) {
+            sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+          }
+        if (lane == 0) {
+          s_nslk[fn] = sl2;
+          s_nrm[fn] = rm2;
+          // <U> Topology.Record in the groups that select the pod
+          if (TOPO && sel_n) {
+            const uint32_t z = KD.nodes0[fn].zvid;
+            topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
+                        [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
+          }
+        }
+        wsync();
+        post(WQ_NFA, nlog, gp, v, fn, rqd);
+        nlog++;
+        continue;
+      }
       if (fn != INF) {
         // ExistingNode.Add: requests and requirements
         int64_t* areq = KD.nodes[fn].req;
         FK* afk = KD.n_fk + (size_t)fn * F;
-        if (lane < R) areq[lane] += rq_lane;
+        int64_t nreq = 0, navl = 0;
+        if (lane < R) {
+          nreq = areq[lane] + rq_lane;
+          navl = KD.nodes[fn].avail[lane];
+          areq[lane] = nreq;
+        }
         if (lane < fk_count) {
           const FKEntry& e = KD.fk_entries[fk_begin + lane];
           FK* nf = afk + e.slot;
           const FK cur = *nf;
           *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
                                          : e.st;
+        }
+        {
+          // the node's LDS codes from its exact remainder
+          const int64_t sl = navl - nreq;
+          const uint32_t c_sl = lane < KD.RQ ? qcode_ceil(sl) : 0u, c_rm = lane < KD.RQ ? qcode_floor(sl) : 0u;
+          const bool over = lane >= 4 && lane < R && sl < 0;
+          uint64_t sl2 = 0, rm2 = 0;
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) {
+            sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+          }
+          const bool anyover = __ballot(over) != 0;
+          if (lane == 0) {
+            s_nslk[fn] = sl2;
+            s_nrm[fn] = rm2;
+            if (anyover) s_nflag[fn] = 0;
+          }
         }
         if (lane == 0) {
           if (TOPO && KD.any_vol) {
@@ -1545,7 +1683,8 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
 
 // the single-wave provisioning Solve: grid-wide state reset, then one wave
 extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims_wave, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+                       wave_node_lds_bytes(d->NN);
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);

@@ -114,6 +114,10 @@ struct TGroupRec {
 };
 static_assert(sizeof(TGroupRec) == 24, "TGroupRec layout");
 
+// LDS bytes of the single-wave Solve's existing-node state: slack and room
+// codes (u64 each) and a flag byte per node, 8-B aligned after the topology state
+__host__ __device__ inline uint32_t wave_node_lds_bytes(uint32_t nn) { return nn ? 8u + nn * 17u : 0u; }
+
 // LDS bytes of the Solve kernels' topology state: known domains [TGZ] u64,
 // per-owned-group minimum counts [OWNMAX] i64, zone counts [TGZ][ZS] i32,
 // hostname totals [TGH] i32
@@ -204,6 +208,8 @@ struct DevProblem {
   uint32_t OW;                                // row / option / threshold stride: max(4, W rounded up to 4)
   uint32_t n_thr;                             // thr_off[R] (host copy: sizes the dynamic LDS)
   uint32_t max_claims;
+  uint32_t max_claims_wave;   // the single-wave kernel's LDS NodeClaims (<= max_claims: node codes share its LDS)
+  uint32_t pad_mcw;
   uint64_t wk_slots;  // free slots whose key is well-known
   // catalog
   const uint32_t* it_vid;      // [K][N]

@@ -206,3 +206,59 @@ def test_gpu_failing_tail_both_kernels():
             s.close()
         d = _diff(got, want)
         assert d is None, d
+
+
+def onto_nodes(n_nodes, n_pending, seed=0x5EED0C40, util=(0.6, 0.9)):
+    """provisioning Solve into a cluster of state nodes (C4 shape) with
+    CM-like pending pods: the single-wave kernel's LDS node codes, its
+    existing-node fast accept and infeasible-prefix hint (the wave
+    kernel beyond 512 existing nodes)"""
+    return synth.make_c4(n_nodes=n_nodes, n_pending=n_pending, seed=seed, util=util)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes,n_pending", [(600, 3000), (2000, 4000), (5000, 2000)])
+def test_gpu_solve_onto_many_existing_nodes(n_nodes, n_pending):
+    from gpusched.lib import Solver
+    p = onto_nodes(n_nodes, n_pending)
+    st, want, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK
+    for flags in (0, abi.GS_CFG_BLOCK_SOLVE):
+        s = Solver(0, flags)
+        try:
+            got, res = s.solve(p)
+        finally:
+            s.close()
+        d = _diff(got, want)
+        assert d is None, (flags, d)
+
+
+@pytest.mark.gpu
+def test_gpu_wave_claim_overflow_reruns_on_block_kernel():
+    """6,000 state nodes leave the single-wave kernel ~2,300 LDS NodeClaims;
+    a Solve opening more reruns on the block kernel (same result as a
+    block-only context)"""
+    from gpusched.lib import Solver
+    from gpusched.problem import ProblemBuilder
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("default")
+    for k in range(6000):
+        b.add_node(f"n{k:05d}", {"topology.kubernetes.io/zone": synth.FAKE_ZONES[k % 3]},
+                   {"cpu": 100, "memory": 1 << 30, "pods": 110_000})
+    # one pod per NodeClaim: required hostname anti-affinity on a shared label
+    for i in range(4000):
+        b.add_pod(f"p{i:05d}", 0, {"cpu": 1000, "memory": 1 << 30, "pods": 1000}, labels={"app": "one-per-node"},
+                  anti_affinity=[{"required": True, "selector": {"labels": {"app": "one-per-node"}}}])
+    p = b.build()
+    outs = []
+    for flags in (0, abi.GS_CFG_BLOCK_SOLVE):
+        s = Solver(0, flags)
+        try:
+            got, res = s.solve(p)
+        finally:
+            s.close()
+        outs.append(got)
+    assert len(outs[0]["claims"]) == 4000 and not outs[0]["errors"]
+    assert outs[0] == outs[1]
