@@ -339,7 +339,11 @@ typedef struct gs_ctx gs_ctx;
 enum {
   /* run the provisioning Solve on the multi-wave block kernel even when the
    * single-wave kernel applies (both are bit-identical; tests compare them) */
-  GS_CFG_BLOCK_SOLVE = 1u << 0
+  GS_CFG_BLOCK_SOLVE = 1u << 0,
+  /* keep the single-wave Solve's claim scan state in HBM from the first run
+     (it moves there by itself when a Solve outgrows the LDS NodeClaims; this
+     flag exercises that mode on any problem) */
+  GS_CFG_CLAIMS_HBM = 1u << 1
 };
 
 /* One Go process, several devices: with n_shards > 1 the context owns one

@@ -139,6 +139,8 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   const size_t PA = sims ? sims->pods.size() : e.P;
   const size_t CA = sims ? sims->pods.size() : d.max_claims;
   const size_t NS = sims ? sims->evaluated.size() : 0;
+  d.claim_cap = (uint32_t)CA;
+  c->ch = false;
   d.OW = std::max<uint32_t>(4, (e.W + 3) & ~3u);
   c->alloc(d.rows, VT * d.OW);
   c->alloc(d.cheapest, VT);
@@ -434,6 +436,40 @@ gs_status gs_prepare(gs_ctx* c, const gs_problem* p) {
   return prepare_one(c, p);
 }
 
+// claim arrays for up to min(P, 65,535) NodeClaims (the packed sort order
+// keeps 16-bit claim ids), hostname counts within 2 GiB; false if that is no
+// more than the LDS already held
+static bool grow_claims(gs_ctx* c, bool force = false) {
+  auto& d = c->dp;
+  const auto& e = c->enc;
+  size_t cap = std::min<size_t>(std::max<uint32_t>(d.P, 1), 65535);
+  const size_t per_h = (size_t)std::max<uint32_t>(e.TGH, 1) * sizeof(int32_t);
+  cap = std::min<size_t>(cap, ((size_t)2 << 30) / per_h);
+  if (cap <= d.max_claims_wave && !force) return false;
+  const size_t F1 = std::max<uint32_t>(e.F, 1);
+  auto get = [&](auto*& dst, size_t n) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(*dst)));
+    c->allocs.push_back(p);
+    dst = (std::remove_reference_t<decltype(dst)>)p;
+  };
+  get(d.c_rec, cap);
+  get(d.c_opts, cap * d.OW);
+  get(d.c_fk, cap * F1);
+  get(d.c_sorted, cap);
+  get(d.c_its, cap * 60);
+  get(d.c_nits, cap);
+  get(d.hc, cap * std::max<uint32_t>(e.TGH, 1));
+  get(d.ch_slk, cap);
+  get(d.ch_rm, cap);
+  get(d.ch_so, cap);
+  get(d.ch_scr, cap);
+  get(d.ch_tmpl, cap);
+  d.claim_cap = (uint32_t)cap;
+  c->ch = true;
+  return true;
+}
+
 gs_status gs_run(gs_ctx* c) {
   if (!c || !c->prepared) return GS_E_INVALID;
   try {
@@ -442,22 +478,25 @@ gs_status gs_run(gs_ctx* c) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     launch_feas(c, 0);
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->wave && !c->ch && (c->cfg_flags & GS_CFG_CLAIMS_HBM) && !grow_claims(c, true))
+      throw HipError{"claim arrays for the HBM claim mode"};
     if (c->wave)
-      HIPCHK(gsk_ffdw(&d, c->stream));
+      HIPCHK(gsk_ffdw(&d, c->ch ? 1u : 0u, c->stream));
     else
       HIPCHK(gsk_ffd(&d, 1, c->stream));
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), 0, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(hipEventSynchronize(c->ev[3]));
-    if (c->wave && d.max_claims_wave < d.max_claims) {
-      // the single-wave kernel ran out of LDS NodeClaims: the block kernel
-      // holds more (no node codes beside them)
+    if (c->wave && !c->ch && d.P > d.max_claims_wave) {
+      // the single-wave kernel ran out of LDS NodeClaims: grow the claim
+      // arrays and rerun it with the claim scan state in HBM (later runs of
+      // this prepared problem start there)
       uint32_t st = 0;
       HIPCHK(hipMemcpy(&st, &d.ctrl->status, sizeof st, hipMemcpyDeviceToHost));
-      if (st == gsd::ST_CLAIMS) {
+      if (st == gsd::ST_CLAIMS && grow_claims(c)) {
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        HIPCHK(gsk_ffd(&d, 1, c->stream));
+        HIPCHK(gsk_ffdw(&d, 1, c->stream));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         HIPCHK(gsk_trunc(&d, trunc_lds_bytes(d.N), 0, c->stream));
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
@@ -524,7 +563,8 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   }
   if (c->ctrl.status == gsd::ST_CLAIMS)
     return fail(c, GS_E_CAPACITY, "NodeClaim count exceeded the device capacity (" +
-                                      std::to_string(c->dp.max_claims) + " in-flight NodeClaims)");
+                                      std::to_string(c->ch ? std::min<uint32_t>(c->dp.claim_cap, 65535) : c->dp.max_claims) +
+                                      " in-flight NodeClaims)");
   if (c->ctrl.status == gsd::ST_POD_COUNT)
     return fail(c, GS_E_CAPACITY, "a NodeClaim would hold more than 65535 pods (16-bit pod count in LDS)");
   if (c->ctrl.status == gsd::ST_INTERNAL) return fail(c, GS_E_HIP, "ffd kernel reported an internal error (queue / channel bound)");

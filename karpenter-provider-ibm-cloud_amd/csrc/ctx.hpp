@@ -27,7 +27,7 @@ extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, 
 extern "C" hipError_t gsk_ffd(const gsd::DevProblem* d, uint32_t blocks, hipStream_t s);
 extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total);
 extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
-extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, hipStream_t s);
+extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, uint32_t ch, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, uint32_t n_slots, hipStream_t s);
 extern "C" hipError_t gsk_mv_rows(const gsd::DevProblem* d, hipStream_t s);
 
@@ -99,6 +99,7 @@ struct gs_ctx {
   gsd::DevProblem dp{};
   bool prepared = false, ran = false;
   bool wave = false;  // the prepared Solve runs the single-wave kernel
+  bool ch = false;    // ... with its claim scan state in HBM (grown past the LDS NodeClaims)
   uint32_t n_nodepools = 0;  // of the prepared problem (the caller's arrays are not kept)
   double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
   // result storage

@@ -46,8 +46,9 @@ struct SplitAcc {
     ord[j] = a;
   }
 };
-struct PackedAcc {
-  lds_u32* so;
+template <class U32>  // lds_u32, or uint32_t (HBM claim state)
+struct PackedAccT {
+  U32* so;
   __device__ __forceinline__ uint32_t key(int i) const { return so[i] & 0xFFFFu; }
   __device__ __forceinline__ void swap(int i, int j) const {
     const uint32_t a = so[i];
@@ -55,6 +56,7 @@ struct PackedAcc {
     so[j] = a;
   }
 };
+using PackedAcc = PackedAccT<lds_u32>;
 
 // Go sort.Slice (src/sort/zsortfunc.go) over 16-bit keys, one thread;
 // pdq_frame() resumes a pdqsort_func loop from a given frame state.
@@ -293,6 +295,7 @@ struct SeqSortT {
 // common case; thr has 4 readable entries past every range.
 using SeqSort = SeqSortT<SplitAcc>;
 using SeqSortP = SeqSortT<PackedAcc>;
+using SeqSortPG = SeqSortT<PackedAccT<uint32_t>>;
 
 __device__ __forceinline__ uint32_t thr_window(const int64_t* thr, uint32_t n, uint32_t m0, int64_t x) {
   uint32_t m = m0;

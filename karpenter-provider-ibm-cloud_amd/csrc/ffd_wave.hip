@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "devutil.hpp"
 #include "ffd_common.hpp"
 #include "layout.hpp"
@@ -61,6 +63,16 @@ enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+// the claim scan state's hand-offs between lanes: in LDS the wave's in-order
+// LDS queue orders them (wsync); in HBM (G) every store must have completed
+// before another lane's load (s_waitcnt 0: a wave's stores and loads share
+// the vector memory counter on gfx9, and the CU's write-through L1 serves the
+// completed store)
+template <bool G>
+__device__ __forceinline__ void wsyncT() {
+  if (G) __builtin_amdgcn_s_waitcnt(0);
+  wsync();
 }
 
 // readlane as an unsigned dword (the builtin returns int: widening it
@@ -141,11 +153,11 @@ __device__ __forceinline__ uint64_t wave_swar_max(uint64_t x) {
 // restatement of pdqsort_func (ffd.hip Blk) with one wave, so every block
 // reduction is a ballot and every barrier an in-order LDS queue.  Ranges up
 // to SEQ elements run the sequential port on lane 0.
-template <int SEQ>
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
 struct WaveSort {
   static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
-  lds_u32* so;
-  lds_u16* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
+  U32* so;
+  U16* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
   lds_frame* stk;
   uint32_t lane, half;
 
@@ -175,7 +187,7 @@ struct WaveSort {
   }
   // positions k in [lo,hi) with pred(k), ascending or descending, to out[]
   template <class Pred>
-  __device__ uint32_t compact(int lo, int hi, bool desc, lds_u16* out, Pred pred) const {
+  __device__ uint32_t compact(int lo, int hi, bool desc, U16* out, Pred pred) const {
     uint32_t total = 0;
     const int n = hi - lo;
     for (int base = 0; base < n; base += 64 * RW) {
@@ -193,7 +205,7 @@ struct WaveSort {
         total += (uint32_t)__popcll(m);
       }
     }
-    wsync();
+    wsyncT<G>();
     return total;
   }
   // swap the k-th left-list position with the k-th right-list position
@@ -201,28 +213,28 @@ struct WaveSort {
     for (uint32_t k = lane; k < s; k += 64) {
       const int x = scr[k], y = scr[half + k];
       const uint32_t a = so[x], b = so[y];
-      wsync();
+      wsyncT<G>();
       so[x] = b;
       so[y] = a;
     }
-    wsync();
+    wsyncT<G>();
   }
   __device__ int partition(int a, int b, int pivot, bool* already) const {
     if (lane == 0) swap(a, pivot);
-    wsync();
+    wsyncT<G>();
     const uint32_t p = key(a);
     const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) < p; });
     const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
     compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
     swap_lists(s);
     if (lane == 0) swap(mid, a);
-    wsync();
+    wsyncT<G>();
     *already = s == 0;
     return mid;
   }
   __device__ int partition_equal(int a, int b, int pivot) const {
     if (lane == 0) swap(a, pivot);
-    wsync();
+    wsyncT<G>();
     const uint32_t p = key(a);
     const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) <= p; });
     const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
@@ -237,7 +249,7 @@ struct WaveSort {
   __device__ void rotate(int lo, int hi, bool left) const {
     if (hi <= lo) return;
     const uint32_t x = so[left ? lo : hi];
-    wsync();
+    wsyncT<G>();
     // RU x 64 positions per pass: every lane loads its RU values (one LDS
     // round trip), then stores them one position over
     constexpr int RU = 4;
@@ -249,13 +261,13 @@ struct WaveSort {
           const int k = base + u * 64 + (int)lane;
           v[u] = k < hi ? so[k + 1] : 0u;
         }
-        wsync();
+        wsyncT<G>();
 #pragma unroll
         for (int u = 0; u < RU; u++) {
           const int k = base + u * 64 + (int)lane;
           if (k < hi) so[k] = v[u];
         }
-        wsync();
+        wsyncT<G>();
       }
       if (lane == 0) so[hi] = x;
     } else {
@@ -266,17 +278,17 @@ struct WaveSort {
           const int k = top - u * 64 - (int)lane;
           v[u] = k >= lo ? so[k] : 0u;
         }
-        wsync();
+        wsyncT<G>();
 #pragma unroll
         for (int u = 0; u < RU; u++) {
           const int k = top - u * 64 - (int)lane;
           if (k >= lo) so[k + 1] = v[u];
         }
-        wsync();
+        wsyncT<G>();
       }
       if (lane == 0) so[lo] = x;
     }
-    wsync();
+    wsyncT<G>();
   }
   // first k in [from, b) with key(k) < key(k-1); b if none
   __device__ int first_inversion(int from, int b) const {
@@ -302,7 +314,7 @@ struct WaveSort {
       if (i == b) return true;
       if (b - a < 50) return false;
       if (lane == 0) swap(i, i - 1);
-      wsync();
+      wsyncT<G>();
       if (i - a >= 2) {
         // the smaller element (now at i-1) moves left past larger elements,
         // down to absolute index 0 (Go's loop runs to j >= 1)
@@ -338,17 +350,17 @@ struct WaveSort {
     const int n = (b - a) / 2;
     for (int k = (int)lane; k < n; k += 64) {
       const uint32_t x = so[a + k], y = so[b - 1 - k];
-      wsync();
+      wsyncT<G>();
       so[a + k] = y;
       so[b - 1 - k] = x;
     }
-    wsync();
+    wsyncT<G>();
   }
   __device__ __forceinline__ void pdqsort_body(int n) const {
-    const SeqSortP seq{{so}};
+    const SeqSortT<PackedAccT<U32>> seq{{so}};
     if (n <= SEQ) {
       if (lane == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
-      wsync();
+      wsyncT<G>();
       return;
     }
     int sp = 0;
@@ -358,17 +370,17 @@ struct WaveSort {
         const int length = f.b - f.a;
         if (length <= SEQ) {
           if (lane == 0) seq.pdq_frame(f);
-          wsync();
+          wsyncT<G>();
           break;
         }
         if (f.limit == 0) {
           if (lane == 0) seq.heap_sort(f.a, f.b);
-          wsync();
+          wsyncT<G>();
           break;
         }
         if (!f.wb) {
           if (lane == 0) seq.break_patterns(f.a, f.b);
-          wsync();
+          wsyncT<G>();
           f.limit--;
         }
         int hint = 0;
@@ -409,7 +421,7 @@ struct WaveSort {
           stk[sp].wb = f.wb;
           stk[sp].wp = f.wp;
         }
-        wsync();
+        wsyncT<G>();
         sp++;
         f = child;
       }
@@ -421,7 +433,7 @@ struct WaveSort {
       f.wb = __builtin_amdgcn_readfirstlane(stk[sp].wb);
       f.wp = __builtin_amdgcn_readfirstlane(stk[sp].wp);
     }
-    wsync();
+    wsyncT<G>();
   }
 };
 
@@ -429,9 +441,9 @@ struct WaveSort {
 // arguments and the sorter is rebuilt locally, so they stay in registers (a
 // member function would reload them through a `this` pointer in scratch
 // after every LDS store)
-template <int SEQ>
-__device__ __noinline__ void wave_pdqsort(lds_u32* so, lds_u16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n) {
-  const WaveSort<SEQ> w{so, scr, stk, lane, half};
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
+__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n) {
+  const WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
   w.pdqsort_body(n);
 }
 
@@ -484,7 +496,10 @@ __device__ __forceinline__ bool pivot_touched(uint32_t modkind, uint32_t modpos,
   return hit;
 }
 
-template <uint32_t RR, bool TOPO>
+// CH: the claim scan state (slack, room, sorted order, sort scratch,
+// template) lives in HBM instead of LDS -- a Solve with more NodeClaims than
+// the LDS holds (capi gs_run reruns it so)
+template <uint32_t RR, bool TOPO, bool CH = false>
 __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
@@ -502,15 +517,16 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
                                               // [3] solver heartbeat (pops)
   constexpr uint32_t R = RR;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t MC = d.max_claims_wave;
+  const uint32_t MC = CH ? (d.claim_cap < 65535u ? d.claim_cap : 65535u) : d.max_claims_wave;
+  const uint32_t MCL = CH ? 0u : MC;  // NodeClaims in LDS
   // dynamic LDS, per claim 23 B (the block kernel's layout, ffd.hip):
   // slack u64 | room u64 | packed order u32 | sort scratch u16 | template u8
-  uint64_t* s_slk = lds64;
-  uint64_t* s_rm = s_slk + MC;
-  uint32_t* s_so = (uint32_t*)(s_rm + MC);
-  uint16_t* s_scr = (uint16_t*)(s_so + MC);
-  uint8_t* s_tmpl = (uint8_t*)(s_scr + MC);
-  const uint32_t thr_base = (23u * MC + 7u) & ~7u;
+  uint64_t* s_slk = CH ? d.ch_slk : lds64;
+  uint64_t* s_rm = CH ? d.ch_rm : s_slk + MC;
+  uint32_t* s_so = CH ? d.ch_so : (uint32_t*)(s_rm + MC);
+  uint16_t* s_scr = CH ? d.ch_scr : (uint16_t*)(s_so + MC);
+  uint8_t* s_tmpl = CH ? d.ch_tmpl : (uint8_t*)(s_scr + MC);
+  const uint32_t thr_base = (23u * MCL + 7u) & ~7u;
   int64_t* s_thr = (int64_t*)((char*)lds64 + thr_base);
   const uint32_t W = d.W, F = d.F, T = d.T, OW = d.OW, P = d.P;
   const uint32_t nthr = d.thr_off[R];
@@ -590,7 +606,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       }
       if (busy) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the writes are done
-        wsync();
+        wsyncT<CH>();
         if (lane == 0) vst(&s_ctl[2], head);
       }
       if (stop) break;
@@ -612,7 +628,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
         for (uint32_t i = 0; i < KB; i++)
           if (i < n && lane < RING_DW) s_ring[(k_fill + i) % RING][lane] = val[i];
-        wsync();
+        wsyncT<CH>();
 #pragma unroll
         for (uint32_t i = 0; i < KB; i++)
           if (i < n && lane == 0) vst(&s_ring_seq[(k_fill + i) % RING], k_fill + i + 1);
@@ -640,8 +656,10 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   }
 
   // ======================================================== solver wave
-  const WaveSort<GS_WAVE_SEQ> ws{(lds_u32*)s_so, (lds_u16*)s_scr, (lds_frame*)s_stk, lane, MC / 2};
-  const PackedAcc acc{(lds_u32*)s_so};
+  using U32 = std::conditional_t<CH, uint32_t, lds_u32>;
+  using U16 = std::conditional_t<CH, uint16_t, lds_u16>;
+  const WaveSort<GS_WAVE_SEQ, U32, U16, CH> ws{(U32*)s_so, (U16*)s_scr, (lds_frame*)s_stk, lane, MC / 2};
+  const PackedAccT<U32> acc{(U32*)s_so};
   uint32_t wq_tail = 0;  // write requests posted
   // Infeasible-prefix hint: sorted positions [0, hint) hold NodeClaims that
   // cannot take a pod with requests >= s_hint_rq (resources 0..3) that
@@ -674,7 +692,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     uint32_t x = lane == 0 ? type : lane == 1 ? idx : lane == 2 ? pod : lane == 3 ? var : lane == 4 ? tgt : 0u;
     if ((type == WQ_FA || type == WQ_NFA) && lane >= 5 && lane < 13) x = rqx;
     if (lane < WQ_DW) s_wq[wq_tail % WQ][lane] = x;
-    wsync();
+    wsyncT<CH>();
     if (lane == 0) vst(&s_ctl[1], wq_tail + 1);
     wq_tail++;
   };
@@ -730,7 +748,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         break;
       }
       const uint32_t x = lane < RING_DW ? vld(&s_ring[rs][lane]) : 0u;
-      wsync();
+      wsyncT<CH>();
       if (lane == 0) vst(&s_ctl[0], qhead + 1);  // the slot may be refilled
       vrd = x;
       rqd = x;
@@ -774,7 +792,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       const auto& KD = *karg();
       const uint64_t vzs = rlane(vrd, 26) | ((uint64_t)rlane(vrd, 27) << 32);
       topo_tmin(KD, ts, own_off, own_n, vzs, lane);
-      wsync();
+      wsyncT<CH>();
     }
 
     // ----------------- existing nodes in order: first ExistingNode.CanAdd wins
@@ -909,7 +927,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
                         [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
           }
         }
-        wsync();
+        wsyncT<CH>();
         post(WQ_NFA, nlog, gp, v, fn, rqd);
         nlog++;
         continue;
@@ -968,7 +986,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
                         [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
           }
         }
-        wsync();
+        wsyncT<CH>();
         post(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0);
         nlog++;
         continue;
@@ -986,8 +1004,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
       if (inversion) {
         if (M <= 12) {
-          if (lane == 0) SeqSortP{{(lds_u32*)s_so}}.insertion_sort(0, (int)M);
-          wsync();
+          if (lane == 0) SeqSortT<PackedAccT<U32>>{{(U32*)s_so}}.insertion_sort(0, (int)M);
+          wsyncT<CH>();
           hint_ok = false;
         } else if (M >= 50 && (!pivot_touched(modkind, modpos, M) || pivot_hint_wave(acc, (int)M, lane) == 1)) {
           // partialInsertionSort fixes the single inversion: one rotation
@@ -1014,7 +1032,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         } else {
           CTR(C_GEN, 1);
-          wave_pdqsort<GS_WAVE_SEQ>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
           hint_ok = false;
         }
       }
@@ -1093,7 +1111,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           break;
         }
       }
-      wsync();
+      wsyncT<CH>();
       TLW(5);  // phase A: LDS prefilter
       if (nex) {
         drain();  // the agent's request totals must be in the claim records
@@ -1328,7 +1346,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
           s_so[f] = e + 1u;
         }
-          wsync();
+          wsyncT<CH>();
           post(WQ_LOG, nlog, gp, v, rlane(j, wl), 0);
           break;
         }
@@ -1375,7 +1393,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             }
           }
         }
-        wsync();
+        wsyncT<CH>();
         post(WQ_FA, nlog, gp, v, j, rqd);  // the agent adds the requests and logs
         CTR(C_FA, 1);
         break;
@@ -1397,7 +1415,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       if (lane < 4) s_hint_rq[lane] = rq_lane;
     }
     if (f != INF) {
-      wsync();
+      wsyncT<CH>();
       modkind = MOD_INC;
       modpos = f;
       nlog++;
@@ -1539,7 +1557,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
       if (TOPO)
         for (uint32_t h = lane; h < KD.TGH; h += 64) KD.hc[(size_t)j * KD.TGH + h] = 0;
-      wsync();
+      wsyncT<CH>();
       if (lane == 0) {
         cr->tmpl = t;
         cr->count = 1;
@@ -1574,7 +1592,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             if (((tr.limit_rmask >> r) & 1) && mxc[r] != 0) KD.t_rem[(size_t)t * R + r] -= (int64_t)(mxc[r] - (1ull << 62));
         }
       }
-      wsync();
+      wsyncT<CH>();
       post(WQ_LOG, nlog, gp, v, j, 0);
       M++;
       modkind = MOD_APPEND;
@@ -1611,7 +1629,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   post(WQ_STOP, 0, 0, 0, 0, 0);
   drain();
   if (chan_err) status = 2;
-  wsync();
+  wsyncT<CH>();
   for (uint32_t i = lane; i < M; i += 64) {
     const uint32_t e = s_so[i];
     d.c_sorted[i] = e >> 16;
@@ -1657,41 +1675,51 @@ extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32
                                       uint32_t topo_bytes);
 static uint32_t g_ffdw_dyn_max = 0;
 
-template <uint32_t RR, bool TOPO>
+template <uint32_t RR, bool TOPO, bool CH>
 static hipError_t ffdw_attr(uint32_t lds_total) {
   hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffdw_kernel<RR, TOPO>);
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)ffdw_kernel<RR, TOPO, CH>);
   if (e != hipSuccess) return e;
   const uint32_t dyn = lds_total > a.sharedSizeBytes ? lds_total - (uint32_t)a.sharedSizeBytes : 0;
   if (!g_ffdw_dyn_max || dyn < g_ffdw_dyn_max) g_ffdw_dyn_max = dyn;
-  return hipFuncSetAttribute((const void*)ffdw_kernel<RR, TOPO>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  return hipFuncSetAttribute((const void*)ffdw_kernel<RR, TOPO, CH>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+}
+
+template <uint32_t RR>
+static hipError_t ffdw_attr_all(uint32_t lds_total) {
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {ffdw_attr<RR, false, false>(lds_total), ffdw_attr<RR, true, false>(lds_total),
+                       ffdw_attr<RR, false, true>(lds_total), ffdw_attr<RR, true, true>(lds_total)})
+    if (x != hipSuccess) e = x;
+  return e;
 }
 
 extern "C" hipError_t gsk_init_ffdw(uint32_t lds_total) {
   hipError_t e = hipSuccess;
-  for (hipError_t x : {ffdw_attr<1, false>(lds_total), ffdw_attr<2, false>(lds_total), ffdw_attr<3, false>(lds_total),
-                       ffdw_attr<4, false>(lds_total), ffdw_attr<5, false>(lds_total), ffdw_attr<6, false>(lds_total),
-                       ffdw_attr<7, false>(lds_total), ffdw_attr<8, false>(lds_total), ffdw_attr<1, true>(lds_total),
-                       ffdw_attr<2, true>(lds_total), ffdw_attr<3, true>(lds_total), ffdw_attr<4, true>(lds_total),
-                       ffdw_attr<5, true>(lds_total), ffdw_attr<6, true>(lds_total), ffdw_attr<7, true>(lds_total),
-                       ffdw_attr<8, true>(lds_total)})
+  for (hipError_t x : {ffdw_attr_all<1>(lds_total), ffdw_attr_all<2>(lds_total), ffdw_attr_all<3>(lds_total),
+                       ffdw_attr_all<4>(lds_total), ffdw_attr_all<5>(lds_total), ffdw_attr_all<6>(lds_total),
+                       ffdw_attr_all<7>(lds_total), ffdw_attr_all<8>(lds_total)})
     if (x != hipSuccess) e = x;
   return e;
 }
 
 extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
 
-// the single-wave provisioning Solve: grid-wide state reset, then one wave
-extern "C" hipError_t gsk_ffdw(const DevProblem* d, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims_wave, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+// the single-wave provisioning Solve: grid-wide state reset, then one wave;
+// ch: the claim scan state in HBM (d->ch_* allocated, claim_cap slots)
+extern "C" hipError_t gsk_ffdw(const DevProblem* d, uint32_t ch, hipStream_t s) {
+  const uint32_t lds = gsk_ffd_lds_bytes(ch ? 0u : d->max_claims_wave, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
                        wave_node_lds_bytes(d->NN);
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;
+  if (ch && !(d->ch_slk && d->ch_rm && d->ch_so && d->ch_scr && d->ch_tmpl)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
-  switch (d->R * 2 + (d->TG || d->any_mv || d->any_vol ? 1 : 0)) {
-#define GSK_CASE(n)                                                                                      \
-  case 2 * n: hipLaunchKernelGGL((ffdw_kernel<n, false>), dim3(1), dim3(128), lds, s, *d); break;      \
-  case 2 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true>), dim3(1), dim3(128), lds, s, *d); break;
+  switch (d->R * 4 + (d->TG || d->any_mv || d->any_vol ? 1 : 0) + (ch ? 2 : 0)) {
+#define GSK_CASE(n)                                                                                             \
+  case 4 * n: hipLaunchKernelGGL((ffdw_kernel<n, false, false>), dim3(1), dim3(128), lds, s, *d); break;      \
+  case 4 * n + 1: hipLaunchKernelGGL((ffdw_kernel<n, true, false>), dim3(1), dim3(128), lds, s, *d); break;   \
+  case 4 * n + 2: hipLaunchKernelGGL((ffdw_kernel<n, false, true>), dim3(1), dim3(128), lds, s, *d); break;   \
+  case 4 * n + 3: hipLaunchKernelGGL((ffdw_kernel<n, true, true>), dim3(1), dim3(128), lds, s, *d); break;
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

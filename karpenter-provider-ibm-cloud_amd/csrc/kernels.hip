@@ -431,7 +431,7 @@ extern "C" hipError_t gsk_trunc(const DevProblem* d, uint32_t lds_bytes, uint32_
     hipLaunchKernelGGL(sim_fix_kernel, dim3((d->n_sims + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, *d);
     return hipGetLastError();
   }
-  const uint32_t grid = d->n_sims ? d->n_sims : d->max_claims;
+  const uint32_t grid = d->n_sims ? d->n_sims : d->claim_cap;
   if (!grid) return hipSuccess;
   hipLaunchKernelGGL(trunc_kernel, dim3(grid), dim3(BLOCK), lds_bytes, s, *d, 0u);
   return hipGetLastError();

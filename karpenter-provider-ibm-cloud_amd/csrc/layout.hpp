@@ -209,7 +209,7 @@ struct DevProblem {
   uint32_t n_thr;                             // thr_off[R] (host copy: sizes the dynamic LDS)
   uint32_t max_claims;
   uint32_t max_claims_wave;   // the single-wave kernel's LDS NodeClaims (<= max_claims: node codes share its LDS)
-  uint32_t pad_mcw;
+  uint32_t claim_cap;         // NodeClaim slots of the claim arrays (c_rec, c_opts, c_fk, hc, c_its, ...)
   uint64_t wk_slots;  // free slots whose key is well-known
   // catalog
   const uint32_t* it_vid;      // [K][N]
@@ -285,6 +285,13 @@ struct DevProblem {
   int64_t* t_rem;              // [T][R] remaining limits (dynamic)
   LogRec* log;                 // [P]
   uint32_t* c_sorted;          // [max_claims] final sort order (debug)
+  // the single-wave kernel's claim scan state in HBM (a Solve that outgrows
+  // the LDS NodeClaims; <= 65,535 claims): the LDS arrays' global twins
+  uint64_t* ch_slk;            // [claim_cap] slack codes
+  uint64_t* ch_rm;             // [claim_cap] room codes
+  uint32_t* ch_so;             // [claim_cap] sorted order (count | id << 16)
+  uint16_t* ch_scr;            // [claim_cap] sort scratch
+  uint8_t* ch_tmpl;            // [claim_cap] template
   Ctrl* ctrl;
   // topology groups
   uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size

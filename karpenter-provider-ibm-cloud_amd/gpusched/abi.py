@@ -151,6 +151,7 @@ class GsFeasResult(C.Structure):
 
 
 GS_CFG_BLOCK_SOLVE = 1  # gs_config.flags: run the Solve on the block kernel
+GS_CFG_CLAIMS_HBM = 2   # gs_config.flags: single-wave Solve with its claim scan state in HBM
 
 
 class GsConfig(C.Structure):

