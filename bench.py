@@ -465,10 +465,53 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
         "roofline": roofline("feas_cursor_kernel + feas_kernel", ab, k_ms, traffic_of(traffic, "c5", "feas", "feas_cursor")),
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1:
+        out["library_shards"] = library_shards(problem, solver, W, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_stress(problem, args.cpu_sample_c5_pods)
     solver.close()
     return out
+
+
+def _hip_device_count():
+    """devices the HIP runtime the library links sees (torch bundles its own
+    runtime; initialising it after the library's can fail in one process)"""
+    import ctypes
+    n = ctypes.c_int(0)
+    try:
+        ctypes.CDLL("libamdhip64.so").hipGetDeviceCount(ctypes.byref(n))
+    except OSError:
+        return 1
+    return n.value
+
+
+def library_shards(problem, single, W, steps):
+    """the library's own multi-GPU (gs_config.n_shards = 2, csrc/multi.cpp):
+    each shard computes half the words on its device, the merge kernel on the
+    parent's device gathers the slices over xGMI peer reads and reduces the
+    counts / keys.  Two devices when the node shows them, else both shards on
+    device 0; merge_ms is the merge kernel alone"""
+    devs = [0, 1] if _hip_device_count() > 1 else [0, 0]
+    s = Solver(devs[0], shard_devices=devs)
+    try:
+        s.prepare(problem)
+        s.feasibility_shard_device(0, W)
+        merge, kern, wall = [], [], []
+        for _ in range(max(steps, 3)):
+            t0 = time.perf_counter()
+            r = s.feasibility_shard_device(0, W)
+            wall.append((time.perf_counter() - t0) * 1e3)
+            merge.append(r.t_merge_ms)
+            kern.append(r.t_kernel_ms)
+        # the merged device matrix through the host API (same buffers, copied out)
+        got, _ = s.feasibility()
+        want, _ = single.feasibility()
+        equal = all(np.array_equal(got[k], want[k]) for k in ("rows", "cheapest", "n_feasible_offerings", "cheapest_key"))
+    finally:
+        s.close()
+    return {"shard_devices": devs, "merge_ms": round(sum(merge) / len(merge), 4),
+            "shard_kernel_ms_max": round(sum(kern) / len(kern), 4), "call_ms": round(sum(wall) / len(wall), 3),
+            "equal_single_device": equal}
 
 
 # ------------------------------------------------------------ small legs

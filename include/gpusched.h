@@ -343,7 +343,13 @@ enum {
   /* keep the single-wave Solve's claim scan state in HBM from the first run
      (it moves there by itself when a Solve outgrows the LDS NodeClaims; this
      flag exercises that mode on any problem) */
-  GS_CFG_CLAIMS_HBM = 1u << 1
+  GS_CFG_CLAIMS_HBM = 1u << 1,
+  /* n_shards > 1 on distinct devices: gs_create also builds an RCCL
+     communicator over the shard devices (ncclCommInitAll); the static
+     matrix's offering counts (SUM) and cheapest keys (MIN) are then all-reduced
+     over it before the row gather.  GS_E_RCCL when RCCL refuses (e.g. a device
+     repeats) */
+  GS_CFG_RCCL = 1u << 2
 };
 
 /* One Go process, several devices: with n_shards > 1 the context owns one
@@ -353,14 +359,17 @@ enum {
  *    parallel (one host thread per shard), then merges the command tables and
  *    replays SingleNode/MultiNode selection (gs_consolidation_choose) on the
  *    host: the result is identical to the single-device call;
- *  - gs_feasibility / gs_feasibility_shard: the requested instance-type words
- *    split evenly over the shards; rows are disjoint (copied), offering counts
- *    added, the cheapest taken as the minimum OrderByPrice key;
+ *  - gs_feasibility / gs_feasibility_shard / gs_feasibility_shard_device:
+ *    the requested instance-type words split evenly over the shards, each
+ *    shard computes its word slice on its device; a merge kernel on `device`
+ *    gathers the slices (peer reads over xGMI; local on a repeated device),
+ *    adds the offering counts and keeps the minimum OrderByPrice key (with
+ *    GS_CFG_RCCL: counts and keys all-reduced over RCCL first).  The merged
+ *    matrix is left in `device`'s memory (gs_feas_device.t_merge_ms);
  *  - the provisioning Solve (gs_prepare/gs_run/gs_fetch) on `device` only: it
  *    is sequential in pod order and does not shard.
- * gs_prepare also encodes and uploads the problem on every shard (in parallel).
- * gs_feasibility_shard_device refuses a sharded context (its results live in
- * one device's memory: use one context per device there). */
+ * gs_prepare encodes the problem once and uploads it to every shard (in
+ * parallel). */
 typedef struct gs_config {
   int32_t device;        /* HIP device ordinal (the Solve's device) */
   uint32_t max_claims;   /* 0 = default */
@@ -498,7 +507,8 @@ typedef struct gs_feas_device {
   const uint32_t* it_name_rank;    /* host [n_its] */
   uint32_t n_pods, n_its;
   uint64_t checks;                 /* pod x offering checks of the WHOLE matrix */
-  double t_kernel_ms;
+  double t_kernel_ms;              /* sharded context: the slowest shard's kernels */
+  double t_merge_ms;               /* sharded context: the device merge (RCCL reduce + gather kernel) */
 } gs_feas_device;
 
 gs_status gs_feasibility_shard_device(gs_ctx* ctx, uint32_t word_begin, uint32_t word_end, gs_feas_device* out);

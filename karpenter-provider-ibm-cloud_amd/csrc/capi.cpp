@@ -287,12 +287,13 @@ void build_grid_orders(gs_ctx* c) {
   d.n_planes = NPL;
 }
 
-void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u) {
+void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi, bool mv_rows) {
   if (apply_limits) build_grid_orders(c);
   HIPCHK(gsk_feas(&c->dp, apply_limits, w_lo, w_hi, c->stream));
   // the static matrix's rows answer CanAdd on a fresh NodeClaim, minValues
-  // included (whole rows only: callers refuse column shards with minValues)
-  if (apply_limits && c->enc.any_mv) HIPCHK(gsk_mv_rows(&c->dp, c->stream));
+  // included (whole rows only: callers refuse column shards with minValues;
+  // a sharded context applies it after the merge)
+  if (apply_limits && mv_rows && c->enc.any_mv) HIPCHK(gsk_mv_rows(&c->dp, c->stream));
 }
 
 // device capacity of the encoded problem (the FFD kernel keeps these in LDS)
@@ -315,6 +316,24 @@ gs_status prepare_one(gs_ctx* c, const gs_problem* p) {
   er = capacity_check(c->enc);
   if (er.code != GS_OK) return fail(c, er.code, er.msg);
   c->n_nodepools = p->n_nodepools;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    auto t1 = Clock::now();
+    upload_problem(c, nullptr);
+    c->t_upload = ms_since(t1);
+  } catch (const HipError& e) {
+    return fail(c, GS_E_HIP, e.msg);
+  }
+  c->prepared = true;
+  return GS_OK;
+}
+
+gs_status prepare_from(gs_ctx* c, const gs_ctx* src) {
+  c->prepared = c->ran = false;
+  c->cons_ready = false;
+  c->enc = src->enc;
+  c->n_nodepools = src->n_nodepools;
+  c->t_encode = 0;
   try {
     HIPCHK(hipSetDevice(c->device));
     auto t1 = Clock::now();
@@ -412,6 +431,30 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
       }
       c->shards.push_back(child);
     }
+    // the merge kernel on `device` reads every shard's slice: peer access to
+    // each other device (xGMI)
+    for (gs_ctx* s : c->shards) {
+      if (s->device == c->device) continue;
+      (void)hipSetDevice(c->device);
+      const hipError_t pe = hipDeviceEnablePeerAccess(s->device, 0);
+      if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+        c->err = std::string("peer access to shard device ") + std::to_string(s->device) + ": " + hipGetErrorString(pe);
+        gs_destroy(c);
+        return GS_E_HIP;
+      }
+    }
+    if (cfg->flags & GS_CFG_RCCL) {
+      std::vector<int> devs;
+      for (gs_ctx* s : c->shards) devs.push_back(s->device);
+      c->comms.assign(devs.size(), nullptr);
+      const ncclResult_t r = ncclCommInitAll(c->comms.data(), (int)devs.size(), devs.data());
+      if (r != ncclSuccess) {
+        c->comms.clear();
+        gs_destroy(c);
+        return GS_E_RCCL;
+      }
+    }
+    (void)hipSetDevice(c->device);
   }
   *out = c;
   return GS_OK;
@@ -419,6 +462,9 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
 
 void gs_destroy(gs_ctx* c) {
   if (!c) return;
+  for (ncclComm_t m : c->comms)
+    if (m) (void)ncclCommDestroy(m);
+  c->comms.clear();
   for (gs_ctx* s : c->shards) gs_destroy(s);
   c->shards.clear();
   (void)hipSetDevice(c->device);
@@ -698,24 +744,32 @@ gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
 
 gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
-  if (c->enc.any_mv && (!c->shards.empty() || word_begin > 0 || word_end < c->enc.W))
-    return fail(c, GS_E_UNSUPPORTED, "minValues needs whole static-matrix rows (no instance-type column shards)");
-  if (!c->shards.empty()) return sharded_feasibility(c, word_begin, word_end, out);
   auto& e = c->enc;
   const uint32_t P = e.P, NP = c->n_nodepools, W = e.W;
   word_end = std::min(word_end, W);
+  if (e.any_mv && (word_begin > 0 || word_end < W))
+    return fail(c, GS_E_UNSUPPORTED, "minValues needs whole static-matrix rows (no instance-type column shards)");
   if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
-  float ms = 0;
+  double ms = 0, merge_ms = 0;
   const uint32_t OW = c->dp.OW;
   std::vector<uint64_t> rows((size_t)e.V * e.T * OW), key((size_t)e.V * e.T);
   std::vector<uint32_t> ch((size_t)e.V * e.T), nfo((size_t)e.V * e.T);
+  if (!c->shards.empty()) {
+    // the shards compute, the parent's device merges: the result is in c->dp
+    const gs_status st = sharded_compute(c, word_begin, word_end, &ms, &merge_ms);
+    if (st != GS_OK) return st;
+  }
   try {
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    launch_feas(c, 1, word_begin, word_end);
-    HIPCHK(hipEventRecord(c->ev[5], c->stream));
-    HIPCHK(hipEventSynchronize(c->ev[5]));
-    HIPCHK(hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
+    if (c->shards.empty()) {
+      float f = 0;
+      HIPCHK(hipEventRecord(c->ev[4], c->stream));
+      launch_feas(c, 1, word_begin, word_end);
+      HIPCHK(hipEventRecord(c->ev[5], c->stream));
+      HIPCHK(hipEventSynchronize(c->ev[5]));
+      HIPCHK(hipEventElapsedTime(&f, c->ev[4], c->ev[5]));
+      ms = f;
+    }
     if (!rows.empty()) HIPCHK(hipMemcpy(rows.data(), c->dp.rows, rows.size() * 8, hipMemcpyDeviceToHost));
     if (!ch.empty()) {
       HIPCHK(hipMemcpy(ch.data(), c->dp.cheapest, ch.size() * 4, hipMemcpyDeviceToHost));
@@ -734,7 +788,8 @@ gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end
     for (uint32_t t = 0; t < e.T; t++) {
       const uint32_t np = e.tmpl[t].np_index;
       const size_t src = (size_t)v * e.T + t, dst = (size_t)p * NP + np;
-      std::memcpy(&c->f_rows[dst * W], &rows[src * OW], W * 8);
+      // words outside [word_begin, word_end) stay zero
+      std::memcpy(&c->f_rows[dst * W + word_begin], &rows[src * OW + word_begin], (size_t)(word_end - word_begin) * 8);
       c->f_cheapest[dst] = ch[src] == gsd::NONE ? -1 : (int32_t)ch[src];
       c->f_nfo[dst] = nfo[src];
       c->f_key[dst] = key[src];
@@ -761,23 +816,28 @@ gs_status gs_feasibility(gs_ctx* c, gs_feas_result* out) { return gs_feasibility
 
 gs_status gs_feasibility_shard_device(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_device* out) {
   if (!c || !c->prepared || !out) return GS_E_INVALID;
-  if (!c->shards.empty())
-    return fail(c, GS_E_UNSUPPORTED, "device-resident shard results on a sharded context (use one context per device)");
   auto& e = c->enc;
   word_end = std::min(word_end, e.W);
   if (e.any_mv && (word_begin > 0 || word_end < e.W))
     return fail(c, GS_E_UNSUPPORTED, "minValues needs whole static-matrix rows (no instance-type column shards)");
   if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
-  float ms = 0;
-  try {
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    launch_feas(c, 1, word_begin, word_end);
-    HIPCHK(hipEventRecord(c->ev[5], c->stream));
-    HIPCHK(hipEventSynchronize(c->ev[5]));
-    HIPCHK(hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
-  } catch (const HipError& ex) {
-    return fail(c, GS_E_HIP, ex.msg);
+  double ms = 0, merge_ms = 0;
+  if (!c->shards.empty()) {
+    const gs_status st = sharded_compute(c, word_begin, word_end, &ms, &merge_ms);
+    if (st != GS_OK) return st;
+  } else {
+    float f = 0;
+    try {
+      HIPCHK(hipSetDevice(c->device));
+      HIPCHK(hipEventRecord(c->ev[4], c->stream));
+      launch_feas(c, 1, word_begin, word_end);
+      HIPCHK(hipEventRecord(c->ev[5], c->stream));
+      HIPCHK(hipEventSynchronize(c->ev[5]));
+      HIPCHK(hipEventElapsedTime(&f, c->ev[4], c->ev[5]));
+    } catch (const HipError& ex) {
+      return fail(c, GS_E_HIP, ex.msg);
+    }
+    ms = f;
   }
   c->f_tmpl_np.resize(e.T);
   for (uint32_t t = 0; t < e.T; t++) c->f_tmpl_np[t] = e.tmpl[t].np_index;
@@ -800,6 +860,7 @@ gs_status gs_feasibility_shard_device(gs_ctx* c, uint32_t word_begin, uint32_t w
   out->n_its = e.N;
   out->checks = e.checks;
   out->t_kernel_ms = ms;
+  out->t_merge_ms = merge_ms;
   return GS_OK;
 }
 

@@ -3,6 +3,7 @@
 // entry points.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -30,6 +31,7 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
 extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, uint32_t ch, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, uint32_t n_slots, hipStream_t s);
 extern "C" hipError_t gsk_mv_rows(const gsd::DevProblem* d, hipStream_t s);
+extern "C" hipError_t gsk_merge_shards(const gsd::ShardMerge* m, hipStream_t s);
 
 namespace gsc {
 
@@ -91,6 +93,7 @@ struct gs_ctx {
   int device = 0;
   uint32_t cfg_flags = 0;  // gs_config.flags
   std::vector<gs_ctx*> shards;  // gs_config.n_shards > 1: one child context per shard (multi.cpp)
+  std::vector<ncclComm_t> comms;  // GS_CFG_RCCL: one communicator rank per shard (ncclCommInitAll)
   std::string err;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
@@ -188,9 +191,12 @@ namespace gsc {
 
 gs_status fail(gs_ctx* c, gs_status s, const std::string& m);
 gs_status prepare_one(gs_ctx* c, const gs_problem* p);  // gs_prepare on one device
+gs_status prepare_from(gs_ctx* c, const gs_ctx* src);    // upload another context's encoding (shards)
+void launch_feas(gs_ctx* c, uint32_t apply_limits, uint32_t w_lo = 0, uint32_t w_hi = ~0u, bool mv_rows = true);
+// the static matrix of words [wb, we) on every shard, merged into the parent's device buffers
+gs_status sharded_compute(gs_ctx* c, uint32_t wb, uint32_t we, double* kernel_ms, double* merge_ms);
 // multi.cpp: contexts with shards
 gs_status sharded_prepare(gs_ctx* c, const gs_problem* p);
-gs_status sharded_feasibility(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out);
 gs_status sharded_consolidate(gs_ctx* c, const gs_consolidation* in, gs_consolidation_result* out);
 CandTable build_cand_table(const gs_problem* p, const uint32_t* cands, uint32_t n);
 int32_t choose_commands(const CandTable& t, const gs_consolidation* in, const gs_command* commands,

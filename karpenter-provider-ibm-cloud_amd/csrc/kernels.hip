@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "devutil.hpp"
 #include "layout.hpp"
 
@@ -419,6 +421,45 @@ extern "C" hipError_t gsk_mv_rows(const DevProblem* d, hipStream_t s) {
   const uint64_t pairs = (uint64_t)d->V * d->T;
   if (!pairs) return hipSuccess;
   hipLaunchKernelGGL(mv_rows_kernel, dim3((uint32_t)((pairs + BLOCK / 64 - 1) / (BLOCK / 64))), dim3(BLOCK), 0, s, *d);
+  return hipGetLastError();
+}
+
+// ==================================================== shard merge (multi-GPU)
+// A sharded context's static matrix: shard k computed instance-type words
+// [lo_k, hi_k) of every (variant, template) row on its own device.  One
+// kernel on the parent's device gathers each word from the shard that owns
+// it (peer loads over xGMI, or local memory when a device repeats), adds the
+// per-shard offering counts and keeps the minimum OrderByPrice key (the
+// cheapest offering's instance type is the key's name rank).  With RCCL the
+// counts and keys were all-reduced already: shard 0's are final (K_red = 1).
+extern "C" __global__ __launch_bounds__(BLOCK) void merge_shards_kernel(ShardMerge m) {
+  const size_t stride = (size_t)gridDim.x * BLOCK, i0 = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t nw = m.we - m.wb;
+  for (size_t i = i0; i < (size_t)m.VT * nw; i += stride) {
+    const size_t vt = i / nw;
+    const uint32_t w = m.wb + (uint32_t)(i % nw);
+    uint32_t k = 0;
+    while (k + 1 < m.K && w >= m.src[k].hi) k++;
+    m.rows[vt * m.OW + w] = m.src[k].rows[vt * m.OW + w];
+  }
+  for (size_t vt = i0; vt < m.VT; vt += stride) {
+    uint32_t n = 0;
+    uint64_t key = 0x7FFFFFFFFFFFFFFFull;
+    for (uint32_t k = 0; k < m.K_red; k++) {
+      n += m.src[k].nfo[vt];
+      const uint64_t x = m.src[k].key[vt];
+      key = x < key ? x : key;
+    }
+    m.nfo[vt] = n;
+    m.key[vt] = key;
+    m.cheapest[vt] = key == 0x7FFFFFFFFFFFFFFFull ? NONE : m.rank_to_it[(uint32_t)key];
+  }
+}
+
+extern "C" hipError_t gsk_merge_shards(const ShardMerge* m, hipStream_t s) {
+  const size_t work = (size_t)m->VT * (m->we - m->wb > 0 ? m->we - m->wb : 1);
+  const uint32_t grid = (uint32_t)std::min<size_t>((work + BLOCK - 1) / BLOCK, 8192);
+  hipLaunchKernelGGL(merge_shards_kernel, dim3(grid ? grid : 1), dim3(BLOCK), 0, s, *m);
   return hipGetLastError();
 }
 

@@ -345,4 +345,24 @@ struct DevProblem {
   NodeVol* ov_vol;             // [grid][ov_cap]
 };
 
+// the parent-side merge of a sharded static matrix (kernels.hip
+// merge_shards_kernel): the shards' device buffers and word slices
+constexpr int SHARDS_MAX = 16;
+struct ShardSrc {
+  const uint64_t* rows;  // [VT][OW] (words [lo, hi) valid)
+  const uint32_t* nfo;   // [VT]
+  const uint64_t* key;   // [VT]
+  uint32_t lo, hi;
+};
+struct ShardMerge {
+  ShardSrc src[SHARDS_MAX];
+  uint32_t K, K_red;     // shards; shards whose counts / keys still need reducing (1 after RCCL)
+  uint32_t VT, OW, wb, we;
+  uint64_t* rows;
+  uint32_t* nfo;
+  uint64_t* key;
+  uint32_t* cheapest;
+  const uint32_t* rank_to_it;
+};
+
 }  // namespace gsd

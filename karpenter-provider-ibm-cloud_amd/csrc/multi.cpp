@@ -7,9 +7,11 @@
 // the SingleNode / MultiNode selection on the host exactly as
 // gs_consolidation_choose does, so the result equals the single-device call.
 // The static feasibility matrix shards by instance-type words: each shard
-// computes a disjoint word range, the parent copies the rows, adds the
-// offering counts and keeps the minimum OrderByPrice key.  The provisioning
-// Solve is sequential in pod order and stays on the parent's device.
+// computes a disjoint word range on its device; a merge kernel on the parent's
+// device gathers the rows (peer reads over xGMI), adds the offering counts
+// and keeps the minimum OrderByPrice key (RCCL all-reduces the counts and keys
+// first with GS_CFG_RCCL).  The provisioning Solve is sequential in pod order
+// and stays on the parent's device.
 #include <thread>
 
 #include "ctx.hpp"
@@ -41,61 +43,93 @@ gs_status first_error(gs_ctx* c, const std::vector<gs_status>& st) {
 
 }  // namespace
 
+// encode once on the parent, upload that encoding to every shard in parallel
 gs_status sharded_prepare(gs_ctx* c, const gs_problem* p) {
-  gs_status mine = GS_OK;
-  std::thread self([&] { mine = prepare_one(c, p); });
-  auto st = on_shards(c, [&](size_t k) { return gs_prepare(c->shards[k], p); });
-  self.join();
+  const gs_status mine = prepare_one(c, p);
   if (mine != GS_OK) return mine;
+  auto st = on_shards(c, [&](size_t k) { return prepare_from(c->shards[k], c); });
   return first_error(c, st);
 }
 
-gs_status sharded_feasibility(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {
-  auto& e = c->enc;
-  const uint32_t W = e.W, P = e.P, NP = c->n_nodepools, K = (uint32_t)c->shards.size();
-  word_end = std::min(word_end, W);
-  if (word_begin > word_end) return fail(c, GS_E_INVALID, "empty or inverted word range");
-  std::vector<gs_feas_result> r(K);
-  auto st = on_shards(c, [&](size_t k) {
-    const uint32_t n = word_end - word_begin;
-    const uint32_t lo = word_begin + (uint32_t)((uint64_t)n * k / K), hi = word_begin + (uint32_t)((uint64_t)n * (k + 1) / K);
-    return gs_feasibility_shard(c->shards[k], lo, hi, &r[k]);
-  });
-  const gs_status es = first_error(c, st);
-  if (es != GS_OK) return es;
-  const size_t PN = (size_t)P * NP;
-  c->f_rows.assign(PN * W, 0);
-  c->f_nfo.assign(PN, 0);
-  c->f_key.assign(PN, 0x7FFFFFFFFFFFFFFFull);
-  c->f_cheapest.assign(PN, -1);
-  double ms = 0;
-  for (uint32_t k = 0; k < K; k++) {
-    // rows: each shard's words are its own (zero elsewhere)
-    for (uint32_t w = r[k].word_begin; w < r[k].word_end; w++)
-      for (size_t q = 0; q < PN; q++) c->f_rows[q * W + w] = r[k].rows[q * W + w];
-    for (size_t q = 0; q < PN; q++) {
-      c->f_nfo[q] += r[k].n_feasible_offerings[q];
-      if (r[k].cheapest_key[q] < c->f_key[q]) {
-        c->f_key[q] = r[k].cheapest_key[q];
-        c->f_cheapest[q] = r[k].cheapest_it[q];
-      }
+// The static matrix of words [wb, we): shard k computes its even slice on its
+// own device (no minValues pass: rows are partial), then -- with RCCL -- the
+// offering counts (SUM) and cheapest keys (MIN) are all-reduced across the
+// shards' buffers in place, and one kernel on the parent's device gathers
+// every word from its owner and finishes the counts / keys (merge_shards_kernel).
+// The merged matrix is the parent's own device buffers; minValues runs on it.
+gs_status sharded_compute(gs_ctx* c, uint32_t wb, uint32_t we, double* kernel_ms, double* merge_ms) {
+  const uint32_t K = (uint32_t)c->shards.size();
+  if (K > (uint32_t)gsd::SHARDS_MAX) return fail(c, GS_E_INVALID, "more than 16 shards");
+  const uint32_t n = we - wb;
+  auto lo_of = [&](uint32_t k) { return wb + (uint32_t)((uint64_t)n * k / K); };
+  std::vector<float> t(K, 0.f);
+  auto st = on_shards(c, [&](size_t k) -> gs_status {
+    gs_ctx* s = c->shards[k];
+    try {
+      HIPCHK(hipSetDevice(s->device));
+      HIPCHK(hipEventRecord(s->ev[4], s->stream));
+      launch_feas(s, 1, lo_of((uint32_t)k), lo_of((uint32_t)k + 1), false);
+      HIPCHK(hipEventRecord(s->ev[5], s->stream));
+      HIPCHK(hipEventSynchronize(s->ev[5]));
+      HIPCHK(hipEventElapsedTime(&t[k], s->ev[4], s->ev[5]));
+    } catch (const HipError& ex) {
+      return fail(s, GS_E_HIP, ex.msg);
     }
-    ms = std::max(ms, r[k].t_kernel_ms);
+    return GS_OK;
+  });
+  gs_status es = first_error(c, st);
+  if (es != GS_OK) return es;
+  *kernel_ms = 0;
+  for (float x : t) *kernel_ms = std::max(*kernel_ms, (double)x);
+  const size_t VT = (size_t)c->enc.V * c->enc.T;
+  auto t0 = Clock::now();
+  if (!c->comms.empty()) {
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t k = 0; k < K && r == ncclSuccess; k++) {
+      gs_ctx* s = c->shards[k];
+      r = ncclAllReduce(s->dp.cheapest_key, s->dp.cheapest_key, VT, ncclUint64, ncclMin, c->comms[k], s->stream);
+      if (r == ncclSuccess) r = ncclAllReduce(s->dp.nfo, s->dp.nfo, VT, ncclUint32, ncclSum, c->comms[k], s->stream);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(c, GS_E_RCCL, std::string("RCCL all-reduce of the shard keys / counts: ") +
+                                    ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (gs_ctx* s : c->shards) {
+      (void)hipSetDevice(s->device);
+      if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(c, GS_E_RCCL, "RCCL stream");
+    }
   }
-  std::memset(out, 0, sizeof(*out));
-  out->n_pods = P;
-  out->n_nodepools = NP;
-  out->n_its = e.N;
-  out->words = W;
-  out->rows = c->f_rows.data();
-  out->cheapest_it = c->f_cheapest.data();
-  out->n_feasible_offerings = c->f_nfo.data();
-  out->checks = e.checks;
-  out->t_kernel_ms = ms;
-  out->cheapest_key = c->f_key.data();
-  out->it_name_rank = e.it_namerank.data();
-  out->word_begin = word_begin;
-  out->word_end = word_end;
+  gsd::ShardMerge m{};
+  for (uint32_t k = 0; k < K; k++) {
+    const gsd::DevProblem& sd = c->shards[k]->dp;
+    m.src[k] = gsd::ShardSrc{sd.rows, sd.nfo, sd.cheapest_key, lo_of(k), lo_of(k + 1)};
+  }
+  m.K = K;
+  m.K_red = c->comms.empty() ? K : 1u;
+  m.VT = (uint32_t)VT;
+  m.OW = c->dp.OW;
+  m.wb = wb;
+  m.we = we;
+  m.rows = c->dp.rows;
+  m.nfo = c->dp.nfo;
+  m.key = c->dp.cheapest_key;
+  m.cheapest = c->dp.cheapest;
+  m.rank_to_it = c->dp.rank_to_it;
+  float mk = 0;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventRecord(c->ev[6], c->stream));
+    HIPCHK(gsk_merge_shards(&m, c->stream));
+    HIPCHK(hipEventRecord(c->ev[7], c->stream));
+    if (c->enc.any_mv) HIPCHK(gsk_mv_rows(&c->dp, c->stream));  // whole rows now
+    HIPCHK(hipEventSynchronize(c->ev[7]));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&mk, c->ev[6], c->ev[7]));
+  } catch (const HipError& ex) {
+    return fail(c, GS_E_HIP, ex.msg);
+  }
+  // the gather kernel; with RCCL the host wall clock over all-reduce + gather
+  *merge_ms = c->comms.empty() ? (double)mk : ms_since(t0);
   return GS_OK;
 }
 

@@ -132,7 +132,7 @@ class GsFeasDevice(C.Structure):
         ("it_name_rank", C.POINTER(C.c_uint32)),
         ("n_pods", _U32), ("n_its", _U32),
         ("checks", C.c_uint64),
-        ("t_kernel_ms", C.c_double),
+        ("t_kernel_ms", C.c_double), ("t_merge_ms", C.c_double),
     ]
 
 
@@ -152,6 +152,7 @@ class GsFeasResult(C.Structure):
 
 GS_CFG_BLOCK_SOLVE = 1  # gs_config.flags: run the Solve on the block kernel
 GS_CFG_CLAIMS_HBM = 2   # gs_config.flags: single-wave Solve with its claim scan state in HBM
+GS_CFG_RCCL = 4         # gs_config.flags: sharded context with an RCCL communicator over the shard devices
 
 
 class GsConfig(C.Structure):

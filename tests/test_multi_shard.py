@@ -95,9 +95,62 @@ def test_sharded_solve_runs_on_parent(single, sharded):
     assert sharded.solve(p)[0] == single.solve(p)[0]
 
 
-def test_sharded_device_results_refused(sharded):
+def _device_result(solver, lo, hi):
+    import torch
+    from gpusched.feasibility import device_views
+    res = solver.feasibility_shard_device(lo, hi)
+    rows, nfo, key = (x.clone() for x in device_views(res, torch.device("cuda", 0)))
+    S = res.row_stride
+    rows = rows.view(-1, S)[:, lo:min(hi, res.words)].cpu()
+    return rows, nfo.cpu(), key.cpu(), res
+
+
+@pytest.mark.parametrize("make", [lambda: synth.make_c3(n_pods=2000), lambda: synth.random_problem(2),
+                                  lambda: synth.make_c5(n_pods=5000)], ids=["c3", "random", "c5"])
+def test_sharded_device_results_equal_single(single, sharded, make):
+    """gs_feasibility_shard_device on a sharded context: the shards' slices
+    gathered and their counts / keys reduced ON the parent's device (the
+    merge kernel) equal one device's matrix, whole and over a word sub-range"""
+    p = make()
+    single.prepare(p)
+    sharded.prepare(p)
+    W = single.feasibility_shard_device(0, 0).words
+    for lo, hi in ((0, W), (W // 3, max(W // 3 + 1, W - 1))):
+        want = _device_result(single, lo, hi)
+        got = _device_result(sharded, lo, hi)
+        for a, b in zip(got[:3], want[:3]):
+            assert torch_equal(a, b)
+        assert got[3].t_merge_ms > 0
+
+
+def torch_equal(a, b):
+    import torch
+    return bool(torch.equal(a, b))
+
+
+def test_rccl_shards():
+    """GS_CFG_RCCL: the shards' counts / keys are all-reduced by RCCL before
+    the gather.  RCCL refuses a communicator whose ranks repeat a device --
+    gs_create then returns GS_E_RCCL; where it accepts them the all-reduced
+    matrix must equal one device's"""
     from gpusched import lib
-    sharded.prepare(synth.random_problem(2))
-    with pytest.raises(lib.GpuSchedError) as e:
-        sharded.feasibility_shard_device(0, 1)
-    assert e.value.status == abi.GS_E_UNSUPPORTED
+    try:
+        s = lib.Solver(shard_devices=[0, 0], flags=abi.GS_CFG_RCCL)
+    except lib.GpuSchedError as e:
+        assert e.status == abi.GS_E_RCCL
+        print("RCCL refused the repeated device: GS_E_RCCL")
+        return
+    print("RCCL accepted the repeated device: all-reduce path")
+    one = lib.Solver()
+    try:
+        p = synth.make_c3(n_pods=2000)
+        one.prepare(p)
+        s.prepare(p)
+        W = one.feasibility_shard_device(0, 0).words
+        want = _device_result(one, 0, W)
+        got = _device_result(s, 0, W)
+        for a, b in zip(got[:3], want[:3]):
+            assert torch_equal(a, b)
+    finally:
+        s.close()
+        one.close()
