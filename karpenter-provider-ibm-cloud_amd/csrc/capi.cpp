@@ -39,7 +39,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     // (single-wave kernel) the existing nodes' slack codes
     // (the block kernel's capacity; the single-wave kernel's is smaller by the
     // node codes -- a Solve that outgrows it reruns on the block kernel)
-    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) + 8;
+    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) + 8;
     const uint32_t dyn = std::min(gsk_ffd_dyn_lds_max(), gsk_ffdw_dyn_lds_max());
     auto claims_fit = [&](uint32_t extra) {
       const uint32_t fit = dyn > other + extra ? (dyn - other - extra) / 23 : 0;
@@ -176,6 +176,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     // the general (topology / volumes / minValues) simulation variant
     c->alloc(d.ov_hn, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1));
     c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
+    c->alloc(d.ov_map, (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
     {
       std::vector<uint64_t> known = sims->known;
       known.resize(std::max<size_t>(NS, 1), 0);

@@ -309,8 +309,7 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     return GS_E_CAPACITY;
   }
   const uint32_t lds = gsk_ffd_lds_bytes(std::max<uint32_t>(sp.max_pods, 1), (uint32_t)e.thr_val.size(),
-                                         (e.NN + 31) / 32, std::max<uint32_t>(sp.ov_cap, 1),
-                                         gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH));
+                                         (e.NN + 31) / 32, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH));
   if (lds > gsk_ffd_dyn_lds_max()) {
     *err = "simulation exceeds the workgroup LDS (pods per simulation or state nodes)";
     return GS_E_CAPACITY;

@@ -21,7 +21,7 @@ extern "C" hipError_t gsk_init_trunc(uint32_t trunc_lds_bytes);
 extern "C" hipError_t gsk_init_ffd(uint32_t lds_total);
 extern "C" uint32_t gsk_ffd_dyn_lds_max(void);
 extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t nt, uint32_t general);
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words,
                                       uint32_t topo_bytes);
 extern "C" hipError_t gsk_feas(const gsd::DevProblem* d, uint32_t apply_limits, uint32_t w_lo, uint32_t w_hi,
                                hipStream_t s);

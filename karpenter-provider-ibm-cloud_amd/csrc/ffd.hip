@@ -597,9 +597,10 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   const uint32_t nthr = d.thr_off[R];
   const int64_t* thr = s_thr;  // gs_prepare refuses nthr > THR_LDS_MAX
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
-  uint32_t* s_ovid = s_nb + d.nb_words;                                                    // SIM: overlay ids
+  // SIM: a touched node's overlay entry (| OV_EXCL: a removed candidate), valid where its s_nb bit is set
+  uint32_t* const ov_map = SIM ? d.ov_map + (size_t)blockIdx.x * d.NN : nullptr;
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
-  const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + d.ov_cap * 4u + 7u) & ~7u;
+  const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
   Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
   Wg<NT> wg{&S.red2[0][0], s_sc, s_ord, tid, tid & 63, tid >> 6, 0};
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       __syncthreads();
       for (uint32_t k = tid; k < ncand; k += FB) {
         const uint32_t n = d.sim_cands[c0 + k];
-        s_ovid[k] = n | OV_EXCL;
+        ov_map[n] = k | OV_EXCL;
         atomicOr(&s_nb[n >> 5], 1u << (n & 31));
       }
       if (TOPO) {
@@ -918,9 +919,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             size_t oe = ~(size_t)0;  // SIM: the node's overlay entry (hostname counts, volume usage)
             if (SIM && feas && ((s_nb[n >> 5] >> (n & 31)) & 1)) {
               // touched by this simulation: removed candidate, or overlay copy
-              uint32_t e = 0;
-              while ((s_ovid[e] & ~OV_EXCL) != n) e++;
-              if (s_ovid[e] & OV_EXCL) {
+              const uint32_t e = ov_map[n];
+              if (e & OV_EXCL) {
                 feas = false;
               } else {
                 oe = (size_t)blockIdx.x * d.ov_cap + e;
@@ -973,12 +973,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (tid == 0) {
               uint32_t e = INF;
               if ((s_nb[fn >> 5] >> (fn & 31)) & 1) {
-                e = 0;
-                while ((s_ovid[e] & ~OV_EXCL) != fn) e++;
+                e = ov_map[fn];  // a kept node (the scan rejects removed ones)
                 S.ov_new = 0;
               } else {
                 e = S.nov++;
-                s_ovid[e] = fn;
+                ov_map[fn] = e;
                 s_nb[fn >> 5] |= 1u << (fn & 31);
                 S.ov_new = 1;
               }
@@ -1799,12 +1798,12 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
 }
 
 // dynamic LDS: slack + room u64, ord/sc/scr u16, tmpl u8 per claim, thresholds,
-// (simulations) the touched-node bitmap + overlay ids, and the topology
+// (simulations) the touched-node bitmap, and the topology
 // spread state (known domains, per-pod minimum, zone counts) of TG groups
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words,
                                       uint32_t topo_bytes) {
   const uint32_t thr = nthr + 4;
-  const uint32_t base = (((23u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + ov_cap * 4u + 7u) & ~7u;
+  const uint32_t base = (((23u * max_claims + 7u) & ~7u) + thr * 8u + nb_words * 4u + 7u) & ~7u;
   return base + topo_bytes;
 }
 
@@ -1871,7 +1870,7 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, d->ov_cap, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations,

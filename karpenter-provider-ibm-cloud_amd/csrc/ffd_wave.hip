@@ -1671,7 +1671,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 }
 
 // ---------------------------------------------------------------- launchers
-extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words, uint32_t ov_cap,
+extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words,
                                       uint32_t topo_bytes);
 static uint32_t g_ffdw_dyn_max = 0;
 
@@ -1708,7 +1708,7 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
 // the single-wave provisioning Solve: grid-wide state reset, then one wave;
 // ch: the claim scan state in HBM (d->ch_* allocated, claim_cap slots)
 extern "C" hipError_t gsk_ffdw(const DevProblem* d, uint32_t ch, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(ch ? 0u : d->max_claims_wave, d->n_thr, 0, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+  const uint32_t lds = gsk_ffd_lds_bytes(ch ? 0u : d->max_claims_wave, d->n_thr, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
                        wave_node_lds_bytes(d->NN);
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;

@@ -343,6 +343,7 @@ struct DevProblem {
   const int32_t* zn_cnt;       // [TGZ][NN]
   int32_t* ov_hn;              // [grid][ov_cap][TGH]
   NodeVol* ov_vol;             // [grid][ov_cap]
+  uint32_t* ov_map;            // [grid][NN] a touched node's overlay entry (valid where the LDS bitmap bit is set)
 };
 
 // the parent-side merge of a sharded static matrix (kernels.hip

@@ -131,3 +131,22 @@ def test_gpu_e2e_consolidation_5000_nodes_sampled(solver):
     st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, cands[:8], mode=abi.CONSOLIDATE_EVAL, sets=sets))
     assert st == abi.GS_OK
     assert multi[:7] == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["c4", "e2e"])
+def test_gpu_multi_prefixes_5000_nodes_sampled(solver, shape):
+    """MultiNodeConsolidation over a 5,000-node cluster:
+    the device evaluates all 100 binary-search prefixes candidates[0:mid+1];
+    a sample across the whole range -- up to the 101-candidate prefix that
+    re-solves ~1,650 pods onto the 4,899 kept nodes -- against the oracle's
+    re-Solve of the same candidate sets"""
+    p = synth.make_c4(n_nodes=5000) if shape == "c4" else synth.e2e_consolidation_cluster(n_nodes=5000)
+    cands = list(range(5000))
+    multi, _, _, _ = solver.consolidate(ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_MULTI))
+    assert len(multi) == 100
+    sample = sorted(set(range(0, 100, 9)) | {99})
+    sets = [(0, j + 2) for j in sample]  # multi[j] simulates candidates[0:j+2]
+    st, want, _, _ = pyoracle.consolidate(ConsolidationInput(p, cands[:101], mode=abi.CONSOLIDATE_EVAL, sets=sets))
+    assert st == abi.GS_OK
+    assert [multi[j] for j in sample] == want
