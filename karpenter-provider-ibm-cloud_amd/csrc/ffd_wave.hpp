@@ -1,0 +1,1676 @@
+// ffd_wave.hpp — the single-wave provisioning Solve kernel template
+// (ffdw_kernel), shared by the per-(R, TOPO) translation units
+// ffd_wave_r.hip compiles (one per resource count and variant: the
+// register-mode instantiations are large, so they build in parallel).
+#pragma once
+//
+// The <U> Scheduler.Solve queue loop is sequential in pod order; its cost
+// per pod is a chain of dependent steps (pop, sort.Slice emulation, first-fit
+// scan of the in-flight NodeClaims, NodeClaim.Add).  A multi-wave workgroup
+// pays a workgroup barrier and an LDS round trip of shared loop state for
+// every step of that chain; one wave pays neither:
+//  * the loop state (queue head/length, epoch, claim count, pending sort
+//    modification) lives in scalar registers;
+//  * the sorted NodeClaim order is one packed u32 per position (count in the
+//    low 16 bits, claim id in the high 16): one LDS access reads or moves
+//    both, and the scan reads a position's claim id and count together;
+//  * every cross-lane LDS hand-off is ordered by the wave's in-order LDS
+//    queue (wsync() only stops the compiler from reordering);
+//  * the next pod's variant record and requests are prefetched into lanes
+//    during the current pod (first pass: records laid out in queue order);
+//  * a fast-accepted NodeClaim.Add (requests only) is LDS updates plus
+//    no-return atomic adds of the requests at L2: no round trip.
+// Results are bit-identical to ffd.hip's block kernel (same restatement of
+// Go's sort.Slice, same candidate order, same Add), which still serves the
+// consolidation simulations and Solves with many existing nodes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "devutil.hpp"
+#include "ffd_common.hpp"
+#include "layout.hpp"
+
+using namespace gsd;
+
+namespace {
+
+constexpr uint32_t VR_DW = sizeof(VarRec) / 4;
+static_assert(VR_DW == 32, "VarRec is one dword per lane of a half wave");
+static_assert(offsetof(VarRec, fk_begin) == 4 && offsetof(VarRec, fk_count) == 8 && offsetof(VarRec, ctb) == 12 &&
+                  offsetof(VarRec, itmask_off) == 16 && offsetof(VarRec, zfull_off) == 48 &&
+                  offsetof(VarRec, cfull_off) == 52 && offsetof(VarRec, zm) == 56 && offsetof(VarRec, cm) == 64 &&
+                  offsetof(VarRec, tol) == 72 && offsetof(VarRec, tolt) == 80 && offsetof(VarRec, own_off) == 88 &&
+                  offsetof(VarRec, own_n) == 92 && offsetof(VarRec, sel_off) == 96 && offsetof(VarRec, sel_n) == 100 &&
+                  offsetof(VarRec, zs) == 104 && offsetof(VarRec, zn) == 112 &&
+                  offsetof(VarRec, zflags) == 120 && offsetof(VarRec, vix) == 124,
+              "VarRec dword map used by ffdw_kernel");
+static_assert(offsetof(ClaimRec, maxa) == 128, "ClaimRec maxa after two 64-B lines");
+
+constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
+// solver <-> memory-agent wave channels (LDS)
+constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the solver
+constexpr uint32_t RING_DW = 52; // VarRec (32 dwords) + requests (<= 16 dwords) + request codes (4 dwords)
+constexpr uint32_t RING_CODES = 48;  // lanes 48..51: floor codes lo/hi dword, ceil codes lo/hi dword
+constexpr uint32_t WQ = 32;      // global-memory write requests in flight
+constexpr uint32_t WQ_DW = 16;
+enum : uint32_t { WQ_LOG = 1, WQ_FA = 2, WQ_STOP = 3, WQ_NFA = 4 };
+constexpr uint32_t SPIN_MAX = 1u << 26;  // bounded waits: a stuck partner ends the kernel, not the GPU
+constexpr uint64_t SWAR_HI = 0x8000800080008000ull;  // top bit of each 16-bit code field
+enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
+#ifndef GS_WAVE_SEQ
+#define GS_WAVE_SEQ 32
+#endif
+
+// compiler barrier for LDS hand-offs between lanes of the one wave: the
+// hardware keeps a wave's LDS accesses in order, the compiler must too
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// the claim scan state's hand-offs between lanes: in LDS the wave's in-order
+// LDS queue orders them (wsync); in HBM (G) every store must have completed
+// before another lane's load (s_waitcnt 0: a wave's stores and loads share
+// the vector memory counter on gfx9, and the CU's write-through L1 serves the
+// completed store)
+template <bool G>
+__device__ __forceinline__ void wsyncT() {
+  if (G) __builtin_amdgcn_s_waitcnt(0);
+  wsync();
+}
+
+// readlane as an unsigned dword (the builtin returns int: widening it
+// directly would sign-extend a low dword with bit 31 set)
+__device__ __forceinline__ uint32_t rlane(uint32_t x, uint32_t i) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)i);
+}
+
+// GS_FFD_TL (diagnostic build): shader cycles per pod-loop segment into Ctrl.dbg
+#ifdef GS_FFD_TL
+#define TLW(k)                                         \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
+    tl[k] += t_ - tl_last;                             \
+    tl_last = t_;                                      \
+  } while (0)
+#else
+#define TLW(k) \
+  do {         \
+  } while (0)
+#endif
+
+// channel words are polled: volatile LDS accesses.  The pointer is cast to
+// the LDS address space explicitly (a volatile access through a generic
+// pointer compiles to a flat, system-coherent load that also waits on every
+// outstanding global memory operation).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t vld(const uint32_t* p) { return *(const volatile lds_u32*)(const lds_u32*)p; }
+__device__ __forceinline__ void vst(uint32_t* p, uint32_t x) { *(volatile lds_u32*)(lds_u32*)p = x; }
+
+// The Solve loop keeps only its own state in scalar registers; its cold
+// paths re-read the kernel arguments through the kernarg pointer (scalar
+// loads from the constant cache) and the pod's variant fields from the
+// record lane (readlane) where they use them, instead of holding ~100
+// scalar values across the loop (which spills them into VGPR lanes).
+__device__ __forceinline__ KArg karg() {
+  KArg p = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// an opaque copy: readlanes of it are not merged with earlier ones
+__device__ __forceinline__ uint32_t fresh(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+__device__ __forceinline__ uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((long long)m) - 1u; }
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t x, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t y = shfl_xor_u64(x, m);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+// ------------------------------------------------ 16-bit code fields (SWAR)
+// a request / slack / room is four 15-bit codes in one u64 (layout.hpp
+// qcode); SWAR_HI keeps the borrow of each field inside the field
+__device__ __forceinline__ bool swar_ge(uint64_t a, uint64_t b) {  // every field a >= b
+  return (((a | SWAR_HI) - b) & SWAR_HI) == SWAR_HI;
+}
+__device__ __forceinline__ uint64_t swar_max(uint64_t a, uint64_t b) {  // field-wise max
+  const uint64_t m = ((((a | SWAR_HI) - b) & SWAR_HI) >> 15) * 0xFFFFull;
+  return (a & m) | (b & ~m);
+}
+__device__ __forceinline__ uint64_t wave_swar_max(uint64_t x) {
+  for (int m = 32; m >= 1; m >>= 1) x = swar_max(x, shfl_xor_u64(x, m));
+  return x;
+}
+
+// -------------------------------------------------------- wave-parallel sort
+// sort.Slice(newNodeClaims, len(Pods) asc) over the packed order: the block
+// restatement of pdqsort_func (ffd.hip Blk) with one wave, so every block
+// reduction is a ballot and every barrier an in-order LDS queue.  Ranges up
+// to SEQ elements run the sequential port on lane 0.
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
+struct WaveSort {
+  static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
+  U32* so;
+  U16* scr;  // compaction scratch: [0, half) left list, [half, 2 half) right list
+  lds_frame* stk;
+  uint32_t lane, half;
+
+  __device__ __forceinline__ uint32_t key(int i) const { return so[i] & 0xFFFFu; }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    const uint32_t a = so[i];
+    so[i] = so[j];
+    so[j] = a;
+  }
+  // the passes below test RW x 64 positions per step: every lane issues its
+  // RW LDS reads before the first ballot (one round trip per step)
+  static constexpr int RW = 4;
+  template <class Pred>
+  __device__ uint32_t count(int lo, int hi, Pred pred) const {
+    uint32_t c = 0;
+    for (int base = lo; base < hi; base += 64 * RW) {
+      bool in[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        in[u] = k < hi && pred(k);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) c += (uint32_t)__popcll(__ballot(in[u]));
+    }
+    return c;
+  }
+  // positions k in [lo,hi) with pred(k), ascending or descending, to out[]
+  template <class Pred>
+  __device__ uint32_t compact(int lo, int hi, bool desc, U16* out, Pred pred) const {
+    uint32_t total = 0;
+    const int n = hi - lo;
+    for (int base = 0; base < n; base += 64 * RW) {
+      bool in[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int idx = base + u * 64 + (int)lane;
+        in[u] = idx < n && pred(desc ? hi - 1 - idx : lo + idx);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int idx = base + u * 64 + (int)lane;
+        const uint64_t m = __ballot(in[u]);
+        if (in[u]) out[total + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(desc ? hi - 1 - idx : lo + idx);
+        total += (uint32_t)__popcll(m);
+      }
+    }
+    wsyncT<G>();
+    return total;
+  }
+  // swap the k-th left-list position with the k-th right-list position
+  __device__ void swap_lists(uint32_t s) const {
+    for (uint32_t k = lane; k < s; k += 64) {
+      const int x = scr[k], y = scr[half + k];
+      const uint32_t a = so[x], b = so[y];
+      wsyncT<G>();
+      so[x] = b;
+      so[y] = a;
+    }
+    wsyncT<G>();
+  }
+  __device__ int partition(int a, int b, int pivot, bool* already) const {
+    if (lane == 0) swap(a, pivot);
+    wsyncT<G>();
+    const uint32_t p = key(a);
+    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) < p; });
+    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
+    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
+    swap_lists(s);
+    if (lane == 0) swap(mid, a);
+    wsyncT<G>();
+    *already = s == 0;
+    return mid;
+  }
+  __device__ int partition_equal(int a, int b, int pivot) const {
+    if (lane == 0) swap(a, pivot);
+    wsyncT<G>();
+    const uint32_t p = key(a);
+    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) <= p; });
+    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
+    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) <= p; });
+    swap_lists(s);
+    return mid + 1;
+  }
+  // one rotation: left = the element at lo lands at hi, (lo, hi] shift left;
+  // otherwise the element at hi lands at lo, [lo, hi) shift right.  Passes of
+  // 64 positions read before they write, in the order that never overwrites
+  // a position a later pass still reads.
+  __device__ void rotate(int lo, int hi, bool left) const {
+    if (hi <= lo) return;
+    const uint32_t x = so[left ? lo : hi];
+    wsyncT<G>();
+    // RU x 64 positions per pass: every lane loads its RU values (one LDS
+    // round trip), then stores them one position over
+    constexpr int RU = 4;
+    if (left) {
+      for (int base = lo; base < hi; base += 64 * RU) {
+        uint32_t v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = base + u * 64 + (int)lane;
+          v[u] = k < hi ? so[k + 1] : 0u;
+        }
+        wsyncT<G>();
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = base + u * 64 + (int)lane;
+          if (k < hi) so[k] = v[u];
+        }
+        wsyncT<G>();
+      }
+      if (lane == 0) so[hi] = x;
+    } else {
+      for (int top = hi - 1; top >= lo; top -= 64 * RU) {
+        uint32_t v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = top - u * 64 - (int)lane;
+          v[u] = k >= lo ? so[k] : 0u;
+        }
+        wsyncT<G>();
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+          const int k = top - u * 64 - (int)lane;
+          if (k >= lo) so[k + 1] = v[u];
+        }
+        wsyncT<G>();
+      }
+      if (lane == 0) so[lo] = x;
+    }
+    wsyncT<G>();
+  }
+  // first k in [from, b) with key(k) < key(k-1); b if none
+  __device__ int first_inversion(int from, int b) const {
+    for (int base = from; base < b; base += 64 * RW) {
+      bool hit[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        hit[u] = k < b && key(k) < key(k - 1);
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const uint64_t m = __ballot(hit[u]);
+        if (m) return base + u * 64 + (int)ffs64(m);
+      }
+    }
+    return b;
+  }
+  __device__ bool partial_insertion_sort(int a, int b) const {
+    int i = a + 1;
+    for (int j = 0; j < 5; j++) {
+      i = first_inversion(i, b);
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      if (lane == 0) swap(i, i - 1);
+      wsyncT<G>();
+      if (i - a >= 2) {
+        // the smaller element (now at i-1) moves left past larger elements,
+        // down to absolute index 0 (Go's loop runs to j >= 1)
+        const uint32_t x = key(i - 1);
+        int q = -1;
+        for (int top = i - 2; top >= 0; top -= 64) {
+          const int k = top - (int)lane;
+          const uint64_t m = __ballot(k >= 0 && key(k) <= x);
+          if (m) {
+            q = top - (int)ffs64(m);  // lowest lane = highest position
+            break;
+          }
+        }
+        rotate(q + 1, i - 1, false);
+      }
+      if (b - i >= 2) {
+        const uint32_t y = key(i);
+        int q = b;
+        for (int base = i + 1; base < b; base += 64) {
+          const int k = base + (int)lane;
+          const uint64_t m = __ballot(k < b && key(k) >= y);
+          if (m) {
+            q = base + (int)ffs64(m);
+            break;
+          }
+        }
+        rotate(i, q - 1, true);
+      }
+    }
+    return false;
+  }
+  __device__ void reverse_range(int a, int b) const {
+    const int n = (b - a) / 2;
+    for (int k = (int)lane; k < n; k += 64) {
+      const uint32_t x = so[a + k], y = so[b - 1 - k];
+      wsyncT<G>();
+      so[a + k] = y;
+      so[b - 1 - k] = x;
+    }
+    wsyncT<G>();
+  }
+  __device__ __forceinline__ void pdqsort_body(int n) const {
+    const SeqSortT<PackedAccT<U32>> seq{{so}};
+    if (n <= SEQ) {
+      if (lane == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
+      wsyncT<G>();
+      return;
+    }
+    int sp = 0;
+    Frame f{0, n, bits_len((uint64_t)n), 1, 1};
+    for (;;) {
+      for (;;) {
+        const int length = f.b - f.a;
+        if (length <= SEQ) {
+          if (lane == 0) seq.pdq_frame(f);
+          wsyncT<G>();
+          break;
+        }
+        if (f.limit == 0) {
+          if (lane == 0) seq.heap_sort(f.a, f.b);
+          wsyncT<G>();
+          break;
+        }
+        if (!f.wb) {
+          if (lane == 0) seq.break_patterns(f.a, f.b);
+          wsyncT<G>();
+          f.limit--;
+        }
+        int hint = 0;
+        int pivot = seq.choose_pivot_fast(f.a, f.b, &hint);  // every lane, same keys
+        pivot = __builtin_amdgcn_readfirstlane(pivot);
+        hint = __builtin_amdgcn_readfirstlane(hint);
+        if (hint == 2) {
+          reverse_range(f.a, f.b);
+          pivot = (f.b - 1) - (pivot - f.a);
+          hint = 1;
+        }
+        if (f.wb && f.wp && hint == 1) {
+          if (partial_insertion_sort(f.a, f.b)) break;
+        }
+        if (f.a > 0 && !(key(f.a - 1) < key(pivot))) {
+          f.a = partition_equal(f.a, f.b, pivot);
+          continue;
+        }
+        bool already;
+        const int mid = partition(f.a, f.b, pivot, &already);
+        f.wp = already;
+        const int leftLen = mid - f.a, rightLen = f.b - mid;
+        const int bal = length / 8;
+        Frame child;
+        if (leftLen < rightLen) {
+          f.wb = leftLen >= bal;
+          child = Frame{f.a, mid, f.limit, 1, 1};
+          f.a = mid + 1;
+        } else {
+          f.wb = rightLen >= bal;
+          child = Frame{mid + 1, f.b, f.limit, 1, 1};
+          f.b = mid;
+        }
+        if (lane == 0) {
+          stk[sp].a = f.a;
+          stk[sp].b = f.b;
+          stk[sp].limit = f.limit;
+          stk[sp].wb = f.wb;
+          stk[sp].wp = f.wp;
+        }
+        wsyncT<G>();
+        sp++;
+        f = child;
+      }
+      if (sp == 0) break;
+      sp--;
+      f.a = __builtin_amdgcn_readfirstlane(stk[sp].a);
+      f.b = __builtin_amdgcn_readfirstlane(stk[sp].b);
+      f.limit = __builtin_amdgcn_readfirstlane(stk[sp].limit);
+      f.wb = __builtin_amdgcn_readfirstlane(stk[sp].wb);
+      f.wp = __builtin_amdgcn_readfirstlane(stk[sp].wp);
+    }
+    wsyncT<G>();
+  }
+};
+
+// The generic sort's one out-of-line body: the members arrive as scalar
+// arguments and the sorter is rebuilt locally, so they stay in registers (a
+// member function would reload them through a `this` pointer in scratch
+// after every LDS store)
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
+__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n) {
+  const WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
+  w.pdqsort_body(n);
+}
+
+// <U> Requirements.Compatible over the variant's free-key entries
+__device__ __forceinline__ bool fk_ok_range(const DevProblem& d, uint32_t fb, uint32_t fc, const FK* cfk, bool strict) {
+  for (uint32_t k = 0; k < fc; k++) {
+    const FKEntry& e = d.fk_entries[fb + k];
+    if (!fk_compatible(cfk[e.slot], e.st, strict ? false : ((d.wk_slots >> e.slot) & 1))) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+// Go's choosePivot on n >= 50 elements samples the adjacent triples around
+// n/4, n/2 and 3n/4 (medianAdjacent) and reports "increasing" iff no
+// comparison swaps.  The array was sorted before this pod's Add, which
+// changed one key: INC raised key(modpos), so the only inversion is
+// (modpos, modpos + 1) and a swap needs both inside one triple (t-1, t, t+1),
+// i.e. modpos in {t-1, t}; otherwise the triple medians stay ordered.  APPEND
+// put the only out-of-order key at n-1, past every sampled position.  Only a
+// touched sample needs the LDS reads of pivot_hint_wave.
+__device__ __forceinline__ bool pivot_touched(uint32_t modkind, uint32_t modpos, uint32_t n) {
+  if (modkind != MOD_INC) return false;
+  const uint32_t q = n / 4;
+  const uint32_t t[3] = {q, 2 * q, 3 * q};
+  bool hit = false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) hit = hit || modpos + 1 == t[k] || modpos == t[k];
+  return hit;
+}
+
+// CH: the claim scan state (slack, room, sorted order, sort scratch,
+// template) lives in HBM instead of LDS -- a Solve with more NodeClaims than
+// the LDS holds (capi gs_run reruns it so)
+template <uint32_t RR, bool TOPO, bool CH = false>
+__global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
+  extern __shared__ uint64_t lds64[];
+  __shared__ Frame s_stk[64];
+  __shared__ uint64_t s_slot[SLOT_LDS_MAX];
+  __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
+  __shared__ uint32_t s_thoff[RMAX + 1];
+  __shared__ uint32_t s_exl[64];  // exact-check batch: position | claim << 16
+  // channels between the solver (wave 0) and the memory agent (wave 1)
+  __shared__ uint32_t s_ring[RING][RING_DW];  // first-pass pod records
+  __shared__ uint32_t s_ring_seq[RING];       // queue position + 1 held by each slot
+  __shared__ uint32_t s_wq[WQ][WQ_DW];        // write requests
+  __shared__ uint32_t s_ctl[4];               // [0] first-pass pops, [1] requests posted, [2] requests completed,
+                                              // [3] solver heartbeat (pops)
+  constexpr uint32_t R = RR;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t MC = CH ? (d.claim_cap < 65535u ? d.claim_cap : 65535u) : d.max_claims_wave;
+  const uint32_t MCL = CH ? 0u : MC;  // NodeClaims in LDS
+  // dynamic LDS, per claim 23 B (the block kernel's layout, ffd.hip):
+  // slack u64 | room u64 | packed order u32 | sort scratch u16 | template u8
+  uint64_t* s_slk = CH ? d.ch_slk : lds64;
+  uint64_t* s_rm = CH ? d.ch_rm : s_slk + MC;
+  uint32_t* s_so = CH ? d.ch_so : (uint32_t*)(s_rm + MC);
+  uint16_t* s_scr = CH ? d.ch_scr : (uint16_t*)(s_so + MC);
+  uint8_t* s_tmpl = CH ? d.ch_tmpl : (uint8_t*)(s_scr + MC);
+  const uint32_t thr_base = (23u * MCL + 7u) & ~7u;
+  int64_t* s_thr = (int64_t*)((char*)lds64 + thr_base);
+  const uint32_t W = d.W, F = d.F, T = d.T, OW = d.OW, P = d.P;
+  const uint32_t nthr = d.thr_off[R];
+  const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
+  // existing nodes (wave_node_lds_bytes): slack codes (upper bound), room
+  // codes (lower bound) of available - requests per resource 0..3, and a
+  // flag byte: bit 0 = plain (ok, no taints, resources 4.. not over)
+  const uint32_t nd_off = (tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u;
+  uint64_t* s_nslk = (uint64_t*)((char*)lds64 + nd_off);
+  uint64_t* s_nrm = (uint64_t*)((char*)lds64 + nd_off + d.NN * 8u);
+  uint8_t* s_nflag = (uint8_t*)((char*)lds64 + nd_off + d.NN * 16u);
+  const int64_t* thr = s_thr;
+  const uint64_t* slot = s_slot;
+
+  for (uint32_t i = tid; i < nthr + 4; i += 128) s_thr[i] = i < nthr ? d.thr_val[i] : INT64_MAX;
+  for (uint32_t i = tid; i < d.Z * d.C * W; i += 128) s_slot[i] = d.slot_set[i];
+  if (tid <= R) s_thoff[tid] = d.thr_off[tid];
+  for (uint32_t t = tid; t < T; t += 128) {
+    s_tzm[t] = d.tmpl[t].zm;
+    s_tcm[t] = d.tmpl[t].cm;
+  }
+  if (TOPO) topo_init(d, ts, d.zknown0, tid, 128);
+  for (uint32_t n = tid; n < d.NN; n += 128) {
+    const NodeRec& nr = d.nodes0[n];
+    int64_t sl[RR];
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++) sl[r] = nr.avail[r] - nr.req[r];
+    uint64_t a = 0, b = 0;
+    bool plain = nr.ok && nr.taints == 0;
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++) {
+      if (r < 4 && r < d.RQ) {
+        a |= (uint64_t)qcode_ceil(sl[r]) << (16 * r);
+        b |= (uint64_t)qcode_floor(sl[r]) << (16 * r);
+      }
+      if (r >= 4) plain = plain && sl[r] >= 0;
+    }
+    s_nslk[n] = a;
+    s_nrm[n] = b;
+    s_nflag[n] = plain ? 1u : 0u;
+  }
+  if (tid < RING) s_ring_seq[tid] = 0;
+  if (tid < 4) s_ctl[tid] = 0;
+  __syncthreads();  // the only workgroup barrier: the waves split here
+
+  if (wave == 1) {
+    // ================================================== memory agent wave
+    // (1) stages the next first-pass pod records (queue order) into the LDS
+    //     ring ahead of the solver; (2) performs the solver's global writes
+    //     (add log, fast-accept request totals) and reports their completion.
+    //     The solver wave thus issues no global memory operation on its
+    //     common path, and never waits on one it did not need.
+    const uint32_t* qv_dw = (const uint32_t*)d.qvars;
+    const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
+    uint32_t k_fill = 0, head = 0, idle = 0, beat = 0;
+    for (;;) {
+      bool busy = false, stop = false;
+      const uint32_t tail = __builtin_amdgcn_readfirstlane(vld(&s_ctl[1]));
+      while (head != tail) {
+        const uint32_t x = lane < WQ_DW ? vld(&s_wq[head % WQ][lane]) : 0u;
+        const uint32_t type = rlane(x, 0), idx = rlane(x, 1), tgt = rlane(x, 4);
+        const uint32_t rlo = (uint32_t)__shfl((int)x, (int)(5 + 2 * (lane & 3))),
+                       rhi = (uint32_t)__shfl((int)x, (int)(6 + 2 * (lane & 3)));
+        if (type == WQ_STOP) {
+          stop = true;
+        } else {
+          if (lane == 0) d.log[idx] = LogRec{rlane(x, 2), rlane(x, 3), type == WQ_NFA ? tgt | 0x80000000u : tgt, 0};
+          const uint64_t a = (uint64_t)rlo | ((uint64_t)rhi << 32);
+          if (type == WQ_FA && lane < R && lane < 4 && a)
+            atomicAdd((unsigned long long*)&d.c_rec[tgt].tot_lo[lane], (unsigned long long)a);
+          if (type == WQ_NFA && lane < R && lane < 4 && a)
+            atomicAdd((unsigned long long*)&d.nodes[tgt].req[lane], (unsigned long long)a);
+        }
+        head++;
+        busy = true;
+      }
+      if (busy) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the writes are done
+        wsyncT<CH>();
+        if (lane == 0) vst(&s_ctl[2], head);
+      }
+      if (stop) break;
+      const uint32_t sq = __builtin_amdgcn_readfirstlane(vld(&s_ctl[0]));
+      const uint32_t lim = P < sq + RING ? P : sq + RING;
+      if (k_fill < lim) {
+        constexpr uint32_t KB = 8;
+        const uint32_t n = lim - k_fill < KB ? lim - k_fill : KB;
+        uint32_t val[KB];
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++) {
+          const size_t k = k_fill + i;
+          val[i] = 0;
+          if (i < n) {
+            if (lane < VR_DW) val[i] = qv_dw[k * VR_DW + lane];
+            else if (lane < 32 + 2 * R) val[i] = qr_dw[k * 2 * R + (lane - 32)];
+            else if (lane >= RING_CODES && lane < RING_CODES + 4) val[i] = d.qcodes[k * 4 + (lane - RING_CODES)];
+          }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++)
+          if (i < n && lane < RING_DW) s_ring[(k_fill + i) % RING][lane] = val[i];
+        wsyncT<CH>();
+#pragma unroll
+        for (uint32_t i = 0; i < KB; i++)
+          if (i < n && lane == 0) vst(&s_ring_seq[(k_fill + i) % RING], k_fill + i + 1);
+        k_fill += n;
+        busy = true;
+      }
+      // the agent leaves on WQ_STOP only; its bounded wait (a stuck solver
+      // ends the kernel, not the GPU) restarts whenever the solver pops a pod,
+      // so a long tail of pods that post nothing (failures, relaxations)
+      // cannot outlast it
+      const uint32_t hb = __builtin_amdgcn_readfirstlane(vld(&s_ctl[3]));
+      if (busy || hb != beat) {
+        idle = 0;
+        beat = hb;
+      } else {
+#ifdef GS_AGENT_SLEEP
+        __builtin_amdgcn_s_sleep(GS_AGENT_SLEEP);
+#else
+        __builtin_amdgcn_s_sleep(1);
+#endif
+        if (++idle > SPIN_MAX) break;
+      }
+    }
+    return;
+  }
+
+  // ======================================================== solver wave
+  using U32 = std::conditional_t<CH, uint32_t, lds_u32>;
+  using U16 = std::conditional_t<CH, uint16_t, lds_u16>;
+  const WaveSort<GS_WAVE_SEQ, U32, U16, CH> ws{(U32*)s_so, (U16*)s_scr, (lds_frame*)s_stk, lane, MC / 2};
+  const PackedAccT<U32> acc{(U32*)s_so};
+  uint32_t wq_tail = 0;  // write requests posted
+  uint32_t wq_seen = 0;  // completions last read from s_ctl[2] (posting waits only when that looks full)
+  // Infeasible-prefix hint: sorted positions [0, hint) hold NodeClaims that
+  // cannot take a pod with requests >= hint_rq (resources 0..3) that
+  // tolerates no template outside hint_tolt.  NodeClaims only fill up
+  // (requests grow, options shrink), so the prefix stays infeasible; every
+  // reorder of the sorted order moves the bound exactly (or drops it).
+  // Pods come sorted by cpu, then memory, descending: runs of equal
+  // requests skip the prefix their predecessors already ruled out.
+  uint32_t hint = 0;
+  bool hint_ok = false;
+  uint64_t hint_tolt = 0;
+  int64_t hint_rq = 0;  // lane r < 4: that pod's request r
+  // Existing nodes: positions [0, nhint) cannot take a pod whose requests are
+  // all >= hint_nrq and that tolerates no taint outside nhint_tol (nodes
+  // only fill up; a pod with requirements, topology or volumes is only more
+  // constrained).  Set by plain pods (no requirements, topology, volumes).
+  uint32_t nhint = 0;
+  bool nhint_ok = false;
+  uint64_t nhint_tol = 0;
+  int64_t hint_nrq = 0;  // lane r < R: that pod's request r
+  bool chan_err = false;  // a channel wait exceeded SPIN_MAX
+  // post one write request (uniform control flow: every lane takes part):
+  // lanes 0..4 the header, lanes 32.. (the record's request dwords) dwords 5..
+  auto post = [&](uint32_t type, uint32_t idx, uint32_t pod, uint32_t var, uint32_t tgt, uint32_t rqd_) {
+    if (wq_tail - wq_seen >= WQ) {
+      for (uint32_t spin = 0;; spin++) {
+        wq_seen = __builtin_amdgcn_readfirstlane(vld(&s_ctl[2]));
+        if (wq_tail - wq_seen < WQ) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > SPIN_MAX) {
+          chan_err = true;
+          break;
+        }
+      }
+    }
+    const uint32_t x = lane == 0 ? type : lane == 1 ? idx : lane == 2 ? pod : lane == 3 ? var : lane == 4 ? tgt : rqd_;
+    const bool rqw = (type == WQ_FA || type == WQ_NFA) && lane >= 32 && lane < 40;
+    if (lane < 5 || rqw) s_wq[wq_tail % WQ][lane < 5 ? lane : lane - 27] = x;
+    wsyncT<CH>();
+    if (lane == 0) vst(&s_ctl[1], wq_tail + 1);
+    wq_tail++;
+  };
+  // wait until every posted write has completed (before reading claim state)
+  auto drain = [&]() {
+    for (uint32_t spin = 0; __builtin_amdgcn_readfirstlane(vld(&s_ctl[2])) != wq_tail; spin++) {
+      __builtin_amdgcn_s_sleep(1);
+      if (spin > SPIN_MAX) {
+        chan_err = true;
+        break;
+      }
+    }
+  };
+
+  // uniform loop state (scalar registers)
+  uint32_t qhead = 0, qlen = P, epoch = 1, M = 0, modkind = MOD_NONE, modpos = 0, nlog = 0, status = 0;
+  bool wrapped = false;
+  uint64_t pops = 0;
+  // instrumentation counters, lane k = counter k (no scalar registers)
+  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG };
+  uint64_t ctr = 0;
+#ifdef GS_NO_CTR  // experiment builds: the counters' cost
+#define CTR(k, x) ((void)0)
+#else
+#define CTR(k, x) (ctr += lane == (k) ? (uint64_t)(x) : 0ull)
+#endif
+  const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
+
+#ifdef GS_FFD_TL
+  uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
+  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0;
+#endif
+  for (;;) {
+    // ---------------------------------------------------------- Queue.Pop
+    TLW(7);  // previous pod's tail (continue paths)
+    if (status) break;
+    if (pops > max_pops) {
+      status = 2;
+      break;
+    }
+    if (qlen == 0) break;
+    uint32_t vrd, rqd, p, v;
+    uint64_t rqq_p = 0, rqc_p = 0;  // request codes (floor / ceil) of resources 0..3, 16 bits each
+    const bool from_ring = !wrapped;
+    if (from_ring) {
+      // first pass: the pod at qhead is queue0[qhead] with its first
+      // variant and was never pushed (no staleness stop); the agent staged
+      // its record in ring slot qhead % RING.  The sequence word and the
+      // record are read in one round trip: the LDS serves a wave's reads in
+      // order and the agent wrote the record before the sequence word.
+      const uint32_t rs = qhead % RING;
+      uint32_t x = 0;
+      for (uint32_t spin = 0;; spin++) {
+        const uint32_t sq = vld(&s_ring_seq[rs]);
+        x = lane < RING_DW ? vld(&s_ring[rs][lane]) : 0u;
+        if (__builtin_amdgcn_readfirstlane(sq) == qhead + 1) break;
+        __builtin_amdgcn_s_sleep(0);
+        if (spin > SPIN_MAX) {
+          chan_err = true;
+          break;
+        }
+      }
+      if (chan_err) {
+        status = 2;
+        break;
+      }
+      wsyncT<CH>();
+      if (lane == 0) vst(&s_ctl[0], qhead + 1);  // the slot may be refilled
+      vrd = x;
+      rqd = x;
+      p = rlane(vrd, 0);
+      v = rlane(vrd, VR_DW - 1);
+      rqq_p = (uint64_t)rlane(x, RING_CODES) | ((uint64_t)rlane(x, RING_CODES + 1) << 32);
+      rqc_p = (uint64_t)rlane(x, RING_CODES + 2) | ((uint64_t)rlane(x, RING_CODES + 3) << 32);
+    } else {
+      p = __builtin_amdgcn_readfirstlane(d.queue[qhead]);
+      const uint32_t le = __builtin_amdgcn_readfirstlane(d.last_epoch[p]);
+      const uint32_t ll = __builtin_amdgcn_readfirstlane(d.last_len[p]);
+      v = __builtin_amdgcn_readfirstlane(d.cur_var[p]);
+      if (le == epoch && ll == qlen) break;
+      vrd = lane < VR_DW ? ((const uint32_t*)(d.vars + v))[lane] : 0u;
+      rqd = lane >= 32 && lane < 32 + 2 * R ? ((const uint32_t*)(d.pod_req + (size_t)p * R))[lane - 32] : 0u;
+    }
+    if (qhead + 1 == P) wrapped = true;
+    qhead = qhead + 1 == P ? 0 : qhead + 1;
+    qlen--;
+    pops++;
+    if (lane == 0) vst(&s_ctl[3], (uint32_t)pops);  // heartbeat for the agent's bounded wait
+    const uint32_t gp = p;
+    auto VD = [&](uint32_t i) -> uint32_t { return rlane(vrd, i); };
+    auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
+    const uint32_t vctb = VD(3);
+    const uint64_t vtolt = VD64(20);
+    // topology: own list (groups the variant owns), selection list (groups counting the pod)
+    const uint32_t own_off = TOPO ? VD(22) : 0u, own_n = TOPO ? VD(23) : 0u;
+    const uint32_t sel_off = TOPO ? VD(24) : 0u, sel_n = TOPO ? VD(25) : 0u;
+    int64_t rq[RR];
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++)
+      rq[r] = (int64_t)((uint64_t)rlane(rqd, 32 + 2 * r) | ((uint64_t)rlane(rqd, 33 + 2 * r) << 32));
+    int64_t rq_lane = 0;  // lane r < R: resource r's request
+#pragma unroll
+    for (uint32_t r = 0; r < RR; r++)
+      if (lane == r) rq_lane = rq[r];
+    if (!from_ring) {
+      // a wrapped pop read its record itself: the request codes too
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++)
+        if (r < d.RQ && r < RR) {
+          rqq_p |= (uint64_t)qcode_floor(rq[r]) << (16 * r);
+          rqc_p |= (uint64_t)qcode_ceil(rq[r]) << (16 * r);
+        }
+    }
+
+    TLW(0);  // pop + record
+    // <U> Topology.AddRequirements: each owned zone group's minimum domain
+    // count over the pod's strict zone domains (domainMinCount)
+    if (TOPO && own_n) {
+      const auto& KD = *karg();
+      const uint64_t vzs = rlane(vrd, 26) | ((uint64_t)rlane(vrd, 27) << 32);
+      topo_tmin(KD, ts, own_off, own_n, vzs, lane);
+      wsyncT<CH>();
+    }
+
+    // ----------------- existing nodes in order: first ExistingNode.CanAdd wins
+    if (d.NN) {
+      const auto& KD = *karg();
+      const uint32_t vx = fresh(vrd);
+      auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+      auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+      const uint32_t fk_begin = VX(1), fk_count = VX(2), zfull_off = VX(12), cfull_off = VX(13);
+      const uint64_t vtol = VX64(18);
+      // <U> VolumeUsage: the pod's pending-volume bits per CSI driver
+      uint64_t pvol[VDMAX] = {0, 0, 0, 0};
+      uint32_t pfresh[VDMAX] = {0, 0, 0, 0};
+      if (TOPO && KD.any_vol)
+#pragma unroll
+        for (uint32_t q = 0; q < VDMAX; q++) {
+          pvol[q] = KD.pod_vol[(size_t)gp * VDMAX + q];
+          pfresh[q] = KD.pod_vfresh[(size_t)gp * VDMAX + q];
+        }
+      // LDS prefilter (per resource 0..3: request code <= slack code) and,
+      // for a plain pod (no requirements, topology or volumes) on a plain
+      // node, the sufficient test (request code <= room code: CanAdd holds
+      // without reading the node); the exact ExistingNode.CanAdd runs on the
+      // prefilter's survivors before the chunk's first fast accept
+      bool pvany = false;
+#pragma unroll
+      for (uint32_t q = 0; q < VDMAX; q++) pvany = pvany || pvol[q] || pfresh[q];
+      bool nplain = (vctb & VF_SIMPLE) && !pvany;
+#pragma unroll
+      for (uint32_t r = 4; r < RR; r++) nplain = nplain && rq[r] == 0;
+      const uint64_t nrqq = rqq_p, nrqc = rqc_p;
+      uint32_t nlo = 0;
+      if (nhint_ok && (vtol & ~nhint_tol) == 0) {
+        const bool ge = lane >= R || rq_lane >= hint_nrq;
+        if (__ballot(!ge) == 0) nlo = nhint;
+      }
+      uint32_t fn = INF;
+      bool nfa_win = false;
+      for (uint32_t base = nlo & ~63u; base < KD.NN; base += 64) {
+        const uint32_t n = base + lane;
+        const bool in = (n < KD.NN) & (n >= nlo);
+        const uint32_t nc = in ? n : 0u;
+        const uint64_t nsl = s_nslk[nc], nrm = s_nrm[nc];
+        const uint32_t nfl = s_nflag[nc];
+        const bool lp = in & swar_ge(nsl, nrqq);
+        const bool fa = lp & nplain & (bool)(nfl & 1u) & swar_ge(nrm, nrqc);
+        const uint64_t lpb = __ballot(lp);
+        CTR(C_NEV, KD.NN - base < 64 ? KD.NN - base : 64);
+        if (!lpb) continue;
+        const uint64_t fab = __ballot(fa);
+        const uint32_t mfl = fab ? ffs64(fab) : 64u;
+        const bool need = lp & !fa & (lane < mfl);
+        bool feas = fa;
+        if (__ballot(need)) {
+          drain();  // node requests the agent still adds (fast accepts)
+          if (need) {
+            const NodeRec& nr = KD.nodes[n];
+            const FK* nfk = KD.n_fk + (size_t)n * F;
+            feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
+#pragma unroll
+            for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
+#pragma unroll
+            for (uint32_t k = 0; k < KMAX_IT; k++) {
+              const uint32_t off = VX(4 + k);
+              if (k >= KD.K || !feas || off == NONE) continue;
+              const uint32_t vid = nr.vid[k];
+              feas = vid != NONE && ((KD.itmask[off + (vid >> 6)] >> (vid & 63)) & 1);
+            }
+            if (feas && zfull_off != NONE)
+              feas = nr.zvid != NONE && ((KD.itmask[zfull_off + (nr.zvid >> 6)] >> (nr.zvid & 63)) & 1);
+            if (feas && cfull_off != NONE)
+              feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
+            if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
+            if (TOPO && feas && own_n)
+              feas = topo_node_ok(KD, ts, own_off, own_n, nr.zvid,
+                                  [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; });
+            if (TOPO && feas && KD.any_vol) {
+              // ExceedsLimits: distinct volumes per driver after the union
+              const NodeVol& nv = KD.n_vol[n];
+#pragma unroll
+              for (uint32_t q = 0; q < VDMAX; q++)
+                if (pvol[q] | pfresh[q]) feas = feas && nv.cnt[q] + (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present) <= nv.lim[q];
+            }
+          }
+        }
+        const uint64_t b = __ballot(feas);
+        if (b) {
+          fn = base + ffs64(b);
+          nfa_win = ((fab >> ffs64(b)) & 1) != 0;
+          break;
+        }
+      }
+      CTR(C_NPRE, fn != INF ? fn + 1 : KD.NN);
+      if (nplain) {
+        // [nlo, fn) (or all) cannot take these requests; nodes only fill up
+        nhint = fn != INF ? fn : KD.NN;
+        nhint_ok = true;
+        nhint_tol = vtol;
+        hint_nrq = rq_lane;
+      }
+      if (fn != INF && nfa_win) {
+        // ExistingNode.Add of a plain pod: requests only.  The LDS codes
+        // shrink by the request (still an upper / lower bound); the agent adds
+        // the requests to the node (an exact check drains the channel first)
+        const uint64_t sl = s_nslk[fn], rm = s_nrm[fn];
+        uint32_t c_sl = 0, c_rm = 0;
+        if (lane < KD.RQ) {
+          const uint32_t sh = 16 * lane;
+          c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - rq_lane);
+          c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - rq_lane);
+        }
+        uint64_t sl2 = 0, rm2 = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++)
+          if (r < KD.RQ) {
+            sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+          }
+        if (lane == 0) {
+          s_nslk[fn] = sl2;
+          s_nrm[fn] = rm2;
+          // <U> Topology.Record in the groups that select the pod
+          if (TOPO && sel_n) {
+            const uint32_t z = KD.nodes0[fn].zvid;
+            topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
+                        [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
+          }
+        }
+        wsyncT<CH>();
+        post(WQ_NFA, nlog, gp, v, fn, rqd);
+        nlog++;
+        continue;
+      }
+      if (fn != INF) {
+        // ExistingNode.Add: requests and requirements
+        int64_t* areq = KD.nodes[fn].req;
+        FK* afk = KD.n_fk + (size_t)fn * F;
+        int64_t nreq = 0, navl = 0;
+        if (lane < R) {
+          nreq = areq[lane] + rq_lane;
+          navl = KD.nodes[fn].avail[lane];
+          areq[lane] = nreq;
+        }
+        if (lane < fk_count) {
+          const FKEntry& e = KD.fk_entries[fk_begin + lane];
+          FK* nf = afk + e.slot;
+          const FK cur = *nf;
+          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+                                         : e.st;
+        }
+        {
+          // the node's LDS codes from its exact remainder
+          const int64_t sl = navl - nreq;
+          const uint32_t c_sl = lane < KD.RQ ? qcode_ceil(sl) : 0u, c_rm = lane < KD.RQ ? qcode_floor(sl) : 0u;
+          const bool over = lane >= 4 && lane < R && sl < 0;
+          uint64_t sl2 = 0, rm2 = 0;
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) {
+            sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+          }
+          const bool anyover = __ballot(over) != 0;
+          if (lane == 0) {
+            s_nslk[fn] = sl2;
+            s_nrm[fn] = rm2;
+            if (anyover) s_nflag[fn] = 0;
+          }
+        }
+        if (lane == 0) {
+          if (TOPO && KD.any_vol) {
+            // VolumeUsage.Add
+            NodeVol& nv = KD.n_vol[fn];
+            uint64_t all = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < VDMAX; q++) {
+              nv.cnt[q] += (int32_t)pfresh[q] + __popcll(pvol[q] & ~nv.present);
+              all |= pvol[q];
+            }
+            nv.present |= all;
+          }
+          // <U> Topology.Record: the node's labels are single domains
+          if (TOPO && sel_n) {
+            const uint32_t z = KD.nodes0[fn].zvid;
+            topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
+                        [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
+          }
+        }
+        wsyncT<CH>();
+        post(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0);
+        nlog++;
+        continue;
+      }
+    }
+
+    TLW(1);  // topology minimum + existing nodes
+    // ------------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
+    if (M > 1) {
+      // at most one NodeClaim changed since the last sort: one pod added at
+      // modpos (INC) or one NodeClaim appended (APPEND)
+      bool inversion = false;
+      if (modkind == MOD_INC) inversion = modpos + 1 < M && acc.key(modpos + 1) < acc.key(modpos);
+      else if (modkind == MOD_APPEND) inversion = acc.key(M - 2) > acc.key(M - 1);
+      inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
+      if (inversion) {
+        if (M <= 12) {
+          if (lane == 0) SeqSortT<PackedAccT<U32>>{{(U32*)s_so}}.insertion_sort(0, (int)M);
+          wsyncT<CH>();
+          hint_ok = false;
+        } else if (M >= 50 && (!pivot_touched(modkind, modpos, M) || pivot_hint_wave(acc, (int)M, lane) == 1)) {
+          // partialInsertionSort fixes the single inversion: one rotation
+          CTR(C_FAST, 1);
+          if (modkind == MOD_INC) {
+            const uint32_t x = acc.key(modpos);
+            const uint32_t e = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
+            ws.rotate((int)modpos, (int)e - 1, true);
+#ifdef GS_FFD_TL
+            n_rot++;
+            n_rotlen += e - 1 - modpos;
+#endif
+            // (modpos, e-1] shift left, the changed claim lands at e-1
+            if (modpos < hint && e - 1 >= hint) hint--;
+          } else {
+            const uint32_t x = acc.key(M - 1);
+            const uint32_t lo = wave_first(0, M - 1, lane, [&](uint32_t k) { return acc.key(k) > x; });
+            ws.rotate((int)lo, (int)M - 1, false);
+#ifdef GS_FFD_TL
+            n_rot++;
+            n_rotlen += M - 1 - lo;
+#endif
+            if (lo < hint) hint = lo;  // the new claim lands at lo
+          }
+        } else {
+          CTR(C_GEN, 1);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
+          hint_ok = false;
+        }
+      }
+      modkind = MOD_NONE;
+    }
+
+    TLW(2);  // sort
+    // rqq_p / rqc_p: the request codes for the LDS slack / room tests, packed
+    // 16 bits per resource (codes < 2^15, so a SWAR subtract compares all four
+    // at once)
+#ifdef GS_NO_FAST
+    bool simple = false;
+#else
+    // a pod with no requirements and no owned topology group (VF_SIMPLE):
+    // its CanAdd is resources and taints only, in either variant
+    bool simple = (vctb & VF_SIMPLE) != 0;
+#endif
+#pragma unroll
+    for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
+#ifdef GS_FFD_TL
+    n_nonsimple += simple ? 0u : 1u;
+#endif
+
+    // --------------------------- in-flight NodeClaims, first that CanAdd wins
+    // Phase A walks the sorted positions in LDS, one 64-position chunk per
+    // step (2 or 4 chunks per step measured slower:
+    // profiles/r2/ffd_scan_width_ab.txt), with the necessary test (template
+    // tolerated, request code <= slack code per resource) and, for simple
+    // pods, the sufficient test
+    // (request code <= room code: CanAdd holds without reading the claim).
+    // It stops at the first fast accept, collecting every candidate before it
+    // that needs the exact check (at most 64 per batch).  Phase B runs the
+    // exact NodeClaim.CanAdd on the batch, one lane per candidate: the first
+    // feasible candidate wins, else the fast accept, else the scan resumes.
+    uint32_t f = INF;
+    bool ovf = false;  // the winner lane's u16 pod count overflowed
+    uint32_t lo_bound = 0;
+    if (hint_ok && (vtolt & ~hint_tolt) == 0) {
+      const bool ge = lane >= 4 || lane >= R || rq_lane >= hint_rq;
+      if (__ballot(!ge) == 0) lo_bound = hint;
+    }
+    uint32_t scan_from = lo_bound & ~63u;
+    for (;;) {
+      uint32_t nex = 0, fa_pos = INF, fa_j = 0, resume = INF;
+      // one 64-position chunk: true = stop the walk
+      auto chunk = [&](uint32_t cb, uint32_t je, uint64_t sq, uint64_t rmv, uint32_t tt) -> bool {
+        const uint32_t pos = cb + lane;
+        // bitwise (not short-circuit) predicates: no branches
+        const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
+        const bool fa = lp & simple & swar_ge(rmv, rqc_p);
+        const uint64_t fab = __ballot(fa), exb = __ballot(lp & !fa);
+        const uint32_t mfl = fab ? ffs64(fab) : 64u;
+        const uint64_t ex = exb & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));
+        const uint32_t cnt = (uint32_t)__popcll(ex);
+        if (nex + cnt > 64) {
+          resume = cb;  // batch full: check it, then rescan from this chunk
+          return true;
+        }
+        CTR(C_CAND, M - cb < 64 ? M - cb : 64);
+        if (ex) {
+          if ((ex >> lane) & 1) s_exl[nex + (uint32_t)__popcll(ex & ((1ull << lane) - 1ull))] = (pos & 0xFFFFu) | (je << 16);
+          nex += cnt;
+        }
+        if (fab) {
+          fa_pos = cb + mfl;
+          fa_j = rlane(je, mfl);
+          return true;
+        }
+        return false;
+      };
+      for (uint32_t cb = scan_from; cb < M; cb += 64) {
+        const uint32_t pos = cb + lane;
+        const uint32_t je = s_so[pos < M ? pos : M - 1] >> 16;
+        if (chunk(cb, je, s_slk[je], s_rm[je], T > 1 ? (uint32_t)s_tmpl[je] : 0u)) break;
+      }
+      wsyncT<CH>();
+      TLW(5);  // phase A: LDS prefilter
+      if (nex) {
+        drain();  // the agent's request totals must be in the claim records
+        const auto& KD = *karg();
+        const uint32_t vx = fresh(vrd);
+        auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+        auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+        const uint32_t fk_begin = VX(1), fk_count = VX(2), vzflags = VX(30);
+        const uint64_t vzm = VX64(14), vcm = VX64(16), vzn = VX64(28);
+        // --- exact NodeClaim.CanAdd, lane i = i-th candidate (ascending
+        // positions): one 64-B header read, option words and the (variant,
+        // template) row, threshold cursors, offering grid
+        CTR(C_FULL, nex);
+#ifdef GS_FFD_TL
+        n_xns += simple ? 0u : nex;
+        n_xb++;
+#endif
+        const uint32_t xe = lane < nex ? s_exl[lane] : 0u;
+        const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
+        const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
+      bool feas = false;
+      uint64_t zset = ~0ull;  // zone domains topology allows on this NodeClaim (~0: unconstrained)
+      uint64_t zm = 0, cm = 0, czf = 0;
+      uint32_t czfl = 0;
+      uint32_t mrow[RR];
+      int64_t tot[RR];
+      uint64_t nx[WREG] = {0, 0, 0, 0};
+      uint64_t G = 0, Gt = 0;
+      if (lane < nex) {
+        const ClaimRec* cr = KD.c_rec + j;
+        uint32_t cur[RR];
+        {
+          const uint4* q = (const uint4*)cr;
+          const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+          const int64_t lo[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                 (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+          const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+          zm = ((uint64_t)h2.w << 32) | h2.z;
+          cm = ((uint64_t)h3.y << 32) | h3.x;
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            tot[r] = r < 4 ? lo[r] : cr->tot_hi[r - 4];
+            cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+          }
+        }
+        const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
+        const uint64_t* opts = KD.c_opts + (size_t)j * OW;
+        if (W <= WREG) {
+          const uint4* oq = (const uint4*)opts;
+          const uint4* rq4 = (const uint4*)row;
+          const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+          const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                 (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                 (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                 (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+          for (uint32_t w = 0; w < WREG; w++) nx[w] = w < W ? a[w] : 0;
+        }
+        bool pre = true;
+        if (fk_count) pre = fk_ok_range(d, fk_begin, fk_count, KD.c_fk + (size_t)j * F, false);
+        if (TOPO && pre && own_n) {
+          // <U> Topology.AddRequirements on the NodeClaim over its (claim AND
+          // pod) zone domains; hostname groups: this NodeClaim's counts
+          czf = cr->zfull;
+          czfl = cr->zflags;
+          const int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+          zset = topo_claim(KD, ts, own_off, own_n, czf & vzn, [&](uint32_t hs) -> int64_t { return hrow[hs]; });
+          pre = zset != 0;
+          if (pre && zset != ~0ull) zm &= topo_catmask(KD, zset);
+        }
+        if (pre) {
+          G = grid_of(zm & vzm, cm & vcm, KD.Z, KD.C);
+          Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, KD.Z, KD.C);
+          uint32_t mm[RR];
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+            mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
+          }
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+            if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
+            mrow[r] = o + r + mm[r];
+          }
+          uint64_t accw = 0;
+          if (W <= WREG) {
+            // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
+            // whose cursor moves narrows the options further
+#pragma unroll
+            for (uint32_t r = 0; r < RR; r++) {
+              if (mm[r] != cur[r]) {
+                const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW);
+                const uint4 t0 = tq[0], t1 = tq[1];
+                nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
+              }
+            }
+            if (G != Gt) {
+              uint64_t off[WREG] = {};
+              for (uint64_t gm = G; gm; gm &= gm - 1) {
+                const uint32_t g = ffs64(gm);
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++)
+                  if (w < W) off[w] |= slot[g * W + w];
+              }
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++) nx[w] &= off[w];
+            }
+#pragma unroll
+            for (uint32_t w = 0; w < WREG; w++) accw |= nx[w];
+          } else {
+            // 4 words per round trip, stop at the first batch with a survivor
+            for (uint32_t w0 = 0; w0 < W && !accw; w0 += 4) {
+              const uint4* oq = (const uint4*)(opts + w0);
+              const uint4* rq4 = (const uint4*)(row + w0);
+              const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+              uint64_t x[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                               (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                               (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                               (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                if (mm[r] == cur[r]) continue;
+                const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW + w0);
+                const uint4 t0 = tq[0], t1 = tq[1];
+                x[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                x[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                x[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                x[3] &= ((uint64_t)t1.w << 32) | t1.z;
+              }
+#pragma unroll
+              for (uint32_t w = 0; w < 4; w++) {
+                if (w0 + w >= W) x[w] = 0;
+                if (x[w] && G != Gt) {
+                  uint64_t off = 0;
+                  for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w0 + w];
+                  x[w] &= off;
+                }
+                accw |= x[w];
+              }
+            }
+          }
+          feas = accw != 0;
+          if (TOPO && feas && KD.tmpl[t].mv_mask) {
+            // minValues over the NodeClaim's options after Add (per lane)
+            feas = mv_ok(KD, KD.tmpl[t], [&](uint32_t w) -> uint64_t {
+              if (W <= WREG) return w == 0 ? nx[0] : w == 1 ? nx[1] : w == 2 ? nx[2] : nx[3];
+              uint64_t x = opts[w] & row[w];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
+              if (G != Gt) {
+                uint64_t off = 0;
+                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                x &= off;
+              }
+              return x;
+            });
+          }
+        }
+      }
+        const uint64_t fm = __ballot(feas);
+        TLW(6);  // phase B: exact checks
+        if (fm) {
+          const uint32_t wl = ffs64(fm);
+          f = rlane(xpos, wl);
+#ifdef GS_FFD_TL
+          n_xwin++;
+#endif
+        if (lane == wl) {
+          // NodeClaim.Add by the winning lane: options, requests, requirements
+          ClaimRec* cr = KD.c_rec + j;
+          uint64_t* opts = KD.c_opts + (size_t)j * OW;
+          if (W <= WREG) {
+  #pragma unroll
+            for (uint32_t w = 0; w < WREG; w++)
+              if (w < W) opts[w] = nx[w];  // already narrowed to the grid
+          } else {
+            const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
+            for (uint32_t w = 0; w < W; w++) {
+              uint64_t x = opts[w] & row[w];
+  #pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
+              if (G != Gt) {
+                uint64_t off = 0;
+                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                x &= off;
+              }
+              opts[w] = x;
+            }
+          }
+          int64_t nt[RR], ma[RR];
+          uint32_t cu[RR];
+  #pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            nt[r] = tot[r] + rq[r];
+            ma[r] = cr->maxa[r];
+            cu[r] = mrow[r] - s_thoff[r] - r;
+            cr->tot(r) = nt[r];
+            cr->thr(r) = (uint16_t)cu[r];
+          }
+          s_slk[j] = pack_slack(d, ma, nt);  // exact re-quantization: no drift
+          s_rm[j] = pack_room(thr, s_thoff, cu, nt, KD.RQ);
+          cr->zm = zm & vzm;  // zm carries the topology narrowing
+          cr->cm &= vcm;
+          cr->ctb &= vctb;
+          if (TOPO) {
+            // zone requirement after Add (+ the topology domain), then
+            // <U> Topology.Record for every group selecting the pod
+            if (!own_n) {
+              czf = cr->zfull;
+              czfl = cr->zflags;
+            }
+            const uint64_t zf = czf & vzn & zset;
+            const uint32_t zl = zset != ~0ull ? 0u : (czfl & vzflags);
+            cr->zfull = zf;
+            cr->zflags = zl;
+            int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+            topo_record(KD, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs]++; });
+          }
+          FK* cf = KD.c_fk + (size_t)j * F;
+          for (uint32_t k = 0; k < fk_count; k++) {
+            const FKEntry& e = KD.fk_entries[fk_begin + k];
+            const FK cur = cf[e.slot];
+            cf[e.slot] = (cur.flags & FK_PRESENT)
+                             ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+                             : e.st;
+          }
+          const uint32_t e = s_so[f];
+          if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+          s_so[f] = e + 1u;
+        }
+          wsyncT<CH>();
+          post(WQ_LOG, nlog, gp, v, rlane(j, wl), 0);
+          break;
+        }
+      }
+      if (fa_pos != INF) {
+        // --- fast accept (simple pod): NodeClaim.Add changes the requests
+        // only; options, cursors and requirements stay.  LDS room and slack
+        // shrink by the request (still a lower / upper bound); the agent wave
+        // adds the requests to the claim's totals (an exact check drains the
+        // channel before it reads them).
+        f = fa_pos;
+        const uint32_t j = fa_j;
+        {
+          // lane r < RQ re-quantizes resource r: room (lower bound) and
+          // slack (upper bound) shrink by the request
+          const uint64_t rm = s_rm[j], sl = s_slk[j];
+          uint32_t c_rm = 0, c_sl = 0;
+          if (lane < d.RQ) {
+            const uint32_t sh = 16 * lane;
+            c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - rq_lane);
+            c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - rq_lane);
+          }
+          uint64_t rm2 = 0, sl2 = 0;
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) {
+            if (r < d.RQ) {
+              rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
+              sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
+            }
+          }
+          if (lane == 0) {
+            s_rm[j] = rm2;
+            s_slk[j] = sl2;
+            const uint32_t e = s_so[f];
+            if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+            s_so[f] = e + 1u;
+            if (TOPO && sel_n) {
+              // <U> Topology.Record in the groups that select the pod: the
+              // NodeClaim's requirements are unchanged by this Add
+              const auto& KD = *karg();
+              const ClaimRec* cr = KD.c_rec + j;
+              int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+              topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
+            }
+          }
+        }
+        wsyncT<CH>();
+        post(WQ_FA, nlog, gp, v, j, rqd);  // the agent adds the requests and logs
+        CTR(C_FA, 1);
+        break;
+      }
+      if (resume == INF) break;
+      scan_from = resume;
+    }
+    if (__ballot(ovf)) status = 3;
+    CTR(C_ALG, f != INF ? f + 1 : M);  // the reference's NodeClaim.CanAdd calls
+    TLW(3);  // scan + Add
+#ifdef GS_FFD_TL
+    n_fsum += f != INF ? f : 0;
+#endif
+    if (simple) {
+      // [0, f) (or all positions) are infeasible for these requests
+      hint = f != INF ? f : M;
+      hint_ok = true;
+      hint_tolt = vtolt;
+      hint_rq = rq_lane;
+    }
+    if (f != INF) {
+      wsyncT<CH>();
+      modkind = MOD_INC;
+      modpos = f;
+      nlog++;
+      continue;
+    }
+
+    // ------------------------------- new NodeClaim from templates, in order
+    bool opened = false;
+    {
+      const auto& KD = *karg();
+      const uint32_t vx = fresh(vrd);
+      auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
+      auto VX64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VX(i) | ((uint64_t)VX(i + 1) << 32); };
+      const uint32_t fk_begin = VX(1), fk_count = VX(2), vzflags = VX(30);
+      const uint64_t vzm = VX64(14), vcm = VX64(16), vzn = VX64(28);
+    for (uint32_t t = 0; t < T; t++) {
+      const TmplRec& tr = KD.tmpl[t];
+      const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
+      // <U> Topology on the fresh NodeClaim (template AND pod zone domains;
+      // a new hostname domain has count 0, always within maxSkew >= 1):
+      // the picked zone narrows the K1 row to that zone's offerings
+      // (pod affinity on the fresh hostname domain, count 0: only the
+      // bootstrap of a self-selecting pod while no selected pod runs)
+      uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
+      if (TOPO && own_n) {
+        tzs = topo_claim(KD, ts, own_off, own_n, tr.zfull & vzn, [](uint32_t) -> int64_t { return 0; });
+        if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(KD, tzs);
+        tzs = (uint64_t)uniform_i64((int64_t)tzs);
+        tzcat = (uint64_t)uniform_i64((int64_t)tzcat);
+        if (tzs == 0 || tzcat == 0) continue;
+      }
+      const uint64_t tcm = tr.cm & vcm;
+      auto rowx = [&](uint32_t w) -> uint64_t {
+        uint64_t x = row[w];
+        if (tzs != ~0ull) {
+          uint64_t off = 0;
+          for (uint64_t zm_ = tzcat; zm_; zm_ &= zm_ - 1) {
+            const uint32_t zc = ffs64(zm_);
+            for (uint32_t c = 0; c < KD.C; c++)
+              if ((tcm >> c) & 1) off |= slot[(zc * KD.C + c) * W + w];
+          }
+          x &= off;
+        }
+        return x;
+      };
+      bool anyl = false;
+      if (KD.fk_ok[(size_t)v * T + t])
+        for (uint32_t w = lane; w < W; w += 64) anyl = anyl || rowx(w) != 0;
+      if (!__ballot(anyl)) continue;
+      if (tr.has_limits) {
+        // <U> filterByRemainingResources on the template's options
+        bool hit = false;
+        for (uint32_t i = lane; i < KD.N; i += 64) {
+          if (!((rowx(i >> 6) >> (i & 63)) & 1)) continue;
+          bool ok = true;
+          for (uint32_t r = 0; r < R; r++)
+            if ((tr.limit_rmask >> r) & 1) ok = ok && KD.it_cap[(size_t)r * KD.N + i] <= KD.t_rem[(size_t)t * R + r];
+          hit = hit || ok;
+        }
+        if (!__ballot(hit)) continue;
+      }
+      // threshold cursors of the fresh claim: lane r < R
+      int64_t tot_l = 0;
+      uint32_t c0_l = 0;
+      if (lane < R) {
+        tot_l = tr.daemon[lane] + rq_lane;
+        const uint32_t o = s_thoff[lane], n = s_thoff[lane + 1] - o;
+        c0_l = thr_search(thr + o, n, 0, tot_l);
+      }
+      uint32_t c0[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) c0[r] = (uint32_t)__shfl((int)c0_l, (int)r);
+      // option words (lane w holds word w, and w + 64)
+      uint64_t xw[2] = {0, 0};
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t w = lane + 64 * h;
+        if (w >= W) continue;
+        uint64_t x = rowx(w);
+        // establish opts ⊆ thr_set[cursor] for the candidate scan
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)(s_thoff[r] + r + c0[r]) * OW + w];
+        if (tr.has_limits) {
+          uint64_t y = 0;
+          for (uint64_t m = x; m; m &= m - 1) {
+            const uint32_t b = ffs64(m);
+            const uint32_t i = w * 64 + b;
+            bool ok = true;
+            for (uint32_t r = 0; r < R; r++)
+              if ((tr.limit_rmask >> r) & 1) ok = ok && KD.it_cap[(size_t)r * KD.N + i] <= KD.t_rem[(size_t)t * R + r];
+            if (ok) y |= 1ull << b;
+          }
+          x = y;
+        }
+        xw[h] = x;
+      }
+      // minValues over the fresh NodeClaim's options (uniform: every lane
+      // evaluates the same words)
+      if (TOPO && tr.mv_mask && !mv_ok(KD, tr, [&](uint32_t w) { return shfl_u64(xw[w >> 6], w & 63); })) continue;
+      if (M >= MC) {
+        status = 1;
+        break;
+      }
+      const uint32_t j = M;
+      ClaimRec* cr = KD.c_rec + j;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++)
+        if (lane + 64 * h < W) KD.c_opts[(size_t)j * OW + lane + 64 * h] = xw[h];
+      if (lane < RR) {
+        cr->tot(lane) = tot_l;
+        cr->thr(lane) = (uint16_t)c0_l;
+      }
+      // max allocatable over the new claim's options (the slack bound), and
+      // (limits) the max capacity for subtractMax: lane = instance type
+      uint64_t mxa[RR], mxc[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) mxa[r] = mxc[r] = 0;
+      for (uint32_t w = 0; w < W; w++) {
+        const uint64_t word = shfl_u64(xw[w >> 6], w & 63);
+        if (!((word >> lane) & 1)) continue;
+        const uint32_t i = w * 64 + lane;
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) {
+          const uint64_t a = (uint64_t)KD.it_alloc[(size_t)r * KD.N + i];
+          mxa[r] = a > mxa[r] ? a : mxa[r];
+          if (tr.has_limits && ((tr.limit_rmask >> r) & 1)) {
+            const uint64_t c = (uint64_t)(KD.it_cap[(size_t)r * KD.N + i] + (1ll << 62));
+            mxc[r] = c > mxc[r] ? c : mxc[r];
+          }
+        }
+      }
+      int64_t ma[RR], nt[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) {
+        ma[r] = (int64_t)wave_max_u64(mxa[r]);
+        if (tr.has_limits) mxc[r] = wave_max_u64(mxc[r]);
+        nt[r] = tr.daemon[r] + rq[r];
+      }
+      // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
+      if (TOPO)
+        for (uint32_t h = lane; h < KD.TGH; h += 64) KD.hc[(size_t)j * KD.TGH + h] = 0;
+      const uint64_t n_sl = pack_slack(d, ma, nt), n_rm = pack_room(thr, s_thoff, c0, nt, KD.RQ);
+      wsyncT<CH>();
+      if (lane == 0) {
+        cr->tmpl = t;
+        cr->count = 1;
+        cr->zm = tr.zm & vzm & tzcat;
+        cr->cm = tr.cm & vcm;
+        cr->ctb = tr.ctb & vctb;
+        cr->zfull = tr.zfull & vzn & tzs;
+        cr->zflags = tzs != ~0ull ? 0u : (tr.zflags & vzflags);
+#pragma unroll
+        for (uint32_t r = 0; r < RR; r++) cr->maxa[r] = ma[r];
+        if (TOPO && sel_n) {
+          // <U> Topology.Record
+          int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
+          topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
+        }
+        FK* cf = KD.c_fk + (size_t)j * F;
+        for (uint32_t s = 0; s < F; s++) cf[s] = KD.t_fk[(size_t)t * F + s];
+        for (uint32_t k = 0; k < fk_count; k++) {
+          const FKEntry& e = KD.fk_entries[fk_begin + k];
+          const FK cur = cf[e.slot];
+          cf[e.slot] = (cur.flags & FK_PRESENT)
+                           ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+                           : e.st;
+        }
+        s_so[M] = 1u | (M << 16);
+        s_tmpl[M] = (uint8_t)t;
+        s_slk[j] = n_sl;
+        s_rm[j] = n_rm;
+        if (tr.has_limits) {
+          // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+          for (uint32_t r = 0; r < R; r++)
+            if (((tr.limit_rmask >> r) & 1) && mxc[r] != 0) KD.t_rem[(size_t)t * R + r] -= (int64_t)(mxc[r] - (1ull << 62));
+        }
+      }
+      wsyncT<CH>();
+      post(WQ_LOG, nlog, gp, v, j, 0);
+      M++;
+      modkind = MOD_APPEND;
+      nlog++;
+      opened = true;
+      break;
+    }
+    }
+    TLW(4);  // new NodeClaim
+    if (status) break;
+    if (opened) continue;
+
+    // -------------------------------------- failed: Relax, then Queue.Push
+    {
+      const auto& KD = *karg();
+      const uint32_t vb = __builtin_amdgcn_readfirstlane(KD.var_begin[gp]);
+      const uint32_t vc = __builtin_amdgcn_readfirstlane(KD.var_count[gp]);
+      const bool relaxed = v + 1 < vb + vc;
+      uint32_t tail = qhead + qlen;
+      if (tail >= P) tail -= P;
+      qlen++;
+      if (lane == 0) {
+        if (relaxed) KD.cur_var[p] = v + 1;
+        KD.queue[tail] = p;
+        if (!relaxed) {
+          KD.last_epoch[p] = epoch;
+          KD.last_len[p] = qlen;
+        }
+      }
+      if (relaxed) epoch++;
+    }
+  }
+  // stop the agent once every posted write is done
+  post(WQ_STOP, 0, 0, 0, 0, 0);
+  drain();
+  if (chan_err) status = 2;
+  wsyncT<CH>();
+  for (uint32_t i = lane; i < M; i += 64) {
+    const uint32_t e = s_so[i];
+    d.c_sorted[i] = e >> 16;
+    d.c_rec[e >> 16].count = e & 0xFFFFu;
+  }
+  auto ctr_at = [&](uint32_t k) -> uint64_t { return (uint64_t)rlane((uint32_t)ctr, k) | ((uint64_t)rlane((uint32_t)(ctr >> 32), k) << 32); };
+  const uint64_t ctr_gen = ctr_at(C_GEN), ctr_fast = ctr_at(C_FAST), ctr_cand = ctr_at(C_CAND), ctr_full = ctr_at(C_FULL),
+                 ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA), ctr_alg = ctr_at(C_ALG);
+  if (lane == 0) {
+    Ctrl c = {};
+    c.status = status;
+    c.n_claims = M;
+    c.n_log = nlog;
+    c.qhead = qhead;
+    c.qlen = qlen;
+    c.epoch = epoch;
+    c.pops = pops;
+    c.generic_sorts = ctr_gen;
+    c.fast_sorts = ctr_fast;
+    c.cand_evals = ctr_cand;
+    c.cand_full = ctr_full;
+    c.node_evals = ctr_nev;
+    c.node_prefix = ctr_npre;
+    c.claim_prefix = ctr_alg;
+    c.dbg[15] = ctr_fa;
+    c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
+#ifdef GS_FFD_TL
+    for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
+    c.dbg[8] = n_fsum;
+    c.dbg[9] = n_xns;
+    c.dbg[10] = n_xb;
+    c.dbg[11] = n_xwin;
+    c.dbg[12] = n_nonsimple;
+    c.dbg[13] = n_rot;
+    c.dbg[14] = n_rotlen;
+#endif
+    *d.ctrl = c;
+  }
+}
