@@ -1002,7 +1002,34 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
     TLW(1);  // topology minimum + existing nodes
     // ------------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
-    if (M > 1) {
+    if (M >= 50 && modkind == MOD_INC && !pivot_touched(modkind, modpos, M)) {
+      // the common case in one LDS round trip: read the 64 positions from
+      // modpos, find the end e of the raised key's run inside them, and
+      // rotate [modpos, e) left there (whole-wave DPP shift); a run that
+      // leaves the window takes the general path below
+      const uint32_t k = modpos + lane;
+      const uint32_t w = k < M ? (uint32_t)acc.so[k] : 0xFFFFu;
+      const uint32_t w0 = rlane(w, 0), x = w0 & 0xFFFFu;
+      const uint64_t b = __ballot(lane >= 1 && (w & 0xFFFFu) >= x);
+      if (b) {
+        const uint32_t eo = ffs64(b);  // e = modpos + eo
+        if (eo > 1) {
+          CTR(C_FAST, 1);
+          const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x130, 0xF, 0xF, false);  // lane i <- i + 1
+          wsyncT<CH>();
+          if (lane < eo) acc.so[k] = lane + 1 == eo ? w0 : sh;
+          wsyncT<CH>();
+#ifdef GS_FFD_TL
+          n_rot++;
+          n_rotlen += eo - 1;
+#endif
+          // (modpos, e-1] shift left, the changed claim lands at e-1
+          if (modpos < hint && modpos + eo - 1 >= hint) hint--;
+        }
+        modkind = MOD_NONE;
+      }
+    }
+    if (M > 1 && modkind != MOD_NONE) {
       // at most one NodeClaim changed since the last sort: one pod added at
       // modpos (INC) or one NodeClaim appended (APPEND)
       bool inversion = false;
@@ -1084,9 +1111,15 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     uint32_t scan_from = lo_bound & ~63u;
     for (;;) {
       uint32_t nex = 0, fa_pos = INF, fa_j = 0, resume = INF;
-      // one 64-position chunk: true = stop the walk
-      auto chunk = [&](uint32_t cb, uint32_t je, uint64_t sq, uint64_t rmv, uint32_t tt) -> bool {
+      // the fast accept's chunk, kept in lanes: its order words, slack and
+      // room codes (the Add reads the winner's lane, no LDS round trip)
+      uint32_t fa_ev = 0;
+      uint64_t fa_sq = 0, fa_rv = 0;
+      for (uint32_t cb = scan_from; cb < M; cb += 64) {
         const uint32_t pos = cb + lane;
+        const uint32_t ev = s_so[pos < M ? pos : M - 1], je = ev >> 16;
+        const uint64_t sq = s_slk[je], rmv = s_rm[je];
+        const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
         const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
         const bool fa = lp & simple & swar_ge(rmv, rqc_p);
@@ -1096,7 +1129,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint32_t cnt = (uint32_t)__popcll(ex);
         if (nex + cnt > 64) {
           resume = cb;  // batch full: check it, then rescan from this chunk
-          return true;
+          break;
         }
         CTR(C_CAND, M - cb < 64 ? M - cb : 64);
         if (ex) {
@@ -1106,14 +1139,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         if (fab) {
           fa_pos = cb + mfl;
           fa_j = rlane(je, mfl);
-          return true;
+          fa_ev = ev;
+          fa_sq = sq;
+          fa_rv = rmv;
+          break;
         }
-        return false;
-      };
-      for (uint32_t cb = scan_from; cb < M; cb += 64) {
-        const uint32_t pos = cb + lane;
-        const uint32_t je = s_so[pos < M ? pos : M - 1] >> 16;
-        if (chunk(cb, je, s_slk[je], s_rm[je], T > 1 ? (uint32_t)s_tmpl[je] : 0u)) break;
       }
       wsyncT<CH>();
       TLW(5);  // phase A: LDS prefilter
@@ -1365,27 +1395,29 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint32_t j = fa_j;
         {
           // lane r < RQ re-quantizes resource r: room (lower bound) and
-          // slack (upper bound) shrink by the request
-          const uint64_t rm = s_rm[j], sl = s_slk[j];
+          // slack (upper bound) shrink by the request.  The old codes and
+          // order word come from the scan's lanes; the new codes are packed
+          // across lanes 0..3 with DPP (no scalar round trip) and lane 0
+          // stores them
+          const uint32_t fl = f & 63u;
+          const uint64_t rm = ((uint64_t)rlane((uint32_t)(fa_rv >> 32), fl) << 32) | rlane((uint32_t)fa_rv, fl);
+          const uint64_t sl = ((uint64_t)rlane((uint32_t)(fa_sq >> 32), fl) << 32) | rlane((uint32_t)fa_sq, fl);
+          const uint32_t e = rlane(fa_ev, fl);
           uint32_t c_rm = 0, c_sl = 0;
           if (lane < d.RQ) {
             const uint32_t sh = 16 * lane;
             c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - rq_lane);
             c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - rq_lane);
           }
-          uint64_t rm2 = 0, sl2 = 0;
-#pragma unroll
-          for (uint32_t r = 0; r < 4; r++) {
-            if (r < d.RQ) {
-              rm2 |= (uint64_t)rlane(c_rm, r) << (16 * r);
-              sl2 |= (uint64_t)rlane(c_sl, r) << (16 * r);
-            }
-          }
+          uint32_t prm = (lane & 1u) ? c_rm << 16 : c_rm, psl = (lane & 1u) ? c_sl << 16 : c_sl;
+          prm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+          psl |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl, 0xB1, 0xF, 0xF, false);
+          const uint32_t hrm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm, 0x102, 0xF, 0xF, false);  // row_shl:2
+          const uint32_t hsl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl, 0x102, 0xF, 0xF, false);
+          if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
           if (lane == 0) {
-            s_rm[j] = rm2;
-            s_slk[j] = sl2;
-            const uint32_t e = s_so[f];
-            if ((e & 0xFFFFu) == 0xFFFFu) ovf = true;
+            s_rm[j] = (uint64_t)prm | ((uint64_t)hrm << 32);
+            s_slk[j] = (uint64_t)psl | ((uint64_t)hsl << 32);
             s_so[f] = e + 1u;
             if (TOPO && sel_n) {
               // <U> Topology.Record in the groups that select the pod: the
