@@ -716,6 +716,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
   uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0;
 #endif
+  uint32_t pf_x = 0, pf_seq = 0;  // prefetched ring record and its sequence word
   for (;;) {
     // ---------------------------------------------------------- Queue.Pop
     TLW(7);  // previous pod's tail (continue paths)
@@ -735,15 +736,17 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // record are read in one round trip: the LDS serves a wave's reads in
       // order and the agent wrote the record before the sequence word.
       const uint32_t rs = qhead % RING;
-      uint32_t x = 0;
-      for (uint32_t spin = 0;; spin++) {
-        const uint32_t sq = vld(&s_ring_seq[rs]);
-        x = lane < RING_DW ? vld(&s_ring[rs][lane]) : 0u;
-        if (__builtin_amdgcn_readfirstlane(sq) == qhead + 1) break;
-        __builtin_amdgcn_s_sleep(0);
-        if (spin > SPIN_MAX) {
-          chan_err = true;
-          break;
+      uint32_t x = pf_x;  // read during the previous pop
+      if (__builtin_amdgcn_readfirstlane(pf_seq) != qhead + 1) {
+        for (uint32_t spin = 0;; spin++) {
+          const uint32_t sq = vld(&s_ring_seq[rs]);
+          x = lane < RING_DW ? vld(&s_ring[rs][lane]) : 0u;
+          if (__builtin_amdgcn_readfirstlane(sq) == qhead + 1) break;
+          __builtin_amdgcn_s_sleep(0);
+          if (spin > SPIN_MAX) {
+            chan_err = true;
+            break;
+          }
         }
       }
       if (chan_err) {
@@ -772,6 +775,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     qlen--;
     pops++;
     if (lane == 0) vst(&s_ctl[3], (uint32_t)pops);  // heartbeat for the agent's bounded wait
+    if (!wrapped) {
+      // the next first-pass record, read now: its round trip overlaps this
+      // pod (a slot the agent has not filled yet is re-read at the pop)
+      pf_seq = vld(&s_ring_seq[qhead % RING]);
+      pf_x = lane < RING_DW ? vld(&s_ring[qhead % RING][lane]) : 0u;
+    }
     const uint32_t gp = p;
     auto VD = [&](uint32_t i) -> uint32_t { return rlane(vrd, i); };
     auto VD64 = [&](uint32_t i) -> uint64_t { return (uint64_t)VD(i) | ((uint64_t)VD(i + 1) << 32); };
@@ -1002,6 +1011,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
     TLW(1);  // topology minimum + existing nodes
     // ------------------------------- sort.Slice(newNodeClaims, len(Pods) asc)
+    uint32_t win_base = INF, win_v = 0;  // positions [win_base, +64) after the rotation (the scan may start there)
     if (M >= 50 && modkind == MOD_INC && !pivot_touched(modkind, modpos, M)) {
       // the common case in one LDS round trip: read the 64 positions from
       // modpos, find the end e of the raised key's run inside them, and
@@ -1016,16 +1026,21 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         if (eo > 1) {
           CTR(C_FAST, 1);
           const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x130, 0xF, 0xF, false);  // lane i <- i + 1
+          const uint32_t nw = lane + 1 == eo ? w0 : sh;
           wsyncT<CH>();
-          if (lane < eo) acc.so[k] = lane + 1 == eo ? w0 : sh;
+          if (lane < eo) acc.so[k] = nw;
           wsyncT<CH>();
+          win_v = lane < eo ? nw : w;
 #ifdef GS_FFD_TL
           n_rot++;
           n_rotlen += eo - 1;
 #endif
           // (modpos, e-1] shift left, the changed claim lands at e-1
           if (modpos < hint && modpos + eo - 1 >= hint) hint--;
+        } else {
+          win_v = w;
         }
+        win_base = modpos;
         modkind = MOD_NONE;
       }
     }
@@ -1108,16 +1123,18 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       const bool ge = lane >= 4 || lane >= R || rq_lane >= hint_rq;
       if (__ballot(!ge) == 0) lo_bound = hint;
     }
-    uint32_t scan_from = lo_bound & ~63u;
+    uint32_t scan_from = lo_bound;  // chunks start at the bound (no dead lanes below it)
     for (;;) {
       uint32_t nex = 0, fa_pos = INF, fa_j = 0, resume = INF;
       // the fast accept's chunk, kept in lanes: its order words, slack and
       // room codes (the Add reads the winner's lane, no LDS round trip)
-      uint32_t fa_ev = 0;
+      uint32_t fa_ev = 0, fa_l = 0;  // fa_l: the fast accept's lane (chunks start at the bound, unaligned)
       uint64_t fa_sq = 0, fa_rv = 0;
       for (uint32_t cb = scan_from; cb < M; cb += 64) {
         const uint32_t pos = cb + lane;
-        const uint32_t ev = s_so[pos < M ? pos : M - 1], je = ev >> 16;
+        // the sort's window is this chunk when the scan starts where the last
+        // Add landed (runs of equal pods): no LDS read of the order words
+        const uint32_t ev = cb == win_base ? win_v : s_so[pos < M ? pos : M - 1], je = ev >> 16;
         const uint64_t sq = s_slk[je], rmv = s_rm[je];
         const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
@@ -1140,6 +1157,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           fa_pos = cb + mfl;
           fa_j = rlane(je, mfl);
           fa_ev = ev;
+          fa_l = mfl;
           fa_sq = sq;
           fa_rv = rmv;
           break;
@@ -1399,7 +1417,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           // order word come from the scan's lanes; the new codes are packed
           // across lanes 0..3 with DPP (no scalar round trip) and lane 0
           // stores them
-          const uint32_t fl = f & 63u;
+          const uint32_t fl = fa_l;
           const uint64_t rm = ((uint64_t)rlane((uint32_t)(fa_rv >> 32), fl) << 32) | rlane((uint32_t)fa_rv, fl);
           const uint64_t sl = ((uint64_t)rlane((uint32_t)(fa_sq >> 32), fl) << 32) | rlane((uint32_t)fa_sq, fl);
           const uint32_t e = rlane(fa_ev, fl);
