@@ -789,21 +789,32 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     // topology: own list (groups the variant owns), selection list (groups counting the pod)
     const uint32_t own_off = TOPO ? VD(22) : 0u, own_n = TOPO ? VD(23) : 0u;
     const uint32_t sel_off = TOPO ? VD(24) : 0u, sel_n = TOPO ? VD(25) : 0u;
-    int64_t rq[RR];
-#pragma unroll
-    for (uint32_t r = 0; r < RR; r++)
-      rq[r] = (int64_t)((uint64_t)rlane(rqd, 32 + 2 * r) | ((uint64_t)rlane(rqd, 33 + 2 * r) << 32));
-    int64_t rq_lane = 0;  // lane r < R: resource r's request
-#pragma unroll
-    for (uint32_t r = 0; r < RR; r++)
-      if (lane == r) rq_lane = rq[r];
+    // the requests stay in the record's lanes 32.. (rqd): every use site
+    // reads them with its own readlanes (RQ), so no 64-bit request is held
+    // in scalar registers across the pod (they spilled into VGPR lanes)
+// (GS_RQ_AT copies the record: use it in uniform control flow only)
+#define GS_RQ_AT(name)                                                                                \
+  const uint32_t name##_x = fresh(rqd);                                                               \
+  auto name = [&](uint32_t r) -> int64_t {                                                            \
+    return (int64_t)((uint64_t)rlane(name##_x, 32 + 2 * r) | ((uint64_t)rlane(name##_x, 33 + 2 * r) << 32)); \
+  }
+    // lane r < R: resource r's request (lanes 2r + 32, 2r + 33 of the record)
+    int64_t rq_lane = 0;
+    {
+      const uint32_t lo = (uint32_t)__shfl((int)rqd, (int)(32 + 2 * (lane & 7))),
+                     hi = (uint32_t)__shfl((int)rqd, (int)(33 + 2 * (lane & 7)));
+      if (lane < RR) rq_lane = (int64_t)(((uint64_t)hi << 32) | lo);
+    }
+    // resources 4.. requested at all (the LDS codes cover resources 0..3)
+    const bool rq_hi = RR > 4 && __ballot(lane >= 4 && lane < RR && rq_lane != 0) != 0;
     if (!from_ring) {
       // a wrapped pop read its record itself: the request codes too
+      GS_RQ_AT(RQ);
 #pragma unroll
       for (uint32_t r = 0; r < 4; r++)
         if (r < d.RQ && r < RR) {
-          rqq_p |= (uint64_t)qcode_floor(rq[r]) << (16 * r);
-          rqc_p |= (uint64_t)qcode_ceil(rq[r]) << (16 * r);
+          rqq_p |= (uint64_t)qcode_floor(RQ(r)) << (16 * r);
+          rqc_p |= (uint64_t)qcode_ceil(RQ(r)) << (16 * r);
         }
     }
 
@@ -843,8 +854,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
       for (uint32_t q = 0; q < VDMAX; q++) pvany = pvany || pvol[q] || pfresh[q];
       bool nplain = (vctb & VF_SIMPLE) && !pvany;
-#pragma unroll
-      for (uint32_t r = 4; r < RR; r++) nplain = nplain && rq[r] == 0;
+      nplain = nplain && !rq_hi;
       const uint64_t nrqq = rqq_p, nrqc = rqc_p;
       uint32_t nlo = 0;
       if (nhint_ok && (vtol & ~nhint_tol) == 0) {
@@ -853,6 +863,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       }
       uint32_t fn = INF;
       bool nfa_win = false;
+      GS_RQ_AT(RQ);  // in uniform control flow: the copy must hold every lane
       for (uint32_t base = nlo & ~63u; base < KD.NN; base += 64) {
         const uint32_t n = base + lane;
         const bool in = (n < KD.NN) & (n >= nlo);
@@ -875,7 +886,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const FK* nfk = KD.n_fk + (size_t)n * F;
             feas = nr.ok && (nr.taints & ~vtol) == 0;  // Taints.ToleratesPod
 #pragma unroll
-            for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + rq[r] <= nr.avail[r];  // Fits
+            for (uint32_t r = 0; r < RR; r++) feas = feas && nr.req[r] + RQ(r) <= nr.avail[r];  // Fits
 #pragma unroll
             for (uint32_t k = 0; k < KMAX_IT; k++) {
               const uint32_t off = VX(4 + k);
@@ -1099,8 +1110,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     // its CanAdd is resources and taints only, in either variant
     bool simple = (vctb & VF_SIMPLE) != 0;
 #endif
-#pragma unroll
-    for (uint32_t r = 4; r < RR; r++) simple = simple && rq[r] == 0;  // room covers resources 0..3
+    simple = simple && !rq_hi;  // room covers resources 0..3
 #ifdef GS_FFD_TL
     n_nonsimple += simple ? 0u : 1u;
 #endif
@@ -1184,6 +1194,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint32_t xe = lane < nex ? s_exl[lane] : 0u;
         const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
         const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
+        GS_RQ_AT(RQ);
       bool feas = false;
       uint64_t zset = ~0ull;  // zone domains topology allows on this NodeClaim (~0: unconstrained)
       uint64_t zm = 0, cm = 0, czf = 0;
@@ -1241,12 +1252,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
             const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
-            mm[r] = thr_window(thr + o, n, cur[r], tot[r] + rq[r]);
+            mm[r] = thr_window(thr + o, n, cur[r], tot[r] + RQ(r));
           }
 #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
             const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
-            if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + rq[r]);
+            if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], tot[r] + RQ(r));
             mrow[r] = o + r + mm[r];
           }
           uint64_t accw = 0;
@@ -1361,7 +1372,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           uint32_t cu[RR];
   #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
-            nt[r] = tot[r] + rq[r];
+            nt[r] = tot[r] + RQ(r);
             ma[r] = cr->maxa[r];
             cu[r] = mrow[r] - s_thoff[r] - r;
             cr->tot(r) = nt[r];
@@ -1602,11 +1613,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         }
       }
       int64_t ma[RR], nt[RR];
+      GS_RQ_AT(RQ);
 #pragma unroll
       for (uint32_t r = 0; r < RR; r++) {
         ma[r] = (int64_t)wave_max_u64(mxa[r]);
         if (tr.has_limits) mxc[r] = wave_max_u64(mxc[r]);
-        nt[r] = tr.daemon[r] + rq[r];
+        nt[r] = tr.daemon[r] + RQ(r);
       }
       // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
       if (TOPO)
