@@ -698,6 +698,29 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     }
   };
 
+  // Solver-side global writes (GS_AGENT_WRITES=0, the default): the add log
+  // entry (lane 0) and, for a requests-only Add, the no-return atomic adds
+  // of the requests (lanes r < min(R, 4)).  They are fire-and-forget: the
+  // next exact check's loads wait on the vector memory counter, which the
+  // wave's earlier stores and atomics precede, instead of draining the
+  // agent's channel.
+#ifndef GS_AGENT_WRITES
+#define GS_AGENT_WRITES 0
+#endif
+  auto emit = [&](uint32_t type, uint32_t idx, uint32_t pod, uint32_t var, uint32_t tgt, uint32_t rqd_, int64_t rql) {
+    if (GS_AGENT_WRITES) {
+      post(type, idx, pod, var, tgt, rqd_);
+      return;
+    }
+    const auto& KD = *karg();
+    if (lane == 0) KD.log[idx] = LogRec{pod, var, type == WQ_NFA ? tgt | 0x80000000u : tgt, 0};
+    if ((type == WQ_FA || type == WQ_NFA) && lane < R && lane < 4 && rql != 0) {
+      unsigned long long* a = type == WQ_FA ? (unsigned long long*)&KD.c_rec[tgt].tot_lo[lane]
+                                            : (unsigned long long*)&KD.nodes[tgt].req[lane];
+      atomicAdd(a, (unsigned long long)rql);
+    }
+  };
+
   // uniform loop state (scalar registers)
   uint32_t qhead = 0, qlen = P, epoch = 1, M = 0, modkind = MOD_NONE, modpos = 0, nlog = 0, status = 0;
   bool wrapped = false;
@@ -880,7 +903,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const bool need = lp & !fa & (lane < mfl);
         bool feas = fa;
         if (__ballot(need)) {
-          drain();  // node requests the agent still adds (fast accepts)
+          if (GS_AGENT_WRITES) drain();  // node requests the agent still adds (fast accepts)
           if (need) {
             const NodeRec& nr = KD.nodes[n];
             const FK* nfk = KD.n_fk + (size_t)n * F;
@@ -955,7 +978,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         }
         wsyncT<CH>();
-        post(WQ_NFA, nlog, gp, v, fn, rqd);
+        emit(WQ_NFA, nlog, gp, v, fn, rqd, rq_lane);
         nlog++;
         continue;
       }
@@ -1014,7 +1037,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         }
         wsyncT<CH>();
-        post(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0);
+        emit(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0, 0);
         nlog++;
         continue;
       }
@@ -1176,7 +1199,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       wsyncT<CH>();
       TLW(5);  // phase A: LDS prefilter
       if (nex) {
-        drain();  // the agent's request totals must be in the claim records
+        if (GS_AGENT_WRITES) drain();  // the agent's request totals must be in the claim records
         const auto& KD = *karg();
         const uint32_t vx = fresh(vrd);
         auto VX = [&](uint32_t i) -> uint32_t { return rlane(vx, i); };
@@ -1410,7 +1433,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           s_so[f] = e + 1u;
         }
           wsyncT<CH>();
-          post(WQ_LOG, nlog, gp, v, rlane(j, wl), 0);
+          emit(WQ_LOG, nlog, gp, v, rlane(j, wl), 0, 0);
           break;
         }
       }
@@ -1459,7 +1482,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         }
         wsyncT<CH>();
-        post(WQ_FA, nlog, gp, v, j, rqd);  // the agent adds the requests and logs
+        emit(WQ_FA, nlog, gp, v, j, rqd, rq_lane);  // the requests into the claim totals, and the log
         CTR(C_FA, 1);
         break;
       }
@@ -1660,7 +1683,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         }
       }
       wsyncT<CH>();
-      post(WQ_LOG, nlog, gp, v, j, 0);
+      emit(WQ_LOG, nlog, gp, v, j, 0, 0);
       M++;
       modkind = MOD_APPEND;
       nlog++;
