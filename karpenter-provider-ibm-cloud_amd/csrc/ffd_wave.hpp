@@ -797,7 +797,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     pops++;
-    if (lane == 0) vst(&s_ctl[3], (uint32_t)pops);  // heartbeat for the agent's bounded wait
+    if ((pops & 15) == 0 && lane == 0) vst(&s_ctl[3], (uint32_t)pops);  // heartbeat for the agent's bounded wait
     if (!wrapped) {
       // the next first-pass record, read now: its round trip overlaps this
       // pod (a slot the agent has not filled yet is re-read at the pop)
