@@ -19,13 +19,14 @@ if [ -z "${SKIP_KT:-}" ]; then
     python3 $R/bench.py --only cm --steps 5 --warmup 1 --latency-steps 0 --no-cpu-baseline > $O/bench_kt_cm.json 2> $O/kt_cm.err
   echo "cm kernel trace done"
 fi
-rm -f $O/traffic.json
+TJ=$O/${TRAFFIC:-traffic.json}
+rm -f $TJ
 for leg in $LEGS; do
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$leg -o fetch -- \
     python3 $R/bench.py --only $leg --steps 1 --warmup 0 --latency-steps 0 --no-cpu-baseline > $O/bench_fetch_$leg.json 2> $O/fetch_$leg.err
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$leg -o write -- \
     python3 $R/bench.py --only $leg --steps 1 --warmup 0 --latency-steps 0 --no-cpu-baseline > $O/bench_write_$leg.json 2> $O/write_$leg.err
-  python3 $R/tools/pmc_traffic.py $leg $O/fetch_$leg/fetch_counter_collection.csv $O/write_$leg/write_counter_collection.csv $O/traffic.json
+  python3 $R/tools/pmc_traffic.py $leg $O/fetch_$leg/fetch_counter_collection.csv $O/write_$leg/write_counter_collection.csv $TJ
   echo "pmc $leg done"
 done
-cat $O/traffic.json
+cat $TJ
