@@ -94,6 +94,11 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.vars, e.vars);
   c->upload(d.itmask, e.itmask);
   c->upload(d.var_itclass, e.var_itclass);
+  {
+    std::vector<uint32_t> vp(std::max<uint32_t>(e.V, 1), 0);
+    for (uint32_t v = 0; v < e.V; v++) vp[v] = e.vars[v].pod;
+    c->upload(d.var_pod, vp);
+  }
   c->upload(d.itclass_mask, e.itclass_mask);
   c->upload(d.fk_entries, e.fk_entries);
   c->upload(d.queue0, e.queue0);

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(BLOCK) void feas_cursor_kernel(DevProblem d) {
   const uint32_t r = (uint32_t)(id % R);
   const uint64_t pair = id / R;
   const uint32_t v = (uint32_t)(pair / T), t = (uint32_t)(pair % T);
-  const int64_t dem = d.tmpl[t].daemon[r] + d.pod_req[(size_t)d.vars[v].pod * R + r];
+  const int64_t dem = d.tmpl[t].daemon[r] + d.pod_req[(size_t)d.var_pod[v] * R + r];
   const uint32_t o = d.thr_off[r];
   d.pair_cur[id] = o + r + lower_bound_i64(d.thr_val + o, d.thr_off[r + 1] - o, dem);
 }

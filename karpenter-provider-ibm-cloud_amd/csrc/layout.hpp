@@ -253,6 +253,7 @@ struct DevProblem {
   const VarRec* vars;          // [V]
   const uint64_t* itmask;      // arena
   const uint32_t* var_itclass; // [V] IT-key requirement class of each variant (NONE: no IT keys)
+  const uint32_t* var_pod;     // [V] each variant's pod (the K1 cursor pass reads 4 B, not the 128-B VarRec)
   const uint64_t* itclass_mask;// [classes][W] instance types each class's IT-key requirements allow
   const FKEntry* fk_entries;
   const uint32_t* queue0;      // [P] initial queue order
