@@ -155,6 +155,17 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.zone_order, e.zone_order);
   c->upload(d.zone_cat, e.zone_cat);
   c->upload(d.hn0, e.hn0);
+  if (sims && e.TGH && e.NN) {
+    // node-major copy: a simulation's overlay entry and its candidates'
+    // exclusion read every group of one node (one contiguous row, not TGH
+    // lines strided by NN)
+    std::vector<int32_t> nm((size_t)e.NN * e.TGH);
+    for (uint32_t g = 0; g < e.TGH; g++)
+      for (uint32_t n = 0; n < e.NN; n++) nm[(size_t)n * e.TGH + g] = e.hn0[(size_t)g * e.NN + n];
+    c->upload(d.hn0_nm, nm);
+  } else {
+    d.hn0_nm = d.hn0;  // not read outside simulations
+  }
   c->alloc(d.hn, e.hn0.size());
   c->upload(d.nodes0, e.nodes);
   c->upload(d.n_fk0, e.n_fk);

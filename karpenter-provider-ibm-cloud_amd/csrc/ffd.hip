@@ -676,7 +676,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const uint32_t z = d.nodes0[n].zvid;
             if (c && z < d.ZS) atomicSub(&ts.zcnt[g * d.ZS + z], c);
           } else {
-            const int32_t c = d.hn0[(size_t)(g - d.TGZ) * d.NN + n];
+            const int32_t c = d.hn0_nm[(size_t)n * d.TGH + (g - d.TGZ)];
             if (c) atomicSub(&ts.htot[g - d.TGZ], c);
           }
         }
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
               if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
               if (TOPO) {
-                for (uint32_t x = tid; x < d.TGH; x += FB) ahn[x] = d.hn0[(size_t)x * d.NN + fn];
+                for (uint32_t x = tid; x < d.TGH; x += FB) ahn[x] = d.hn0_nm[(size_t)fn * d.TGH + x];
                 if (d.any_vol && tid == 128) *avol = d.n_vol0[fn];
               }
             }

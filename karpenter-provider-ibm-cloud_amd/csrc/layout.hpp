@@ -307,6 +307,7 @@ struct DevProblem {
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)
   const uint32_t* zone_cat;    // [64] zone vocabulary id -> catalog zone index (NONE)
   const int32_t* hn0;          // [TGH][NN] hostname counts per existing node before the Solve
+  const int32_t* hn0_nm;       // [NN][TGH] the same, node-major (simulations copy a node's whole row)
   int32_t* hn;                 // [TGH][NN] working copy
   int32_t* hc;                 // [max_claims][TGH] per NodeClaim (one row per claim)
   // truncation outputs
