@@ -174,7 +174,10 @@ struct WaveSort {
   }
   // the passes below test RW x 64 positions per step: every lane issues its
   // RW LDS reads before the first ballot (one round trip per step)
-  static constexpr int RW = 4;
+#ifndef GS_SORT_RW
+#define GS_SORT_RW 4
+#endif
+  static constexpr int RW = GS_SORT_RW;
   template <class Pred>
   __device__ uint32_t count(int lo, int hi, Pred pred) const {
     uint32_t c = 0;
@@ -737,7 +740,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
 #ifdef GS_FFD_TL
   uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
-  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0;
+  uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0, n_gen_cyc = 0;
 #endif
   uint32_t pf_x = 0, pf_seq = 0;  // prefetched ring record and its sequence word
   for (;;) {
@@ -1115,7 +1118,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         } else {
           CTR(C_GEN, 1);
+#ifdef GS_FFD_TL
+          const uint64_t g0_ = __builtin_amdgcn_s_memtime();
+#endif
           wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
+#ifdef GS_FFD_TL
+          n_gen_cyc += __builtin_amdgcn_s_memtime() - g0_;
+#endif
           hint_ok = false;
         }
       }
@@ -1748,7 +1757,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
-    c.dbg[8] = n_fsum;
+    c.dbg[8] = n_gen_cyc;  // shader cycles in Go's full pdqsort (generic sorts)
     c.dbg[9] = n_xns;
     c.dbg[10] = n_xb;
     c.dbg[11] = n_xwin;

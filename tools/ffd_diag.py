@@ -35,7 +35,8 @@ if "--tl" in sys.argv and "--block" not in sys.argv:
     names = ["pop_record", "nodes", "sort", "scan_add", "new_claim", "scanA_lds", "scanB_exact", "tail"]
     base["cycles_per_pop"] = {n: round(out[i] / max(res.pops, 1), 1) for i, n in enumerate(names) if n != "-"}
     base["cycles_per_pop_total"] = round(sum(out[i] for i in range(8)) / max(res.pops, 1), 1)
-    base["mean_winner_pos"] = round(out[8] / max(res.pops, 1), 1)
+    base["generic_sort_cycles_per_pop"] = round(out[8] / max(res.pops, 1), 1)
+    base["cycles_per_generic_sort"] = round(out[8] / max(res.sorts_generic, 1), 1)
     base["fast_accepts"] = out[15]
     base["exact_cands_nonsimple"] = out[9]
     base["exact_batches"] = out[10]
