@@ -64,6 +64,17 @@ def ffd_bytes(res, n_types):
     return int(res.claim_prefix) * ((n_types + 7) // 8) + 32 * int(res.pops) + 40 * int(res.node_prefix)
 
 
+def ffd_unique_bytes(res, n_types, n_res, n_claims, n_nodes):
+    """unique HBM bytes of one K4 launch: every popped pod's variant record and
+    requests (128 + 8 R B) and its add-log entry (16 B), every NodeClaim's
+    record and option words written (192 + 8 OW B), every existing node read
+    once (184 B).  The claim visits of ffd_bytes() are served from LDS and L2,
+    so they are priced against the L2 in a second roofline object."""
+    words = (n_types + 63) // 64
+    ow = max(4, (words + 3) // 4 * 4)
+    return int(res.pops) * (128 + 8 * n_res + 16) + n_claims * (192 + 8 * ow) + n_nodes * 184
+
+
 def feas_bytes(V, T, O, words):
     """per-launch algorithmic bytes of feas_kernel over `words` instance-type
     words: variant records (128 B), the offering list (48 B), rows + cheapest
@@ -168,7 +179,14 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         "ffd_candidates_scanned": int(res.cand_evals),
         "ffd_candidates_exact_checked": int(res.cand_full),
         "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
-        "roofline": roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        # unique HBM bytes (PMC-comparable); SURVEY §8(d)'s K4 figure (claim
+        # visits, LDS/L2-resident by design) priced against the L2; and the
+        # latency per pod §8(d) asks for
+        "roofline": roofline(names["ffd"], ffd_unique_bytes(res, n_types, min(8, len(np.unique(problem.quantities["resource"]))), len(out["claims"]),
+                                                            len(problem.nodes)),
+                             kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        "roofline_l2_claim_visits": roofline(names["ffd"], ab["ffd"], kms["ffd"], None, L2_PEAK_GBS, "l2"),
+        "ffd_us_per_pop": round(kms["ffd"] * 1e3 / max(int(res.pops), 1), 4),
         "roofline_feasibility_kernel": roofline("feas_cursor_kernel + feas_kernel", ab["feas"], kms["feas"],
                                                 traffic_of(traffic or {}, leg, "feas", "feas_cursor")),
         "_result": out,
