@@ -215,6 +215,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->alloc(d.ov_fk, (size_t)sims->blocks * d.ov_cap * F1);
     // the general (topology / volumes / minValues) simulation variant
     c->alloc(d.ov_hn, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1));
+    c->alloc(d.ov_hmask, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>((e.TGH + 31) / 32, 1));
     c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
     c->alloc(d.ov_map, (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
     {

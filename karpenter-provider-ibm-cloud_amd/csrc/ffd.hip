@@ -599,6 +599,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   // SIM: a touched node's overlay entry (| OV_EXCL: a removed candidate), valid where its s_nb bit is set
   uint32_t* const ov_map = SIM ? d.ov_map + (size_t)blockIdx.x * d.NN : nullptr;
+  const uint32_t HW = (d.TGH + 31u) >> 5;  // words of an overlay entry's counted-group mask
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
@@ -946,7 +947,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (TOPO && feas && own_n)
               feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
                 if (!SIM) return d.hn[(size_t)hs * d.NN + n];
-                return oe != ~(size_t)0 ? d.ov_hn[oe * d.TGH + hs] : d.hn0[(size_t)hs * d.NN + n];
+                // an overlay row holds only the groups this simulation counted on the node
+                if (oe != ~(size_t)0 && ((d.ov_hmask[oe * HW + (hs >> 5)] >> (hs & 31)) & 1)) return d.ov_hn[oe * d.TGH + hs];
+                return d.hn0[(size_t)hs * d.NN + n];
               });
             if (TOPO && feas && d.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
@@ -968,6 +971,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           int32_t* ahn = nullptr;   // the node's hostname counts (row stride ahs)
           size_t ahs = 0;
           NodeVol* avol = nullptr;  // the node's volume usage
+          size_t ovx = 0;           // SIM: the node's overlay entry
           if (SIM) {
             // copy-on-write overlay entry for the node
             if (tid == 0) {
@@ -985,6 +989,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             }
             __syncthreads();
             const size_t oe = (size_t)blockIdx.x * d.ov_cap + S.ove;
+            ovx = oe;
             areq = d.ov_req + oe * RMAX;
             afk = d.ov_fk + oe * F;
             if (TOPO) {
@@ -996,7 +1001,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
               if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
               if (TOPO) {
-                for (uint32_t x = tid; x < d.TGH; x += FB) ahn[x] = d.hn0_nm[(size_t)fn * d.TGH + x];
+                for (uint32_t x = tid; x < HW; x += FB) d.ov_hmask[oe * HW + x] = 0;  // no group counted yet
                 if (d.any_vol && tid == 128) *avol = d.n_vol0[fn];
               }
             }
@@ -1033,8 +1038,21 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             // <U> Topology.Record: the node's labels are single domains
             if (TOPO && sel_n) {
               const uint32_t z = d.nodes0[fn].zvid;
-              topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
-                          [&](uint32_t hs) { ahn[(size_t)hs * ahs]++; });
+              topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u, [&](uint32_t hs) {
+                if (SIM) {
+                  // copy-on-write per group: the first count takes the node's base
+                  uint32_t* mw = d.ov_hmask + ovx * HW + (hs >> 5);
+                  const uint32_t bit = 1u << (hs & 31);
+                  if (*mw & bit) {
+                    ahn[hs]++;
+                  } else {
+                    ahn[hs] = d.hn0_nm[(size_t)fn * d.TGH + hs] + 1;
+                    *mw |= bit;
+                  }
+                } else {
+                  ahn[(size_t)hs * ahs]++;
+                }
+              });
             }
           }
           pf_stage2();

@@ -346,6 +346,7 @@ struct DevProblem {
   const int32_t* zn_cnt;       // [TGZ][NN]
   int32_t* ov_hn;              // [grid][ov_cap][TGH]
   NodeVol* ov_vol;             // [grid][ov_cap]
+  uint32_t* ov_hmask;          // [grid][ov_cap][ceil(TGH / 32)] hostname groups whose overlay count is written (others read hn0_nm)
   uint32_t* ov_map;            // [grid][NN] a touched node's overlay entry (valid where the LDS bitmap bit is set)
 };
 
