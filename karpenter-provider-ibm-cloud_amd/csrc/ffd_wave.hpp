@@ -1,7 +1,7 @@
 // ffd_wave.hpp — the single-wave provisioning Solve kernel template
 // (ffdw_kernel), shared by the per-(R, TOPO) translation units
-// ffd_wave_r.hip compiles (one per resource count and variant: the
-// register-mode instantiations are large, so they build in parallel).
+// ffd_wave_r.hip compiles (one per resource count and variant, built in
+// parallel).
 #pragma once
 //
 // The <U> Scheduler.Solve queue loop is sequential in pod order; its cost
@@ -19,7 +19,10 @@
 //  * the next pod's variant record and requests are prefetched into lanes
 //    during the current pod (first pass: records laid out in queue order);
 //  * a fast-accepted NodeClaim.Add (requests only) is LDS updates plus
-//    no-return atomic adds of the requests at L2: no round trip.
+//    no-return atomic adds of the requests at L2, issued by the solver
+//    itself: no round trip (the agent wave only stages first-pass records);
+//  * the one-claim sort.Slice rotation moves a 64-position window in one
+//    LDS round trip (whole-wave DPP shift).
 // Results are bit-identical to ffd.hip's block kernel (same restatement of
 // Go's sort.Slice, same candidate order, same Add), which still serves the
 // consolidation simulations and Solves with many existing nodes.
@@ -562,10 +565,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   if (wave == 1) {
     // ================================================== memory agent wave
     // (1) stages the next first-pass pod records (queue order) into the LDS
-    //     ring ahead of the solver; (2) performs the solver's global writes
-    //     (add log, fast-accept request totals) and reports their completion.
-    //     The solver wave thus issues no global memory operation on its
-    //     common path, and never waits on one it did not need.
+    //     ring ahead of the solver; (2) with GS_AGENT_WRITES=1 only (the
+    //     round-2 design), performs the solver's posted global writes (add
+    //     log, fast-accept request totals) and reports their completion; by
+    //     default the solver issues them itself (fire-and-forget) and only
+    //     the final WQ_STOP is posted.
     const uint32_t* qv_dw = (const uint32_t*)d.qvars;
     const uint32_t* qr_dw = (const uint32_t*)d.qreqs;
     uint32_t k_fill = 0, head = 0, idle = 0, beat = 0;
