@@ -737,6 +737,14 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   uint64_t ctr = 0;
 #ifdef GS_NO_CTR  // experiment builds: the counters' cost
 #define CTR(k, x) ((void)0)
+#elif defined(GS_CTR_LDS)  // experiment: counters as no-return LDS atomic adds by lane 0
+  __shared__ unsigned long long s_ctr[8];
+  if (lane < 8) s_ctr[lane] = 0;
+  wsync();
+#define CTR(k, x)                                                        \
+  do {                                                                   \
+    if (lane == 0) atomicAdd(&s_ctr[(k)], (unsigned long long)(x));     \
+  } while (0)
 #else
 #define CTR(k, x) (ctr += lane == (k) ? (uint64_t)(x) : 0ull)
 #endif
@@ -1738,7 +1746,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     d.c_sorted[i] = e >> 16;
     d.c_rec[e >> 16].count = e & 0xFFFFu;
   }
+#ifdef GS_CTR_LDS
+  wsync();
+  auto ctr_at = [&](uint32_t k) -> uint64_t { return (uint64_t)s_ctr[k]; };
+#else
   auto ctr_at = [&](uint32_t k) -> uint64_t { return (uint64_t)rlane((uint32_t)ctr, k) | ((uint64_t)rlane((uint32_t)(ctr >> 32), k) << 32); };
+#endif
   const uint64_t ctr_gen = ctr_at(C_GEN), ctr_fast = ctr_at(C_FAST), ctr_cand = ctr_at(C_CAND), ctr_full = ctr_at(C_FULL),
                  ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA), ctr_alg = ctr_at(C_ALG);
   if (lane == 0) {
