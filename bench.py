@@ -122,6 +122,122 @@ def digest(res_dict):
     return hashlib.sha256(json.dumps(res_dict, sort_keys=True, separators=(",", ":")).encode()).hexdigest()
 
 
+# ------------------------------------------------------------ output lines
+HEADLINE_MAX_BYTES = 6144  # the driver keeps the last 8 KB of stdout: the headline must fit wholly
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "solve_latency_ms",
+                 "ffd_us_per_pop")
+
+
+def _r(x, nd=4):
+    """round floats for the compact line (None and ints pass through)"""
+    if isinstance(x, float):
+        return float(f"{x:.{nd}g}") if abs(x) >= 1e5 or (x != 0 and abs(x) < 1e-3) else round(x, nd)
+    return x
+
+
+def _compact_roofline(rf):
+    if not rf:
+        return None
+    keep = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes", "avg_ms")
+    return {k: _r(rf.get(k)) for k in keep if k in rf}
+
+
+def _compact_cpu(cb):
+    if not cb:
+        return cb
+    out = {k: _r(cb[k]) for k in ("value", "unit", "cores", "kind", "solve_ms", "ms_per_call", "value_1_core",
+                                  "gpu_result_bit_exact") if k in cb}
+    out["sample"] = (cb.get("sample") or "")[:160]
+    return out
+
+
+def _leg_summary(leg):
+    """a few numbers per leg for the headline; the whole leg is in the detail file"""
+    s = {}
+    for k in ("ms_per_step", "ms_per_sweep", "solve_latency_ms", "ffd_us_per_pop", "ms_per_call_pcie_inclusive",
+              "kernel_ms"):
+        if k in leg and leg[k] is not None:
+            v = leg[k]
+            s[k] = {a: _r(b) for a, b in v.items() if a != "trunc"} if isinstance(v, dict) else _r(v)
+    rf = leg.get("roofline")
+    if rf:
+        s["frac"] = _r(rf.get("frac"), 3)
+    cb = leg.get("cpu_baseline")
+    if cb:
+        s["cpu"] = _r(cb.get("solve_ms") or cb.get("ms_per_call") or cb.get("value"))
+        if "gpu_result_bit_exact" in cb:
+            s["cpu_exact"] = cb["gpu_result_bit_exact"]
+    for k in ("oracle_digest_equal", "shards_equal_whole"):
+        if leg.get(k) is not None:
+            s[k] = leg[k]
+    return s
+
+
+def headline(line):
+    """the driver's line: the contract keys, the K4 roofline on SURVEY §8(d)'s
+    claim-visit bytes (the unique-byte and L2 views beside it), the CPU
+    baseline, latency, and one small summary per leg; <= HEADLINE_MAX_BYTES"""
+    h = {k: line.get(k) for k in HEADLINE_KEYS}
+    for k in ("value", "ms_per_step", "solve_latency_ms", "ffd_us_per_pop"):
+        h[k] = _r(h[k], 6)
+    h["roofline"] = _compact_roofline(line.get("roofline"))
+    views = {}
+    for name, key in (("unique_hbm_bytes", "roofline_unique_bytes"), ("l2_claim_visits", "roofline_l2_claim_visits"),
+                      ("feasibility_kernel", "roofline_feasibility_kernel")):
+        rf = line.get(key)
+        if rf:
+            views[name] = {k: _r(rf.get(k)) for k in ("kernel", "bound", "achieved", "peak", "frac", "traffic",
+                                                      "algorithmic_bytes") if k in rf}
+    if views:
+        h["roofline_views"] = views
+    h["cpu_baseline"] = _compact_cpu(line.get("cpu_baseline"))
+    for k in ("solve_latency_phases_ms", "queue_pops", "new_nodeclaims", "pod_errors", "go_sort_emulation",
+              "device_kernel_ms"):
+        if line.get(k) is not None:
+            h[k] = line[k]
+    legs = {}
+    for grp in ("configs", "consolidation_legs"):
+        for name, leg in (line.get(grp) or {}).items():
+            legs[name] = _leg_summary(leg)
+    for name in ("stress", "create_filter", "ranking"):
+        if line.get(name):
+            legs[name] = _leg_summary(line[name])
+    if legs:
+        h["legs"] = legs
+    if line.get("detail_file"):
+        h["detail_file"] = line["detail_file"]
+    # shed detail (never the contract keys) until the line fits
+    for drop in ("legs", "roofline_views", "solve_latency_phases_ms", "go_sort_emulation", "device_kernel_ms"):
+        if len(json.dumps(h)) <= HEADLINE_MAX_BYTES:
+            break
+        h.pop(drop, None)
+    return h
+
+
+def emit(line, detail_path, rank):
+    """rank 0: the whole record to `detail_path`, one `# leg <name> {...}`
+    line per leg on stdout, then the compact headline as the LAST stdout line"""
+    if rank != 0:
+        return None
+    if detail_path:
+        d = os.path.dirname(detail_path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(detail_path, "w") as f:
+            json.dump(line, f, indent=1)
+        line["detail_file"] = os.path.relpath(detail_path, ROOT)
+    for grp in ("configs", "consolidation_legs"):
+        for name, leg in (line.get(grp) or {}).items():
+            print(f"# leg {name} " + json.dumps(leg))
+    for name in ("stress", "create_filter", "ranking"):
+        if line.get(name):
+            print(f"# leg {name} " + json.dumps(line[name]))
+    h = headline(line)
+    print(json.dumps(h), flush=True)
+    return h
+
+
 # ------------------------------------------------------------- Solve legs
 def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_over_ranks=None, traffic=None,
               leg=None):
@@ -179,12 +295,14 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         "ffd_candidates_scanned": int(res.cand_evals),
         "ffd_candidates_exact_checked": int(res.cand_full),
         "go_sort_emulation": {"fast": int(res.sorts_fast), "generic": int(res.sorts_generic)},
-        # unique HBM bytes (PMC-comparable); SURVEY §8(d)'s K4 figure (claim
-        # visits, LDS/L2-resident by design) priced against the L2; and the
-        # latency per pod §8(d) asks for
-        "roofline": roofline(names["ffd"], ffd_unique_bytes(res, n_types, min(8, len(np.unique(problem.quantities["resource"]))), len(out["claims"]),
-                                                            len(problem.nodes)),
-                             kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        # SURVEY §8(d)'s K4 figure (claim visits + request sums + node visits)
+        # priced against HBM; beside it the unique HBM bytes (PMC-comparable)
+        # and the claim visits priced against the L2 they are served from;
+        # and the latency per pod §8(d) asks for
+        "roofline": roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        "roofline_unique_bytes": roofline(names["ffd"], ffd_unique_bytes(
+            res, n_types, min(8, len(np.unique(problem.quantities["resource"]))), len(out["claims"]),
+            len(problem.nodes)), kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
         "roofline_l2_claim_visits": roofline(names["ffd"], ab["ffd"], kms["ffd"], None, L2_PEAK_GBS, "l2"),
         "ffd_us_per_pop": round(kms["ffd"] * 1e3 / max(int(res.pops), 1), 4),
         "roofline_feasibility_kernel": roofline("feas_cursor_kernel + feas_kernel", ab["feas"], kms["feas"],
@@ -651,6 +769,8 @@ def main():
                                                  "ranking (profiling passes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r3", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per leg (tools/pmc_traffic.py, committed under profiles/)")
+    ap.add_argument("--detail-json", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="the whole record (every leg); stdout's last line is the compact headline")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -802,8 +922,7 @@ def main():
     if _POOL is not None:
         _POOL.close()
         _POOL.join()
-    if rank == 0:
-        print(json.dumps(line))
+    emit(line, args.detail_json, rank)
     if dist is not None:
         dist.destroy_process_group()
 
