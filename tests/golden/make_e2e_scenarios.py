@@ -15,10 +15,16 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ZONES = ["us-south-1", "us-south-2", "us-south-3"]
-# GetMultipleInstanceTypes(3): the first three 2-4 vCPU / 4-16 GB profiles
-# (reference test/e2e/instance_discovery.go:39-66) of the fake catalog order
-# (pkg/fake/zz_generated_ibm_test_data.go:27-243)
-SMALL3 = ["bx2-2x8", "bx2-4x16", "cx2-2x4"]
+# GetMultipleInstanceTypes(n) (reference test/e2e/instance_discovery.go:39-66):
+# the first n of the 2-4 vCPU / 4-16 GB profiles sorted by vCPU, then memory,
+# then bx2 first, then name (filterSmallProfiles, instance_profiles.go:26-67),
+# over the fake catalog (pkg/fake/zz_generated_ibm_test_data.go:27-243)
+FAKE = [("bx2-2x8", 2, 8), ("bx2-4x16", 4, 16), ("bx2-8x32", 8, 32), ("cx2-2x4", 2, 4), ("cx2-4x8", 4, 8),
+        ("mx2-2x16", 2, 16), ("mx2-4x32", 4, 32), ("gx2-8x64x1v100", 8, 64)]
+SMALL = [n for n, v, m in sorted(((n, v, m) for n, v, m in FAKE if 2 <= v <= 4 and 4 <= m <= 16),
+                                 key=lambda x: (x[1], x[2], not x[0].startswith("bx2-"), x[0]))]
+SMALL3 = SMALL[:3]
+SMALL4 = SMALL[:4]
 IT = "node.kubernetes.io/instance-type"
 Z = "topology.kubernetes.io/zone"
 H = "kubernetes.io/hostname"
@@ -27,6 +33,17 @@ H = "kubernetes.io/hostname"
 TEST_NODEPOOL = {"requirements": [[IT, "In", SMALL3]]}
 # createMultiZoneNodePool (reference test/e2e/multizone_test.go:474-521)
 MULTIZONE_NODEPOOL = {"requirements": [[IT, "In", ["bx2-4x16", "bx2-2x8"]], [Z, "In", ZONES]]}
+# createTestNodePoolWithMultipleInstanceTypes (reference test/e2e/resources.go:311-368)
+MULTI_TYPE_NODEPOOL = {"requirements": [[IT, "In", SMALL4], ["kubernetes.io/arch", "In", ["amd64"]],
+                                        ["karpenter.sh/capacity-type", "In", ["on-demand"]]],
+                       "labels": {"provisioner": "karpenter-vpc", "cluster-type": "self-managed", "test": "e2e",
+                                  "test-name": "nodepool-instance-selection"}}
+# TestE2ETaintsBasicScheduling's NodePool (reference test/e2e/e2e_taints_test.go:495-531): one instance type
+# (GetMultipleInstanceTypes(t, 1)), a NoSchedule taint, template label test=<testName>.  The workload's own
+# comment sizes it for an 8 GB 2-vCPU profile (bx2a-2x8, :1106-1110): 1000m / 4Gi does not fit the first small
+# fake profile (cx2-2x4: 4 GB - 2.5 GiB calculateOverhead), so the fake catalog's 8 GB 2-vCPU profile stands in.
+TAINTED_NODEPOOL = {"requirements": [[IT, "In", ["bx2-2x8"]]], "labels": {"test": "basic-taints"},
+                    "taints": [["dedicated", "gpu-workload", "NoSchedule"]]}
 
 SCENARIOS = [
     {
@@ -79,6 +96,47 @@ SCENARIOS = [
         # (:152-156) the emptied nodes consolidate
         "expect": {"kind": "multi_node_then_consolidate", "app": "consolidation-pdb-app", "min_nodes": 2,
                    "scale_to": 2},
+    },
+    {
+        "id": "tainted_nodepool_tolerant_split",
+        "ref": "test/e2e/e2e_taints_test.go:458-611 (TestE2ETaintsBasicScheduling), workload :1074-1119",
+        "nodepool": TAINTED_NODEPOOL,
+        # createResourceIntensiveWorkload: 1 replica, 1000m / 4Gi; the tolerant one tolerates
+        # dedicated=gpu-workload:NoSchedule (Equal) and selects the template label; the intolerant one
+        # (created after the first is ready, :598-608) has neither and must stay pending
+        "workloads": [{"app": "tolerant-deployment", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "tolerations": [["dedicated", "Equal", "gpu-workload", "NoSchedule"]],
+                       "node_selector": {"test": "basic-taints"}},
+                      {"app": "intolerant-deployment", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "node_selector": {}}],
+        "arrival": "by_workload",
+        "expect": {"kind": "taint_split", "app": "tolerant-deployment", "pending_app": "intolerant-deployment",
+                   "taint": ["dedicated", "gpu-workload", "NoSchedule"]},
+    },
+    {
+        "id": "instance_types_within_allowed",
+        "ref": "test/e2e/basic_workflow_test.go:76-115 (TestE2ENodePoolInstanceTypeSelection), NodePool "
+               "resources.go:311-368, workload resources.go:548-623, assertion verification.go:102-132 and "
+               "verifyNodePoolRequirementsOnNodes :135-",
+        "nodepool": MULTI_TYPE_NODEPOOL,
+        # 2 replicas, 1500m / 2Gi, required hostname anti-affinity on their own app
+        "workloads": [{"app": "nodepool-instance-selection-workload", "replicas": 2, "cpu_m": 1500,
+                       "memory_mi": 2048, "anti_affinity": [{"key": H, "required": True}]}],
+        "arrival": "together",
+        "expect": {"kind": "types_within_allowed", "app": "nodepool-instance-selection-workload",
+                   "allowed": SMALL4, "n": 2},
+    },
+    {
+        "id": "zone_spread_survives_scale_up",
+        "ref": "test/e2e/multizone_test.go:384-431 (TestE2EZoneFailover), deployment :578-649",
+        "nodepool": MULTIZONE_NODEPOOL,
+        # 4 replicas of 500m / 512Mi with a preferred (weight 50) zone anti-affinity on their own app;
+        # once placed, the Deployment scales to 8 (:410-416) and the pods must still span > 1 zone (:425)
+        "workloads": [{"app": "zone-failover-app", "replicas": 4, "cpu_m": 500, "memory_mi": 512,
+                       "anti_affinity": [{"key": Z, "required": False, "weight": 50}]}],
+        "arrival": "scale",
+        "scale_to": 8,
+        "expect": {"kind": "min_zones", "app": "zone-failover-app", "min_zones": 2, "placed": 8},
     },
 ]
 

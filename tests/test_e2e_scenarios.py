@@ -12,6 +12,12 @@ its reference file:line:
   * multizone_test.go:83-174    preferred zone anti-affinity -> > 1 zone
   * scheduling_test.go:38-176   4 replicas, preferred hostname anti-affinity
                                 -> several nodes; scaled down, consolidation
+  * e2e_taints_test.go:458-611  tainted NodePool: the tolerating pod lands on
+                                its NodeClaim, the intolerant one stays pending
+  * basic_workflow_test.go:76-115  every NodeClaim's types within the
+                                NodePool's allowed list, its requirements met
+  * multizone_test.go:384-431   preferred zone anti-affinity, 4 -> 8 replicas:
+                                still more than one zone
 The CPU tests run every scenario through the oracle and assert the reference
 test's property; the GPU tests require both HIP Solve kernels (and the
 consolidation simulation kernel) to equal the oracle at every step, so the
@@ -69,12 +75,15 @@ class Cluster:
             req_terms = []
             if w.get("node_affinity_first_node_type"):
                 req_terms = [[(IT, "In", [self.first_type])]]
+            sel = w.get("node_selector", {"karpenter.sh/nodepool": NP})
+            tols = [tuple(t) for t in w.get("tolerations", [])]
             out.append(dict(uid=f"{w['app']}-{r:02d}", app=w["app"], cpu=w["cpu_m"], mem=w["memory_mi"] * MI * 1000,
-                            anti=anti, spreads=spreads, req_terms=req_terms, ts=len(self.pods) + len(out)))
+                            anti=anti, spreads=spreads, req_terms=req_terms, ts=len(self.pods) + len(out),
+                            sel=sel, tols=tols))
         return out
 
     def _add(self, b, p, node=None):
-        kw = dict(node_selector={"karpenter.sh/nodepool": NP}, required_terms=p["req_terms"],
+        kw = dict(node_selector=p["sel"], required_terms=p["req_terms"], tolerations=p["tols"],
                   labels={"app": p["app"], "test": "e2e"}, anti_affinity=p["anti"], spreads=p["spreads"])
         req = {"cpu": p["cpu"], "memory": p["mem"], "pods": 1000}
         ts = 1_700_000_000_000_000_000 + p["ts"] * 1_000_000_000
@@ -86,16 +95,21 @@ class Cluster:
     def problem(self, pending):
         b = ProblemBuilder()
         synth.build_catalog(b, synth.FAKE_PROFILES, ZONES, spot=False, prices=synth.price_table(synth.FAKE_PROFILES))
-        b.add_nodepool(NP, requirements=[tuple(r) for r in self.sc["nodepool"]["requirements"]])
+        npd = self.sc["nodepool"]
+        taints = [tuple(t) for t in npd.get("taints", [])]
+        b.add_nodepool(NP, requirements=[tuple(r) for r in npd["requirements"]], labels=npd.get("labels"),
+                       taints=taints)
         for k, n in enumerate(self.nodes):
             it = self.its[n["it"]]
-            labels = {r[0]: r[2][0] for r in it.requirements}
+            # a launched node carries the template's labels and taints (NodeClaimTemplate.ToNodeClaim)
+            labels = dict(npd.get("labels") or {})
+            labels.update({r[0]: r[2][0] for r in it.requirements})
             labels.update({Z: n["zone"], "karpenter.sh/capacity-type": "on-demand", "karpenter.sh/nodepool": NP,
                            H: n["name"]})
             alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
             used = {"cpu": sum(p["cpu"] for p in n["pods"]), "memory": sum(p["mem"] for p in n["pods"]),
                     "pods": 1000 * len(n["pods"])}
-            b.add_node(n["name"], labels, {r: alloc[r] - used.get(r, 0) for r in alloc})
+            b.add_node(n["name"], labels, {r: alloc[r] - used.get(r, 0) for r in alloc}, taints=taints)
         for k, n in enumerate(self.nodes):
             for p in n["pods"]:
                 self._add(b, p, node=k)
@@ -144,6 +158,14 @@ def run_scenario(sc, solvers=(), consolidator=None):
                 pending = errors + cl.make_pods(w, first=r, count=1)
                 res = _solve_all(cl.problem(pending), solvers)
                 errors = cl.launch(res, pending)
+    elif arrival == "scale":  # the replicas together, launched; then the Deployment scales up
+        for w in sc["workloads"]:
+            pending = cl.make_pods(w)
+            res = _solve_all(cl.problem(pending), solvers)
+            errors = cl.launch(res, pending)
+            pending = errors + cl.make_pods(w, first=w["replicas"], count=sc["scale_to"] - w["replicas"])
+            res = _solve_all(cl.problem(pending), solvers)
+            errors = cl.launch(res, pending)
     else:  # by_workload: each deployment after the previous one launched
         for w in sc["workloads"]:
             pending = cl.make_pods(w)
@@ -187,6 +209,28 @@ def check_expectation(sc, cl, res, pending, consolidator=None):
     elif e["kind"] == "min_zones":
         zones = {n["zone"] for n in cl.nodes if any(p["app"] == app for p in n["pods"])}
         assert len(zones) >= e["min_zones"]
+        if "placed" in e:
+            assert sum(p["app"] == app for n in cl.nodes for p in n["pods"]) == e["placed"]
+    elif e["kind"] == "taint_split":
+        # by_workload: the tolerant deployment launched a node of the tainted pool; the
+        # intolerant pod was solved last (res/pending) and found no NodePool or node
+        tol_nodes = [n for n in cl.nodes if any(p["app"] == app for p in n["pods"])]
+        assert len(tol_nodes) == 1
+        assert [pending[i]["app"] for i in res["errors"]] == [e["pending_app"]]
+        assert not res["claims"] and not any(res["nodes"])
+    elif e["kind"] == "types_within_allowed":
+        assert not res["errors"]
+        claims = _app_claims(res, pending, app)
+        assert len(claims) == e["n"]
+        names = [cl.its[k].name for k in range(len(cl.its))]
+        allowed = set(e["allowed"])
+        for c in claims:
+            assert c["its"] and {names[i] for i in c["its"]} <= allowed
+            lines = {ln.split("|")[0]: ln.split("|") for ln in c["requirements"].split("\n") if ln}
+            for key, op, vals in sc["nodepool"]["requirements"]:
+                if key == IT:
+                    continue  # FinalizeScheduling rewrites it as the ordered options
+                assert lines[key][1] == op and set(lines[key][2].split(",")) <= set(vals), (key, lines.get(key))
     elif e["kind"] == "multi_node_then_consolidate":
         assert not res["errors"]
         assert len(_app_claims(res, pending, app)) >= e["min_nodes"]

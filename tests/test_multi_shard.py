@@ -138,9 +138,7 @@ def test_rccl_shards():
         s = lib.Solver(shard_devices=[0, 0], flags=abi.GS_CFG_RCCL)
     except lib.GpuSchedError as e:
         assert e.status == abi.GS_E_RCCL
-        print("RCCL refused the repeated device: GS_E_RCCL")
-        return
-    print("RCCL accepted the repeated device: all-reduce path")
+        pytest.skip("RCCL refused the repeated device (GS_E_RCCL): the all-reduce path did not run")
     one = lib.Solver()
     try:
         p = synth.make_c3(n_pods=2000)
@@ -154,3 +152,39 @@ def test_rccl_shards():
     finally:
         s.close()
         one.close()
+
+
+def _hip_device_count():
+    import ctypes
+    n = ctypes.c_int(0)
+    ctypes.CDLL("libamdhip64.so").hipGetDeviceCount(ctypes.byref(n))
+    return n.value
+
+
+@pytest.mark.parametrize("flags", [0, abi.GS_CFG_RCCL], ids=["peer", "rccl"])
+@pytest.mark.parametrize("make", [lambda: synth.make_c3(n_pods=2000), lambda: synth.make_c5(n_pods=5000)],
+                         ids=["c3", "c5"])
+def test_distinct_devices_equal_single(single, make, flags):
+    """shards on DISTINCT devices [0, 1], so the merge kernel reads
+    the other shard's slice over xGMI peer access (and, with GS_CFG_RCCL, the
+    RCCL all-reduce runs between two real ranks); the merged device matrix and
+    the consolidation commands equal one device's.  Skipped on a one-GPU box."""
+    if _hip_device_count() < 2:
+        pytest.skip("one visible device: the peer-read / RCCL path needs two")
+    from gpusched import lib
+    s = lib.Solver(shard_devices=[0, 1], flags=flags)
+    try:
+        p = make()
+        single.prepare(p)
+        s.prepare(p)
+        W = single.feasibility_shard_device(0, 0).words
+        for lo, hi in ((0, W), (W // 3, max(W // 3 + 1, W - 1))):
+            want = _device_result(single, lo, hi)
+            got = _device_result(s, lo, hi)
+            for a, b in zip(got[:3], want[:3]):
+                assert torch_equal(a, b)
+        c = synth.make_c4(n_nodes=60, n_pending=4, seed=3, util=(0.9, 0.99), full_frac=0.5, big_frac=1.0, pack=True)
+        cands = list(range(len(c.nodes)))
+        assert s.consolidate(ConsolidationInput(c, cands))[:3] == single.consolidate(ConsolidationInput(c, cands))[:3]
+    finally:
+        s.close()
