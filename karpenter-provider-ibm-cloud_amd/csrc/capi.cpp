@@ -155,16 +155,30 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.zone_order, e.zone_order);
   c->upload(d.zone_cat, e.zone_cat);
   c->upload(d.hn0, e.hn0);
-  if (sims && e.TGH && e.NN) {
-    // node-major copy: a simulation's overlay entry and its candidates'
-    // exclusion read every group of one node (one contiguous row, not TGH
-    // lines strided by NN)
-    std::vector<int32_t> nm((size_t)e.NN * e.TGH);
+  if (sims && (e.TGH || e.TGZ) && e.NN) {
+    // each node's nonzero counts, node-major sparse: a simulation excludes its
+    // candidates' pods by reading their few entries (the dense
+    // node row was ~TGH x 4 B per simulation on the e2e shape)
+    std::vector<uint32_t> off(e.NN + 1, 0);
+    for (uint32_t g = 0; g < e.TGZ; g++)
+      for (uint32_t n = 0; n < e.NN; n++) off[n + 1] += e.zn_cnt[(size_t)g * e.NN + n] != 0;
     for (uint32_t g = 0; g < e.TGH; g++)
-      for (uint32_t n = 0; n < e.NN; n++) nm[(size_t)n * e.TGH + g] = e.hn0[(size_t)g * e.NN + n];
-    c->upload(d.hn0_nm, nm);
+      for (uint32_t n = 0; n < e.NN; n++) off[n + 1] += e.hn0[(size_t)g * e.NN + n] != 0;
+    for (uint32_t n = 0; n < e.NN; n++) off[n + 1] += off[n];
+    std::vector<uint64_t> sp(std::max<uint32_t>(off[e.NN], 1));
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    auto put = [&](uint32_t g, int32_t c, uint32_t n) { sp[fill[n]++] = (uint64_t)g << 32 | (uint32_t)c; };
+    for (uint32_t g = 0; g < e.TGZ; g++)
+      for (uint32_t n = 0; n < e.NN; n++)
+        if (int32_t c = e.zn_cnt[(size_t)g * e.NN + n]) put(g, c, n);
+    for (uint32_t g = 0; g < e.TGH; g++)
+      for (uint32_t n = 0; n < e.NN; n++)
+        if (int32_t c = e.hn0[(size_t)g * e.NN + n]) put(e.TGZ + g, c, n);
+    c->upload(d.nsp_off, off);
+    c->upload(d.nsp, sp);
   } else {
-    d.hn0_nm = d.hn0;  // not read outside simulations
+    d.nsp_off = nullptr;
+    d.nsp = nullptr;
   }
   c->alloc(d.hn, e.hn0.size());
   c->upload(d.nodes0, e.nodes);
@@ -214,8 +228,9 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->alloc(d.ov_req, (size_t)sims->blocks * d.ov_cap * gsd::RMAX);
     c->alloc(d.ov_fk, (size_t)sims->blocks * d.ov_cap * F1);
     // the general (topology / volumes / minValues) simulation variant
-    c->alloc(d.ov_hn, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1));
-    c->alloc(d.ov_hmask, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>((e.TGH + 31) / 32, 1));
+    c->alloc_zero(d.ov_hn, (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1));
+    c->ov_hn_bytes = (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1) * sizeof(uint64_t);
+    d.ov_epoch = 0;
     c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
     c->alloc(d.ov_map, (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
     {
@@ -223,7 +238,6 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
       known.resize(std::max<size_t>(NS, 1), 0);
       c->upload(d.sim_known, known);
     }
-    c->upload(d.zn_cnt, e.zn_cnt);
     c->alloc(d.slot_its, e.any_mv ? CA * 60 : 1);
     c->alloc(d.slot_nits, e.any_mv ? CA : 1);
     c->alloc(d.slot_drop, e.any_mv ? CA : 1);
@@ -674,7 +688,7 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     }
     if (l.target >= M) return fail(c, GS_E_HIP, "corrupt add log");
     cp[l.target].push_back(l.pod);
-    for (auto& kv : e.variants[l.var].reqs) gsh::reqs_add(e, creq[l.target], kv.first, kv.second);
+    for (auto& kv : e.variants[e.var_sv[l.var]].reqs) gsh::reqs_add(e, creq[l.target], kv.first, kv.second);
   }
   c->claim_nodepool.assign(M, 0);
   c->claim_pod_offsets.assign(1, 0);

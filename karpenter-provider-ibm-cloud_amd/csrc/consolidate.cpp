@@ -304,6 +304,10 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     sp.max_pods = std::max<uint32_t>(sp.max_pods, (uint32_t)merged.size());
     sp.ov_cap = std::max<uint32_t>(sp.ov_cap, (uint32_t)(merged.size() + sp.sets[s].size()));
   }
+  if (sp.evaluated.size() >= (1u << 20) - 1u) {
+    *err = "more than 1,048,574 simulations in one call";
+    return GS_E_CAPACITY;
+  }
   if (sp.max_pods > 0xFFFFu) {
     *err = "a simulation holds more than 65535 pods";
     return GS_E_CAPACITY;
@@ -325,7 +329,7 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt, general ? 1u : 0u);
   sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
   // per-block overlays of hostname counts: at most 1 GiB (fewer persistent blocks otherwise)
-  const size_t ov_row = (size_t)std::max<uint32_t>(sp.ov_cap, 1) * e.TGH * sizeof(int32_t);
+  const size_t ov_row = (size_t)std::max<uint32_t>(sp.ov_cap, 1) * e.TGH * sizeof(uint64_t);
   if (ov_row) sp.blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(sp.blocks, (size_t)(1u << 30) / ov_row));
   return GS_OK;
 }
@@ -349,6 +353,13 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (NS) {
       HIPCHK(hipMemsetAsync(d.sim_next, 0, sizeof(uint32_t), c->stream));
+      // a fresh overlay stamp prefix per launch; cells of 4,095 launches ago
+      // could match again, so the cells are cleared when the prefix wraps
+      d.ov_epoch = (d.ov_epoch + 1u) & 0xFFFu;
+      if (!d.ov_epoch) {
+        if (c->ov_hn_bytes) HIPCHK(hipMemsetAsync(d.ov_hn, 0, c->ov_hn_bytes, c->stream));
+        d.ov_epoch = 1;
+      }
       HIPCHK(gsk_ffd(&d, sp.blocks, c->stream));
     }
     HIPCHK(hipEventRecord(c->ev[2], c->stream));

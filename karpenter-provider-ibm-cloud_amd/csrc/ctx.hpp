@@ -169,14 +169,21 @@ struct gs_ctx {
     void** dst;
     size_t off, bytes;
     std::vector<char> host;
+    bool zero = false;
   };
   std::vector<Planned> plan;
   size_t plan_bytes = 0;
+  size_t ov_hn_bytes = 0;  // the simulation overlay cells (cleared when the stamp prefix wraps)
   template <class P>
   void alloc(P*& dst, size_t n) {
     const size_t b = std::max<size_t>(n, 1) * sizeof(P);
     plan.push_back(Planned{(void**)&dst, plan_bytes, b, {}});
     plan_bytes += (b + 255) & ~(size_t)255;
+  }
+  template <class P>
+  void alloc_zero(P*& dst, size_t n) {
+    alloc(dst, n);
+    plan.back().zero = true;
   }
   template <class P, class T>
   void upload(P*& dst, const std::vector<T>& v) {
@@ -216,6 +223,7 @@ inline void gs_ctx::commit() {
   for (auto& q : plan) {
     *q.dst = (char*)base + q.off;
     if (!q.host.empty()) HIPCHK(hipMemcpyAsync(*q.dst, q.host.data(), q.host.size(), hipMemcpyHostToDevice, stream));
+    if (q.zero) HIPCHK(hipMemsetAsync(*q.dst, 0, q.bytes, stream));
   }
   HIPCHK(hipStreamSynchronize(stream));
   plan.clear();

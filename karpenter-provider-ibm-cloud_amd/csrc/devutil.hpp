@@ -1,6 +1,6 @@
 // devutil.hpp — device helpers shared by the gfx950 kernels: wave64
 // reductions, (zone x capacity-type) grid masks and the free-key requirement
-// algebra (<U> scheduling.Requirement on <= 64-value vocabularies).
+// algebra (<U> scheduling.Requirement on <= 256-value vocabularies).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -38,9 +38,15 @@ __device__ __forceinline__ uint64_t grid_of(uint64_t zm, uint64_t cm, uint32_t Z
 }
 
 // ------------------------------------------------- free-key requirement ops
+__device__ __forceinline__ bool fk_any(const uint64_t* w) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < FKW; i++) x |= w[i];
+  return x != 0;
+}
 __device__ __forceinline__ bool fk_exempt(const FK& q) {
   // Operator() in {NotIn, DoesNotExist}
-  return (q.flags & FK_COMP) ? (q.excl != 0) : (q.has == 0);
+  return (q.flags & FK_COMP) ? fk_any(q.excl) : !fk_any(q.has);
 }
 
 // <U> Requirements.Compatible for one free key (AllowUndefinedWellKnownLabels)
@@ -55,13 +61,17 @@ __device__ __forceinline__ bool fk_compatible(const FK& c, const FK& p, bool wel
     if ((c.flags & FK_LT) && (p.flags & FK_LT)) lt = c.lt < p.lt ? c.lt : p.lt;
     len0 = hg && hl && gt >= lt;
   } else {
-    len0 = (c.has & p.has) == 0;
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < FKW; i++) x |= c.has[i] & p.has[i];
+    len0 = x == 0;
   }
   return !len0 || (fk_exempt(c) && fk_exempt(p));
 }
 
-// <U> Requirement.Intersection for one free key
-__device__ FK fk_intersect(const FK& a, const FK& b, const int64_t* ival, uint64_t isint) {
+// <U> Requirement.Intersection for one free key; ival [FKV], isint [FKW]
+// (the key's vocabulary: integer values and which entries are integers)
+__device__ FK fk_intersect(const FK& a, const FK& b, const int64_t* ival, const uint64_t* isint) {
   FK r;
   r.pad = 0;
   bool comp = (a.flags & FK_COMP) && (b.flags & FK_COMP);
@@ -71,31 +81,32 @@ __device__ FK fk_intersect(const FK& a, const FK& b, const int64_t* ival, uint64
   int64_t lt = (a.flags & FK_LT) ? a.lt : b.lt;
   if ((a.flags & FK_LT) && (b.flags & FK_LT)) lt = a.lt < b.lt ? a.lt : b.lt;
   if (hg && hl && gt >= lt) {
-    r.has = 0;
-    r.excl = 0;
+    for (int i = 0; i < FKW; i++) r.has[i] = r.excl[i] = 0;
     r.gt = r.lt = 0;
     r.flags = FK_PRESENT;
     return r;
   }
-  r.has = a.has & b.has;
+  for (int i = 0; i < FKW; i++) r.has[i] = a.has[i] & b.has[i];
   if (comp) {
-    uint64_t w = ~0ull;
-    if (hg || hl) {
-      w = 0;
-      for (int i = 0; i < 64; i++) {
-        if (!((isint >> i) & 1)) continue;
-        int64_t x = ival[i];
-        if (hg && gt >= x) continue;
-        if (hl && lt <= x) continue;
-        w |= 1ull << i;
+    for (int k = 0; k < FKW; k++) {
+      uint64_t w = ~0ull;
+      if (hg || hl) {
+        w = 0;
+        for (int i = 0; i < 64; i++) {
+          if (!((isint[k] >> i) & 1)) continue;
+          int64_t x = ival[k * 64 + i];
+          if (hg && gt >= x) continue;
+          if (hl && lt <= x) continue;
+          w |= 1ull << i;
+        }
       }
+      r.excl[k] = (a.excl[k] | b.excl[k]) & w;
     }
-    r.excl = (a.excl | b.excl) & w;
     r.gt = hg ? gt : 0;
     r.lt = hl ? lt : 0;
     r.flags = FK_PRESENT | FK_COMP | (hg ? FK_GT : 0) | (hl ? FK_LT : 0);
   } else {
-    r.excl = 0;
+    for (int i = 0; i < FKW; i++) r.excl[i] = 0;
     r.gt = r.lt = 0;
     r.flags = FK_PRESENT;
   }

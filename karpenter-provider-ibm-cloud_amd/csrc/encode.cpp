@@ -12,7 +12,11 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <climits>
+#include <cstdlib>
+#include <exception>
+#include <thread>
 #include <functional>
 #include <tuple>
 #include <cmath>
@@ -20,6 +24,7 @@
 #include <numeric>
 #include <set>
 #include <stdexcept>
+#include <system_error>
 #include <string_view>
 
 namespace gsh {
@@ -31,6 +36,53 @@ const char* kHostname = "kubernetes.io/hostname";
 const char* kNodePool = "karpenter.sh/nodepool";
 const char* kPNS = "PreferNoSchedule";
 const char* kOmega = "\x01<unmentioned>";
+
+// host threads of the encoder: GS_ENCODE_THREADS, else the hardware's, at
+// most 16 (a shared host's share; the GPU boxes give a process 16)
+uint32_t enc_threads() {
+  static const uint32_t n = [] {
+    if (const char* s = std::getenv("GS_ENCODE_THREADS")) {
+      const int v = std::atoi(s);
+      if (v >= 1) return (uint32_t)std::min(v, 64);
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (uint32_t)std::max(1u, std::min(hw ? hw : 1u, 16u));
+  }();
+  return n;
+}
+
+// f(i) for every i in [0, n), chunks of `grain` handed out to up to
+// enc_threads() threads; f must not throw (callers keep per-item errors and
+// raise the first by index afterwards, as the serial encoder would)
+template <class F>
+void par_for(uint32_t n, uint32_t grain, F&& f) {
+  grain = std::max<uint32_t>(grain, 1);
+  const uint32_t T = std::min<uint32_t>(enc_threads(), (n + grain - 1) / grain);
+  if (T <= 1) {
+    for (uint32_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  auto work = [&] {
+    for (;;) {
+      const uint32_t b = next.fetch_add(grain);
+      if (b >= n) break;
+      const uint32_t e = std::min(n, b + grain);
+      for (uint32_t i = b; i < e; i++) f(i);
+    }
+  };
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (uint32_t t = 1; t < T; t++) {
+    try {
+      th.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;  // fewer threads: the atomic counter still covers every chunk
+    }
+  }
+  work();
+  for (auto& t : th) t.join();
+}
 
 // <U> v1.WellKnownLabels + IBM keys (reference pkg/apis/v1alpha1/labels.go:37-45)
 bool is_wellknown(const std::string& k) {
@@ -225,10 +277,28 @@ struct Ctx {
   // may repeat a string under several ids)
   std::vector<uint32_t> canon;
   void build_canon() {
-    canon.resize(strs.size());
-    std::unordered_map<std::string_view, uint32_t> first;
-    first.reserve(strs.size() * 2);
-    for (uint32_t i = 0; i < strs.size(); i++) canon[i] = first.emplace(std::string_view(strs[i]), i).first->second;
+    const uint32_t n = (uint32_t)strs.size();
+    canon.resize(n);
+    // strings hashed in parallel, then each shard's first-id map built by its
+    // own thread over its ids in ascending order
+    const uint32_t SH = 64;
+    std::vector<uint64_t> hs(n);
+    par_for(n, 4096, [&](uint32_t i) { hs[i] = std::hash<std::string_view>{}(std::string_view(strs[i])); });
+    std::vector<uint32_t> cnt(SH + 1, 0), ids(n);
+    for (uint32_t i = 0; i < n; i++) cnt[hs[i] % SH + 1]++;
+    for (uint32_t k = 0; k < SH; k++) cnt[k + 1] += cnt[k];
+    {
+      std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+      for (uint32_t i = 0; i < n; i++) ids[fill[hs[i] % SH]++] = i;
+    }
+    par_for(SH, 1, [&](uint32_t k) {
+      std::unordered_map<std::string_view, uint32_t> first;
+      first.reserve((cnt[k + 1] - cnt[k]) * 2);
+      for (uint32_t x = cnt[k]; x < cnt[k + 1]; x++) {
+        const uint32_t i = ids[x];
+        canon[i] = first.emplace(std::string_view(strs[i]), i).first->second;
+      }
+    });
   }
   uint32_t C(uint32_t id) const {
     if (id >= canon.size()) throw Fail{GS_E_INVALID, "string id out of range"};
@@ -746,8 +816,7 @@ struct Ctx {
   };
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
-  std::vector<std::string> pod_ns;
-  std::vector<PodSel> pod_sel;  // pending pods
+  std::vector<PodSel> pod_sel;  // per pod spec (spec_of)
   std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
   uint32_t bound_alias = gsd::NONE;  // bound pod b is also pod bound_alias + b (consolidation)
 
@@ -985,6 +1054,7 @@ struct Ctx {
     e.pod_vfresh.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
     for (uint32_t i = 0; i < e.P; i++) {
       const gs_pod& pd = p->pods[i];
+      if (!pd.volumes.count) continue;
       std::set<std::pair<std::string, std::string>> mine;
       for (uint32_t k = 0; k < pd.volumes.count; k++) mine.insert(volkey(p->volumes[pd.volumes.begin + k]));
       for (auto& vk : mine) {
@@ -1120,30 +1190,41 @@ struct Ctx {
         }
       }
     }
-    // per pod: the selection list (shared by its variants), then each
-    // variant's own list with the self flag
+    // per spec: the selection list (shared by its pods' variants), then each
+    // spec variant's own list with the self flag; a pod's variants point at
+    // its spec's lists
     e.tg_list.clear();
     std::vector<uint8_t> selected(e.TG, 0);
     std::vector<uint32_t> mine;
-    for (uint32_t i = 0; i < e.P; i++) {
-      six.candidates(pod_sel[i], &cand);
+    const uint32_t NS = (uint32_t)spec_rep.size();
+    std::vector<uint32_t> sel_off(NS), sel_n(NS), own_off(e.variants.size()), own_n(e.variants.size());
+    for (uint32_t s = 0; s < NS; s++) {
+      six.candidates(pod_sel[s], &cand);
       mine.clear();
       for (uint32_t g : cand)
-        if (group_counts(groups[g], pod_sel[i])) mine.push_back(g);
-      const uint32_t so = (uint32_t)e.tg_list.size();
+        if (group_counts(groups[g], pod_sel[s])) mine.push_back(g);
+      sel_off[s] = (uint32_t)e.tg_list.size();
+      sel_n[s] = (uint32_t)mine.size();
       for (uint32_t g : mine) {
         selected[g] = 1;
         e.tg_list.push_back(e.tgroups[g].slot | (e.tgroups[g].kind << 24));
       }
-      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
-        gsd::VarRec& vr = e.vars[v];
-        vr.sel_off = so;
-        vr.sel_n = (uint32_t)mine.size();
-        vr.own_off = (uint32_t)e.tg_list.size();
-        for (uint32_t g : e.variants[v].own) e.tg_list.push_back(g | (selected[g] ? gsd::TL_SELF : 0u));
-        vr.own_n = (uint32_t)e.variants[v].own.size();
+      for (uint32_t sv = sv_begin[s]; sv < sv_begin[s] + sv_count[s]; sv++) {
+        own_off[sv] = (uint32_t)e.tg_list.size();
+        for (uint32_t g : e.variants[sv].own) e.tg_list.push_back(g | (selected[g] ? gsd::TL_SELF : 0u));
+        own_n[sv] = (uint32_t)e.variants[sv].own.size();
       }
       for (uint32_t g : mine) selected[g] = 0;
+    }
+    for (uint32_t i = 0; i < e.P; i++) {
+      const uint32_t s = spec_of[i];
+      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
+        gsd::VarRec& vr = e.vars[v];
+        vr.sel_off = sel_off[s];
+        vr.sel_n = sel_n[s];
+        vr.own_off = own_off[e.var_sv[v]];
+        vr.own_n = own_n[e.var_sv[v]];
+      }
     }
     if (e.tg_list.empty()) e.tg_list.push_back(0);
   }
@@ -1179,8 +1260,10 @@ struct Ctx {
   }
   gsd::FK to_fk(const KReq& q) const {
     gsd::FK f{};
-    f.has = q.has.w.empty() ? 0 : q.has.w[0];
-    f.excl = q.excl.w.empty() ? 0 : q.excl.w[0];
+    for (int i = 0; i < gsd::FKW; i++) {
+      f.has[i] = i < (int)q.has.w.size() ? q.has.w[i] : 0;
+      f.excl[i] = i < (int)q.excl.w.size() ? q.excl.w[i] : 0;
+    }
     f.gt = q.gt;
     f.lt = q.lt;
     f.flags = gsd::FK_PRESENT | (q.comp ? gsd::FK_COMP : 0) | (q.hg ? gsd::FK_GT : 0) | (q.hl ? gsd::FK_LT : 0);
@@ -1365,20 +1448,21 @@ struct Ctx {
   void build_free_slots() {
     for (uint32_t k = 0; k < e.keys.size(); k++) {
       if (e.keys[k].cls != KEY_FREE) continue;
-      if (e.keys[k].vocab.size() > 64) throw Fail{GS_E_UNSUPPORTED, "free key vocabulary > 63 values: " + e.keys[k].name};
+      if (e.keys[k].vocab.size() > (size_t)gsd::FKV)
+        throw Fail{GS_E_UNSUPPORTED, "free key vocabulary > 255 values: " + e.keys[k].name};
       if (e.free_keys.size() >= (size_t)gsd::FMAX) throw Fail{GS_E_UNSUPPORTED, "more than 16 free requirement keys"};
       e.keys[k].slot = (int)e.free_keys.size();
       if (e.keys[k].wellknown) e.wk_slots |= 1ull << e.free_keys.size();
       e.free_keys.push_back(k);
     }
     e.F = (uint32_t)e.free_keys.size();
-    e.fk_ival.assign((size_t)std::max<uint32_t>(e.F, 1) * 64, 0);
-    e.fk_isint.assign(std::max<uint32_t>(e.F, 1), 0);
+    e.fk_ival.assign((size_t)std::max<uint32_t>(e.F, 1) * gsd::FKV, 0);
+    e.fk_isint.assign((size_t)std::max<uint32_t>(e.F, 1) * gsd::FKW, 0);
     for (uint32_t s = 0; s < e.F; s++) {
       auto& v = e.keys[e.free_keys[s]].vocab;
       for (uint32_t i = 0; i < v.size(); i++) {
-        e.fk_ival[(size_t)s * 64 + i] = v.ival[i];
-        if (v.isint[i]) e.fk_isint[s] |= 1ull << i;
+        e.fk_ival[(size_t)s * gsd::FKV + i] = v.ival[i];
+        if (v.isint[i]) e.fk_isint[(size_t)s * gsd::FKW + i / 64] |= 1ull << (i % 64);
       }
     }
     e.t_fk.assign((size_t)e.T * std::max<uint32_t>(e.F, 1), gsd::FK{});
@@ -1388,25 +1472,393 @@ struct Ctx {
           e.t_fk[(size_t)t * e.F + e.keys[kv.first].slot] = to_fk(kv.second);
   }
 
+  // A pod's spec as bytes: everything but its uid, creation time, requests
+  // and volumes (canonical string ids, so equal text is equal bytes).  Pods
+  // with equal bytes have the same variants, groups and selection lists
+  // (Deployments: thousands of replicas, one spec).  false: a range or id is
+  // out of bounds (the pod is its own spec; its encode raises the error).
+  bool pod_sig(const gs_pod& pd, std::vector<uint32_t>& out) const {
+    auto u32 = [&](uint32_t x) { out.push_back(x); };
+    auto sid = [&](uint32_t id) {
+      if (id >= canon.size()) return false;
+      u32(canon[id]);
+      return true;
+    };
+    auto rng = [&](gs_range r, uint32_t n) { return (uint64_t)r.begin + r.count <= n; };
+    auto labels = [&](gs_range r) {
+      if (!rng(r, p->n_labels)) return false;
+      u32(r.count);
+      for (uint32_t k = 0; k < r.count; k++)
+        if (!sid(p->labels[r.begin + k].key) || !sid(p->labels[r.begin + k].value)) return false;
+      return true;
+    };
+    auto vids = [&](gs_range r) {
+      if (!rng(r, p->n_value_ids)) return false;
+      u32(r.count);
+      for (uint32_t k = 0; k < r.count; k++)
+        if (!sid(p->value_ids[r.begin + k])) return false;
+      return true;
+    };
+    auto reqs = [&](gs_range r) {
+      if (!rng(r, p->n_reqs)) return false;
+      u32(r.count);
+      for (uint32_t k = 0; k < r.count; k++) {
+        const gs_requirement& q = p->reqs[r.begin + k];
+        if (!sid(q.key)) return false;
+        u32(q.op);
+        u32((uint32_t)q.min_values);
+        if (!vids(q.values)) return false;
+      }
+      return true;
+    };
+    auto terms = [&](gs_range r) {
+      if (!rng(r, p->n_terms)) return false;
+      u32(r.count);
+      for (uint32_t k = 0; k < r.count; k++) {
+        u32((uint32_t)p->terms[r.begin + k].weight);
+        if (!reqs(p->terms[r.begin + k].requirements)) return false;
+      }
+      return true;
+    };
+    auto aff = [&](gs_range r) {
+      if (!rng(r, p->n_affinity_terms)) return false;
+      u32(r.count);
+      for (uint32_t k = 0; k < r.count; k++) {
+        const gs_affinity_term& q = p->affinity_terms[r.begin + k];
+        if (!sid(q.topology_key)) return false;
+        u32(q.required);
+        u32((uint32_t)q.weight);
+        u32(q.has_selector);
+        u32(q.has_ns_selector);
+        if (!labels(q.match_labels) || !reqs(q.match_expressions) || !vids(q.namespaces) ||
+            !labels(q.ns_match_labels) || !reqs(q.ns_match_expressions))
+          return false;
+      }
+      return true;
+    };
+    out.clear();
+    u32(pd.flags);
+    if (!sid(pd.ns) || !labels(pd.node_selector) || !terms(pd.required_terms) || !terms(pd.preferred_terms) ||
+        !labels(pd.labels) || !rng(pd.tolerations, p->n_tolerations) || !rng(pd.spreads, p->n_spreads) ||
+        !rng(pd.host_ports, p->n_host_ports))
+      return false;
+    u32(pd.tolerations.count);
+    for (uint32_t k = 0; k < pd.tolerations.count; k++) {
+      const gs_toleration& t = p->tolerations[pd.tolerations.begin + k];
+      u32(t.op);
+      if (!sid(t.key) || !sid(t.value) || !sid(t.effect)) return false;
+    }
+    u32(pd.spreads.count);
+    for (uint32_t k = 0; k < pd.spreads.count; k++) {
+      const gs_spread& q = p->spreads[pd.spreads.begin + k];
+      if (!sid(q.topology_key)) return false;
+      u32((uint32_t)q.max_skew);
+      u32(q.when_unsatisfiable);
+      u32((uint32_t)q.min_domains);
+      u32(q.has_selector);
+      u32(q.node_affinity_policy);
+      u32(q.node_taints_policy);
+      if (!labels(q.match_labels) || !reqs(q.match_expressions) || !vids(q.match_label_keys)) return false;
+    }
+    if (!aff(pd.anti_affinity) || !aff(pd.affinity)) return false;
+    u32(pd.host_ports.count);
+    for (uint32_t k = 0; k < pd.host_ports.count; k++) {
+      const gs_host_port& h = p->host_ports[pd.host_ports.begin + k];
+      u32((uint32_t)h.port);
+      if (!sid(h.protocol) || !sid(h.ip)) return false;
+    }
+    return true;
+  }
+
+  // Per-spec encode work.  Phase A (parallel over specs) builds everything
+  // the spec determines; phase B (serial, in the order pods first carry each
+  // spec) assigns topology group ids, numbered in the order pods first name
+  // them; phase C (parallel) builds the Relax variants.  An error is the
+  // serial encoder's: the first failing pod's.
+  struct GroupKey {
+    std::string key;
+    GroupEnc g;
+    bool required = false;
+    int32_t weight = 0;
+  };
+  struct PodWork {
+    std::exception_ptr err;
+    Reqs ns;
+    std::vector<Reqs> req_terms;
+    std::vector<std::pair<int32_t, Reqs>> pref;
+    std::vector<SpreadEnc> sps;
+    std::vector<std::string> sp_hash;
+    std::vector<GroupKey> g_anti, g_aff, g_inv, g_port;  // in the order the pod names them
+    std::vector<Tol> tols;
+    std::vector<uint32_t> sgid, own_static;
+    std::vector<std::pair<int32_t, uint32_t>> anti_pref, aff_pref;  // (weight, group)
+    std::vector<PodVariant> vars;
+    std::vector<std::vector<Tol>> var_tols;
+  };
+  // pods -> specs: spec_of[pod], spec_rep[spec] (its first pod), and per spec
+  // its variants' range in e.variants (sv_begin / sv_count)
+  std::vector<uint32_t> spec_of, spec_rep, sv_begin, sv_count;
+
+  void pod_phase_a(uint32_t i, PodWork& w, const std::map<std::string, AntiEnc>& inv_terms, bool topo_inputs) {
+    auto& pd = p->pods[i];
+    w.ns = labels_reqs(pd.node_selector);
+    for (uint32_t k = 0; k < pd.required_terms.count; k++) {
+      no_min_values(p->terms[pd.required_terms.begin + k].requirements);
+      w.req_terms.push_back(reqs_of(p->terms[pd.required_terms.begin + k].requirements));
+    }
+    for (uint32_t k = 0; k < pd.preferred_terms.count; k++) {
+      auto& tm = p->terms[pd.preferred_terms.begin + k];
+      no_min_values(tm.requirements);
+      w.pref.push_back({tm.weight, reqs_of(tm.requirements)});
+    }
+    if (w.pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred node-affinity terms"};
+    // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
+    std::stable_sort(w.pref.begin(), w.pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+    // topology spread constraints -> groups (owners); namespace / labels for selectors
+    const std::string& pns = S(pd.ns);
+    chk(pd.labels, p->n_labels, "labels");
+    w.sps = spreads_of(pd);
+    if (!w.sps.empty() && (pd.node_selector.count || pd.required_terms.count))
+      for (auto& sp : w.sps)
+        if (!sp.ignore_aff)
+          throw Fail{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
+    for (auto& sp : w.sps) w.sp_hash.push_back(sp.hash(pns));
+    // anti-affinity, inverse anti-affinity and host-port groups
+    if (topo_inputs) {
+      const PodSel& me = pod_sel[spec_of[i]];
+      for (auto& a : antis_of(pd)) {
+        const bool self = a.selects(me.ns, me.labels);
+        GroupEnc g = host_group(1, self, a.sel.key);
+        g.anti = a;
+        w.g_anti.push_back(GroupKey{"A|" + a.hash() + (self ? "|s" : "|n"), std::move(g), a.required, a.weight});
+      }
+      for (auto& a : terms_of(pd, pd.affinity, true)) {
+        GroupEnc g = host_group(4, false);
+        g.anti = a;
+        w.g_aff.push_back(GroupKey{"F|" + a.hash(), std::move(g), a.required, a.weight});
+      }
+      for (auto& kv : inv_terms) {
+        if (!kv.second.selects(me.ns, me.labels)) continue;
+        const bool self = me.carried.count(kv.first) != 0;
+        GroupEnc g = host_group(2, self, kv.second.sel.key);
+        g.inv_hash = kv.first;
+        w.g_inv.push_back(GroupKey{"I|" + kv.first + (self ? "|s" : "|n"), std::move(g)});
+      }
+      for (auto& pe : me.ports) {
+        GroupEnc g = host_group(3, true);
+        g.port = pe;
+        w.g_port.push_back(GroupKey{"P|" + pe.key(), std::move(g)});
+      }
+    }
+    chk(pd.tolerations, p->n_tolerations, "tolerations");
+    for (uint32_t k = 0; k < pd.tolerations.count; k++) {
+      auto& t = p->tolerations[pd.tolerations.begin + k];
+      w.tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
+    }
+  }
+
+  void pod_phase_b(uint32_t i, PodWork& w) {
+    const std::string pns = S(p->pods[i].ns);
+    for (size_t k = 0; k < w.sps.size(); k++) {
+      auto f = group_idx.find(w.sp_hash[k]);
+      if (f == group_idx.end()) {
+        if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
+        f = group_idx.emplace(w.sp_hash[k], (uint32_t)groups.size()).first;
+        groups.push_back(GroupEnc{w.sps[k], pns});
+      }
+      w.sgid.push_back(f->second);
+    }
+    for (auto& gk : w.g_anti) {
+      const uint32_t gid = group_id(gk.key, std::move(gk.g));
+      if (gk.required) w.own_static.push_back(gid);
+      else w.anti_pref.push_back({gk.weight, gid});
+    }
+    if (w.anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
+    for (auto& gk : w.g_aff) {
+      const uint32_t gid = group_id(gk.key, std::move(gk.g));
+      if (gk.required) w.own_static.push_back(gid);
+      else w.aff_pref.push_back({gk.weight, gid});
+    }
+    if (w.aff_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
+    // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
+    std::stable_sort(w.aff_pref.begin(), w.aff_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+    std::stable_sort(w.anti_pref.begin(), w.anti_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
+    for (auto& gk : w.g_inv) w.own_static.push_back(group_id(gk.key, std::move(gk.g)));
+    for (auto& gk : w.g_port) w.own_static.push_back(group_id(gk.key, std::move(gk.g)));
+    // the first variant owns every group (later ones only drop groups)
+    std::vector<uint32_t> own = w.sgid;
+    own.insert(own.end(), w.own_static.begin(), w.own_static.end());
+    for (auto& x : w.anti_pref) own.push_back(x.second);
+    for (auto& x : w.aff_pref) own.push_back(x.second);
+    std::sort(own.begin(), own.end());
+    if (std::unique(own.begin(), own.end()) - own.begin() > (ptrdiff_t)gsd::OWNMAX)
+      throw Fail{GS_E_UNSUPPORTED, "a pod owns more than 64 topology groups"};
+    w.g_anti.clear();
+    w.g_aff.clear();
+    w.g_inv.clear();
+    w.g_port.clear();
+  }
+
+  // <U> NewPodRequirements + Preferences.Relax: every variant of one spec
+  void pod_phase_c(PodWork& w) {
+    std::vector<uint32_t> cur(w.sps.size());  // current constraints (swap-remove order)
+    std::iota(cur.begin(), cur.end(), 0);
+    std::vector<Tol> tols = w.tols;
+    size_t ri = 0, pi = 0, ai = 0, fi = 0;
+    for (;;) {
+      // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
+      PodVariant v;
+      v.reqs = w.ns;
+      v.strict = w.ns;
+      if (pi < w.pref.size()) reqs_add_all(e, v.reqs, w.pref[pi].second);
+      if (ri < w.req_terms.size()) {
+        reqs_add_all(e, v.reqs, w.req_terms[ri]);
+        reqs_add_all(e, v.strict, w.req_terms[ri]);
+      }
+      v.tol = tol_mask(tols);
+      for (uint32_t k : cur) v.own.push_back(w.sgid[k]);
+      v.own.insert(v.own.end(), w.own_static.begin(), w.own_static.end());
+      for (size_t k = ai; k < w.anti_pref.size(); k++) v.own.push_back(w.anti_pref[k].second);
+      for (size_t k = fi; k < w.aff_pref.size(); k++) v.own.push_back(w.aff_pref[k].second);
+      std::sort(v.own.begin(), v.own.end());
+      v.own.erase(std::unique(v.own.begin(), v.own.end()), v.own.end());
+      w.vars.push_back(std::move(v));
+      w.var_tols.push_back(tols);
+      // <U> Preferences.Relax
+      if (w.req_terms.size() - ri > 1) {
+        ri++;
+        continue;
+      }
+      // removePreferredPodAffinityTerm, then ...AntiAffinityTerm (the heaviest)
+      if (fi < w.aff_pref.size()) {
+        fi++;
+        continue;
+      }
+      if (ai < w.anti_pref.size()) {
+        ai++;
+        continue;
+      }
+      if (pi < w.pref.size()) {
+        pi++;
+        continue;
+      }
+      // removeTopologySpreadScheduleAnyway: swap-remove the first one
+      bool removed = false;
+      for (size_t k = 0; k < cur.size() && !removed; k++)
+        if (w.sps[cur[k]].sa) {
+          cur[k] = cur.back();
+          cur.pop_back();
+          removed = true;
+        }
+      if (removed) continue;
+      if (tolerate_pns) {
+        bool has = false;
+        for (auto& t : tols)
+          if (t.k.empty() && t.op == GS_TOL_EXISTS && t.v.empty() && t.eff == kPNS) has = true;
+        if (!has) {
+          tols.push_back({"", "", kPNS, GS_TOL_EXISTS});
+          continue;
+        }
+      }
+      break;
+    }
+  }
+
   void build_pods() {
     e.P = p->n_pods;
-    std::vector<uint8_t> uid_seen(strs.size(), 0);
-    e.variants.reserve((size_t)e.P + (e.P >> 2));
     e.pod_req.assign((size_t)e.P * e.R, 0);
-    std::vector<int64_t> cpu(e.P, 0), mem(e.P, 0);
-    auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
+    // pods -> specs (first-carrier order): a 64-bit hash of each pod's spec
+    // bytes in parallel, specs numbered by first hash occurrence, then every
+    // pod's bytes compared with its spec's first pod's (a hash collision
+    // falls back to an exact map over the bytes)
+    spec_of.assign(e.P, 0);
+    spec_rep.clear();
+    {
+      auto mix = [](const std::vector<uint32_t>& v) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ v.size();
+        for (uint32_t x : v) {
+          h ^= x;
+          h *= 0xFF51AFD7ED558CCDull;
+          h ^= h >> 32;
+        }
+        return h;
+      };
+      std::vector<uint64_t> hs(e.P);
+      std::vector<uint8_t> ok(e.P, 0);
+      par_for(e.P, 1024, [&](uint32_t i) {
+        thread_local std::vector<uint32_t> buf;
+        buf.clear();
+        ok[i] = pod_sig(p->pods[i], buf);
+        hs[i] = mix(buf);
+      });
+      std::unordered_map<uint64_t, uint32_t> first;
+      first.reserve(256);
+      for (uint32_t i = 0; i < e.P; i++) {
+        if (!ok[i]) {
+          spec_of[i] = (uint32_t)spec_rep.size();
+          spec_rep.push_back(i);
+          continue;
+        }
+        auto f = first.emplace(hs[i], (uint32_t)spec_rep.size());
+        if (f.second) spec_rep.push_back(i);
+        spec_of[i] = f.first->second;
+      }
+      std::vector<uint8_t> clash(e.P, 0);
+      par_for(e.P, 1024, [&](uint32_t i) {
+        const uint32_t r = spec_rep[spec_of[i]];
+        if (r == i) return;
+        thread_local std::vector<uint32_t> a, b;
+        a.clear();
+        b.clear();
+        pod_sig(p->pods[i], a);
+        pod_sig(p->pods[r], b);
+        clash[i] = a != b;
+      });
+      std::map<std::vector<uint32_t>, uint32_t> exact;  // specs a collision split off
+      for (uint32_t i = 0; i < e.P; i++) {
+        if (!clash[i]) continue;
+        std::vector<uint32_t> a;
+        pod_sig(p->pods[i], a);
+        auto f = exact.emplace(std::move(a), (uint32_t)spec_rep.size());
+        if (f.second) spec_rep.push_back(i);
+        spec_of[i] = f.first->second;
+      }
+      // specs numbered in first-carrier order (a collision's spec was appended)
+      std::vector<uint32_t> order(spec_rep.size());
+      std::iota(order.begin(), order.end(), 0);
+      std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return spec_rep[x] < spec_rep[y]; });
+      std::vector<uint32_t> rank(spec_rep.size());
+      for (uint32_t k = 0; k < order.size(); k++) rank[order[k]] = k;
+      std::vector<uint32_t> rep2(spec_rep.size());
+      for (uint32_t k = 0; k < order.size(); k++) rep2[k] = spec_rep[order[k]];
+      spec_rep.swap(rep2);
+      for (uint32_t i = 0; i < e.P; i++) spec_of[i] = rank[spec_of[i]];
+    }
+    const uint32_t NS = (uint32_t)spec_rep.size();
     // <U> the inverse anti-affinity groups: required terms of pending and
     // bound pods (Topology.updateInverseAntiAffinity / updateInverseAffinities)
     // a problem without spreads, affinity terms or host ports builds no
-    // group: the per-pod selection state (labels, carried terms) is skipped
+    // group: the per-spec selection state (labels, carried terms) is skipped
     const bool topo_inputs = p->n_spreads || p->n_affinity_terms || p->n_host_ports;
     std::map<std::string, AntiEnc> inv_terms;
     if (topo_inputs) {
-      pod_sel.reserve(e.P);
-      for (uint32_t i = 0; i < e.P; i++) {
-        pod_sel.push_back(sel_of(p->pods[i]));
-        for (auto& a : antis_of(p->pods[i]))
-          if (a.required) inv_terms.emplace(a.hash(), a);
+      pod_sel.assign(NS, PodSel{});
+      std::vector<std::vector<AntiEnc>> req_antis(NS);
+      std::vector<std::exception_ptr> serr(NS);
+      par_for(NS, 8, [&](uint32_t s) {
+        try {
+          pod_sel[s] = sel_of(p->pods[spec_rep[s]]);
+          for (auto& a : antis_of(p->pods[spec_rep[s]]))
+            if (a.required) req_antis[s].push_back(std::move(a));
+        } catch (...) {
+          serr[s] = std::current_exception();
+        }
+      });
+      // specs in first-carrier order: the first error and the first-inserted
+      // term are the serial encoder's
+      for (uint32_t s = 0; s < NS; s++) {
+        if (serr[s]) std::rethrow_exception(serr[s]);
+        for (auto& a : req_antis[s]) inv_terms.emplace(a.hash(), a);
       }
       chk(gs_range{0, p->n_bound_pods}, p->n_bound_pods, "bound pods");
       for (uint32_t b = 0; b < p->n_bound_pods; b++)
@@ -1419,159 +1871,90 @@ struct Ctx {
         chk(p->pods[i].host_ports, p->n_host_ports, "host_ports");
       }
     }
+    // the first pod whose uid an earlier pod carries (or names no string)
+    uint32_t dup_at = e.P;
+    bool dup_bad_id = false;
+    {
+      std::vector<uint8_t> uid_seen(strs.size(), 0);
+      for (uint32_t i = 0; i < e.P && dup_at == e.P; i++) {
+        if (p->pods[i].uid >= canon.size()) {
+          dup_at = i;
+          dup_bad_id = true;
+          break;
+        }
+        const uint32_t cu = canon[p->pods[i].uid];
+        if (uid_seen[cu]) dup_at = i;
+        uid_seen[cu] = 1;
+      }
+    }
+    // requests per pod, the spec's work per spec
+    std::vector<std::exception_ptr> rerr(e.P);
+    par_for(e.P, 1024, [&](uint32_t i) {
+      try {
+        resvec_fn(p->pods[i].requests, &e.pod_req[(size_t)i * e.R], nullptr);
+      } catch (...) {
+        rerr[i] = std::current_exception();
+      }
+    });
+    std::vector<PodWork> work(NS);
+    par_for(NS, 8, [&](uint32_t s) {
+      const uint32_t i = spec_rep[s];
+      if (p->pods[i].flags || i >= dup_at) return;
+      try {
+        pod_phase_a(i, work[s], inv_terms, topo_inputs);
+      } catch (...) {
+        work[s].err = std::current_exception();
+      }
+    });
     for (uint32_t i = 0; i < e.P; i++) {
-      auto& pd = p->pods[i];
-      if (pd.flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
-      const uint32_t cu = C(pd.uid);
-      if (uid_seen[cu]) throw Fail{GS_E_INVALID, "duplicate pod uid"};
-      uid_seen[cu] = 1;
-      resvec_fn(pd.requests, &e.pod_req[(size_t)i * e.R], nullptr);
+      if (p->pods[i].flags) throw Fail{GS_E_UNSUPPORTED, "pod topology spread / pod affinity / host ports / volumes"};
+      if (i == dup_at) throw Fail{GS_E_INVALID, dup_bad_id ? "string id out of range" : "duplicate pod uid"};
+      if (rerr[i]) std::rethrow_exception(rerr[i]);
+      const uint32_t s = spec_of[i];
+      if (spec_rep[s] != i) continue;
+      if (work[s].err) std::rethrow_exception(work[s].err);
+      pod_phase_b(i, work[s]);
+    }
+    par_for(NS, 8, [&](uint32_t s) {
+      try {
+        pod_phase_c(work[s]);
+      } catch (...) {
+        work[s].err = std::current_exception();
+      }
+    });
+    for (uint32_t s = 0; s < NS; s++)
+      if (work[s].err) std::rethrow_exception(work[s].err);
+    // spec variants (e.variants), then the device variants: each pod's
+    // spec's variants in order (e.var_sv: device variant -> spec variant)
+    sv_begin.assign(NS, 0);
+    sv_count.assign(NS, 0);
+    for (uint32_t s = 0; s < NS; s++) {
+      sv_begin[s] = (uint32_t)e.variants.size();
+      sv_count[s] = (uint32_t)work[s].vars.size();
+      for (auto& v : work[s].vars) e.variants.push_back(std::move(v));
+      for (auto& t : work[s].var_tols) variant_tols.push_back(std::move(t));
+    }
+    e.var_begin.resize(e.P);
+    e.var_count.resize(e.P);
+    uint32_t nv = 0;
+    for (uint32_t i = 0; i < e.P; i++) {
+      e.var_begin[i] = nv;
+      e.var_count[i] = sv_count[spec_of[i]];
+      nv += e.var_count[i];
+    }
+    e.var_sv.resize(nv);
+    par_for(e.P, 2048, [&](uint32_t i) {
+      const uint32_t b = sv_begin[spec_of[i]];
+      for (uint32_t k = 0; k < e.var_count[i]; k++) e.var_sv[e.var_begin[i] + k] = b + k;
+    });
+    std::vector<int64_t> cpu(e.P, 0), mem(e.P, 0);
+    auto rc = rid_map.find("cpu"), rmm = rid_map.find("memory");
+    for (uint32_t i = 0; i < e.P; i++) {
       if (rc != rid_map.end()) cpu[i] = e.pod_req[(size_t)i * e.R + rc->second];
       if (rmm != rid_map.end()) mem[i] = e.pod_req[(size_t)i * e.R + rmm->second];
-      // spec pieces
-      Reqs ns = labels_reqs(pd.node_selector);
-      std::vector<Reqs> req_terms;
-      for (uint32_t k = 0; k < pd.required_terms.count; k++) {
-        no_min_values(p->terms[pd.required_terms.begin + k].requirements);
-        req_terms.push_back(reqs_of(p->terms[pd.required_terms.begin + k].requirements));
-      }
-      std::vector<std::pair<int32_t, Reqs>> pref;
-      for (uint32_t k = 0; k < pd.preferred_terms.count; k++) {
-        auto& tm = p->terms[pd.preferred_terms.begin + k];
-        no_min_values(tm.requirements);
-        pref.push_back({tm.weight, reqs_of(tm.requirements)});
-      }
-      if (pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred node-affinity terms"};
-      // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
-      std::stable_sort(pref.begin(), pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
-      // topology spread constraints -> groups (owners); namespace / labels for selectors
-      pod_ns.push_back(S(pd.ns));
-      chk(pd.labels, p->n_labels, "labels");
-      const std::vector<SpreadEnc> sps = spreads_of(pd);
-      if (!sps.empty() && (pd.node_selector.count || pd.required_terms.count))
-        for (auto& sp : sps)
-          if (!sp.ignore_aff)
-            throw Fail{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
-      std::vector<uint32_t> sgid;
-      for (auto& sp : sps) {
-        const std::string h = sp.hash(pod_ns.back());
-        auto f = group_idx.find(h);
-        if (f == group_idx.end()) {
-          if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
-          f = group_idx.emplace(h, (uint32_t)groups.size()).first;
-          groups.push_back(GroupEnc{sp, pod_ns.back()});
-        }
-        sgid.push_back(f->second);
-      }
-      std::vector<uint32_t> cur(sps.size());  // current constraints (swap-remove order)
-      std::iota(cur.begin(), cur.end(), 0);
-      // anti-affinity, inverse anti-affinity and host-port groups
-      std::vector<uint32_t> own_static;
-      std::vector<std::pair<int32_t, uint32_t>> anti_pref, aff_pref;  // (weight, group)
-      if (topo_inputs) {
-      const PodSel& me = pod_sel[i];
-      for (auto& a : antis_of(pd)) {
-        const bool self = a.selects(me.ns, me.labels);
-        GroupEnc g = host_group(1, self, a.sel.key);
-        g.anti = a;
-        const uint32_t gid = group_id("A|" + a.hash() + (self ? "|s" : "|n"), std::move(g));
-        if (a.required) own_static.push_back(gid);
-        else anti_pref.push_back({a.weight, gid});
-      }
-      if (anti_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred anti-affinity terms"};
-      for (auto& a : terms_of(pd, pd.affinity, true)) {
-        GroupEnc g = host_group(4, false);
-        g.anti = a;
-        const uint32_t gid = group_id("F|" + a.hash(), std::move(g));
-        if (a.required) own_static.push_back(gid);
-        else aff_pref.push_back({a.weight, gid});
-      }
-      if (aff_pref.size() > 12) throw Fail{GS_E_UNSUPPORTED, "more than 12 preferred pod affinity terms"};
-      std::stable_sort(aff_pref.begin(), aff_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
-      // sort.Slice by weight desc on <= 12 elements is insertion sort: stable
-      std::stable_sort(anti_pref.begin(), anti_pref.end(), [](auto& a, auto& b) { return a.first > b.first; });
-      for (auto& kv : inv_terms) {
-        if (!kv.second.selects(me.ns, me.labels)) continue;
-        const bool self = me.carried.count(kv.first) != 0;
-        GroupEnc g = host_group(2, self, kv.second.sel.key);
-        g.inv_hash = kv.first;
-        own_static.push_back(group_id("I|" + kv.first + (self ? "|s" : "|n"), std::move(g)));
-      }
-      for (auto& pe : me.ports) {
-        GroupEnc g = host_group(3, true);
-        g.port = pe;
-        own_static.push_back(group_id("P|" + pe.key(), std::move(g)));
-      }
-      }
-      chk(pd.tolerations, p->n_tolerations, "tolerations");
-      std::vector<Tol> tols;
-      for (uint32_t k = 0; k < pd.tolerations.count; k++) {
-        auto& t = p->tolerations[pd.tolerations.begin + k];
-        tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
-      }
-      e.var_begin.push_back((uint32_t)e.variants.size());
-      size_t ri = 0, pi = 0, ai = 0, fi = 0;
-      for (;;) {
-        // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
-        PodVariant v;
-        v.reqs = ns;
-        v.strict = ns;
-        if (pi < pref.size()) reqs_add_all(e, v.reqs, pref[pi].second);
-        if (ri < req_terms.size()) {
-          reqs_add_all(e, v.reqs, req_terms[ri]);
-          reqs_add_all(e, v.strict, req_terms[ri]);
-        }
-        v.tol = tol_mask(tols);
-        for (uint32_t k : cur) v.own.push_back(sgid[k]);
-        v.own.insert(v.own.end(), own_static.begin(), own_static.end());
-        for (size_t k = ai; k < anti_pref.size(); k++) v.own.push_back(anti_pref[k].second);
-        for (size_t k = fi; k < aff_pref.size(); k++) v.own.push_back(aff_pref[k].second);
-        std::sort(v.own.begin(), v.own.end());
-        v.own.erase(std::unique(v.own.begin(), v.own.end()), v.own.end());
-        if (v.own.size() > (size_t)gsd::OWNMAX) throw Fail{GS_E_UNSUPPORTED, "a pod owns more than 64 topology groups"};
-        e.variants.push_back(std::move(v));
-        variant_tols.push_back(tols);
-        // <U> Preferences.Relax
-        if (req_terms.size() - ri > 1) {
-          ri++;
-          continue;
-        }
-        // removePreferredPodAffinityTerm, then ...AntiAffinityTerm (the heaviest)
-        if (fi < aff_pref.size()) {
-          fi++;
-          continue;
-        }
-        if (ai < anti_pref.size()) {
-          ai++;
-          continue;
-        }
-        if (pi < pref.size()) {
-          pi++;
-          continue;
-        }
-        // removeTopologySpreadScheduleAnyway: swap-remove the first one
-        bool removed = false;
-        for (size_t k = 0; k < cur.size() && !removed; k++)
-          if (sps[cur[k]].sa) {
-            cur[k] = cur.back();
-            cur.pop_back();
-            removed = true;
-          }
-        if (removed) continue;
-        if (tolerate_pns) {
-          bool has = false;
-          for (auto& t : tols)
-            if (t.k.empty() && t.op == GS_TOL_EXISTS && t.v.empty() && t.eff == kPNS) has = true;
-          if (!has) {
-            tols.push_back({"", "", kPNS, GS_TOL_EXISTS});
-            continue;
-          }
-        }
-        break;
-      }
-      e.var_count.push_back((uint32_t)e.variants.size() - e.var_begin.back());
     }
-    e.V = (uint32_t)e.variants.size();
+    { std::vector<PodWork>().swap(work); }
+    e.V = nv;
     // device variant records; identical has-bitsets share one arena slot and
     // identical IT-key requirement sets one class
     e.vars.resize(e.V);
@@ -1586,57 +1969,68 @@ struct Ctx {
       arena_slot.emplace(words, off);
       return off;
     };
-    for (uint32_t i = 0; i < e.P; i++)
-      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
-        auto& pv = e.variants[v];
-        gsd::VarRec& vr = e.vars[v];
-        std::memset(&vr, 0, sizeof vr);
-        vr.pod = i;
-        for (int k = 0; k < gsd::KMAX_IT; k++) vr.itmask_off[k] = gsd::NONE;
-        bool itk = false;
-        for (uint32_t k = 0; k < e.K; k++) {
-          auto f = pv.reqs.find(e.it_keys[k]);
-          if (f == pv.reqs.end()) continue;
-          vr.itmask_off[k] = arena(f->second.has.w);
-          itk = true;
-        }
-        if (itk) {
-          // the class key: the arena slots of the constrained keys
-          std::vector<uint64_t> sig(vr.itmask_off, vr.itmask_off + e.K);
-          auto f = itclass_of.find(sig);
-          if (f == itclass_of.end()) {
-            f = itclass_of.emplace(sig, (uint32_t)class_offs.size()).first;
-            class_offs.emplace_back(vr.itmask_off, vr.itmask_off + e.K);
-          }
-          e.var_itclass[v] = f->second;
-        }
-        vr.zfull_off = vr.cfull_off = gsd::NONE;
-        for (int kk = 0; kk < 2; kk++) {
-          auto f = pv.reqs.find(kk ? e.k_ct : e.k_zone);
-          if (f == pv.reqs.end()) continue;
-          (kk ? vr.cfull_off : vr.zfull_off) = arena(f->second.has.w);
-        }
-        vr.zm = zone_has(pv.reqs);
-        vr.cm = ct_has(pv.reqs);
-        vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && pv.own.empty() ? gsd::VF_SIMPLE : 0u);
-        vr.zs = zone_full(pv.strict);
-        vr.zn = zone_full(pv.reqs);
-        vr.zflags = zone_flags(pv.reqs);
-        vr.vix = v;
-        vr.tol = pv.tol;
-        vr.tolt = 0;
-        for (uint32_t t = 0; t < e.T; t++)
-          if ((e.tmpl[t].taints & ~pv.tol) == 0) vr.tolt |= 1ull << t;
-        vr.fk_begin = (uint32_t)e.fk_entries.size();
-        for (auto& kv : pv.reqs)
-          if (e.keys[kv.first].cls == KEY_FREE) {
-            gsd::FKEntry fe{};
-            fe.slot = (uint32_t)e.keys[kv.first].slot;
-            fe.st = to_fk(kv.second);
-            e.fk_entries.push_back(fe);
-          }
-        vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
+    // one record per spec variant (serial: arena slots, classes and free-key
+    // entries in first-use order), then every device variant a copy of its
+    // spec variant's with its pod and index
+    const uint32_t SV = (uint32_t)e.variants.size();
+    std::vector<gsd::VarRec> sv_rec(SV);
+    std::vector<uint32_t> sv_itclass(SV, gsd::NONE);
+    for (uint32_t sv = 0; sv < SV; sv++) {
+      auto& pv = e.variants[sv];
+      gsd::VarRec& vr = sv_rec[sv];
+      std::memset(&vr, 0, sizeof vr);
+      for (int k = 0; k < gsd::KMAX_IT; k++) vr.itmask_off[k] = gsd::NONE;
+      bool itk = false;
+      for (uint32_t k = 0; k < e.K; k++) {
+        auto f = pv.reqs.find(e.it_keys[k]);
+        if (f == pv.reqs.end()) continue;
+        vr.itmask_off[k] = arena(f->second.has.w);
+        itk = true;
       }
+      if (itk) {
+        // the class key: the arena slots of the constrained keys
+        std::vector<uint64_t> sig(vr.itmask_off, vr.itmask_off + e.K);
+        auto f = itclass_of.find(sig);
+        if (f == itclass_of.end()) {
+          f = itclass_of.emplace(sig, (uint32_t)class_offs.size()).first;
+          class_offs.emplace_back(vr.itmask_off, vr.itmask_off + e.K);
+        }
+        sv_itclass[sv] = f->second;
+      }
+      vr.zfull_off = vr.cfull_off = gsd::NONE;
+      for (int kk = 0; kk < 2; kk++) {
+        auto f = pv.reqs.find(kk ? e.k_ct : e.k_zone);
+        if (f == pv.reqs.end()) continue;
+        (kk ? vr.cfull_off : vr.zfull_off) = arena(f->second.has.w);
+      }
+      vr.zm = zone_has(pv.reqs);
+      vr.cm = ct_has(pv.reqs);
+      vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && pv.own.empty() ? gsd::VF_SIMPLE : 0u);
+      vr.zs = zone_full(pv.strict);
+      vr.zn = zone_full(pv.reqs);
+      vr.zflags = zone_flags(pv.reqs);
+      vr.tol = pv.tol;
+      vr.tolt = 0;
+      for (uint32_t t = 0; t < e.T; t++)
+        if ((e.tmpl[t].taints & ~pv.tol) == 0) vr.tolt |= 1ull << t;
+      vr.fk_begin = (uint32_t)e.fk_entries.size();
+      for (auto& kv : pv.reqs)
+        if (e.keys[kv.first].cls == KEY_FREE) {
+          gsd::FKEntry fe{};
+          fe.slot = (uint32_t)e.keys[kv.first].slot;
+          fe.st = to_fk(kv.second);
+          e.fk_entries.push_back(fe);
+        }
+      vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
+    }
+    par_for(e.P, 1024, [&](uint32_t i) {
+      for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
+        e.vars[v] = sv_rec[e.var_sv[v]];
+        e.vars[v].pod = i;
+        e.vars[v].vix = v;
+        e.var_itclass[v] = sv_itclass[e.var_sv[v]];
+      }
+    });
     if (e.itmask.empty()) e.itmask.push_back(0);
     e.itclass_mask.assign(std::max<size_t>(class_offs.size(), 1) * e.W, 0);
     for (size_t c = 0; c < class_offs.size(); c++)
@@ -1660,19 +2054,37 @@ struct Ctx {
       uint32_t i;
     };
     std::vector<QK> qk(e.P);
-    for (uint32_t i = 0; i < e.P; i++) {
-      const std::string& u = S(p->pods[i].uid);
+    par_for(e.P, 4096, [&](uint32_t i) {
+      const std::string& u = strs[p->pods[i].uid];  // checked by the uid pass
       uint64_t x = 0;
       for (size_t b = 0; b < 8; b++) x = (x << 8) | (b < u.size() ? (uint8_t)u[b] : 0u);
       qk[i] = QK{cpu[i], mem[i], p->pods[i].creation_ns, x, i};
-    }
-    std::sort(qk.begin(), qk.end(), [&](const QK& a, const QK& b) {
+    });
+    auto qless = [&](const QK& a, const QK& b) {
       if (a.cpu != b.cpu) return a.cpu > b.cpu;
       if (a.mem != b.mem) return a.mem > b.mem;
       if (a.ts != b.ts) return a.ts < b.ts;
       if (a.u8 != b.u8) return a.u8 < b.u8;
       return strs[p->pods[a.i].uid] < strs[p->pods[b.i].uid];
-    });
+    };
+    // a total order (uids are unique): chunks sorted in parallel, then merged
+    // pairwise; the result is the one order whatever the split
+    {
+      const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>(enc_threads(), e.P / 8192));
+      std::vector<uint32_t> cut(T + 1);
+      for (uint32_t t = 0; t <= T; t++) cut[t] = (uint32_t)((uint64_t)e.P * t / T);
+      par_for(T, 1, [&](uint32_t t) { std::sort(qk.begin() + cut[t], qk.begin() + cut[t + 1], qless); });
+      std::vector<QK> tmp(e.P);
+      for (uint32_t w = 1; w < T; w *= 2) {
+        std::vector<uint32_t> pairs;
+        for (uint32_t t = 0; t + w < T; t += 2 * w) pairs.push_back(t);
+        par_for((uint32_t)pairs.size(), 1, [&](uint32_t k) {
+          const uint32_t t = pairs[k], a = cut[t], m = cut[t + w], b = cut[std::min(T, t + 2 * w)];
+          std::merge(qk.begin() + a, qk.begin() + m, qk.begin() + m, qk.begin() + b, tmp.begin() + a, qless);
+          std::copy(tmp.begin() + a, tmp.begin() + b, qk.begin() + a);
+        });
+      }
+    }
     e.queue0.resize(e.P);
     for (uint32_t k = 0; k < e.P; k++) e.queue0[k] = qk[k].i;
     e.checks = (uint64_t)e.P * e.checks_per_pod;
@@ -1734,7 +2146,9 @@ struct Ctx {
     }
     // taints of nodes enter the vocabulary after the pods' tolerations were
     // encoded: recompute the tolerated masks over the final vocabulary
-    for (uint32_t v = 0; v < e.V; v++) e.vars[v].tol = tol_mask(variant_tols[v]);
+    std::vector<uint64_t> sv_tol(variant_tols.size());
+    for (size_t sv = 0; sv < variant_tols.size(); sv++) sv_tol[sv] = tol_mask(variant_tols[sv]);
+    for (uint32_t v = 0; v < e.V; v++) e.vars[v].tol = sv_tol[e.var_sv[v]];
   }
 };
 
@@ -1781,8 +2195,10 @@ Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
   Ctx c{p, e, {}};
   c.bound_alias = bound_alias;
   try {
-    c.strs.reserve(p->n_strings);
-    for (uint32_t i = 0; i < p->n_strings; i++) c.strs.push_back(p->strings[i] ? p->strings[i] : "");
+    c.strs.resize(p->n_strings);
+    par_for(p->n_strings, 4096, [&](uint32_t i) {
+      if (p->strings[i]) c.strs[i] = p->strings[i];
+    });
     c.build_canon();
     c.build_vocab();
     c.build_catalog();

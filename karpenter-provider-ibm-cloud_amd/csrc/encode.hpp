@@ -118,6 +118,7 @@ struct Encoded {
   std::vector<gsd::FK> t_fk;
   std::vector<int64_t> pod_req;
   std::vector<uint32_t> var_begin, var_count, queue0;
+  std::vector<uint32_t> var_sv;  // [V] device variant -> its spec variant (index into `variants`)
   std::vector<gsd::VarRec> vars;
   std::vector<uint64_t> itmask;
   // variants with IT-key requirements, deduplicated by those requirements:
@@ -148,7 +149,7 @@ struct Encoded {
   std::vector<int32_t> zone_nodes;   // [64]
   // host-only, for decode
   std::vector<Reqs> tmpl_reqs;  // incl. hostname In[omega]
-  std::vector<PodVariant> variants;
+  std::vector<PodVariant> variants;  // per spec variant: pods with equal specs share them (var_sv)
 };
 
 // status + message

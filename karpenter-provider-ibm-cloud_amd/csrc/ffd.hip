@@ -599,7 +599,6 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   uint32_t* s_nb = (uint32_t*)((char*)lds64 + ((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u);  // SIM: touched nodes
   // SIM: a touched node's overlay entry (| OV_EXCL: a removed candidate), valid where its s_nb bit is set
   uint32_t* const ov_map = SIM ? d.ov_map + (size_t)blockIdx.x * d.NN : nullptr;
-  const uint32_t HW = (d.TGH + 31u) >> 5;  // words of an overlay entry's counted-group mask
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
@@ -631,6 +630,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
     const uint32_t sim = S.sim;
     if (sim >= (SIM ? d.n_sims : 1u)) break;  // block-uniform: every wave leaves
     const uint32_t qoff = SIM ? d.sim_pod_off[sim] : 0u;
+    // SIM: this simulation's overlay stamp (launch epoch, simulation)
+    const uint32_t ov_stamp = (d.ov_epoch << 20) | (sim + 1u);
     const uint32_t P = SIM ? d.sim_pod_off[sim + 1] - qoff : d.P;
     const uint32_t MCs = SIM ? P : MC;  // claim arena of this solve (one claim per pod at most)
     uint32_t* const queue = d.queue + qoff;
@@ -669,16 +670,18 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       if (TOPO) {
         // SimulateScheduling reschedules the candidates' pods: Topology
         // excludes them from the counts (excludedPods)
-        const uint32_t ng = d.TGZ + d.TGH;
-        for (uint32_t x = tid; x < ncand * ng; x += FB) {
-          const uint32_t n = d.sim_cands[c0 + x / ng], g = x % ng;
-          if (g < d.TGZ) {
-            const int32_t c = d.zn_cnt[(size_t)g * d.NN + n];
-            const uint32_t z = d.nodes0[n].zvid;
-            if (c && z < d.ZS) atomicSub(&ts.zcnt[g * d.ZS + z], c);
-          } else {
-            const int32_t c = d.hn0_nm[(size_t)n * d.TGH + (g - d.TGZ)];
-            if (c) atomicSub(&ts.htot[g - d.TGZ], c);
+        for (uint32_t k = 0; k < ncand && d.nsp_off; k++) {
+          const uint32_t n = d.sim_cands[c0 + k], e0 = d.nsp_off[n], e1 = d.nsp_off[n + 1];
+          for (uint32_t x = e0 + tid; x < e1; x += FB) {
+            const uint64_t en = d.nsp[x];
+            const uint32_t g = (uint32_t)(en >> 32);
+            const int32_t c = (int32_t)(uint32_t)en;
+            if (g < d.TGZ) {
+              const uint32_t z = d.nodes0[n].zvid;
+              if (z < d.ZS) atomicSub(&ts.zcnt[g * d.ZS + z], c);
+            } else {
+              atomicSub(&ts.htot[g - d.TGZ], c);
+            }
           }
         }
       }
@@ -947,8 +950,12 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (TOPO && feas && own_n)
               feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
                 if (!SIM) return d.hn[(size_t)hs * d.NN + n];
-                // an overlay row holds only the groups this simulation counted on the node
-                if (oe != ~(size_t)0 && ((d.ov_hmask[oe * HW + (hs >> 5)] >> (hs & 31)) & 1)) return d.ov_hn[oe * d.TGH + hs];
+                // an overlay cell counts only where this simulation wrote it
+                // (its stamp); other groups keep the node's base count
+                if (oe != ~(size_t)0) {
+                  const uint64_t x = d.ov_hn[oe * d.TGH + hs];
+                  if ((uint32_t)(x >> 32) == ov_stamp) return (int32_t)(uint32_t)x;
+                }
                 return d.hn0[(size_t)hs * d.NN + n];
               });
             if (TOPO && feas && d.any_vol) {
@@ -992,18 +999,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             ovx = oe;
             areq = d.ov_req + oe * RMAX;
             afk = d.ov_fk + oe * F;
-            if (TOPO) {
-              ahn = d.ov_hn + oe * d.TGH;
-              ahs = 1;
-              avol = d.ov_vol + oe;
-            }
+            if (TOPO) avol = d.ov_vol + oe;
             if (S.ov_new) {
               if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
               if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
-              if (TOPO) {
-                for (uint32_t x = tid; x < HW; x += FB) d.ov_hmask[oe * HW + x] = 0;  // no group counted yet
-                if (d.any_vol && tid == 128) *avol = d.n_vol0[fn];
-              }
+              if (TOPO && d.any_vol && tid == 128) *avol = d.n_vol0[fn];
             }
             __syncthreads();
           } else {
@@ -1018,7 +1018,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const FKEntry& e = d.fk_entries[vr.fk_begin + (tid - 64)];
             FK* nf = afk + e.slot;
             const FK cur = *nf;
-            *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+            *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * FKV, d.fk_isint + (size_t)e.slot * FKW)
                                            : e.st;
           }
           if (tid == 0) {
@@ -1040,15 +1040,12 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               const uint32_t z = d.nodes0[fn].zvid;
               topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u, [&](uint32_t hs) {
                 if (SIM) {
-                  // copy-on-write per group: the first count takes the node's base
-                  uint32_t* mw = d.ov_hmask + ovx * HW + (hs >> 5);
-                  const uint32_t bit = 1u << (hs & 31);
-                  if (*mw & bit) {
-                    ahn[hs]++;
-                  } else {
-                    ahn[hs] = d.hn0_nm[(size_t)fn * d.TGH + hs] + 1;
-                    *mw |= bit;
-                  }
+                  // copy-on-write per group: the first count this simulation
+                  // writes takes the node's base (a cell without its stamp)
+                  uint64_t* cell = d.ov_hn + ovx * d.TGH + hs;
+                  const uint64_t x = *cell;
+                  const int32_t cnt = ((uint32_t)(x >> 32) == ov_stamp ? (int32_t)(uint32_t)x : d.hn0[(size_t)hs * d.NN + fn]) + 1;
+                  *cell = ((uint64_t)ov_stamp << 32) | (uint32_t)cnt;
                 } else {
                   ahn[(size_t)hs * ahs]++;
                 }
@@ -1525,7 +1522,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               const FKEntry& e = dd.fk_entries[vr.fk_begin + k];
               const FK cur = cf[e.slot];
               cf[e.slot] = (cur.flags & FK_PRESENT)
-                               ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * 64, dd.fk_isint[e.slot])
+                               ? fk_intersect(cur, e.st, dd.fk_ival + (size_t)e.slot * FKV, dd.fk_isint + (size_t)e.slot * FKW)
                                : e.st;
             }
             if (s_sc[f] == 0xFFFFu) HN.status = 3;
@@ -1679,7 +1676,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const FKEntry& e = d.fk_entries[vr.fk_begin + k];
             const FK cur = cf[e.slot];
             cf[e.slot] = (cur.flags & FK_PRESENT)
-                             ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * 64, d.fk_isint[e.slot])
+                             ? fk_intersect(cur, e.st, d.fk_ival + (size_t)e.slot * FKV, d.fk_isint + (size_t)e.slot * FKW)
                              : e.st;
           }
           s_ord[M] = (uint16_t)M;

@@ -15,6 +15,7 @@ namespace {
 struct Frame {
   int a, b, limit;
   int wb, wp;  // wasBalanced, wasPartitioned
+  int uni;     // WaveSort: every key in [a, b) is known equal (0: unknown)
 };
 
 // LDS-qualified element types: a pointer of these types keeps ds_* addressing

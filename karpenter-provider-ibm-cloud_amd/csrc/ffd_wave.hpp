@@ -230,26 +230,115 @@ struct WaveSort {
     }
     wsyncT<G>();
   }
-  __device__ int partition(int a, int b, int pivot, bool* already) const {
+  // the count pass of a partition: how many keys in [lo, hi) are below the
+  // pivot (<= it with LE), and whether the keys on each side are all equal
+  // (the sides become the child frames: a side of equal keys is sorted by a
+  // few swaps, see pdqsort_body)
+  // *mk: lane c keeps the predicate's ballot of chunk c (positions
+  // lo + 64c ...): with hi - lo <= 4096 the misplaced lists come from these
+  // masks (lists_from_masks) instead of two more passes over the keys
+  template <bool LE>
+  __device__ uint32_t count_split(int lo, int hi, uint32_t p, bool* lo_uni, bool* hi_uni, uint64_t* mk) const {
+    uint32_t c = 0, amin = 0xFFFFu, amax = 0, bmin = 0xFFFFu, bmax = 0;
+    uint64_t mine = 0;
+    for (int base = lo; base < hi; base += 64 * RW) {
+      bool in[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        const bool valid = k < hi;
+        const uint32_t kk = valid ? key(k) : 0u;
+        in[u] = valid && (LE ? kk <= p : kk < p);
+        if (in[u]) {
+          amin = kk < amin ? kk : amin;
+          amax = kk > amax ? kk : amax;
+        } else if (valid) {
+          bmin = kk < bmin ? kk : bmin;
+          bmax = kk > bmax ? kk : bmax;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const uint64_t b = __ballot(in[u]);
+        c += (uint32_t)__popcll(b);
+        if (lane == (uint32_t)((base - lo) / 64 + u)) mine = b;
+      }
+    }
+    *mk = mine;
+    for (int m = 32; m >= 1; m >>= 1) {
+      const uint32_t x0 = (uint32_t)__shfl_xor((int)amin, m), x1 = (uint32_t)__shfl_xor((int)amax, m);
+      const uint32_t x2 = (uint32_t)__shfl_xor((int)bmin, m), x3 = (uint32_t)__shfl_xor((int)bmax, m);
+      amin = x0 < amin ? x0 : amin;
+      amax = x1 > amax ? x1 : amax;
+      bmin = x2 < bmin ? x2 : bmin;
+      bmax = x3 > bmax ? x3 : bmax;
+    }
+    *lo_uni = amin >= amax;  // empty (0xFFFF > 0) or one key value
+    *hi_uni = bmin >= bmax;
+    return c;
+  }
+  static constexpr int MASK_MAX = 64 * 64;  // positions the lanes' chunk masks cover
+  // a partition's two misplaced lists from the lanes' masks of [lo, lo + n):
+  // x < nl is the left side, misplaced where the predicate fails (ascending
+  // positions to scr[0 ..]); x >= nl the right side, misplaced where it holds
+  // (descending positions to scr[half ..]); returns the left list's length
+  __device__ uint32_t lists_from_masks(int lo, uint32_t nl, uint32_t n, uint64_t mk) const {
+    const uint32_t x0 = lane * 64u;
+    const uint64_t valid = x0 >= n ? 0ull : (n - x0 >= 64u ? ~0ull : ((1ull << (n - x0)) - 1ull));
+    const uint64_t left = x0 >= nl ? 0ull : (nl - x0 >= 64u ? ~0ull : ((1ull << (nl - x0)) - 1ull));
+    const uint64_t lm = ~mk & left & valid, rm = mk & ~left & valid;
+    const uint32_t lc = (uint32_t)__popcll(lm), rc = (uint32_t)__popcll(rm);
+    uint32_t lpre = lc, rsuf = rc;  // inclusive: lanes <= this one / lanes >= this one
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)lpre, d), z = (uint32_t)__shfl_down((int)rsuf, d);
+      if ((int)lane >= d) lpre += y;
+      if ((int)lane + d < 64) rsuf += z;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)lpre, 63);
+    uint32_t k = lpre - lc;
+    for (uint64_t m = lm; m; m &= m - 1) scr[k++] = (uint16_t)(lo + (int)(x0 + ffs64(m)));
+    k = rsuf - rc;
+    for (uint64_t m = rm; m;) {
+      const uint32_t bit = 63u - (uint32_t)__clzll((long long)m);
+      scr[half + k++] = (uint16_t)(lo + (int)(x0 + bit));
+      m &= ~(1ull << bit);
+    }
+    wsyncT<G>();
+    return total;
+  }
+  __device__ int partition(int a, int b, int pivot, bool* already, bool* luni, bool* runi) const {
     if (lane == 0) swap(a, pivot);
     wsyncT<G>();
     const uint32_t p = key(a);
-    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) < p; });
-    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
-    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
+    uint64_t mk;
+    const int mid = a + (int)count_split<false>(a + 1, b, p, luni, runi, &mk);
+    uint32_t s;
+    if (b - a - 1 <= MASK_MAX) {
+      s = lists_from_masks(a + 1, (uint32_t)(mid - a), (uint32_t)(b - a - 1), mk);
+    } else {
+      s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
+      compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
+    }
     swap_lists(s);
     if (lane == 0) swap(mid, a);
     wsyncT<G>();
     *already = s == 0;
     return mid;
   }
-  __device__ int partition_equal(int a, int b, int pivot) const {
+  __device__ int partition_equal(int a, int b, int pivot, bool* runi) const {
     if (lane == 0) swap(a, pivot);
     wsyncT<G>();
     const uint32_t p = key(a);
-    const int mid = a + (int)count(a + 1, b, [&](int k) { return key(k) <= p; });
-    const uint32_t s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
-    compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) <= p; });
+    bool luni;
+    uint64_t mk;
+    const int mid = a + (int)count_split<true>(a + 1, b, p, &luni, runi, &mk);
+    uint32_t s;
+    if (b - a - 1 <= MASK_MAX) {
+      s = lists_from_masks(a + 1, (uint32_t)(mid - a), (uint32_t)(b - a - 1), mk);
+    } else {
+      s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
+      compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) <= p; });
+    }
     swap_lists(s);
     return mid + 1;
   }
@@ -367,7 +456,24 @@ struct WaveSort {
     }
     wsyncT<G>();
   }
+#ifdef GS_SORT_TL
+  // diagnostic: shader cycles per part of the generic sort (lane 0 sums into stl[])
+  uint64_t* stl = nullptr;
+#define STL(k)                                                     \
+  do {                                                             \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();            \
+    if (lane == 0 && stl) stl[k] += now_ - t_last_;                \
+    t_last_ = now_;                                                \
+  } while (0)
+#else
+#define STL(k) \
+  do {         \
+  } while (0)
+#endif
   __device__ __forceinline__ void pdqsort_body(int n) const {
+#ifdef GS_SORT_TL
+    uint64_t t_last_ = __builtin_amdgcn_s_memtime();
+#endif
     const SeqSortT<PackedAccT<U32>> seq{{so}};
     if (n <= SEQ) {
       if (lane == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
@@ -379,20 +485,47 @@ struct WaveSort {
     for (;;) {
       for (;;) {
         const int length = f.b - f.a;
+        STL(6);  // frame bookkeeping
         if (length <= SEQ) {
           if (lane == 0) seq.pdq_frame(f);
           wsyncT<G>();
+          STL(0);
           break;
         }
         if (f.limit == 0) {
           if (lane == 0) seq.heap_sort(f.a, f.b);
           wsyncT<G>();
+          STL(0);
           break;
         }
         if (!f.wb) {
           if (lane == 0) seq.break_patterns(f.a, f.b);
           wsyncT<G>();
           f.limit--;
+          STL(0);
+        }
+        if (f.uni) {
+          // every key in [a, b) is equal (swaps keep it so): choosePivot makes
+          // no swap (hint increasing, pivot the middle sample), a partial
+          // insertion sort finds no inversion, partitionEqual takes the whole
+          // range and partition none of it; only their first swap remains
+          const int pivot = f.a + length / 4 * 2;
+          if (f.wb && f.wp) break;
+          const bool eq = f.a > 0 && !(key(f.a - 1) < key(pivot));
+          if (lane == 0) swap(f.a, pivot);
+          wsyncT<G>();
+          if (eq) {
+            f.a = f.b;
+            STL(1);
+            continue;
+          }
+          // partition: mid = a, already partitioned; the empty left side is
+          // the smaller child, so the frame continues with [a + 1, b)
+          f.wp = 1;
+          f.wb = 0 >= length / 8;
+          f.a = f.a + 1;
+          STL(1);
+          continue;
         }
         int hint = 0;
         int pivot = seq.choose_pivot_fast(f.a, f.b, &hint);  // every lane, same keys
@@ -403,27 +536,36 @@ struct WaveSort {
           pivot = (f.b - 1) - (pivot - f.a);
           hint = 1;
         }
+        STL(2);
         if (f.wb && f.wp && hint == 1) {
-          if (partial_insertion_sort(f.a, f.b)) break;
+          const bool done = partial_insertion_sort(f.a, f.b);
+          STL(3);
+          if (done) break;
         }
         if (f.a > 0 && !(key(f.a - 1) < key(pivot))) {
-          f.a = partition_equal(f.a, f.b, pivot);
+          bool runi;
+          f.a = partition_equal(f.a, f.b, pivot, &runi);
+          f.uni = runi;
+          STL(4);
           continue;
         }
-        bool already;
-        const int mid = partition(f.a, f.b, pivot, &already);
+        bool already, luni, runi;
+        const int mid = partition(f.a, f.b, pivot, &already, &luni, &runi);
+        STL(5);
         f.wp = already;
         const int leftLen = mid - f.a, rightLen = f.b - mid;
         const int bal = length / 8;
         Frame child;
         if (leftLen < rightLen) {
           f.wb = leftLen >= bal;
-          child = Frame{f.a, mid, f.limit, 1, 1};
+          child = Frame{f.a, mid, f.limit, 1, 1, luni};
           f.a = mid + 1;
+          f.uni = runi;
         } else {
           f.wb = rightLen >= bal;
-          child = Frame{mid + 1, f.b, f.limit, 1, 1};
+          child = Frame{mid + 1, f.b, f.limit, 1, 1, runi};
           f.b = mid;
+          f.uni = luni;
         }
         if (lane == 0) {
           stk[sp].a = f.a;
@@ -431,6 +573,7 @@ struct WaveSort {
           stk[sp].limit = f.limit;
           stk[sp].wb = f.wb;
           stk[sp].wp = f.wp;
+          stk[sp].uni = f.uni;
         }
         wsyncT<G>();
         sp++;
@@ -443,6 +586,7 @@ struct WaveSort {
       f.limit = __builtin_amdgcn_readfirstlane(stk[sp].limit);
       f.wb = __builtin_amdgcn_readfirstlane(stk[sp].wb);
       f.wp = __builtin_amdgcn_readfirstlane(stk[sp].wp);
+      f.uni = __builtin_amdgcn_readfirstlane(stk[sp].uni);
     }
     wsyncT<G>();
   }
@@ -453,8 +597,17 @@ struct WaveSort {
 // member function would reload them through a `this` pointer in scratch
 // after every LDS store)
 template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
-__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n) {
+__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n
+#ifdef GS_SORT_TL
+                                          , uint64_t* stl = nullptr
+#endif
+) {
+#ifdef GS_SORT_TL
+  WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
+  w.stl = stl;
+#else
   const WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
+#endif
   w.pdqsort_body(n);
 }
 
@@ -494,6 +647,10 @@ template <uint32_t RR, bool TOPO, bool CH = false>
 __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
+#ifdef GS_SORT_TL
+  __shared__ uint64_t s_stl[8];
+  if (threadIdx.x < 8) s_stl[threadIdx.x] = 0;
+#endif
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
   __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
   __shared__ uint32_t s_thoff[RMAX + 1];
@@ -1011,7 +1168,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           const FKEntry& e = KD.fk_entries[fk_begin + lane];
           FK* nf = afk + e.slot;
           const FK cur = *nf;
-          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+          *nf = (cur.flags & FK_PRESENT) ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * FKV, KD.fk_isint + (size_t)e.slot * FKW)
                                          : e.st;
         }
         {
@@ -1133,7 +1290,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
           const uint64_t g0_ = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef GS_SORT_TL
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, s_stl);
+#else
           wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
+#endif
 #ifdef GS_FFD_TL
           n_gen_cyc += __builtin_amdgcn_s_memtime() - g0_;
 #endif
@@ -1235,9 +1396,16 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         n_xns += simple ? 0u : nex;
         n_xb++;
 #endif
-        const uint32_t xe = lane < nex ? s_exl[lane] : 0u;
+        // wide option rows (W > WREG words): a small batch spreads each
+        // candidate over L lanes, each testing every L-th 4-word chunk, so a
+        // candidate takes W / 4L dependent round trips instead of W / 4
+        const uint32_t lgL = W <= WREG ? 0u : nex <= 8 ? 3u : nex <= 16 ? 2u : nex <= 32 ? 1u : 0u;
+        const uint32_t lgW = W <= 4 ? 0u : W <= 8 ? 1u : W <= 16 ? 2u : 3u;  // no more lanes than 4-word chunks
+        const uint32_t lg = lgL < lgW ? lgL : lgW;
+        const uint32_t cx = lane >> lg, sub = lane & ((1u << lg) - 1u);
+        const uint32_t xe = cx < nex ? s_exl[cx] : 0u;
         const uint32_t j = xe >> 16, xpos = xe & 0xFFFFu;
-        const uint32_t t = lane < nex ? (uint32_t)s_tmpl[j] : 0u;
+        const uint32_t t = cx < nex ? (uint32_t)s_tmpl[j] : 0u;
         GS_RQ_AT(RQ);
       bool feas = false;
       uint64_t zset = ~0ull;  // zone domains topology allows on this NodeClaim (~0: unconstrained)
@@ -1247,7 +1415,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       int64_t tot[RR];
       uint64_t nx[WREG] = {0, 0, 0, 0};
       uint64_t G = 0, Gt = 0;
-      if (lane < nex) {
+      if (cx < nex) {
         const ClaimRec* cr = KD.c_rec + j;
         uint32_t cur[RR];
         {
@@ -1334,7 +1502,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             for (uint32_t w = 0; w < WREG; w++) accw |= nx[w];
           } else {
             // 4 words per round trip, stop at the first batch with a survivor
-            for (uint32_t w0 = 0; w0 < W && !accw; w0 += 4) {
+            for (uint32_t w0 = sub * 4; w0 < W && !accw; w0 += 4u << lg) {
               const uint4* oq = (const uint4*)(opts + w0);
               const uint4* rq4 = (const uint4*)(row + w0);
               const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
@@ -1364,7 +1532,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               }
             }
           }
-          feas = accw != 0;
+          // the candidate's lanes (all active: pre is per candidate)
+          const uint64_t gb = __ballot(accw != 0);
+          feas = ((gb >> (lane & ~((1u << lg) - 1u))) & ((1ull << (1u << lg)) - 1ull)) != 0;
           if (TOPO && feas && KD.tmpl[t].mv_mask) {
             // minValues over the NodeClaim's options after Add (per lane)
             feas = mv_ok(KD, KD.tmpl[t], [&](uint32_t w) -> uint64_t {
@@ -1390,27 +1560,39 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
           n_xwin++;
 #endif
+        if (W > WREG) {
+          // the winner's option words after Add, one lane per word (one
+          // round trip per 64 words instead of one per word): its threshold
+          // rows and offering grid come from its lane
+          const uint32_t jw = rlane(j, wl), tw = rlane(t, wl);
+          uint32_t mw[RR];
+  #pragma unroll
+          for (uint32_t r = 0; r < RR; r++) mw[r] = rlane(mrow[r], wl);
+          const uint64_t Gw = ((uint64_t)rlane((uint32_t)(G >> 32), wl) << 32) | rlane((uint32_t)G, wl);
+          const uint64_t Gtw = ((uint64_t)rlane((uint32_t)(Gt >> 32), wl) << 32) | rlane((uint32_t)Gt, wl);
+          uint64_t* wopts = KD.c_opts + (size_t)jw * OW;
+          const uint64_t* row = KD.rows + ((size_t)v * T + tw) * OW;
+          for (uint32_t w = lane; w < W; w += 64) {
+            uint64_t x = wopts[w] & row[w];
+  #pragma unroll
+            for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mw[r] * OW + w];
+            if (Gw != Gtw) {
+              uint64_t off = 0;
+              for (uint64_t gm = Gw; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+              x &= off;
+            }
+            wopts[w] = x;
+          }
+        }
         if (lane == wl) {
-          // NodeClaim.Add by the winning lane: options, requests, requirements
+          // NodeClaim.Add by the winning lane: options (wide rows: above),
+          // requests, requirements
           ClaimRec* cr = KD.c_rec + j;
           uint64_t* opts = KD.c_opts + (size_t)j * OW;
           if (W <= WREG) {
   #pragma unroll
             for (uint32_t w = 0; w < WREG; w++)
               if (w < W) opts[w] = nx[w];  // already narrowed to the grid
-          } else {
-            const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
-            for (uint32_t w = 0; w < W; w++) {
-              uint64_t x = opts[w] & row[w];
-  #pragma unroll
-              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
-              if (G != Gt) {
-                uint64_t off = 0;
-                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
-                x &= off;
-              }
-              opts[w] = x;
-            }
           }
           int64_t nt[RR], ma[RR];
           uint32_t cu[RR];
@@ -1446,7 +1628,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const FKEntry& e = KD.fk_entries[fk_begin + k];
             const FK cur = cf[e.slot];
             cf[e.slot] = (cur.flags & FK_PRESENT)
-                             ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+                             ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * FKV, KD.fk_isint + (size_t)e.slot * FKW)
                              : e.st;
           }
           const uint32_t e = s_so[f];
@@ -1690,7 +1872,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           const FKEntry& e = KD.fk_entries[fk_begin + k];
           const FK cur = cf[e.slot];
           cf[e.slot] = (cur.flags & FK_PRESENT)
-                           ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * 64, KD.fk_isint[e.slot])
+                           ? fk_intersect(cur, e.st, KD.fk_ival + (size_t)e.slot * FKV, KD.fk_isint + (size_t)e.slot * FKW)
                            : e.st;
         }
         s_so[M] = 1u | (M << 16);
@@ -1775,12 +1957,16 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
     c.dbg[8] = n_gen_cyc;  // shader cycles in Go's full pdqsort (generic sorts)
+#ifdef GS_SORT_TL
+    for (int q = 0; q < 7; q++) c.dbg[9 + q] = s_stl[q];  // generic sort: seq, uniform, pivot, partial, peq, part, frames
+#else
     c.dbg[9] = n_xns;
     c.dbg[10] = n_xb;
     c.dbg[11] = n_xwin;
     c.dbg[12] = n_nonsimple;
     c.dbg[13] = n_rot;
     c.dbg[14] = n_rotlen;
+#endif
 #endif
     *d.ctrl = c;
   }

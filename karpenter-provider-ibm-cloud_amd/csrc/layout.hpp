@@ -53,10 +53,12 @@ enum : uint32_t { VF_SIMPLE = 1u << 31 };
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)
 enum : uint32_t { FK_PRESENT = 1u, FK_COMP = 2u, FK_GT = 4u, FK_LT = 8u };
+constexpr int FKW = 4;          // words of a free key's value bitsets (<= 256 vocabulary values, omega included)
+constexpr int FKV = 64 * FKW;
 struct FK {
-  uint64_t has;   // Has(v) for each vocabulary value
-  uint64_t excl;  // complement: explicit excluded values (after bound filtering)
-  int64_t gt, lt; // bounds (complement sets only)
+  uint64_t has[FKW];   // Has(v) for each vocabulary value
+  uint64_t excl[FKW];  // complement: explicit excluded values (after bound filtering)
+  int64_t gt, lt;      // bounds (complement sets only)
   uint32_t flags;
   uint32_t pad;
 };
@@ -239,8 +241,8 @@ struct DevProblem {
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
   const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
-  const int64_t* fk_ival;      // [F][64] integer value of vocabulary entries
-  const uint64_t* fk_isint;    // [F]
+  const int64_t* fk_ival;      // [F][FKV] integer value of vocabulary entries
+  const uint64_t* fk_isint;    // [F][FKW] entries that are integers
   // templates
   const TmplRec* tmpl;         // [T]
   const uint64_t* t_opts;      // [T][W]
@@ -307,7 +309,12 @@ struct DevProblem {
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)
   const uint32_t* zone_cat;    // [64] zone vocabulary id -> catalog zone index (NONE)
   const int32_t* hn0;          // [TGH][NN] hostname counts per existing node before the Solve
-  const int32_t* hn0_nm;       // [NN][TGH] the same, node-major (simulations copy a node's whole row)
+  // simulations: each node's nonzero counts before the Solve, node-major
+  // sparse (CSR): entries (group << 32 | count), group < TGZ a zone group,
+  // else hostname group (group - TGZ).  Excluding a candidate's pods reads
+  // its few entries, not a TGZ + TGH row
+  const uint32_t* nsp_off;     // [NN + 1]
+  const uint64_t* nsp;         // [nsp_off[NN]]
   int32_t* hn;                 // [TGH][NN] working copy
   int32_t* hc;                 // [max_claims][TGH] per NodeClaim (one row per claim)
   // truncation outputs
@@ -343,10 +350,13 @@ struct DevProblem {
   // group and node (the candidates' pods are rescheduled, not counted); per
   // block the hostname counts and volume usage of the overlay nodes
   const uint64_t* sim_known;   // [n_sims]
-  const int32_t* zn_cnt;       // [TGZ][NN]
-  int32_t* ov_hn;              // [grid][ov_cap][TGH]
+  // [grid][ov_cap][TGH] (stamp << 32 | count): a hostname count a
+  // simulation wrote on one of its overlay nodes, stamp = ov_epoch << 20 |
+  // simulation + 1; a cell with another stamp is unwritten (the node's hn0
+  // count holds), so an entry's cells are never cleared
+  uint64_t* ov_hn;
   NodeVol* ov_vol;             // [grid][ov_cap]
-  uint32_t* ov_hmask;          // [grid][ov_cap][ceil(TGH / 32)] hostname groups whose overlay count is written (others read hn0_nm)
+  uint32_t ov_epoch;            // 1..4095: the launch's stamp prefix (ov_hn zeroed when it wraps)
   uint32_t* ov_map;            // [grid][NN] a touched node's overlay entry (valid where the LDS bitmap bit is set)
 };
 

@@ -225,3 +225,34 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   *out_n = kept;
   return GS_OK;
 }
+
+// Test hook (not in gpusched.h; tests/test_wave_sort.py binds it): the
+// single-wave sort.Slice restatement (WaveSort, the Solve's NodeClaim sort)
+// over n u16 keys on the current device; perm[k] = the input index that lands
+// at position k.  Parity with Go's pdqsort is checked against the oracle's
+// restatement on adversarial key arrays (one raised key, two or three values).
+extern "C" gs_status gs_debug_go_sort(const uint16_t* keys, uint32_t n, uint32_t* perm) {
+  if (n && (!keys || !perm)) return GS_E_INVALID;
+  if (n > GS_RANK_MAX) return GS_E_CAPACITY;
+  if (n == 0) return GS_OK;
+  std::vector<uint16_t> h((size_t)n * 2);
+  for (uint32_t k = 0; k < n; k++) {
+    h[k] = keys[k];
+    h[n + k] = (uint16_t)k;
+  }
+  void* d = nullptr;
+  const size_t bytes = (size_t)n * 4 + 16;
+  if (hipMalloc(&d, bytes) != hipSuccess) return GS_E_HIP;
+  uint16_t* dk = (uint16_t*)d;
+  uint16_t* dp = dk + n;
+  uint32_t* dn = (uint32_t*)((char*)d + (((size_t)n * 4 + 3) & ~(size_t)3));
+  gs_status st = GS_OK;
+  if (hipMemcpy(dk, h.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dn, &n, 4, hipMemcpyHostToDevice) != hipSuccess || gsk_rank_sort(dk, dp, dn, n, 0) != hipSuccess ||
+      hipMemcpy(h.data(), dk, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    st = GS_E_HIP;
+  (void)hipFree(d);
+  if (st == GS_OK)
+    for (uint32_t k = 0; k < n; k++) perm[k] = h[n + k];
+  return st;
+}

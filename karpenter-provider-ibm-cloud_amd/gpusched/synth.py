@@ -251,8 +251,10 @@ _KEYS_FREE = ["kubernetes.io/os", "karpenter.sh/nodepool", "team", "karpenter-ib
               "kubernetes.io/hostname", "tier"]
 
 
-def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
-    """small adversarial problem over the whole supported feature set"""
+def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_values=3):
+    """small adversarial problem over the whole supported feature set;
+    free_values > 3 widens the custom (free) keys team / tier to that many
+    values (tier's integers then reach free_values - 1 for Gt / Lt)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
@@ -280,11 +282,13 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
         "karpenter.sh/capacity-type": ["on-demand", "spot"],
         "kubernetes.io/os": ["linux", "windows"],
         "karpenter.sh/nodepool": ["np0", "np1", "np2"],
-        "team": ["a", "b", "c"],
+        "team": ["a", "b", "c"] if free_values <= 3 else [f"t{i:03d}" for i in range(free_values)],
         "karpenter-ibm.sh/instance-cpu": ["2", "4", "8", "x"],
         "kubernetes.io/hostname": ["host-a", "host-b"],
-        "tier": ["1", "2", "3"],
+        "tier": ["1", "2", "3"] if free_values <= 3 else [str(i) for i in range(free_values)],
     }
+    nteam = len(vocab["team"])
+    bound_hi = 10 if free_values <= 3 else free_values
     all_keys = _KEYS_IT + _KEYS_OFF + _KEYS_FREE
 
     def rand_req(keys=all_keys):
@@ -295,7 +299,7 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
         if op in ("Gt", "Lt"):
             if rng.random() < 0.4:
                 op = op + "e"  # Gte / Lte
-            return (k, op, [str(int(rng.integers(0, 10)))])
+            return (k, op, [str(int(rng.integers(0, bound_hi)))])
         if op in ("Exists", "DoesNotExist"):
             return (k, op, [])
         n = int(rng.integers(1, min(3, len(vals)) + 1))
@@ -305,7 +309,7 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
     n_np = int(rng.integers(1, 4))
     for j in range(n_np):
         reqs = [rand_req(_KEYS_IT + _KEYS_OFF + ["kubernetes.io/os", "team"]) for _ in range(int(rng.integers(0, 3)))]
-        labels = {"team": vocab["team"][rng.integers(0, 3)]} if rng.random() < 0.4 else {}
+        labels = {"team": vocab["team"][rng.integers(0, nteam)]} if rng.random() < 0.4 else {}
         taints = [("dedicated", str(rng.choice(["x", "y"])), str(rng.choice(effects)))] if rng.random() < 0.4 else []
         limits = None
         if with_limits and rng.random() < 0.3:
@@ -321,7 +325,7 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True):
             labels["karpenter.sh/capacity-type"] = "on-demand"
             labels["kubernetes.io/hostname"] = f"node-{k}"
             if rng.random() < 0.5:
-                labels["team"] = vocab["team"][rng.integers(0, 3)]
+                labels["team"] = vocab["team"][rng.integers(0, nteam)]
             avail = {"cpu": int(rng.choice([500, 1000, 4000])), "memory": int(rng.choice([1, 4, 16])) * GI * 1000,
                      "pods": 10_000}
             taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.3 else []

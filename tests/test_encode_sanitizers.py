@@ -28,7 +28,7 @@ def harness(tmp_path_factory):
         pytest.skip("g++ absent")
     out = str(tmp_path_factory.mktemp("asan") / "encode_harness_asan")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-o", out, os.path.join(ROOT, "tools", "encode_harness.cpp"),
+           "-fno-sanitize-recover=undefined", "-pthread", "-o", out, os.path.join(ROOT, "tools", "encode_harness.cpp"),
            os.path.join(CSRC, "encode.cpp")]
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)
     return out

@@ -1,0 +1,104 @@
+"""The single-wave sort.Slice restatement (WaveSort in ffd_wave.hpp: the
+Solve's per-pod `sort.Slice(newNodeClaims, len(Pods) asc)`) against the
+oracle's restatement of Go's pdqsort (oracle/gosort.h), permutation for
+permutation, on the inputs the Solve hands it: a sorted array with one key
+raised by one (anywhere, and on choosePivot's samples), arrays of two or three
+key values, the e2e shape (a long run of low counts, then the raised claim and
+the active runs), and random keys.  Ties decide which NodeClaim a pod lands
+on, so the permutation -- not just the sorted keys -- must match."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+
+def go_perm(keys):
+    n = len(keys)
+    k = (C.c_int64 * max(1, n))(*keys)
+    p = (C.c_uint32 * max(1, n))()
+    pyoracle.lib().oracle_go_sort_ints(k, p, n)
+    return list(p)[:n]
+
+
+def wave_perm(keys):
+    from gpusched import lib
+    L = lib.load()
+    n = len(keys)
+    f = L.gs_debug_go_sort
+    f.argtypes = [C.POINTER(C.c_uint16), C.c_uint32, C.POINTER(C.c_uint32)]
+    f.restype = C.c_int
+    k = (C.c_uint16 * max(1, n))(*keys)
+    p = (C.c_uint32 * max(1, n))()
+    assert f(k, n, p) == 0
+    return list(p)[:n]
+
+
+def check(keys):
+    keys = [int(x) for x in keys]
+    assert wave_perm(keys) == go_perm(keys), keys if len(keys) < 80 else len(keys)
+
+
+def raised(runs, pos):
+    """the sorted array given as (key, length) runs, with the key at `pos` raised by one"""
+    a = [k for k, n in runs for _ in range(n)]
+    a[pos] += 1
+    return a
+
+
+@pytest.mark.parametrize("n", [13, 20, 49, 50, 51, 64, 100, 200, 333])
+def test_one_raised_key_every_position(n):
+    rng = np.random.default_rng(n)
+    for pos in range(n):
+        runs = [(3, int(rng.integers(1, n))), (4, n)]
+        a = raised(runs, pos)[:n]
+        check(a)
+
+
+@pytest.mark.parametrize("n", [100, 250, 1000, 1999, 4096])
+def test_raised_on_pivot_samples(n):
+    q = n // 4
+    for s in (q, 2 * q, 3 * q):
+        for d in (-2, -1, 0, 1):
+            for lo in (0, n // 8, n // 2, n - 3):
+                runs = [(16, lo), (17, n - lo)]
+                check(raised(runs, max(0, min(n - 1, s + d))))
+
+
+@pytest.mark.parametrize("low,mid,m", [(500, 1, 19), (500, 1, 2), (500, 1, 100), (250, 1, 40), (10, 1, 5),
+                                       (700, 1, 150)])
+def test_e2e_shape(low, mid, m):
+    """a run of idle claims at a low count, then the raised claim and the
+    active runs (tests/golden e2e Solve: 12,494 of 30k sorts look like this)"""
+    n = 1000
+    a = [16] * low + [18] * mid + [17] * m + [18] * (n - low - mid - m)
+    check(a[:n])
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_few_values(seed):
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(0, 3000))
+    vals = int(rng.integers(1, 5))
+    check(rng.integers(0, vals, size=n))
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_random_sorted_runs_with_swaps(seed):
+    rng = np.random.default_rng(200 + seed)
+    n = int(rng.integers(13, 4096))
+    a = np.sort(rng.integers(0, int(rng.integers(1, 40)), size=n))
+    for _ in range(int(rng.integers(0, 4))):
+        i, j = rng.integers(0, n, size=2)
+        a[i], a[j] = a[j], a[i]
+    check(a)
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_keys(seed):
+    rng = np.random.default_rng(300 + seed)
+    n = int(rng.integers(0, 4096))
+    check(rng.integers(0, 65535, size=n))

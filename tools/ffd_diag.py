@@ -1,4 +1,4 @@
-"""Diagnostic: FFD kernel phase breakdown on the CM workload (--c1 / --c2 / --c3 / --e2e: those workloads).
+"""Diagnostic: FFD kernel phase breakdown on the CM workload (--c1 / --c2 / --c3 / --c5 / --e2e: those workloads).
 
 default build: barrier-to-barrier wall-clock timers (Ctrl.dbg);
 `make tl` build + --tl: shader cycles per pod-loop segment (GS_FFD_TL)."""
@@ -18,6 +18,8 @@ elif "--c3" in sys.argv:
     p = synth.make_c3()
 elif "--e2e" in sys.argv:
     p = synth.e2e_deployments(n_deployments=60, replicas=500)
+elif "--c5" in sys.argv:
+    p = synth.make_c5(n_pods=int(args[0]) if args else 200000)
 elif "--c2" in sys.argv:
     p = synth.make_c2()
 else:
@@ -38,6 +40,9 @@ if "--tl" in sys.argv and "--block" not in sys.argv:
     base["generic_sort_cycles_per_pop"] = round(out[8] / max(res.pops, 1), 1)
     base["cycles_per_generic_sort"] = round(out[8] / max(res.sorts_generic, 1), 1)
     base["fast_accepts"] = out[15]
+    if "--sorttl" in sys.argv:  # GS_SORT_TL build: the generic sort's parts (shader cycles per generic sort)
+        base["generic_sort_parts_per_sort"] = {n: round(out[9 + i] / max(res.sorts_generic, 1), 1) for i, n in enumerate(
+            ["seq_breakpatterns", "uniform", "pivot", "partial_insertion", "partition_equal", "partition", "frames"])}
     base["exact_cands_nonsimple"] = out[9]
     base["exact_batches"] = out[10]
     base["exact_wins"] = out[11]
