@@ -163,7 +163,7 @@ typedef struct gs_spread {
   gs_range match_labels;         /* into labels */
   gs_range match_expressions;    /* into reqs: In / NotIn / Exists / DoesNotExist over pod labels */
   uint32_t node_affinity_policy; /* GS_POLICY_HONOR (default) or GS_POLICY_IGNORE */
-  uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is refused */
+  uint32_t node_taints_policy;   /* GS_POLICY_IGNORE (default); HONOR is accepted where every taint of the problem is tolerated by the owner (it then equals IGNORE), else GS_E_UNSUPPORTED */
   gs_range match_label_keys;     /* into value_ids: label keys (string ids) */
 } gs_spread;
 

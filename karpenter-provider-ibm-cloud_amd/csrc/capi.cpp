@@ -232,7 +232,8 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->ov_hn_bytes = (size_t)sims->blocks * d.ov_cap * std::max<uint32_t>(e.TGH, 1) * sizeof(uint64_t);
     d.ov_epoch = 0;
     c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
-    c->alloc(d.ov_map, (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
+    d.ovh_slots = gsd::ovh_slots_for(d.ov_cap);
+    c->alloc(d.ov_map, d.ovh_slots ? 1 : (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
     {
       std::vector<uint64_t> known = sims->known;
       known.resize(std::max<size_t>(NS, 1), 0);
@@ -242,6 +243,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->alloc(d.slot_nits, e.any_mv ? CA : 1);
     c->alloc(d.slot_drop, e.any_mv ? CA : 1);
     c->alloc(d.sim_ctrl, NS);
+    c->alloc(d.sim_blk, sims->blocks);
     c->alloc(d.sim_hdr, NS);
     c->alloc(d.sim_next, 1);
     d.n_pending = c->n_pending;

@@ -313,7 +313,8 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     return GS_E_CAPACITY;
   }
   const uint32_t lds = gsk_ffd_lds_bytes(std::max<uint32_t>(sp.max_pods, 1), (uint32_t)e.thr_val.size(),
-                                         (e.NN + 31) / 32, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH));
+                                         (e.NN + 31) / 32, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) +
+                       8u * gsd::ovh_slots_for(sp.ov_cap);
   if (lds > gsk_ffd_dyn_lds_max()) {
     *err = "simulation exceeds the workgroup LDS (pods per simulation or state nodes)";
     return GS_E_CAPACITY;
@@ -341,7 +342,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   const gs_consolidation* in = &c->cons_in;
   auto& d = c->dp;
   const size_t NS = sp.evaluated.size();
-  const gsd::Ctrl* ctrl = c->h_ctrl;
+  const gsd::SimCtrl* ctrl = c->h_ctrl;
   const gsd::ClaimRec* hdr = c->h_hdr;
   const uint32_t* its = c->h_its;
   const uint32_t* nits = c->h_nits;
@@ -380,7 +381,10 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     if (NS) {
       // per simulation: control block (NodeClaim count, failed pods), the
       // single NodeClaim's header and its OrderByPrice/Truncate(60) list
-      HIPCHK(hipMemcpyAsync(c->h_ctrl, d.sim_ctrl, NS * sizeof(gsd::Ctrl), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_ctrl, d.sim_ctrl, NS * sizeof(gsd::SimCtrl), hipMemcpyDeviceToHost, c->stream));
+      c->h_blk.resize(sp.blocks);
+      HIPCHK(hipMemcpyAsync(c->h_blk.data(), d.sim_blk, sp.blocks * sizeof(gsd::Ctrl), hipMemcpyDeviceToHost,
+                            c->stream));
       HIPCHK(hipMemcpyAsync(c->h_hdr, d.sim_hdr, NS * sizeof(gsd::ClaimRec), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipMemcpyAsync(c->h_its, d.c_its, NS * 60 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipMemcpyAsync(c->h_nits, d.c_nits, NS * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
@@ -397,17 +401,20 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     c->commands[s].n_candidates = (uint32_t)sp.sets[s].size();
   }
   uint64_t checks = 0, node_evals = 0, pops = 0, node_prefix = 0;
+  if (NS)
+    for (const gsd::Ctrl& b : c->h_blk) {
+      node_evals += b.node_evals;
+      node_prefix += b.node_prefix;
+      pops += b.pops;
+    }
   for (size_t k = 0; k < NS; k++) {
     const uint32_t s = sp.evaluated[k];
-    const gsd::Ctrl& ct = ctrl[k];
+    const gsd::SimCtrl& ct = ctrl[k];
     if (ct.status == gsd::ST_POD_COUNT)
       return fail(c, GS_E_CAPACITY, "a simulated NodeClaim would hold more than 65535 pods (16-bit pod count)");
     if (ct.status != 0) return fail(c, GS_E_HIP, "simulation kernel reported an internal error");
     const uint32_t q0 = sp.pod_off[k], P = sp.pod_off[k + 1] - q0;
     checks += (uint64_t)P * (e.NN - sp.sets[s].size() + e.checks_per_pod);
-    node_evals += ct.node_evals;
-    node_prefix += ct.node_prefix;
-    pops += ct.pops;
     gs_command& cmd = c->commands[s];
     cmd.decision = GS_DECISION_NOOP;
     cmd.n_new_claims = ct.n_claims;

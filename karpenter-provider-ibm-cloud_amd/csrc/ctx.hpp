@@ -133,7 +133,8 @@ struct gs_ctx {
   std::vector<uint32_t> multi_opts;
   bool cons_ready = false;
   // pinned per-simulation result staging (allocated with the plan)
-  gsd::Ctrl* h_ctrl = nullptr;
+  gsd::SimCtrl* h_ctrl = nullptr;
+  std::vector<gsd::Ctrl> h_blk;  // the simulation workgroups' counter sums
   gsd::ClaimRec* h_hdr = nullptr;
   uint32_t* h_its = nullptr;
   uint32_t* h_nits = nullptr;

@@ -717,7 +717,7 @@ struct Ctx {
   struct SpreadEnc {
     std::string key;
     int32_t skew = 1, mind = 0;
-    bool sa = false, has_sel = false, ignore_aff = false;
+    bool sa = false, has_sel = false, ignore_aff = false, honor_taints = false;
     std::map<std::string, std::string> ml;
     std::vector<std::tuple<std::string, uint32_t, std::set<std::string>>> ex;
     // metav1.LabelSelector (nil selects nothing)
@@ -836,9 +836,15 @@ struct Ctx {
       if (sp.key != kZone && sp.key != kHostname)
         throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / hostname"};
       if (q.max_skew < 1) throw Fail{GS_E_INVALID, "maxSkew < 1"};
-      if (q.node_taints_policy != GS_POLICY_IGNORE) throw Fail{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor"};
-      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE)
+      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE ||
+          q.node_taints_policy > GS_POLICY_IGNORE)
         throw Fail{GS_E_INVALID, "bad topology spread enum"};
+      // nodeTaintsPolicy Honor (TopologyNodeFilter.Matches: the owner's
+      // tolerations must tolerate a node's / NodeClaim's taints for it to
+      // count and for its domain to enter the minimum) is accepted when the
+      // owner tolerates every taint of the problem, where it equals Ignore;
+      // checked in build_nodes once every taint is known
+      sp.honor_taints = q.node_taints_policy == GS_POLICY_HONOR;
       sp.skew = q.max_skew;
       sp.mind = q.min_domains > 0 ? q.min_domains : 0;
       sp.sa = q.when_unsatisfiable == GS_SPREAD_SCHEDULE_ANYWAY;
@@ -1321,6 +1327,7 @@ struct Ctx {
   // --------------------------------------------------------- templates
   bool tolerate_pns = false;
   std::vector<std::vector<Tol>> variant_tols;
+  std::vector<uint32_t> honor_specs;  // specs owning a nodeTaintsPolicy Honor spread
   void build_templates() {
     // dense per-key value ids of the catalog (minValues counting)
     e.it_dvid.assign((size_t)e.K * e.N, 0);
@@ -1594,6 +1601,7 @@ struct Ctx {
     std::vector<std::pair<int32_t, uint32_t>> anti_pref, aff_pref;  // (weight, group)
     std::vector<PodVariant> vars;
     std::vector<std::vector<Tol>> var_tols;
+    bool honor_taints = false;  // a spread with nodeTaintsPolicy Honor
   };
   // pods -> specs: spec_of[pod], spec_rep[spec] (its first pod), and per spec
   // its variants' range in e.variants (sv_begin / sv_count)
@@ -1618,6 +1626,7 @@ struct Ctx {
     const std::string& pns = S(pd.ns);
     chk(pd.labels, p->n_labels, "labels");
     w.sps = spreads_of(pd);
+    for (auto& sp : w.sps) w.honor_taints = w.honor_taints || sp.honor_taints;
     if (!w.sps.empty() && (pd.node_selector.count || pd.required_terms.count))
       for (auto& sp : w.sps)
         if (!sp.ignore_aff)
@@ -1933,6 +1942,7 @@ struct Ctx {
       sv_count[s] = (uint32_t)work[s].vars.size();
       for (auto& v : work[s].vars) e.variants.push_back(std::move(v));
       for (auto& t : work[s].var_tols) variant_tols.push_back(std::move(t));
+      if (work[s].honor_taints) honor_specs.push_back(s);
     }
     e.var_begin.resize(e.P);
     e.var_count.resize(e.P);
@@ -2149,6 +2159,13 @@ struct Ctx {
     std::vector<uint64_t> sv_tol(variant_tols.size());
     for (size_t sv = 0; sv < variant_tols.size(); sv++) sv_tol[sv] = tol_mask(variant_tols[sv]);
     for (uint32_t v = 0; v < e.V; v++) e.vars[v].tol = sv_tol[e.var_sv[v]];
+    // nodeTaintsPolicy Honor: the group's filter holds the owner's own
+    // tolerations (before Relax adds PreferNoSchedule); tolerating every
+    // NodePool and node taint makes TopologyNodeFilter.Matches always true
+    const uint64_t all_taints = taint_list.size() >= 64 ? ~0ull : (1ull << taint_list.size()) - 1;
+    for (uint32_t s : honor_specs)
+      if (all_taints & ~sv_tol[sv_begin[s]])
+        throw Fail{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor with a taint its owner does not tolerate"};
   }
 };
 

@@ -101,7 +101,7 @@ struct Shared {
   uint32_t use_pf;
   // solve in this block: simulation id, pod/claim arena offset, global pod id,
   // overlay entry count / the entry being written (and whether it is new)
-  uint32_t sim, qoff, gpod, nov, ove, ov_new;
+  uint32_t sim, qoff, gpod, nov, ove, ov_new, ov_fk;
   alignas(16) uint32_t vrb[2][(sizeof(VarRec) / 4 + 3) & ~3u];
   alignas(16) int64_t reqb[2][RMAX];
 };
@@ -573,6 +573,7 @@ struct Blk {
 // from residency than they lose to the spills.
 constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? 3 : 4; }
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
+constexpr uint32_t OV_FK = 0x40000000u;    // the entry holds its own free-key state (copied on the first Add that needs it)
 
 template <uint32_t RR, bool SIM, uint32_t NT, bool TOPO>
 __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel(DevProblem d) {
@@ -602,6 +603,32 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
+  // SIM, small simulations: node -> overlay entry in an LDS hash (keys node + 1,
+  // open addressing), after the topology state
+  const uint32_t ovh = SIM ? d.ovh_slots : 0u, ovh_mask = ovh - 1u;
+  uint32_t* const s_ovk = (uint32_t*)((char*)lds64 + ((tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u));
+  uint32_t* const s_ovv = s_ovk + ovh;
+  auto ovm_get = [&](uint32_t n) -> uint32_t {
+    if (!ovh) return ov_map[n];
+    uint32_t h = (n * 2654435761u) & ovh_mask;
+    for (uint32_t i = 0; i < ovh; i++, h = (h + 1u) & ovh_mask)
+      if (s_ovk[h] == n + 1u) return s_ovv[h];
+    return OV_EXCL;  // unreachable: callers ask only for nodes the bitmap marks
+  };
+  auto ovm_put = [&](uint32_t n, uint32_t v) {  // one thread per node at a time
+    if (!ovh) {
+      ov_map[n] = v;
+      return;
+    }
+    uint32_t h = (n * 2654435761u) & ovh_mask;
+    for (uint32_t i = 0; i < ovh; i++, h = (h + 1u) & ovh_mask) {
+      const uint32_t k = atomicCAS(&s_ovk[h], 0u, n + 1u);
+      if (k == 0u || k == n + 1u) {
+        s_ovv[h] = v;
+        return;
+      }
+    }
+  };
   Blk<NT> blk{s_sc, s_ord, s_scr, S, tid, tid & 63, tid >> 6, 0, MC / 2};
   Wg<NT> wg{&S.red2[0][0], s_sc, s_ord, tid, tid & 63, tid >> 6, 0};
 
@@ -623,6 +650,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   }
   const uint32_t wave = tid >> 6, lane = tid & 63;
 
+  // SIM, thread 0: this workgroup's sums of its simulations' counters
+  uint64_t b_pops = 0, b_gen = 0, b_fast = 0, b_cand = 0, b_full = 0, b_nev = 0, b_npre = 0, b_cpre = 0;
   for (uint32_t iter = 0;; iter++) {
     // ------------------------------------------------ next simulation (SIM)
     if (tid == 0) S.sim = SIM ? atomicAdd(d.sim_next, 1u) : iter;
@@ -661,10 +690,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       const uint32_t c0 = d.sim_cand_off[sim];
       ncand = d.sim_cand_off[sim + 1] - c0;
       for (uint32_t i = tid; i < d.nb_words; i += FB) s_nb[i] = 0;
+      for (uint32_t i = tid; i < ovh; i += FB) s_ovk[i] = 0;
       __syncthreads();
       for (uint32_t k = tid; k < ncand; k += FB) {
         const uint32_t n = d.sim_cands[c0 + k];
-        ov_map[n] = k | OV_EXCL;
+        ovm_put(n, k | OV_EXCL);
         atomicOr(&s_nb[n >> 5], 1u << (n & 31));
       }
       if (TOPO) {
@@ -923,13 +953,13 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             size_t oe = ~(size_t)0;  // SIM: the node's overlay entry (hostname counts, volume usage)
             if (SIM && feas && ((s_nb[n >> 5] >> (n & 31)) & 1)) {
               // touched by this simulation: removed candidate, or overlay copy
-              const uint32_t e = ov_map[n];
+              const uint32_t e = ovm_get(n);
               if (e & OV_EXCL) {
                 feas = false;
               } else {
-                oe = (size_t)blockIdx.x * d.ov_cap + e;
+                oe = (size_t)blockIdx.x * d.ov_cap + (e & ~OV_FK);
                 nreq = d.ov_req + oe * RMAX;
-                nfk = d.ov_fk + oe * F;
+                if (e & OV_FK) nfk = d.ov_fk + oe * F;  // else the node's base free-key state still holds
               }
             }
 #pragma unroll
@@ -984,15 +1014,19 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (tid == 0) {
               uint32_t e = INF;
               if ((s_nb[fn >> 5] >> (fn & 31)) & 1) {
-                e = ov_map[fn];  // a kept node (the scan rejects removed ones)
+                e = ovm_get(fn);  // a kept node (the scan rejects removed ones)
                 S.ov_new = 0;
               } else {
                 e = S.nov++;
-                ov_map[fn] = e;
+                ovm_put(fn, e);
                 s_nb[fn >> 5] |= 1u << (fn & 31);
                 S.ov_new = 1;
               }
-              S.ove = e;
+              S.ove = e & ~OV_FK;
+              S.ov_fk = (e & OV_FK) != 0;
+              // a pod with free-key requirements narrows the node's state: the
+              // entry takes its own copy now (below) and keeps it
+              if (vr.fk_count && !(e & OV_FK)) ovm_put(fn, e | OV_FK);
             }
             __syncthreads();
             const size_t oe = (size_t)blockIdx.x * d.ov_cap + S.ove;
@@ -1002,9 +1036,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             if (TOPO) avol = d.ov_vol + oe;
             if (S.ov_new) {
               if (tid < R) areq[tid] = d.nodes0[fn].req[tid];
-              if (tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
-              if (TOPO && d.any_vol && tid == 128) *avol = d.n_vol0[fn];
+              if (TOPO && d.any_vol && tid == FB - 1) *avol = d.n_vol0[fn];
             }
+            if (vr.fk_count && !S.ov_fk && tid >= 64 && tid < 64 + F) afk[tid - 64] = d.n_fk0[(size_t)fn * F + (tid - 64)];
             __syncthreads();
           } else {
             areq = d.nodes[fn].req;
@@ -1774,7 +1808,19 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       if (lane == 0 && cnt) atomicAdd(&S.failed, cnt);
       __syncthreads();
     }
-    if (tid == 0) {
+    if (SIM && tid == 0) {
+      // the outcome in one store; the counters into this workgroup's sums
+      d.sim_ctrl[sim] = SimCtrl{S.hb[par ^ 1u].status, S.hb[par ^ 1u].M, S.hb[par ^ 1u].nlog, S.failed};
+      b_pops += S.hb[par ^ 1u].pops;
+      b_gen += S.generic;
+      b_fast += S.fast;
+      b_cand += S.cand;
+      b_full += S.cand_full;
+      b_nev += S.node_evals;
+      b_npre += S.node_prefix;
+      b_cpre += S.claim_prefix;
+    }
+    if (!SIM && tid == 0) {
       Ctrl c;
       c.status = S.hb[par ^ 1u].status;
       c.n_claims = S.hb[par ^ 1u].M;
@@ -1806,9 +1852,21 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
 #else
       for (int q = 0; q < 16; q++) c.dbg[q] = S.dbg[q];
 #endif
-      *(SIM ? d.sim_ctrl + sim : d.ctrl) = c;
+      *d.ctrl = c;
     }
     __syncthreads();
+  }
+  if (SIM && tid == 0) {
+    Ctrl c = {};
+    c.pops = b_pops;
+    c.generic_sorts = b_gen;
+    c.fast_sorts = b_fast;
+    c.cand_evals = b_cand;
+    c.cand_full = b_full;
+    c.node_evals = b_nev;
+    c.node_prefix = b_npre;
+    c.claim_prefix = b_cpre;
+    d.sim_blk[blockIdx.x] = c;
   }
 }
 
@@ -1885,7 +1943,8 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH));
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+                       (d->n_sims ? 8u * d->ovh_slots : 0u);
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations,

@@ -52,6 +52,9 @@ static_assert(offsetof(VarRec, fk_begin) == 4 && offsetof(VarRec, fk_count) == 8
 static_assert(offsetof(ClaimRec, maxa) == 128, "ClaimRec maxa after two 64-B lines");
 
 constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
+#ifndef GS_ADD_LANES  // experiment builds: 0 = the winner lane updates every option word
+#define GS_ADD_LANES 1
+#endif
 // solver <-> memory-agent wave channels (LDS)
 constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the solver
 constexpr uint32_t RING_DW = 52; // VarRec (32 dwords) + requests (<= 16 dwords) + request codes (4 dwords)
@@ -278,6 +281,9 @@ struct WaveSort {
     return c;
   }
   static constexpr int MASK_MAX = 64 * 64;  // positions the lanes' chunk masks cover
+#ifndef GS_MASK_LISTS  // experiment builds: 0 = the two compaction passes instead
+#define GS_MASK_LISTS 1
+#endif
   // a partition's two misplaced lists from the lanes' masks of [lo, lo + n):
   // x < nl is the left side, misplaced where the predicate fails (ascending
   // positions to scr[0 ..]); x >= nl the right side, misplaced where it holds
@@ -313,7 +319,7 @@ struct WaveSort {
     uint64_t mk;
     const int mid = a + (int)count_split<false>(a + 1, b, p, luni, runi, &mk);
     uint32_t s;
-    if (b - a - 1 <= MASK_MAX) {
+    if (GS_MASK_LISTS && b - a - 1 <= MASK_MAX) {
       s = lists_from_masks(a + 1, (uint32_t)(mid - a), (uint32_t)(b - a - 1), mk);
     } else {
       s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
@@ -333,7 +339,7 @@ struct WaveSort {
     uint64_t mk;
     const int mid = a + (int)count_split<true>(a + 1, b, p, &luni, runi, &mk);
     uint32_t s;
-    if (b - a - 1 <= MASK_MAX) {
+    if (GS_MASK_LISTS && b - a - 1 <= MASK_MAX) {
       s = lists_from_masks(a + 1, (uint32_t)(mid - a), (uint32_t)(b - a - 1), mk);
     } else {
       s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) > p; });
@@ -456,6 +462,9 @@ struct WaveSort {
     }
     wsyncT<G>();
   }
+#ifndef GS_UNIFORM  // experiment builds: 0 = no equal-key frame shortcut
+#define GS_UNIFORM 1
+#endif
 #ifdef GS_SORT_TL
   // diagnostic: shader cycles per part of the generic sort (lane 0 sums into stl[])
   uint64_t* stl = nullptr;
@@ -504,7 +513,7 @@ struct WaveSort {
           f.limit--;
           STL(0);
         }
-        if (f.uni) {
+        if (GS_UNIFORM && f.uni) {
           // every key in [a, b) is equal (swaps keep it so): choosePivot makes
           // no swap (hint increasing, pivot the middle sample), a partial
           // insertion sort finds no inversion, partitionEqual takes the whole
@@ -1399,7 +1408,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         // wide option rows (W > WREG words): a small batch spreads each
         // candidate over L lanes, each testing every L-th 4-word chunk, so a
         // candidate takes W / 4L dependent round trips instead of W / 4
+#ifdef GS_NO_EXACT_LANES  // experiment builds: one lane per candidate at every width
+        const uint32_t lgL = 0u;
+#else
         const uint32_t lgL = W <= WREG ? 0u : nex <= 8 ? 3u : nex <= 16 ? 2u : nex <= 32 ? 1u : 0u;
+#endif
         const uint32_t lgW = W <= 4 ? 0u : W <= 8 ? 1u : W <= 16 ? 2u : 3u;  // no more lanes than 4-word chunks
         const uint32_t lg = lgL < lgW ? lgL : lgW;
         const uint32_t cx = lane >> lg, sub = lane & ((1u << lg) - 1u);
@@ -1560,7 +1573,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
           n_xwin++;
 #endif
-        if (W > WREG) {
+        if (GS_ADD_LANES && W > WREG) {
           // the winner's option words after Add, one lane per word (one
           // round trip per 64 words instead of one per word): its threshold
           // rows and offering grid come from its lane
@@ -1593,6 +1606,19 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   #pragma unroll
             for (uint32_t w = 0; w < WREG; w++)
               if (w < W) opts[w] = nx[w];  // already narrowed to the grid
+          } else if (!GS_ADD_LANES) {
+            const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
+            for (uint32_t w = 0; w < W; w++) {
+              uint64_t x = opts[w] & row[w];
+  #pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
+              if (G != Gt) {
+                uint64_t off = 0;
+                for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                x &= off;
+              }
+              opts[w] = x;
+            }
           }
           int64_t nt[RR], ma[RR];
           uint32_t cu[RR];

@@ -310,7 +310,7 @@ extern "C" __global__ __launch_bounds__(BLOCK) void trunc_kernel(DevProblem d, u
 extern "C" __global__ __launch_bounds__(BLOCK) void sim_fix_kernel(DevProblem d) {
   const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
   if (s >= d.n_sims) return;
-  Ctrl& c = d.sim_ctrl[s];
+  SimCtrl& c = d.sim_ctrl[s];
   if (c.status) return;
   const uint32_t off = d.sim_pod_off[s], nc = c.n_claims;
   uint32_t surv = 0, sj = NONE;

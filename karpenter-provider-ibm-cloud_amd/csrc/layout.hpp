@@ -28,6 +28,16 @@ namespace gsd {
 
 constexpr int RMAX = 8;        // resource dimensions per vector
 constexpr int KMAX_IT = 8;     // requirement keys carried by instance types
+// simulations with at most OVH_MAX overlay entries keep their node -> entry
+// map in an LDS hash (2 slots per entry, power of two) instead of a per-block
+// NN-entry array in HBM
+constexpr uint32_t OVH_MAX = 128;
+inline uint32_t ovh_slots_for(uint32_t ov_cap) {
+  if (ov_cap > OVH_MAX) return 0;
+  uint32_t s = 16;
+  while (s < 2 * ov_cap) s <<= 1;
+  return s;
+}
 constexpr int FMAX = 16;       // "free" key slots (keys on neither ITs nor offerings)
 constexpr int TMAX = 64;       // NodeClaim templates (NodePools)
 constexpr uint32_t THR_LDS_MAX = 2048;   // fit thresholds staged in the FFD kernel's LDS
@@ -53,7 +63,10 @@ enum : uint32_t { VF_SIMPLE = 1u << 31 };
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)
 enum : uint32_t { FK_PRESENT = 1u, FK_COMP = 2u, FK_GT = 4u, FK_LT = 8u };
-constexpr int FKW = 4;          // words of a free key's value bitsets (<= 256 vocabulary values, omega included)
+#ifndef GS_FKW
+#define GS_FKW 4
+#endif
+constexpr int FKW = GS_FKW;     // words of a free key's value bitsets (<= 256 vocabulary values, omega included)
 constexpr int FKV = 64 * FKW;
 struct FK {
   uint64_t has[FKW];   // Has(v) for each vocabulary value
@@ -202,6 +215,12 @@ struct Ctrl {
   uint64_t dbg[16];                            // diagnostic phase counters
 };
 
+// a consolidation simulation's outcome: one 16-B store per simulation (the
+// counters of Ctrl are summed per workgroup into DevProblem::sim_blk)
+struct SimCtrl {
+  uint32_t status, n_claims, n_log, failed;
+};
+
 struct DevProblem {
   // sizes
   uint32_t N, W, R, Z, C, T, F, V, P, K, NT;  // K = IT keys, NT = taint vocab
@@ -342,7 +361,8 @@ struct DevProblem {
   const uint32_t* sim_cands;   // node positions removed by each simulation
   int64_t* ov_req;             // [grid][ov_cap][RMAX]
   FK* ov_fk;                   // [grid][ov_cap][F]
-  Ctrl* sim_ctrl;              // [n_sims]
+  SimCtrl* sim_ctrl;           // [n_sims]
+  Ctrl* sim_blk;               // [grid] per-workgroup sums of the simulations' counters
   ClaimRec* sim_hdr;           // [n_sims] header of the single NodeClaim (trunc_kernel copies it)
   uint32_t* sim_next;          // work counter (reset before each launch)
   // simulations with topology groups / volumes: per simulation the zone
@@ -358,6 +378,7 @@ struct DevProblem {
   NodeVol* ov_vol;             // [grid][ov_cap]
   uint32_t ov_epoch;            // 1..4095: the launch's stamp prefix (ov_hn zeroed when it wraps)
   uint32_t* ov_map;            // [grid][NN] a touched node's overlay entry (valid where the LDS bitmap bit is set)
+  uint32_t ovh_slots;          // > 0: simulations this small keep node -> entry in an LDS hash of that many slots instead
 };
 
 // the parent-side merge of a sharded static matrix (kernels.hip

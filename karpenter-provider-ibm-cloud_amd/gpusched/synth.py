@@ -524,12 +524,15 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
     return b.build()
 
 
-def random_topology(seed, n_pods=None):
+def random_topology(seed, n_pods=None, taint_policy=None):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
     with node affinity), NodePools with and without zone requirements,
-    existing nodes with labelled bound pods, taints and relaxation"""
+    existing nodes with labelled bound pods, taints and relaxation.
+    taint_policy "Honor" / "Ignore": every pod with a spread tolerates the
+    NodePools' taint and its spreads carry that nodeTaintsPolicy (the random
+    stream is the same for both, so the two problems differ only in it)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
@@ -602,6 +605,10 @@ def random_topology(seed, n_pods=None):
         if rng.random() < 0.1 and not spreads:
             sel["topology.kubernetes.io/zone"] = str(rng.choice(zones))
         tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+        if taint_policy and spreads:
+            tols = [("dedicated", "Exists", "", "")]
+            for sp in spreads:
+                sp["node_taints_policy"] = taint_policy
         labels = {"app": app}
         if rng.random() < 0.6:
             labels["pod-template-hash"] = str(rng.choice(["h1", "h2"]))

@@ -367,6 +367,7 @@ struct Spread {
   };
   vector<Expr> exprs;
   bool ignore_affinity = false;
+  bool honor_taints = false;  // nodeTaintsPolicy Honor (checked in Builder::check_taint_policy)
   // metav1.LabelSelector over a pod's labels (nil selects nothing)
   bool matches(const std::map<string, string>& labels) const {
     if (!has_selector) return false;
@@ -696,9 +697,10 @@ struct Builder {
       if (sp.key != kZone && sp.key != kHostname)
         throw Unsupported{GS_E_UNSUPPORTED, "topology spread key other than zone / hostname"};
       if (q.max_skew < 1) throw Unsupported{GS_E_INVALID, "maxSkew < 1"};
-      if (q.node_taints_policy != GS_POLICY_IGNORE) throw Unsupported{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor"};
-      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE)
+      if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE ||
+          q.node_taints_policy > GS_POLICY_IGNORE)
         throw Unsupported{GS_E_INVALID, "bad topology spread enum"};
+      sp.honor_taints = q.node_taints_policy == GS_POLICY_HONOR;
       sp.max_skew = q.max_skew;
       sp.schedule_anyway = q.when_unsatisfiable == GS_SPREAD_SCHEDULE_ANYWAY;
       if (q.min_domains > 0) sp.min_domains = q.min_domains;
@@ -920,6 +922,24 @@ struct Builder {
     }
   }
 
+  // <U> TopologyNodeFilter.Matches with TaintPolicy Honor: a node or
+  // NodeClaim counts in the group (Record, countDomains) and its domain enters
+  // the minimum (TopologyDomainGroup.ForEachDomain) only if the owner
+  // tolerates its taints.  When the owner tolerates every NodePool and node
+  // taint of the problem the filter always matches and Honor equals Ignore;
+  // otherwise refused (the product refuses the same inputs)
+  void check_taint_policy() {
+    vector<Taint> all;
+    for (uint32_t i = 0; i < p->n_nodepools; i++)
+      for (auto& t : taints_of(p->nodepools[i].taints)) all.push_back(t);
+    for (uint32_t i = 0; i < p->n_nodes; i++)
+      for (auto& t : taints_of(p->nodes[i].taints)) all.push_back(t);
+    for (auto& pd : st.pods)
+      for (auto& sp : pd.spreads)
+        if (sp.honor_taints && !tolerates_all(all, pd.tolerations))
+          throw Unsupported{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor with a taint its owner does not tolerate"};
+  }
+
   void build() {
     st.strings.clear();
     for (uint32_t i = 0; i < p->n_strings; i++) st.strings.push_back(p->strings[i] ? p->strings[i] : "");
@@ -1041,6 +1061,7 @@ struct Builder {
         n.vol_limits[str(l.driver)] = l.limit;
       }
     }
+    check_taint_policy();
     st.node_order.resize(p->n_nodes);
     for (uint32_t i = 0; i < p->n_nodes; i++) st.node_order[i] = i;
     std::stable_sort(st.node_order.begin(), st.node_order.end(), [&](uint32_t a, uint32_t b) {

@@ -105,13 +105,41 @@ def test_refusals():
     b = _base(n_pods=1, spread={"key": "karpenter.sh/capacity-type", "max_skew": 1, "selector": {}})
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+    # nodeTaintsPolicy Honor with a taint the owner does not tolerate
     b = _base(n_pods=1, spread={"key": Z, "max_skew": 1, "selector": {}, "node_taints_policy": "Honor"})
+    b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0},
+               taints=[("dedicated", "x", "NoSchedule")])
+    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
     b = _base(n_pods=0)
     b.add_pod("x", 0, {"cpu": 1}, node_selector={Z: "us-south-1"},
               spreads=[{"key": Z, "max_skew": 1, "selector": {}}])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+def test_taint_policy_honor_without_taints_equals_ignore():
+    """TopologyNodeFilter.Matches: with no taint in the problem Honor filters
+    nothing (the group is the Ignore group)"""
+    out = []
+    for pol in ("Honor", "Ignore"):
+        b = _base(n_pods=4, spread={"key": Z, "max_skew": 1, "selector": {}, "node_taints_policy": pol})
+        st, res, _ = pyoracle.solve(b.build())
+        assert st == abi.GS_OK and lib.validate(b.build())[0] == abi.GS_OK
+        out.append(_zones(res))
+    assert out[0] == out[1] and len(out[0]) == 3
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_taint_policy_honor_tolerated_equals_ignore(seed):
+    """owners that tolerate every NodePool / node taint: Honor == Ignore,
+    accepted by the encoder and the oracle alike"""
+    ph = synth.random_topology(seed, taint_policy="Honor")
+    pi = synth.random_topology(seed, taint_policy="Ignore")
+    sh, rh, _ = pyoracle.solve(ph)
+    si, ri, _ = pyoracle.solve(pi)
+    assert sh == si == abi.GS_OK and rh == ri
+    assert lib.validate(ph)[0] == abi.GS_OK
 
 
 @pytest.mark.parametrize("seed", range(40))
@@ -143,6 +171,12 @@ def _check(solver, p):
 @pytest.mark.parametrize("seed", range(150))
 def test_gpu_topology_random(solver, seed):
     _check(solver, synth.random_topology(seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(20))
+def test_gpu_topology_taint_policy_honor(solver, seed):
+    _check(solver, synth.random_topology(seed, taint_policy="Honor"))
 
 
 @pytest.mark.gpu
