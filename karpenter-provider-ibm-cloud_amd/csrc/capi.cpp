@@ -215,7 +215,12 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->alloc(d.ctrl, 1);
   c->alloc(d.c_its, (sims ? NS : CA) * 60);
   c->alloc(d.c_nits, sims ? NS : CA);
-  c->alloc(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
+  // simulations keep the NodeClaims' hostname counts zero at rest (ffd.hip):
+  // zeroed once per upload
+  if (sims)
+    c->alloc_zero(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
+  else
+    c->alloc(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
   if (sims) {
     d.n_sims = (uint32_t)NS;
     d.sim_nt = sims->nt;

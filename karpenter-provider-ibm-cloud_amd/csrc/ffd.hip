@@ -571,7 +571,10 @@ struct Blk {
 // kernel's HBM bytes on C4); at 3 (168 registers) the narrow shape is
 // spill-free.  The wide shape keeps 4: its few long simulations gain more
 // from residency than they lose to the spills.
-constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? 3 : 4; }
+#ifndef GS_SIM_NARROW_WPE  // experiment builds: the narrow shape's waves per SIMD
+#define GS_SIM_NARROW_WPE 3
+#endif
+constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? GS_SIM_NARROW_WPE : 4; }
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
 constexpr uint32_t OV_FK = 0x40000000u;    // the entry holds its own free-key state (copied on the first Add that needs it)
 
@@ -1686,8 +1689,9 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           cr->thr(tid) = (uint16_t)c0;
           S.red64[tid] = 0;
         }
-        // <U> Topology.Register(hostname placeholder): the claim's counts start at 0
-        if (TOPO) {
+        // <U> Topology.Register(hostname placeholder): the claim's counts start
+        // at 0 (simulations: the rows are zero at rest, see the sim's end)
+        if (TOPO && !SIM) {
           for (uint32_t h = tid; h < d.TGH; h += FB) d.hc[(size_t)(cbase + j) * d.TGH + h] = 0;
           __syncthreads();
         }
@@ -1791,6 +1795,22 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
     __syncthreads();
     if (!SIM)
       for (uint32_t i = tid; i < S.hb[par ^ 1u].M; i += FB) d.c_sorted[i] = s_ord[i];
+    if (SIM && TOPO && d.TGH) {
+      // the NodeClaims' hostname counts back to zero, cell by recorded cell
+      // (a pod placed on NodeClaim j counted in the hostname groups of its
+      // selection list), so the next simulation's NodeClaims start from zero
+      // rows without writing TGH counts each
+      for (uint32_t i = tid; i < S.hb[par ^ 1u].nlog; i += FB) {
+        const LogRec l = logp[i];
+        if (l.target & 0x80000000u) continue;
+        const VarRec& lv = d.vars[l.var];
+        int32_t* hrow = d.hc + (size_t)(qoff + l.target) * d.TGH;
+        for (uint32_t k = 0; k < lv.sel_n; k++) {
+          const uint32_t e = d.tg_list[lv.sel_off + k];
+          if ((e >> 24) & TK_HOST) hrow[e & 0xFFFFFFu] = 0;
+        }
+      }
+    }
     if (SIM) {
       // SimulateScheduling's error pods that are not pending: still queued,
       // or placed on an uninitialized existing node

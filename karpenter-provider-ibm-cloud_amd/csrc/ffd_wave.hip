@@ -32,7 +32,7 @@ extern "C" __global__ __launch_bounds__(256) void ffd_init_kernel(DevProblem d) 
 extern "C" uint32_t gsk_ffd_lds_bytes(uint32_t max_claims, uint32_t nthr, uint32_t nb_words,
                                       uint32_t topo_bytes);
 #define GSK_DECL(n, t)                                                                                  \
-  extern "C" hipError_t gsk_ffdw_launch_r##n##_t##t(const DevProblem* d, uint32_t ch, uint32_t lds, hipStream_t s); \
+  extern "C" hipError_t gsk_ffdw_launch_r##n##_t##t(const DevProblem* d, uint32_t mode, uint32_t lds, hipStream_t s); \
   extern "C" hipError_t gsk_ffdw_attr_r##n##_t##t(uint32_t lds_total, uint32_t* dyn_min);
 #define GSK_DECL2(n) GSK_DECL(n, 0) GSK_DECL(n, 1)
 GSK_DECL2(1) GSK_DECL2(2) GSK_DECL2(3) GSK_DECL2(4) GSK_DECL2(5) GSK_DECL2(6) GSK_DECL2(7) GSK_DECL2(8)
@@ -65,10 +65,11 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, uint32_t ch, hipStream_t s) 
   if (ch && !(d->ch_slk && d->ch_rm && d->ch_so && d->ch_scr && d->ch_tmpl)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ffd_init_kernel, dim3(256), dim3(256), 0, s, *d);
   const bool topo = d->TG || d->any_mv || d->any_vol;
+  const uint32_t mode = (ch ? 1u : 0u) | (d->W > WREG ? 2u : 0u);
   switch (d->R * 2 + (topo ? 1 : 0)) {
 #define GSK_CASE(n)                                                     \
-  case 2 * n: return gsk_ffdw_launch_r##n##_t0(d, ch, lds, s);          \
-  case 2 * n + 1: return gsk_ffdw_launch_r##n##_t1(d, ch, lds, s);
+  case 2 * n: return gsk_ffdw_launch_r##n##_t0(d, mode, lds, s);        \
+  case 2 * n + 1: return gsk_ffdw_launch_r##n##_t1(d, mode, lds, s);
     GSK_CASE(1) GSK_CASE(2) GSK_CASE(3) GSK_CASE(4) GSK_CASE(5) GSK_CASE(6) GSK_CASE(7) GSK_CASE(8)
 #undef GSK_CASE
     default:

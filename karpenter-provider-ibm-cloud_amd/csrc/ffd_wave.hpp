@@ -652,7 +652,10 @@ __device__ __forceinline__ bool pivot_touched(uint32_t modkind, uint32_t modpos,
 // CH: the claim scan state (slack, room, sorted order, sort scratch,
 // template) lives in HBM instead of LDS -- a Solve with more NodeClaims than
 // the LDS holds (capi gs_run reruns it so)
-template <uint32_t RR, bool TOPO, bool CH = false>
+// WIDE: option rows of more than WREG words (the launcher picks it from d.W):
+// the narrow instantiation keeps a candidate's words in registers and
+// carries none of the wide rows' lane-split code, and the other way round
+template <uint32_t RR, bool TOPO, bool CH = false, bool WIDE = false>
 __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
@@ -684,6 +687,10 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   const uint32_t thr_base = (23u * MCL + 7u) & ~7u;
   int64_t* s_thr = (int64_t*)((char*)lds64 + thr_base);
   const uint32_t W = d.W, F = d.F, T = d.T, OW = d.OW, P = d.P;
+  if (WIDE)
+    __builtin_assume(W > WREG);
+  else
+    __builtin_assume(W <= WREG);
   const uint32_t nthr = d.thr_off[R];
   const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
   const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
@@ -1411,7 +1418,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_NO_EXACT_LANES  // experiment builds: one lane per candidate at every width
         const uint32_t lgL = 0u;
 #else
-        const uint32_t lgL = W <= WREG ? 0u : nex <= 8 ? 3u : nex <= 16 ? 2u : nex <= 32 ? 1u : 0u;
+        const uint32_t lgL = !WIDE ? 0u : nex <= 8 ? 3u : nex <= 16 ? 2u : nex <= 32 ? 1u : 0u;
 #endif
         const uint32_t lgW = W <= 4 ? 0u : W <= 8 ? 1u : W <= 16 ? 2u : 3u;  // no more lanes than 4-word chunks
         const uint32_t lg = lgL < lgW ? lgL : lgW;
@@ -1447,7 +1454,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         }
         const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
         const uint64_t* opts = KD.c_opts + (size_t)j * OW;
-        if (W <= WREG) {
+        if (!WIDE) {
           const uint4* oq = (const uint4*)opts;
           const uint4* rq4 = (const uint4*)row;
           const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
@@ -1486,7 +1493,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             mrow[r] = o + r + mm[r];
           }
           uint64_t accw = 0;
-          if (W <= WREG) {
+          if (!WIDE) {
             // opts ⊆ thr_set[cur] (invariant of every Add): only a resource
             // whose cursor moves narrows the options further
 #pragma unroll
@@ -1551,7 +1558,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if (TOPO && feas && KD.tmpl[t].mv_mask) {
             // minValues over the NodeClaim's options after Add (per lane)
             feas = mv_ok(KD, KD.tmpl[t], [&](uint32_t w) -> uint64_t {
-              if (W <= WREG) return w == 0 ? nx[0] : w == 1 ? nx[1] : w == 2 ? nx[2] : nx[3];
+              if (!WIDE) return w == 0 ? nx[0] : w == 1 ? nx[1] : w == 2 ? nx[2] : nx[3];
               uint64_t x = opts[w] & row[w];
 #pragma unroll
               for (uint32_t r = 0; r < RR; r++) x &= KD.thr_set[(size_t)mrow[r] * OW + w];
@@ -1573,7 +1580,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifdef GS_FFD_TL
           n_xwin++;
 #endif
-        if (GS_ADD_LANES && W > WREG) {
+        if (GS_ADD_LANES && WIDE) {
           // the winner's option words after Add, one lane per word (one
           // round trip per 64 words instead of one per word): its threshold
           // rows and offering grid come from its lane
@@ -1602,11 +1609,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           // requests, requirements
           ClaimRec* cr = KD.c_rec + j;
           uint64_t* opts = KD.c_opts + (size_t)j * OW;
-          if (W <= WREG) {
+          if (!WIDE) {
   #pragma unroll
             for (uint32_t w = 0; w < WREG; w++)
               if (w < W) opts[w] = nx[w];  // already narrowed to the grid
-          } else if (!GS_ADD_LANES) {
+          } else if (WIDE && !GS_ADD_LANES) {
             const uint64_t* row = KD.rows + ((size_t)v * T + t) * OW;
             for (uint32_t w = 0; w < W; w++) {
               uint64_t x = opts[w] & row[w];

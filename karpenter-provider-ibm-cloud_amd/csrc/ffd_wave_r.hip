@@ -1,7 +1,7 @@
 // ffd_wave_r.hip — the instantiations of ffdw_kernel (ffd_wave.hpp) for one
 // resource count GS_WAVE_R and one variant GS_WAVE_TOPO (0: the plain
 // variant, 1: the general one), with the claim scan state in LDS (register
-// mode) or in HBM (ch): compiled once per (R, TOPO) so the large register-
+// mode) or in HBM (ch), for narrow and wide option rows: compiled once per (R, TOPO) so the large register-
 // mode bodies build in parallel (Makefile ffd_wave_r<R>_t<T>.o).
 #include "ffd_wave.hpp"
 
@@ -16,9 +16,9 @@ using namespace gsd;
 #define GSK_LAUNCH GSK_CAT(gsk_ffdw_launch_r, GS_WAVE_R, _t, GS_WAVE_TOPO)
 #define GSK_ATTR GSK_CAT(gsk_ffdw_attr_r, GS_WAVE_R, _t, GS_WAVE_TOPO)
 
-template <bool CH>
+template <bool CH, bool WIDE>
 static hipError_t ffdw_attr_one(uint32_t lds_total, uint32_t* dyn_min) {
-  const void* fn = (const void*)ffdw_kernel<GS_WAVE_R, GS_WAVE_TOPO != 0, CH>;
+  const void* fn = (const void*)ffdw_kernel<GS_WAVE_R, GS_WAVE_TOPO != 0, CH, WIDE>;
   hipFuncAttributes a;
   hipError_t e = hipFuncGetAttributes(&a, fn);
   if (e != hipSuccess) return e;
@@ -28,14 +28,21 @@ static hipError_t ffdw_attr_one(uint32_t lds_total, uint32_t* dyn_min) {
 }
 
 extern "C" hipError_t GSK_ATTR(uint32_t lds_total, uint32_t* dyn_min) {
-  const hipError_t a = ffdw_attr_one<false>(lds_total, dyn_min), b = ffdw_attr_one<true>(lds_total, dyn_min);
-  return a != hipSuccess ? a : b;
+  const hipError_t e[4] = {ffdw_attr_one<false, false>(lds_total, dyn_min), ffdw_attr_one<true, false>(lds_total, dyn_min),
+                           ffdw_attr_one<false, true>(lds_total, dyn_min), ffdw_attr_one<true, true>(lds_total, dyn_min)};
+  for (hipError_t x : e)
+    if (x != hipSuccess) return x;
+  return hipSuccess;
 }
 
-extern "C" hipError_t GSK_LAUNCH(const DevProblem* d, uint32_t ch, uint32_t lds, hipStream_t s) {
-  if (ch)
-    hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, GS_WAVE_TOPO != 0, true>), dim3(1), dim3(128), lds, s, *d);
-  else
-    hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, GS_WAVE_TOPO != 0, false>), dim3(1), dim3(128), lds, s, *d);
+// mode: bit 0 = claim scan state in HBM, bit 1 = wide option rows (W > WREG)
+extern "C" hipError_t GSK_LAUNCH(const DevProblem* d, uint32_t mode, uint32_t lds, hipStream_t s) {
+  constexpr bool T = GS_WAVE_TOPO != 0;
+  switch (mode & 3u) {
+    case 0: hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, T, false, false>), dim3(1), dim3(128), lds, s, *d); break;
+    case 1: hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, T, true, false>), dim3(1), dim3(128), lds, s, *d); break;
+    case 2: hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, T, false, true>), dim3(1), dim3(128), lds, s, *d); break;
+    default: hipLaunchKernelGGL((ffdw_kernel<GS_WAVE_R, T, true, true>), dim3(1), dim3(128), lds, s, *d); break;
+  }
   return hipGetLastError();
 }
