@@ -1283,9 +1283,12 @@ struct Ctx {
   };
   std::map<TaintKey, uint32_t> taint_id;
   std::vector<TaintKey> taint_list;
-  uint64_t taint_mask(gs_range r) {
+  // the distinct taints of a NodePool / node (raw ids); the device masks are
+  // over taint classes (build_taint_classes), so the raw vocabulary may
+  // exceed 64
+  std::vector<uint32_t> taint_ids(gs_range r) {
     chk(r, p->n_taints, "taints");
-    uint64_t m = 0;
+    std::vector<uint32_t> ids;
     for (uint32_t i = 0; i < r.count; i++) {
       auto& t = p->taints[r.begin + i];
       TaintKey tk{S(t.key), S(t.value), S(t.effect)};
@@ -1293,36 +1296,75 @@ struct Ctx {
       uint32_t id;
       if (f == taint_id.end()) {
         id = (uint32_t)taint_list.size();
-        if (id >= 64) throw Fail{GS_E_UNSUPPORTED, "more than 64 distinct taints"};
+        if (id >= (1u << 16)) throw Fail{GS_E_UNSUPPORTED, "more than 65536 distinct taints"};
         taint_id[tk] = id;
         taint_list.push_back(tk);
       } else {
         id = f->second;
       }
-      m |= 1ull << id;
+      ids.push_back(id);
     }
-    return m;
+    return ids;
   }
+  std::vector<std::vector<uint32_t>> tmpl_taints, node_taints;  // raw ids per template / node position
   struct Tol {
     std::string k, v, eff;
     uint32_t op;
   };
-  uint64_t tol_mask(const std::vector<Tol>& tols) const {
-    uint64_t m = 0;
-    for (uint32_t id = 0; id < taint_list.size(); id++) {
-      auto& tn = taint_list[id];
-      for (auto& t : tols) {
-        // corev1 Toleration.ToleratesTaint
-        if (!t.eff.empty() && t.eff != tn.eff) continue;
-        if (!t.k.empty() && t.k != tn.k) continue;
-        if (t.op == GS_TOL_EQUAL ? t.v == tn.v : t.op == GS_TOL_EXISTS) {
-          m |= 1ull << id;
-          break;
-        }
-      }
+  // corev1 Toleration.ToleratesTaint by some toleration of the list
+  static bool tolerated(const std::vector<Tol>& tols, const TaintKey& tn) {
+    for (auto& t : tols) {
+      if (!t.eff.empty() && t.eff != tn.eff) continue;
+      if (!t.k.empty() && t.k != tn.k) continue;
+      if (t.op == GS_TOL_EQUAL ? t.v == tn.v : t.op == GS_TOL_EXISTS) return true;
     }
-    return m;
+    return false;
   }
+  // Taint classes: two taints that exactly the same spec variants tolerate are
+  // interchangeable in every Taints.ToleratesPod (a NodePool / node is
+  // tolerated iff each of its taints is), so the device masks carry one bit
+  // per class of equal toleration pattern; more than 64 classes is refused.
+  // Sets the templates' and nodes' taint masks and every variant's tol / tolt.
+  void build_taint_classes() {
+    const size_t NSV = variant_tols.size(), NW = (NSV + 63) / 64;
+    std::map<std::vector<uint64_t>, uint32_t> cls_of;
+    std::vector<uint32_t> cls(taint_list.size());
+    std::vector<uint64_t> sv_tol(NSV, 0);
+    std::vector<uint64_t> sig(NW);
+    for (size_t id = 0; id < taint_list.size(); id++) {
+      std::fill(sig.begin(), sig.end(), 0ull);
+      for (size_t sv = 0; sv < NSV; sv++)
+        if (tolerated(variant_tols[sv], taint_list[id])) sig[sv / 64] |= 1ull << (sv % 64);
+      auto f = cls_of.find(sig);
+      if (f == cls_of.end()) {
+        if (cls_of.size() >= 64) throw Fail{GS_E_UNSUPPORTED, "more than 64 taint classes (distinct toleration patterns over the taints)"};
+        const uint32_t c = (uint32_t)cls_of.size();
+        f = cls_of.emplace(sig, c).first;
+        for (size_t sv = 0; sv < NSV; sv++)
+          if (sig[sv / 64] >> (sv % 64) & 1) sv_tol[sv] |= 1ull << c;
+      }
+      cls[id] = f->second;
+    }
+    n_taint_classes = (uint32_t)cls_of.size();
+    auto mask = [&](const std::vector<uint32_t>& ids) {
+      uint64_t m = 0;
+      for (uint32_t id : ids) m |= 1ull << cls[id];
+      return m;
+    };
+    for (uint32_t t = 0; t < e.T; t++) e.tmpl[t].taints = mask(tmpl_taints[t]);
+    for (uint32_t pos = 0; pos < e.NN; pos++) e.nodes[pos].taints = mask(node_taints[pos]);
+    for (uint32_t v = 0; v < e.V; v++) {
+      gsd::VarRec& vr = e.vars[v];
+      vr.tol = sv_tol[e.var_sv[v]];
+      vr.tolt = 0;
+      for (uint32_t t = 0; t < e.T; t++)
+        if ((e.tmpl[t].taints & ~vr.tol) == 0) vr.tolt |= 1ull << t;
+    }
+    for (size_t sv = 0; sv < NSV; sv++) e.variants[sv].tol = sv_tol[sv];
+    final_sv_tol = std::move(sv_tol);
+  }
+  uint32_t n_taint_classes = 0;
+  std::vector<uint64_t> final_sv_tol;
 
   // --------------------------------------------------------- templates
   bool tolerate_pns = false;
@@ -1385,7 +1427,7 @@ struct Ctx {
         opts[i / 64] |= 1ull << (i % 64);
         any = true;
       }
-      uint64_t tm = taint_mask(np.taints);
+      std::vector<uint32_t> tm = taint_ids(np.taints);
       np_universe.emplace_back(tr, has_its);
       // <U> minValues (Strict): NewScheduler's filterInstanceTypesByRequirements
       // drops the NodePool when its options miss a minimum.  Instance types
@@ -1414,7 +1456,7 @@ struct Ctx {
       t.np_index = npi;
       t.zm = zm;
       t.cm = cm;
-      t.taints = tm;
+      t.taints = 0;  // build_taint_classes
       bool present[gsd::RMAX] = {false};
       resvec_fn(np.daemon_requests, t.daemon, nullptr);
       if (np.has_limits) {
@@ -1445,6 +1487,7 @@ struct Ctx {
       for (int k = 0; k < gsd::KMAX_IT; k++) t.mv[k] = mvk[k];
       if (mv_mask) e.any_mv = true;
       e.tmpl.push_back(t);
+      tmpl_taints.push_back(std::move(tm));
       e.t_opts.insert(e.t_opts.end(), opts.begin(), opts.end());
       e.tmpl_reqs.push_back(tr);
       e.T++;
@@ -1724,7 +1767,7 @@ struct Ctx {
         reqs_add_all(e, v.reqs, w.req_terms[ri]);
         reqs_add_all(e, v.strict, w.req_terms[ri]);
       }
-      v.tol = tol_mask(tols);
+      v.tol = 0;  // build_taint_classes
       for (uint32_t k : cur) v.own.push_back(w.sgid[k]);
       v.own.insert(v.own.end(), w.own_static.begin(), w.own_static.end());
       for (size_t k = ai; k < w.anti_pref.size(); k++) v.own.push_back(w.anti_pref[k].second);
@@ -2019,10 +2062,7 @@ struct Ctx {
       vr.zs = zone_full(pv.strict);
       vr.zn = zone_full(pv.reqs);
       vr.zflags = zone_flags(pv.reqs);
-      vr.tol = pv.tol;
-      vr.tolt = 0;
-      for (uint32_t t = 0; t < e.T; t++)
-        if ((e.tmpl[t].taints & ~pv.tol) == 0) vr.tolt |= 1ull << t;
+      vr.tol = vr.tolt = 0;  // build_taint_classes
       vr.fk_begin = (uint32_t)e.fk_entries.size();
       for (auto& kv : pv.reqs)
         if (e.keys[kv.first].cls == KEY_FREE) {
@@ -2112,6 +2152,7 @@ struct Ctx {
     });
     e.node_order = order;
     e.nodes.assign(e.NN, gsd::NodeRec{});
+    node_taints.assign(e.NN, {});
     e.n_fk.assign((size_t)std::max<uint32_t>(e.NN, 1) * std::max<uint32_t>(e.F, 1), gsd::FK{});
     // keys some pod variant constrains with NotIn/DoesNotExist: a node lacking
     // such a non-free key would gain dynamic state there (refused below)
@@ -2151,18 +2192,17 @@ struct Ctx {
       for (uint32_t r = 0; r < e.R; r++)
         if (present[r] && nr.avail[r] < 0) nr.ok = 0;  // <U> Fits: negative total never fits
       resvec_fn(g.requests, nr.req, nullptr);
-      nr.taints = taint_mask(g.taints);
+      nr.taints = 0;  // build_taint_classes
+      node_taints[pos] = taint_ids(g.taints);
       nr.init = g.initialized ? 1u : 0u;
     }
-    // taints of nodes enter the vocabulary after the pods' tolerations were
-    // encoded: recompute the tolerated masks over the final vocabulary
-    std::vector<uint64_t> sv_tol(variant_tols.size());
-    for (size_t sv = 0; sv < variant_tols.size(); sv++) sv_tol[sv] = tol_mask(variant_tols[sv]);
-    for (uint32_t v = 0; v < e.V; v++) e.vars[v].tol = sv_tol[e.var_sv[v]];
+    // every taint is known now (NodePools', then nodes'): the class masks
+    build_taint_classes();
+    const std::vector<uint64_t>& sv_tol = final_sv_tol;
     // nodeTaintsPolicy Honor: the group's filter holds the owner's own
     // tolerations (before Relax adds PreferNoSchedule); tolerating every
     // NodePool and node taint makes TopologyNodeFilter.Matches always true
-    const uint64_t all_taints = taint_list.size() >= 64 ? ~0ull : (1ull << taint_list.size()) - 1;
+    const uint64_t all_taints = n_taint_classes >= 64 ? ~0ull : (1ull << n_taint_classes) - 1;
     for (uint32_t s : honor_specs)
       if (all_taints & ~sv_tol[sv_begin[s]])
         throw Fail{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor with a taint its owner does not tolerate"};

@@ -1,13 +1,15 @@
 #!/bin/bash
 # round-4: the narrow simulation shape at 2 waves per SIMD (no VGPR spills,
 # 4 workgroups per CU) against 3 (spills, 6 per CU): consolidation timings and
-# write traffic
+# write traffic (after the taint-class parity tests)
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r4q
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_taint_classes.py tests/test_topology.py tests/test_gpu_parity.py tests/test_consolidation.py -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
   for v in base w2; do
     lib=libgpusched_$v.so; [ "$v" = base ] && lib=libgpusched.so
