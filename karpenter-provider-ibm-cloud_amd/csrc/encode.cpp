@@ -2059,6 +2059,9 @@ struct Ctx {
       vr.zm = zone_has(pv.reqs);
       vr.cm = ct_has(pv.reqs);
       vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && pv.own.empty() ? gsd::VF_SIMPLE : 0u);
+      // owns a zone spread group: only those read the per-pod minimum counts
+      for (uint32_t g : pv.own)
+        if (groups[g].sp.key == kZone && groups[g].kind == 0) vr.ctb |= gsd::VF_ZSPREAD;
       vr.zs = zone_full(pv.strict);
       vr.zn = zone_full(pv.reqs);
       vr.zflags = zone_flags(pv.reqs);

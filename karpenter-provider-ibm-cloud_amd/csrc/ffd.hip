@@ -926,10 +926,15 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
       // topology: the groups the pod owns (own list) and that count it (selection list)
       const uint32_t own_n = TOPO ? vr.own_n : 0u, own_off = TOPO ? vr.own_off : 0u;
       const uint32_t sel_n = TOPO ? vr.sel_n : 0u, sel_off = TOPO ? vr.sel_off : 0u;
+      // the owned groups staged in LDS (the topology checks of every node /
+      // NodeClaim candidate read them there instead of two dependent loads)
+      __shared__ OwnG s_own[OWNMAX];
       if (TOPO && own_n) {
-        if (tid < 64) topo_tmin(d, ts, own_off, own_n, vr.zs, tid);
+        if (tid < own_n) s_own[tid] = OwnMem<DevProblem>{d, own_off}(tid);
+        if (tid < 64 && (vr.ctb & VF_ZSPREAD)) topo_tmin(d, ts, own_off, own_n, vr.zs, tid);
         __syncthreads();
       }
+      auto OWN = [&](uint32_t k) -> OwnG { return s_own[k]; };
 
       // --------------- existing nodes in order: first ExistingNode.CanAdd wins
       if (d.NN) {
@@ -981,7 +986,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
             if (TOPO && feas && own_n)
-              feas = topo_node_ok(d, ts, own_off, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
+              feas = topo_node_ok_g(d, ts, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
                 if (!SIM) return d.hn[(size_t)hs * d.NN + n];
                 // an overlay cell counts only where this simulation wrote it
                 // (its stamp); other groups keep the node's base count
@@ -990,7 +995,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
                   if ((uint32_t)(x >> 32) == ov_stamp) return (int32_t)(uint32_t)x;
                 }
                 return d.hn0[(size_t)hs * d.NN + n];
-              });
+              }, OWN);
             if (TOPO && feas && d.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
               const NodeVol& nv = !SIM ? d.n_vol[n] : oe != ~(size_t)0 ? d.ov_vol[oe] : d.n_vol0[n];
@@ -1322,7 +1327,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               czf = cr->zfull;
               czfl = cr->zflags;
               const int32_t* hrow = dd.hc + (size_t)(cb + j) * dd.TGH;
-              zset = topo_claim(dd, ts, own_off, own_n, czf & vr.zn, [&](uint32_t hs) -> int64_t { return hrow[hs]; });
+              zset = topo_claim_g(dd, ts, own_n, czf & vr.zn, [&](uint32_t hs) -> int64_t { return hrow[hs]; }, OWN);
               pre = zset != 0;
               if (pre && zset != ~0ull) zm &= topo_catmask(dd, zset);
             }
@@ -1603,7 +1608,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         // bootstrap of a self-selecting pod while no selected pod runs)
         uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
         if (TOPO && own_n) {
-          tzs = topo_claim(d, ts, own_off, own_n, tr.zfull & vr.zn, [](uint32_t) -> int64_t { return 0; });
+          tzs = topo_claim_g(d, ts, own_n, tr.zfull & vr.zn, [](uint32_t) -> int64_t { return 0; }, OWN);
           if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(d, tzs);
           if (tzs == 0 || tzcat == 0) continue;
         }

@@ -533,15 +533,34 @@ __device__ __forceinline__ void topo_tmin(const DP& d, const TopoS& ts, uint32_t
   ts.tmin[lane] = mn;
 }
 
+// one owned group as the topology checks use it: its own-list entry (group
+// id | TL_SELF) and the group's skew, slot and kind
+struct OwnG {
+  uint32_t e;
+  int32_t skew;
+  uint32_t slot, kind;
+};
+// the own list read from HBM at each use (own(k) of an own list at own_off)
+template <class DP>
+struct OwnMem {
+  const DP& d;
+  uint32_t own_off;
+  __device__ __forceinline__ OwnG operator()(uint32_t k) const {
+    const uint32_t e = d.tg_list[own_off + k];
+    const TGroupRec& tr = d.tgroups[e & TL_GID];
+    return OwnG{e, tr.skew, tr.slot, tr.kind};
+  }
+};
+
 // <U> Topology.AddRequirements for an existing node: its zone label z is its
 // only zone domain (a node without one fails the strict Compatible), its
 // hostname count in group slot is hcount(slot)
-template <class DP, class HCount>
-__device__ __forceinline__ bool topo_node_ok(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint32_t z,
-                                             HCount hcount) {
+template <class DP, class HCount, class Own>
+__device__ __forceinline__ bool topo_node_ok_g(const DP& d, const TopoS& ts, uint32_t own_n, uint32_t z, HCount hcount,
+                                               Own own) {
   for (uint32_t k = 0; k < own_n; k++) {
-    const uint32_t e = d.tg_list[own_off + k];
-    const TGroupRec& tr = d.tgroups[e & TL_GID];
+    const OwnG tr = own(k);
+    const uint32_t e = tr.e;
     const int64_t self = (e & TL_SELF) ? 1 : 0;
     if (tr.kind & TK_HOST) {
       const int64_t c = hcount(tr.slot);
@@ -562,6 +581,11 @@ __device__ __forceinline__ bool topo_node_ok(const DP& d, const TopoS& ts, uint3
   }
   return true;
 }
+template <class DP, class HCount>
+__device__ __forceinline__ bool topo_node_ok(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint32_t z,
+                                             HCount hcount) {
+  return topo_node_ok_g(d, ts, own_n, z, hcount, OwnMem<DP>{d, own_off});
+}
 
 // <U> Topology.AddRequirements for a NodeClaim whose zone domains (claim AND
 // pod requirements) are D: every owned zone group's domains, intersected --
@@ -570,13 +594,13 @@ __device__ __forceinline__ bool topo_node_ok(const DP& d, const TopoS& ts, uint3
 // count 0 (nextDomainAntiAffinity).  Hostname groups test the claim's count
 // hcount(slot) (0 on a fresh NodeClaim).  Returns the allowed zone set, ~0 when
 // no zone group applies, 0 when some group leaves no domain.
-template <class DP, class HCount>
-__device__ __forceinline__ uint64_t topo_claim(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint64_t D,
-                                               HCount hcount) {
+template <class DP, class HCount, class Own>
+__device__ __forceinline__ uint64_t topo_claim_g(const DP& d, const TopoS& ts, uint32_t own_n, uint64_t D, HCount hcount,
+                                                 Own own) {
   uint64_t allow = ~0ull;
   for (uint32_t k = 0; k < own_n; k++) {
-    const uint32_t e = d.tg_list[own_off + k];
-    const TGroupRec& tr = d.tgroups[e & TL_GID];
+    const OwnG tr = own(k);
+    const uint32_t e = tr.e;
     const int64_t self = (e & TL_SELF) ? 1 : 0;
     if (tr.kind & TK_HOST) {
       const int64_t c = hcount(tr.slot);
@@ -611,6 +635,11 @@ __device__ __forceinline__ uint64_t topo_claim(const DP& d, const TopoS& ts, uin
   }
   return allow;
 }
+template <class DP, class HCount>
+__device__ __forceinline__ uint64_t topo_claim(const DP& d, const TopoS& ts, uint32_t own_off, uint32_t own_n, uint64_t D,
+                                               HCount hcount) {
+  return topo_claim_g(d, ts, own_n, D, hcount, OwnMem<DP>{d, own_off});
+}
 
 // catalog zone mask of a zone-vocabulary set (zones outside the catalog have no offerings)
 template <class DP>
@@ -628,13 +657,13 @@ __device__ __forceinline__ uint64_t topo_catmask(const DP& d, uint64_t zset) {
 // spread group a single non-complement zone, an anti-affinity group (or its
 // inverse) every zone of a non-complement requirement (zf, zl: the target's
 // zone Has and flags; an existing node: its label)
-template <class DP, class HInc>
-__device__ __forceinline__ void topo_record(const DP& d, const TopoS& ts, uint32_t sel_off, uint32_t sel_n, uint64_t zf,
-                                            uint32_t zl, HInc hinc) {
+template <class DP, class HInc, class Sel>
+__device__ __forceinline__ void topo_record_g(const DP& d, const TopoS& ts, uint32_t sel_n, uint64_t zf, uint32_t zl,
+                                              HInc hinc, Sel sel) {
   const uint64_t zmask = d.ZS >= 64 ? ~0ull : (1ull << d.ZS) - 1ull;
   zf &= zmask;
   for (uint32_t k = 0; k < sel_n; k++) {
-    const uint32_t e = d.tg_list[sel_off + k];
+    const uint32_t e = sel(k);
     const uint32_t slot = e & 0xFFFFFFu, kind = e >> 24;
     if (kind & TK_HOST) {
       hinc(slot);
@@ -649,6 +678,11 @@ __device__ __forceinline__ void topo_record(const DP& d, const TopoS& ts, uint32
       }
     }
   }
+}
+template <class DP, class HInc>
+__device__ __forceinline__ void topo_record(const DP& d, const TopoS& ts, uint32_t sel_off, uint32_t sel_n, uint64_t zf,
+                                            uint32_t zl, HInc hinc) {
+  topo_record_g(d, ts, sel_n, zf, zl, hinc, [&](uint32_t k) -> uint32_t { return d.tg_list[sel_off + k]; });
 }
 
 }  // namespace

@@ -1000,6 +1000,23 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     // topology: own list (groups the variant owns), selection list (groups counting the pod)
     const uint32_t own_off = TOPO ? VD(22) : 0u, own_n = TOPO ? VD(23) : 0u;
     const uint32_t sel_off = TOPO ? VD(24) : 0u, sel_n = TOPO ? VD(25) : 0u;
+    // the owned groups staged in lanes 0..own_n-1 now (own_n <= OWNMAX = 64):
+    // the topology checks of the node scan, the exact batch and the fresh
+    // NodeClaim read them by readlane instead of two dependent HBM loads each
+    uint32_t og_e = 0, og_skew = 0, og_slot = 0, og_kind = 0;
+    if (TOPO && own_n) {
+      const auto& KD = *karg();
+      if (lane < own_n) {
+        og_e = KD.tg_list[own_off + lane];
+        const TGroupRec& tg = KD.tgroups[og_e & TL_GID];
+        og_skew = (uint32_t)tg.skew;
+        og_slot = tg.slot;
+        og_kind = tg.kind;
+      }
+    }
+    auto OWN = [&](uint32_t k) -> OwnG {
+      return OwnG{rlane(og_e, k), (int32_t)rlane(og_skew, k), rlane(og_slot, k), rlane(og_kind, k)};
+    };
     // the requests stay in the record's lanes 32.. (rqd): every use site
     // reads them with its own readlanes (RQ), so no 64-bit request is held
     // in scalar registers across the pod (they spilled into VGPR lanes)
@@ -1031,8 +1048,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 
     TLW(0);  // pop + record
     // <U> Topology.AddRequirements: each owned zone group's minimum domain
-    // count over the pod's strict zone domains (domainMinCount)
-    if (TOPO && own_n) {
+    // count over the pod's strict zone domains (domainMinCount); only a pod
+    // owning a zone spread group reads them
+    if (TOPO && own_n && (vctb & VF_ZSPREAD)) {
       const auto& KD = *karg();
       const uint64_t vzs = rlane(vrd, 26) | ((uint64_t)rlane(vrd, 27) << 32);
       topo_tmin(KD, ts, own_off, own_n, vzs, lane);
@@ -1111,8 +1129,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
             if (TOPO && feas && own_n)
-              feas = topo_node_ok(KD, ts, own_off, own_n, nr.zvid,
-                                  [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; });
+              feas = topo_node_ok_g(KD, ts, own_n, nr.zvid,
+                                    [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; }, OWN);
             if (TOPO && feas && KD.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
               const NodeVol& nv = KD.n_vol[n];
@@ -1473,7 +1491,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           czf = cr->zfull;
           czfl = cr->zflags;
           const int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
-          zset = topo_claim(KD, ts, own_off, own_n, czf & vzn, [&](uint32_t hs) -> int64_t { return hrow[hs]; });
+          zset = topo_claim_g(KD, ts, own_n, czf & vzn, [&](uint32_t hs) -> int64_t { return hrow[hs]; }, OWN);
           pre = zset != 0;
           if (pre && zset != ~0ull) zm &= topo_catmask(KD, zset);
         }
@@ -1765,7 +1783,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // bootstrap of a self-selecting pod while no selected pod runs)
       uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
       if (TOPO && own_n) {
-        tzs = topo_claim(KD, ts, own_off, own_n, tr.zfull & vzn, [](uint32_t) -> int64_t { return 0; });
+        tzs = topo_claim_g(KD, ts, own_n, tr.zfull & vzn, [](uint32_t) -> int64_t { return 0; }, OWN);
         if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(KD, tzs);
         tzs = (uint64_t)uniform_i64((int64_t)tzs);
         tzcat = (uint64_t)uniform_i64((int64_t)tzcat);

@@ -58,7 +58,7 @@ enum : uint32_t { CT_SPOT = 1u, CT_OD = 2u };
 // VarRec.ctb flag: the variant has no requirements and no topology spread, so
 // NodeClaim.Add changes nothing but the requests (claims never carry it:
 // their ctb is the template's AND the pods')
-enum : uint32_t { VF_SIMPLE = 1u << 31 };
+enum : uint32_t { VF_SIMPLE = 1u << 31, VF_ZSPREAD = 1u << 30 };  // VarRec.ctb flags (VF_ZSPREAD: owns a zone spread group)
 
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)

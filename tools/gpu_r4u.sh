@@ -1,0 +1,17 @@
+#!/bin/bash
+# round-4: owned groups staged (this tree) vs + staged selection lists (sel) vs
+# the reconstructed round-4 r4r wave source (r4r), e2e / C3 / CM
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r4u
+mkdir -p $O
+cd $R
+for rep in 1 2 3; do
+  for v in prev base sel r4r; do
+    lib=libgpusched_$v.so; [ "$v" = base ] && lib=libgpusched.so
+    for w in --e2e --c3 ""; do
+      ms=$(GPUSCHED_LIB=$lib timeout -k 10 150 python3 tools/ffd_diag.py $w | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ffd_ms"],1), d["claims"])') || exit 1
+      echo "$rep $v ${w:-cm} $ms" | tee -a $O/ab.txt
+    done
+  done
+done
