@@ -1670,7 +1670,14 @@ struct Ctx {
     chk(pd.labels, p->n_labels, "labels");
     w.sps = spreads_of(pd);
     for (auto& sp : w.sps) w.honor_taints = w.honor_taints || sp.honor_taints;
-    if (!w.sps.empty() && (pd.node_selector.count || pd.required_terms.count))
+    // nodeAffinityPolicy Honor equals Ignore when the node selector and the
+    // required terms constrain the zone key alone (oracle/solve.cpp: the
+    // filter then drops only nodes / NodeClaims outside the owner's zones)
+    bool zone_only = true;
+    for (auto& kv : w.ns) zone_only = zone_only && kv.first == e.k_zone;
+    for (auto& t : w.req_terms)
+      for (auto& kv : t) zone_only = zone_only && kv.first == e.k_zone;
+    if (!w.sps.empty() && !zone_only)
       for (auto& sp : w.sps)
         if (!sp.ignore_aff)
           throw Fail{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};

@@ -1539,34 +1539,58 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #pragma unroll
             for (uint32_t w = 0; w < WREG; w++) accw |= nx[w];
           } else {
-            // 4 words per round trip, stop at the first batch with a survivor
-            for (uint32_t w0 = sub * 4; w0 < W && !accw; w0 += 4u << lg) {
-              const uint4* oq = (const uint4*)(opts + w0);
-              const uint4* rq4 = (const uint4*)(row + w0);
-              const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
-              uint64_t x[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
-                               (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
-                               (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
-                               (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+            // GS_XC chunks of 4 words per round trip (the loads of all of them
+            // issued before any is used), stop at the first batch with a survivor
+#ifndef GS_XC
+#define GS_XC 2
+#endif
+            for (uint32_t w0 = sub * 4; w0 < W && !accw; w0 += (4u * GS_XC) << lg) {
+              uint4 o[GS_XC][2], rw[GS_XC][2], tt[GS_XC][RR][2];
 #pragma unroll
-              for (uint32_t r = 0; r < RR; r++) {
-                if (mm[r] == cur[r]) continue;
-                const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW + w0);
-                const uint4 t0 = tq[0], t1 = tq[1];
-                x[0] &= ((uint64_t)t0.y << 32) | t0.x;
-                x[1] &= ((uint64_t)t0.w << 32) | t0.z;
-                x[2] &= ((uint64_t)t1.y << 32) | t1.x;
-                x[3] &= ((uint64_t)t1.w << 32) | t1.z;
+              for (uint32_t c = 0; c < GS_XC; c++) {
+                const uint32_t wc = w0 + (c * 4u << lg);
+                if (wc < W) {
+                  const uint4* oq = (const uint4*)(opts + wc);
+                  const uint4* rq4 = (const uint4*)(row + wc);
+                  o[c][0] = oq[0];
+                  o[c][1] = oq[1];
+                  rw[c][0] = rq4[0];
+                  rw[c][1] = rq4[1];
+#pragma unroll
+                  for (uint32_t r = 0; r < RR; r++) {
+                    if (mm[r] == cur[r]) continue;
+                    const uint4* tq = (const uint4*)(KD.thr_set + (size_t)mrow[r] * OW + wc);
+                    tt[c][r][0] = tq[0];
+                    tt[c][r][1] = tq[1];
+                  }
+                }
               }
 #pragma unroll
-              for (uint32_t w = 0; w < 4; w++) {
-                if (w0 + w >= W) x[w] = 0;
-                if (x[w] && G != Gt) {
-                  uint64_t off = 0;
-                  for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w0 + w];
-                  x[w] &= off;
+              for (uint32_t c = 0; c < GS_XC; c++) {
+                const uint32_t wc = w0 + (c * 4u << lg);
+                if (wc >= W) continue;
+                uint64_t x[4] = {(((uint64_t)o[c][0].y << 32) | o[c][0].x) & (((uint64_t)rw[c][0].y << 32) | rw[c][0].x),
+                                 (((uint64_t)o[c][0].w << 32) | o[c][0].z) & (((uint64_t)rw[c][0].w << 32) | rw[c][0].z),
+                                 (((uint64_t)o[c][1].y << 32) | o[c][1].x) & (((uint64_t)rw[c][1].y << 32) | rw[c][1].x),
+                                 (((uint64_t)o[c][1].w << 32) | o[c][1].z) & (((uint64_t)rw[c][1].w << 32) | rw[c][1].z)};
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) {
+                  if (mm[r] == cur[r]) continue;
+                  x[0] &= ((uint64_t)tt[c][r][0].y << 32) | tt[c][r][0].x;
+                  x[1] &= ((uint64_t)tt[c][r][0].w << 32) | tt[c][r][0].z;
+                  x[2] &= ((uint64_t)tt[c][r][1].y << 32) | tt[c][r][1].x;
+                  x[3] &= ((uint64_t)tt[c][r][1].w << 32) | tt[c][r][1].z;
                 }
-                accw |= x[w];
+#pragma unroll
+                for (uint32_t w = 0; w < 4; w++) {
+                  if (wc + w >= W) x[w] = 0;
+                  if (x[w] && G != Gt) {
+                    uint64_t off = 0;
+                    for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + wc + w];
+                    x[w] &= off;
+                  }
+                  accw |= x[w];
+                }
               }
             }
           }

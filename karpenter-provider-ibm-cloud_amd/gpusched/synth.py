@@ -524,7 +524,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
     return b.build()
 
 
-def random_topology(seed, n_pods=None, taint_policy=None):
+def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore"):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
@@ -532,7 +532,9 @@ def random_topology(seed, n_pods=None, taint_policy=None):
     existing nodes with labelled bound pods, taints and relaxation.
     taint_policy "Honor" / "Ignore": every pod with a spread tolerates the
     NodePools' taint and its spreads carry that nodeTaintsPolicy (the random
-    stream is the same for both, so the two problems differ only in it)"""
+    stream is the same for both, so the two problems differ only in it).
+    affinity_policy: the nodeAffinityPolicy of the spreads of pods with a
+    (zone-only) required node-affinity term"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
@@ -600,7 +602,7 @@ def random_topology(seed, n_pods=None, taint_policy=None):
         if rng.random() < 0.2:
             if spreads:
                 for sp in spreads:
-                    sp["node_affinity_policy"] = "Ignore"
+                    sp["node_affinity_policy"] = affinity_policy
             required.append([("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(zones))])])
         if rng.random() < 0.1 and not spreads:
             sel["topology.kubernetes.io/zone"] = str(rng.choice(zones))

@@ -1036,7 +1036,18 @@ struct Builder {
         pd.tolerations.push_back({str(t.key), str(t.value), str(t.effect), (int)t.op});
       }
       pod_meta(g, pd);
-      if (!pd.spreads.empty() && (!pd.node_selector.empty() || !pd.required.empty()))
+      // <U> TopologyNodeFilter with AffinityPolicy Honor: a node / NodeClaim
+      // counts only where its requirements are Compatible with the owner's
+      // node selector or one of its required terms.  When those constrain the
+      // zone key alone, every node or NodeClaim the filter drops lies outside
+      // the owner's own zone domains, which neither domainMinCount (zone;
+      // hostname minimum is 0) nor the owner's placements ever consult:
+      // Honor equals Ignore.  Other node affinity under Honor is refused.
+      bool zone_only = true;
+      for (auto& kv : pd.node_selector) zone_only = zone_only && normalize_key(kv.first) == kZone;
+      for (auto& tm : pd.required)
+        for (auto& q : tm.reqs) zone_only = zone_only && q.key == kZone;
+      if (!pd.spreads.empty() && !zone_only)
         for (auto& sp : pd.spreads)
           if (!sp.ignore_affinity)
             throw Unsupported{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};

@@ -111,11 +111,42 @@ def test_refusals():
                taints=[("dedicated", "x", "NoSchedule")])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+    # nodeAffinityPolicy Honor (the default) with node affinity on a key
+    # other than zone
     b = _base(n_pods=0)
-    b.add_pod("x", 0, {"cpu": 1}, node_selector={Z: "us-south-1"},
+    b.add_pod("x", 0, {"cpu": 1}, node_selector={"node.kubernetes.io/instance-type": "bx2-4x16"},
               spreads=[{"key": Z, "max_skew": 1, "selector": {}}])
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+def test_affinity_policy_honor_zone_only_equals_ignore():
+    """nodeAffinityPolicy Honor with a zone-only node selector: the filter
+    drops only nodes outside the owner's zones, so Honor == Ignore"""
+    out = []
+    for pol in ("Honor", "Ignore"):
+        b = _base(n_pods=0)
+        b.add_node("n0", {Z: "us-south-3", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0})
+        b.add_bound_pod(0, "b0", 0, {"cpu": 1}, labels={"app": "web"})
+        for i in range(4):
+            b.add_pod(f"p{i}", i, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                      node_selector={Z: "us-south-1"} if i % 2 else {},
+                      spreads=[{"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}},
+                                "node_affinity_policy": pol}])
+        st, res, _ = pyoracle.solve(b.build())
+        assert st == abi.GS_OK and lib.validate(b.build())[0] == abi.GS_OK
+        out.append(_zones(res))
+    assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_affinity_policy_honor_random_equals_ignore(seed):
+    ph = synth.random_topology(seed, affinity_policy="Honor")
+    pi = synth.random_topology(seed, affinity_policy="Ignore")
+    sh, rh, _ = pyoracle.solve(ph)
+    si, ri, _ = pyoracle.solve(pi)
+    assert sh == si == abi.GS_OK and rh == ri
+    assert lib.validate(ph)[0] == abi.GS_OK
 
 
 def test_taint_policy_honor_without_taints_equals_ignore():
@@ -177,6 +208,12 @@ def test_gpu_topology_random(solver, seed):
 @pytest.mark.parametrize("seed", range(20))
 def test_gpu_topology_taint_policy_honor(solver, seed):
     _check(solver, synth.random_topology(seed, taint_policy="Honor"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(20))
+def test_gpu_topology_affinity_policy_honor(solver, seed):
+    _check(solver, synth.random_topology(seed, affinity_policy="Honor"))
 
 
 @pytest.mark.gpu
