@@ -1379,11 +1379,26 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // room codes (the Add reads the winner's lane, no LDS round trip)
       uint32_t fa_ev = 0, fa_l = 0;  // fa_l: the fast accept's lane (chunks start at the bound, unaligned)
       uint64_t fa_sq = 0, fa_rv = 0;
+      // the next chunk's order words are read with this chunk's codes, one
+      // LDS round trip less per further chunk (C5 1,266 -> 1,241 ms, CM 325 ->
+      // 322); the general narrow variant measured no better (e2e, C3) and
+      // keeps the plain loop (profiles/r4/scan_prefetch_ab.txt)
+#ifndef GS_SCAN_PF
+#define GS_SCAN_PF 1
+#endif
+      constexpr bool SPF = GS_SCAN_PF && (WIDE || !TOPO);
+      uint32_t ev_next = 0;
+      bool have_next = false;
       for (uint32_t cb = scan_from; cb < M; cb += 64) {
         const uint32_t pos = cb + lane;
         // the sort's window is this chunk when the scan starts where the last
         // Add landed (runs of equal pods): no LDS read of the order words
-        const uint32_t ev = cb == win_base ? win_v : s_so[pos < M ? pos : M - 1], je = ev >> 16;
+        const uint32_t ev = cb == win_base ? win_v : (SPF && have_next) ? ev_next : s_so[pos < M ? pos : M - 1], je = ev >> 16;
+        if (SPF) {
+          const uint32_t pn = pos + 64u;
+          ev_next = s_so[pn < M ? pn : M - 1];
+          have_next = true;
+        }
         const uint64_t sq = s_slk[je], rmv = s_rm[je];
         const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
