@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-4 record: the whole GPU suite, per-pop timelines (TL build) of the
+# Solve legs, then the default bench (headline line + detail)
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r4ab
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+for w in --e2e "" --c3 --c5; do
+  GPUSCHED_LIB=libgpusched_tl.so timeout -k 10 150 python3 tools/ffd_diag.py $w --tl > $O/tl$w.json 2>&1 || exit 1
+  echo "tl $w: $(head -c 120 $O/tl$w.json)"
+done
+timeout -k 10 600 python bench.py --detail-json $O/bench_detail.json > $O/bench.out 2> $O/bench.err
+rc=$?; tail -c 400 $O/bench.out; exit $rc
