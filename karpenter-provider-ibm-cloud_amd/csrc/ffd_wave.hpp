@@ -1387,20 +1387,39 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #define GS_SCAN_PF 1
 #endif
       constexpr bool SPF = GS_SCAN_PF && (WIDE || !TOPO);
-      uint32_t ev_next = 0;
+      // GS_SCAN_PF 2 (wide rows): the next chunk's codes are gathered too,
+      // once its order words are in
+      constexpr bool SPF2 = WIDE && GS_SCAN_PF >= 2;
+      uint32_t ev_next = 0, tt_next = 0;
+      uint64_t sq_next = 0, rm_next = 0;
       bool have_next = false;
       for (uint32_t cb = scan_from; cb < M; cb += 64) {
         const uint32_t pos = cb + lane;
         // the sort's window is this chunk when the scan starts where the last
         // Add landed (runs of equal pods): no LDS read of the order words
         const uint32_t ev = cb == win_base ? win_v : (SPF && have_next) ? ev_next : s_so[pos < M ? pos : M - 1], je = ev >> 16;
+        uint64_t sq, rmv;
+        uint32_t tt;
+        if (SPF2 && have_next) {
+          sq = sq_next;
+          rmv = rm_next;
+          tt = tt_next;
+        } else {
+          sq = s_slk[je];
+          rmv = s_rm[je];
+          tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
+        }
         if (SPF) {
           const uint32_t pn = pos + 64u;
           ev_next = s_so[pn < M ? pn : M - 1];
           have_next = true;
+          if (SPF2) {
+            const uint32_t jn = ev_next >> 16;
+            sq_next = s_slk[jn];
+            rm_next = s_rm[jn];
+            tt_next = T > 1 ? (uint32_t)s_tmpl[jn] : 0u;
+          }
         }
-        const uint64_t sq = s_slk[je], rmv = s_rm[je];
-        const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
         const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
         const bool fa = lp & simple & swar_ge(rmv, rqc_p);
