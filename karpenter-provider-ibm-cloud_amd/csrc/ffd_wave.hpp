@@ -1382,44 +1382,26 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // the next chunk's order words are read with this chunk's codes, one
       // LDS round trip less per further chunk (C5 1,266 -> 1,241 ms, CM 325 ->
       // 322); the general narrow variant measured no better (e2e, C3) and
-      // keeps the plain loop (profiles/r4/scan_prefetch_ab.txt)
+      // keeps the plain loop; gathering the next chunk's codes too measured
+      // slower (C5 1,245 -> 1,270; profiles/r4/scan_prefetch_ab.txt)
 #ifndef GS_SCAN_PF
 #define GS_SCAN_PF 1
 #endif
       constexpr bool SPF = GS_SCAN_PF && (WIDE || !TOPO);
-      // GS_SCAN_PF 2 (wide rows): the next chunk's codes are gathered too,
-      // once its order words are in
-      constexpr bool SPF2 = WIDE && GS_SCAN_PF >= 2;
-      uint32_t ev_next = 0, tt_next = 0;
-      uint64_t sq_next = 0, rm_next = 0;
+      uint32_t ev_next = 0;
       bool have_next = false;
       for (uint32_t cb = scan_from; cb < M; cb += 64) {
         const uint32_t pos = cb + lane;
         // the sort's window is this chunk when the scan starts where the last
         // Add landed (runs of equal pods): no LDS read of the order words
         const uint32_t ev = cb == win_base ? win_v : (SPF && have_next) ? ev_next : s_so[pos < M ? pos : M - 1], je = ev >> 16;
-        uint64_t sq, rmv;
-        uint32_t tt;
-        if (SPF2 && have_next) {
-          sq = sq_next;
-          rmv = rm_next;
-          tt = tt_next;
-        } else {
-          sq = s_slk[je];
-          rmv = s_rm[je];
-          tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
-        }
         if (SPF) {
           const uint32_t pn = pos + 64u;
           ev_next = s_so[pn < M ? pn : M - 1];
           have_next = true;
-          if (SPF2) {
-            const uint32_t jn = ev_next >> 16;
-            sq_next = s_slk[jn];
-            rm_next = s_rm[jn];
-            tt_next = T > 1 ? (uint32_t)s_tmpl[jn] : 0u;
-          }
         }
+        const uint64_t sq = s_slk[je], rmv = s_rm[je];
+        const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
         const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
         const bool fa = lp & simple & swar_ge(rmv, rqc_p);
@@ -1485,11 +1467,24 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       uint32_t czfl = 0;
       uint32_t mrow[RR];
       int64_t tot[RR];
+      // GS_MAXA_PF: each candidate lane also loads its claim's maxa (the
+      // slack bound the Add re-quantizes with) with the header, so the
+      // winner's Add does not wait on a load of its own
+#ifndef GS_MAXA_PF
+#define GS_MAXA_PF 1
+#endif
+      int64_t maxa_pre[RR];
+#pragma unroll
+      for (uint32_t r = 0; r < RR; r++) maxa_pre[r] = 0;
       uint64_t nx[WREG] = {0, 0, 0, 0};
       uint64_t G = 0, Gt = 0;
       if (cx < nex) {
         const ClaimRec* cr = KD.c_rec + j;
         uint32_t cur[RR];
+        if (GS_MAXA_PF) {
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) maxa_pre[r] = cr->maxa[r];
+        }
         {
           const uint4* q = (const uint4*)cr;
           const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
@@ -1708,7 +1703,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   #pragma unroll
           for (uint32_t r = 0; r < RR; r++) {
             nt[r] = tot[r] + RQ(r);
-            ma[r] = cr->maxa[r];
+            ma[r] = GS_MAXA_PF ? maxa_pre[r] : cr->maxa[r];
             cu[r] = mrow[r] - s_thoff[r] - r;
             cr->tot(r) = nt[r];
             cr->thr(r) = (uint16_t)cu[r];
