@@ -2069,6 +2069,13 @@ struct Ctx {
       // owns a zone spread group: only those read the per-pod minimum counts
       for (uint32_t g : pv.own)
         if (groups[g].sp.key == kZone && groups[g].kind == 0) vr.ctb |= gsd::VF_ZSPREAD;
+      // hostname-only topology (spread, anti-affinity, inverse, host ports;
+      // not pod affinity): the wave kernel's fast accept reads the counts
+      if (pv.reqs.empty() && !pv.own.empty() && pv.own.size() <= 4) {
+        bool host = true;
+        for (uint32_t g : pv.own) host = host && groups[g].sp.key == kHostname && groups[g].kind != 4;
+        if (host) vr.ctb |= gsd::VF_HOSTFA;
+      }
       vr.zs = zone_full(pv.strict);
       vr.zn = zone_full(pv.reqs);
       vr.zflags = zone_flags(pv.reqs);

@@ -1350,6 +1350,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     bool simple = (vctb & VF_SIMPLE) != 0;
 #endif
     simple = simple && !rq_hi;  // room covers resources 0..3
+    // hostname-only topology (VF_HOSTFA): the scan reads each candidate's
+    // counts of the owned groups; a candidate over a skew is infeasible
+    // (dropped), one within them that passes the room test is a fast accept
+#ifndef GS_HOSTFA
+#define GS_HOSTFA 1
+#endif
+    const bool hostfa = GS_HOSTFA && TOPO && !rq_hi && (vctb & VF_HOSTFA) != 0;
 #ifdef GS_FFD_TL
     n_nonsimple += simple ? 0u : 1u;
 #endif
@@ -1403,8 +1410,26 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint64_t sq = s_slk[je], rmv = s_rm[je];
         const uint32_t tt = T > 1 ? (uint32_t)s_tmpl[je] : 0u;
         // bitwise (not short-circuit) predicates: no branches
-        const bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
-        const bool fa = lp & simple & swar_ge(rmv, rqc_p);
+        bool lp = (pos >= lo_bound) & (pos < M) & (bool)((vtolt >> tt) & 1) & swar_ge(sq, rqq_p);
+        if (TOPO && hostfa && lp) {
+          const auto& KD = *karg();
+          const int32_t* hrow = KD.hc + (size_t)je * KD.TGH;
+#ifdef GS_HOSTFA_UNROLL
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++) {
+            if (k < own_n) {
+              const int64_t c = hrow[rlane(og_slot, k)] + ((rlane(og_e, k) & TL_SELF) ? 1 : 0);
+              lp = lp && c <= (int64_t)(int32_t)rlane(og_skew, k);
+            }
+          }
+#else
+          for (uint32_t k = 0; k < own_n; k++) {
+            const int64_t c = hrow[rlane(og_slot, k)] + ((rlane(og_e, k) & TL_SELF) ? 1 : 0);
+            lp = lp && c <= (int64_t)(int32_t)rlane(og_skew, k);
+          }
+#endif
+        }
+        const bool fa = lp & (simple | hostfa) & swar_ge(rmv, rqc_p);
         const uint64_t fab = __ballot(fa), exb = __ballot(lp & !fa);
         const uint32_t mfl = fab ? ffs64(fab) : 64u;
         const uint64_t ex = exb & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));

@@ -58,7 +58,10 @@ enum : uint32_t { CT_SPOT = 1u, CT_OD = 2u };
 // VarRec.ctb flag: the variant has no requirements and no topology spread, so
 // NodeClaim.Add changes nothing but the requests (claims never carry it:
 // their ctb is the template's AND the pods')
-enum : uint32_t { VF_SIMPLE = 1u << 31, VF_ZSPREAD = 1u << 30 };  // VarRec.ctb flags (VF_ZSPREAD: owns a zone spread group)
+// VarRec.ctb flags: VF_SIMPLE no requirements and no owned topology group;
+// VF_ZSPREAD owns a zone spread group; VF_HOSTFA no requirements and 1..4
+// owned groups, all hostname groups admitted by count + self <= skew
+enum : uint32_t { VF_SIMPLE = 1u << 31, VF_ZSPREAD = 1u << 30, VF_HOSTFA = 1u << 29 };
 
 // requirement on one free key, vocabulary <= 64 values (last one is the
 // "unmentioned value" omega used for hostname placeholders)
