@@ -241,15 +241,34 @@ typedef struct gs_pod {
   gs_range volumes;         /* CSI volumes, into volumes (<U> ExistingNode.CanAdd VolumeUsage) */
 } gs_pod;
 
-/* an existing (state) node: ExistingNode inputs */
+/* an existing (state) node: ExistingNode inputs.
+ *
+ * Taints.  ExistingNode.CanAdd tolerates against <U> StateNode.Taints()
+ * (karpenter pkg/controllers/state/statenode.go), which the library computes
+ * from the raw fields below, so the caller marshals them as the cluster state
+ * holds them and applies no filter of its own:
+ *   source   = (managed && !initialized) ? claim_taints : taints
+ *   rejected = KnownEphemeralTaints, plus startup_taints when managed && !initialized
+ *   Taints() = the source taints that match no rejected taint
+ * where a taint matches another when key and effect are equal (corev1
+ * Taint.MatchTaint: the value is not compared) and KnownEphemeralTaints are
+ *   node.kubernetes.io/not-ready:NoSchedule, node.kubernetes.io/unreachable:NoSchedule,
+ *   node.cloudprovider.kubernetes.io/uninitialized:NoSchedule, karpenter.sh/unregistered:NoExecute.
+ * So an in-flight node that karpenter launched (its NodeClaim's
+ * spec.startupTaints, e.g. NodePool startupTaints, reference test/e2e/
+ * e2e_taints_test.go:105-115, CRD karpenter.sh_nodepools.yaml:334) takes the
+ * pods its NodeClaim's taints admit while it initializes. */
 typedef struct gs_node {
   uint32_t name;        /* string id (also its hostname) */
-  uint32_t initialized;
+  uint32_t initialized; /* StateNode.Initialized() */
   gs_range labels;      /* node labels */
-  gs_range taints;
+  gs_range taints;      /* Node.Spec.Taints (a registered node's current taints) */
   gs_range available;   /* StateNode.Available() */
   gs_range requests;    /* remaining daemonset requests already owed */
   gs_range volume_limits; /* into volume_limits; a driver without an entry has no limit */
+  uint32_t managed;     /* StateNode.Managed(): a NodeClaim owns the node (karpenter launched it) */
+  gs_range claim_taints;   /* into taints: NodeClaim.Spec.Taints (managed nodes) */
+  gs_range startup_taints; /* into taints: NodeClaim.Spec.StartupTaints (managed nodes) */
 } gs_node;
 
 typedef struct gs_problem {

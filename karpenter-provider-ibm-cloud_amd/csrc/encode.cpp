@@ -1286,12 +1286,16 @@ struct Ctx {
   // the distinct taints of a NodePool / node (raw ids); the device masks are
   // over taint classes (build_taint_classes), so the raw vocabulary may
   // exceed 64
-  std::vector<uint32_t> taint_ids(gs_range r) {
+  std::vector<uint32_t> taint_ids(gs_range r, const std::vector<std::pair<std::string, std::string>>* reject = nullptr) {
     chk(r, p->n_taints, "taints");
     std::vector<uint32_t> ids;
     for (uint32_t i = 0; i < r.count; i++) {
       auto& t = p->taints[r.begin + i];
       TaintKey tk{S(t.key), S(t.value), S(t.effect)};
+      bool drop = false;
+      if (reject)
+        for (auto& kr : *reject) drop = drop || (kr.first == tk.k && kr.second == tk.eff);  // Taint.MatchTaint
+      if (drop) continue;
       auto f = taint_id.find(tk);
       uint32_t id;
       if (f == taint_id.end()) {
@@ -1307,6 +1311,25 @@ struct Ctx {
     return ids;
   }
   std::vector<std::vector<uint32_t>> tmpl_taints, node_taints;  // raw ids per template / node position
+  // <U> StateNode.Taints() (include/gpusched.h gs_node): while a managed node
+  // initializes its NodeClaim's taints stand for the node's, and its startup
+  // taints are ignored like the known ephemeral ones; matched by key + effect
+  std::vector<uint32_t> state_taint_ids(const gs_node& g) {
+    chk(g.taints, p->n_taints, "taints");
+    chk(g.claim_taints, p->n_taints, "taints");
+    chk(g.startup_taints, p->n_taints, "taints");
+    const bool starting = g.managed && !g.initialized;
+    std::vector<std::pair<std::string, std::string>> reject = {{"node.kubernetes.io/not-ready", "NoSchedule"},
+                                                               {"node.kubernetes.io/unreachable", "NoSchedule"},
+                                                               {"node.cloudprovider.kubernetes.io/uninitialized", "NoSchedule"},
+                                                               {"karpenter.sh/unregistered", "NoExecute"}};
+    if (starting)
+      for (uint32_t i = 0; i < g.startup_taints.count; i++) {
+        auto& t = p->taints[g.startup_taints.begin + i];
+        reject.emplace_back(S(t.key), S(t.effect));
+      }
+    return taint_ids(starting ? g.claim_taints : g.taints, &reject);
+  }
   struct Tol {
     std::string k, v, eff;
     uint32_t op;
@@ -2210,7 +2233,7 @@ struct Ctx {
         if (present[r] && nr.avail[r] < 0) nr.ok = 0;  // <U> Fits: negative total never fits
       resvec_fn(g.requests, nr.req, nullptr);
       nr.taints = 0;  // build_taint_classes
-      node_taints[pos] = taint_ids(g.taints);
+      node_taints[pos] = state_taint_ids(g);
       nr.init = g.initialized ? 1u : 0u;
     }
     // every taint is known now (NodePools', then nodes'): the class masks

@@ -58,7 +58,12 @@ DT_SPREAD = np.dtype([("topology_key", "<u4"), ("max_skew", "<i4"), ("when_unsat
                       ("match_expressions", RANGE), ("node_affinity_policy", "<u4"),
                       ("node_taints_policy", "<u4"), ("match_label_keys", RANGE)], align=True)
 DT_NODE = np.dtype([("name", "<u4"), ("initialized", "<u4"), ("labels", RANGE), ("taints", RANGE),
-                    ("available", RANGE), ("requests", RANGE), ("volume_limits", RANGE)], align=True)
+                    ("available", RANGE), ("requests", RANGE), ("volume_limits", RANGE), ("managed", "<u4"),
+                    ("claim_taints", RANGE), ("startup_taints", RANGE)], align=True)
+# <U> scheduling.KnownEphemeralTaints (key, effect): StateNode.Taints() drops them
+EPHEMERAL_TAINTS = (("node.kubernetes.io/not-ready", "NoSchedule"), ("node.kubernetes.io/unreachable", "NoSchedule"),
+                    ("node.cloudprovider.kubernetes.io/uninitialized", "NoSchedule"),
+                    ("karpenter.sh/unregistered", "NoExecute"))
 
 _P = C.c_void_p
 _U32 = C.c_uint32

@@ -212,12 +212,17 @@ class ProblemBuilder:
         self.claim_queries.append((self._reqs(requirements), self._qty(requests or {})))
         return len(self.claim_queries) - 1
 
-    def add_node(self, name, labels, available, requests=None, taints=(), initialized=True, volume_limits=None):
-        """volume_limits: {csi driver: CSINode allocatable count}"""
+    def add_node(self, name, labels, available, requests=None, taints=(), initialized=True, volume_limits=None,
+                 managed=False, claim_taints=(), startup_taints=()):
+        """volume_limits: {csi driver: CSINode allocatable count}; taints:
+        Node.Spec.Taints; managed nodes also carry their NodeClaim's
+        spec.taints and spec.startupTaints (the library derives
+        StateNode.Taints() from them, include/gpusched.h gs_node)"""
         lb = len(self.volume_limits)
         self.volume_limits.extend((self.s(k), int(v)) for k, v in (volume_limits or {}).items())
         self.nodes.append((self.s(name), 1 if initialized else 0, self._labels(labels), self._taints(taints),
-                           self._qty(available), self._qty(requests or {}), (lb, len(self.volume_limits) - lb)))
+                           self._qty(available), self._qty(requests or {}), (lb, len(self.volume_limits) - lb),
+                           1 if managed else 0, self._taints(claim_taints), self._taints(startup_taints)))
         return len(self.nodes) - 1
 
     def build(self):

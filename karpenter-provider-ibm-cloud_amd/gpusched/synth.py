@@ -251,10 +251,12 @@ _KEYS_FREE = ["kubernetes.io/os", "karpenter.sh/nodepool", "team", "karpenter-ib
               "kubernetes.io/hostname", "tier"]
 
 
-def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_values=3):
+def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_values=3, inflight=False):
     """small adversarial problem over the whole supported feature set;
     free_values > 3 widens the custom (free) keys team / tier to that many
-    values (tier's integers then reach free_values - 1 for Gt / Lt)"""
+    values (tier's integers then reach free_values - 1 for Gt / Lt);
+    inflight: the existing nodes are karpenter-launched ones, some still
+    initializing, with startup / ephemeral taints (inflight_node)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
@@ -307,10 +309,12 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_va
 
     effects = ["NoSchedule", "PreferNoSchedule", "NoExecute"]
     n_np = int(rng.integers(1, 4))
+    np_taints = []
     for j in range(n_np):
         reqs = [rand_req(_KEYS_IT + _KEYS_OFF + ["kubernetes.io/os", "team"]) for _ in range(int(rng.integers(0, 3)))]
         labels = {"team": vocab["team"][rng.integers(0, nteam)]} if rng.random() < 0.4 else {}
         taints = [("dedicated", str(rng.choice(["x", "y"])), str(rng.choice(effects)))] if rng.random() < 0.4 else []
+        np_taints.append(taints)
         limits = None
         if with_limits and rng.random() < 0.3:
             limits = {"cpu": int(rng.choice([8, 16, 32, 64])) * 1000}
@@ -328,8 +332,11 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_va
                 labels["team"] = vocab["team"][rng.integers(0, nteam)]
             avail = {"cpu": int(rng.choice([500, 1000, 4000])), "memory": int(rng.choice([1, 4, 16])) * GI * 1000,
                      "pods": 10_000}
-            taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.3 else []
-            b.add_node(f"node-{k}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.8))
+            if inflight:
+                b.add_node(f"node-{k}", labels, avail, **inflight_node(rng, np_taints[rng.integers(0, n_np)]))
+            else:
+                taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.3 else []
+                b.add_node(f"node-{k}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.8))
     n = int(n_pods if n_pods is not None else rng.integers(1, 40))
     for i in range(n):
         req = {"cpu": int(rng.choice([100, 500, 1000, 3000, 9000])),
@@ -352,9 +359,43 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_va
                          str(rng.choice(effects + [""]))))
         if rng.random() < 0.1:
             tols.append(("", "Exists", "", ""))
+        if inflight and rng.random() < 0.3:
+            tols.append(("example.com/initializing", str(rng.choice(["Equal", "Exists"])), "true", "NoSchedule"))
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 4)) * 1_000_000_000, req,
                   node_selector=sel, required_terms=required, preferred_terms=preferred, tolerations=tols)
     return b.build()
+
+
+# NodeClaim spec.startupTaints seen on in-flight nodes (e.g. NodePool
+# startupTaints, reference test/e2e/e2e_taints_test.go:105-115) and the taints
+# a registering node carries (<U> scheduling.KnownEphemeralTaints)
+STARTUP_TAINTS = [("example.com/initializing", "true", "NoSchedule"), ("node.kubernetes.io/not-ready", "", "NoSchedule"),
+                  ("cilium.io/agent-not-ready", "true", "NoExecute")]
+EPHEMERAL_TAINTS = [("node.kubernetes.io/not-ready", "", "NoSchedule"), ("node.kubernetes.io/unreachable", "", "NoSchedule"),
+                    ("node.cloudprovider.kubernetes.io/uninitialized", "true", "NoSchedule"),
+                    ("karpenter.sh/unregistered", "", "NoExecute")]
+
+
+def inflight_node(rng, claim_taints):
+    """add_node keyword arguments of a state node as the cluster state holds
+    it: karpenter-launched (managed) or not, initialized or not, its
+    Node.Spec.Taints (the NodeClaim's taints, startup taints and ephemeral
+    ones while it registers; a startup taint that came back after
+    initialization) and its NodeClaim's taints / startup taints"""
+    managed = bool(rng.random() < 0.8)
+    initialized = bool(rng.random() < 0.5)
+    startup = [t for t in STARTUP_TAINTS if rng.random() < 0.5] if managed else []
+    node_taints = list(claim_taints) if managed else []
+    if not initialized:
+        node_taints += startup + [t for t in EPHEMERAL_TAINTS if rng.random() < 0.4]
+    elif startup and rng.random() < 0.3:
+        node_taints.append(startup[0])
+    if rng.random() < 0.2:
+        node_taints.append(EPHEMERAL_TAINTS[int(rng.integers(0, len(EPHEMERAL_TAINTS)))])
+    if rng.random() < 0.2:
+        node_taints.append(("dedicated", "x", "NoSchedule"))
+    return dict(managed=managed, initialized=initialized, taints=node_taints,
+                claim_taints=list(claim_taints) if managed else [], startup_taints=startup)
 
 
 def make_c4_sim(n_nodes=500, n_pods=2000, seed=0x5EED0004):
@@ -459,7 +500,7 @@ def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=2
 CONFIGS["C4"] = make_c4
 
 
-def random_consolidation(seed, n_nodes=None, n_pending=None):
+def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False):
     """small adversarial consolidation cluster: nodes with taints, custom
     labels, spot/on-demand, uninitialized nodes and bound pods with
     selectors/tolerations; pending pods; 1-3 NodePools (taints, limits)"""
@@ -477,6 +518,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
     its = build_catalog(b, profs, zones, spot=True, prices=prices, rng=rng, unavailable_frac=0.1)
     effects = ["NoSchedule", "PreferNoSchedule"]
     n_np = int(rng.integers(1, 4))
+    np_taints = []
     for j in range(n_np):
         reqs = []
         if rng.random() < 0.3:
@@ -484,6 +526,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
         if rng.random() < 0.2:
             reqs.append(("karpenter-ibm.sh/instance-family", "NotIn", ["mx2"]))
         taints = [("dedicated", "x", str(rng.choice(effects)))] if rng.random() < 0.3 else []
+        np_taints.append(taints)
         limits = {"cpu": int(rng.choice([16, 64, 256])) * 1000} if rng.random() < 0.2 else None
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10, 50])), requirements=reqs,
                        labels={"team": str(rng.choice(["a", "b"]))} if rng.random() < 0.4 else {},
@@ -512,11 +555,16 @@ def random_consolidation(seed, n_nodes=None, n_pending=None):
             used["pods"] += 1000
             sel = {"team": labels["team"]} if "team" in labels and rng.random() < 0.3 else {}
             tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
+            if inflight and rng.random() < 0.3:
+                tols.append(("example.com/initializing", "Exists", "", ""))
             b.add_bound_pod(k, _uid(rng), ts, {"cpu": cpu, "memory": mem, "pods": 1000}, node_selector=sel,
                             tolerations=tols)
         avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
-        taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.15 else []
-        b.add_node(f"n-{k:03d}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.85))
+        if inflight:
+            b.add_node(f"n-{k:03d}", labels, avail, **inflight_node(rng, np_taints[int(labels["karpenter.sh/nodepool"][2:])]))
+        else:
+            taints = [("dedicated", "x", "NoSchedule")] if rng.random() < 0.15 else []
+            b.add_node(f"n-{k:03d}", labels, avail, taints=taints, initialized=bool(rng.random() < 0.85))
     npend = int(n_pending if n_pending is not None else rng.choice([0, 0, 1, 3]))
     for i in range(npend):
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000, {"cpu": int(rng.choice([100, 1000, 3000])),

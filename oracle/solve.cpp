@@ -678,6 +678,31 @@ struct Builder {
     }
     return out;
   }
+  // <U> StateNode.Taints() (karpenter pkg/controllers/state/statenode.go,
+  // restated from upstream v1.x; the contract is spelled out at gs_node in
+  // include/gpusched.h): reject KnownEphemeralTaints, and while a managed node
+  // is not initialized also its NodeClaim's startup taints, from the
+  // NodeClaim's taints (uninitialized managed node) or the node's; a rejected
+  // taint matches by key and effect (corev1 Taint.MatchTaint)
+  vector<Taint> state_taints(const gs_node& g) {
+    const bool starting = g.managed != 0 && g.initialized == 0;
+    vector<Taint> reject = {{"node.kubernetes.io/not-ready", "", "NoSchedule"},
+                            {"node.kubernetes.io/unreachable", "", "NoSchedule"},
+                            {"node.cloudprovider.kubernetes.io/uninitialized", "true", "NoSchedule"},
+                            {"karpenter.sh/unregistered", "", "NoExecute"}};
+    const vector<Taint> startup = taints_of(g.startup_taints);
+    const vector<Taint> claim = taints_of(g.claim_taints);
+    const vector<Taint> node = taints_of(g.taints);
+    if (starting) reject.insert(reject.end(), startup.begin(), startup.end());
+    vector<Taint> out;
+    for (auto& t : starting ? claim : node) {
+      bool matched = false;
+      for (auto& r : reject)
+        if (r.key == t.key && r.effect == t.effect) matched = true;
+      if (!matched) out.push_back(t);
+    }
+    return out;
+  }
   std::map<string, string> labels_of(gs_range r) {
     check_range(r, p->n_labels, "labels");
     std::map<string, string> out;
@@ -932,8 +957,8 @@ struct Builder {
     vector<Taint> all;
     for (uint32_t i = 0; i < p->n_nodepools; i++)
       for (auto& t : taints_of(p->nodepools[i].taints)) all.push_back(t);
-    for (uint32_t i = 0; i < p->n_nodes; i++)
-      for (auto& t : taints_of(p->nodes[i].taints)) all.push_back(t);
+    for (auto& n : st.nodes)
+      for (auto& t : n.taints) all.push_back(t);
     for (auto& pd : st.pods)
       for (auto& sp : pd.spreads)
         if (sp.honor_taints && !tolerates_all(all, pd.tolerations))
@@ -1063,7 +1088,7 @@ struct Builder {
       n.initialized = g.initialized != 0;
       for (auto& kv : labels_of(g.labels)) n.reqs.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
       n.reqs.add(make_req(kHostname, GS_OP_IN, {n.name}, std::nullopt));
-      n.taints = taints_of(g.taints);
+      n.taints = state_taints(g);
       n.available = res_of(g.available);
       n.requests = res_of(g.requests);
       check_range(g.volume_limits, p->n_volume_limits, "volume_limits");

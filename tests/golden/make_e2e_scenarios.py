@@ -44,6 +44,16 @@ MULTI_TYPE_NODEPOOL = {"requirements": [[IT, "In", SMALL4], ["kubernetes.io/arch
 # fake profile (cx2-2x4: 4 GB - 2.5 GiB calculateOverhead), so the fake catalog's 8 GB 2-vCPU profile stands in.
 TAINTED_NODEPOOL = {"requirements": [[IT, "In", ["bx2-2x8"]]], "labels": {"test": "basic-taints"},
                     "taints": [["dedicated", "gpu-workload", "NoSchedule"]]}
+# TestE2EStartupTaints' NodePool (reference test/e2e/e2e_taints_test.go:80-119): one instance type (the same
+# bx2-2x8 stand-in as above for the 1000m / 4Gi workload), template label test=<testName>, two startup taints
+STARTUP_NODEPOOL = {"requirements": [[IT, "In", ["bx2-2x8"]]], "labels": {"test": "startup-taints"},
+                    "startup_taints": [["node.kubernetes.io/not-ready", "", "NoSchedule"],
+                                       ["example.com/initializing", "true", "NoSchedule"]]}
+# TestE2ETaintValues' NodePool (reference test/e2e/e2e_taints_test.go:650-691): a NoSchedule and a
+# PreferNoSchedule taint with values
+TAINT_VALUES_NODEPOOL = {"requirements": [[IT, "In", ["bx2-2x8"]]], "labels": {"test": "taint-values"},
+                         "taints": [["workload-type", "batch-processing", "NoSchedule"],
+                                    ["priority", "high", "PreferNoSchedule"]]}
 
 SCENARIOS = [
     {
@@ -137,6 +147,48 @@ SCENARIOS = [
         "arrival": "scale",
         "scale_to": 8,
         "expect": {"kind": "min_zones", "app": "zone-failover-app", "min_zones": 2, "placed": 8},
+    },
+    {
+        "id": "startup_taints_inflight_node",
+        "ref": "test/e2e/e2e_taints_test.go:43-258 (TestE2EStartupTaints), workload :1074-1119",
+        "nodepool": STARTUP_NODEPOOL,
+        # the reference deployment: 1 replica, 1000m / 4Gi, tolerating both startup taints (:129-141) and
+        # selecting the template label; it must get a NodeClaim of this pool (:149-184) and schedule (:242-254).
+        # Derived step (marked "derived"): while that node initializes (managed, not initialized, its Node
+        # carrying the startup taints and not-ready), a second pod WITHOUT those tolerations packs onto it:
+        # <U> StateNode.Taints() ignores startup and ephemeral taints until initialization; once the node is
+        # initialized and a startup taint is still there, the same pod opens a NodeClaim instead.
+        "workloads": [{"app": "startup-taints-deployment", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "tolerations": [["node.kubernetes.io/not-ready", "Equal", "", "NoSchedule"],
+                                       ["example.com/initializing", "Equal", "true", "NoSchedule"]],
+                       "node_selector": {"test": "startup-taints"}},
+                      {"app": "startup-followup", "replicas": 1, "cpu_m": 500, "memory_mi": 1024,
+                       "node_selector": {"test": "startup-taints"}, "derived": True}],
+        "arrival": "startup",
+        "expect": {"kind": "startup_taints", "app": "startup-taints-deployment", "followup_app": "startup-followup"},
+    },
+    {
+        "id": "taint_values_equal_tolerations",
+        "ref": "test/e2e/e2e_taints_test.go:614-776 (TestE2ETaintValues), workload :1074-1119",
+        "nodepool": TAINT_VALUES_NODEPOOL,
+        # the reference deployment tolerates both taints with Operator Equal and their exact values
+        # (:700-715) and must become ready on this pool's node (:723-735).  Derived workloads: one tolerating
+        # only the NoSchedule taint schedules after <U> Preferences.Relax tolerates PreferNoSchedule (the
+        # pool carries such a taint); one whose Equal toleration names another value stays pending.
+        "workloads": [{"app": "taint-values-deployment", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "tolerations": [["workload-type", "Equal", "batch-processing", "NoSchedule"],
+                                       ["priority", "Equal", "high", "PreferNoSchedule"]],
+                       "node_selector": {"test": "taint-values"}},
+                      {"app": "prefer-relaxed", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "tolerations": [["workload-type", "Equal", "batch-processing", "NoSchedule"]],
+                       "node_selector": {"test": "taint-values"}, "derived": True},
+                      {"app": "value-mismatch", "replicas": 1, "cpu_m": 1000, "memory_mi": 4096,
+                       "tolerations": [["workload-type", "Equal", "streaming", "NoSchedule"],
+                                       ["priority", "Equal", "high", "PreferNoSchedule"]],
+                       "node_selector": {"test": "taint-values"}, "derived": True}],
+        "arrival": "together",
+        "expect": {"kind": "taint_values", "app": "taint-values-deployment", "relaxed_app": "prefer-relaxed",
+                   "pending_app": "value-mismatch"},
     },
 ]
 

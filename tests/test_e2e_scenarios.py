@@ -18,6 +18,15 @@ its reference file:line:
                                 NodePool's allowed list, its requirements met
   * multizone_test.go:384-431   preferred zone anti-affinity, 4 -> 8 replicas:
                                 still more than one zone
+  * e2e_taints_test.go:43-258   NodePool startup taints: the pod gets a
+                                NodeClaim of the pool; (derived) a pod without
+                                the tolerations packs onto the initializing
+                                node, not once it is initialized and tainted
+  * e2e_taints_test.go:614-776  Equal tolerations of a NoSchedule and a
+                                PreferNoSchedule taint with values; (derived)
+                                Relax tolerates PreferNoSchedule, a wrong
+                                value stays pending
+Workloads marked "derived" extend a reference test with a step it implies.
 The CPU tests run every scenario through the oracle and assert the reference
 test's property; the GPU tests require both HIP Solve kernels (and the
 consolidation simulation kernel) to equal the oracle at every step, so the
@@ -97,6 +106,7 @@ class Cluster:
         synth.build_catalog(b, synth.FAKE_PROFILES, ZONES, spot=False, prices=synth.price_table(synth.FAKE_PROFILES))
         npd = self.sc["nodepool"]
         taints = [tuple(t) for t in npd.get("taints", [])]
+        startup = [tuple(t) for t in npd.get("startup_taints", [])]
         b.add_nodepool(NP, requirements=[tuple(r) for r in npd["requirements"]], labels=npd.get("labels"),
                        taints=taints)
         for k, n in enumerate(self.nodes):
@@ -109,7 +119,10 @@ class Cluster:
             alloc = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
             used = {"cpu": sum(p["cpu"] for p in n["pods"]), "memory": sum(p["mem"] for p in n["pods"]),
                     "pods": 1000 * len(n["pods"])}
-            b.add_node(n["name"], labels, {r: alloc[r] - used.get(r, 0) for r in alloc}, taints=taints)
+            # karpenter launched it: its NodeClaim carries the template's taints and startup taints
+            b.add_node(n["name"], labels, {r: alloc[r] - used.get(r, 0) for r in alloc},
+                       taints=n.get("node_taints", taints), initialized=n.get("initialized", True), managed=True,
+                       claim_taints=taints, startup_taints=startup)
         for k, n in enumerate(self.nodes):
             for p in n["pods"]:
                 self._add(b, p, node=k)
@@ -117,15 +130,17 @@ class Cluster:
             self._add(b, p)
         return b.build()
 
-    def launch(self, res, pending):
+    def launch(self, res, pending, **node):
         """NodeClaims become nodes (Create: the first compatible type in
-        catalog order, the first allowed zone); placed pods become bound"""
+        catalog order, the first allowed zone); placed pods become bound.
+        node: initialized / node_taints of the new nodes (default: ready,
+        carrying the template's taints)"""
         for k, pods in enumerate(res["nodes"]):
             self.nodes[k]["pods"].extend(pending[i] for i in pods)
         for c in res["claims"]:
             it = min(c["its"])
             self.nodes.append(dict(name=f"launched-{len(self.nodes):02d}", it=it, zone=zones_of(c)[0],
-                                   pods=[pending[i] for i in c["pods"]]))
+                                   pods=[pending[i] for i in c["pods"]], **node))
             if self.first_type is None:
                 self.first_type = self.its[it].name
         self.pods.extend(pending)
@@ -147,9 +162,28 @@ def _solve_all(problem, solvers):
 def run_scenario(sc, solvers=(), consolidator=None):
     """replays the scenario; returns (cluster, last result, last pending)"""
     cl = Cluster(sc)
+    cl.steps = {}
     arrival = sc["arrival"]
     res, pending, errors = None, [], []
-    if arrival == "together":
+    if arrival == "startup":
+        # the pod, its NodeClaim launched as a node that is still initializing
+        # (Node.Spec.Taints: the startup taints and not-ready); then a second
+        # workload while it initializes, and again once it is initialized
+        # with one startup taint still on it
+        w0, w1 = sc["workloads"]
+        startup = [tuple(t) for t in sc["nodepool"]["startup_taints"]]
+        pending = cl.make_pods(w0)
+        res = _solve_all(cl.problem(pending), solvers)
+        cl.steps["first"] = (res, pending)
+        cl.launch(res, pending, initialized=False, node_taints=startup + [("node.kubernetes.io/not-ready", "", "NoSchedule")])
+        pending = cl.make_pods(w1)
+        res = _solve_all(cl.problem(pending), solvers)
+        cl.steps["initializing"] = (res, pending)
+        for n in cl.nodes:
+            n.update(initialized=True, node_taints=[("example.com/initializing", "true", "NoSchedule")])
+        res = _solve_all(cl.problem(pending), solvers)
+        cl.steps["initialized"] = (res, pending)
+    elif arrival == "together":
         pending = [p for w in sc["workloads"] for p in cl.make_pods(w)]
         res = _solve_all(cl.problem(pending), solvers)
     elif arrival == "one_by_one":
@@ -254,6 +288,21 @@ def check_expectation(sc, cl, res, pending, consolidator=None):
             assert st == abi.GS_OK
             g, gc, gm, _ = consolidator.consolidate(mcin)
             assert (g, gc, gm) == (mw, mc, mm)
+    elif e["kind"] == "startup_taints":
+        first, fp = cl.steps["first"]
+        assert not first["errors"] and not any(first["nodes"])
+        claims = _app_claims(first, fp, app)
+        assert len(claims) == 1 and claims[0]["nodepool"] == 0
+        res1, p1 = cl.steps["initializing"]
+        assert not res1["errors"] and not res1["claims"]
+        assert res1["nodes"] == [[0]] and p1[0]["app"] == e["followup_app"]
+        res2, _ = cl.steps["initialized"]
+        assert not res2["errors"] and res2["nodes"] == [[]] and len(res2["claims"]) == 1
+    elif e["kind"] == "taint_values":
+        assert [pending[i]["app"] for i in res["errors"]] == [e["pending_app"]]
+        for a in (app, e["relaxed_app"]):
+            cs = _app_claims(res, pending, a)
+            assert len(cs) == 1 and cs[0]["nodepool"] == 0
     else:
         raise AssertionError(e["kind"])
 
