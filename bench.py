@@ -270,14 +270,15 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         t2 = time.perf_counter()
         r = solver.solve_raw(problem)
         lat.append((time.perf_counter() - t2) * 1e3)
-        phases.append((r.t_encode_ms, r.t_upload_ms, r.t_feas_ms, r.t_ffd_ms, r.t_truncate_ms, r.t_fetch_ms))
+        phases.append((r.t_encode_ms, r.t_upload_ms, r.t_feas_ms, r.t_ffd_ms, r.t_truncate_ms, r.t_fetch_ms,
+                       r.t_run_wall_ms, r.t_wall_ms))
     kms = {k: sum(x[i] for x in kt) / len(kt) for i, k in enumerate(("feas", "ffd", "trunc"))}
     n_types = len(problem.instance_types)
     ab = {"feas": feas_bytes(res.n_variants, res.n_templates, len(problem.offerings), res.words),
           "ffd": ffd_bytes(res, n_types)}
     names = {"feas": "feas_kernel", "ffd": "ffdw_kernel" if solver.flags == 0 and len(problem.nodes) <= 6144
              else "ffd_kernel"}
-    ph = np.mean(np.array(phases), axis=0) if phases else np.zeros(6)
+    ph = np.mean(np.array(phases), axis=0) if phases else np.zeros(8)
     return {
         "ms_per_step": elapsed * 1e3 / steps,
         "checks": problem.checks(),
@@ -286,7 +287,11 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         "solve_latency_ms_each": [round(x, 2) for x in lat],
         "solve_latency_phases_ms": {"encode": round(ph[0], 2), "upload": round(ph[1], 2), "feas": round(ph[2], 3),
                                     "ffd": round(ph[3], 2), "truncate": round(ph[4], 3),
-                                    "fetch_decode": round(ph[5], 2)},
+                                    "fetch_decode": round(ph[5], 2),
+                                    # the host wall clock of gs_run (kernels + launches + synchronisation),
+                                    # the C-ABI call's own wall clock and what the phases leave of it
+                                    "run_wall": round(ph[6], 2), "gs_solve_wall": round(ph[7], 2),
+                                    "unaccounted": round(ph[7] - ph[0] - ph[1] - ph[5] - ph[6], 2)},
         "prepare_ms_first_call": round(prep_ms, 2),
         "python_result_copy_ms": round(fetch_py_ms, 2),
         "new_nodeclaims": len(out["claims"]),

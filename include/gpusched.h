@@ -329,6 +329,8 @@ typedef struct gs_result {
   uint64_t claim_prefix;             /* in-flight NodeClaims a sequential first-fit visits (first feasible
                                         position + 1, or all): the reference's NodeClaim.CanAdd calls */
   uint64_t node_prefix;              /* ... and existing nodes (ExistingNode.CanAdd calls) */
+  double t_run_wall_ms;              /* host wall clock of the last gs_run (launches, kernels, synchronisation) */
+  double t_wall_ms;                  /* gs_solve: wall clock of the whole call (prepare + run + fetch); 0 from gs_fetch */
 } gs_result;
 
 /* Static pod x offering feasibility (K1/K2): for every (pod, nodepool) the

@@ -70,7 +70,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   {
     std::vector<int64_t> tv = e.thr_val;  // 4 sentinels: the device reads a 4-wide window past each range
     tv.insert(tv.end(), 4, INT64_MAX);
-    c->upload(d.thr_val, tv);
+    c->upload(d.thr_val, std::move(tv));
   }
   c->upload(d.thr_off, e.thr_off);
   {
@@ -80,7 +80,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     std::vector<uint64_t> ts(std::max<size_t>(nrows, 1) * OW, 0);
     for (size_t q = 0; q < nrows; q++)
       std::copy(e.thr_set.begin() + q * e.W, e.thr_set.begin() + (q + 1) * e.W, ts.begin() + q * OW);
-    c->upload(d.thr_set, ts);
+    c->upload(d.thr_set, std::move(ts));
   }
   c->upload(d.fk_ival, e.fk_ival);
   c->upload(d.fk_isint, e.fk_isint);
@@ -97,7 +97,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   {
     std::vector<uint32_t> vp(std::max<uint32_t>(e.V, 1), 0);
     for (uint32_t v = 0; v < e.V; v++) vp[v] = e.vars[v].pod;
-    c->upload(d.var_pod, vp);
+    c->upload(d.var_pod, std::move(vp));
   }
   c->upload(d.itclass_mask, e.itclass_mask);
   c->upload(d.fk_entries, e.fk_entries);
@@ -136,9 +136,9 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
       qcs[(size_t)k * 4 + 2] = (uint32_t)ce;
       qcs[(size_t)k * 4 + 3] = (uint32_t)(ce >> 32);
     }
-    c->upload(d.qvars, qv);
-    c->upload(d.qreqs, qr);
-    c->upload(d.qcodes, qcs);
+    c->upload(d.qvars, std::move(qv));
+    c->upload(d.qreqs, std::move(qr));
+    c->upload(d.qcodes, std::move(qcs));
   }
   d.NN = e.NN;
   // topology spread groups
@@ -174,8 +174,8 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     for (uint32_t g = 0; g < e.TGH; g++)
       for (uint32_t n = 0; n < e.NN; n++)
         if (int32_t c = e.hn0[(size_t)g * e.NN + n]) put(e.TGZ + g, c, n);
-    c->upload(d.nsp_off, off);
-    c->upload(d.nsp, sp);
+    c->upload(d.nsp_off, std::move(off));
+    c->upload(d.nsp, std::move(sp));
   } else {
     d.nsp_off = nullptr;
     d.nsp = nullptr;
@@ -217,10 +217,13 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->alloc(d.c_nits, sims ? NS : CA);
   // simulations keep the NodeClaims' hostname counts zero at rest (ffd.hip):
   // zeroed once per upload
-  if (sims)
+  c->hc_bytes = 0;
+  if (sims) {
     c->alloc_zero(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
-  else
+    c->hc_bytes = (size_t)std::max<uint32_t>(e.TGH, 1) * CA * sizeof(int32_t);
+  } else {
     c->alloc(d.hc, (size_t)std::max<uint32_t>(e.TGH, 1) * CA);
+  }
   if (sims) {
     d.n_sims = (uint32_t)NS;
     d.sim_nt = sims->nt;
@@ -242,7 +245,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     {
       std::vector<uint64_t> known = sims->known;
       known.resize(std::max<size_t>(NS, 1), 0);
-      c->upload(d.sim_known, known);
+      c->upload(d.sim_known, std::move(known));
     }
     c->alloc(d.slot_its, e.any_mv ? CA * 60 : 1);
     c->alloc(d.slot_nits, e.any_mv ? CA : 1);
@@ -532,6 +535,8 @@ void gs_destroy(gs_ctx* c) {
   c->shards.clear();
   (void)hipSetDevice(c->device);
   c->free_all();
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->stage) (void)hipHostFree(c->stage);
   if (c->cf_dev) (void)hipFree(c->cf_dev);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -581,6 +586,7 @@ static bool grow_claims(gs_ctx* c, bool force = false) {
 
 gs_status gs_run(gs_ctx* c) {
   if (!c || !c->prepared) return GS_E_INVALID;
+  const auto tw = Clock::now();
   try {
     HIPCHK(hipSetDevice(c->device));
     auto& d = c->dp;
@@ -622,6 +628,7 @@ gs_status gs_run(gs_ctx* c) {
   } catch (const HipError& e) {
     return fail(c, GS_E_HIP, e.msg);
   }
+  c->t_run_wall = ms_since(tw);
   c->ran = true;
   return GS_OK;
 }
@@ -794,15 +801,20 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
   out->t_truncate_ms = c->t_trunc;
   out->t_fetch_ms = c->t_fetch;
   out->t_total_ms = c->t_encode + c->t_upload + c->t_feas + c->t_ffd + c->t_trunc + c->t_fetch;
+  out->t_run_wall_ms = c->t_run_wall;
+  out->t_wall_ms = 0;
   return GS_OK;
 }
 
 gs_status gs_solve(gs_ctx* c, const gs_problem* p, gs_result* out) {
+  const auto tw = Clock::now();
   gs_status s = gs_prepare(c, p);
   if (s != GS_OK) return s;
   s = gs_run(c);
   if (s != GS_OK) return s;
-  return gs_fetch(c, out);
+  s = gs_fetch(c, out);
+  if (s == GS_OK) out->t_wall_ms = ms_since(tw);
+  return s;
 }
 
 gs_status gs_feasibility_shard(gs_ctx* c, uint32_t word_begin, uint32_t word_end, gs_feas_result* out) {

@@ -336,6 +336,17 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
 }
 
 // launch the device part and decide every evaluated simulation
+// A simulation clears the NodeClaim hostname-count cells it recorded at its
+// own end (ffd.hip: the rows stay zero at rest).  A launch that failed, or a
+// simulation that stopped early, may leave cells set: clear the rows so a
+// gs_consolidate_rerun on this upload starts from zero, or, when even that
+// fails, require a fresh gs_consolidate.
+void reset_sim_counts(gs_ctx* c) {
+  if (!c->hc_bytes || !c->dp.hc) return;
+  if (hipMemsetAsync(c->dp.hc, 0, c->hc_bytes, c->stream) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+    c->cons_ready = false;
+}
+
 gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   const gsh::Encoded& e = c->enc;
   const SimPlan& sp = c->sims;
@@ -371,6 +382,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
     HIPCHK(hipEventElapsedTime(&x, c->ev[2], c->ev[3]));
   } catch (const HipError& ex) {
+    reset_sim_counts(c);
     return fail(c, GS_E_HIP, ex.msg);
   }
   c->t_feas = a;
@@ -410,6 +422,7 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
   for (size_t k = 0; k < NS; k++) {
     const uint32_t s = sp.evaluated[k];
     const gsd::SimCtrl& ct = ctrl[k];
+    if (ct.status != 0) reset_sim_counts(c);
     if (ct.status == gsd::ST_POD_COUNT)
       return fail(c, GS_E_CAPACITY, "a simulated NodeClaim would hold more than 65535 pods (16-bit pod count)");
     if (ct.status != 0) return fail(c, GS_E_HIP, "simulation kernel reported an internal error");

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <string>
 #include <map>
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -104,7 +105,7 @@ struct gs_ctx {
   bool wave = false;  // the prepared Solve runs the single-wave kernel
   bool ch = false;    // ... with its claim scan state in HBM (grown past the LDS NodeClaims)
   uint32_t n_nodepools = 0;  // of the prepared problem (the caller's arrays are not kept)
-  double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0;
+  double t_encode = 0, t_upload = 0, t_feas = 0, t_ffd = 0, t_trunc = 0, t_fetch = 0, t_run_wall = 0;
   // result storage
   std::vector<uint32_t> claim_nodepool, claim_pod_offsets, claim_pods, claim_it_offsets, claim_its;
   std::vector<std::string> req_text;
@@ -166,19 +167,29 @@ struct gs_ctx {
   // Device buffers of one prepared problem come from ONE allocation (an arena
   // of 256-B aligned sub-buffers): large pages, few TLB entries for the
   // single-workgroup FFD kernel's gathers.  plan() records, commit() places.
+  // The arena and a pinned staging image of the uploaded buffers persist
+  // across prepares and only grow: commit() lays the
+  // uploaded buffers out first, copies their host arrays once into the
+  // pinned image and issues one H2D copy, without re-hipMalloc per prepare.
   struct Planned {
     void** dst;
-    size_t off, bytes;
-    std::vector<char> host;
-    bool zero = false;
+    size_t bytes;
+    const void* src;  // uploaded host bytes (nullptr: device-only buffer)
+    bool zero;
   };
   std::vector<Planned> plan;
+  std::vector<std::shared_ptr<void>> keep;  // host arrays built for one upload (live until commit)
   size_t plan_bytes = 0;
   size_t ov_hn_bytes = 0;  // the simulation overlay cells (cleared when the stamp prefix wraps)
+  size_t hc_bytes = 0;     // simulations: the NodeClaim hostname-count rows (zero at rest)
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  void* stage = nullptr;  // pinned
+  size_t stage_bytes = 0;
   template <class P>
   void alloc(P*& dst, size_t n) {
     const size_t b = std::max<size_t>(n, 1) * sizeof(P);
-    plan.push_back(Planned{(void**)&dst, plan_bytes, b, {}});
+    plan.push_back(Planned{(void**)&dst, b, nullptr, false});
     plan_bytes += (b + 255) & ~(size_t)255;
   }
   template <class P>
@@ -186,12 +197,21 @@ struct gs_ctx {
     alloc(dst, n);
     plan.back().zero = true;
   }
+  // v must live until commit(): the encoder's arrays (c->enc) or, through
+  // the rvalue overload, a temporary kept here
   template <class P, class T>
   void upload(P*& dst, const std::vector<T>& v) {
     static_assert(sizeof(P) == sizeof(T), "upload type");
     alloc(dst, v.size());
-    plan.back().host.assign((const char*)v.data(), (const char*)v.data() + v.size() * sizeof(T));
+    if (!v.empty()) plan.back().src = v.data();
   }
+  template <class P, class T>
+  void upload(P*& dst, std::vector<T>&& v) {
+    auto h = std::make_shared<std::vector<T>>(std::move(v));
+    keep.push_back(h);
+    upload(dst, *h);
+  }
+  double t_stage_ms = 0, t_h2d_ms = 0;  // commit's split: host copy into the pinned image, H2D + memsets
   void commit();
 };
 
@@ -218,15 +238,55 @@ void upload_problem(gs_ctx* c, const SimPlan* sims);
 
 inline void gs_ctx::commit() {
   using gsc::HipError;
-  void* base = nullptr;
-  HIPCHK(hipMalloc(&base, std::max<size_t>(plan_bytes, 256)));
-  allocs.push_back(base);
-  for (auto& q : plan) {
-    *q.dst = (char*)base + q.off;
-    if (!q.host.empty()) HIPCHK(hipMemcpyAsync(*q.dst, q.host.data(), q.host.size(), hipMemcpyHostToDevice, stream));
-    if (q.zero) HIPCHK(hipMemsetAsync(*q.dst, 0, q.bytes, stream));
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  // uploaded buffers first (one contiguous image), then zeroed, then the rest
+  size_t off_up = 0, off_zero = 0, off_rest = 0;
+  for (auto& q : plan)
+    if (q.src) off_up += up(q.bytes);
+    else if (q.zero) off_zero += up(q.bytes);
+    else off_rest += up(q.bytes);
+  const size_t n_up = off_up, n_zero = off_zero, total = std::max<size_t>(n_up + n_zero + off_rest, 256);
+  if (total > arena_bytes) {
+    if (arena) HIPCHK(hipFree(arena));
+    arena = nullptr;
+    arena_bytes = 0;
+    const size_t want = total + total / 4;  // headroom: a slightly larger problem reuses it
+    HIPCHK(hipMalloc(&arena, want));
+    arena_bytes = want;
   }
+  if (n_up > stage_bytes) {
+    if (stage) HIPCHK(hipHostFree(stage));
+    stage = nullptr;
+    stage_bytes = 0;
+    const size_t want = n_up + n_up / 4;
+    HIPCHK(hipHostMalloc(&stage, want, hipHostMallocDefault));
+    stage_bytes = want;
+  }
+  char* base = (char*)arena;
+  std::vector<gsh::HostCopy> copies;
+  size_t a = 0, z = n_up, r = n_up + n_zero;
+  for (auto& q : plan) {
+    if (q.src) {
+      *q.dst = base + a;
+      copies.push_back({q.src, a, q.bytes});
+      a += up(q.bytes);
+    } else if (q.zero) {
+      *q.dst = base + z;
+      z += up(q.bytes);
+    } else {
+      *q.dst = base + r;
+      r += up(q.bytes);
+    }
+  }
+  const auto t0 = gsc::Clock::now();
+  gsh::host_copy_parallel(stage, copies.data(), copies.size());
+  t_stage_ms = gsc::ms_since(t0);
+  const auto t1 = gsc::Clock::now();
+  if (n_up) HIPCHK(hipMemcpyAsync(base, stage, n_up, hipMemcpyHostToDevice, stream));
+  if (n_zero) HIPCHK(hipMemsetAsync(base + n_up, 0, n_zero, stream));
   HIPCHK(hipStreamSynchronize(stream));
+  t_h2d_ms = gsc::ms_since(t1);
   plan.clear();
+  keep.clear();
   plan_bytes = 0;
 }

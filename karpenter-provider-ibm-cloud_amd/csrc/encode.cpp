@@ -17,6 +17,12 @@
 #include <cstdlib>
 #include <exception>
 #include <thread>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <sched.h>
+#include <unistd.h>
 #include <functional>
 #include <tuple>
 #include <cmath>
@@ -37,18 +43,85 @@ const char* kNodePool = "karpenter.sh/nodepool";
 const char* kPNS = "PreferNoSchedule";
 const char* kOmega = "\x01<unmentioned>";
 
-// host threads of the encoder: GS_ENCODE_THREADS, else the hardware's, at
-// most 16 (a shared host's share; the GPU boxes give a process 16)
+// host threads of the encoder: GS_ENCODE_THREADS, else the CPUs this process
+// may run on (sched_getaffinity) shared among LOCAL_WORLD_SIZE ranks of a
+// torchrun job on the host, at most 16 (the GPU boxes give a process 16)
 uint32_t enc_threads() {
   static const uint32_t n = [] {
     if (const char* s = std::getenv("GS_ENCODE_THREADS")) {
       const int v = std::atoi(s);
       if (v >= 1) return (uint32_t)std::min(v, 64);
     }
-    const unsigned hw = std::thread::hardware_concurrency();
-    return (uint32_t)std::max(1u, std::min(hw ? hw : 1u, 16u));
+    unsigned cpus = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
+    if (!cpus) cpus = std::thread::hardware_concurrency();
+    if (const char* s = std::getenv("LOCAL_WORLD_SIZE")) {
+      const int w = std::atoi(s);
+      if (w > 1) cpus /= (unsigned)w;
+    }
+    return (uint32_t)std::max(1u, std::min(cpus ? cpus : 1u, 16u));
   }();
   return n;
+}
+
+// One process-wide pool of enc_threads() - 1 workers (started on first use,
+// never torn down) serves every par_for: a call posts tokens for its job and
+// works on it itself, so it completes even when every worker is busy (nested
+// or concurrent calls from several contexts' threads).  A forked child has
+// no workers and runs its loops serially.
+struct PoolJob {
+  std::function<void(uint32_t)> f;
+  uint32_t n = 0, grain = 1;
+  std::atomic<uint32_t> next{0}, done{0};
+  std::mutex m;
+  std::condition_variable cv;
+  void work() {
+    for (;;) {
+      const uint32_t b = next.fetch_add(grain);
+      if (b >= n) break;
+      const uint32_t e = std::min(n, b + grain);
+      for (uint32_t i = b; i < e; i++) f(i);
+      if (done.fetch_add(e - b) + (e - b) == n) {
+        std::lock_guard<std::mutex> g(m);
+        cv.notify_all();
+      }
+    }
+  }
+};
+struct Pool {
+  pid_t pid = getpid();
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<PoolJob>> tokens;
+  uint32_t workers = 0;
+  explicit Pool(uint32_t n) {
+    for (uint32_t t = 0; t < n; t++) {
+      try {
+        std::thread([this] { loop(); }).detach();
+        workers++;
+      } catch (const std::system_error&) {
+        break;  // fewer workers: callers still finish their own jobs
+      }
+    }
+  }
+  void loop() {
+    for (;;) {
+      std::shared_ptr<PoolJob> j;
+      {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return !tokens.empty(); });
+        j = std::move(tokens.front());
+        tokens.pop_front();
+      }
+      j->work();
+    }
+  }
+};
+Pool* pool() {
+  static Pool* p = new Pool(enc_threads() - 1);  // intentionally never destroyed (workers block on it)
+  return p;
 }
 
 // f(i) for every i in [0, n), chunks of `grain` handed out to up to
@@ -58,30 +131,23 @@ template <class F>
 void par_for(uint32_t n, uint32_t grain, F&& f) {
   grain = std::max<uint32_t>(grain, 1);
   const uint32_t T = std::min<uint32_t>(enc_threads(), (n + grain - 1) / grain);
-  if (T <= 1) {
+  Pool* pl = T > 1 ? pool() : nullptr;
+  if (T <= 1 || !pl->workers || pl->pid != getpid()) {
     for (uint32_t i = 0; i < n; i++) f(i);
     return;
   }
-  std::atomic<uint32_t> next{0};
-  auto work = [&] {
-    for (;;) {
-      const uint32_t b = next.fetch_add(grain);
-      if (b >= n) break;
-      const uint32_t e = std::min(n, b + grain);
-      for (uint32_t i = b; i < e; i++) f(i);
-    }
-  };
-  std::vector<std::thread> th;
-  th.reserve(T - 1);
-  for (uint32_t t = 1; t < T; t++) {
-    try {
-      th.emplace_back(work);
-    } catch (const std::system_error&) {
-      break;  // fewer threads: the atomic counter still covers every chunk
-    }
+  auto j = std::make_shared<PoolJob>();
+  j->f = [&f](uint32_t i) { f(i); };
+  j->n = n;
+  j->grain = grain;
+  {
+    std::lock_guard<std::mutex> g(pl->m);
+    for (uint32_t t = 1; t < T && t <= pl->workers; t++) pl->tokens.push_back(j);
   }
-  work();
-  for (auto& t : th) t.join();
+  pl->cv.notify_all();
+  j->work();
+  std::unique_lock<std::mutex> g(j->m);
+  j->cv.wait(g, [&] { return j->done.load() == n; });
 }
 
 // <U> v1.WellKnownLabels + IBM keys (reference pkg/apis/v1alpha1/labels.go:37-45)
@@ -2311,6 +2377,20 @@ Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
     return Err{GS_E_INVALID, std::string("unknown vocabulary value: ") + ex.what()};
   }
   return Err{};
+}
+
+void host_copy_parallel(void* dst_base, const HostCopy* copies, size_t n) {
+  // pieces of at most 1 MiB, handed out to the encoder's threads
+  constexpr size_t kPiece = 1u << 20;
+  std::vector<HostCopy> pieces;
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++)
+    for (size_t o = 0; o < copies[i].bytes; o += kPiece)
+      pieces.push_back({(const char*)copies[i].src + o, copies[i].off + o, std::min(kPiece, copies[i].bytes - o)});
+  for (auto& p : pieces) total += p.bytes;
+  char* dst = (char*)dst_base;
+  par_for((uint32_t)pieces.size(), total >= (8u << 20) ? 1u : (uint32_t)pieces.size() + 1,
+          [&](uint32_t i) { std::memcpy(dst + pieces[i].off, pieces[i].src, pieces[i].bytes); });
 }
 
 // label helpers shared with the launch-time re-filter (filter.hip)

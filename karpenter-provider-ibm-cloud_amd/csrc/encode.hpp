@@ -173,4 +173,12 @@ KReq kreq_intersect(const Vocab& v, const KReq& a, const KReq& b);
 void reqs_add(const Encoded& e, Reqs& r, uint32_t key, const KReq& q);
 std::string canonical(const Encoded& e, const Reqs& r);
 
+// host -> host copies of an upload image (gs_ctx::commit), split over the
+// encoder's threads when large
+struct HostCopy {
+  const void* src;
+  size_t off, bytes;
+};
+void host_copy_parallel(void* dst_base, const HostCopy* copies, size_t n);
+
 }  // namespace gsh

@@ -124,6 +124,7 @@ class GsResult(C.Structure):
         ("t_total_ms", C.c_double),
         ("t_ffd_sort_ms", C.c_double), ("t_ffd_scan_ms", C.c_double), ("t_ffd_template_ms", C.c_double),
         ("claim_prefix", C.c_uint64), ("node_prefix", C.c_uint64),
+        ("t_run_wall_ms", C.c_double), ("t_wall_ms", C.c_double),
     ]
 
 
