@@ -1584,6 +1584,60 @@ struct Ctx {
   }
 
   // --------------------------------------------------------------- pods
+  // <U> ExistingNode.CanAdd: a node lacking a label satisfies a pod's
+  // NotIn / DoesNotExist on it (Requirements.Compatible), and Add then gives
+  // the node a requirement on that key, which later pods meet by intersection.
+  // Instance-type, zone and capacity-type keys hold a node's label as one
+  // value id; where some node lacks such a key that some pod term constrains
+  // with NotIn / DoesNotExist, the key also gets a free slot ("shadow") that
+  // carries the nodes' full requirement state, and the node check runs on it
+  // instead of the value id.  Claims keep their own checks (the shadow entry
+  // is a redundant, well-known free key there).  Not for a zone key that
+  // topology counts on (a node's zone domain comes from its label).
+  void choose_shadow_keys() {
+    if (!p->n_nodes) return;
+    std::set<uint32_t> constrained;
+    // every key a pod's node selector or terms mention: a variant's
+    // requirement can come out NotIn / DoesNotExist from In / Gt / Lt terms
+    // too (an empty intersection is DoesNotExist)
+    auto scan = [&](const gs_pod* pods, uint32_t n) {
+      for (uint32_t i = 0; i < n; i++) {
+        const gs_range sr = pods[i].node_selector;
+        chk(sr, p->n_labels, "labels");
+        for (uint32_t j = 0; j < sr.count; j++) constrained.insert(key_of(p->labels[sr.begin + j].key));
+        for (gs_range tr : {pods[i].required_terms, pods[i].preferred_terms}) {
+          chk(tr, p->n_terms, "terms");
+          for (uint32_t t = 0; t < tr.count; t++) {
+            const gs_range rr = p->terms[tr.begin + t].requirements;
+            chk(rr, p->n_reqs, "reqs");
+            for (uint32_t q = 0; q < rr.count; q++) constrained.insert(key_of(p->reqs[rr.begin + q].key));
+          }
+        }
+      }
+    };
+    scan(p->pods, p->n_pods);
+    if (p->bound_pods) scan(p->bound_pods, p->n_bound_pods);
+    bool zone_topology = false;
+    for (uint32_t i = 0; i < p->n_spreads; i++) zone_topology = zone_topology || normalize(S(p->spreads[i].topology_key)) == kZone;
+    for (uint32_t i = 0; i < p->n_affinity_terms; i++)
+      zone_topology = zone_topology || normalize(S(p->affinity_terms[i].topology_key)) == kZone;
+    for (uint32_t k : constrained) {
+      Key& key = e.keys[k];
+      if (key.cls == KEY_FREE || !key.wellknown || key.vocab.size() > (size_t)gsd::FKV) continue;
+      if (key.cls == KEY_ZONE && zone_topology) continue;
+      bool lacking = false;
+      for (uint32_t i = 0; i < p->n_nodes && !lacking; i++) {
+        const gs_range lr = p->nodes[i].labels;
+        chk(lr, p->n_labels, "labels");
+        bool has = false;
+        for (uint32_t j = 0; j < lr.count && !has; j++) has = key_of(p->labels[lr.begin + j].key) == k;
+        lacking = !has;
+      }
+      if (lacking) shadow_keys.push_back(k);
+    }
+  }
+  std::vector<uint32_t> shadow_keys;
+
   void build_free_slots() {
     for (uint32_t k = 0; k < e.keys.size(); k++) {
       if (e.keys[k].cls != KEY_FREE) continue;
@@ -1592,6 +1646,13 @@ struct Ctx {
       if (e.free_keys.size() >= (size_t)gsd::FMAX) throw Fail{GS_E_UNSUPPORTED, "more than 16 free requirement keys"};
       e.keys[k].slot = (int)e.free_keys.size();
       if (e.keys[k].wellknown) e.wk_slots |= 1ull << e.free_keys.size();
+      e.free_keys.push_back(k);
+    }
+    choose_shadow_keys();
+    for (uint32_t k : shadow_keys) {
+      if (e.free_keys.size() >= (size_t)gsd::FMAX) break;  // build_nodes refuses what stays unshadowed
+      e.keys[k].shadow = (int)e.free_keys.size();
+      e.wk_slots |= 1ull << e.free_keys.size();
       e.free_keys.push_back(k);
     }
     e.F = (uint32_t)e.free_keys.size();
@@ -1606,9 +1667,11 @@ struct Ctx {
     }
     e.t_fk.assign((size_t)e.T * std::max<uint32_t>(e.F, 1), gsd::FK{});
     for (uint32_t t = 0; t < e.T; t++)
-      for (auto& kv : e.tmpl_reqs[t])
-        if (e.keys[kv.first].cls == KEY_FREE)
-          e.t_fk[(size_t)t * e.F + e.keys[kv.first].slot] = to_fk(kv.second);
+      for (auto& kv : e.tmpl_reqs[t]) {
+        const Key& key = e.keys[kv.first];
+        if (key.cls == KEY_FREE || key.shadow >= 0)
+          e.t_fk[(size_t)t * e.F + (key.cls == KEY_FREE ? key.slot : key.shadow)] = to_fk(kv.second);
+      }
   }
 
   // A pod's spec as bytes: everything but its uid, creation time, requests
@@ -2170,13 +2233,19 @@ struct Ctx {
       vr.zflags = zone_flags(pv.reqs);
       vr.tol = vr.tolt = 0;  // build_taint_classes
       vr.fk_begin = (uint32_t)e.fk_entries.size();
-      for (auto& kv : pv.reqs)
-        if (e.keys[kv.first].cls == KEY_FREE) {
-          gsd::FKEntry fe{};
-          fe.slot = (uint32_t)e.keys[kv.first].slot;
-          fe.st = to_fk(kv.second);
-          e.fk_entries.push_back(fe);
-        }
+      for (auto& kv : pv.reqs) {
+        const Key& key = e.keys[kv.first];
+        if (key.cls != KEY_FREE && key.shadow < 0) continue;
+        gsd::FKEntry fe{};
+        fe.slot = (uint32_t)(key.cls == KEY_FREE ? key.slot : key.shadow);
+        fe.st = to_fk(kv.second);
+        e.fk_entries.push_back(fe);
+        // the existing-node check of a shadowed key runs on its free slot
+        // (the IT-key class above already has this key's mask)
+        if (key.cls == KEY_IT) vr.itmask_off[key.slot] = gsd::NONE;
+        else if (key.cls == KEY_ZONE) vr.zfull_off = gsd::NONE;
+        else vr.cfull_off = gsd::NONE;
+      }
       vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
     }
     par_for(e.P, 1024, [&](uint32_t i) {
@@ -2265,7 +2334,8 @@ struct Ctx {
     std::set<uint32_t> exempt_keys;
     for (auto& pv : e.variants)
       for (auto& kv : pv.reqs)
-        if (e.keys[kv.first].cls != KEY_FREE && exempt(kv.second)) exempt_keys.insert(kv.first);
+        if (e.keys[kv.first].cls != KEY_FREE && e.keys[kv.first].shadow < 0 && exempt(kv.second))
+          exempt_keys.insert(kv.first);
     for (uint32_t pos = 0; pos < e.NN; pos++) {
       const gs_node& g = p->nodes[order[pos]];
       gsd::NodeRec& nr = e.nodes[pos];
@@ -2280,6 +2350,7 @@ struct Ctx {
           e.n_fk[(size_t)pos * e.F + key.slot] = to_fk(kv.second);
           continue;
         }
+        if (key.shadow >= 0) e.n_fk[(size_t)pos * e.F + key.shadow] = to_fk(kv.second);
         // a label is In[v]: exactly one has-bit
         uint32_t vid = gsd::NONE;
         for (size_t i = 0; i < key.vocab.size(); i++)
@@ -2290,7 +2361,9 @@ struct Ctx {
       }
       for (uint32_t k : exempt_keys) {
         bool has = reqs.count(k) != 0;
-        if (!has) throw Fail{GS_E_UNSUPPORTED, "existing node lacks a label that a pod constrains with NotIn/DoesNotExist"};
+        if (!has)
+          throw Fail{GS_E_UNSUPPORTED, "existing node lacks a label that a pod constrains with NotIn/DoesNotExist (" +
+                                           e.keys[k].name + ": no free slot left, or its vocabulary exceeds 255 values)"};
       }
       bool present[gsd::RMAX] = {false};
       resvec_fn(g.available, nr.avail, present);

@@ -72,6 +72,10 @@ struct Key {
   KeyClass cls = KEY_FREE;
   bool wellknown = false;
   int slot = -1;  // IT-key index or free slot
+  // instance-type / zone / capacity-type key that an existing node lacks while
+  // a pod constrains it (possibly NotIn / DoesNotExist): the nodes' requirement on it
+  // lives in this free slot (the node gains state there, <U> ExistingNode.Add)
+  int shadow = -1;
 };
 
 using Reqs = std::map<uint32_t, KReq>;  // key id -> requirement

@@ -251,12 +251,15 @@ _KEYS_FREE = ["kubernetes.io/os", "karpenter.sh/nodepool", "team", "karpenter-ib
               "kubernetes.io/hostname", "tier"]
 
 
-def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_values=3, inflight=False):
+def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_values=3, inflight=False,
+                   partial_labels=False):
     """small adversarial problem over the whole supported feature set;
     free_values > 3 widens the custom (free) keys team / tier to that many
     values (tier's integers then reach free_values - 1 for Gt / Lt);
     inflight: the existing nodes are karpenter-launched ones, some still
-    initializing, with startup / ephemeral taints (inflight_node)"""
+    initializing, with startup / ephemeral taints (inflight_node);
+    partial_labels: nodes may lack instance-type / zone / capacity-type labels
+    (nodes karpenter did not launch, drop_node_labels)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3"][: int(rng.integers(1, 4))]
@@ -332,6 +335,8 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_va
                 labels["team"] = vocab["team"][rng.integers(0, nteam)]
             avail = {"cpu": int(rng.choice([500, 1000, 4000])), "memory": int(rng.choice([1, 4, 16])) * GI * 1000,
                      "pods": 10_000}
+            if partial_labels:
+                drop_node_labels(rng, labels)
             if inflight:
                 b.add_node(f"node-{k}", labels, avail, **inflight_node(rng, np_taints[rng.integers(0, n_np)]))
             else:
@@ -364,6 +369,20 @@ def random_problem(seed, n_pods=None, with_nodes=True, with_limits=True, free_va
         b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + int(rng.integers(0, 4)) * 1_000_000_000, req,
                   node_selector=sel, required_terms=required, preferred_terms=preferred, tolerations=tols)
     return b.build()
+
+
+PARTIAL_LABEL_KEYS = ["karpenter-ibm.sh/instance-family", "karpenter-ibm.sh/instance-size", "kubernetes.io/arch",
+                      "karpenter.sh/capacity-type", "node.kubernetes.io/instance-type", "topology.kubernetes.io/zone"]
+
+
+def drop_node_labels(rng, labels, p=0.6):
+    """a node karpenter did not launch (no karpenter-ibm.sh/* labels, labels.go:37-45) or
+    without some well-known label: drops a random subset of those keys, in place"""
+    if rng.random() < p:
+        for k in PARTIAL_LABEL_KEYS:
+            if k in labels and rng.random() < 0.4:
+                del labels[k]
+    return labels
 
 
 # NodeClaim spec.startupTaints seen on in-flight nodes (e.g. NodePool
@@ -500,7 +519,7 @@ def make_c4(n_nodes=5000, n_pending=0, seed=0x5EED0004, util=(0.6, 0.9), n_its=2
 CONFIGS["C4"] = make_c4
 
 
-def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False):
+def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False, partial_labels=False):
     """small adversarial consolidation cluster: nodes with taints, custom
     labels, spot/on-demand, uninitialized nodes and bound pods with
     selectors/tolerations; pending pods; 1-3 NodePools (taints, limits)"""
@@ -557,9 +576,22 @@ def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False):
             tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []
             if inflight and rng.random() < 0.3:
                 tols.append(("example.com/initializing", "Exists", "", ""))
+            req_terms = []
+            if partial_labels:
+                r = rng.random()
+                if r < 0.3:
+                    req_terms = [[("karpenter-ibm.sh/instance-family", "NotIn", [str(rng.choice(["mx2", "gx2"]))])]]
+                elif r < 0.4:
+                    req_terms = [[("karpenter-ibm.sh/instance-size", "DoesNotExist", [])]]
+                elif r < 0.5:
+                    req_terms = [[("karpenter.sh/capacity-type", "NotIn", ["spot"])]]
+                elif r < 0.6:
+                    req_terms = [[("kubernetes.io/arch", "In", ["amd64"])]]
             b.add_bound_pod(k, _uid(rng), ts, {"cpu": cpu, "memory": mem, "pods": 1000}, node_selector=sel,
-                            tolerations=tols)
+                            tolerations=tols, required_terms=req_terms)
         avail = {r: alloc[r] - used.get(r, 0) for r in alloc}
+        if partial_labels:
+            drop_node_labels(rng, labels)
         if inflight:
             b.add_node(f"n-{k:03d}", labels, avail, **inflight_node(rng, np_taints[int(labels["karpenter.sh/nodepool"][2:])]))
         else:
