@@ -194,6 +194,8 @@ def headline(line):
     if views:
         h["roofline_views"] = views
     h["cpu_baseline"] = _compact_cpu(line.get("cpu_baseline"))
+    if line.get("strong_scaling"):
+        h["strong_scaling"] = line["strong_scaling"]
     for k in ("solve_latency_phases_ms", "queue_pops", "new_nodeclaims", "pod_errors", "go_sort_emulation",
               "device_kernel_ms"):
         if line.get(k) is not None:
@@ -210,11 +212,31 @@ def headline(line):
     if line.get("detail_file"):
         h["detail_file"] = line["detail_file"]
     # shed detail (never the contract keys) until the line fits
-    for drop in ("legs", "roofline_views", "solve_latency_phases_ms", "go_sort_emulation", "device_kernel_ms"):
+    for drop in ("legs", "roofline_views", "solve_latency_phases_ms", "go_sort_emulation", "device_kernel_ms",
+                 "strong_scaling"):
         if len(json.dumps(h)) <= HEADLINE_MAX_BYTES:
             break
         h.pop(drop, None)
     return h
+
+
+def strong_scaling_section(per_rank, world, backend, max_over_ranks):
+    """N > 1: the legs that shard a fixed job over the ranks,
+    for the headline -- the C5 static matrix split by instance-type words
+    (each rank's kernel, then the RCCL all-gather of the word slices + SUM /
+    MIN) and the C4 consolidation sweep split by candidate (each rank's
+    simulation kernel, then the all-gather of the commands + the host policy
+    replay).  per_rank: this rank's {leg: {timing: ms}}; every timing is the
+    max over ranks (the job waits for the slowest), taken with
+    max_over_ranks; the other fields come from rank 0's record."""
+    out = {"ranks": world, "backend": backend, "scaling": "strong"}
+    for leg in sorted(per_rank):
+        rec = dict(per_rank[leg])
+        for k in sorted(rec):
+            if k.endswith("_ms"):
+                rec[k] = _r(max_over_ranks(float(rec[k])))
+        out[leg] = rec
+    return out
 
 
 def emit(line, detail_path, rank):
@@ -447,16 +469,21 @@ def consolidation_leg(problem, mode, args, rank, world, local, dist, device, bar
     solver.consolidate(cin)  # encode + upload + first run
     prep_ms = (time.perf_counter() - t0) * 1e3
 
+    gch = []
+
     def sweep():
         r = solver.consolidate_rerun(raw=True)
         if world == 1:
             return None, int(r.chosen), r
+        t1 = time.perf_counter()
         merged = gather_arrays(*result_arrays(r), rank, world, dist, device)
         chosen, _ = choose_arrays(full, *merged)
+        gch.append((time.perf_counter() - t1) * 1e3)
         return merged, chosen, r
 
     for _ in range(args.warmup):
         sweep()
+    gch.clear()
     kt = []
     steps = args.steps
     barrier()
@@ -496,6 +523,8 @@ def consolidation_leg(problem, mode, args, rank, world, local, dist, device, bar
         "node_checks_per_s": r.checks * world / (ms * 1e-3),
         "kernel_ms": {"feas": round(feas_ms, 4), "sim": round(sim_ms, 4), "trunc": round(trunc_ms, 4)},
         "host_decide_fetch_ms": round(decide_ms, 3),
+        # N > 1: all-gather of the command tables over the ranks + the host policy replay (this rank)
+        "gather_choose_ms": round(sum(gch) / len(gch), 3) if gch else 0.0,
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "pods_simulated": int(r.pods_simulated),
         "node_prefix": int(r.node_prefix),
@@ -559,16 +588,21 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
     W = (len(problem.instance_types) + 63) // 64
     wb, we = word_range(W, rank, world)
 
+    comb = []
+
     def step():
         r = solver.feasibility_shard_device(wb, we)  # returns after the kernel
         if world > 1:
+            t1 = time.perf_counter()
             device_combine(r, dist, device)
             import torch
             torch.cuda.synchronize(device)
+            comb.append((time.perf_counter() - t1) * 1e3)
         return r
 
     for _ in range(args.warmup):
         step()
+    comb.clear()
     kms = []
     barrier()
     t0 = time.perf_counter()
@@ -579,6 +613,7 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
     elapsed = max_over_ranks(time.perf_counter() - t0)
     ms = elapsed * 1e3 / args.steps
     k_ms = sum(kms) / len(kms)
+    combine_ms = sum(comb) / len(comb) if comb else 0.0
     equal = None
     if world > 1:
         import torch
@@ -603,6 +638,7 @@ def bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks
         "words_per_rank": we - wb,
         "variants": r.n_variants,
         "kernel_ms": round(k_ms, 4),
+        "combine_ms": round(combine_ms, 4),  # N > 1: RCCL all-gather of the word slices + SUM / MIN (this rank)
         "prepare_ms_encode_plus_pcie_upload": round(prep_ms, 1),
         "shards_equal_whole": equal,
         "roofline": roofline("feas_cursor_kernel + feas_kernel", ab, k_ms, traffic_of(traffic, "c5", "feas", "feas_cursor")),
@@ -933,6 +969,21 @@ def main():
         line["stress"] = bench_stress(args, rank, world, local, dist, device, barrier, max_over_ranks, traffic)
     if solo and only in (None, "ranking"):
         line["ranking"] = bench_ranking(args)
+    if world > 1:
+        per_rank = {}
+        st = line.get("stress")
+        if st:
+            per_rank["c5_static_matrix_it_columns"] = {
+                "ms_per_step": st["ms_per_step"], "kernel_ms": st["kernel_ms"], "combine_ms": st["combine_ms"],
+                "words_per_rank": st["words_per_rank"], "checks_per_s": _r(st["value"]),
+                "shards_equal_whole": st["shards_equal_whole"]}
+        for name, leg in (line.get("consolidation_legs") or {}).items():
+            per_rank[f"{name}_candidates"] = {
+                "ms_per_sweep": leg["ms_per_sweep"], "sim_kernel_ms": leg["kernel_ms"]["sim"],
+                "gather_choose_ms": leg["gather_choose_ms"], "simulations": leg["simulations"],
+                "simulations_per_s": _r(leg["value"])}
+        backend = dist.get_backend() if dist is not None else None
+        line["strong_scaling"] = strong_scaling_section(per_rank, dist.get_world_size(), backend, max_over_ranks)
     if _POOL is not None:
         _POOL.close()
         _POOL.join()

@@ -93,7 +93,15 @@ __device__ __forceinline__ uint32_t rlane(uint32_t x, uint32_t i) {
 }
 
 // GS_FFD_TL (diagnostic build): shader cycles per pod-loop segment into Ctrl.dbg
-#ifdef GS_FFD_TL
+#if defined(GS_FFD_TL) && defined(GS_CAT_SEG)
+// with GS_CAT_TL: the segments of the pods of category GS_CAT_SEG only
+#define TLW(k)                                         \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
+    ptl[k] += t_ - tl_last;                            \
+    tl_last = t_;                                      \
+  } while (0)
+#elif defined(GS_FFD_TL)
 #define TLW(k)                                         \
   do {                                                 \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
@@ -906,7 +914,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   bool wrapped = false;
   uint64_t pops = 0;
   // instrumentation counters, lane k = counter k (no scalar registers)
-  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG };
+  enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG,
+         // run mode (diagnostics, Ctrl.dbg[8..13] outside the timeline build)
+         C_RPODS, C_RENTER, C_RX_PIVOT, C_RX_WIN, C_RX_SPEC, C_RX_SCAN };
   uint64_t ctr = 0;
 #ifdef GS_NO_CTR  // experiment builds: the counters' cost
 #define CTR(k, x) ((void)0)
@@ -924,19 +934,225 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   const uint64_t max_pops = ((uint64_t)(d.V - d.P) + 2) * (uint64_t)P + P + 16;
 
 #ifdef GS_FFD_TL
+#ifdef GS_CAT_SEG
+  uint64_t ptl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, n_cat = 0;
+#endif
   uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_last = __builtin_amdgcn_s_memtime();
   uint64_t n_fsum = 0, n_xns = 0, n_xb = 0, n_xwin = 0, n_nonsimple = 0, n_rot = 0, n_rotlen = 0, n_gen_cyc = 0;
 #endif
   uint32_t pf_x = 0, pf_seq = 0;  // prefetched ring record and its sequence word
+  // Runs of identical simple pods (GS_RUNS).  Queue order puts equal
+  // requests together (cpu, memory descending), so most first-pass pods
+  // repeat the previous pod's spec (CM: 88 % of pods, runs of 8 on average).
+  // For such a pod the whole NodeClaim.CanAdd chain -- the pending one-claim
+  // sort.Slice rotation, the scan from the infeasible-prefix bound, the fast
+  // accept -- only reads and writes the 64 sorted positions from the last
+  // Add on: the run keeps that window (order word, slack and room codes,
+  // template tolerated) in registers and places pod after pod there, with the
+  // same rotation, ballots and code arithmetic as the LDS path, so the result
+  // is bit-identical.  Anything else (a pivot sample touched, a run of equal
+  // keys leaving the window, a candidate needing the exact check, no
+  // candidate in the window, another spec) writes the window back and hands
+  // the pod to the general path below.
+#ifndef GS_RUNS
+#define GS_RUNS 1
+#endif
+#ifdef GS_RUN_TL
+  uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
+#endif
+#ifdef GS_CAT_TL
+  // diagnostic build: shader cycles per pod category (lane k = category k):
+  // 0 run mode, 1 simple pod on an in-flight claim, 3 other pod on an
+  // in-flight claim, 4 new NodeClaim, 5 failed (relax / push), 6 on an
+  // existing node
+  uint64_t cat_cyc = 0, cat_n = 0, cat_t = __builtin_amdgcn_s_memtime();
+  uint32_t cat_k = 7;
+#define CAT(k) (cat_k = (k))
+#else
+#define CAT(k) ((void)0)
+#endif
+  bool run_prev = false;  // the last pod was a first-pass simple pod placed on an in-flight NodeClaim
+  uint32_t run_rec = 0;   // its ring record (lanes: VarRec dwords, requests, request codes)
   for (;;) {
     // ---------------------------------------------------------- Queue.Pop
     TLW(7);  // previous pod's tail (continue paths)
+#ifdef GS_CAT_TL
+    {
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();
+      cat_cyc += lane == cat_k ? t_ - cat_t : 0ull;
+      cat_n += lane == cat_k && cat_k != 0 ? 1ull : 0ull;
+      cat_t = t_;
+#if defined(GS_FFD_TL) && defined(GS_CAT_SEG)
+      if (cat_k == GS_CAT_SEG) {
+        n_cat++;
+#pragma unroll
+        for (int q = 0; q < 8; q++) tl[q] += ptl[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) ptl[q] = 0;
+#endif
+      cat_k = 7;
+    }
+#endif
     if (status) break;
     if (pops > max_pops) {
       status = 2;
       break;
     }
     if (qlen == 0) break;
+    // (the narrow non-topology instantiation only: the topology and wide-row
+    // instantiations measured slower with the run code in them, C3 398 -> 420,
+    // e2e 273 -> 283, C5 1,245 -> 1,292 ms, profiles/r5/runs_ab.txt)
+    if (GS_RUNS && !TOPO && !WIDE && run_prev && !wrapped && modkind == MOD_INC && M >= 50 && d.NN == 0) {
+      run_prev = false;
+      auto same_spec = [&](uint32_t x) {
+        return __ballot(lane >= 1 && lane < RING_DW && lane != VR_DW - 1 && x != run_rec) == 0;
+      };
+      if (__builtin_amdgcn_readfirstlane(pf_seq) == qhead + 1 && same_spec(pf_x)) {
+        // the run's spec: tolerated templates, request codes and requests
+        const uint64_t r_tolt = (uint64_t)rlane(run_rec, 20) | ((uint64_t)rlane(run_rec, 21) << 32);
+        const uint64_t r_rqq = (uint64_t)rlane(run_rec, RING_CODES) | ((uint64_t)rlane(run_rec, RING_CODES + 1) << 32);
+        const uint64_t r_rqc = (uint64_t)rlane(run_rec, RING_CODES + 2) | ((uint64_t)rlane(run_rec, RING_CODES + 3) << 32);
+        int64_t r_rq = 0;  // lane r < R: request r
+        {
+          const uint32_t lo = (uint32_t)__shfl((int)run_rec, (int)(32 + 2 * (lane & 7))),
+                         hi = (uint32_t)__shfl((int)run_rec, (int)(33 + 2 * (lane & 7)));
+          if (lane < RR) r_rq = (int64_t)(((uint64_t)hi << 32) | lo);
+        }
+        // the window: sorted positions [base, base + 64), the last Add's claim at lane 0
+        const uint32_t base = modpos;
+        const uint32_t wpos = base + lane;
+        const bool valid = wpos < M;
+        uint32_t ow = valid ? (uint32_t)s_so[wpos] : 0xFFFFu;  // past M: key 0xFFFF ends every run of equal keys
+        uint64_t wsl = 0, wrm = 0;
+        uint32_t wtok = 0;
+        if (valid) {
+          const uint32_t je = ow >> 16;
+          wsl = s_slk[je];
+          wrm = s_rm[je];
+          wtok = (uint32_t)((r_tolt >> (T > 1 ? (uint32_t)s_tmpl[je] : 0u)) & 1u);
+        }
+        uint32_t lf = 0;  // lane of the claim the last Add raised
+        bool dirty = false;
+        CTR(C_RENTER, 1);
+        CAT(0);
+#ifdef GS_RUN_TL
+        const uint64_t rt0 = __builtin_amdgcn_s_memtime();
+#endif
+        for (;;) {
+          if (pivot_touched(MOD_INC, modpos, M)) {
+            CTR(C_RX_PIVOT, 1);
+            break;
+          }
+          // sort.Slice: the raised claim moves to the end of its run of equal keys
+          const uint32_t x = rlane(ow, lf) & 0xFFFFu;
+          const uint64_t b = __ballot(lane > lf && (ow & 0xFFFFu) >= x);
+          if (!b) {  // the run leaves the window: the general sort (modkind stays INC)
+            CTR(C_RX_WIN, 1);
+            break;
+          }
+          const uint32_t eo = ffs64(b);
+          if (eo > lf + 1) {
+            CTR(C_FAST, 1);
+            auto rot = [&](uint32_t y) -> uint32_t {
+              const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x130, 0xF, 0xF, false);  // lane i <- i + 1
+              const uint32_t y0 = rlane(y, lf);
+              return lane + 1 == eo ? y0 : (lane >= lf && lane + 1 < eo) ? sh : y;
+            };
+            ow = rot(ow);
+            wsl = ((uint64_t)rot((uint32_t)(wsl >> 32)) << 32) | rot((uint32_t)wsl);
+            wrm = ((uint64_t)rot((uint32_t)(wrm >> 32)) << 32) | rot((uint32_t)wrm);
+            wtok = rot(wtok);
+            dirty = true;
+          }
+          modkind = MOD_NONE;
+          // the next pod: the same spec, staged in the ring?
+          if (!(__builtin_amdgcn_readfirstlane(pf_seq) == qhead + 1 && same_spec(pf_x))) {
+            CTR(C_RX_SPEC, 1);
+            break;
+          }
+          if (pops + 1 > max_pops || qhead + 1 == P) break;
+          // the scan from the infeasible-prefix bound (the last Add's
+          // position): the first candidate must be a fast accept
+          const uint32_t lo = modpos - base;
+          const bool lp = (lane >= lo) & valid & (wtok != 0) & swar_ge(wsl, r_rqq);
+          const uint64_t lpb = __ballot(lp), fab = __ballot(lp & swar_ge(wrm, r_rqc));
+          if (!lpb || !(fab & 1ull << ffs64(lpb))) {
+            CTR(C_RX_SCAN, 1);
+            break;
+          }
+          const uint32_t fl = ffs64(lpb);
+          const uint32_t e = rlane(ow, fl);
+          if ((e & 0xFFFFu) == 0xFFFFu) {
+            status = 3;  // the u16 pod count would overflow
+            break;
+          }
+          // Queue.Pop of the pod (first pass: the ring record at qhead)
+          const uint32_t x_rec = pf_x;
+          const uint32_t pp = rlane(x_rec, 0), pv = rlane(x_rec, VR_DW - 1);
+          wsyncT<CH>();
+          if (lane == 0) vst(&s_ctl[0], qhead + 1);  // the slot may be refilled
+          qhead++;
+          qlen--;
+          pops++;
+          if ((pops & 15) == 0 && lane == 0) vst(&s_ctl[3], (uint32_t)pops);
+          pf_seq = vld(&s_ring_seq[qhead % RING]);
+          pf_x = lane < RING_DW ? vld(&s_ring[qhead % RING][lane]) : 0u;
+          // fast accept: NodeClaim.Add changes the requests only; room and
+          // slack of lane fl shrink by the request (lanes r < RQ re-quantize
+          // resource r, packed across lanes 0..3 as in the general path)
+          const uint64_t rm = ((uint64_t)rlane((uint32_t)(wrm >> 32), fl) << 32) | rlane((uint32_t)wrm, fl);
+          const uint64_t sl = ((uint64_t)rlane((uint32_t)(wsl >> 32), fl) << 32) | rlane((uint32_t)wsl, fl);
+          uint32_t c_rm = 0, c_sl = 0;
+          if (lane < d.RQ) {
+            const uint32_t sh = 16 * lane;
+            c_rm = qcode_floor(qcode_value((uint32_t)(rm >> sh) & 0xFFFFu) - r_rq);
+            c_sl = qcode_ceil(qcode_value((uint32_t)(sl >> sh) & 0xFFFFu) - r_rq);
+          }
+          uint32_t prm = (lane & 1u) ? c_rm << 16 : c_rm, psl = (lane & 1u) ? c_sl << 16 : c_sl;
+          prm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+          psl |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl, 0xB1, 0xF, 0xF, false);
+          const uint32_t hrm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm, 0x102, 0xF, 0xF, false);  // row_shl:2
+          const uint32_t hsl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl, 0x102, 0xF, 0xF, false);
+          const uint64_t nrm = (uint64_t)rlane(prm, 0) | ((uint64_t)rlane(hrm, 0) << 32);
+          const uint64_t nsl = (uint64_t)rlane(psl, 0) | ((uint64_t)rlane(hsl, 0) << 32);
+          if (lane == fl) {
+            wrm = nrm;
+            wsl = nsl;
+            ow = e + 1u;
+          }
+          dirty = true;
+          const uint32_t f = base + fl;
+          emit(WQ_FA, nlog, pp, pv, e >> 16, run_rec, r_rq);  // the requests into the claim totals, and the log
+          nlog++;
+          CTR(C_CAND, M - modpos < 64 ? M - modpos : 64);
+          CTR(C_FA, 1);
+          CTR(C_ALG, f + 1);
+          CTR(C_RPODS, 1);
+#ifdef GS_CAT_TL
+          cat_n += lane == 0 ? 1ull : 0ull;
+#endif
+          hint = f;
+          modkind = MOD_INC;
+          modpos = f;
+          lf = fl;
+        }
+        if (dirty) {
+          // the window back to LDS: positions, and the codes of its claims
+          wsyncT<CH>();
+          if (valid) {
+            s_so[wpos] = ow;
+            s_slk[ow >> 16] = wsl;
+            s_rm[ow >> 16] = wrm;
+          }
+          wsyncT<CH>();
+        }
+#ifdef GS_RUN_TL
+        run_cyc += __builtin_amdgcn_s_memtime() - rt0;
+#endif
+        continue;
+      }
+    }
     uint32_t vrd, rqd, p, v;
     uint64_t rqq_p = 0, rqc_p = 0;  // request codes (floor / ceil) of resources 0..3, 16 bits each
     const bool from_ring = !wrapped;
@@ -1186,6 +1402,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         wsyncT<CH>();
         emit(WQ_NFA, nlog, gp, v, fn, rqd, rq_lane);
         nlog++;
+        CAT(6);
         continue;
       }
       if (fn != INF) {
@@ -1245,6 +1462,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         wsyncT<CH>();
         emit(WQ_LOG, nlog, gp, v, fn | 0x80000000u, 0, 0);
         nlog++;
+        CAT(6);
         continue;
       }
     }
@@ -1839,6 +2057,10 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       modkind = MOD_INC;
       modpos = f;
       nlog++;
+      // the next pod may repeat this one's spec (runs, above)
+      run_prev = GS_RUNS && !TOPO && !WIDE && from_ring && simple && !__ballot(ovf);
+      CAT(simple ? 1 : 3);
+      run_rec = vrd;
       continue;
     }
 
@@ -2025,7 +2247,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     }
     TLW(4);  // new NodeClaim
     if (status) break;
-    if (opened) continue;
+    if (opened) {
+      CAT(4);
+      continue;
+    }
+    CAT(5);
 
     // -------------------------------------- failed: Relax, then Queue.Push
     {
@@ -2065,6 +2291,17 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #endif
   const uint64_t ctr_gen = ctr_at(C_GEN), ctr_fast = ctr_at(C_FAST), ctr_cand = ctr_at(C_CAND), ctr_full = ctr_at(C_FULL),
                  ctr_nev = ctr_at(C_NEV), ctr_npre = ctr_at(C_NPRE), ctr_fa = ctr_at(C_FA), ctr_alg = ctr_at(C_ALG);
+#ifdef GS_CAT_TL
+  uint64_t cat_cyc_l[8], cat_n_l[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8; q++) {
+    cat_cyc_l[q] = (uint64_t)rlane((uint32_t)cat_cyc, q) | ((uint64_t)rlane((uint32_t)(cat_cyc >> 32), q) << 32);
+    cat_n_l[q] = (uint64_t)rlane((uint32_t)cat_n, q) | ((uint64_t)rlane((uint32_t)(cat_n >> 32), q) << 32);
+  }
+#endif
+  uint64_t ctr_run[6];
+#pragma unroll
+  for (uint32_t q = 0; q < 6; q++) ctr_run[q] = ctr_at(C_RPODS + q);
   if (lane == 0) {
     Ctrl c = {};
     c.status = status;
@@ -2082,6 +2319,17 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.node_prefix = ctr_npre;
     c.claim_prefix = ctr_alg;
     c.dbg[15] = ctr_fa;
+#ifdef GS_CAT_TL
+    for (uint32_t q = 0; q < 8; q++) {
+      c.dbg[q] = cat_cyc_l[q];
+      c.dbg[8 + q] = cat_n_l[q];
+    }
+#elif !defined(GS_FFD_TL)
+    for (uint32_t q = 0; q < 6; q++) c.dbg[8 + q] = ctr_run[q];
+#ifdef GS_RUN_TL
+    c.dbg[14] = run_cyc;
+#endif
+#endif
     c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
 #ifdef GS_FFD_TL
     for (int q = 0; q < 8; q++) c.dbg[q] = tl[q];
@@ -2092,7 +2340,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.dbg[9] = n_xns;
     c.dbg[10] = n_xb;
     c.dbg[11] = n_xwin;
+#ifdef GS_CAT_SEG
+    c.dbg[12] = n_cat;
+#else
     c.dbg[12] = n_nonsimple;
+#endif
     c.dbg[13] = n_rot;
     c.dbg[14] = n_rotlen;
 #endif

@@ -57,6 +57,16 @@ elif "--tl" in sys.argv:
     base["last_wave_lateness_vs_wave0"] = round(out[11] / max(res.pops, 1), 1)
     base["last_wave_hist_w0_w1_w2_w3plus"] = [out[12], out[13], out[14], out[15]]
 else:
+    # single-wave kernel: run-mode counters (pods placed in runs, entries, exits by cause)
+    base["runs"] = {n: int(out[8 + i]) for i, n in enumerate(["pods", "entries", "x_pivot", "x_window", "x_spec",
+                                                            "x_scan"])}
+    base["runs"]["memtime_ticks_in_runs"] = int(out[14])
+    if "--cat" in sys.argv:  # GS_CAT_TL build: shader cycles per pod category
+        names = ["run_mode", "simple_claim", "-", "other_claim", "new_claim", "failed", "existing_node", "unknown"]
+        base["categories"] = {n: {"pods": int(out[8 + i]), "mcycles": round(out[i] / 1e6, 2),
+                                  "cycles_per_pod": round(out[i] / max(out[8 + i], 1), 1)}
+                              for i, n in enumerate(names) if n != "-"}
+        del base["runs"]
     base.update({"sort": res.t_ffd_sort_ms, "scan": res.t_ffd_scan_ms, "tmpl": res.t_ffd_template_ms,
                  "scan_tid0_work_ms": out[0] * 1e-5, "scan_wait_ms": out[1] * 1e-5, "chunks": out[2],
                  "sort_decide_ms": out[3] * 1e-5, "pop_ms": out[4] * 1e-5, "end_to_pop_ms": out[5] * 1e-5,
