@@ -241,6 +241,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     d.ov_epoch = 0;
     c->alloc(d.ov_vol, e.any_vol ? (size_t)sims->blocks * d.ov_cap : 1);
     d.ovh_slots = gsd::ovh_slots_for(d.ov_cap);
+    d.sim_lds = sims->sim_lds ? 1u : 0u;
     c->alloc(d.ov_map, d.ovh_slots ? 1 : (size_t)sims->blocks * std::max<uint32_t>(e.NN, 1));
     {
       std::vector<uint64_t> known = sims->known;

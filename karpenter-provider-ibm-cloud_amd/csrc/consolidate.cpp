@@ -21,6 +21,9 @@
 
 #include "ctx.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace gsc {
 namespace {
 
@@ -327,7 +330,20 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
   // (each simulation's latency) -- ffd.hip FB_SIM / FB_SIM_NARROW
   sp.nt = sp.evaluated.size() >= 4 * (size_t)std::max(cus, 1) ? 128u : 256u;
   const bool general = e.TG || e.any_mv || e.any_vol;
-  const uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt, general ? 1u : 0u);
+  uint32_t per_cu = gsk_ffd_sim_blocks_per_cu(e.R, lds, sp.nt, general ? 1u : 0u);
+  // the simulations' queue arrays and add logs in LDS when that costs no
+  // resident workgroup (ffd.hip s_simq / s_simlog)
+  const uint32_t lds_q = lds + 32u * std::max<uint32_t>(sp.max_pods, 1);
+  sp.sim_lds = false;
+  if (lds_q <= gsk_ffd_dyn_lds_max() && gsk_ffd_sim_blocks_per_cu(e.R, lds_q, sp.nt, general ? 1u : 0u) >= per_cu) {
+    sp.sim_lds = true;
+  }
+  if (const char* x = std::getenv("GS_SIM_LDS"))  // A/B experiments: 0 off, 1 on whenever it fits
+    sp.sim_lds = std::atoi(x) != 0 && lds_q <= gsk_ffd_dyn_lds_max();
+  if (std::getenv("GS_SIM_DEBUG"))
+    std::fprintf(stderr, "gpusched sim plan: sims %zu max_pods %u nt %u lds %u per_cu %u lds_q per_cu %u sim_lds %d\n",
+                 sp.evaluated.size(), sp.max_pods, sp.nt, lds, per_cu,
+                 gsk_ffd_sim_blocks_per_cu(e.R, lds_q, sp.nt, general ? 1u : 0u), (int)sp.sim_lds);
   sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
   // per-block overlays of hostname counts: at most 1 GiB (fewer persistent blocks otherwise)
   const size_t ov_row = (size_t)std::max<uint32_t>(sp.ov_cap, 1) * e.TGH * sizeof(uint64_t);

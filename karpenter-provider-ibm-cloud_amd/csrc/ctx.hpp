@@ -84,6 +84,7 @@ struct SimPlan {
   std::vector<uint32_t> pod_off, pods;      // per evaluated simulation: pod ids in queue order
   std::vector<uint32_t> cand_off, cands;    // per evaluated simulation: device node positions removed
   uint32_t max_pods = 0, ov_cap = 0, blocks = 0, nt = 256;
+  bool sim_lds = false;                     // per-simulation queue arrays and add log in LDS
   std::vector<uint64_t> known;              // per evaluated simulation: zone domains known without its candidates
   uint32_t multi_max = 0;                   // MULTI: firstNConsolidationOption's max
 };

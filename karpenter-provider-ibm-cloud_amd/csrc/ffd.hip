@@ -611,6 +611,13 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   const uint32_t ovh = SIM ? d.ovh_slots : 0u, ovh_mask = ovh - 1u;
   uint32_t* const s_ovk = (uint32_t*)((char*)lds64 + ((tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u));
   uint32_t* const s_ovv = s_ovk + ovh;
+  // SIM with d.sim_lds: each simulation's queue, staleness (last epoch /
+  // length), current variant and add log in LDS after the hash (4 x u32 +
+  // 16 B per pod): none of them leaves the workgroup, so they cost no HBM
+  // writes (those partial-line stores were most of a
+  // simulation's write traffic)
+  uint32_t* const s_simq = s_ovv + ovh;
+  LogRec* const s_simlog = (LogRec*)(s_simq + 4u * MC);
   auto ovm_get = [&](uint32_t n) -> uint32_t {
     if (!ovh) return ov_map[n];
     uint32_t h = (n * 2654435761u) & ovh_mask;
@@ -666,11 +673,12 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
     const uint32_t ov_stamp = (d.ov_epoch << 20) | (sim + 1u);
     const uint32_t P = SIM ? d.sim_pod_off[sim + 1] - qoff : d.P;
     const uint32_t MCs = SIM ? P : MC;  // claim arena of this solve (one claim per pod at most)
-    uint32_t* const queue = d.queue + qoff;
-    uint32_t* const last_len = d.last_len + qoff;
-    uint32_t* const last_epoch = d.last_epoch + qoff;
-    uint32_t* const cur_var = d.cur_var + qoff;
-    LogRec* const logp = d.log + qoff;
+    const bool qlds = SIM && d.sim_lds;
+    uint32_t* const queue = qlds ? s_simq : d.queue + qoff;
+    uint32_t* const last_len = qlds ? s_simq + MC : d.last_len + qoff;
+    uint32_t* const last_epoch = qlds ? s_simq + 2u * MC : d.last_epoch + qoff;
+    uint32_t* const cur_var = qlds ? s_simq + 3u * MC : d.cur_var + qoff;
+    LogRec* const logp = qlds ? s_simlog : d.log + qoff;
     int64_t* const t_rem = d.t_rem + (SIM ? (size_t)sim * T * R : 0);
     auto gpod = [&](uint32_t local) -> uint32_t { return SIM ? d.sim_pods[qoff + local] : local; };
 
@@ -1501,7 +1509,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             s_slk[j] = sl2;
             if (s_sc[f] == 0xFFFFu) HN.status = 3;
             s_sc[f]++;
-            dd.log[cb + h.nlog] = LogRec{gp, v, j, 0};
+            logp[h.nlog] = LogRec{gp, v, j, 0};
             S.dbg[15]++;
           } else if (pos == f) {
             // NodeClaim.Add by the winning lane: options, requests, requirements
@@ -1569,7 +1577,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             }
             if (s_sc[f] == 0xFFFFu) HN.status = 3;
             s_sc[f]++;
-            dd.log[cb + h.nlog] = LogRec{gp, v, j, 0};
+            logp[h.nlog] = LogRec{gp, v, j, 0};
           }
           break;
         }
@@ -1969,7 +1977,7 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
   const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
-                       (d->n_sims ? 8u * d->ovh_slots : 0u);
+                       (d->n_sims ? 8u * d->ovh_slots + (d->sim_lds ? 32u * d->max_claims : 0u) : 0u);
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;
   // shape: 0 provisioning, 1 provisioning (general variant), 2 simulations, 3 narrow simulations,

@@ -382,6 +382,7 @@ struct DevProblem {
   uint32_t ov_epoch;            // 1..4095: the launch's stamp prefix (ov_hn zeroed when it wraps)
   uint32_t* ov_map;            // [grid][NN] a touched node's overlay entry (valid where the LDS bitmap bit is set)
   uint32_t ovh_slots;          // > 0: simulations this small keep node -> entry in an LDS hash of that many slots instead
+  uint32_t sim_lds;            // simulations keep queue / staleness / variant / add log in LDS (32 B per pod)
 };
 
 // the parent-side merge of a sharded static matrix (kernels.hip
