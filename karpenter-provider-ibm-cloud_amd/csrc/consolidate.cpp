@@ -344,6 +344,8 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     std::fprintf(stderr, "gpusched sim plan: sims %zu max_pods %u nt %u lds %u per_cu %u lds_q per_cu %u sim_lds %d\n",
                  sp.evaluated.size(), sp.max_pods, sp.nt, lds, per_cu,
                  gsk_ffd_sim_blocks_per_cu(e.R, lds_q, sp.nt, general ? 1u : 0u), (int)sp.sim_lds);
+  if (const char* x = std::getenv("GS_SIM_PER_CU"))  // experiments: fewer persistent workgroups per CU
+    per_cu = std::max<uint32_t>(1, std::min<uint32_t>(per_cu, (uint32_t)std::atoi(x)));
   sp.blocks = (uint32_t)std::min<size_t>(sp.evaluated.size(), (size_t)std::max(cus, 1) * per_cu);
   // per-block overlays of hostname counts: at most 1 GiB (fewer persistent blocks otherwise)
   const size_t ov_row = (size_t)std::max<uint32_t>(sp.ov_cap, 1) * e.TGH * sizeof(uint64_t);
