@@ -105,40 +105,10 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   if (!sims) {
     // the first pass over the queue pops pods in queue0 order with their first
     // variant: records laid out in that order let the kernel prefetch the next
-    // pod in one round trip
-    std::vector<gsd::VarRec> qv(std::max<uint32_t>(e.P, 1));
-    std::vector<int64_t> qr((size_t)std::max<uint32_t>(e.P, 1) * std::max<uint32_t>(e.R, 1), 0);
-    for (uint32_t k = 0; k < e.P; k++) {
-      const uint32_t p = e.queue0[k];
-      qv[k] = e.vars[e.var_begin[p]];
-      for (uint32_t r = 0; r < e.R; r++) qr[(size_t)k * e.R + r] = e.pod_req[(size_t)p * e.R + r];
-    }
-    // the request codes of resources 0..3 (ffd_common.hpp qcode_floor /
-    // qcode_ceil, restated on the host), packed as the kernel's SWAR operands
-    auto qc = [](int64_t v, bool up) -> uint32_t {
-      if (v <= 0) return 0;
-      const uint64_t x = (uint64_t)v;
-      const uint32_t b = 64u - (uint32_t)__builtin_clzll(x);
-      if (b <= 10) return (uint32_t)x;
-      const uint32_t s = b - 10;
-      const uint32_t c = 1024u + (s - 1) * 512u + (uint32_t)((x >> s) - 512u);
-      return c + ((up && (x & ((1ull << s) - 1))) ? 1u : 0u);
-    };
-    std::vector<uint32_t> qcs((size_t)std::max<uint32_t>(e.P, 1) * 4, 0);
-    for (uint32_t k = 0; k < e.P; k++) {
-      uint64_t fl = 0, ce = 0;
-      for (uint32_t r = 0; r < std::min<uint32_t>(e.R, 4); r++) {
-        fl |= (uint64_t)qc(qr[(size_t)k * e.R + r], false) << (16 * r);
-        ce |= (uint64_t)qc(qr[(size_t)k * e.R + r], true) << (16 * r);
-      }
-      qcs[(size_t)k * 4 + 0] = (uint32_t)fl;
-      qcs[(size_t)k * 4 + 1] = (uint32_t)(fl >> 32);
-      qcs[(size_t)k * 4 + 2] = (uint32_t)ce;
-      qcs[(size_t)k * 4 + 3] = (uint32_t)(ce >> 32);
-    }
-    c->upload(d.qvars, std::move(qv));
-    c->upload(d.qreqs, std::move(qr));
-    c->upload(d.qcodes, std::move(qcs));
+    // pod in one round trip (gathered on the device after the upload)
+    c->alloc(d.qvars, std::max<uint32_t>(e.P, 1));
+    c->alloc(d.qreqs, (size_t)std::max<uint32_t>(e.P, 1) * std::max<uint32_t>(e.R, 1));
+    c->alloc(d.qcodes, (size_t)std::max<uint32_t>(e.P, 1) * 4);
   }
   d.NN = e.NN;
   // topology spread groups
@@ -268,6 +238,10 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     pinned(c->h_nits, NS);
   }
   c->commit();
+  if (!sims) {
+    HIPCHK(gsk_queue_records(&d, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
 }
 
 uint32_t trunc_lds_bytes(uint32_t N) {

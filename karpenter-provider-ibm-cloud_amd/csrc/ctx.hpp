@@ -2,6 +2,8 @@
 // helpers shared by the Solve (capi.cpp) and consolidation (consolidate.cpp)
 // entry points.
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -32,6 +34,7 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void);
 extern "C" hipError_t gsk_ffdw(const gsd::DevProblem* d, uint32_t ch, hipStream_t s);
 extern "C" hipError_t gsk_trunc(const gsd::DevProblem* d, uint32_t lds_bytes, uint32_t n_slots, hipStream_t s);
 extern "C" hipError_t gsk_mv_rows(const gsd::DevProblem* d, hipStream_t s);
+extern "C" hipError_t gsk_queue_records(const gsd::DevProblem* d, hipStream_t s);
 extern "C" hipError_t gsk_merge_shards(const gsd::ShardMerge* m, hipStream_t s);
 
 namespace gsc {
@@ -287,6 +290,10 @@ inline void gs_ctx::commit() {
   if (n_zero) HIPCHK(hipMemsetAsync(base + n_up, 0, n_zero, stream));
   HIPCHK(hipStreamSynchronize(stream));
   t_h2d_ms = gsc::ms_since(t1);
+  static const bool prof = std::getenv("GS_ENCODE_PROFILE") != nullptr;
+  if (prof)
+    std::fprintf(stderr, "upload.stage %.3f ms  upload.h2d %.3f ms  (%zu B uploaded, %zu B zeroed, %zu B total)\n",
+                 t_stage_ms, t_h2d_ms, n_up, n_zero, total);
   plan.clear();
   keep.clear();
   plan_bytes = 0;

@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <climits>
 #include <cstdlib>
 #include <exception>
@@ -330,6 +332,15 @@ struct Ctx {
   const gs_problem* p;
   Encoded& e;
   std::vector<std::string> strs;
+  // GS_ENCODE_PROFILE: sub-phase wall clock on stderr (diagnostics)
+  bool pprof = std::getenv("GS_ENCODE_PROFILE") != nullptr;
+  std::chrono::steady_clock::time_point pt_last = std::chrono::steady_clock::now();
+  void ph(const char* name) {
+    if (!pprof) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  pods.%-18s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - pt_last).count());
+    pt_last = t;
+  }
 
   const std::string& S(uint32_t id) const {
     if (id >= strs.size()) throw Fail{GS_E_INVALID, "string id out of range"};
@@ -619,7 +630,10 @@ struct Ctx {
     e.C = (uint32_t)e.cat_ct.size();
     if (e.Z * e.C > 64) throw Fail{GS_E_UNSUPPORTED, "zones x capacity types > 64"};
     // resources
+    // (canonical string ids of the resource names: the first id carrying
+    // each text, so a resource's lowest string id is its canonical id)
     std::set<std::string> rn;
+    std::vector<uint32_t> res_cids;
     {
       std::vector<uint8_t> seen(strs.size(), 0);
       for (uint32_t i = 0; i < p->n_quantities; i++) {
@@ -627,6 +641,7 @@ struct Ctx {
         if (!seen[c]) {
           seen[c] = 1;
           rn.insert(strs[c]);
+          res_cids.push_back(c);
         }
       }
     }
@@ -635,20 +650,24 @@ struct Ctx {
     if (e.R > (uint32_t)gsd::RMAX) throw Fail{GS_E_UNSUPPORTED, "more than 8 distinct resources"};
     std::unordered_map<std::string, uint32_t> rid;
     for (uint32_t r = 0; r < e.R; r++) rid[e.res_names[r]] = r;
-    for (auto& nm : e.res_names) {
-      uint32_t sid = 0;
-      for (uint32_t i = 0; i < strs.size(); i++)
-        if (strs[i] == nm) {
-          sid = i;
-          break;
-        }
-      e.res_name_ids.push_back(sid);
+    e.res_name_ids.assign(e.R, 0);
+    std::vector<uint32_t> rid_of_cid(res_cids.size());
+    for (size_t k = 0; k < res_cids.size(); k++) {
+      const uint32_t r = rid.at(strs[res_cids[k]]);
+      e.res_name_ids[r] = res_cids[k];
+      rid_of_cid[k] = r;
     }
     rid_map = rid;
+    // string id -> resource index for every string a quantity names (the
+    // only ids resvec_fn looks up)
     rid_of_sid.assign(strs.size(), gsd::NONE);
-    for (uint32_t i = 0; i < strs.size(); i++) {
-      auto f = rid.find(strs[canon[i]]);
-      if (f != rid.end()) rid_of_sid[i] = f->second;
+    {
+      std::unordered_map<uint32_t, uint32_t> by_cid;
+      for (size_t k = 0; k < res_cids.size(); k++) by_cid[res_cids[k]] = rid_of_cid[k];
+      for (uint32_t i = 0; i < p->n_quantities; i++) {
+        const uint32_t sid = p->quantities[i].resource;
+        if (rid_of_sid[sid] == gsd::NONE) rid_of_sid[sid] = by_cid.at(C(sid));
+      }
     }
     auto resvec = [this](gs_range r, int64_t* out, bool* present) { resvec_fn(r, out, present); };
     // per IT arrays
@@ -1122,8 +1141,10 @@ struct Ctx {
         if (f != users.end()) f->second.insert(who);  // only volumes pods in the list mount matter
       }
     }
-    e.pod_vol.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
-    e.pod_vfresh.assign((size_t)std::max<uint32_t>(e.P, 1) * gsd::VDMAX, 0);
+    // without pending volumes the kernels never read these (any_vol)
+    const size_t PV = users.empty() ? 1 : std::max<uint32_t>(e.P, 1);
+    e.pod_vol.assign(PV * gsd::VDMAX, 0);
+    e.pod_vfresh.assign(PV * gsd::VDMAX, 0);
     for (uint32_t i = 0; i < e.P; i++) {
       const gs_pod& pd = p->pods[i];
       if (!pd.volumes.count) continue;
@@ -1976,6 +1997,7 @@ struct Ctx {
   }
 
   void build_pods() {
+    pt_last = std::chrono::steady_clock::now();
     e.P = p->n_pods;
     e.pod_req.assign((size_t)e.P * e.R, 0);
     // pods -> specs (first-carrier order): a 64-bit hash of each pod's spec
@@ -2046,6 +2068,7 @@ struct Ctx {
       for (uint32_t i = 0; i < e.P; i++) spec_of[i] = rank[spec_of[i]];
     }
     const uint32_t NS = (uint32_t)spec_rep.size();
+    ph("specs");
     // <U> the inverse anti-affinity groups: required terms of pending and
     // bound pods (Topology.updateInverseAntiAffinity / updateInverseAffinities)
     // a problem without spreads, affinity terms or host ports builds no
@@ -2082,6 +2105,7 @@ struct Ctx {
         chk(p->pods[i].host_ports, p->n_host_ports, "host_ports");
       }
     }
+    ph("groups");
     // the first pod whose uid an earlier pod carries (or names no string)
     uint32_t dup_at = e.P;
     bool dup_bad_id = false;
@@ -2098,6 +2122,7 @@ struct Ctx {
         uid_seen[cu] = 1;
       }
     }
+    ph("uids");
     // requests per pod, the spec's work per spec
     std::vector<std::exception_ptr> rerr(e.P);
     par_for(e.P, 1024, [&](uint32_t i) {
@@ -2135,6 +2160,7 @@ struct Ctx {
     });
     for (uint32_t s = 0; s < NS; s++)
       if (work[s].err) std::rethrow_exception(work[s].err);
+    ph("spec_work");
     // spec variants (e.variants), then the device variants: each pod's
     // spec's variants in order (e.var_sv: device variant -> spec variant)
     sv_begin.assign(NS, 0);
@@ -2167,6 +2193,7 @@ struct Ctx {
     }
     { std::vector<PodWork>().swap(work); }
     e.V = nv;
+    ph("variants");
     // device variant records; identical has-bitsets share one arena slot and
     // identical IT-key requirement sets one class
     e.vars.resize(e.V);
@@ -2270,12 +2297,17 @@ struct Ctx {
         if (ok) e.itclass_mask[c * e.W + it / 64] |= 1ull << (it % 64);
       }
     if (e.fk_entries.empty()) e.fk_entries.push_back(gsd::FKEntry{});
+    ph("var_records");
     // <U> NewQueue: cpu desc, memory desc, creationTimestamp asc, UID asc (total order)
     // sorted on packed keys: the UID's first 8 bytes (big-endian, so integer
     // order is byte order) decide most ties without touching the strings
+    // the fields as order-preserving unsigned integers (cpu and memory
+    // descending, creation time ascending; signed -> unsigned by flipping the
+    // sign bit) and the UID's first 8 bytes, in two 128-bit words: the sort
+    // compares integers; keys that tie (UIDs sharing 8 bytes) are put in full
+    // order afterwards
     struct QK {
-      int64_t cpu, mem, ts;
-      uint64_t u8;
+      unsigned __int128 k, k2;
       uint32_t i;
     };
     std::vector<QK> qk(e.P);
@@ -2283,13 +2315,15 @@ struct Ctx {
       const std::string& u = strs[p->pods[i].uid];  // checked by the uid pass
       uint64_t x = 0;
       for (size_t b = 0; b < 8; b++) x = (x << 8) | (b < u.size() ? (uint8_t)u[b] : 0u);
-      qk[i] = QK{cpu[i], mem[i], p->pods[i].creation_ns, x, i};
+      auto bias = [](int64_t v) { return (uint64_t)v ^ (1ull << 63); };
+      qk[i] = QK{((unsigned __int128)~bias(cpu[i]) << 64) | ~bias(mem[i]),
+                 ((unsigned __int128)bias(p->pods[i].creation_ns) << 64) | x, i};
     });
+    ph("queue_keys");
+    auto kless = [](const QK& a, const QK& b) { return a.k != b.k ? a.k < b.k : a.k2 < b.k2; };
     auto qless = [&](const QK& a, const QK& b) {
-      if (a.cpu != b.cpu) return a.cpu > b.cpu;
-      if (a.mem != b.mem) return a.mem > b.mem;
-      if (a.ts != b.ts) return a.ts < b.ts;
-      if (a.u8 != b.u8) return a.u8 < b.u8;
+      if (a.k != b.k) return a.k < b.k;
+      if (a.k2 != b.k2) return a.k2 < b.k2;
       return strs[p->pods[a.i].uid] < strs[p->pods[b.i].uid];
     };
     // a total order (uids are unique): chunks sorted in parallel, then merged
@@ -2298,18 +2332,55 @@ struct Ctx {
       const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>(enc_threads(), e.P / 8192));
       std::vector<uint32_t> cut(T + 1);
       for (uint32_t t = 0; t <= T; t++) cut[t] = (uint32_t)((uint64_t)e.P * t / T);
-      par_for(T, 1, [&](uint32_t t) { std::sort(qk.begin() + cut[t], qk.begin() + cut[t + 1], qless); });
+      par_for(T, 1, [&](uint32_t t) { std::sort(qk.begin() + cut[t], qk.begin() + cut[t + 1], kless); });
+      ph("queue_sort_chunks");
+      // pairwise merge rounds between two buffers; each merge is split into
+      // T output pieces by co-rank (merge path) so every round runs on all
+      // threads
       std::vector<QK> tmp(e.P);
+      std::vector<QK>* src = &qk;
+      std::vector<QK>* dst = &tmp;
       for (uint32_t w = 1; w < T; w *= 2) {
-        std::vector<uint32_t> pairs;
-        for (uint32_t t = 0; t + w < T; t += 2 * w) pairs.push_back(t);
-        par_for((uint32_t)pairs.size(), 1, [&](uint32_t k) {
-          const uint32_t t = pairs[k], a = cut[t], m = cut[t + w], b = cut[std::min(T, t + 2 * w)];
-          std::merge(qk.begin() + a, qk.begin() + m, qk.begin() + m, qk.begin() + b, tmp.begin() + a, qless);
-          std::copy(tmp.begin() + a, tmp.begin() + b, qk.begin() + a);
+        struct Piece {
+          uint32_t a, m, b, k0, k1;
+        };
+        std::vector<Piece> pieces;
+        for (uint32_t t = 0; t < T; t += 2 * w) {
+          const uint32_t a = cut[t], m = cut[std::min(T, t + w)], b = cut[std::min(T, t + 2 * w)];
+          for (uint32_t q = 0; q < T; q++)
+            pieces.push_back({a, m, b, (uint32_t)((uint64_t)(b - a) * q / T), (uint32_t)((uint64_t)(b - a) * (q + 1) / T)});
+        }
+        const std::vector<QK>& S = *src;
+        std::vector<QK>& D = *dst;
+        // co-rank: how many of the output's first k come from the left run
+        auto corank = [&](uint32_t a, uint32_t m, uint32_t b, uint32_t k) {
+          uint32_t lo = k > b - m ? k - (b - m) : 0u, hi = std::min(k, m - a);
+          while (lo < hi) {
+            const uint32_t i = (lo + hi) / 2, j = k - i;  // i from the left, j from the right
+            if (kless(S[m + j - 1], S[a + i])) hi = i;   // right[j-1] < left[i]: take fewer from the left
+            else lo = i + 1;
+          }
+          return lo;
+        };
+        par_for((uint32_t)pieces.size(), 1, [&](uint32_t x) {
+          const Piece& pc = pieces[x];
+          const uint32_t i0 = corank(pc.a, pc.m, pc.b, pc.k0), i1 = corank(pc.a, pc.m, pc.b, pc.k1);
+          std::merge(S.begin() + pc.a + i0, S.begin() + pc.a + i1, S.begin() + pc.m + (pc.k0 - i0),
+                     S.begin() + pc.m + (pc.k1 - i1), D.begin() + pc.a + pc.k0, kless);
         });
+        std::swap(src, dst);
+      }
+      if (src != &qk) qk.swap(tmp);
+      ph("queue_sort_merge");
+      // runs of equal keys (UIDs that share their first 8 bytes): full order
+      for (uint32_t a = 0; a < e.P;) {
+        uint32_t b = a + 1;
+        while (b < e.P && qk[b].k == qk[a].k && qk[b].k2 == qk[a].k2) b++;
+        if (b - a > 1) std::sort(qk.begin() + a, qk.begin() + b, qless);
+        a = b;
       }
     }
+    ph("queue_sort");
     e.queue0.resize(e.P);
     for (uint32_t k = 0; k < e.P; k++) e.queue0[k] = qk[k].i;
     e.checks = (uint64_t)e.P * e.checks_per_pod;
@@ -2427,23 +2498,59 @@ std::string canonical(const Encoded& e, const Reqs& r) {
 }
 
 Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
+  // the per-pod arrays keep their capacity across the prepares of one
+  // context: a repeated Solve of a similar batch refills mapped memory
+  // instead of faulting in fresh pages (~13 MB of variant records at CM)
+  auto vars = std::move(e.vars);
+  auto pod_req = std::move(e.pod_req);
+  auto var_begin = std::move(e.var_begin), var_count = std::move(e.var_count), var_sv = std::move(e.var_sv),
+       var_itclass = std::move(e.var_itclass), queue0 = std::move(e.queue0);
   e = Encoded();
+  for (auto* v : {&var_begin, &var_count, &var_sv, &var_itclass, &queue0}) v->clear();
+  vars.clear();
+  pod_req.clear();
+  e.vars = std::move(vars);
+  e.pod_req = std::move(pod_req);
+  e.var_begin = std::move(var_begin);
+  e.var_count = std::move(var_count);
+  e.var_sv = std::move(var_sv);
+  e.var_itclass = std::move(var_itclass);
+  e.queue0 = std::move(queue0);
   Ctx c{p, e, {}};
   c.bound_alias = bound_alias;
+  // GS_ENCODE_PROFILE: per-phase wall clock on stderr (diagnostics)
+  static const bool prof = std::getenv("GS_ENCODE_PROFILE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "encode %-12s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   try {
     c.strs.resize(p->n_strings);
     par_for(p->n_strings, 4096, [&](uint32_t i) {
       if (p->strings[i]) c.strs[i] = p->strings[i];
     });
+    phase("strings");
     c.build_canon();
+    phase("canon");
     c.build_vocab();
+    phase("vocab");
     c.build_catalog();
+    phase("catalog");
     c.build_templates();
+    phase("templates");
     c.build_free_slots();
+    phase("free_slots");
     c.build_pods();
+    phase("pods");
     c.build_nodes();
+    phase("nodes");
     c.build_topology();
+    phase("topology");
     c.build_volumes();
+    phase("volumes");
   } catch (const Fail& f) {
     return Err{f.code, f.msg};
   } catch (const std::out_of_range& ex) {

@@ -2004,3 +2004,42 @@ extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t 
   }
   return hipGetLastError();
 }
+
+// ================================================ first-pass queue records
+// The Solve's first pass pops pods in queue0 order with their first variant:
+// the records are gathered into queue order here, on the device, from the
+// arrays the upload already holds (one thread per queue position; HBM-bound,
+// ~0.2 KB per pod), instead of being built on the host and copied a second
+// time over PCIe.  qcodes: qcode_floor / qcode_ceil of resources 0..3 packed
+// 16 bits each, the wave Solve's SWAR operands.
+__global__ __launch_bounds__(256) void queue_records_kernel(DevProblem d) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= d.P) return;
+  const uint32_t p = d.queue0[k];
+  const uint4* src = (const uint4*)(d.vars + d.var_begin[p]);
+  uint4* dst = (uint4*)(const_cast<VarRec*>(d.qvars) + k);
+#pragma unroll
+  for (uint32_t q = 0; q < sizeof(VarRec) / sizeof(uint4); q++) dst[q] = src[q];
+  int64_t* qr = const_cast<int64_t*>(d.qreqs) + (size_t)k * d.R;
+  uint64_t fl = 0, ce = 0;
+  for (uint32_t r = 0; r < d.R; r++) {
+    const int64_t v = d.pod_req[(size_t)p * d.R + r];
+    qr[r] = v;
+    if (r < 4) {
+      fl |= (uint64_t)qcode_floor(v) << (16 * r);
+      ce |= (uint64_t)qcode_ceil(v) << (16 * r);
+    }
+  }
+  uint4 c;
+  c.x = (uint32_t)fl;
+  c.y = (uint32_t)(fl >> 32);
+  c.z = (uint32_t)ce;
+  c.w = (uint32_t)(ce >> 32);
+  ((uint4*)const_cast<uint32_t*>(d.qcodes))[k] = c;
+}
+
+extern "C" hipError_t gsk_queue_records(const DevProblem* d, hipStream_t s) {
+  if (!d->P) return hipSuccess;
+  hipLaunchKernelGGL(queue_records_kernel, dim3((d->P + 255) / 256), dim3(256), 0, s, *d);
+  return hipGetLastError();
+}

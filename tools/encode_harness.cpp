@@ -99,8 +99,8 @@ int main(int argc, char** argv) {
     }
     gsh::Err er;
     double best = 1e300;
+    gsh::Encoded e;  // one per dump, reused across reps (as a context reuses its encoding)
     for (int r = 0; r < reps; r++) {
-      gsh::Encoded e;
       auto t0 = std::chrono::steady_clock::now();
       er = gsh::encode(&d.p, e);
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
