@@ -152,6 +152,29 @@ void par_for(uint32_t n, uint32_t grain, F&& f) {
   j->cv.wait(g, [&] { return j->done.load() == n; });
 }
 
+// g() on a pool worker, not waited for (the calling thread runs it itself
+// when there are no workers, and under AddressSanitizer so that its leak
+// check at exit sees no work in flight)
+void run_detached(std::function<void()> g) {
+#if defined(__SANITIZE_ADDRESS__)
+  g();
+#else
+  Pool* pl = enc_threads() > 1 ? pool() : nullptr;
+  if (!pl || !pl->workers || pl->pid != getpid()) {
+    g();
+    return;
+  }
+  auto j = std::make_shared<PoolJob>();
+  j->f = [g = std::move(g)](uint32_t) { g(); };
+  j->n = 1;
+  {
+    std::lock_guard<std::mutex> l(pl->m);
+    pl->tokens.push_back(j);
+  }
+  pl->cv.notify_one();
+#endif
+}
+
 // <U> v1.WellKnownLabels + IBM keys (reference pkg/apis/v1alpha1/labels.go:37-45)
 bool is_wellknown(const std::string& k) {
   static const std::set<std::string> s = {
@@ -2498,6 +2521,15 @@ std::string canonical(const Encoded& e, const Reqs& r) {
 }
 
 Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
+  // GS_ENCODE_PROFILE: per-phase wall clock on stderr (diagnostics)
+  static const bool prof = std::getenv("GS_ENCODE_PROFILE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "encode %-12s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   // the per-pod arrays keep their capacity across the prepares of one
   // context: a repeated Solve of a similar batch refills mapped memory
   // instead of faulting in fresh pages (~13 MB of variant records at CM)
@@ -2516,47 +2548,49 @@ Err encode(const gs_problem* p, Encoded& e, uint32_t bound_alias) {
   e.var_sv = std::move(var_sv);
   e.var_itclass = std::move(var_itclass);
   e.queue0 = std::move(queue0);
-  Ctx c{p, e, {}};
-  c.bound_alias = bound_alias;
-  // GS_ENCODE_PROFILE: per-phase wall clock on stderr (diagnostics)
-  static const bool prof = std::getenv("GS_ENCODE_PROFILE") != nullptr;
-  auto t_last = std::chrono::steady_clock::now();
-  auto phase = [&](const char* name) {
-    if (!prof) return;
-    const auto t = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "encode %-12s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_last).count());
-    t_last = t;
-  };
-  try {
-    c.strs.resize(p->n_strings);
-    par_for(p->n_strings, 4096, [&](uint32_t i) {
-      if (p->strings[i]) c.strs[i] = p->strings[i];
-    });
-    phase("strings");
-    c.build_canon();
-    phase("canon");
-    c.build_vocab();
-    phase("vocab");
-    c.build_catalog();
-    phase("catalog");
-    c.build_templates();
-    phase("templates");
-    c.build_free_slots();
-    phase("free_slots");
-    c.build_pods();
-    phase("pods");
-    c.build_nodes();
-    phase("nodes");
-    c.build_topology();
-    phase("topology");
-    c.build_volumes();
-    phase("volumes");
-  } catch (const Fail& f) {
-    return Err{f.code, f.msg};
-  } catch (const std::out_of_range& ex) {
-    return Err{GS_E_INVALID, std::string("unknown vocabulary value: ") + ex.what()};
+  phase("reset");
+  Err r{};
+  // the encoder's scratch (strings, maps, per-spec tables: ~10^5 heap blocks
+  // at CM) is freed on a pool worker after encode returns, off the Solve's
+  // critical path
+  std::shared_ptr<Ctx> cp(new Ctx{p, e, {}});
+  {
+    Ctx& c = *cp;
+    c.bound_alias = bound_alias;
+    try {
+      c.strs.resize(p->n_strings);
+      par_for(p->n_strings, 4096, [&](uint32_t i) {
+        if (p->strings[i]) c.strs[i] = p->strings[i];
+      });
+      phase("strings");
+      c.build_canon();
+      phase("canon");
+      c.build_vocab();
+      phase("vocab");
+      c.build_catalog();
+      phase("catalog");
+      c.build_templates();
+      phase("templates");
+      c.build_free_slots();
+      phase("free_slots");
+      c.build_pods();
+      phase("pods");
+      c.build_nodes();
+      phase("nodes");
+      c.build_topology();
+      phase("topology");
+      c.build_volumes();
+      phase("volumes");
+    } catch (const Fail& f) {
+      r = Err{f.code, f.msg};
+    } catch (const std::out_of_range& ex) {
+      r = Err{GS_E_INVALID, std::string("unknown vocabulary value: ") + ex.what()};
+    }
   }
-  return Err{};
+  run_detached([cp]() mutable { cp.reset(); });
+  cp.reset();
+  phase("teardown");
+  return r;
 }
 
 void host_copy_parallel(void* dst_base, const HostCopy* copies, size_t n) {
