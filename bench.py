@@ -107,10 +107,17 @@ def traffic_of(traffic, leg, *kernels):
     return tot if seen else None
 
 
+# where `traffic` comes from: a committed PMC pass (tools/profile_round.sh ->
+# tools/pmc_traffic.py), not a counter read inside this run
+TRAFFIC_SOURCE = {"path": None}
+
+
 def roofline(kernel, algo_bytes, avg_ms, traffic=None, peak=HBM_PEAK_GBS, bound="hbm"):
     ach = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     out = {"kernel": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": "GB/s",
            "frac": ach / peak, "algorithmic_bytes": int(algo_bytes), "avg_ms": round(avg_ms, 4), "traffic": traffic}
+    if traffic is not None and TRAFFIC_SOURCE["path"]:
+        out["traffic_source"] = "committed PMC profile " + TRAFFIC_SOURCE["path"] + " (not measured in this run)"
     if traffic and avg_ms > 0:
         # the rate the PMC bytes imply: a frac above it by more than 1.2x is not HBM evidence
         out["pmc_rate_gbs"] = round(traffic / (avg_ms * 1e-3) / 1e9, 3)
@@ -139,7 +146,8 @@ def _r(x, nd=4):
 def _compact_roofline(rf):
     if not rf:
         return None
-    keep = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes", "avg_ms")
+    keep = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "basis",
+            "algorithmic_bytes", "avg_ms")
     return {k: _r(rf.get(k)) for k in keep if k in rf}
 
 
@@ -328,7 +336,9 @@ def solve_leg(problem, solver, steps, warmup, latency_steps, barrier=None, max_o
         # priced against HBM; beside it the unique HBM bytes (PMC-comparable)
         # and the claim visits priced against the L2 they are served from;
         # and the latency per pod §8(d) asks for
-        "roofline": roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+        "roofline": dict(roofline(names["ffd"], ab["ffd"], kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
+                         basis="SURVEY 8(d) claim-visit bytes, served from LDS/L2; HBM-unique bytes: "
+                               "roofline_views.unique_hbm_bytes"),
         "roofline_unique_bytes": roofline(names["ffd"], ffd_unique_bytes(
             res, n_types, min(8, len(np.unique(problem.quantities["resource"]))), len(out["claims"]),
             len(problem.nodes)), kms["ffd"], traffic_of(traffic or {}, leg, "ffd")),
@@ -845,6 +855,8 @@ def main():
         return float(t.item())
 
     traffic = load_traffic(args.traffic_json)
+    if traffic:
+        TRAFFIC_SOURCE["path"] = os.path.relpath(os.path.abspath(args.traffic_json), ROOT)
     only = args.only
     solo = rank == 0 and world == 1
     global _POOL
