@@ -826,6 +826,11 @@ struct Ctx {
     std::string key;
     int32_t skew = 1, mind = 0;
     bool sa = false, has_sel = false, ignore_aff = false, honor_taints = false;
+    // <U> TopologyGroup.Hash's node-filter part (oracle/solve.cpp
+    // node_filter): taint policy, the filter terms' keys (not their values)
+    // and the owner's tolerations; ftext: the terms with their values (a
+    // group's owners under AffinityPolicy Honor must agree on it)
+    std::string fid, ftext;
     std::map<std::string, std::string> ml;
     std::vector<std::tuple<std::string, uint32_t, std::set<std::string>>> ex;
     // metav1.LabelSelector (nil selects nothing)
@@ -847,9 +852,10 @@ struct Ctx {
       }
       return true;
     }
+    // (minDomains is not part of it: a group keeps its first owner's)
     std::string hash(const std::string& ns) const {
-      std::string h = key + "|" + std::to_string(skew) + "|" + std::to_string(mind) + "|" + ns + "|" +
-                      (has_sel ? "1" : "0") + (ignore_aff ? "I" : "H");
+      std::string h = key + "|" + std::to_string(skew) + "|" + ns + "|" + (has_sel ? "1" : "0") +
+                      (ignore_aff ? "I" : "H") + (honor_taints ? "H" : "I") + "|f:" + fid;
       for (auto& kv : ml) h += "|l:" + kv.first + "=" + kv.second;
       for (auto& x : ex) {
         h += "|e:" + std::get<0>(x) + ":" + std::to_string(std::get<1>(x));
@@ -1866,6 +1872,49 @@ struct Ctx {
     chk(pd.labels, p->n_labels, "labels");
     w.sps = spreads_of(pd);
     for (auto& sp : w.sps) w.honor_taints = w.honor_taints || sp.honor_taints;
+    chk(pd.tolerations, p->n_tolerations, "tolerations");
+    for (uint32_t k = 0; k < pd.tolerations.count; k++) {
+      auto& t = p->tolerations[pd.tolerations.begin + k];
+      w.tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
+    }
+    if (!w.sps.empty()) {
+      // <U> MakeTopologyNodeFilter: node selector AND each required term
+      std::vector<Reqs> fr;
+      if (w.req_terms.empty()) fr.push_back(w.ns);
+      for (auto& t : w.req_terms) {
+        Reqs r = w.ns;
+        for (auto& kv : t) reqs_add(e, r, kv.first, kv.second);
+        fr.push_back(std::move(r));
+      }
+      std::vector<std::string> terms, tl, texts;
+      for (auto& r : fr) {
+        std::vector<std::string> ks;
+        for (auto& kv : r) ks.push_back(e.keys[kv.first].name);
+        std::sort(ks.begin(), ks.end());
+        std::string k;
+        for (auto& x : ks) k += x + ",";
+        terms.push_back(std::move(k));
+      }
+      for (auto& t : w.tols) tl.push_back(t.k + "=" + t.v + ":" + t.eff + "/" + std::to_string(t.op));
+      std::sort(terms.begin(), terms.end());
+      std::sort(tl.begin(), tl.end());
+      std::string fid;
+      for (auto& t : terms) fid += t + ";";
+      fid += "#";
+      for (auto& t : tl) fid += t + ";";
+      std::string ftext;
+      bool honor_aff = false;
+      for (auto& sp : w.sps) honor_aff = honor_aff || !sp.ignore_aff;
+      if (honor_aff) {
+        for (auto& r : fr) texts.push_back(canonical(e, r));
+        std::sort(texts.begin(), texts.end());
+        for (auto& t : texts) ftext += t + "\x1e";
+      }
+      for (auto& sp : w.sps) {
+        sp.fid = fid;
+        if (!sp.ignore_aff) sp.ftext = ftext;
+      }
+    }
     // nodeAffinityPolicy Honor equals Ignore when the node selector and the
     // required terms constrain the zone key alone (oracle/solve.cpp: the
     // filter then drops only nodes / NodeClaims outside the owner's zones)
@@ -1905,11 +1954,6 @@ struct Ctx {
         w.g_port.push_back(GroupKey{"P|" + pe.key(), std::move(g)});
       }
     }
-    chk(pd.tolerations, p->n_tolerations, "tolerations");
-    for (uint32_t k = 0; k < pd.tolerations.count; k++) {
-      auto& t = p->tolerations[pd.tolerations.begin + k];
-      w.tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
-    }
   }
 
   void pod_phase_b(uint32_t i, PodWork& w) {
@@ -1920,6 +1964,12 @@ struct Ctx {
         if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
         f = group_idx.emplace(w.sp_hash[k], (uint32_t)groups.size()).first;
         groups.push_back(GroupEnc{w.sps[k], pns});
+      } else if (!w.sps[k].ignore_aff && groups[f->second].sp.ftext != w.sps[k].ftext) {
+        // upstream keys the group by the filter's keys and keeps its first
+        // owner's filter: later owners with other values would see counts
+        // filtered by someone else's node affinity
+        throw Fail{GS_E_UNSUPPORTED,
+                   "pods sharing a topology spread (nodeAffinityPolicy Honor) with different node affinity values"};
       }
       w.sgid.push_back(f->second);
     }

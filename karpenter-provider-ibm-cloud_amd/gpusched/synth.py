@@ -604,7 +604,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False, par
     return b.build()
 
 
-def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore"):
+def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore", multi_term=False):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
@@ -614,7 +614,8 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     NodePools' taint and its spreads carry that nodeTaintsPolicy (the random
     stream is the same for both, so the two problems differ only in it).
     affinity_policy: the nodeAffinityPolicy of the spreads of pods with a
-    (zone-only) required node-affinity term"""
+    (zone-only) required node-affinity term; multi_term: those spread owners
+    carry two zone In terms instead (OR; relaxation drops the first)"""
     rng = np.random.default_rng(seed)
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
@@ -672,6 +673,9 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
         if selector is not None and rng.random() < 0.25:
             sp["match_label_keys"] = ["pod-template-hash"] + (["absent-key"] if rng.random() < 0.3 else [])
         palette.append(sp)
+    side = np.random.default_rng(seed + 0x7A11)
+    avoid = str(side.choice(zones))
+    two = [str(z) for z in side.choice(zones, size=2, replace=False)]
     n = int(n_pods if n_pods is not None else rng.integers(1, 40))
     for i in range(n):
         app = str(rng.choice(APPS[:3]))
@@ -683,7 +687,15 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
             if spreads:
                 for sp in spreads:
                     sp["node_affinity_policy"] = affinity_policy
-            required.append([("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(zones))])])
+            # one avoided zone per problem (a deployment's replicas share their
+            # node affinity): a Honor group keeps its first owner's filter, so
+            # owners with different filter values are refused by the product
+            drawn = str(rng.choice(zones))
+            if spreads and multi_term:
+                required += [[("topology.kubernetes.io/zone", "In", [two[0]])],
+                             [("topology.kubernetes.io/zone", "In", [two[1]])]]
+            else:
+                required.append([("topology.kubernetes.io/zone", "NotIn", [avoid if spreads else drawn])])
         if rng.random() < 0.1 and not spreads:
             sel["topology.kubernetes.io/zone"] = str(rng.choice(zones))
         tols = [("dedicated", "Exists", "", "")] if rng.random() < 0.3 else []

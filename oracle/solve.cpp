@@ -367,7 +367,17 @@ struct Spread {
   };
   vector<Expr> exprs;
   bool ignore_affinity = false;
-  bool honor_taints = false;  // nodeTaintsPolicy Honor (checked in Builder::check_taint_policy)
+  bool honor_taints = false;  // nodeTaintsPolicy Honor
+  // <U> TopologyNodeFilter (MakeTopologyNodeFilter): the owner's node selector
+  // AND each required node-affinity term (OR over terms; the node selector
+  // alone without terms), and the owner's tolerations
+  vector<Reqs> filter;
+  vector<Toleration> filter_tols;
+  // the filter's part of TopologyGroup.Hash: hashstructure skips unexported
+  // fields, so of each term's Requirements only the keys enter the hash (not
+  // the values); Tolerations and both policies do (slices as sets: restated
+  // as sorted lists)
+  string filter_id;
   // metav1.LabelSelector over a pod's labels (nil selects nothing)
   bool matches(const std::map<string, string>& labels) const {
     if (!has_selector) return false;
@@ -385,10 +395,12 @@ struct Spread {
     }
     return true;
   }
-  // TopologyGroup identity (whenUnsatisfiable is not part of it)
+  // <U> TopologyGroup.Hash: key, type, namespaces, selector, maxSkew and the
+  // node filter; neither whenUnsatisfiable nor minDomains is part of it (a
+  // group keeps its first owner's minDomains)
   string hash(const string& ns) const {
-    string h = key + "|" + std::to_string(max_skew) + "|" + (min_domains ? std::to_string(*min_domains) : "-") + "|" +
-               ns + "|" + (has_selector ? "1" : "0") + "|" + (ignore_affinity ? "I" : "H");
+    string h = key + "|" + std::to_string(max_skew) + "|" + ns + "|" + (has_selector ? "1" : "0") + "|" +
+               (ignore_affinity ? "I" : "H") + (honor_taints ? "H" : "I") + "|f:" + filter_id;
     for (auto& kv : match_labels) h += "|l:" + kv.first + "=" + kv.second;
     for (auto& e : exprs) {
       h += "|e:" + e.key + ":" + std::to_string(e.op);
@@ -600,6 +612,25 @@ struct TGroup {
   Spread sel;
   std::map<string, int64_t> domains;  // known domains and their counts
   std::set<uint32_t> owners;          // pod indices
+  // <U> TopologyNodeFilter of a spread group (its first owner's; affinity
+  // and anti-affinity groups have none and always match)
+  bool spread = false;
+  bool honor_affinity = false, honor_taints = false;
+  vector<Reqs> filter;
+  vector<Toleration> filter_tols;
+  // <U> TopologyDomainGroup: the taints of every NodePool / node providing a
+  // domain (ForEachDomain under TaintPolicy Honor)
+  std::map<string, vector<vector<Taint>>> dom_taints;
+  // TopologyNodeFilter.Matches(taints, requirements, compatibility options)
+  bool filter_matches(const vector<Taint>& taints, const Reqs& reqs, bool allow_wellknown) const {
+    if (!spread) return true;
+    if (honor_affinity && !filter.empty()) {
+      bool any = false;
+      for (auto& f : filter) any = any || reqs.compatible(f, allow_wellknown);
+      if (!any) return false;
+    }
+    return !honor_taints || tolerates_all(taints, filter_tols);
+  }
   bool selects(const Pod& p) const {
     return (anti || aff ? nss.count(p.ns) > 0 : p.ns == ns) && sel.matches(p.labels);
   }
@@ -710,6 +741,34 @@ struct Builder {
     return out;
   }
 
+  // <U> MakeTopologyNodeFilter over the pod's node selector, required
+  // node-affinity terms and tolerations (set before pod_meta by build())
+  static void node_filter(const Pod& pd, Spread& sp) {
+    Reqs sel;
+    for (auto& kv : pd.node_selector) sel.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
+    sp.filter.clear();
+    if (pd.required.empty()) sp.filter.push_back(sel);
+    for (auto& tm : pd.required) {
+      Reqs r = sel;
+      for (auto& q : tm.reqs) r.add(q);
+      sp.filter.push_back(std::move(r));
+    }
+    sp.filter_tols = pd.tolerations;
+    vector<string> terms, tols;
+    for (auto& r : sp.filter) {
+      string k;
+      for (auto& kv : r.m) k += kv.first + ",";
+      terms.push_back(k);
+    }
+    for (auto& t : pd.tolerations) tols.push_back(t.key + "=" + t.value + ":" + t.effect + "/" + std::to_string(t.op));
+    std::sort(terms.begin(), terms.end());
+    std::sort(tols.begin(), tols.end());
+    sp.filter_id.clear();
+    for (auto& t : terms) sp.filter_id += t + ";";
+    sp.filter_id += "#";
+    for (auto& t : tols) sp.filter_id += t + ";";
+  }
+
   // namespace, labels and topology spread constraints of a pod
   void pod_meta(const gs_pod& g, Pod& pd, bool pending = true) {
     pd.ns = str(g.ns);
@@ -748,6 +807,7 @@ struct Builder {
         if (f != pd.labels.end()) sp.exprs.push_back(Spread::Expr{k, GS_OP_IN, {f->second}});
       }
       sp.ignore_affinity = q.node_affinity_policy == GS_POLICY_IGNORE;
+      node_filter(pd, sp);
       pd.spreads.push_back(std::move(sp));
     }
     auto terms = [&](gs_range rg, bool affinity) {
@@ -850,7 +910,8 @@ struct Builder {
   // scheduled; domain universe = In values of NodePool (+labels, + instance
   // type) requirements of NodePools that have instance types, plus existing
   // nodes' labels; counts = selected bound pods on existing nodes
-  void build_topology(const vector<Reqs>& np_reqs, const vector<bool>& np_has_its) {
+  void build_topology(const vector<Reqs>& np_reqs, const vector<bool>& np_has_its,
+                      const vector<vector<Taint>>& np_taints) {
     for (auto& pd : st.pods)
       for (auto& sp : pd.spreads) {
         const string h = sp.hash(pd.ns);
@@ -865,6 +926,11 @@ struct Builder {
           g.min_domains = sp.min_domains;
           g.ns = pd.ns;
           g.sel = sp;
+          g.spread = true;
+          g.honor_affinity = !sp.ignore_affinity;
+          g.honor_taints = sp.honor_taints;
+          g.filter = sp.filter;
+          g.filter_tols = sp.filter_tols;
           st.groups.push_back(std::move(g));
         } else {
           gi = f->second;
@@ -914,21 +980,31 @@ struct Builder {
         if (!np_has_its[i] || !np_reqs[i].has_key(g.key)) continue;
         const Req q = np_reqs[i].get(g.key);
         if (q.op() == GS_OP_IN)
-          for (auto& v : q.values) g.domains.emplace(v, 0);
+          for (auto& v : q.values) {
+            g.domains.emplace(v, 0);
+            g.dom_taints[v].push_back(np_taints[i]);
+          }
       }
       for (auto& n : st.nodes) {
         if (!n.reqs.has_key(g.key)) continue;
         const Req q = n.reqs.get(g.key);
         if (q.op() == GS_OP_IN)
-          for (auto& v : q.values) g.domains.emplace(v, 0);
+          for (auto& v : q.values) {
+            g.domains.emplace(v, 0);
+            g.dom_taints[v].push_back(n.taints);
+          }
       }
     }
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
       const Pod& bp = bound[b];
       const ExistingNode& n = st.nodes[p->bound_pod_node[b]];
-      // countDomains: selected bound pods on their nodes' domains
+      // countDomains: selected bound pods on their nodes' domains, where
+      // the node passes the group's filter (the Node's own taints and labels,
+      // strict Compatible)
+      const vector<Taint> node_taints = taints_of(p->nodes[p->bound_pod_node[b]].taints);
       for (auto& g : st.groups) {
         if (!g.selects(bp) || !n.reqs.has_key(g.key)) continue;
+        if (!g.filter_matches(node_taints, n.reqs, false)) continue;
         const Req q = n.reqs.get(g.key);
         if (q.op() != GS_OP_IN) continue;
         if (g.anti)
@@ -945,24 +1021,6 @@ struct Builder {
           for (auto& v : q.values) g.domains[v]++;
       }
     }
-  }
-
-  // <U> TopologyNodeFilter.Matches with TaintPolicy Honor: a node or
-  // NodeClaim counts in the group (Record, countDomains) and its domain enters
-  // the minimum (TopologyDomainGroup.ForEachDomain) only if the owner
-  // tolerates its taints.  When the owner tolerates every NodePool and node
-  // taint of the problem the filter always matches and Honor equals Ignore;
-  // otherwise refused (the product refuses the same inputs)
-  void check_taint_policy() {
-    vector<Taint> all;
-    for (uint32_t i = 0; i < p->n_nodepools; i++)
-      for (auto& t : taints_of(p->nodepools[i].taints)) all.push_back(t);
-    for (auto& n : st.nodes)
-      for (auto& t : n.taints) all.push_back(t);
-    for (auto& pd : st.pods)
-      for (auto& sp : pd.spreads)
-        if (sp.honor_taints && !tolerates_all(all, pd.tolerations))
-          throw Unsupported{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor with a taint its owner does not tolerate"};
   }
 
   void build() {
@@ -996,6 +1054,7 @@ struct Builder {
     });
     vector<Reqs> np_reqs;
     vector<bool> np_has_its;
+    vector<vector<Taint>> np_taints;
     for (uint32_t npi : order) {
       auto& np = p->nodepools[npi];
       Template t;
@@ -1023,6 +1082,7 @@ struct Builder {
       }
       np_reqs.push_back(t.reqs);
       np_has_its.push_back(!its.empty());
+      np_taints.push_back(t.taints);
       // <U> NewScheduler: pre-filter instance types per template
       t.options = filter_its(its, t.reqs, Res{});
       if (t.has_limits) st.remaining[t.name] = res_of(np.limits);
@@ -1061,21 +1121,6 @@ struct Builder {
         pd.tolerations.push_back({str(t.key), str(t.value), str(t.effect), (int)t.op});
       }
       pod_meta(g, pd);
-      // <U> TopologyNodeFilter with AffinityPolicy Honor: a node / NodeClaim
-      // counts only where its requirements are Compatible with the owner's
-      // node selector or one of its required terms.  When those constrain the
-      // zone key alone, every node or NodeClaim the filter drops lies outside
-      // the owner's own zone domains, which neither domainMinCount (zone;
-      // hostname minimum is 0) nor the owner's placements ever consult:
-      // Honor equals Ignore.  Other node affinity under Honor is refused.
-      bool zone_only = true;
-      for (auto& kv : pd.node_selector) zone_only = zone_only && normalize_key(kv.first) == kZone;
-      for (auto& tm : pd.required)
-        for (auto& q : tm.reqs) zone_only = zone_only && q.key == kZone;
-      if (!pd.spreads.empty() && !zone_only)
-        for (auto& sp : pd.spreads)
-          if (!sp.ignore_affinity)
-            throw Unsupported{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
       update_pod_reqs(pd);
     }
     // existing nodes: <U> initialized first, then by name (sort.SliceStable)
@@ -1097,7 +1142,6 @@ struct Builder {
         n.vol_limits[str(l.driver)] = l.limit;
       }
     }
-    check_taint_policy();
     st.node_order.resize(p->n_nodes);
     for (uint32_t i = 0; i < p->n_nodes; i++) st.node_order[i] = i;
     std::stable_sort(st.node_order.begin(), st.node_order.end(), [&](uint32_t a, uint32_t b) {
@@ -1106,7 +1150,7 @@ struct Builder {
       if (A.initialized != B.initialized) return A.initialized;
       return A.name < B.name;
     });
-    build_topology(np_reqs, np_has_its);
+    build_topology(np_reqs, np_has_its, np_taints);
     // resource vocabulary (for dense claim requests)
     std::set<string> rn;
     for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(str(p->quantities[i].resource));
@@ -1170,13 +1214,24 @@ struct Scheduler {
   OracleState& st;
 
   // ---------------------------------------------------------- <U> Topology
+  // <U> TopologyDomainGroup.ForEachDomain: under TaintPolicy Honor a domain
+  // takes part only if some NodePool / node providing it has taints the pod
+  // tolerates (a domain with no recorded provider is kept)
+  static bool domain_tolerated(const TGroup& g, const string& d, const Pod& pod) {
+    if (!g.honor_taints) return true;
+    auto f = g.dom_taints.find(d);
+    if (f == g.dom_taints.end() || f->second.empty()) return true;
+    for (auto& ts : f->second)
+      if (tolerates_all(ts, pod.tolerations)) return true;
+    return false;
+  }
   // TopologyGroup.domainMinCount
-  int64_t domain_min_count(const TGroup& g, const Req& pod_domains) const {
+  int64_t domain_min_count(const TGroup& g, const Req& pod_domains, const Pod& pod) const {
     if (g.key == kHostname) return 0;
     int64_t mn = INT32_MAX;
     int32_t n = 0;
     for (auto& kv : g.domains)
-      if (pod_domains.has(kv.first)) {
+      if (pod_domains.has(kv.first) && domain_tolerated(g, kv.first, pod)) {
         n++;
         mn = std::min(mn, kv.second);
       }
@@ -1219,7 +1274,7 @@ struct Scheduler {
       if (opts.empty()) return make_req(g.key, GS_OP_DOES_NOT_EXIST, {}, std::nullopt);
       return make_req(g.key, GS_OP_IN, opts, std::nullopt);
     }
-    const int64_t mn = domain_min_count(g, pod_domains);
+    const int64_t mn = domain_min_count(g, pod_domains, pod);
     const int64_t self = g.selects(pod) ? 1 : 0;
     string best;
     int64_t best_count = INT32_MAX;
@@ -1264,9 +1319,13 @@ struct Scheduler {
   }
   // Topology.Record: every group that selects the pod counts the domain it
   // landed in, when that domain is known (a single value)
-  void topo_record(const Pod& pod, const Reqs& reqs) {
+  // (TopologyGroup.Counts: the group selects the pod and its filter matches
+  // the node / NodeClaim: taints, requirements; NodeClaims with
+  // AllowUndefinedWellKnownLabels)
+  void topo_record(const Pod& pod, const Reqs& reqs, const vector<Taint>& taints, bool allow_wellknown) {
     for (auto& g : st.groups) {
       if (!g.selects(pod) || !reqs.has_key(g.key)) continue;
+      if (!g.filter_matches(taints, reqs, allow_wellknown)) continue;
       const Req d = reqs.get(g.key);
       if (d.complement) continue;
       if (g.anti) {
@@ -1381,7 +1440,7 @@ struct Scheduler {
         n.pods.push_back(&pod);
         n.ports.insert(n.ports.end(), pod.ports.begin(), pod.ports.end());
         for (auto& v : pod.volumes) n.vols[v.first].insert(v.second);
-        topo_record(pod, n.reqs);
+        topo_record(pod, n.reqs, n.taints, false);
         return true;
       }
     }
@@ -1403,7 +1462,7 @@ struct Scheduler {
         nc->requests = std::move(q);
         nc->pods.push_back(&pod);
         nc->ports.insert(nc->ports.end(), pod.ports.begin(), pod.ports.end());
-        topo_record(pod, nc->reqs);
+        topo_record(pod, nc->reqs, nc->tmpl->taints, true);
         return true;
       }
     }
@@ -1441,7 +1500,7 @@ struct Scheduler {
       nc->requests = std::move(q);
       nc->pods.push_back(&pod);
       nc->ports.insert(nc->ports.end(), pod.ports.begin(), pod.ports.end());
-      topo_record(pod, nc->reqs);
+      topo_record(pod, nc->reqs, nc->tmpl->taints, true);
       if (rem != st.remaining.end()) {
         // <U> subtractMax(remaining, nodeClaim.InstanceTypeOptions)
         Res mx;

@@ -105,19 +105,122 @@ def test_refusals():
     b = _base(n_pods=1, spread={"key": "karpenter.sh/capacity-type", "max_skew": 1, "selector": {}})
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
-    # nodeTaintsPolicy Honor with a taint the owner does not tolerate
-    b = _base(n_pods=1, spread={"key": Z, "max_skew": 1, "selector": {}, "node_taints_policy": "Honor"})
+
+
+# ---------------------------------------------- <U> TopologyNodeFilter (oracle)
+# The oracle applies the filter itself: a node / NodeClaim counts in a spread
+# group (countDomains, Record) only when its requirements are Compatible with
+# the owner's node selector AND one of its required terms (AffinityPolicy
+# Honor) and the owner tolerates its taints (TaintPolicy Honor); under taint
+# Honor a domain enters the minimum only if a NodePool / node providing it
+# has taints the pod tolerates (TopologyDomainGroup.ForEachDomain).  Where the
+# filter changes the answer the product refuses (it keeps Ignore semantics);
+# where it cannot (zone-only affinity, tolerated taints) both accept and the
+# Honor run must equal the Ignore run.
+def _tainted_node_case(pol):
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_taints_policy": pol}
+    b = _base(n_pods=0)
     b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0},
                taints=[("dedicated", "x", "NoSchedule")])
-    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
-    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
-    # nodeAffinityPolicy Honor (the default) with node affinity on a key
-    # other than zone
+    for q in range(2):
+        b.add_bound_pod(0, f"b{q}", 0, {"cpu": 1}, labels={"app": "web"})
+    for i in range(2):
+        b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    return b.build()
+
+
+def test_filter_taint_honor_drops_intolerable_node():
+    # Ignore: the tainted node's two web pods count -> the pods avoid us-south-1
+    st, res, _ = pyoracle.solve(_tainted_node_case("Ignore"))
+    assert st == abi.GS_OK and _zones(res) == [([0], "us-south-2"), ([1], "us-south-3")]
+    # Honor: the owner does not tolerate the node's taint -> its pods do not count
+    p = _tainted_node_case("Honor")
+    st, res, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK and _zones(res) == [([0], "us-south-1"), ([1], "us-south-2")]
+    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+
+
+def _family_node_case(pol):
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_affinity_policy": pol}
     b = _base(n_pods=0)
-    b.add_pod("x", 0, {"cpu": 1}, node_selector={"node.kubernetes.io/instance-type": "bx2-4x16"},
-              spreads=[{"key": Z, "max_skew": 1, "selector": {}}])
-    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
-    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+    b.add_node("n0", {Z: "us-south-1", H: "n0", "karpenter-ibm.sh/instance-family": "gx2"},
+               {"cpu": 0, "memory": 0, "pods": 0})
+    for q in range(2):
+        b.add_bound_pod(0, f"b{q}", 0, {"cpu": 1}, labels={"app": "web"})
+    for i in range(2):
+        b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  node_selector={"karpenter-ibm.sh/instance-family": "bx2"}, spreads=[sp])
+    return b.build()
+
+
+def test_filter_affinity_honor_drops_incompatible_node():
+    st, res, _ = pyoracle.solve(_family_node_case("Ignore"))
+    assert st == abi.GS_OK and _zones(res) == [([0], "us-south-2"), ([1], "us-south-3")]
+    assert lib.validate(_family_node_case("Ignore"))[0] == abi.GS_OK
+    # Honor: n0 (family gx2) is not Compatible with the owner's bx2 selector
+    p = _family_node_case("Honor")
+    st, res, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK and _zones(res) == [([0], "us-south-1"), ([1], "us-south-2")]
+    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+
+
+def _tainted_pool_case(pol):
+    # NodePool "a" offers us-south-1/2; NodePool "b" alone offers us-south-3
+    # and carries a taint the pods do not tolerate
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_taints_policy": pol}
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("a", requirements=[(Z, "In", synth.FAKE_ZONES[:2])])
+    b.add_nodepool("b", requirements=[(Z, "In", synth.FAKE_ZONES[2:])], taints=[("dedicated", "x", "NoSchedule")])
+    for i in range(4):
+        b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    return b.build()
+
+
+def test_filter_taint_honor_drops_intolerable_domain_from_minimum():
+    # Ignore: us-south-3 (count 0, unreachable) holds the minimum at 0 -> with
+    # maxSkew 1 only one pod per reachable zone schedules
+    st, res, _ = pyoracle.solve(_tainted_pool_case("Ignore"))
+    assert st == abi.GS_OK and res["errors"] == [2, 3]
+    # Honor: ForEachDomain skips us-south-3 (its only provider is intolerable)
+    p = _tainted_pool_case("Honor")
+    st, res, _ = pyoracle.solve(p)
+    assert st == abi.GS_OK and not res["errors"]
+    assert sorted(z for pods, z in _zones(res) for _ in pods) == ["us-south-1", "us-south-1", "us-south-2",
+                                                                  "us-south-2"]
+    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+
+
+def _shared_group_case(zones_per_pod, pol="Honor"):
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_affinity_policy": pol}
+    b = _base(n_pods=0)
+    for i, zs in enumerate(zones_per_pod):
+        b.add_pod(f"p{i}", i, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  required_terms=[[(Z, "In", zs)]], spreads=[sp])
+    return b.build()
+
+
+def test_filter_group_keeps_first_owners_filter():
+    """TopologyGroup.Hash covers the filter's requirement keys, not values
+    (hashstructure skips unexported fields): owners with zone In [1] and
+    zone In [2, 3] share one group whose filter is the first owner's, so the
+    us-south-2/3 pods are never counted and the later owners always see 0"""
+    zs = [["us-south-1"], ["us-south-2", "us-south-3"], ["us-south-2", "us-south-3"],
+          ["us-south-2", "us-south-3"]]
+    st, res, _ = pyoracle.solve(_shared_group_case(zs))
+    assert st == abi.GS_OK
+    honor = _zones(res)
+    st, res, _ = pyoracle.solve(_shared_group_case(zs, "Ignore"))
+    ignore = _zones(res)
+    assert ignore == [([0], "us-south-1"), ([1, 3], "us-south-2"), ([2], "us-south-3")]
+    assert honor == [([0], "us-south-1"), ([1, 2, 3], "us-south-2")]
+    assert lib.validate(_shared_group_case(zs))[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(_shared_group_case(zs, "Ignore"))[0] == abi.GS_OK
+    # the same filter on every owner: Honor == Ignore, accepted
+    same = [["us-south-2", "us-south-3"]] * 4
+    assert pyoracle.solve(_shared_group_case(same))[1] == pyoracle.solve(_shared_group_case(same, "Ignore"))[1]
+    assert lib.validate(_shared_group_case(same))[0] == abi.GS_OK
 
 
 def test_affinity_policy_honor_zone_only_equals_ignore():
@@ -139,10 +242,13 @@ def test_affinity_policy_honor_zone_only_equals_ignore():
     assert out[0] == out[1]
 
 
-@pytest.mark.parametrize("seed", range(40))
-def test_affinity_policy_honor_random_equals_ignore(seed):
-    ph = synth.random_topology(seed, affinity_policy="Honor")
-    pi = synth.random_topology(seed, affinity_policy="Ignore")
+@pytest.mark.parametrize("multi_term", [False, True])
+@pytest.mark.parametrize("seed", range(60))
+def test_affinity_policy_honor_random_equals_ignore(seed, multi_term):
+    """the oracle's real filter on random problems whose spread owners carry
+    zone-only node affinity (NotIn, or two In terms OR'd): Honor == Ignore"""
+    ph = synth.random_topology(seed, affinity_policy="Honor", multi_term=multi_term)
+    pi = synth.random_topology(seed, affinity_policy="Ignore", multi_term=multi_term)
     sh, rh, _ = pyoracle.solve(ph)
     si, ri, _ = pyoracle.solve(pi)
     assert sh == si == abi.GS_OK and rh == ri
@@ -161,7 +267,7 @@ def test_taint_policy_honor_without_taints_equals_ignore():
     assert out[0] == out[1] and len(out[0]) == 3
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(60))
 def test_taint_policy_honor_tolerated_equals_ignore(seed):
     """owners that tolerate every NodePool / node taint: Honor == Ignore,
     accepted by the encoder and the oracle alike"""
