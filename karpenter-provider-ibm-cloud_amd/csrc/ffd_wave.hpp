@@ -916,7 +916,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   // instrumentation counters, lane k = counter k (no scalar registers)
   enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG,
          // run mode (diagnostics, Ctrl.dbg[8..13] outside the timeline build)
-         C_RPODS, C_RENTER, C_RX_PIVOT, C_RX_WIN, C_RX_SPEC, C_RX_SCAN };
+         C_RPODS, C_RENTER, C_RX_PIVOT, C_RX_WIN, C_RX_SPEC, C_RX_SCAN, C_RX_XC };
   uint64_t ctr = 0;
 #ifdef GS_NO_CTR  // experiment builds: the counters' cost
 #define CTR(k, x) ((void)0)
@@ -956,6 +956,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   // the pod to the general path below.
 #ifndef GS_RUNS
 #define GS_RUNS 1
+#endif
+#ifndef GS_RUN_EXACT
+#define GS_RUN_EXACT 1
 #endif
 #ifdef GS_RUN_TL
   uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
@@ -1077,11 +1080,132 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           const uint32_t lo = modpos - base;
           const bool lp = (lane >= lo) & valid & (wtok != 0) & swar_ge(wsl, r_rqq);
           const uint64_t lpb = __ballot(lp), fab = __ballot(lp & swar_ge(wrm, r_rqc));
-          if (!lpb || !(fab & 1ull << ffs64(lpb))) {
+          if (!lpb) {
             CTR(C_RX_SCAN, 1);
             break;
           }
-          const uint32_t fl = ffs64(lpb);
+          uint32_t fl = ffs64(lpb);
+          // The exact NodeClaim.CanAdd inside the run (GS_RUN_EXACT): the
+          // window's candidates before its first fast accept that need it (a
+          // threshold cursor would move) are checked one lane each, as the
+          // general path's phase B checks the same batch; the first feasible
+          // one wins, else the fast accept; with neither in the window the pod
+          // leaves the run (the general path scans on past it)
+          bool xwin = false;
+          uint64_t x_nx[WREG] = {0, 0, 0, 0};
+          int64_t x_tot[RR], x_ma[RR];
+          uint32_t x_mrow[RR];
+          uint64_t x_zm = 0;
+#pragma unroll
+          for (uint32_t r = 0; r < RR; r++) {
+            x_tot[r] = 0;
+            x_ma[r] = 0;
+            x_mrow[r] = 0;
+          }
+          const uint64_t vzm = (uint64_t)rlane(run_rec, 14) | ((uint64_t)rlane(run_rec, 15) << 32);
+          const uint64_t vcm = (uint64_t)rlane(run_rec, 16) | ((uint64_t)rlane(run_rec, 17) << 32);
+          auto RQV = [&](uint32_t r) -> int64_t {
+            return (int64_t)((uint64_t)rlane(run_rec, 32 + 2 * r) | ((uint64_t)rlane(run_rec, 33 + 2 * r) << 32));
+          };
+          if (!(fab & 1ull << fl)) {
+            if (!GS_RUN_EXACT || rlane(run_rec, 2) != 0) {  // free-key entries: the general path
+              CTR(C_RX_SCAN, 1);
+              break;
+            }
+            const uint32_t mfl = fab ? ffs64(fab) : 64u;
+            const uint64_t ex = lpb & ~fab & (mfl == 64 ? ~0ull : ((1ull << mfl) - 1ull));
+            const auto& KD = *karg();
+            const uint32_t pvx = rlane(pf_x, VR_DW - 1);  // the next pod's variant (its K1 rows)
+            bool feas = false;
+            if ((ex >> lane) & 1) {
+              const uint32_t j = ow >> 16;
+              const uint32_t t = T > 1 ? (uint32_t)s_tmpl[j] : 0u;
+              const ClaimRec* cr = KD.c_rec + j;
+              uint32_t cur[RR];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) x_ma[r] = cr->maxa[r];
+              uint64_t x_cm;
+              {
+                const uint4* q = (const uint4*)cr;
+                const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+                const int64_t tl4[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                        (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+                const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+                x_zm = ((uint64_t)h2.w << 32) | h2.z;
+                x_cm = ((uint64_t)h3.y << 32) | h3.x;
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) {
+                  x_tot[r] = r < 4 ? tl4[r] : cr->tot_hi[r - 4];
+                  cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+                }
+              }
+              const uint64_t* row = KD.rows + ((size_t)pvx * T + t) * OW;
+              const uint64_t* opts = KD.c_opts + (size_t)j * OW;
+              {
+                const uint4* oq = (const uint4*)opts;
+                const uint4* rq4 = (const uint4*)row;
+                const uint4 o0 = oq[0], o1 = oq[1], r0 = rq4[0], r1 = rq4[1];
+                const uint64_t a[4] = {(((uint64_t)o0.y << 32) | o0.x) & (((uint64_t)r0.y << 32) | r0.x),
+                                       (((uint64_t)o0.w << 32) | o0.z) & (((uint64_t)r0.w << 32) | r0.z),
+                                       (((uint64_t)o1.y << 32) | o1.x) & (((uint64_t)r1.y << 32) | r1.x),
+                                       (((uint64_t)o1.w << 32) | o1.z) & (((uint64_t)r1.w << 32) | r1.z)};
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++) x_nx[w] = w < W ? a[w] : 0;
+              }
+              const uint64_t G = grid_of(x_zm & vzm, x_cm & vcm, KD.Z, KD.C);
+              const uint64_t Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, KD.Z, KD.C);
+              uint32_t mm[RR];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+                mm[r] = thr_window(thr + o, n, cur[r], x_tot[r] + RQV(r));
+              }
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+                if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], x_tot[r] + RQV(r));
+                x_mrow[r] = o + r + mm[r];
+              }
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                if (mm[r] != cur[r]) {
+                  const uint4* tq = (const uint4*)(KD.thr_set + (size_t)x_mrow[r] * OW);
+                  const uint4 t0 = tq[0], t1 = tq[1];
+                  x_nx[0] &= ((uint64_t)t0.y << 32) | t0.x;
+                  x_nx[1] &= ((uint64_t)t0.w << 32) | t0.z;
+                  x_nx[2] &= ((uint64_t)t1.y << 32) | t1.x;
+                  x_nx[3] &= ((uint64_t)t1.w << 32) | t1.z;
+                }
+              }
+              if (G != Gt) {
+                uint64_t off[WREG] = {};
+                for (uint64_t gm = G; gm; gm &= gm - 1) {
+                  const uint32_t g = ffs64(gm);
+#pragma unroll
+                  for (uint32_t w = 0; w < WREG; w++)
+                    if (w < W) off[w] |= slot[g * W + w];
+                }
+#pragma unroll
+                for (uint32_t w = 0; w < WREG; w++) x_nx[w] &= off[w];
+              }
+              uint64_t accw = 0;
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++) accw |= x_nx[w];
+              feas = accw != 0;
+            }
+            CTR(C_FULL, __popcll(ex));
+            CTR(C_RX_XC, 1);
+            const uint64_t fm = __ballot(feas);
+            if (fm) {
+              fl = ffs64(fm);
+              xwin = true;
+            } else if (fab) {
+              fl = mfl;
+            } else {
+              CTR(C_RX_SCAN, 1);
+              break;
+            }
+          }
           const uint32_t e = rlane(ow, fl);
           if ((e & 0xFFFFu) == 0xFFFFu) {
             status = 3;  // the u16 pod count would overflow
@@ -1098,6 +1222,54 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if ((pops & 15) == 0 && lane == 0) vst(&s_ctl[3], (uint32_t)pops);
           pf_seq = vld(&s_ring_seq[qhead % RING]);
           pf_x = lane < RING_DW ? vld(&s_ring[qhead % RING][lane]) : 0u;
+          if (xwin) {
+            // NodeClaim.Add after the exact check, by the winning lane (as
+            // the general path's): options, requests, cursors, the exact
+            // slack / room codes, requirements; the window takes the codes
+            const auto& KD = *karg();
+            const uint32_t vctb = rlane(run_rec, 3);
+            if (lane == fl) {
+              const uint32_t j = ow >> 16;
+              ClaimRec* cr = KD.c_rec + j;
+              uint64_t* opts = KD.c_opts + (size_t)j * OW;
+#pragma unroll
+              for (uint32_t w = 0; w < WREG; w++)
+                if (w < W) opts[w] = x_nx[w];
+              int64_t nt[RR];
+              uint32_t cu[RR];
+#pragma unroll
+              for (uint32_t r = 0; r < RR; r++) {
+                nt[r] = x_tot[r] + RQV(r);
+                cu[r] = x_mrow[r] - s_thoff[r] - r;
+                cr->tot(r) = nt[r];
+                cr->thr(r) = (uint16_t)cu[r];
+              }
+              wsl = pack_slack(d, x_ma, nt);
+              wrm = pack_room(thr, s_thoff, cu, nt, KD.RQ);
+              s_slk[j] = wsl;
+              s_rm[j] = wrm;
+              cr->zm = x_zm & vzm;
+              cr->cm &= vcm;
+              cr->ctb &= vctb;
+              ow = e + 1u;
+            }
+            dirty = true;
+            const uint32_t f = base + fl;
+            wsyncT<CH>();
+            emit(WQ_LOG, nlog, pp, pv, e >> 16, 0, 0);
+            nlog++;
+            CTR(C_CAND, M - modpos < 64 ? M - modpos : 64);
+            CTR(C_ALG, f + 1);
+            CTR(C_RPODS, 1);
+#ifdef GS_CAT_TL
+            cat_n += lane == 0 ? 1ull : 0ull;
+#endif
+            hint = f;
+            modkind = MOD_INC;
+            modpos = f;
+            lf = fl;
+            continue;
+          }
           // fast accept: NodeClaim.Add changes the requests only; room and
           // slack of lane fl shrink by the request (lanes r < RQ re-quantize
           // resource r, packed across lanes 0..3 as in the general path)
@@ -2299,9 +2471,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     cat_n_l[q] = (uint64_t)rlane((uint32_t)cat_n, q) | ((uint64_t)rlane((uint32_t)(cat_n >> 32), q) << 32);
   }
 #endif
-  uint64_t ctr_run[6];
+  uint64_t ctr_run[7];
 #pragma unroll
-  for (uint32_t q = 0; q < 6; q++) ctr_run[q] = ctr_at(C_RPODS + q);
+  for (uint32_t q = 0; q < 7; q++) ctr_run[q] = ctr_at(C_RPODS + q);
   if (lane == 0) {
     Ctrl c = {};
     c.status = status;
@@ -2328,6 +2500,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     for (uint32_t q = 0; q < 6; q++) c.dbg[8 + q] = ctr_run[q];
 #ifdef GS_RUN_TL
     c.dbg[14] = run_cyc;
+#else
+    c.dbg[14] = ctr_run[6];  // run-mode exact batches
 #endif
 #endif
     c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1
