@@ -960,6 +960,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifndef GS_RUN_EXACT
 #define GS_RUN_EXACT 1
 #endif
+#ifndef GS_RUN_REBASE
+#define GS_RUN_REBASE 1
+#endif
 #ifdef GS_RUN_TL
   uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
 #endif
@@ -1023,18 +1026,26 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           if (lane < RR) r_rq = (int64_t)(((uint64_t)hi << 32) | lo);
         }
         // the window: sorted positions [base, base + 64), the last Add's claim at lane 0
-        const uint32_t base = modpos;
-        const uint32_t wpos = base + lane;
-        const bool valid = wpos < M;
-        uint32_t ow = valid ? (uint32_t)s_so[wpos] : 0xFFFFu;  // past M: key 0xFFFF ends every run of equal keys
+        uint32_t base = modpos;
+        uint32_t wpos = base + lane;
+        bool valid = wpos < M;
+        uint32_t ow = 0;
         uint64_t wsl = 0, wrm = 0;
         uint32_t wtok = 0;
-        if (valid) {
-          const uint32_t je = ow >> 16;
-          wsl = s_slk[je];
-          wrm = s_rm[je];
-          wtok = (uint32_t)((r_tolt >> (T > 1 ? (uint32_t)s_tmpl[je] : 0u)) & 1u);
-        }
+        auto load_window = [&]() {
+          wpos = base + lane;
+          valid = wpos < M;
+          ow = valid ? (uint32_t)s_so[wpos] : 0xFFFFu;  // past M: key 0xFFFF ends every run of equal keys
+          wsl = wrm = 0;
+          wtok = 0;
+          if (valid) {
+            const uint32_t je = ow >> 16;
+            wsl = s_slk[je];
+            wrm = s_rm[je];
+            wtok = (uint32_t)((r_tolt >> (T > 1 ? (uint32_t)s_tmpl[je] : 0u)) & 1u);
+          }
+        };
+        load_window();
         uint32_t lf = 0;  // lane of the claim the last Add raised
         bool dirty = false;
         CTR(C_RENTER, 1);
@@ -1050,12 +1061,33 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           // sort.Slice: the raised claim moves to the end of its run of equal keys
           const uint32_t x = rlane(ow, lf) & 0xFFFFu;
           const uint64_t b = __ballot(lane > lf && (ow & 0xFFFFu) >= x);
-          if (!b) {  // the run leaves the window: the general sort (modkind stays INC)
+          const uint32_t eo = b ? ffs64(b) : 64u;
+          if (!b) {
+            // the raised claim's run of equal keys leaves the window
+            // (GS_RUN_REBASE): the window goes back to LDS, the general
+            // path's one rotation moves the claim past the run there, and
+            // the window is re-read at the infeasible-prefix bound (modpos:
+            // the claims after it moved one position left)
             CTR(C_RX_WIN, 1);
-            break;
-          }
-          const uint32_t eo = ffs64(b);
-          if (eo > lf + 1) {
+            if (!GS_RUN_REBASE) break;
+            wsyncT<CH>();
+            if (dirty && valid) {
+              s_so[wpos] = ow;
+              s_slk[ow >> 16] = wsl;
+              s_rm[ow >> 16] = wrm;
+            }
+            wsyncT<CH>();
+            dirty = false;
+            const uint32_t e2 = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
+            if (e2 > modpos + 1) {
+              CTR(C_FAST, 1);
+              ws.rotate((int)modpos, (int)e2 - 1, true);
+              if (modpos < hint && e2 - 1 >= hint) hint--;
+            }
+            base = modpos;
+            load_window();
+            lf = 0;
+          } else if (eo > lf + 1) {
             CTR(C_FAST, 1);
             auto rot = [&](uint32_t y) -> uint32_t {
               const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0x130, 0xF, 0xF, false);  // lane i <- i + 1

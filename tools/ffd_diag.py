@@ -60,7 +60,8 @@ else:
     # single-wave kernel: run-mode counters (pods placed in runs, entries, exits by cause)
     base["runs"] = {n: int(out[8 + i]) for i, n in enumerate(["pods", "entries", "x_pivot", "x_window", "x_spec",
                                                             "x_scan"])}
-    base["runs"]["memtime_ticks_in_runs"] = int(out[14])
+    # dbg[14]: s_memtime ticks in run mode (GS_RUN_TL builds), else run-mode exact batches
+    base["runs"]["exact_batches_or_run_ticks"] = int(out[14])
     if "--cat" in sys.argv:  # GS_CAT_TL build: shader cycles per pod category
         names = ["run_mode", "simple_claim", "-", "other_claim", "new_claim", "failed", "existing_node", "unknown"]
         base["categories"] = {n: {"pods": int(out[8 + i]), "mcycles": round(out[i] / 1e6, 2),
