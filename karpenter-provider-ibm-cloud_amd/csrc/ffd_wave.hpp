@@ -1054,21 +1054,20 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         const uint64_t rt0 = __builtin_amdgcn_s_memtime();
 #endif
         for (;;) {
-          if (pivot_touched(MOD_INC, modpos, M)) {
-            CTR(C_RX_PIVOT, 1);
-            break;
-          }
           // sort.Slice: the raised claim moves to the end of its run of equal keys
           const uint32_t x = rlane(ow, lf) & 0xFFFFu;
-          const uint64_t b = __ballot(lane > lf && (ow & 0xFFFFu) >= x);
+          const bool ptouch = pivot_touched(MOD_INC, modpos, M);
+          const uint64_t b = ptouch ? 0ull : __ballot(lane > lf && (ow & 0xFFFFu) >= x);
           const uint32_t eo = b ? ffs64(b) : 64u;
           if (!b) {
-            // the raised claim's run of equal keys leaves the window
-            // (GS_RUN_REBASE): the window goes back to LDS, the general
-            // path's one rotation moves the claim past the run there, and
+            // a pivot sample touched, or the raised claim's run of equal keys
+            // leaves the window (GS_RUN_REBASE): the window goes back to LDS,
+            // the general path's sort step runs there (one rotation past the
+            // run; with a touched sample only when choosePivot still reports
+            // "increasing", else the pod leaves for the general sort), and
             // the window is re-read at the infeasible-prefix bound (modpos:
             // the claims after it moved one position left)
-            CTR(C_RX_WIN, 1);
+            CTR(ptouch ? C_RX_PIVOT : C_RX_WIN, 1);
             if (!GS_RUN_REBASE) break;
             wsyncT<CH>();
             if (dirty && valid) {
@@ -1080,6 +1079,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             dirty = false;
             const uint32_t e2 = wave_first(modpos + 1, M, lane, [&](uint32_t k) { return acc.key(k) >= x; });
             if (e2 > modpos + 1) {
+              if (ptouch && pivot_hint_wave(acc, (int)M, lane) != 1) break;  // Go's full pdqsort: the general path
               CTR(C_FAST, 1);
               ws.rotate((int)modpos, (int)e2 - 1, true);
               if (modpos < hint && e2 - 1 >= hint) hint--;

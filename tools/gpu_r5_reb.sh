@@ -17,3 +17,6 @@ for w in "" --c2 --c3 --e2e --c5; do
   done
 done
 done
+# shader cycles per pod category on CM (GS_CAT_TL build)
+GPUSCHED_LIB=libgpusched_cat.so timeout -k 10 150 python3 tools/ffd_diag.py --cat > $O/diag_cat.json 2>&1 || exit 1
+head -c 1500 $O/diag_cat.json
