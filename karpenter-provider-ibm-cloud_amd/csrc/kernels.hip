@@ -77,7 +77,7 @@ template <uint32_t LP>
 __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t static_mode, uint32_t w_lo,
                                                      uint32_t w_hi) {
   constexpr uint32_t PP = 64 / LP;
-  __shared__ uint64_t s_row[BLOCK / 64][128];  // the wave's rows (PP x LP words, or 128 when LP = 64)
+  __shared__ uint64_t s_row[BLOCK / 64][256];  // the wave's rows (PP x W words, or the first 256 when LP = 64)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t sub = lane / LP, wl = lane % LP;
   const uint32_t VT = d.V * d.T;
@@ -137,8 +137,9 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
     }
     if (valid && w < W) {
       rowout[w] = x;
-      if (LP < 64) s_row[wv][lane] = x;
-      else if (w < 128) s_row[wv][w] = x;
+      // the pair's row words in LDS for the cheapest-offering scan (PP x W <= 256)
+      if (LP < 64) s_row[wv][sub * W + w] = x;
+      else if (w < 256) s_row[wv][w] = x;
       // offerings: sum over grid pairs of row AND slot_set[g]
       // (the Solve's rows need neither the offering count nor the cheapest type)
       if (static_mode && G)
@@ -158,10 +159,13 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
     // instance types with an available offering in G, sorted by (min price
     // rank over G, name rank); the first one in the row is the cheapest.
     // Every lane group scans its own pair's list, KS x LP keys per step.
-    constexpr uint32_t KS = LP >= 16 ? 2 : (64 / LP > 8 ? 8 : 64 / LP);
+#ifndef GS_K1_KS
+#define GS_K1_KS 2
+#endif
+    constexpr uint32_t KS = LP >= 16 ? GS_K1_KS : (64 / LP > 8 ? 8 : 64 / LP);
     const uint64_t gmask = (LP == 64 ? ~0ull : ((1ull << LP) - 1)) << (sub * LP);
     const uint32_t kb = d.grid_off[gi], ke = d.grid_off[gi + 1];
-    const uint64_t* srow = s_row[wv] + (LP < 64 ? sub * LP : 0);
+    const uint64_t* srow = s_row[wv] + (LP < 64 ? sub * W : 0);
     bool active = valid && ((nonempty & gmask) != 0);
     for (uint32_t base = kb; __ballot(active); base += KS * LP) {
       uint32_t it[KS];
@@ -361,8 +365,16 @@ extern "C" hipError_t gsk_feas(const DevProblem* d, uint32_t static_mode, uint32
   if (!d->V || !d->T) return hipSuccess;
   const uint64_t nc = (uint64_t)d->V * d->T * d->R;
   if (nc) hipLaunchKernelGGL(feas_cursor_kernel, dim3((uint32_t)((nc + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, *d);
-  // lanes per pair: the row's word count rounded up to a power of two
-  const uint32_t W = d->W;
+  // lanes per pair: the row's word count rounded up to a power of two, at
+  // most GS_K1_LPMAX (a lane then takes W / LP words; PP x W <= 256 keeps the
+  // pairs' rows in the wave's LDS slice).  The kernel is a chain of dependent
+  // loads per wave: more pairs per wave is fewer chains.  C5 (W = 32), same
+  // session: LP 32 0.1268 ms, 16 0.1200, 8 0.1354 (profiles/r5/k1_lanes_ab.txt)
+#ifndef GS_K1_LPMAX
+#define GS_K1_LPMAX 16
+#endif
+  uint32_t W = d->W;
+  if (GS_K1_LPMAX < 64 && W > GS_K1_LPMAX && W <= 32 && W * (64 / GS_K1_LPMAX) <= 256) W = GS_K1_LPMAX;
   if (W <= 1) launch_feas_lp<1>(d, static_mode, w_lo, w_hi, s);
   else if (W <= 2) launch_feas_lp<2>(d, static_mode, w_lo, w_hi, s);
   else if (W <= 4) launch_feas_lp<4>(d, static_mode, w_lo, w_hi, s);
