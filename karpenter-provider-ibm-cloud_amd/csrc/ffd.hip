@@ -574,7 +574,10 @@ struct Blk {
 #ifndef GS_SIM_NARROW_WPE  // experiment builds: the narrow shape's waves per SIMD
 #define GS_SIM_NARROW_WPE 3
 #endif
-constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? GS_SIM_NARROW_WPE : 4; }
+#ifndef GS_SIM_WIDE_WPE  // experiment builds: the wide shape's waves per SIMD
+#define GS_SIM_WIDE_WPE 4
+#endif
+constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? GS_SIM_NARROW_WPE : GS_SIM_WIDE_WPE; }
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
 constexpr uint32_t OV_FK = 0x40000000u;    // the entry holds its own free-key state (copied on the first Add that needs it)
 
