@@ -569,13 +569,15 @@ struct Blk {
 // Waves per SIMD the SIM shapes are compiled for.  At 4 the register budget
 // is 128 and the simulation loop spills (scratch traffic was 2/3 of the
 // kernel's HBM bytes on C4); at 3 (168 registers) the narrow shape is
-// spill-free.  The wide shape keeps 4: its few long simulations gain more
-// from residency than they lose to the spills.
+// spill-free.  The wide shape (few long simulations: MultiNode prefixes)
+// runs at 2 (256 registers, no VGPR spills): round 5, same session, c4_multi
+// 9.73 -> 8.03 ms at 2 (8.11 at 3, 4 before), c4_e2e_multi 2.06 -> 2.01
+// (profiles/r5/sim_wide_wpe_ab.txt).
 #ifndef GS_SIM_NARROW_WPE  // experiment builds: the narrow shape's waves per SIMD
 #define GS_SIM_NARROW_WPE 3
 #endif
 #ifndef GS_SIM_WIDE_WPE  // experiment builds: the wide shape's waves per SIMD
-#define GS_SIM_WIDE_WPE 4
+#define GS_SIM_WIDE_WPE 2
 #endif
 constexpr int sim_waves_per_eu(uint32_t nt) { return nt <= (uint32_t)FB_SIM_NARROW ? GS_SIM_NARROW_WPE : GS_SIM_WIDE_WPE; }
 constexpr uint32_t OV_EXCL = 0x80000000u;  // overlay entry of a removed (candidate) node
