@@ -303,27 +303,45 @@ void build_grid_orders(gs_ctx* c) {
     keys.push_back(0);
     its.push_back(0);
   }
+  // rank blocks: grid g's list positions [64k, 64k + 64) as an instance-type
+  // bitset, so the cheapest-offering search tests 64 list entries per AND
+  // instead of walking the list (at most 64 MiB; the list walk otherwise)
+  uint32_t NB = 0;
+  for (size_t g = 0; g + 1 < off.size(); g++) NB = std::max<uint32_t>(NB, (off[g + 1] - off[g] + 63) / 64);
+  std::vector<uint64_t> blocks;
+  if (!list.empty() && NB && list.size() * NB * (size_t)e.W * 8 <= ((size_t)64 << 20)) {
+    blocks.assign(list.size() * NB * (size_t)e.W, 0);
+    for (size_t g = 0; g + 1 < off.size(); g++)
+      for (uint32_t q = off[g]; q < off[g + 1]; q++) {
+        const uint32_t k = (q - off[g]) / 64, it = its[q];
+        blocks[((size_t)g * NB + k) * e.W + it / 64] |= 1ull << (it % 64);
+      }
+  }
   const size_t bl = list.size() * 8, bo = off.size() * 4, bk = keys.size() * 8, bi = its.size() * 4,
-               bp = planes.size() * 8;
+               bp = planes.size() * 8, bb = blocks.size() * 8;
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   char* p = nullptr;
-  HIPCHK(hipMalloc((void**)&p, up(bl) + up(bo) + up(bk) + up(bi) + up(bp)));
+  HIPCHK(hipMalloc((void**)&p, up(bl) + up(bo) + up(bk) + up(bi) + up(bp) + up(bb)));
   c->allocs.push_back(p);
   char* po = p + up(bl);
   char* pk = po + up(bo);
   char* pi = pk + up(bk);
   char* pp = pi + up(bi);
+  char* pb = pp + up(bp);
   HIPCHK(hipMemcpyAsync(p, list.data(), bl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(po, off.data(), bo, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(pk, keys.data(), bk, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(pi, its.data(), bi, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(pp, planes.data(), bp, hipMemcpyHostToDevice, c->stream));
+  if (bb) HIPCHK(hipMemcpyAsync(pb, blocks.data(), bb, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   d.grid_list = (const uint64_t*)p;
   d.grid_off = (const uint32_t*)po;
   d.grid_keys = (const uint64_t*)pk;
   d.grid_its = (const uint32_t*)pi;
   d.grid_planes = (const uint64_t*)pp;
+  d.grid_blocks = bb ? (const uint64_t*)pb : nullptr;
+  d.grid_nb = bb ? NB : 0u;
   d.n_grids = (uint32_t)list.size();
   d.n_planes = NPL;
 }

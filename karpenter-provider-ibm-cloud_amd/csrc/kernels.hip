@@ -120,6 +120,7 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
 
   uint32_t nf = 0;
   uint64_t any = 0;
+  uint64_t xr[2] = {0, 0};  // this lane's row words wl and wl + LP (W <= 2 LP)
   for (uint32_t w0 = 0; w0 < W; w0 += LP) {
     const uint32_t w = w0 + wl;
     uint64_t x = 0;
@@ -145,6 +146,8 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
       if (static_mode && G)
         for (uint32_t b = 0; b < d.n_planes; b++) nf += (uint32_t)__popcll(x & planes[(size_t)b * W + w]) << b;
     }
+    if (w0 == 0) xr[0] = x;
+    else if (w0 == LP) xr[1] = x;
     any |= x;
   }
   // group reductions (LP lanes, xor partners stay inside the group)
@@ -167,6 +170,60 @@ __global__ __launch_bounds__(BLOCK) void feas_kernel(DevProblem d, uint32_t stat
     const uint32_t kb = d.grid_off[gi], ke = d.grid_off[gi + 1];
     const uint64_t* srow = s_row[wv] + (LP < 64 ? sub * W : 0);
     bool active = valid && ((nonempty & gmask) != 0);
+#ifndef GS_K1_BLOCKS
+#define GS_K1_BLOCKS 1
+#endif
+    if (GS_K1_BLOCKS && d.grid_blocks) {
+      // rank blocks: the first block of the grid's list the row intersects
+      // (8 blocks per step, every block one AND per row word), then the first
+      // list entry of that block in the row
+      const uint32_t NB = d.grid_nb;
+      const uint64_t* Bg = d.grid_blocks + (size_t)gi * NB * W;
+      const uint32_t nbg = (ke - kb + 63) / 64;
+      uint32_t fk = NONE;
+      for (uint32_t k0 = 0; __ballot(active); k0 += 8) {
+        uint32_t hm = 0;
+        if (active) {
+#pragma unroll
+          for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t k = k0 + q;
+            if (k < nbg) {
+              const uint64_t* bk = Bg + (size_t)k * W;
+              bool h = wl < W && (xr[0] & bk[wl]) != 0;
+              if (wl + LP < W) h = h || (xr[1] & bk[wl + LP]) != 0;
+              hm |= h ? 1u << q : 0u;
+            }
+          }
+        }
+#pragma unroll
+        for (uint32_t m = LP / 2; m >= 1; m >>= 1) hm |= (uint32_t)__shfl_xor((int)hm, (int)m);
+        if (active && hm) {
+          fk = k0 + (uint32_t)__ffs((int)hm) - 1;
+          active = false;
+        }
+        if (k0 + 8 >= nbg) active = false;
+      }
+      const uint32_t p0 = kb + 64 * (fk != NONE ? fk : 0u);
+      uint32_t best = NONE;
+#pragma unroll
+      for (uint32_t e = 0; e < 64; e += LP) {
+        const uint32_t j = p0 + e + wl;
+        if (fk != NONE && e + wl < 64 && j < ke) {
+          const uint32_t it = d.grid_its[j];
+          if (((srow[it >> 6] >> (it & 63)) & 1) && e + wl < best) best = e + wl;
+        }
+      }
+#pragma unroll
+      for (uint32_t m = LP / 2; m >= 1; m >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)best, (int)m);
+        best = y < best ? y : best;
+      }
+      if (fk != NONE && best != NONE) {
+        cheapest = d.grid_its[p0 + best];
+        ckey = d.grid_keys[p0 + best];
+      }
+      active = false;
+    }
     for (uint32_t base = kb; __ballot(active); base += KS * LP) {
       uint32_t it[KS];
       bool hit[KS];

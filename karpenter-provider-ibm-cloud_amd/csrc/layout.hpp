@@ -259,7 +259,11 @@ struct DevProblem {
   const uint64_t* grid_keys;
   const uint32_t* grid_its;
   const uint64_t* grid_planes;
-  uint32_t n_grids, n_planes;
+  // grid_blocks[g][k][W] (may be null): the instance types at list positions
+  // [64k, 64k + 64) of grid g's OrderByPrice list, as a bitset; the cheapest
+  // type in a row is in the first block the row intersects
+  const uint64_t* grid_blocks;
+  uint32_t n_grids, n_planes, grid_nb;
   const int64_t* thr_val;      // thresholds: sorted distinct alloc per resource
   const uint32_t* thr_off;     // [R+1] offsets into thr_val
   const uint64_t* thr_set;     // [(n_r+1) per r][OW], offsets thr_off[r]+r
