@@ -963,6 +963,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifndef GS_RUN_REBASE
 #define GS_RUN_REBASE 1
 #endif
+#ifndef GS_RUN_NODES
+#define GS_RUN_NODES 1
+#endif
 #ifdef GS_RUN_TL
   uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
 #endif
@@ -1009,7 +1012,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     // (the narrow non-topology instantiation only: the topology and wide-row
     // instantiations measured slower with the run code in them, C3 398 -> 420,
     // e2e 273 -> 283, C5 1,245 -> 1,292 ms, profiles/r5/runs_ab.txt)
-    if (GS_RUNS && !TOPO && !WIDE && run_prev && !wrapped && modkind == MOD_INC && M >= 50 && d.NN == 0) {
+    // (existing nodes: only once the run's spec is known to fit none of them --
+    // its last general pod, a plain pod, set the node hint past the last node;
+    // nodes only fill up and no run pod is placed on one)
+    if (GS_RUNS && !TOPO && !WIDE && run_prev && !wrapped && modkind == MOD_INC && M >= 50 &&
+        (d.NN == 0 || (GS_RUN_NODES && nhint_ok && nhint >= d.NN))) {
       run_prev = false;
       auto same_spec = [&](uint32_t x) {
         return __ballot(lane >= 1 && lane < RING_DW && lane != VR_DW - 1 && x != run_rec) == 0;
@@ -1292,6 +1299,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             nlog++;
             CTR(C_CAND, M - modpos < 64 ? M - modpos : 64);
             CTR(C_ALG, f + 1);
+            CTR(C_NPRE, d.NN);  // every existing node was tried first
             CTR(C_RPODS, 1);
 #ifdef GS_CAT_TL
             cat_n += lane == 0 ? 1ull : 0ull;
@@ -1332,6 +1340,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           CTR(C_CAND, M - modpos < 64 ? M - modpos : 64);
           CTR(C_FA, 1);
           CTR(C_ALG, f + 1);
+          CTR(C_NPRE, d.NN);  // every existing node was tried first
           CTR(C_RPODS, 1);
 #ifdef GS_CAT_TL
           cat_n += lane == 0 ? 1ull : 0ull;

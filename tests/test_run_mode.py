@@ -8,8 +8,9 @@ touched choosePivot sample sorted in place.  Run mode needs >= 50 in-flight
 NodeClaims, so the random suites (small problems) never reach it; these
 problems do: CM- and C2-distributed batches of 2,500-8,000 pods (queue order
 interleaves pods with node selectors and GPU requests among each spec's
-simple pods), compared bit for bit with the oracle, with the kernel's own
-counters showing each run-mode path was taken.
+simple pods) and CM pods onto 150 state nodes, compared bit for bit with the
+oracle (the first-fit CanAdd counters too), with the kernel's own counters
+showing each run-mode path was taken.
 """
 import ctypes as C
 
@@ -19,12 +20,17 @@ from gpusched import abi, synth
 from oracle import pyoracle
 
 CASES = [("cm", 2500 + 700 * k, 0x5EED0100 + k) for k in range(8)] + \
-        [("c2", 3000 + 900 * k, 0x5EED0200 + k) for k in range(6)]
+        [("c2", 3000 + 900 * k, 0x5EED0200 + k) for k in range(6)] + \
+        [("c4", 4000 + 1000 * k, 0x5EED0300 + k) for k in range(4)]
 
 
 def _problem(kind, n, seed):
     if kind == "cm":
         return synth.make_cm(n_pods=n, seed=seed)
+    if kind == "c4":
+        # CM-distributed pods onto 150 state nodes first (runs start once
+        # the nodes are full for a spec: the node hint covers every node)
+        return synth.make_c4(n_nodes=150, n_pending=n, seed=seed)
     return synth.make_c2(n_pods=n, seed=seed)
 
 
@@ -55,13 +61,15 @@ def test_gpu_run_mode_parity(wave, k):
     from test_gpu_parity import _diff
     kind, n, seed = CASES[k]
     p = _problem(kind, n, seed)
-    st, want, _ = pyoracle.solve(p)
+    st, want, raw = pyoracle.solve(p)
     assert st == abi.GS_OK
     wave.prepare(p)
     wave.run()
     got, res = wave.fetch()
     d = _diff(got, want)
     assert d is None, d
+    # the first-fit NodeClaim.CanAdd / ExistingNode.CanAdd call counts
+    assert (int(res.claim_prefix), int(res.node_prefix)) == (int(raw.claim_prefix), int(raw.node_prefix))
     ctr = _run_counters(wave)
     _SEEN.append(ctr)
     if len(want["claims"]) >= 60:
@@ -75,3 +83,4 @@ def test_gpu_run_mode_paths_taken():
         pytest.skip("needs the parity cases of this module first")
     tot = {key: sum(c[key] for c in _SEEN) for key in _SEEN[0]}
     assert tot["pods"] > 1000 and tot["exact"] > 0 and tot["window"] > 0, tot
+    assert sum(c["pods"] for c in _SEEN[-4:]) > 0  # with existing nodes too
