@@ -84,3 +84,23 @@ def test_gpu_run_mode_paths_taken():
     tot = {key: sum(c[key] for c in _SEEN) for key in _SEEN[0]}
     assert tot["pods"] > 1000 and tot["exact"] > 0 and tot["window"] > 0, tot
     assert sum(c["pods"] for c in _SEEN[-4:]) > 0  # with existing nodes too
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nodes,pods", [(1000, 20000), (2500, 30000)])
+def test_gpu_run_mode_state_nodes_midsize(wave, nodes, pods):
+    """CM-distributed pods onto 1,000 / 2,500 C4-style state nodes: the nodes
+    fill first, then the runs take over behind the node hint (the bench's
+    CM_C4 shape at a size the oracle finishes in seconds)"""
+    from test_gpu_parity import _diff
+    p = synth.make_c4(n_nodes=nodes, n_pending=pods, seed=0x5EED0400 + nodes)
+    st, want, raw = pyoracle.solve(p)
+    assert st == abi.GS_OK
+    wave.prepare(p)
+    wave.run()
+    got, res = wave.fetch()
+    d = _diff(got, want)
+    assert d is None, d
+    assert (int(res.claim_prefix), int(res.node_prefix)) == (int(raw.claim_prefix), int(raw.node_prefix))
+    assert _run_counters(wave)["pods"] > 0
+
