@@ -966,6 +966,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifndef GS_RUN_NODES
 #define GS_RUN_NODES 1
 #endif
+#ifndef GS_RUN_WIDE  // the wide-row instantiation in run mode (fast accepts only)
+#define GS_RUN_WIDE 0
+#endif
 #ifdef GS_RUN_TL
   uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
 #endif
@@ -1015,7 +1018,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     // (existing nodes: only once the run's spec is known to fit none of them --
     // its last general pod, a plain pod, set the node hint past the last node;
     // nodes only fill up and no run pod is placed on one)
-    if (GS_RUNS && !TOPO && !WIDE && run_prev && !wrapped && modkind == MOD_INC && M >= 50 &&
+    if (GS_RUNS && !TOPO && (!WIDE || GS_RUN_WIDE) && run_prev && !wrapped && modkind == MOD_INC && M >= 50 &&
         (d.NN == 0 || (GS_RUN_NODES && nhint_ok && nhint >= d.NN))) {
       run_prev = false;
       auto same_spec = [&](uint32_t x) {
@@ -1147,7 +1150,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             return (int64_t)((uint64_t)rlane(run_rec, 32 + 2 * r) | ((uint64_t)rlane(run_rec, 33 + 2 * r) << 32));
           };
           if (!(fab & 1ull << fl)) {
-            if (!GS_RUN_EXACT || rlane(run_rec, 2) != 0) {  // free-key entries: the general path
+            if (!GS_RUN_EXACT || WIDE || rlane(run_rec, 2) != 0) {  // free-key entries, wide rows: the general path
               CTR(C_RX_SCAN, 1);
               break;
             }
@@ -2271,7 +2274,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       modpos = f;
       nlog++;
       // the next pod may repeat this one's spec (runs, above)
-      run_prev = GS_RUNS && !TOPO && !WIDE && from_ring && simple && !__ballot(ovf);
+      run_prev = GS_RUNS && !TOPO && (!WIDE || GS_RUN_WIDE) && from_ring && simple && !__ballot(ovf);
       CAT(simple ? 1 : 3);
       run_rec = vrd;
       continue;
