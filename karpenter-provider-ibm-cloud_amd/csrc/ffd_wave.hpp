@@ -966,8 +966,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifndef GS_RUN_NODES
 #define GS_RUN_NODES 1
 #endif
-#ifndef GS_RUN_WIDE  // the wide-row instantiation in run mode (fast accepts only)
+#ifndef GS_RUN_WIDE  // the wide-row instantiation in run mode
 #define GS_RUN_WIDE 0
+#endif
+#ifndef GS_RUN_WIDE_EXACT  // ... with the window's exact checks, one candidate at a time over all lanes
+#define GS_RUN_WIDE_EXACT 1
 #endif
 #ifdef GS_RUN_TL
   uint64_t run_cyc = 0;  // s_memtime ticks inside run mode
@@ -1135,6 +1138,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           // leaves the run (the general path scans on past it)
           bool xwin = false;
           uint64_t x_nx[WREG] = {0, 0, 0, 0};
+          uint64_t x_w[2] = {0, 0};  // wide rows: this lane's option words (lane, lane + 64) after the Add
           int64_t x_tot[RR], x_ma[RR];
           uint32_t x_mrow[RR];
           uint64_t x_zm = 0;
@@ -1150,7 +1154,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             return (int64_t)((uint64_t)rlane(run_rec, 32 + 2 * r) | ((uint64_t)rlane(run_rec, 33 + 2 * r) << 32));
           };
           if (!(fab & 1ull << fl)) {
-            if (!GS_RUN_EXACT || WIDE || rlane(run_rec, 2) != 0) {  // free-key entries, wide rows: the general path
+            if (!GS_RUN_EXACT || (WIDE && !GS_RUN_WIDE_EXACT) || rlane(run_rec, 2) != 0) {  // free-key entries: the general path
               CTR(C_RX_SCAN, 1);
               break;
             }
@@ -1159,7 +1163,71 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             const auto& KD = *karg();
             const uint32_t pvx = rlane(pf_x, VR_DW - 1);  // the next pod's variant (its K1 rows)
             bool feas = false;
-            if ((ex >> lane) & 1) {
+            uint64_t fm = 0;
+            if (WIDE) {
+              // wide rows: the candidates one after another in window order,
+              // every lane one option word (and the word 64 on); the first
+              // feasible one wins, as in the general path's batch
+              for (uint64_t exw = ex; exw; exw &= exw - 1) {
+                const uint32_t c = ffs64(exw);
+                const uint32_t j = rlane(ow, c) >> 16;
+                const uint32_t t = T > 1 ? (uint32_t)s_tmpl[j] : 0u;
+                const ClaimRec* cr = KD.c_rec + j;
+                uint32_t cur[RR];
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) x_ma[r] = cr->maxa[r];
+                uint64_t x_cm;
+                {
+                  const uint4* q = (const uint4*)cr;
+                  const uint4 h0 = q[0], h1 = q[1], h2 = q[2], h3 = q[3];
+                  const int64_t tl4[4] = {(int64_t)(((uint64_t)h0.y << 32) | h0.x), (int64_t)(((uint64_t)h0.w << 32) | h0.z),
+                                          (int64_t)(((uint64_t)h1.y << 32) | h1.x), (int64_t)(((uint64_t)h1.w << 32) | h1.z)};
+                  const uint32_t cl[4] = {h2.x & 0xFFFFu, h2.x >> 16, h2.y & 0xFFFFu, h2.y >> 16};
+                  x_zm = ((uint64_t)h2.w << 32) | h2.z;
+                  x_cm = ((uint64_t)h3.y << 32) | h3.x;
+#pragma unroll
+                  for (uint32_t r = 0; r < RR; r++) {
+                    x_tot[r] = r < 4 ? tl4[r] : cr->tot_hi[r - 4];
+                    cur[r] = r < 4 ? cl[r] : cr->thr_hi[r - 4];
+                  }
+                }
+                const uint64_t G = grid_of(x_zm & vzm, x_cm & vcm, KD.Z, KD.C);
+                const uint64_t Gt = grid_of(s_tzm[t] & vzm, s_tcm[t] & vcm, KD.Z, KD.C);
+                uint32_t mm[RR];
+#pragma unroll
+                for (uint32_t r = 0; r < RR; r++) {
+                  const uint32_t o = s_thoff[r], n = s_thoff[r + 1] - o;
+                  mm[r] = thr_window(thr + o, n, cur[r], x_tot[r] + RQV(r));
+                  if (mm[r] == cur[r] + 4 && mm[r] < n) mm[r] = thr_search(thr + o, n, mm[r], x_tot[r] + RQV(r));
+                  x_mrow[r] = o + r + mm[r];
+                }
+                const uint64_t* row = KD.rows + ((size_t)pvx * T + t) * OW;
+                const uint64_t* opts = KD.c_opts + (size_t)j * OW;
+                bool anyw = false;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; h++) {
+                  const uint32_t w = lane + 64 * h;
+                  uint64_t x = 0;
+                  if (w < W) {
+                    x = opts[w] & row[w];
+#pragma unroll
+                    for (uint32_t r = 0; r < RR; r++)
+                      if (mm[r] != cur[r]) x &= KD.thr_set[(size_t)x_mrow[r] * OW + w];
+                    if (G != Gt) {
+                      uint64_t off = 0;
+                      for (uint64_t gm = G; gm; gm &= gm - 1) off |= slot[(size_t)ffs64(gm) * W + w];
+                      x &= off;
+                    }
+                  }
+                  x_w[h] = x;
+                  anyw = anyw || x != 0;
+                }
+                if (__ballot(anyw)) {
+                  fm = 1ull << c;
+                  break;
+                }
+              }
+            } else if ((ex >> lane) & 1) {
               const uint32_t j = ow >> 16;
               const uint32_t t = T > 1 ? (uint32_t)s_tmpl[j] : 0u;
               const ClaimRec* cr = KD.c_rec + j;
@@ -1237,7 +1305,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             }
             CTR(C_FULL, __popcll(ex));
             CTR(C_RX_XC, 1);
-            const uint64_t fm = __ballot(feas);
+            if (!WIDE) fm = __ballot(feas);
             if (fm) {
               fl = ffs64(fm);
               xwin = true;
@@ -1270,13 +1338,22 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             // slack / room codes, requirements; the window takes the codes
             const auto& KD = *karg();
             const uint32_t vctb = rlane(run_rec, 3);
+            if (WIDE) {
+              // the winner's option words, one lane per word
+              uint64_t* wopts = KD.c_opts + (size_t)(e >> 16) * OW;
+#pragma unroll
+              for (uint32_t h = 0; h < 2; h++)
+                if (lane + 64 * h < W) wopts[lane + 64 * h] = x_w[h];
+            }
             if (lane == fl) {
               const uint32_t j = ow >> 16;
               ClaimRec* cr = KD.c_rec + j;
               uint64_t* opts = KD.c_opts + (size_t)j * OW;
+              if (!WIDE) {
 #pragma unroll
-              for (uint32_t w = 0; w < WREG; w++)
-                if (w < W) opts[w] = x_nx[w];
+                for (uint32_t w = 0; w < WREG; w++)
+                  if (w < W) opts[w] = x_nx[w];
+              }
               int64_t nt[RR];
               uint32_t cu[RR];
 #pragma unroll
