@@ -647,6 +647,8 @@ typedef struct gs_catalog_env {
   const char* system_reserved_cpu;
   const char* system_reserved_memory;
   const char* eviction_memory_available;      /* evictionHard["memory.available"] */
+  const char* region;                         /* client.GetRegion(), only for the "no zones found for region %s"
+                                                 reason (instancetype.go:738-740); NULL reads as "" */
 } gs_catalog_env;
 
 /* The converted catalog in gs_problem form (its own string table): splice

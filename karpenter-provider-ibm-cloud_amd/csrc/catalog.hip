@@ -195,7 +195,7 @@ extern "C" gs_status gs_build_catalog(gs_ctx* c, const gs_vpc_profile* prof, uin
     else if (p.vcpu_kind != GS_VPC_VALUE) err = "instance profile " + name + " has unsupported CPU count type";
     else if (p.memory_kind == GS_VPC_NIL) err = "instance profile " + name + " has no memory";
     else if (p.memory_kind != GS_VPC_VALUE) err = "instance profile " + name + " has unsupported memory type";
-    else if (Z == 0) err = "no zones found for region";
+    else if (Z == 0) err = std::string("no zones found for region ") + (env->region ? env->region : "");
     if (!err.empty()) {
       c->cat_skipped.push_back(i);
       c->cat_reasons.push_back(err);

@@ -329,6 +329,7 @@ class GsCatalogEnv(C.Structure):
         ("kube_reserved_cpu", C.c_char_p), ("kube_reserved_memory", C.c_char_p),
         ("system_reserved_cpu", C.c_char_p), ("system_reserved_memory", C.c_char_p),
         ("eviction_memory_available", C.c_char_p),
+        ("region", C.c_char_p),
     ]
 
 

@@ -137,13 +137,14 @@ class InstanceType:
     offerings: list  # (zone, ct, price, available)
 
 
-def convert_profile(p: Profile, zones, price_of, spot_discount_percent=60, unavailable=(), kubelet=None):
+def convert_profile(p: Profile, zones, price_of, spot_discount_percent=60, unavailable=(), kubelet=None,
+                    region=""):
     """convertVPCProfileToInstanceType.  price_of(name, zone) -> float or None
     (None = GetPrice error -> 0.0, reference instancetype.go:753)."""
     if not p.name:
         raise ValueError("instance profile has empty name")
     if not zones:
-        raise ValueError("no zones found for region")
+        raise ValueError(f"no zones found for region {region}")  # instancetype.go:738-740
     arch = p.arch or "amd64"
     gpu = p.gpu or 0
     pods = 110

@@ -228,7 +228,7 @@ class Solver:
         return abi.claim_filter_to_list(res, len(problem.instance_types))
 
     def build_catalog(self, profiles, zones, price_rows=(), unavailable=(), now_ns=0, spot_discount_percent=0,
-                      kubelet=None, raw=False):
+                      kubelet=None, raw=False, region=None):
         """gs_build_catalog.  profiles: dicts with name, vcpu, memory_gib, arch,
         gpu, availability_class (None | ("enum", [..]) | ("fixed", v)) and
         optional vcpu_kind / memory_kind / gpu_kind; price_rows: (name, zone
@@ -267,6 +267,7 @@ class Solver:
         e.prices, e.n_prices = pr, len(price_rows)
         e.unavailable, e.n_unavailable = ua, len(unavailable)
         e.now_unix_ns = now_ns
+        e.region = enc(region)
         if kubelet is not None:
             e.has_kubelet = 1
             kr, sr, eh = kubelet.get("kubeReserved", {}), kubelet.get("systemReserved", {}), kubelet.get("evictionHard", {})

@@ -215,7 +215,7 @@ extern "C" gs_status oracle_convert_profile(const oracle_profile* pr, const orac
   if (cpu <= 2) pods = 30;
   else if (cpu <= 4) pods = 60;
   if (!env->has_client) return fail("IBM client not initialized - cannot determine zones for instance offerings");
-  if (env->n_zones == 0) return fail("no zones found for region");
+  if (env->n_zones == 0) return fail(string("no zones found for region ") + (env->region ? env->region : ""));  // instancetype.go:738-740
   // GetSupportedCapacityTypes
   vector<string> cts;
   if (pr->avail_kind == 1) {

@@ -59,6 +59,7 @@ typedef struct oracle_catalog_env {
   const char* const* price_zones;      /* NULL, or per price entry its zone (NULL entry: every zone) */
   const int64_t* unavailable_expiry;   /* NULL: entries never expire; else unavailable while now <= expiry */
   int64_t now_ns;
+  const char* region;                  /* p.client.GetRegion() (NULL = "") */
 } oracle_catalog_env;
 
 /* convertVPCProfileToInstanceType.  On success returns GS_OK and a

@@ -36,6 +36,7 @@ class OracleEnv(C.Structure):
         ("price_zones", C.POINTER(C.c_char_p)),
         ("unavailable_expiry", C.POINTER(C.c_int64)),
         ("now_ns", C.c_int64),
+        ("region", C.c_char_p),
     ]
 
 
@@ -119,7 +120,7 @@ def _cstrs(xs):
 def convert_profile(name, vcpu=None, memory_gib=None, arch=None, gpu=None, availability_class=None,
                     zones=(), prices=None, spot_discount_percent=0, unavailable=(), has_client=True,
                     kubelet=None, vcpu_kind=None, memory_kind=None, price_rows=None, unavailable_expiry=None,
-                    now_ns=0, gpu_kind=None):
+                    now_ns=0, gpu_kind=None, region=None):
     """returns (status, text).  price_rows: [(name, zone or None, price)]
     instead of the name-keyed `prices`; unavailable_expiry: per key expiry (ns)"""
     keep = []
@@ -143,6 +144,7 @@ def convert_profile(name, vcpu=None, memory_gib=None, arch=None, gpu=None, avail
         p.avail_values, p.n_avail_values = arr, n
     e = OracleEnv()
     e.has_client = 1 if has_client else 0
+    e.region = region.encode() if region is not None else None
     za, zn = _cstrs(list(zones))
     keep.append(za)
     e.zones, e.n_zones = za, zn

@@ -138,3 +138,11 @@ def test_quantity_parse_rejects(q):
     assert pyoracle.lib().oracle_parse_quantity_milli(q.encode(), C.byref(v)) != 0
     with pytest.raises(ValueError):
         cat.parse_quantity_milli(q)
+
+
+def test_no_zones_reason_names_region():
+    """"no zones found for region %s" carries client.GetRegion() (instancetype.go:738-740)"""
+    st, text = pyoracle.convert_profile("bx2-2x8", vcpu=2, memory_gib=8, zones=[], region="us-south")
+    assert st != 0 and text == "no zones found for region us-south"
+    with pytest.raises(ValueError, match="^no zones found for region us-south$"):
+        cat.convert_profile(cat.Profile("bx2-2x8", 2, 8), [], lambda n, z: None, region="us-south")
