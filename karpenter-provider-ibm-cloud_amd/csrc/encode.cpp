@@ -831,6 +831,11 @@ struct Ctx {
     // and the owner's tolerations; ftext: the terms with their values (a
     // group's owners under AffinityPolicy Honor must agree on it)
     std::string fid, ftext;
+    // AffinityPolicy Honor with a filter on more than the zone key: the first
+    // owner's filter terms (build_topology applies them to the bound pods'
+    // nodes and requires every counted pending spec to carry the same terms)
+    bool strict_aff = false;
+    std::vector<Reqs> filter;
     std::map<std::string, std::string> ml;
     std::vector<std::tuple<std::string, uint32_t, std::set<std::string>>> ex;
     // metav1.LabelSelector (nil selects nothing)
@@ -1291,6 +1296,20 @@ struct Ctx {
     if (p->n_bound_pods && !p->bound_pod_node) throw Fail{GS_E_INVALID, "bound pods without their nodes"};
     SelIndex six(groups);
     std::vector<uint32_t> cand;
+    // <U> countDomains under AffinityPolicy Honor: a bound pod counts only on
+    // a node whose labels (+ hostname) are strictly Compatible with one of the
+    // group's filter terms (oracle/solve.cpp TGroup::filter_matches)
+    std::vector<std::unique_ptr<Reqs>> nreqs(e.NN);
+    auto node_matches = [&](const SpreadEnc& sp, uint32_t raw) {
+      if (!nreqs[raw]) {
+        const gs_node& g = p->nodes[raw];
+        nreqs[raw].reset(new Reqs(node_labels_reqs(g.labels)));
+        reqs_add(e, *nreqs[raw], e.k_hostname, in_one_or_omega(e.k_hostname, S(g.name)));
+      }
+      for (auto& f : sp.filter)
+        if (reqs_compatible(e, *nreqs[raw], f, false)) return true;
+      return false;
+    };
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
       const gs_pod& bp = p->bound_pods[b];
       if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
@@ -1299,6 +1318,8 @@ struct Ctx {
       six.candidates(ps, &cand);
       for (uint32_t g : cand) {
         if (!group_counts(groups[g], ps)) continue;
+        if (groups[g].kind == 0 && groups[g].sp.strict_aff && !node_matches(groups[g].sp, p->bound_pod_node[b]))
+          continue;
         gsd::TGroupRec& t = e.tgroups[g];
         if (t.kind & gsd::TK_HOST) {
           e.hn0[(size_t)t.slot * e.NN + pos]++;
@@ -1325,6 +1346,21 @@ struct Ctx {
       mine.clear();
       for (uint32_t g : cand)
         if (group_counts(groups[g], pod_sel[s])) mine.push_back(g);
+      for (uint32_t g : mine) {
+        const SpreadEnc& sp = groups[g].sp;
+        if (groups[g].kind != 0 || !sp.strict_aff) continue;
+        // the NodeClaims / nodes this spec lands on match the owner's filter
+        // only if it carries the same terms and no preference narrows them
+        if (spec_aff_text[s] != sp.ftext)
+          throw Fail{GS_E_UNSUPPORTED,
+                     "a pod counted by a topology spread (nodeAffinityPolicy Honor) without its owner's node affinity"};
+        for (uint32_t k : spec_pref_keys[s])
+          for (auto& f : sp.filter)
+            if (f.count(k))
+              throw Fail{GS_E_UNSUPPORTED,
+                         "a pod counted by a topology spread (nodeAffinityPolicy Honor) with preferred node affinity "
+                         "on a key of the spread's filter"};
+      }
       sel_off[s] = (uint32_t)e.tg_list.size();
       sel_n[s] = (uint32_t)mine.size();
       for (uint32_t g : mine) {
@@ -1847,10 +1883,14 @@ struct Ctx {
     std::vector<PodVariant> vars;
     std::vector<std::vector<Tol>> var_tols;
     bool honor_taints = false;  // a spread with nodeTaintsPolicy Honor
+    std::string aff_text;             // the node filter's terms with their values
+    std::vector<uint32_t> pref_keys;  // keys of the preferred node-affinity terms
   };
   // pods -> specs: spec_of[pod], spec_rep[spec] (its first pod), and per spec
   // its variants' range in e.variants (sv_begin / sv_count)
   std::vector<uint32_t> spec_of, spec_rep, sv_begin, sv_count;
+  std::vector<std::string> spec_aff_text;               // PodWork::aff_text per spec
+  std::vector<std::vector<uint32_t>> spec_pref_keys;    // PodWork::pref_keys per spec
 
   void pod_phase_a(uint32_t i, PodWork& w, const std::map<std::string, AntiEnc>& inv_terms, bool topo_inputs) {
     auto& pd = p->pods[i];
@@ -1877,16 +1917,27 @@ struct Ctx {
       auto& t = p->tolerations[pd.tolerations.begin + k];
       w.tols.push_back({S(t.key), S(t.value), S(t.effect), t.op});
     }
-    if (!w.sps.empty()) {
-      // <U> MakeTopologyNodeFilter: node selector AND each required term
-      std::vector<Reqs> fr;
+    // <U> MakeTopologyNodeFilter: node selector AND each required term.  Its
+    // text (terms with values) is kept for every spec of a problem with
+    // topology inputs: a spec counted by a group whose Honor filter reaches
+    // past the zone key must carry that same filter (build_topology)
+    std::vector<Reqs> fr;
+    if (topo_inputs) {
       if (w.req_terms.empty()) fr.push_back(w.ns);
       for (auto& t : w.req_terms) {
         Reqs r = w.ns;
         for (auto& kv : t) reqs_add(e, r, kv.first, kv.second);
         fr.push_back(std::move(r));
       }
-      std::vector<std::string> terms, tl, texts;
+      std::vector<std::string> texts;
+      for (auto& r : fr) texts.push_back(canonical(e, r));
+      std::sort(texts.begin(), texts.end());
+      for (auto& t : texts) w.aff_text += t + "\x1e";
+      for (auto& pr : w.pref)
+        for (auto& kv : pr.second) w.pref_keys.push_back(kv.first);
+    }
+    if (!w.sps.empty()) {
+      std::vector<std::string> terms, tl;
       for (auto& r : fr) {
         std::vector<std::string> ks;
         for (auto& kv : r) ks.push_back(e.keys[kv.first].name);
@@ -1902,30 +1953,28 @@ struct Ctx {
       for (auto& t : terms) fid += t + ";";
       fid += "#";
       for (auto& t : tl) fid += t + ";";
-      std::string ftext;
-      bool honor_aff = false;
-      for (auto& sp : w.sps) honor_aff = honor_aff || !sp.ignore_aff;
-      if (honor_aff) {
-        for (auto& r : fr) texts.push_back(canonical(e, r));
-        std::sort(texts.begin(), texts.end());
-        for (auto& t : texts) ftext += t + "\x1e";
-      }
       for (auto& sp : w.sps) {
         sp.fid = fid;
-        if (!sp.ignore_aff) sp.ftext = ftext;
+        if (!sp.ignore_aff) sp.ftext = w.aff_text;
       }
     }
     // nodeAffinityPolicy Honor equals Ignore when the node selector and the
     // required terms constrain the zone key alone (oracle/solve.cpp: the
-    // filter then drops only nodes / NodeClaims outside the owner's zones)
+    // filter then drops only nodes / NodeClaims outside the owner's zones).
+    // Other filters are applied exactly where they can differ: a bound pod
+    // counts only on a node the filter matches, and the pending pods the
+    // group counts must carry the owner's filter terms (build_topology), so
+    // every NodeClaim / node they land on matches it
     bool zone_only = true;
     for (auto& kv : w.ns) zone_only = zone_only && kv.first == e.k_zone;
     for (auto& t : w.req_terms)
       for (auto& kv : t) zone_only = zone_only && kv.first == e.k_zone;
     if (!w.sps.empty() && !zone_only)
       for (auto& sp : w.sps)
-        if (!sp.ignore_aff)
-          throw Fail{GS_E_UNSUPPORTED, "topology spread (nodeAffinityPolicy Honor) on a pod with node affinity"};
+        if (!sp.ignore_aff) {
+          sp.strict_aff = true;
+          sp.filter = fr;
+        }
     for (auto& sp : w.sps) w.sp_hash.push_back(sp.hash(pns));
     // anti-affinity, inverse anti-affinity and host-port groups
     if (topo_inputs) {
@@ -2233,6 +2282,12 @@ struct Ctx {
     });
     for (uint32_t s = 0; s < NS; s++)
       if (work[s].err) std::rethrow_exception(work[s].err);
+    spec_aff_text.assign(NS, std::string());
+    spec_pref_keys.assign(NS, {});
+    for (uint32_t s = 0; s < NS; s++) {
+      spec_aff_text[s] = std::move(work[s].aff_text);
+      spec_pref_keys[s] = std::move(work[s].pref_keys);
+    }
     ph("spec_work");
     // spec variants (e.variants), then the device variants: each pod's
     // spec's variants in order (e.var_sv: device variant -> spec variant)

@@ -712,6 +712,94 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     return b.build()
 
 
+def random_honor_filter(seed, n_pods=None, affinity_policy="Honor", consolidation=False):
+    """small problems for nodeAffinityPolicy Honor past the zone key: each
+    deployment (app) shares one node affinity on instance family / instance
+    type (In, NotIn, two OR'd terms, with or without a zone term) and spreads
+    over zone or hostname selecting its own app; existing nodes of every
+    family hold bound pods of those apps, which count only where the node
+    matches the deployment's filter (<U> TopologyNodeFilter).  The random
+    stream does not depend on affinity_policy, so the Honor and Ignore
+    problems of one seed differ only in it.  consolidation: the bound pods
+    carry their deployment's node affinity and spreads too (consolidation
+    reschedules them as pending pods), nodes belong to a NodePool (they are
+    candidates) and few pods are pending."""
+    F, IT = "karpenter-ibm.sh/instance-family", "node.kubernetes.io/instance-type"
+    rng = np.random.default_rng(seed)
+    b = ProblemBuilder()
+    zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
+    fams = ["bx2", "cx2", "mx2"]
+    profs = [(f"{f}-{v}x{v * MEM_RATIO[f[0]]}", v, v * MEM_RATIO[f[0]], None) for f in fams for v in (2, 4, 8)]
+    prices = {p_[0]: round(0.05 * p_[1] + 0.01 * float(rng.random()), 4) for p_ in profs}
+    its = build_catalog(b, profs, zones, spot=bool(rng.random() < 0.5), prices=prices, rng=rng,
+                        unavailable_frac=0.1)
+    for j in range(int(rng.integers(1, 3))):
+        reqs = []
+        if rng.random() < 0.5:
+            zs = sorted(rng.choice(zones, size=int(rng.integers(1, len(zones) + 1)), replace=False).tolist())
+            reqs.append(("topology.kubernetes.io/zone", "In", zs))
+        limits = {"cpu": int(rng.choice([16, 64])) * 1000} if rng.random() < 0.2 else None
+        b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
+                       daemon={"cpu": 100, "pods": 1000})
+    apps = APPS[:3]
+    # one node affinity and one or two spreads per deployment
+    deps = []
+    for app in apps:
+        f1, f2 = [str(x) for x in rng.choice(fams, size=2, replace=False)]
+        r = rng.random()
+        if r < 0.3:
+            terms = [[(F, "In", [f1])]]
+        elif r < 0.45:
+            terms = [[(F, "In", sorted([f1, f2]))]]
+        elif r < 0.6:
+            terms = [[(F, "NotIn", [f1])]]
+        elif r < 0.75:
+            terms = [[(F, "In", [f1])], [(F, "In", [f2])]]
+        elif r < 0.9:
+            terms = [[(F, "In", [f1]), ("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(zones))])]]
+        else:
+            names = sorted({str(its[int(x)].name) for x in rng.choice(len(its), size=3)})
+            terms = [[(IT, "In", names)]]
+        sps = []
+        for _ in range(int(rng.integers(1, 3))):
+            sps.append({"key": "topology.kubernetes.io/zone" if rng.random() < 0.7 else "kubernetes.io/hostname",
+                        "max_skew": int(rng.choice([1, 1, 2])),
+                        "when": "ScheduleAnyway" if rng.random() < 0.3 else "DoNotSchedule",
+                        "selector": {"labels": {"app": app}}, "node_affinity_policy": affinity_policy})
+        deps.append((app, terms, sps))
+    for k in range(int(rng.integers(0, 7))):
+        it = its[rng.integers(0, len(its))]
+        labels = {r[0]: r[2][0] for r in it.requirements}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(zones))
+        labels["karpenter.sh/capacity-type"] = "on-demand"
+        labels["kubernetes.io/hostname"] = f"n{k}"
+        avail = {"cpu": int(rng.choice([1000, 3000, 6000])), "memory": 8 * GI * 1000, "pods": 20_000}
+        if consolidation:
+            labels["karpenter.sh/nodepool"] = "np0"
+            avail = {r: it.capacity[r] - it.overhead.get(r, 0) for r in it.capacity}
+        for q in range(int(rng.integers(0, 5))):
+            app, terms, sps = deps[int(rng.integers(0, len(deps)))]
+            extra = {"required_terms": terms, "spreads": [dict(sp) for sp in sps]} if consolidation else {}
+            b.add_bound_pod(k, _uid(rng), 0, {"cpu": 100, "pods": 1000}, labels={"app": app}, **extra)
+            if consolidation:
+                avail["cpu"] -= 100
+                avail["pods"] -= 1000
+        b.add_node(f"n{k}", labels, avail, initialized=True)
+    n = int(n_pods if n_pods is not None else (rng.choice([0, 0, 1, 2]) if consolidation else rng.integers(4, 40)))
+    for i in range(n):
+        req = {"cpu": int(rng.choice([250, 500, 1000, 2000])), "memory": int(rng.choice([1, 2, 4])) * GI * 1000,
+               "pods": 1000}
+        if rng.random() < 0.15:  # a pod no spread counts, with its own affinity
+            b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + i, req, labels={"app": "cache"},
+                      required_terms=[[(F, "In", [str(rng.choice(fams))])]] if rng.random() < 0.5 else (),
+                      preferred_terms=[(10, [(F, "In", [str(rng.choice(fams))])])] if rng.random() < 0.3 else ())
+            continue
+        app, terms, sps = deps[int(rng.integers(0, len(deps)))]
+        b.add_pod(_uid(rng), 1_700_000_000_000_000_000 + i, req, labels={"app": app}, required_terms=terms,
+                  spreads=[dict(sp) for sp in sps])
+    return b.build()
+
+
 def _selector(rng, tgt):
     r = rng.random()
     if r < 0.6:

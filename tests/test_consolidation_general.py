@@ -49,6 +49,22 @@ def test_oracle_general_consolidation_sees_constraints():
     assert changed > 0
 
 
+def test_oracle_honor_filter_consolidation_changes_commands():
+    """the filter changes consolidation commands on these clusters"""
+    differ = 0
+    for seed in range(24):
+        p = synth.random_honor_filter(seed, consolidation=True)
+        pi = synth.random_honor_filter(seed, consolidation=True, affinity_policy="Ignore")
+        if len(p.nodes) == 0:
+            continue
+        cands = list(range(len(p.nodes)))
+        a = pyoracle.consolidate(ConsolidationInput(p, cands, mode=abi.CONSOLIDATE_SINGLE))
+        b = pyoracle.consolidate(ConsolidationInput(pi, cands, mode=abi.CONSOLIDATE_SINGLE))
+        assert a[0] == b[0] == abi.GS_OK
+        differ += a[1] != b[1]
+    assert differ > 0
+
+
 def test_oracle_e2e_consolidation_shape_small():
     p = synth.e2e_consolidation_cluster(n_nodes=30)
     cin = ConsolidationInput(p, list(range(30)), mode=abi.CONSOLIDATE_SINGLE)
@@ -87,6 +103,18 @@ def check(solver, p, mode, cands=None, shard=(0, 0)):
 @pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
 def test_gpu_general_consolidation(solver, seed, mode):
     check(solver, synth.random_consolidation_general(seed), mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
+def test_gpu_consolidation_honor_filter(solver, seed, mode):
+    """spreads with nodeAffinityPolicy Honor on instance family / type: the
+    kept nodes' bound pods count only where the node matches the filter"""
+    p = synth.random_honor_filter(seed, consolidation=True)
+    if len(p.nodes) == 0:
+        pytest.skip("no nodes")
+    check(solver, p, mode)
 
 
 @pytest.mark.gpu

@@ -114,9 +114,12 @@ def test_refusals():
 # Honor) and the owner tolerates its taints (TaintPolicy Honor); under taint
 # Honor a domain enters the minimum only if a NodePool / node providing it
 # has taints the pod tolerates (TopologyDomainGroup.ForEachDomain).  Where the
-# filter changes the answer the product refuses (it keeps Ignore semantics);
-# where it cannot (zone-only affinity, tolerated taints) both accept and the
-# Honor run must equal the Ignore run.
+# filter cannot change the answer (zone-only affinity, tolerated taints) both
+# accept and the Honor run must equal the Ignore run.  Round 5: an affinity
+# filter past the zone key is applied by the product too -- bound pods count
+# only on matching nodes, and the pending pods a group counts must carry the
+# owner's terms (every NodeClaim / node they land on then matches); other
+# Honor inputs stay refused.
 def _tainted_node_case(pol):
     sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_taints_policy": pol}
     b = _base(n_pods=0)
@@ -161,7 +164,32 @@ def test_filter_affinity_honor_drops_incompatible_node():
     p = _family_node_case("Honor")
     st, res, _ = pyoracle.solve(p)
     assert st == abi.GS_OK and _zones(res) == [([0], "us-south-1"), ([1], "us-south-2")]
-    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(p)[0] == abi.GS_OK  # the product drops n0's pods too (GPU: test_gpu_topology_kats)
+
+
+def _family_counted_case(other_sel=None, other_pref=None):
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_affinity_policy": "Honor"}
+    b = _base(n_pods=0)
+    for i in range(2):
+        b.add_pod(f"p{i}", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  node_selector={"karpenter-ibm.sh/instance-family": "bx2"}, spreads=[sp])
+    b.add_pod("q", 1, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+              node_selector=other_sel, preferred_terms=other_pref or ())
+    return b.build()
+
+
+def test_filter_affinity_honor_counted_pods_must_carry_the_filter():
+    """a pod the group counts but whose node affinity differs from the
+    owner's may land where the filter does not match (upstream then does not
+    count it): the product refuses; the same affinity is accepted, and so is a
+    preference on another key, but not one on a filter key"""
+    F = "karpenter-ibm.sh/instance-family"
+    assert pyoracle.solve(_family_counted_case())[0] == abi.GS_OK
+    assert lib.validate(_family_counted_case())[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(_family_counted_case({F: "cx2"}))[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(_family_counted_case({F: "bx2"}))[0] == abi.GS_OK
+    assert lib.validate(_family_counted_case({F: "bx2"}, [(10, [(Z, "In", ["us-south-2"])])]))[0] == abi.GS_OK
+    assert lib.validate(_family_counted_case({F: "bx2"}, [(10, [(F, "In", ["bx2"])])]))[0] == abi.GS_E_UNSUPPORTED
 
 
 def _tainted_pool_case(pol):
@@ -255,6 +283,26 @@ def test_affinity_policy_honor_random_equals_ignore(seed, multi_term):
     assert lib.validate(ph)[0] == abi.GS_OK
 
 
+@pytest.mark.parametrize("seed", range(60))
+def test_affinity_policy_honor_family_filter_accepted(seed):
+    """deployments with node affinity on instance family / type and Honor
+    spreads, bound pods on nodes of every family: oracle and encoder accept
+    (the GPU parity runs are test_gpu_topology_honor_filter)"""
+    p = synth.random_honor_filter(seed)
+    assert pyoracle.solve(p)[0] == abi.GS_OK
+    assert lib.validate(p)[0] == abi.GS_OK
+
+
+def test_affinity_policy_honor_family_filter_changes_answers():
+    """the filter matters on these problems: Honor differs from Ignore"""
+    differ = 0
+    for seed in range(30):
+        rh = pyoracle.solve(synth.random_honor_filter(seed))[1]
+        ri = pyoracle.solve(synth.random_honor_filter(seed, affinity_policy="Ignore"))[1]
+        differ += rh != ri
+    assert differ >= 5, differ
+
+
 def test_taint_policy_honor_without_taints_equals_ignore():
     """TopologyNodeFilter.Matches: with no taint in the problem Honor filters
     nothing (the group is the Ignore group)"""
@@ -323,6 +371,18 @@ def test_gpu_topology_affinity_policy_honor(solver, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_gpu_topology_honor_filter(solver, seed):
+    _check(solver, synth.random_honor_filter(seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_topology_honor_filter_many_pods(solver, seed):
+    _check(solver, synth.random_honor_filter(700 + seed, n_pods=400))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(10))
 def test_gpu_topology_random_many_pods(solver, seed):
     _check(solver, synth.random_topology(900 + seed, n_pods=300))
@@ -343,6 +403,8 @@ def test_gpu_topology_kats(solver):
                       labels={"app": "web", "pod-template-hash": "h2"}, spreads=[sp])
         _check(solver, b.build())
     _check(solver, _base(n_pods=7, spread={"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}).build())
+    _check(solver, _family_node_case("Honor"))
+    _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 
 
