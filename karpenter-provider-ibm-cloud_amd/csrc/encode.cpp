@@ -935,6 +935,12 @@ struct Ctx {
   };
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
+  // spread groups whose node filter cannot matter (both policies Ignore, or
+  // affinity Honor over an empty filter with taints Ignore) and that agree on
+  // everything else, minDomains included, count the same pods in the same
+  // domains: upstream keeps one group per filter (TopologyGroup.Hash), the
+  // product shares one (pod_phase_b)
+  std::map<std::string, uint32_t> merge_idx;
   std::vector<PodSel> pod_sel;  // per pod spec (spec_of)
   std::vector<std::pair<Reqs, bool>> np_universe;  // NodePool requirements (+labels), has instance types
   uint32_t bound_alias = gsd::NONE;  // bound pod b is also pod bound_alias + b (consolidation)
@@ -1875,7 +1881,7 @@ struct Ctx {
     std::vector<Reqs> req_terms;
     std::vector<std::pair<int32_t, Reqs>> pref;
     std::vector<SpreadEnc> sps;
-    std::vector<std::string> sp_hash;
+    std::vector<std::string> sp_hash, sp_merge;
     std::vector<GroupKey> g_anti, g_aff, g_inv, g_port;  // in the order the pod names them
     std::vector<Tol> tols;
     std::vector<uint32_t> sgid, own_static;
@@ -1975,7 +1981,20 @@ struct Ctx {
           sp.strict_aff = true;
           sp.filter = fr;
         }
-    for (auto& sp : w.sps) w.sp_hash.push_back(sp.hash(pns));
+    bool filter_empty = true;
+    for (auto& r : fr) filter_empty = filter_empty && r.empty();
+    for (auto& sp : w.sps) {
+      w.sp_hash.push_back(sp.hash(pns));
+      std::string mk;
+      // GS_GROUP_MERGE=0: one group per upstream group (A/B knob)
+      static const bool merge_on = !std::getenv("GS_GROUP_MERGE") || std::atoi(std::getenv("GS_GROUP_MERGE")) != 0;
+      if (merge_on && !sp.honor_taints && (sp.ignore_aff || filter_empty)) {
+        SpreadEnc x = sp;
+        x.fid = "-";
+        mk = x.hash(pns) + "|m:" + std::to_string(sp.mind);
+      }
+      w.sp_merge.push_back(std::move(mk));
+    }
     // anti-affinity, inverse anti-affinity and host-port groups
     if (topo_inputs) {
       const PodSel& me = pod_sel[spec_of[i]];
@@ -2010,9 +2029,15 @@ struct Ctx {
     for (size_t k = 0; k < w.sps.size(); k++) {
       auto f = group_idx.find(w.sp_hash[k]);
       if (f == group_idx.end()) {
-        if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
-        f = group_idx.emplace(w.sp_hash[k], (uint32_t)groups.size()).first;
-        groups.push_back(GroupEnc{w.sps[k], pns});
+        auto m = w.sp_merge[k].empty() ? merge_idx.end() : merge_idx.find(w.sp_merge[k]);
+        if (m != merge_idx.end()) {
+          f = group_idx.emplace(w.sp_hash[k], m->second).first;
+        } else {
+          if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
+          f = group_idx.emplace(w.sp_hash[k], (uint32_t)groups.size()).first;
+          if (!w.sp_merge[k].empty()) merge_idx.emplace(w.sp_merge[k], (uint32_t)groups.size());
+          groups.push_back(GroupEnc{w.sps[k], pns});
+        }
       } else if (!w.sps[k].ignore_aff && groups[f->second].sp.ftext != w.sps[k].ftext) {
         // upstream keys the group by the filter's keys and keeps its first
         // owner's filter: later owners with other values would see counts

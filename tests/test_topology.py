@@ -251,6 +251,31 @@ def test_filter_group_keeps_first_owners_filter():
     assert lib.validate(_shared_group_case(same))[0] == abi.GS_OK
 
 
+def _merge_case(second_mind):
+    """owners of one zone spread that differ only in tolerations: upstream
+    keeps a group per toleration set (TopologyGroup.Hash), each with its first
+    owner's minDomains; the product shares the groups whose minDomains agree"""
+    b = _base(n_pods=0)
+    b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 0, "memory": 0, "pods": 0})
+    b.add_bound_pod(0, "b0", 0, {"cpu": 1}, labels={"app": "web"})
+    for i in range(9):
+        sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}
+        tols = [("spot", "Exists", "", "")] if i % 3 == 1 else []
+        if i == 1 and second_mind is not None:
+            sp["min_domains"] = second_mind
+        b.add_pod(f"p{i}", i, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+                  tolerations=tols, spreads=[sp])
+    return b.build()
+
+
+def test_groups_differing_in_tolerations_only():
+    for mind in (None, 2, 5):
+        assert pyoracle.solve(_merge_case(mind))[0] == abi.GS_OK
+        assert lib.validate(_merge_case(mind))[0] == abi.GS_OK
+    # minDomains 5 > 3 zones holds the first owner's group at a global minimum of 0
+    assert pyoracle.solve(_merge_case(5))[1] != pyoracle.solve(_merge_case(None))[1]
+
+
 def test_affinity_policy_honor_zone_only_equals_ignore():
     """nodeAffinityPolicy Honor with a zone-only node selector: the filter
     drops only nodes outside the owner's zones, so Honor == Ignore"""
@@ -404,6 +429,8 @@ def test_gpu_topology_kats(solver):
         _check(solver, b.build())
     _check(solver, _base(n_pods=7, spread={"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}).build())
     _check(solver, _family_node_case("Honor"))
+    for mind in (None, 2, 5):
+        _check(solver, _merge_case(mind))
     _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 
