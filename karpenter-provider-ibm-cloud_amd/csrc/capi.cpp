@@ -117,6 +117,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.TGZ = e.TGZ;
   d.ZS = e.ZS;
   d.NZV = e.NZV;
+  d.dom_ct = e.dom_ct ? 1u : 0u;
   d.zknown0 = e.zknown0;
   c->upload(d.tgroups, e.tgroups);
   c->upload(d.tg_list, e.tg_list);
@@ -726,15 +727,15 @@ gs_status gs_fetch(gs_ctx* c, gs_result* out) {
     c->claim_pod_offsets.push_back((uint32_t)c->claim_pods.size());
     c->claim_its.insert(c->claim_its.end(), its.begin() + (size_t)j * 60, its.begin() + (size_t)j * 60 + nits[j]);
     c->claim_it_offsets.push_back((uint32_t)c->claim_its.size());
-    if (e.TG && e.keys[e.k_zone].vocab.size() <= (size_t)gsd::ZVMAX && !(hdr[j].zflags & gsd::ZF_COMP)) {
+    if (e.TG && e.keys[e.k_dom].vocab.size() <= (size_t)gsd::ZVMAX && !(hdr[j].zflags & gsd::ZF_COMP)) {
       // topology spread narrowed the zone to In[domain]: the device's zone
       // Has already includes it (template AND pods AND topology)
       gsh::KReq q;
       q.comp = false;
-      q.has = gsh::Bits(e.keys[e.k_zone].vocab.words());
-      q.excl = gsh::Bits(e.keys[e.k_zone].vocab.words());
+      q.has = gsh::Bits(e.keys[e.k_dom].vocab.words());
+      q.excl = gsh::Bits(e.keys[e.k_dom].vocab.words());
       q.has.w[0] = hdr[j].zfull;
-      gsh::reqs_add(e, creq[j], e.k_zone, q);
+      gsh::reqs_add(e, creq[j], e.k_dom, q);
     }
     creq[j].erase(e.k_hostname);  // FinalizeScheduling
     c->req_text[kept] = gsh::canonical(e, creq[j]);

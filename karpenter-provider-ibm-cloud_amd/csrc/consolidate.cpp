@@ -480,8 +480,20 @@ gs_status run_and_decide(gs_ctx* c, gs_consolidation_result* out) {
     cmd.candidate_price = cp;
     // the NodeClaim's capacity-type requirement: template AND every added pod
     const gsd::ClaimRec& h = hdr[k];
-    const bool has_spot = (h.ctb & gsd::CT_SPOT) != 0;
-    const bool has_od = (h.ctb & gsd::CT_OD) != 0;
+    bool has_spot = (h.ctb & gsd::CT_SPOT) != 0;
+    bool has_od = (h.ctb & gsd::CT_OD) != 0;
+    if (e.dom_ct && !(h.zflags & gsd::ZF_COMP)) {
+      // capacity-type topology domains: the In set after the spreads'
+      // narrowing is the claim's domain Has (as the decoder writes it)
+      const auto& v = e.keys[e.k_ct].vocab;
+      auto in = [&](const char* x) {
+        auto g = v.id.find(x);
+        const uint32_t id = g == v.id.end() ? v.omega : g->second;
+        return id < 64 && ((h.zfull >> id) & 1);
+      };
+      has_spot = has_spot && in("spot");
+      has_od = has_od && in("on-demand");
+    }
     if (all_spot && has_spot) {  // SpotToSpotConsolidation disabled
       cmd.reason = GS_NOOP_SPOT_TO_SPOT;
       continue;

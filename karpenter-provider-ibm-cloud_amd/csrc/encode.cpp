@@ -511,6 +511,12 @@ struct Ctx {
     e.k_ct = e.key_id[kCapacityType];
     e.k_hostname = e.key_id[kHostname];
     e.k_nodepool = e.key_id[kNodePool];
+    // spreads on the capacity-type key move the domain machinery onto it
+    // (build_nodes / build_pods swap the zone and capacity-type fields)
+    e.dom_ct = false;
+    for (uint32_t i = 0; i < p->n_spreads; i++)
+      e.dom_ct = e.dom_ct || normalize(S(p->spreads[i].topology_key)) == kCapacityType;
+    e.k_dom = e.dom_ct ? e.k_ct : e.k_zone;
   }
 
   uint32_t key_of(uint32_t sid) const { return e.key_id.at(normalize(S(sid))); }
@@ -813,11 +819,11 @@ struct Ctx {
   // zone Has over the zone vocabulary (first word; topology needs <= 64
   // values) and the complement flag of the zone requirement
   uint64_t zone_full(const Reqs& r) const {
-    auto f = r.find(e.k_zone);
+    auto f = r.find(e.k_dom);
     return f == r.end() ? ~0ull : f->second.has.w[0];
   }
   uint32_t zone_flags(const Reqs& r) const {
-    auto f = r.find(e.k_zone);
+    auto f = r.find(e.k_dom);
     return f == r.end() || f->second.comp ? gsd::ZF_COMP : 0u;
   }
 
@@ -958,8 +964,10 @@ struct Ctx {
       const gs_spread& q = p->spreads[pd.spreads.begin + k];
       SpreadEnc sp;
       sp.key = normalize(S(q.topology_key));
-      if (sp.key != kZone && sp.key != kHostname)
-        throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / hostname"};
+      if (sp.key != kZone && sp.key != kHostname && sp.key != kCapacityType)
+        throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / capacity type / hostname"};
+      if (e.dom_ct && sp.key == kZone)
+        throw Fail{GS_E_UNSUPPORTED, "topology spreads on both the zone and the capacity-type key"};
       if (q.max_skew < 1) throw Fail{GS_E_INVALID, "maxSkew < 1"};
       if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE ||
           q.node_taints_policy > GS_POLICY_IGNORE)
@@ -1011,6 +1019,8 @@ struct Ctx {
       if (tk != kHostname && !(tk == kZone && !affinity))
         throw Fail{GS_E_UNSUPPORTED, affinity ? "pod affinity topologyKey other than hostname"
                                               : "pod anti-affinity topologyKey other than hostname / zone"};
+      if (e.dom_ct && tk == kZone)
+        throw Fail{GS_E_UNSUPPORTED, "zone-key pod anti-affinity beside capacity-type topology spreads"};
       AntiEnc a;
       a.required = q.required != 0;
       a.weight = q.weight;
@@ -1249,23 +1259,28 @@ struct Ctx {
   void build_topology() {
     e.TG = (uint32_t)groups.size();
     if (!e.TG) return;
-    const Vocab& zv = e.keys[e.k_zone].vocab;
+    const Vocab& zv = e.keys[e.k_dom].vocab;
     bool any_zone = false;
-    for (auto& g : groups) any_zone = any_zone || g.sp.key == kZone;
+    for (auto& g : groups) any_zone = any_zone || g.sp.key != kHostname;
     if (any_zone && zv.size() > (size_t)gsd::ZVMAX)
-      throw Fail{GS_E_UNSUPPORTED, "zone topology groups over more than 63 zone values"};
+      throw Fail{GS_E_UNSUPPORTED, "zone / capacity-type topology groups over more than 63 domain values"};
     e.NZV = (uint32_t)std::min<size_t>(zv.size() - 1, gsd::ZVMAX);
     e.ZS = std::max<uint32_t>(e.NZV, 1);
     e.zone_order.resize(e.NZV);
     std::iota(e.zone_order.begin(), e.zone_order.end(), 0);
     std::sort(e.zone_order.begin(), e.zone_order.end(), [&](uint32_t a, uint32_t b) { return zv.vals[a] < zv.vals[b]; });
     e.zone_cat.assign(gsd::ZVMAX, gsd::NONE);
-    for (uint32_t z = 0; z < e.Z; z++)
-      if (e.cat_zone[z] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_zone[z]] = z;
+    if (e.dom_ct) {
+      for (uint32_t c = 0; c < e.C; c++)
+        if (e.cat_ct[c] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_ct[c]] = c;
+    } else {
+      for (uint32_t z = 0; z < e.Z; z++)
+        if (e.cat_zone[z] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_zone[z]] = z;
+    }
     uint64_t known_zone = 0;
     for (auto& u : np_universe) {
       if (!u.second) continue;
-      auto f = u.first.find(e.k_zone);
+      auto f = u.first.find(e.k_dom);
       if (f != u.first.end() && !f->second.comp) known_zone |= f->second.has.w[0];  // operator In
     }
     e.known_np = known_zone;
@@ -1717,6 +1732,7 @@ struct Ctx {
       Key& key = e.keys[k];
       if (key.cls == KEY_FREE || !key.wellknown || key.vocab.size() > (size_t)gsd::FKV) continue;
       if (key.cls == KEY_ZONE && zone_topology) continue;
+      if (key.cls == KEY_CT && e.dom_ct) continue;
       bool lacking = false;
       for (uint32_t i = 0; i < p->n_nodes && !lacking; i++) {
         const gs_range lr = p->nodes[i].labels;
@@ -2400,7 +2416,7 @@ struct Ctx {
       vr.ctb = ct_bits(pv.reqs) | (pv.reqs.empty() && pv.own.empty() ? gsd::VF_SIMPLE : 0u);
       // owns a zone spread group: only those read the per-pod minimum counts
       for (uint32_t g : pv.own)
-        if (groups[g].sp.key == kZone && groups[g].kind == 0) vr.ctb |= gsd::VF_ZSPREAD;
+        if (groups[g].sp.key != kHostname && groups[g].kind == 0) vr.ctb |= gsd::VF_ZSPREAD;
       // hostname-only topology (spread, anti-affinity, inverse, host ports;
       // not pod affinity): the wave kernel's fast accept reads the counts
       if (pv.reqs.empty() && !pv.own.empty() && pv.own.size() <= 4) {
@@ -2427,6 +2443,9 @@ struct Ctx {
         else vr.cfull_off = gsd::NONE;
       }
       vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
+      // dom_ct: the nodes' zvid / cvid are swapped (build_nodes), so are the
+      // existing-node checks' masks
+      if (e.dom_ct) std::swap(vr.zfull_off, vr.cfull_off);
     }
     par_for(e.P, 1024, [&](uint32_t i) {
       for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
@@ -2583,6 +2602,7 @@ struct Ctx {
         else if (key.cls == KEY_ZONE) nr.zvid = vid;
         else nr.cvid = vid;
       }
+      if (e.dom_ct) std::swap(nr.zvid, nr.cvid);  // zvid: the topology domain's value
       for (uint32_t k : exempt_keys) {
         bool has = reqs.count(k) != 0;
         if (!has)

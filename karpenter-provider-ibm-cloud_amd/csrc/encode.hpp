@@ -92,6 +92,11 @@ struct Encoded {
   std::vector<Key> keys;
   std::unordered_map<std::string, uint32_t> key_id;
   uint32_t k_zone = gsd::NONE, k_ct = gsd::NONE, k_hostname = gsd::NONE, k_nodepool = gsd::NONE;
+  // the topology domain key of the zone-count machinery: the zone, or the
+  // capacity type when the problem's spreads use that key (dom_ct; the
+  // kernels then narrow a NodeClaim's catalog capacity types, not zones)
+  uint32_t k_dom = gsd::NONE;
+  bool dom_ct = false;
   std::vector<uint32_t> it_keys;    // key ids, IT key order
   std::vector<uint32_t> free_keys;  // key ids, free slot order
   std::vector<uint32_t> cat_zone;   // catalog zone id -> vocab id

@@ -1342,7 +1342,12 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               const int32_t* hrow = dd.hc + (size_t)(cb + j) * dd.TGH;
               zset = topo_claim_g(dd, ts, own_n, czf & vr.zn, [&](uint32_t hs) -> int64_t { return hrow[hs]; }, OWN);
               pre = zset != 0;
-              if (pre && zset != ~0ull) zm &= topo_catmask(dd, zset);
+              if (pre && zset != ~0ull) {
+                // the domains narrow the catalog zones, or (dom_ct) capacity types
+                const uint64_t dcat = topo_catmask(dd, zset);
+                if (dd.dom_ct) cm &= dcat;
+                else zm &= dcat;
+              }
             }
             if (pre) {
               G = grid_of(zm & vr.zm, cm & vr.cm, dd.Z, dd.C);
@@ -1554,8 +1559,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             }
             s_slk[j] = pack_slack(dd, ma, nt);  // exact re-quantization: no drift
             s_rm[j] = pack_room(thr, s_thoff, cu, nt, dd.RQ);
-            cr->zm = zm & vr.zm;  // zm carries the topology narrowing
-            cr->cm &= vr.cm;
+            cr->zm = zm & vr.zm;  // zm (dom_ct: cm) carries the topology narrowing
+            cr->cm = cm & vr.cm;
             cr->ctb &= vr.ctb;
             cr->count++;
             if (TOPO) {
@@ -1625,12 +1630,14 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(d, tzs);
           if (tzs == 0 || tzcat == 0) continue;
         }
-        const uint64_t tcm = tr.cm & vr.cm;
+        // dom_ct: the picked domains are capacity types of the template's zones
+        const bool dct = d.dom_ct != 0;
+        const uint64_t tcm = tr.cm & vr.cm & (dct ? tzcat : ~0ull), tzsel = dct ? tr.zm & vr.zm : tzcat;
         auto rowx = [&](uint32_t w) -> uint64_t {
           uint64_t x = row[w];
           if (tzs != ~0ull) {
             uint64_t off = 0;
-            for (uint64_t zm_ = tzcat; zm_; zm_ &= zm_ - 1) {
+            for (uint64_t zm_ = tzsel; zm_; zm_ &= zm_ - 1) {
               const uint32_t zc = (uint32_t)__ffsll((long long)zm_) - 1u;
               for (uint32_t c = 0; c < d.C; c++)
                 if ((tcm >> c) & 1) off |= slot[(zc * d.C + c) * W + w];
@@ -1716,8 +1723,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         if (tid == 0) {
           cr->tmpl = t;
           cr->count = 1;
-          cr->zm = tr.zm & vr.zm & tzcat;
-          cr->cm = tr.cm & vr.cm;
+          cr->zm = tr.zm & vr.zm & (dct ? ~0ull : tzcat);
+          cr->cm = tcm;
           cr->ctb = tr.ctb & vr.ctb;
           cr->zfull = tr.zfull & vr.zn & tzs;
           cr->zflags = tzs != ~0ull ? 0u : (tr.zflags & vr.zflags);

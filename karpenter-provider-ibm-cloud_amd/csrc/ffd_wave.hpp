@@ -2058,7 +2058,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           const int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
           zset = topo_claim_g(KD, ts, own_n, czf & vzn, [&](uint32_t hs) -> int64_t { return hrow[hs]; }, OWN);
           pre = zset != 0;
-          if (pre && zset != ~0ull) zm &= topo_catmask(KD, zset);
+          if (pre && zset != ~0ull) {
+            // the domains narrow the catalog zones, or (dom_ct) capacity types
+            const uint64_t dcat = topo_catmask(KD, zset);
+            if (KD.dom_ct) cm &= dcat;
+            else zm &= dcat;
+          }
         }
         if (pre) {
           G = grid_of(zm & vzm, cm & vcm, KD.Z, KD.C);
@@ -2246,8 +2251,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
           s_slk[j] = pack_slack(d, ma, nt);  // exact re-quantization: no drift
           s_rm[j] = pack_room(thr, s_thoff, cu, nt, KD.RQ);
-          cr->zm = zm & vzm;  // zm carries the topology narrowing
-          cr->cm &= vcm;
+          cr->zm = zm & vzm;  // zm (dom_ct: cm) carries the topology narrowing
+          cr->cm = cm & vcm;
           cr->ctb &= vctb;
           if (TOPO) {
             // zone requirement after Add (+ the topology domain), then
@@ -2382,12 +2387,14 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         tzcat = (uint64_t)uniform_i64((int64_t)tzcat);
         if (tzs == 0 || tzcat == 0) continue;
       }
-      const uint64_t tcm = tr.cm & vcm;
+      // dom_ct: the picked domains are capacity types of the template's zones
+      const bool dct = KD.dom_ct != 0;
+      const uint64_t tcm = tr.cm & vcm & (dct ? tzcat : ~0ull), tzsel = dct ? tr.zm & vzm : tzcat;
       auto rowx = [&](uint32_t w) -> uint64_t {
         uint64_t x = row[w];
         if (tzs != ~0ull) {
           uint64_t off = 0;
-          for (uint64_t zm_ = tzcat; zm_; zm_ &= zm_ - 1) {
+          for (uint64_t zm_ = tzsel; zm_; zm_ &= zm_ - 1) {
             const uint32_t zc = ffs64(zm_);
             for (uint32_t c = 0; c < KD.C; c++)
               if ((tcm >> c) & 1) off |= slot[(zc * KD.C + c) * W + w];
@@ -2498,8 +2505,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       if (lane == 0) {
         cr->tmpl = t;
         cr->count = 1;
-        cr->zm = tr.zm & vzm & tzcat;
-        cr->cm = tr.cm & vcm;
+        cr->zm = tr.zm & vzm & (dct ? ~0ull : tzcat);
+        cr->cm = tcm;
         cr->ctb = tr.ctb & vctb;
         cr->zfull = tr.zfull & vzn & tzs;
         cr->zflags = tzs != ~0ull ? 0u : (tr.zflags & vzflags);

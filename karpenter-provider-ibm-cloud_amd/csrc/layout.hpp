@@ -326,6 +326,7 @@ struct DevProblem {
   // topology groups
   uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size
   uint32_t TGZ, ZS;            // zone groups, zone-count stride (max(NZV, 1))
+  uint32_t dom_ct;             // the "zone" groups' domain key is the capacity type (zone_cat -> catalog capacity types)
   uint32_t pad_tg;
   uint64_t zknown0;            // zone domains known before the Solve (universe + counted), every zone group
   const TGroupRec* tgroups;    // [TG]

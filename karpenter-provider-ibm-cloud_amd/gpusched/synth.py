@@ -604,7 +604,8 @@ def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False, par
     return b.build()
 
 
-def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore", multi_term=False):
+def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore", multi_term=False,
+                    domain_key="topology.kubernetes.io/zone"):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
@@ -615,8 +616,13 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     stream is the same for both, so the two problems differ only in it).
     affinity_policy: the nodeAffinityPolicy of the spreads of pods with a
     (zone-only) required node-affinity term; multi_term: those spread owners
-    carry two zone In terms instead (OR; relaxation drops the first)"""
+    carry two zone In terms instead (OR; relaxation drops the first).
+    domain_key "karpenter.sh/capacity-type": the non-hostname spreads use
+    that key, NodePools constrain it and nodes carry spot / on-demand (those
+    draws come from their own stream)"""
     rng = np.random.default_rng(seed)
+    ctk = "karpenter.sh/capacity-type"
+    cts = np.random.default_rng(seed + 0xC7) if domain_key == ctk else None
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
     profs = []
@@ -627,7 +633,8 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     if not profs:
         profs = [("bx2-4x16", 4, 16, None)]
     prices = {p_[0]: round(0.05 * p_[1] + 0.01 * float(rng.random()), 4) for p_ in profs}
-    its = build_catalog(b, profs, zones, spot=bool(rng.random() < 0.5), prices=prices, rng=rng,
+    spot = bool(rng.random() < 0.5)
+    its = build_catalog(b, profs, zones, spot=spot or cts is not None, prices=prices, rng=rng,
                         unavailable_frac=0.1)
     n_np = int(rng.integers(1, 3))
     for j in range(n_np):
@@ -635,6 +642,8 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
         if rng.random() < 0.7:
             zs = sorted(rng.choice(zones, size=int(rng.integers(1, len(zones) + 1)), replace=False).tolist())
             reqs.append(("topology.kubernetes.io/zone", "In", zs))
+        if cts is not None and cts.random() < 0.8:
+            reqs.append((ctk, "In", [["spot"], ["on-demand"], ["on-demand", "spot"]][int(cts.integers(0, 3))]))
         taints = [("dedicated", "x", "PreferNoSchedule")] if rng.random() < 0.3 else []
         limits = {"cpu": int(rng.choice([8, 32])) * 1000} if rng.random() < 0.2 else None
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, taints=taints, limits=limits,
@@ -644,7 +653,7 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
         it = its[rng.integers(0, len(its))]
         labels = {r[0]: r[2][0] for r in it.requirements}
         labels["topology.kubernetes.io/zone"] = str(rng.choice(zones + ["z9"]))
-        labels["karpenter.sh/capacity-type"] = "on-demand"
+        labels["karpenter.sh/capacity-type"] = "on-demand" if cts is None or cts.random() < 0.5 else "spot"
         labels["kubernetes.io/hostname"] = f"n{k}"
         avail = {"cpu": int(rng.choice([1000, 3000, 6000])), "memory": 8 * GI * 1000, "pods": 20_000}
         b.add_node(f"n{k}", labels, avail, initialized=True)
@@ -655,7 +664,7 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     # a palette of constraints (deployments share them): at most 16 groups
     palette = []
     for _ in range(int(rng.integers(1, 9))):
-        key = "topology.kubernetes.io/zone" if rng.random() < 0.7 else "kubernetes.io/hostname"
+        key = domain_key if rng.random() < 0.7 else "kubernetes.io/hostname"
         tgt = str(rng.choice(APPS[:3]))
         r = rng.random()
         if r < 0.6:
@@ -1054,12 +1063,14 @@ def random_volumes(seed, n_pods=None):
     return b.build()
 
 
-def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None):
+def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None, ct_spreads=False):
     """small adversarial consolidation clusters for the general simulation
     variant: bound and pending pods with zone / hostname topology spread,
     hostname and zone pod anti-affinity (required, preferred, inverse
     carriers), hostname pod affinity, host ports, CSI volumes (shared and
-    per-pod, node attach limits) and NodePools with minValues"""
+    per-pod, node attach limits) and NodePools with minValues.  ct_spreads:
+    the spreads use the capacity-type key instead of the zone (anti-affinity
+    then stays on the hostname key)"""
     rng = np.random.default_rng(0xC0A50000 + seed)
     b = ProblemBuilder()
     zones = FAKE_ZONES[: int(rng.integers(2, 4))]
@@ -1082,12 +1093,14 @@ def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
                        daemon={"cpu": 100, "pods": 1000})
     apps = ["web", "db", "cache"]
-    anti_pal = [{"key": str(rng.choice(["kubernetes.io/hostname", "topology.kubernetes.io/zone"])),
+    dkey = "karpenter.sh/capacity-type" if ct_spreads else "topology.kubernetes.io/zone"
+    anti_keys = ["kubernetes.io/hostname"] * 2 if ct_spreads else ["kubernetes.io/hostname", "topology.kubernetes.io/zone"]
+    anti_pal = [{"key": str(rng.choice(anti_keys)),
                  "required": bool(rng.random() < 0.3), "weight": int(rng.choice([1, 50, 100])),
                  "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(1, 4)))]
     aff_pal = [{"required": bool(rng.random() < 0.3), "weight": 10,
                 "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(0, 2)))]
-    spread_pal = [{"key": str(rng.choice(["topology.kubernetes.io/zone", "kubernetes.io/hostname"])),
+    spread_pal = [{"key": str(rng.choice([dkey, "kubernetes.io/hostname"])),
                    "max_skew": int(rng.choice([1, 2])), "node_affinity_policy": "Ignore",
                    "when": "ScheduleAnyway" if rng.random() < 0.5 else "DoNotSchedule",
                    "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(0, 3)))]

@@ -102,9 +102,68 @@ def test_match_label_keys_split_the_group():
 
 
 def test_refusals():
-    b = _base(n_pods=1, spread={"key": "karpenter.sh/capacity-type", "max_skew": 1, "selector": {}})
+    b = _base(n_pods=1, spread={"key": "karpenter.sh/nodepool", "max_skew": 1, "selector": {}})
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+    # zone and capacity-type spreads in one problem: the product has one
+    # domain key beside the hostname (the oracle computes both)
+    b = _base(n_pods=0)
+    b.add_pod("p0", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+              spreads=[{"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}},
+                       {"key": CT, "max_skew": 1, "selector": {"labels": {"app": "web"}}}])
+    assert pyoracle.solve(b.build())[0] == abi.GS_OK
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+CT = "karpenter.sh/capacity-type"
+
+
+def _ct_case(np_cts, n_pods=6, skew=1, when="DoNotSchedule"):
+    """pods spread over the capacity-type key; NodePools constrain it"""
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=True,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    for j, cts in enumerate(np_cts):
+        b.add_nodepool(f"np{j}", requirements=[(CT, "In", cts)] if cts else [])
+    sp = {"key": CT, "max_skew": skew, "when": when, "selector": {"labels": {"app": "web"}}}
+    for i in range(n_pods):
+        b.add_pod(f"p{i}", i, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    return b.build()
+
+
+def _cts(res):
+    """the capacity types of each NodeClaim's requirement, pods sorted"""
+    out = []
+    for c in res["claims"]:
+        vals = None
+        for line in c["requirements"].split("\n"):
+            f = line.split("|")
+            if f[0] == CT and f[1] == "In":
+                vals = f[2]
+        out.append((sorted(c["pods"]), vals))
+    return sorted(out)
+
+
+def test_capacity_type_spread_balances_over_the_nodepool_domains():
+    """<U> TopologyGroup on karpenter.sh/capacity-type: the domains are the
+    NodePools' In values; maxSkew 1 alternates spot and on-demand claims"""
+    st, res, _ = pyoracle.solve(_ct_case([["spot", "on-demand"]]))
+    assert st == abi.GS_OK and not res["errors"]
+    per = {}
+    for pods, v in _cts(res):
+        per[v] = per.get(v, 0) + len(pods)
+    assert per == {"on-demand": 3, "spot": 3}, per
+    assert lib.validate(_ct_case([["spot", "on-demand"]]))[0] == abi.GS_OK
+    # one capacity type only in the universe: every pod lands there
+    st, res, _ = pyoracle.solve(_ct_case([["on-demand"]]))
+    assert st == abi.GS_OK and not res["errors"] and {v for _, v in _cts(res)} == {"on-demand"}
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_capacity_type_spread_random_accepted(seed):
+    p = synth.random_topology(seed, domain_key=CT)
+    assert pyoracle.solve(p)[0] == abi.GS_OK
+    assert lib.validate(p)[0] == abi.GS_OK
 
 
 # ---------------------------------------------- <U> TopologyNodeFilter (oracle)
@@ -408,6 +467,18 @@ def test_gpu_topology_honor_filter_many_pods(solver, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_gpu_topology_capacity_type_spread(solver, seed):
+    _check(solver, synth.random_topology(seed, domain_key=CT))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_topology_capacity_type_spread_many_pods(solver, seed):
+    _check(solver, synth.random_topology(900 + seed, n_pods=300, domain_key=CT))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(10))
 def test_gpu_topology_random_many_pods(solver, seed):
     _check(solver, synth.random_topology(900 + seed, n_pods=300))
@@ -431,6 +502,9 @@ def test_gpu_topology_kats(solver):
     _check(solver, _family_node_case("Honor"))
     for mind in (None, 2, 5):
         _check(solver, _merge_case(mind))
+    for np_cts in ([["spot", "on-demand"]], [["on-demand"]], [["spot"], ["on-demand"]], [None]):
+        _check(solver, _ct_case(np_cts))
+        _check(solver, _ct_case(np_cts, n_pods=9, skew=2, when="ScheduleAnyway"))
     _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 
