@@ -118,6 +118,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.ZS = e.ZS;
   d.NZV = e.NZV;
   d.dom_ct = e.dom_ct ? 1u : 0u;
+  d.dom_np = e.dom_np ? 1u : 0u;
   d.zknown0 = e.zknown0;
   c->upload(d.tgroups, e.tgroups);
   c->upload(d.tg_list, e.tg_list);

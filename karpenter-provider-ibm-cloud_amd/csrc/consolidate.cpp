@@ -289,7 +289,7 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
       // NodePools' zones plus the zones of the remaining nodes
       std::copy(e.zone_nodes.begin(), e.zone_nodes.end(), zn.begin());
       for (uint32_t n : sp.sets[s]) {
-        const uint32_t z = e.nodes[pos_of[n]].zvid;
+        const uint32_t z = e.nodes[pos_of[n]].dvid;
         if (z < 64) zn[z]--;
       }
       uint64_t k = e.known_np;

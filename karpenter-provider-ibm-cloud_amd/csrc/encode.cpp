@@ -459,6 +459,9 @@ struct Ctx {
     // on instance-type / offering keys, or as integers under Gt/Lt bounds.
     // Any other value behaves exactly like the unmentioned value omega.
     std::set<std::string> label_keys = {kZone, kCapacityType}, bounded;
+    // a NodePool-key spread tells nodes of unknown NodePools apart (domains)
+    for (uint32_t i = 0; i < p->n_spreads; i++)
+      if (normalize(S(p->spreads[i].topology_key)) == kNodePool) label_keys.insert(kNodePool);
     if (p->n_instance_types) {
       auto& it0 = p->instance_types[0];
       chk(it0.requirements, p->n_reqs, "reqs");
@@ -513,10 +516,13 @@ struct Ctx {
     e.k_nodepool = e.key_id[kNodePool];
     // spreads on the capacity-type key move the domain machinery onto it
     // (build_nodes / build_pods swap the zone and capacity-type fields)
-    e.dom_ct = false;
-    for (uint32_t i = 0; i < p->n_spreads; i++)
-      e.dom_ct = e.dom_ct || normalize(S(p->spreads[i].topology_key)) == kCapacityType;
-    e.k_dom = e.dom_ct ? e.k_ct : e.k_zone;
+    e.dom_ct = e.dom_np = false;
+    for (uint32_t i = 0; i < p->n_spreads; i++) {
+      const std::string k = normalize(S(p->spreads[i].topology_key));
+      e.dom_ct = e.dom_ct || k == kCapacityType;
+      e.dom_np = e.dom_np || k == kNodePool;
+    }
+    e.k_dom = e.dom_np ? e.k_nodepool : e.dom_ct ? e.k_ct : e.k_zone;
   }
 
   uint32_t key_of(uint32_t sid) const { return e.key_id.at(normalize(S(sid))); }
@@ -964,10 +970,10 @@ struct Ctx {
       const gs_spread& q = p->spreads[pd.spreads.begin + k];
       SpreadEnc sp;
       sp.key = normalize(S(q.topology_key));
-      if (sp.key != kZone && sp.key != kHostname && sp.key != kCapacityType)
-        throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / capacity type / hostname"};
-      if (e.dom_ct && sp.key == kZone)
-        throw Fail{GS_E_UNSUPPORTED, "topology spreads on both the zone and the capacity-type key"};
+      if (sp.key != kZone && sp.key != kHostname && sp.key != kCapacityType && sp.key != kNodePool)
+        throw Fail{GS_E_UNSUPPORTED, "topology spread key other than zone / capacity type / NodePool / hostname"};
+      if (sp.key != kHostname && sp.key != e.keys[e.k_dom].name)
+        throw Fail{GS_E_UNSUPPORTED, "topology spreads on more than one of the zone, capacity-type and NodePool keys"};
       if (q.max_skew < 1) throw Fail{GS_E_INVALID, "maxSkew < 1"};
       if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE ||
           q.node_taints_policy > GS_POLICY_IGNORE)
@@ -1019,8 +1025,8 @@ struct Ctx {
       if (tk != kHostname && !(tk == kZone && !affinity))
         throw Fail{GS_E_UNSUPPORTED, affinity ? "pod affinity topologyKey other than hostname"
                                               : "pod anti-affinity topologyKey other than hostname / zone"};
-      if (e.dom_ct && tk == kZone)
-        throw Fail{GS_E_UNSUPPORTED, "zone-key pod anti-affinity beside capacity-type topology spreads"};
+      if (e.k_dom != e.k_zone && tk == kZone)
+        throw Fail{GS_E_UNSUPPORTED, "zone-key pod anti-affinity beside capacity-type / NodePool topology spreads"};
       AntiEnc a;
       a.required = q.required != 0;
       a.weight = q.weight;
@@ -1270,7 +1276,9 @@ struct Ctx {
     std::iota(e.zone_order.begin(), e.zone_order.end(), 0);
     std::sort(e.zone_order.begin(), e.zone_order.end(), [&](uint32_t a, uint32_t b) { return zv.vals[a] < zv.vals[b]; });
     e.zone_cat.assign(gsd::ZVMAX, gsd::NONE);
-    if (e.dom_ct) {
+    if (e.dom_np) {
+      // a NodePool domain narrows no catalog zone or capacity type
+    } else if (e.dom_ct) {
       for (uint32_t c = 0; c < e.C; c++)
         if (e.cat_ct[c] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_ct[c]] = c;
     } else {
@@ -1286,9 +1294,9 @@ struct Ctx {
     e.known_np = known_zone;
     e.zone_nodes.assign(gsd::ZVMAX, 0);
     for (auto& nr : e.nodes)
-      if (nr.zvid != gsd::NONE && nr.zvid < e.ZS) {
-        known_zone |= 1ull << nr.zvid;
-        e.zone_nodes[nr.zvid]++;
+      if (nr.dvid != gsd::NONE && nr.dvid < e.ZS) {
+        known_zone |= 1ull << nr.dvid;
+        e.zone_nodes[nr.dvid]++;
       }
     e.zknown0 = known_zone;
     e.tgroups.assign(e.TG, gsd::TGroupRec{});
@@ -1305,6 +1313,23 @@ struct Ctx {
         t.slot = e.TGZ++;
         t.known0 = known_zone;
       }
+    }
+    // <U> Topology.AddRequirements intersects every owned group's domains: two
+    // groups that pick different domains leave an empty requirement, which a
+    // node lacking the domain label passes (strict Compatible: DoesNotExist).
+    // The kernels test each group against the node's own domain instead, so
+    // such a node beside a pod owning two or more zone-count groups is refused
+    if (e.TGZ) {
+      bool lacking = false;
+      for (auto& nr : e.nodes) lacking = lacking || nr.dvid == gsd::NONE;
+      if (lacking)
+        for (auto& pv : e.variants) {
+          uint32_t nz = 0;
+          for (uint32_t g : pv.own) nz += groups[g].sp.key != kHostname;
+          if (nz >= 2)
+            throw Fail{GS_E_UNSUPPORTED, "an existing node lacking the " + e.keys[e.k_dom].name +
+                                             " label beside a pod owning several topology groups on that key"};
+        }
     }
     if (gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH) > 64u * 1024u)
       throw Fail{GS_E_UNSUPPORTED, "topology group state exceeds 64 KiB of LDS (zone groups x zones)"};
@@ -1346,7 +1371,7 @@ struct Ctx {
           e.hn0[(size_t)t.slot * e.NN + pos]++;
           e.htot0[t.slot]++;  // the total over domains (affinity bootstrap)
         } else {
-          const uint32_t z = e.nodes[pos].zvid;
+          const uint32_t z = e.nodes[pos].dvid;
           if (z == gsd::NONE || z >= e.ZS) continue;
           e.zcnt0[(size_t)t.slot * e.ZS + z]++;
           e.zn_cnt[(size_t)t.slot * e.NN + pos]++;
@@ -2443,9 +2468,7 @@ struct Ctx {
         else vr.cfull_off = gsd::NONE;
       }
       vr.fk_count = (uint32_t)e.fk_entries.size() - vr.fk_begin;
-      // dom_ct: the nodes' zvid / cvid are swapped (build_nodes), so are the
-      // existing-node checks' masks
-      if (e.dom_ct) std::swap(vr.zfull_off, vr.cfull_off);
+
     }
     par_for(e.P, 1024, [&](uint32_t i) {
       for (uint32_t v = e.var_begin[i]; v < e.var_begin[i] + e.var_count[i]; v++) {
@@ -2583,7 +2606,7 @@ struct Ctx {
       const gs_node& g = p->nodes[order[pos]];
       gsd::NodeRec& nr = e.nodes[pos];
       for (int k = 0; k < gsd::KMAX_IT; k++) nr.vid[k] = gsd::NONE;
-      nr.zvid = nr.cvid = gsd::NONE;
+      nr.zvid = nr.cvid = nr.dvid = gsd::NONE;
       Reqs reqs = node_labels_reqs(g.labels);
       uint32_t hk = e.k_hostname;
       reqs_add(e, reqs, hk, in_one_or_omega(hk, S(g.name)));
@@ -2602,7 +2625,13 @@ struct Ctx {
         else if (key.cls == KEY_ZONE) nr.zvid = vid;
         else nr.cvid = vid;
       }
-      if (e.dom_ct) std::swap(nr.zvid, nr.cvid);  // zvid: the topology domain's value
+      {
+        // the topology domain key's value (zone, capacity type or NodePool)
+        auto fd = reqs.find(e.k_dom);
+        if (fd != reqs.end())
+          for (size_t i = 0; i < e.keys[e.k_dom].vocab.size(); i++)
+            if (fd->second.has.test(i)) nr.dvid = (uint32_t)i;
+      }
       for (uint32_t k : exempt_keys) {
         bool has = reqs.count(k) != 0;
         if (!has)

@@ -96,7 +96,7 @@ struct Encoded {
   // capacity type when the problem's spreads use that key (dom_ct; the
   // kernels then narrow a NodeClaim's catalog capacity types, not zones)
   uint32_t k_dom = gsd::NONE;
-  bool dom_ct = false;
+  bool dom_ct = false, dom_np = false;
   std::vector<uint32_t> it_keys;    // key ids, IT key order
   std::vector<uint32_t> free_keys;  // key ids, free slot order
   std::vector<uint32_t> cat_zone;   // catalog zone id -> vocab id

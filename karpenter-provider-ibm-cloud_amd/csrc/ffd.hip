@@ -723,7 +723,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             const uint32_t g = (uint32_t)(en >> 32);
             const int32_t c = (int32_t)(uint32_t)en;
             if (g < d.TGZ) {
-              const uint32_t z = d.nodes0[n].zvid;
+              const uint32_t z = d.nodes0[n].dvid;
               if (z < d.ZS) atomicSub(&ts.zcnt[g * d.ZS + z], c);
             } else {
               atomicSub(&ts.htot[g - d.TGZ], c);
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               feas = nr.cvid != NONE && ((d.itmask[vr.cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && vr.fk_count) feas = var_fk_ok_strict(d, vr, nfk);
             if (TOPO && feas && own_n)
-              feas = topo_node_ok_g(d, ts, own_n, nr.zvid, [&](uint32_t hs) -> int64_t {
+              feas = topo_node_ok_g(d, ts, own_n, nr.dvid, [&](uint32_t hs) -> int64_t {
                 if (!SIM) return d.hn[(size_t)hs * d.NN + n];
                 // an overlay cell counts only where this simulation wrote it
                 // (its stamp); other groups keep the node's base count
@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
             S.found = 1;
             // <U> Topology.Record: the node's labels are single domains
             if (TOPO && sel_n) {
-              const uint32_t z = d.nodes0[fn].zvid;
+              const uint32_t z = d.nodes0[fn].dvid;
               topo_record(d, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u, [&](uint32_t hs) {
                 if (SIM) {
                   // copy-on-write per group: the first count this simulation
@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
                 // the domains narrow the catalog zones, or (dom_ct) capacity types
                 const uint64_t dcat = topo_catmask(dd, zset);
                 if (dd.dom_ct) cm &= dcat;
-                else zm &= dcat;
+                else if (!dd.dom_np) zm &= dcat;
               }
             }
             if (pre) {
@@ -1627,15 +1627,16 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
         if (TOPO && own_n) {
           tzs = topo_claim_g(d, ts, own_n, tr.zfull & vr.zn, [](uint32_t) -> int64_t { return 0; }, OWN);
-          if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(d, tzs);
+          if (tzs != 0 && tzs != ~0ull && !d.dom_np) tzcat = topo_catmask(d, tzs);
           if (tzs == 0 || tzcat == 0) continue;
         }
         // dom_ct: the picked domains are capacity types of the template's zones
         const bool dct = d.dom_ct != 0;
         const uint64_t tcm = tr.cm & vr.cm & (dct ? tzcat : ~0ull), tzsel = dct ? tr.zm & vr.zm : tzcat;
+        const bool dnp = d.dom_np != 0;  // a NodePool domain narrows no offering
         auto rowx = [&](uint32_t w) -> uint64_t {
           uint64_t x = row[w];
-          if (tzs != ~0ull) {
+          if (tzs != ~0ull && !dnp) {
             uint64_t off = 0;
             for (uint64_t zm_ = tzsel; zm_; zm_ &= zm_ - 1) {
               const uint32_t zc = (uint32_t)__ffsll((long long)zm_) - 1u;

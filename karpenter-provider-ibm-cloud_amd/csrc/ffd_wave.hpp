@@ -1638,7 +1638,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               feas = nr.cvid != NONE && ((KD.itmask[cfull_off + (nr.cvid >> 6)] >> (nr.cvid & 63)) & 1);
             if (feas && fk_count) feas = fk_ok_range(d, fk_begin, fk_count, nfk, true);
             if (TOPO && feas && own_n)
-              feas = topo_node_ok_g(KD, ts, own_n, nr.zvid,
+              feas = topo_node_ok_g(KD, ts, own_n, nr.dvid,
                                     [&](uint32_t hs) -> int64_t { return KD.hn[(size_t)hs * KD.NN + n]; }, OWN);
             if (TOPO && feas && KD.any_vol) {
               // ExceedsLimits: distinct volumes per driver after the union
@@ -1687,7 +1687,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           s_nrm[fn] = rm2;
           // <U> Topology.Record in the groups that select the pod
           if (TOPO && sel_n) {
-            const uint32_t z = KD.nodes0[fn].zvid;
+            const uint32_t z = KD.nodes0[fn].dvid;
             topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
                         [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
           }
@@ -1747,7 +1747,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
           // <U> Topology.Record: the node's labels are single domains
           if (TOPO && sel_n) {
-            const uint32_t z = KD.nodes0[fn].zvid;
+            const uint32_t z = KD.nodes0[fn].dvid;
             topo_record(KD, ts, sel_off, sel_n, z < 64u ? 1ull << z : 0ull, 0u,
                         [&](uint32_t hs) { KD.hn[(size_t)hs * KD.NN + fn]++; });
           }
@@ -2062,7 +2062,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             // the domains narrow the catalog zones, or (dom_ct) capacity types
             const uint64_t dcat = topo_catmask(KD, zset);
             if (KD.dom_ct) cm &= dcat;
-            else zm &= dcat;
+            else if (!KD.dom_np) zm &= dcat;
           }
         }
         if (pre) {
@@ -2382,7 +2382,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       uint64_t tzs = ~0ull, tzcat = ~0ull;  // allowed zone domains / their catalog zones
       if (TOPO && own_n) {
         tzs = topo_claim_g(KD, ts, own_n, tr.zfull & vzn, [](uint32_t) -> int64_t { return 0; }, OWN);
-        if (tzs != 0 && tzs != ~0ull) tzcat = topo_catmask(KD, tzs);
+        if (tzs != 0 && tzs != ~0ull && !KD.dom_np) tzcat = topo_catmask(KD, tzs);
         tzs = (uint64_t)uniform_i64((int64_t)tzs);
         tzcat = (uint64_t)uniform_i64((int64_t)tzcat);
         if (tzs == 0 || tzcat == 0) continue;
@@ -2390,9 +2390,10 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       // dom_ct: the picked domains are capacity types of the template's zones
       const bool dct = KD.dom_ct != 0;
       const uint64_t tcm = tr.cm & vcm & (dct ? tzcat : ~0ull), tzsel = dct ? tr.zm & vzm : tzcat;
+      const bool dnp = KD.dom_np != 0;  // a NodePool domain narrows no offering
       auto rowx = [&](uint32_t w) -> uint64_t {
         uint64_t x = row[w];
-        if (tzs != ~0ull) {
+        if (tzs != ~0ull && !dnp) {
           uint64_t off = 0;
           for (uint64_t zm_ = tzsel; zm_; zm_ &= zm_ - 1) {
             const uint32_t zc = ffs64(zm_);

@@ -178,6 +178,7 @@ struct NodeRec {
   uint32_t zvid, cvid;   // zone / capacity-type label value ids (NONE = unlabeled)
   uint32_t vid[KMAX_IT]; // instance-type-key label value ids (NONE = unlabeled)
   uint32_t init;         // StateNode.Initialized()
+  uint32_t dvid;         // the topology domain key's label value id (zone, capacity type or NodePool)
 };
 
 // <U> VolumeUsage of an existing node over the CSI drivers that pending pods
@@ -327,6 +328,7 @@ struct DevProblem {
   uint32_t TG, TGH, NZV;       // groups, hostname groups, zone vocabulary size
   uint32_t TGZ, ZS;            // zone groups, zone-count stride (max(NZV, 1))
   uint32_t dom_ct;             // the "zone" groups' domain key is the capacity type (zone_cat -> catalog capacity types)
+  uint32_t dom_np;             // ... is the NodePool (a template's fixed domain: no catalog narrowing)
   uint32_t pad_tg;
   uint64_t zknown0;            // zone domains known before the Solve (universe + counted), every zone group
   const TGroupRec* tgroups;    // [TG]

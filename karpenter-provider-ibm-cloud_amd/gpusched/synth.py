@@ -619,10 +619,13 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     carry two zone In terms instead (OR; relaxation drops the first).
     domain_key "karpenter.sh/capacity-type": the non-hostname spreads use
     that key, NodePools constrain it and nodes carry spot / on-demand (those
-    draws come from their own stream)"""
+    draws come from their own stream); "karpenter.sh/nodepool": nodes carry
+    NodePool labels (np0..np2, some of no NodePool of the problem; a node
+    lacking the label beside multi-group owners is refused)"""
     rng = np.random.default_rng(seed)
     ctk = "karpenter.sh/capacity-type"
     cts = np.random.default_rng(seed + 0xC7) if domain_key == ctk else None
+    nps = np.random.default_rng(seed + 0xD7) if domain_key == "karpenter.sh/nodepool" else None
     b = ProblemBuilder()
     zones = ["z1", "z2", "z3", "z4"][: int(rng.integers(2, 5))]
     profs = []
@@ -655,6 +658,8 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
         labels["topology.kubernetes.io/zone"] = str(rng.choice(zones + ["z9"]))
         labels["karpenter.sh/capacity-type"] = "on-demand" if cts is None or cts.random() < 0.5 else "spot"
         labels["kubernetes.io/hostname"] = f"n{k}"
+        if nps is not None:
+            labels["karpenter.sh/nodepool"] = f"np{int(nps.integers(0, 3))}"
         avail = {"cpu": int(rng.choice([1000, 3000, 6000])), "memory": 8 * GI * 1000, "pods": 20_000}
         b.add_node(f"n{k}", labels, avail, initialized=True)
         for q in range(int(rng.integers(0, 4))):
@@ -1063,14 +1068,15 @@ def random_volumes(seed, n_pods=None):
     return b.build()
 
 
-def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None, ct_spreads=False):
+def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None, ct_spreads=False,
+                                 np_spreads=False):
     """small adversarial consolidation clusters for the general simulation
     variant: bound and pending pods with zone / hostname topology spread,
     hostname and zone pod anti-affinity (required, preferred, inverse
     carriers), hostname pod affinity, host ports, CSI volumes (shared and
     per-pod, node attach limits) and NodePools with minValues.  ct_spreads:
     the spreads use the capacity-type key instead of the zone (anti-affinity
-    then stays on the hostname key)"""
+    then stays on the hostname key); np_spreads: the NodePool key"""
     rng = np.random.default_rng(0xC0A50000 + seed)
     b = ProblemBuilder()
     zones = FAKE_ZONES[: int(rng.integers(2, 4))]
@@ -1093,8 +1099,9 @@ def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
                        daemon={"cpu": 100, "pods": 1000})
     apps = ["web", "db", "cache"]
-    dkey = "karpenter.sh/capacity-type" if ct_spreads else "topology.kubernetes.io/zone"
-    anti_keys = ["kubernetes.io/hostname"] * 2 if ct_spreads else ["kubernetes.io/hostname", "topology.kubernetes.io/zone"]
+    dkey = ("karpenter.sh/capacity-type" if ct_spreads else "karpenter.sh/nodepool" if np_spreads
+            else "topology.kubernetes.io/zone")
+    anti_keys = ["kubernetes.io/hostname"] * 2 if ct_spreads or np_spreads else ["kubernetes.io/hostname", "topology.kubernetes.io/zone"]
     anti_pal = [{"key": str(rng.choice(anti_keys)),
                  "required": bool(rng.random() < 0.3), "weight": int(rng.choice([1, 50, 100])),
                  "selector": {"labels": {"app": str(rng.choice(apps))}}} for _ in range(int(rng.integers(1, 4)))]

@@ -778,8 +778,8 @@ struct Builder {
       const gs_spread& q = p->spreads[g.spreads.begin + k];
       Spread sp;
       sp.key = normalize_key(str(q.topology_key));
-      if (sp.key != kZone && sp.key != kHostname && sp.key != kCapacityType)
-        throw Unsupported{GS_E_UNSUPPORTED, "topology spread key other than zone / capacity type / hostname"};
+      if (sp.key != kZone && sp.key != kHostname && sp.key != kCapacityType && sp.key != kNodePool)
+        throw Unsupported{GS_E_UNSUPPORTED, "topology spread key other than zone / capacity type / NodePool / hostname"};
       if (q.max_skew < 1) throw Unsupported{GS_E_INVALID, "maxSkew < 1"};
       if (q.when_unsatisfiable > GS_SPREAD_SCHEDULE_ANYWAY || q.node_affinity_policy > GS_POLICY_IGNORE ||
           q.node_taints_policy > GS_POLICY_IGNORE)

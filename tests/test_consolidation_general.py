@@ -116,6 +116,14 @@ def test_gpu_consolidation_capacity_type_spread(solver, seed, mode):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(24))
 @pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
+def test_gpu_consolidation_nodepool_spread(solver, seed, mode):
+    """spreads on the NodePool key in kept and candidate nodes' pods"""
+    check(solver, synth.random_consolidation_general(seed, np_spreads=True), mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("mode", [abi.CONSOLIDATE_SINGLE, abi.CONSOLIDATE_MULTI])
 def test_gpu_consolidation_honor_filter(solver, seed, mode):
     """spreads with nodeAffinityPolicy Honor on instance family / type: the
     kept nodes' bound pods count only where the node matches the filter"""

@@ -102,7 +102,7 @@ def test_match_label_keys_split_the_group():
 
 
 def test_refusals():
-    b = _base(n_pods=1, spread={"key": "karpenter.sh/nodepool", "max_skew": 1, "selector": {}})
+    b = _base(n_pods=1, spread={"key": "karpenter-ibm.sh/instance-family", "max_skew": 1, "selector": {}})
     assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
     assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
     # zone and capacity-type spreads in one problem: the product has one
@@ -157,6 +157,67 @@ def test_capacity_type_spread_balances_over_the_nodepool_domains():
     # one capacity type only in the universe: every pod lands there
     st, res, _ = pyoracle.solve(_ct_case([["on-demand"]]))
     assert st == abi.GS_OK and not res["errors"] and {v for _, v in _cts(res)} == {"on-demand"}
+
+
+NP = "karpenter.sh/nodepool"
+
+
+def _np_case(n_pools=2, n_pods=6, node_pool=None):
+    """pods spread over the NodePool key (a NodeClaim's domain is its
+    template's NodePool; the universe is the NodePools and labelled nodes)"""
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    for j in range(n_pools):
+        b.add_nodepool(f"np{j}", weight=10 * (n_pools - j))
+    if node_pool is not None:
+        b.add_node("n0", {Z: "us-south-1", H: "n0", NP: node_pool}, {"cpu": 0, "memory": 0, "pods": 0})
+        for q in range(2):
+            b.add_bound_pod(0, f"b{q}", 0, {"cpu": 1}, labels={"app": "web"})
+    sp = {"key": NP, "max_skew": 1, "selector": {"labels": {"app": "web"}}}
+    for i in range(n_pods):
+        b.add_pod(f"p{i}", i, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    return b.build()
+
+
+def test_nodepool_spread_balances_over_nodepools():
+    """the heavier NodePool alone would take every pod; maxSkew 1 over the
+    NodePool key alternates the two (and counts a labelled node's pods)"""
+    st, res, _ = pyoracle.solve(_np_case())
+    assert st == abi.GS_OK and not res["errors"]
+    per = {}
+    for c in res["claims"]:
+        per[c["nodepool"]] = per.get(c["nodepool"], 0) + len(c["pods"])
+    assert sorted(per.values()) == [3, 3], per
+    assert lib.validate(_np_case())[0] == abi.GS_OK
+    st, res, _ = pyoracle.solve(_np_case(node_pool="np0"))
+    per = {}
+    for c in res["claims"]:
+        per[c["nodepool"]] = per.get(c["nodepool"], 0) + len(c["pods"])
+    assert st == abi.GS_OK and sorted(per.values()) == [2, 4], per
+
+
+def test_unlabeled_node_beside_multi_group_owner_refused():
+    """two NodePool-key groups that pick different domains leave an empty
+    requirement, which upstream lets a node lacking the label pass: the
+    product refuses that input (one group per pod is exact)"""
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("np0")
+    b.add_nodepool("np1")
+    b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 8000, "memory": 32 << 30, "pods": 20000})
+    two = [{"key": NP, "max_skew": 1, "selector": {"labels": {"app": a}}} for a in ("web", "api")]
+    b.add_pod("p0", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=two)
+    assert pyoracle.solve(b.build())[0] == abi.GS_OK
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_nodepool_spread_random_accepted(seed):
+    p = synth.random_topology(seed, domain_key=NP)
+    assert pyoracle.solve(p)[0] == abi.GS_OK
+    assert lib.validate(p)[0] == abi.GS_OK
 
 
 @pytest.mark.parametrize("seed", range(60))
@@ -473,6 +534,18 @@ def test_gpu_topology_capacity_type_spread(solver, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_gpu_topology_nodepool_spread(solver, seed):
+    _check(solver, synth.random_topology(seed, domain_key=NP))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_topology_nodepool_spread_many_pods(solver, seed):
+    _check(solver, synth.random_topology(900 + seed, n_pods=300, domain_key=NP))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(4))
 def test_gpu_topology_capacity_type_spread_many_pods(solver, seed):
     _check(solver, synth.random_topology(900 + seed, n_pods=300, domain_key=CT))
@@ -505,6 +578,8 @@ def test_gpu_topology_kats(solver):
     for np_cts in ([["spot", "on-demand"]], [["on-demand"]], [["spot"], ["on-demand"]], [None]):
         _check(solver, _ct_case(np_cts))
         _check(solver, _ct_case(np_cts, n_pods=9, skew=2, when="ScheduleAnyway"))
+    for npools, node_pool in ((2, None), (2, "np0"), (3, "np1"), (1, "other")):
+        _check(solver, _np_case(npools, node_pool=node_pool))
     _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 

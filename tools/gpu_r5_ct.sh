@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r5_ct
 mkdir -p $O
 cd $R
-timeout -k 10 700 python -u -m pytest tests/test_topology.py tests/test_consolidation_general.py tests/test_consolidation.py tests/test_affinity.py tests/test_zone_anti_affinity.py tests/test_e2e_scenarios.py tests/test_gpu_parity.py tests/test_node_labels.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_topology.py tests/test_consolidation_general.py tests/test_consolidation.py tests/test_affinity.py tests/test_zone_anti_affinity.py tests/test_e2e_scenarios.py tests/test_gpu_parity.py tests/test_node_labels.py tests/test_startup_taints.py tests/test_run_mode.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py -m gpu -x -q -k "c3 or cm" --timeout 300 --timeout-method thread > $O/tests_full.log 2>&1
 rc=$?; tail -2 $O/tests_full.log; [ $rc -eq 0 ] || exit $rc
