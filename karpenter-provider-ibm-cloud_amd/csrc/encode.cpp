@@ -1294,7 +1294,7 @@ struct Ctx {
     e.known_np = known_zone;
     e.zone_nodes.assign(gsd::ZVMAX, 0);
     for (auto& nr : e.nodes)
-      if (nr.dvid != gsd::NONE && nr.dvid < e.ZS) {
+      if (nr.dvid < e.ZS) {
         known_zone |= 1ull << nr.dvid;
         e.zone_nodes[nr.dvid]++;
       }
@@ -1321,7 +1321,7 @@ struct Ctx {
     // such a node beside a pod owning two or more zone-count groups is refused
     if (e.TGZ) {
       bool lacking = false;
-      for (auto& nr : e.nodes) lacking = lacking || nr.dvid == gsd::NONE;
+      for (auto& nr : e.nodes) lacking = lacking || nr.dvid == gsd::DVID_NONE;
       if (lacking)
         for (auto& pv : e.variants) {
           uint32_t nz = 0;
@@ -2606,7 +2606,8 @@ struct Ctx {
       const gs_node& g = p->nodes[order[pos]];
       gsd::NodeRec& nr = e.nodes[pos];
       for (int k = 0; k < gsd::KMAX_IT; k++) nr.vid[k] = gsd::NONE;
-      nr.zvid = nr.cvid = nr.dvid = gsd::NONE;
+      nr.zvid = nr.cvid = gsd::NONE;
+      nr.dvid = gsd::DVID_NONE;
       Reqs reqs = node_labels_reqs(g.labels);
       uint32_t hk = e.k_hostname;
       reqs_add(e, reqs, hk, in_one_or_omega(hk, S(g.name)));
@@ -2630,7 +2631,7 @@ struct Ctx {
         auto fd = reqs.find(e.k_dom);
         if (fd != reqs.end())
           for (size_t i = 0; i < e.keys[e.k_dom].vocab.size(); i++)
-            if (fd->second.has.test(i)) nr.dvid = (uint32_t)i;
+            if (fd->second.has.test(i)) nr.dvid = (uint16_t)i;
       }
       for (uint32_t k : exempt_keys) {
         bool has = reqs.count(k) != 0;

@@ -177,9 +177,10 @@ struct NodeRec {
   uint32_t ok;           // 0 if any available quantity is negative (never fits)
   uint32_t zvid, cvid;   // zone / capacity-type label value ids (NONE = unlabeled)
   uint32_t vid[KMAX_IT]; // instance-type-key label value ids (NONE = unlabeled)
-  uint32_t init;         // StateNode.Initialized()
-  uint32_t dvid;         // the topology domain key's label value id (zone, capacity type or NodePool)
+  uint16_t init;         // StateNode.Initialized()
+  uint16_t dvid;         // the topology domain key's label value id (zone, capacity type or NodePool; DVID_NONE)
 };
+constexpr uint16_t DVID_NONE = 0xFFFFu;
 
 // <U> VolumeUsage of an existing node over the CSI drivers that pending pods
 // use (<= VDMAX): which of the pending pods' volumes (<= 64) it already
