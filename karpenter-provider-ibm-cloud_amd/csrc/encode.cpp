@@ -944,6 +944,7 @@ struct Ctx {
     AntiEnc anti;
     std::string inv_hash;
     PortEnc port;
+    uint32_t owner_spec = gsd::NONE;  // spread groups: the first owner's spec
   };
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
@@ -1314,6 +1315,44 @@ struct Ctx {
         t.known0 = known_zone;
       }
     }
+    // <U> TopologyDomainGroup.ForEachDomain under TaintPolicy Honor: a domain
+    // enters domainMinCount only if a NodePool (with instance types) or a node
+    // providing it has taints the pod (this relaxation) tolerates.  Folded into
+    // the variant's strict domains, which only the minimum reads (topo_tmin)
+    {
+      bool any_honor = false;
+      for (auto& g : groups) any_honor = any_honor || (g.kind == 0 && g.sp.honor_taints && g.sp.key != kHostname);
+      if (any_honor) {
+        std::vector<std::pair<uint64_t, uint64_t>> prov;  // (taint classes, domains)
+        for (size_t i = 0; i < np_universe.size(); i++) {
+          if (!np_universe[i].second) continue;
+          auto f = np_universe[i].first.find(e.k_dom);
+          if (f == np_universe[i].first.end() || f->second.comp) continue;
+          uint64_t cm = 0;
+          for (uint32_t id : np_universe_taints[i]) cm |= 1ull << taint_cls[id];
+          prov.emplace_back(cm, f->second.has.w[0]);
+        }
+        for (auto& nr : e.nodes)
+          if (nr.dvid < e.ZS) prov.emplace_back(nr.taints, 1ull << nr.dvid);
+        for (uint32_t v = 0; v < e.V; v++) {
+          const uint32_t sv = e.var_sv[v];
+          uint32_t nh = 0, ni = 0;
+          for (uint32_t g : e.variants[sv].own)
+            if (groups[g].kind == 0 && groups[g].sp.key != kHostname) (groups[g].sp.honor_taints ? nh : ni)++;
+          if (!nh) continue;
+          if (ni)
+            throw Fail{GS_E_UNSUPPORTED, "a pod owning zone-key spreads with both nodeTaintsPolicy Honor and Ignore"};
+          // a domain no NodePool or node provides (one a Record adds during
+          // the Solve) has no taints to tolerate: it stays
+          uint64_t dm = 0, provided = 0;
+          for (auto& pr : prov) {
+            provided |= pr.second;
+            if ((pr.first & ~final_sv_tol[sv]) == 0) dm |= pr.second;
+          }
+          e.vars[v].zs &= dm | ~provided;
+        }
+      }
+    }
     // <U> Topology.AddRequirements intersects every owned group's domains: two
     // groups that pick different domains leave an empty requirement, which a
     // node lacking the domain label passes (strict Compatible: DoesNotExist).
@@ -1356,6 +1395,22 @@ struct Ctx {
         if (reqs_compatible(e, *nreqs[raw], f, false)) return true;
       return false;
     };
+    // nodeTaintsPolicy Honor: the group's first owner's tolerations (before
+    // Relax) against a bound pod's Node taints in countDomains, and its
+    // tolerated taint classes for the counted specs below
+    std::vector<uint64_t> g_otol(e.TG, ~0ull);
+    for (uint32_t g = 0; g < e.TG; g++)
+      if (groups[g].kind == 0 && groups[g].sp.honor_taints) g_otol[g] = final_sv_tol[sv_begin[groups[g].owner_spec]];
+    auto node_tolerated = [&](uint32_t g, uint32_t raw) {
+      const std::vector<Tol>& tols = variant_tols[sv_begin[groups[g].owner_spec]];
+      const gs_range r = p->nodes[raw].taints;
+      chk(r, p->n_taints, "taints");
+      for (uint32_t k = 0; k < r.count; k++) {
+        const gs_taint& t = p->taints[r.begin + k];
+        if (!tolerated(tols, TaintKey{S(t.key), S(t.value), S(t.effect)})) return false;
+      }
+      return true;
+    };
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
       const gs_pod& bp = p->bound_pods[b];
       if (p->bound_pod_node[b] >= e.NN) throw Fail{GS_E_INVALID, "bound pod node out of range"};
@@ -1366,6 +1421,7 @@ struct Ctx {
         if (!group_counts(groups[g], ps)) continue;
         if (groups[g].kind == 0 && groups[g].sp.strict_aff && !node_matches(groups[g].sp, p->bound_pod_node[b]))
           continue;
+        if (groups[g].kind == 0 && groups[g].sp.honor_taints && !node_tolerated(g, p->bound_pod_node[b])) continue;
         gsd::TGroupRec& t = e.tgroups[g];
         if (t.kind & gsd::TK_HOST) {
           e.hn0[(size_t)t.slot * e.NN + pos]++;
@@ -1392,6 +1448,16 @@ struct Ctx {
       mine.clear();
       for (uint32_t g : cand)
         if (group_counts(groups[g], pod_sel[s])) mine.push_back(g);
+      for (uint32_t g : mine) {
+        // taint Honor: every NodeClaim / node a counted pod can land on (it
+        // tolerates the taints) must be one the owner tolerates, in every
+        // relaxation of the pod (Relax may add the PreferNoSchedule toleration)
+        if (groups[g].kind == 0 && groups[g].sp.honor_taints)
+          for (uint32_t sv = sv_begin[s]; sv < sv_begin[s] + sv_count[s]; sv++)
+            if (final_sv_tol[sv] & ~g_otol[g])
+              throw Fail{GS_E_UNSUPPORTED, "a pod counted by a topology spread (nodeTaintsPolicy Honor) tolerating a "
+                                           "taint its owner does not"};
+      }
       for (uint32_t g : mine) {
         const SpreadEnc& sp = groups[g].sp;
         if (groups[g].kind != 0 || !sp.strict_aff) continue;
@@ -1583,9 +1649,12 @@ struct Ctx {
     }
     for (size_t sv = 0; sv < NSV; sv++) e.variants[sv].tol = sv_tol[sv];
     final_sv_tol = std::move(sv_tol);
+    taint_cls = cls;
   }
   uint32_t n_taint_classes = 0;
   std::vector<uint64_t> final_sv_tol;
+  std::vector<uint32_t> taint_cls;                        // taint id -> class (build_taint_classes)
+  std::vector<std::vector<uint32_t>> np_universe_taints;  // per np_universe entry: its taint ids
 
   // --------------------------------------------------------- templates
   bool tolerate_pns = false;
@@ -1650,6 +1719,7 @@ struct Ctx {
       }
       std::vector<uint32_t> tm = taint_ids(np.taints);
       np_universe.emplace_back(tr, has_its);
+      np_universe_taints.push_back(tm);
       // <U> minValues (Strict): NewScheduler's filterInstanceTypesByRequirements
       // drops the NodePool when its options miss a minimum.  Instance types
       // carry no value for a key outside the IT keys (Values() is empty).
@@ -2078,6 +2148,7 @@ struct Ctx {
           f = group_idx.emplace(w.sp_hash[k], (uint32_t)groups.size()).first;
           if (!w.sp_merge[k].empty()) merge_idx.emplace(w.sp_merge[k], (uint32_t)groups.size());
           groups.push_back(GroupEnc{w.sps[k], pns});
+          groups.back().owner_spec = spec_of[i];
         }
       } else if (!w.sps[k].ignore_aff && groups[f->second].sp.ftext != w.sps[k].ftext) {
         // upstream keys the group by the filter's keys and keeps its first
@@ -2655,10 +2726,7 @@ struct Ctx {
     // nodeTaintsPolicy Honor: the group's filter holds the owner's own
     // tolerations (before Relax adds PreferNoSchedule); tolerating every
     // NodePool and node taint makes TopologyNodeFilter.Matches always true
-    const uint64_t all_taints = n_taint_classes >= 64 ? ~0ull : (1ull << n_taint_classes) - 1;
-    for (uint32_t s : honor_specs)
-      if (all_taints & ~sv_tol[sv_begin[s]])
-        throw Fail{GS_E_UNSUPPORTED, "nodeTaintsPolicy Honor with a taint its owner does not tolerate"};
+    (void)sv_tol;  // nodeTaintsPolicy Honor: applied in build_topology
   }
 };
 

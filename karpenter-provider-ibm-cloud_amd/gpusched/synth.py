@@ -605,7 +605,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False, par
 
 
 def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore", multi_term=False,
-                    domain_key="topology.kubernetes.io/zone"):
+                    domain_key="topology.kubernetes.io/zone", tol_by_app=False):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
@@ -619,7 +619,9 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
     carry two zone In terms instead (OR; relaxation drops the first).
     domain_key "karpenter.sh/capacity-type": the non-hostname spreads use
     that key, NodePools constrain it and nodes carry spot / on-demand (those
-    draws come from their own stream); "karpenter.sh/nodepool": nodes carry
+    draws come from their own stream).  tol_by_app (with taint_policy): each
+    app's pods tolerate the NodePools' taint or not, as a whole, so Honor
+    groups see intolerable NodePools and nodes; "karpenter.sh/nodepool": nodes carry
     NodePool labels (np0..np2, some of no NodePool of the problem; a node
     lacking the label beside multi-group owners is refused)"""
     rng = np.random.default_rng(seed)
@@ -688,6 +690,7 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
             sp["match_label_keys"] = ["pod-template-hash"] + (["absent-key"] if rng.random() < 0.3 else [])
         palette.append(sp)
     side = np.random.default_rng(seed + 0x7A11)
+    tol_apps = {str(a) for a in np.random.default_rng(seed + 0x70A).choice(APPS[:3], size=2, replace=False)}
     avoid = str(side.choice(zones))
     two = [str(z) for z in side.choice(zones, size=2, replace=False)]
     n = int(n_pods if n_pods is not None else rng.integers(1, 40))
@@ -717,6 +720,8 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
             tols = [("dedicated", "Exists", "", "")]
             for sp in spreads:
                 sp["node_taints_policy"] = taint_policy
+        if taint_policy and tol_by_app:
+            tols = [("dedicated", "Exists", "", "")] if app in tol_apps else []
         labels = {"app": app}
         if rng.random() < 0.6:
             labels["pod-template-hash"] = str(rng.choice(["h1", "h2"]))

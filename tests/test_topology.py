@@ -260,7 +260,7 @@ def test_filter_taint_honor_drops_intolerable_node():
     p = _tainted_node_case("Honor")
     st, res, _ = pyoracle.solve(p)
     assert st == abi.GS_OK and _zones(res) == [([0], "us-south-1"), ([1], "us-south-2")]
-    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(p)[0] == abi.GS_OK  # applied by the product too (GPU: test_gpu_topology_kats)
 
 
 def _family_node_case(pol):
@@ -337,7 +337,33 @@ def test_filter_taint_honor_drops_intolerable_domain_from_minimum():
     assert st == abi.GS_OK and not res["errors"]
     assert sorted(z for pods, z in _zones(res) for _ in pods) == ["us-south-1", "us-south-1", "us-south-2",
                                                                   "us-south-2"]
-    assert lib.validate(p)[0] == abi.GS_E_UNSUPPORTED
+    assert lib.validate(p)[0] == abi.GS_OK  # applied by the product too (GPU: test_gpu_topology_kats)
+
+
+def test_taint_honor_counted_pod_tolerating_more_than_owner_refused():
+    """a counted pod that tolerates a taint the owner does not may land where
+    upstream does not count it: refused (the oracle computes it)"""
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_taints_policy": "Honor"}
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("a", taints=[("dedicated", "x", "NoSchedule")])
+    b.add_nodepool("b")
+    b.add_pod("p0", 0, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    b.add_pod("p1", 1, {"cpu": 1500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"},
+              tolerations=[("dedicated", "Exists", "", "")])
+    assert pyoracle.solve(b.build())[0] == abi.GS_OK
+    assert lib.validate(b.build())[0] == abi.GS_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_taint_policy_honor_by_app_accepted_or_refused(seed):
+    """apps tolerating the NodePools' taint or not: the oracle computes every
+    problem; the product accepts it or refuses the counted-pod case"""
+    p = synth.random_topology(seed, taint_policy="Honor", tol_by_app=True)
+    assert pyoracle.solve(p)[0] == abi.GS_OK
+    st, msg = lib.validate(p)
+    assert st == abi.GS_OK or "tolerating a taint its owner does not" in msg
 
 
 def _shared_group_case(zones_per_pod, pol="Honor"):
@@ -534,6 +560,15 @@ def test_gpu_topology_capacity_type_spread(solver, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(60))
+def test_gpu_topology_taint_honor_by_app(solver, seed):
+    p = synth.random_topology(seed, taint_policy="Honor", tol_by_app=True)
+    if lib.validate(p)[0] != abi.GS_OK:
+        pytest.skip("refused (counted pod tolerating more than its owner)")
+    _check(solver, p)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(40))
 def test_gpu_topology_nodepool_spread(solver, seed):
     _check(solver, synth.random_topology(seed, domain_key=NP))
@@ -580,6 +615,8 @@ def test_gpu_topology_kats(solver):
         _check(solver, _ct_case(np_cts, n_pods=9, skew=2, when="ScheduleAnyway"))
     for npools, node_pool in ((2, None), (2, "np0"), (3, "np1"), (1, "other")):
         _check(solver, _np_case(npools, node_pool=node_pool))
+    _check(solver, _tainted_node_case("Honor"))
+    _check(solver, _tainted_pool_case("Honor"))
     _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 
