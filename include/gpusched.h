@@ -694,6 +694,11 @@ uint32_t gs_abi_sizes(uint32_t* out, uint32_t n);
 
 size_t gs_last_error(const gs_ctx* ctx, char* buf, size_t len);
 const char* gs_version(void);
+/* the first 16 hex digits of the sha256 of the library's sources
+ * (karpenter-provider-ibm-cloud_amd/csrc/Makefile SRC_SHA): a binding or a
+ * test compares it with the tree it ships with, so a stale prebuilt library
+ * is caught before it runs */
+const char* gs_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,31 @@ LIB_PATH = os.path.join(HERE, os.environ.get("GPUSCHED_LIB", "libgpusched.so"))
 EXPORTS = ["gs_create", "gs_destroy", "gs_prepare", "gs_run", "gs_fetch", "gs_solve", "gs_feasibility",
            "gs_last_error", "gs_version", "gs_validate", "gs_abi_sizes", "gs_last_run_ms",
            "gs_consolidate", "gs_consolidate_rerun", "gs_consolidation_choose", "gs_feasibility_shard",
-           "gs_feasibility_shard_device", "gs_rank_instance_types", "gs_create_filter", "gs_build_catalog"]
+           "gs_feasibility_shard_device", "gs_rank_instance_types", "gs_create_filter", "gs_build_catalog", "gs_build_id"]
+
+
+def source_digest():
+    """The digest csrc/Makefile bakes into gs_build_id(): sha256 over the
+    library's sources in make's $(sort) order, first 16 hex digits."""
+    import hashlib
+    csrc = os.path.join(HERE, "..", "csrc")
+    names = [n for n in os.listdir(csrc) if n.endswith((".hip", ".cpp", ".hpp"))] + ["Makefile"]
+    paths = {n: os.path.join(csrc, n) for n in names}
+    paths["../../include/gpusched.h"] = os.path.join(csrc, "..", "..", "include", "gpusched.h")
+    h = hashlib.sha256()
+    for n in sorted(paths):
+        with open(paths[n], "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def check_build_id():
+    """Fail loudly when the loaded library was built from other sources."""
+    got = load().gs_build_id().decode()
+    want = source_digest()
+    if got != want:
+        raise GpuSchedError(abi.GS_E_INVALID, f"{LIB_PATH} was built from sources {got}, the tree holds {want}: rebuild")
+    return got
 
 
 class GpuSchedError(RuntimeError):
@@ -66,6 +90,8 @@ def load():
         L.gs_last_error.restype = C.c_size_t
         L.gs_version.argtypes = []
         L.gs_version.restype = C.c_char_p
+        L.gs_build_id.argtypes = []
+        L.gs_build_id.restype = C.c_char_p
         L.gs_validate.argtypes = [C.POINTER(abi.GsProblem), C.c_char_p, C.c_size_t]
         L.gs_validate.restype = C.c_int
         L.gs_abi_sizes.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]

@@ -24,6 +24,18 @@ def test_exports_every_declared_symbol():
         assert hasattr(L, n), n
 
 
+def test_build_id_matches_sources():
+    """The shipped libgpusched.so was built from this tree's sources."""
+    assert lib.check_build_id() == lib.source_digest()
+
+
+@pytest.mark.gpu
+def test_gpu_box_build_id_matches_sources():
+    """Same check in the GPU run: the library the -m gpu suite loads on the
+    box is the one built from the sources it ships with."""
+    assert lib.check_build_id() == lib.source_digest()
+
+
 def test_version():
     assert b"gfx950" in lib.load().gs_version()
 

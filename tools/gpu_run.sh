@@ -1,0 +1,56 @@
+#!/bin/bash
+# One parametrised GPU-box pass (replaces the per-experiment gpu_r4* / gpu_r5*
+# scripts).  Every GPU step runs under its own time limit and the chain stops
+# at the first failure (set -e).  Run from the repo root through gpurun:
+#   gpurun -- bash tools/gpu_run.sh <tag> <step>...
+# steps:
+#   suite          whole -m gpu suite + smoke
+#   tests:<expr>   pytest -m gpu -k <expr>
+#   file:<path>    pytest -m gpu on one test file
+#   bench          the default bench line (+ per-leg detail json)
+#   only:<leg>     bench.py --only <leg> (5 steps)
+#   ffd            tools/ffd_diag.py FFD device ms on cm / c3 / e2e / c2
+#   prof           tools/profile_round.sh (kernel stats + PMC traffic)
+#   lib:<name>     use gpusched/libgpusched_<name>.so for the steps after it
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:?tag}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+PYT="python -u -m pytest -m gpu -x -q --timeout 240 --timeout-method thread"
+for step in "$@"; do
+  case $step in
+    suite)
+      timeout -k 10 900 $PYT tests > $O/pytest_gpu_all.log 2>&1
+      tail -3 $O/pytest_gpu_all.log
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      tail -3 $O/smoke.log ;;
+    tests:*)
+      k=${step#tests:}
+      timeout -k 10 600 $PYT tests -k "$k" > $O/pytest_${k//[^a-zA-Z0-9_]/_}.log 2>&1
+      tail -3 $O/pytest_${k//[^a-zA-Z0-9_]/_}.log ;;
+    file:*)
+      f=${step#file:}
+      b=$(basename $f .py)
+      timeout -k 10 600 $PYT $f > $O/pytest_$b.log 2>&1
+      tail -3 $O/pytest_$b.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --detail-json $O/bench_detail.json > $O/bench.out 2> $O/bench.err
+      tail -c 700 $O/bench.out ;;
+    only:*)
+      leg=${step#only:}
+      timeout -k 10 300 python -u bench.py --only $leg --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$leg.out 2> $O/bench_$leg.err
+      tail -c 400 $O/bench_$leg.out ;;
+    ffd)
+      timeout -k 10 400 python -u tools/ffd_diag.py > $O/ffd_diag.txt 2>&1
+      tail -20 $O/ffd_diag.txt ;;
+    prof)
+      bash tools/profile_round.sh ;;
+    lib:*)
+      export GPUSCHED_LIB=$R/karpenter-provider-ibm-cloud_amd/gpusched/libgpusched_${step#lib:}.so ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
