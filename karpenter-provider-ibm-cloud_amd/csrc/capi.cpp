@@ -122,6 +122,12 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   d.zknown0 = e.zknown0;
   c->upload(d.tgroups, e.tgroups);
   c->upload(d.tg_list, e.tg_list);
+  d.n_lazy = e.n_lazy;
+  c->upload(d.var_lazy, e.var_lazy);
+  c->upload(d.lazy_slot, e.lazy_slot);
+  d.lazy_host = e.lazy_host;
+  c->upload(d.var_lmind_off, e.var_lmind_off);
+  c->upload(d.lmind, e.lmind);
   c->upload(d.zcnt0, e.zcnt0);
   c->upload(d.htot0, e.htot0);
   c->upload(d.zone_order, e.zone_order);

@@ -945,6 +945,13 @@ struct Ctx {
     std::string inv_hash;
     PortEnc port;
     uint32_t owner_spec = gsd::NONE;  // spread groups: the first owner's spec
+    // a spread group no pod's first variant keys: Topology.Update creates it
+    // when a relaxation first moves a pod to this hash (lazy index; the
+    // kernels record into it only once some pod has relaxed into it)
+    bool lazy = false;
+    uint32_t lazy_idx = 0;
+    uint32_t owner_state = 0;         // the first owner's relaxation state (PodWork filter states)
+    uint32_t owner_sv = gsd::NONE;    // the first owner's spec variant in that state
   };
   std::vector<GroupEnc> groups;
   std::map<std::string, uint32_t> group_idx;
@@ -1265,6 +1272,10 @@ struct Ctx {
   // pod the selection list (layout.hpp VarRec own_off / sel_off)
   void build_topology() {
     e.TG = (uint32_t)groups.size();
+    e.var_lazy.assign(1, 0);
+    e.lazy_slot.assign(64, 0);
+    e.var_lmind_off.assign(1, 0);
+    e.lmind.assign(1, 0);
     if (!e.TG) return;
     const Vocab& zv = e.keys[e.k_dom].vocab;
     bool any_zone = false;
@@ -1304,7 +1315,9 @@ struct Ctx {
     for (uint32_t g = 0; g < e.TG; g++) {
       gsd::TGroupRec& t = e.tgroups[g];
       t.skew = groups[g].sp.skew;
-      t.mind = groups[g].sp.mind;
+      // a lazy group's minDomains is its creator's, known at the Relax that
+      // creates it: -(lazy index + 1) reads the kernels' lazy minDomains
+      t.mind = groups[g].lazy ? -(int32_t)groups[g].lazy_idx - 1 : groups[g].sp.mind;
       const int kind = groups[g].kind;
       if (groups[g].sp.key == kHostname) {
         t.kind = gsd::TK_HOST | (kind == 4 ? gsd::TK_AFF : 0u);
@@ -1400,9 +1413,9 @@ struct Ctx {
     // tolerated taint classes for the counted specs below
     std::vector<uint64_t> g_otol(e.TG, ~0ull);
     for (uint32_t g = 0; g < e.TG; g++)
-      if (groups[g].kind == 0 && groups[g].sp.honor_taints) g_otol[g] = final_sv_tol[sv_begin[groups[g].owner_spec]];
+      if (groups[g].kind == 0 && groups[g].sp.honor_taints) g_otol[g] = final_sv_tol[groups[g].owner_sv];
     auto node_tolerated = [&](uint32_t g, uint32_t raw) {
-      const std::vector<Tol>& tols = variant_tols[sv_begin[groups[g].owner_spec]];
+      const std::vector<Tol>& tols = variant_tols[groups[g].owner_sv];
       const gs_range r = p->nodes[raw].taints;
       chk(r, p->n_taints, "taints");
       for (uint32_t k = 0; k < r.count; k++) {
@@ -1477,7 +1490,10 @@ struct Ctx {
       sel_n[s] = (uint32_t)mine.size();
       for (uint32_t g : mine) {
         selected[g] = 1;
-        e.tg_list.push_back(e.tgroups[g].slot | (e.tgroups[g].kind << 24));
+        if (groups[g].lazy)  // slots < 4096: the lazy index rides in bits 16..21
+          e.tg_list.push_back(e.tgroups[g].slot | (groups[g].lazy_idx << 16) | ((e.tgroups[g].kind | gsd::TK_LAZY) << 24));
+        else
+          e.tg_list.push_back(e.tgroups[g].slot | (e.tgroups[g].kind << 24));
       }
       for (uint32_t sv = sv_begin[s]; sv < sv_begin[s] + sv_count[s]; sv++) {
         own_off[sv] = (uint32_t)e.tg_list.size();
@@ -1497,6 +1513,35 @@ struct Ctx {
       }
     }
     if (e.tg_list.empty()) e.tg_list.push_back(0);
+    // per device variant: the lazy groups a pod owns once it relaxes into it
+    // (the kernels activate them at that Relax)
+    e.n_lazy = n_lazy;
+    e.lazy_host = 0;
+    e.lazy_slot.assign(64, 0);
+    for (uint32_t g = 0; g < e.TG; g++)
+      if (groups[g].lazy) {
+        e.lazy_slot[groups[g].lazy_idx] = e.tgroups[g].slot;
+        if (e.tgroups[g].kind & gsd::TK_HOST) e.lazy_host |= 1ull << groups[g].lazy_idx;
+      }
+    e.var_lazy.assign(n_lazy ? e.V : 1, 0);
+    e.var_lmind_off.assign(n_lazy ? e.V : 1, 0);
+    e.lmind.assign(1, 0);
+    if (n_lazy) {
+      // per spec variant its lazy groups' minDomains in lazy-index order
+      std::vector<uint32_t> sv_off(e.variants.size(), 0);
+      for (size_t sv = 0; sv < e.variants.size(); sv++) {
+        auto lm = e.variants[sv].lazy_mind;
+        std::sort(lm.begin(), lm.end());
+        lm.erase(std::unique(lm.begin(), lm.end(), [](auto& a, auto& b) { return a.first == b.first; }), lm.end());
+        sv_off[sv] = (uint32_t)e.lmind.size();
+        for (auto& x : lm) e.lmind.push_back(x.second);
+      }
+      for (uint32_t v = 0; v < e.V; v++) {
+        for (uint32_t g : e.variants[e.var_sv[v]].own)
+          if (groups[g].lazy) e.var_lazy[v] |= 1ull << groups[g].lazy_idx;
+        e.var_lmind_off[v] = sv_off[e.var_sv[v]];
+      }
+    }
   }
 
   // CT_SPOT | CT_OD: Requirement.Has("spot") / Has("on-demand") of the
@@ -2002,7 +2047,72 @@ struct Ctx {
     bool honor_taints = false;  // a spread with nodeTaintsPolicy Honor
     std::string aff_text;             // the node filter's terms with their values
     std::vector<uint32_t> pref_keys;  // keys of the preferred node-affinity terms
+    // relaxation states of the spreads' node filter (<U> MakeTopologyNodeFilter
+    // of the relaxed pod): state r < nT keeps the required terms from r on,
+    // state nT adds the PreferNoSchedule toleration; per state the spreads
+    // as that pod would key them, their hashes and group ids
+    uint32_t n_states = 1;
+    std::vector<std::vector<SpreadEnc>> st_sps;
+    std::vector<std::vector<std::string>> st_hash;
+    std::vector<std::vector<uint32_t>> st_gid;
+    std::vector<uint32_t> var_state;  // per variant
   };
+  // <U> MakeTopologyNodeFilter of one relaxation state: node selector AND
+  // each required term from ri on (the selector alone without terms), the
+  // tolerations; fid = TopologyGroup.Hash's part (term keys, tolerations),
+  // text = the terms with their values, zone_only = no key past the zone
+  struct FilterState {
+    std::vector<Reqs> fr;
+    std::string fid, text;
+    bool zone_only = true, empty = true;
+  };
+  FilterState filter_state(const PodWork& w, size_t ri, const std::vector<Tol>& tols) const {
+    FilterState f;
+    if (w.req_terms.empty()) f.fr.push_back(w.ns);
+    for (size_t t = ri; t < w.req_terms.size(); t++) {
+      Reqs r = w.ns;
+      for (auto& kv : w.req_terms[t]) reqs_add(e, r, kv.first, kv.second);
+      f.fr.push_back(std::move(r));
+    }
+    std::vector<std::string> texts, terms, tl;
+    for (auto& r : f.fr) {
+      texts.push_back(canonical(e, r));
+      std::vector<std::string> ks;
+      for (auto& kv : r) ks.push_back(e.keys[kv.first].name);
+      std::sort(ks.begin(), ks.end());
+      std::string k;
+      for (auto& x : ks) k += x + ",";
+      terms.push_back(std::move(k));
+      f.empty = f.empty && r.empty();
+    }
+    std::sort(texts.begin(), texts.end());
+    for (auto& t : texts) f.text += t + "\x1e";
+    for (auto& t : tols) tl.push_back(t.k + "=" + t.v + ":" + t.eff + "/" + std::to_string(t.op));
+    std::sort(terms.begin(), terms.end());
+    std::sort(tl.begin(), tl.end());
+    for (auto& t : terms) f.fid += t + ";";
+    f.fid += "#";
+    for (auto& t : tl) f.fid += t + ";";
+    for (auto& kv : w.ns) f.zone_only = f.zone_only && kv.first == e.k_zone;
+    for (size_t t = ri; t < w.req_terms.size(); t++)
+      for (auto& kv : w.req_terms[t]) f.zone_only = f.zone_only && kv.first == e.k_zone;
+    return f;
+  }
+  // the spreads keyed under one filter state.  nodeAffinityPolicy Honor
+  // equals Ignore when the filter constrains the zone key alone
+  // (oracle/solve.cpp: it then drops only nodes / NodeClaims outside the
+  // owner's zones); other filters are applied exactly where they can differ:
+  // a bound pod counts only on a node the filter matches, and the pending
+  // pods the group counts must carry the owner's filter terms
+  // (build_topology), so every NodeClaim / node they land on matches it
+  static void key_spreads(std::vector<SpreadEnc>& sps, const FilterState& f) {
+    for (auto& sp : sps) {
+      sp.fid = f.fid;
+      sp.ftext = sp.ignore_aff ? std::string() : f.text;
+      sp.strict_aff = !f.zone_only && !sp.ignore_aff;
+      sp.filter = sp.strict_aff ? f.fr : std::vector<Reqs>();
+    }
+  }
   // pods -> specs: spec_of[pod], spec_rep[spec] (its first pod), and per spec
   // its variants' range in e.variants (sv_begin / sv_count)
   std::vector<uint32_t> spec_of, spec_rep, sv_begin, sv_count;
@@ -2038,62 +2148,33 @@ struct Ctx {
     // text (terms with values) is kept for every spec of a problem with
     // topology inputs: a spec counted by a group whose Honor filter reaches
     // past the zone key must carry that same filter (build_topology)
-    std::vector<Reqs> fr;
+    FilterState f0;
+    if (topo_inputs || !w.sps.empty()) f0 = filter_state(w, 0, w.tols);
     if (topo_inputs) {
-      if (w.req_terms.empty()) fr.push_back(w.ns);
-      for (auto& t : w.req_terms) {
-        Reqs r = w.ns;
-        for (auto& kv : t) reqs_add(e, r, kv.first, kv.second);
-        fr.push_back(std::move(r));
-      }
-      std::vector<std::string> texts;
-      for (auto& r : fr) texts.push_back(canonical(e, r));
-      std::sort(texts.begin(), texts.end());
-      for (auto& t : texts) w.aff_text += t + "\x1e";
+      w.aff_text = f0.text;
       for (auto& pr : w.pref)
         for (auto& kv : pr.second) w.pref_keys.push_back(kv.first);
     }
     if (!w.sps.empty()) {
-      std::vector<std::string> terms, tl;
-      for (auto& r : fr) {
-        std::vector<std::string> ks;
-        for (auto& kv : r) ks.push_back(e.keys[kv.first].name);
-        std::sort(ks.begin(), ks.end());
-        std::string k;
-        for (auto& x : ks) k += x + ",";
-        terms.push_back(std::move(k));
-      }
-      for (auto& t : w.tols) tl.push_back(t.k + "=" + t.v + ":" + t.eff + "/" + std::to_string(t.op));
-      std::sort(terms.begin(), terms.end());
-      std::sort(tl.begin(), tl.end());
-      std::string fid;
-      for (auto& t : terms) fid += t + ";";
-      fid += "#";
-      for (auto& t : tl) fid += t + ";";
-      for (auto& sp : w.sps) {
-        sp.fid = fid;
-        if (!sp.ignore_aff) sp.ftext = w.aff_text;
+      key_spreads(w.sps, f0);
+      // the states Relax moves the filter through: each dropped required
+      // term, then the PreferNoSchedule toleration (pod_phase_c's order)
+      const size_t nT = std::max<size_t>(w.req_terms.size(), 1);
+      bool has_pns = false;
+      for (auto& t : w.tols) has_pns = has_pns || (t.k.empty() && t.op == GS_TOL_EXISTS && t.v.empty() && t.eff == kPNS);
+      w.n_states = (uint32_t)nT + (tolerate_pns && !has_pns ? 1u : 0u);
+      w.st_sps.resize(w.n_states);
+      w.st_hash.resize(w.n_states);
+      w.st_gid.resize(w.n_states);
+      for (uint32_t st = 1; st < w.n_states; st++) {
+        std::vector<Tol> tols = w.tols;
+        if (st == nT) tols.push_back({"", "", kPNS, GS_TOL_EXISTS});
+        w.st_sps[st] = w.sps;
+        key_spreads(w.st_sps[st], filter_state(w, std::min<size_t>(st, nT - 1), tols));
+        for (auto& sp : w.st_sps[st]) w.st_hash[st].push_back(sp.hash(pns));
       }
     }
-    // nodeAffinityPolicy Honor equals Ignore when the node selector and the
-    // required terms constrain the zone key alone (oracle/solve.cpp: the
-    // filter then drops only nodes / NodeClaims outside the owner's zones).
-    // Other filters are applied exactly where they can differ: a bound pod
-    // counts only on a node the filter matches, and the pending pods the
-    // group counts must carry the owner's filter terms (build_topology), so
-    // every NodeClaim / node they land on matches it
-    bool zone_only = true;
-    for (auto& kv : w.ns) zone_only = zone_only && kv.first == e.k_zone;
-    for (auto& t : w.req_terms)
-      for (auto& kv : t) zone_only = zone_only && kv.first == e.k_zone;
-    if (!w.sps.empty() && !zone_only)
-      for (auto& sp : w.sps)
-        if (!sp.ignore_aff) {
-          sp.strict_aff = true;
-          sp.filter = fr;
-        }
-    bool filter_empty = true;
-    for (auto& r : fr) filter_empty = filter_empty && r.empty();
+    const bool filter_empty = f0.empty;
     for (auto& sp : w.sps) {
       w.sp_hash.push_back(sp.hash(pns));
       std::string mk;
@@ -2190,12 +2271,46 @@ struct Ctx {
     w.g_port.clear();
   }
 
+  uint32_t n_lazy = 0;
+  void pod_phase_b2(uint32_t s, PodWork& w) {
+    const std::string pns = S(p->pods[spec_rep[s]].ns);
+    for (uint32_t st = 1; st < w.n_states; st++) {
+      w.st_gid[st].clear();
+      for (size_t k = 0; k < w.st_sps[st].size(); k++) {
+        const SpreadEnc& sp = w.st_sps[st][k];
+        auto f = group_idx.find(w.st_hash[st][k]);
+        if (f == group_idx.end()) {
+          // Topology.Update's new group counts the cluster's bound pods only
+          // (a hostname group also lacks the in-flight NodeClaims registered
+          // before it: the kernels mark those HC_UNKNOWN when it is created)
+          if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
+          if (n_lazy >= 64) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups created by relaxation"};
+          f = group_idx.emplace(w.st_hash[st][k], (uint32_t)groups.size()).first;
+          groups.push_back(GroupEnc{sp, pns});
+          GroupEnc& g = groups.back();
+          g.owner_spec = s;
+          g.lazy = true;
+          g.lazy_idx = n_lazy++;
+          g.owner_state = st;
+        } else {
+          const GroupEnc& g = groups[f->second];
+          if (!sp.ignore_aff && g.sp.ftext != sp.ftext)
+            throw Fail{GS_E_UNSUPPORTED,
+                       "pods sharing a topology spread (nodeAffinityPolicy Honor) with different node affinity values"};
+        }
+        w.st_gid[st].push_back(f->second);
+      }
+    }
+  }
+
   // <U> NewPodRequirements + Preferences.Relax: every variant of one spec
   void pod_phase_c(PodWork& w) {
     std::vector<uint32_t> cur(w.sps.size());  // current constraints (swap-remove order)
     std::iota(cur.begin(), cur.end(), 0);
     std::vector<Tol> tols = w.tols;
     size_t ri = 0, pi = 0, ai = 0, fi = 0;
+    uint32_t state = 0;  // the spreads' filter state (pod_phase_a)
+    if (!w.sps.empty()) w.st_gid[0] = w.sgid;
     for (;;) {
       // <U> NewPodRequirements: nodeSelector + heaviest preferred + first required
       PodVariant v;
@@ -2207,7 +2322,14 @@ struct Ctx {
         reqs_add_all(e, v.strict, w.req_terms[ri]);
       }
       v.tol = 0;  // build_taint_classes
-      for (uint32_t k : cur) v.own.push_back(w.sgid[k]);
+      for (uint32_t k : cur) {
+        const uint32_t g = w.st_gid[state][k];
+        v.own.push_back(g);
+        // the pod that relaxes first creates a lazy group with its own
+        // minDomains (the kernels set it at that Relax)
+        if (groups[g].lazy) v.lazy_mind.emplace_back(groups[g].lazy_idx, w.st_sps[state][k].mind);
+      }
+      w.var_state.push_back(state);
       v.own.insert(v.own.end(), w.own_static.begin(), w.own_static.end());
       for (size_t k = ai; k < w.anti_pref.size(); k++) v.own.push_back(w.anti_pref[k].second);
       for (size_t k = fi; k < w.aff_pref.size(); k++) v.own.push_back(w.aff_pref[k].second);
@@ -2218,6 +2340,7 @@ struct Ctx {
       // <U> Preferences.Relax
       if (w.req_terms.size() - ri > 1) {
         ri++;
+        state = (uint32_t)ri;
         continue;
       }
       // removePreferredPodAffinityTerm, then ...AntiAffinityTerm (the heaviest)
@@ -2248,6 +2371,7 @@ struct Ctx {
           if (t.k.empty() && t.op == GS_TOL_EXISTS && t.v.empty() && t.eff == kPNS) has = true;
         if (!has) {
           tols.push_back({"", "", kPNS, GS_TOL_EXISTS});
+          state = w.n_states - 1;
           continue;
         }
       }
@@ -2410,6 +2534,10 @@ struct Ctx {
       if (work[s].err) std::rethrow_exception(work[s].err);
       pod_phase_b(i, work[s]);
     }
+    // <U> Topology.Update after a relaxation: every spread keyed under the
+    // relaxed filter joins the group of that hash; a hash no pod's first
+    // variant keys is a group created at that moment (lazy), in spec order
+    for (uint32_t s = 0; s < NS; s++) pod_phase_b2(s, work[s]);
     par_for(NS, 8, [&](uint32_t s) {
       try {
         pod_phase_c(work[s]);
@@ -2430,12 +2558,26 @@ struct Ctx {
     // spec's variants in order (e.var_sv: device variant -> spec variant)
     sv_begin.assign(NS, 0);
     sv_count.assign(NS, 0);
+    std::vector<std::vector<uint32_t>> spec_var_state(NS);
     for (uint32_t s = 0; s < NS; s++) {
+      spec_var_state[s] = std::move(work[s].var_state);
       sv_begin[s] = (uint32_t)e.variants.size();
       sv_count[s] = (uint32_t)work[s].vars.size();
       for (auto& v : work[s].vars) e.variants.push_back(std::move(v));
       for (auto& t : work[s].var_tols) variant_tols.push_back(std::move(t));
       if (work[s].honor_taints) honor_specs.push_back(s);
+    }
+    // a group's first owner variant: the first variant of its first owner
+    // spec (lazy groups: the first in the state that keys them)
+    for (auto& g : groups) {
+      if (g.owner_spec == gsd::NONE) continue;
+      g.owner_sv = sv_begin[g.owner_spec];
+      if (!g.lazy) continue;
+      const auto& vs = spec_var_state[g.owner_spec];
+      uint32_t k = 0;
+      while (k < vs.size() && vs[k] != g.owner_state) k++;
+      if (k == vs.size()) throw Fail{GS_E_INVALID, "internal: lazy topology group without its relaxation state"};
+      g.owner_sv += k;
     }
     e.var_begin.resize(e.P);
     e.var_count.resize(e.P);

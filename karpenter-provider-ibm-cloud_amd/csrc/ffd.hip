@@ -610,7 +610,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   uint32_t* const ov_map = SIM ? d.ov_map + (size_t)blockIdx.x * d.NN : nullptr;
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
-  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH);
   // SIM, small simulations: node -> overlay entry in an LDS hash (keys node + 1,
   // open addressing), after the topology state
   const uint32_t ovh = SIM ? d.ovh_slots : 0u, ovh_mask = ovh - 1u;
@@ -1575,7 +1575,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
               cr->zfull = zf;
               cr->zflags = zl;
               int32_t* hrow = dd.hc + (size_t)(cb + j) * dd.TGH;
-              topo_record(dd, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs]++; });
+              topo_record(dd, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs] = (hrow[hs] & HC_COUNT) + 1; });
             }
             FK* cf = dd.c_fk + (size_t)(cb + j) * F;
             for (uint32_t k = 0; k < vr.fk_count; k++) {
@@ -1732,7 +1732,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           if (TOPO && sel_n) {
             // <U> Topology.Record
             int32_t* hrow = d.hc + (size_t)(cbase + j) * d.TGH;
-            topo_record(d, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
+            topo_record(d, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs] = (hrow[hs] & HC_COUNT) + 1; });
           }
           FK* cf = d.c_fk + (size_t)(cbase + j) * F;
           for (uint32_t s = 0; s < F; s++) cf[s] = d.t_fk[(size_t)t * F + s];
@@ -1803,6 +1803,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         if (v + 1 < d.var_begin[gp] + d.var_count[gp]) {
           cur_var[p] = v + 1;
           relaxed = true;
+          if (TOPO && d.n_lazy) {
+            const uint64_t fresh = topo_relaxed(d, ts, v + 1);
+            topo_mark_unknown(d, fresh, d.hc + (size_t)(SIM ? qoff : 0u) * d.TGH, M, 0u, 1u);
+            topo_activate(d, ts, v + 1, fresh);
+          }
         }
         uint32_t tail = HN.qhead + HN.qlen;
         if (tail >= P) tail -= P;
@@ -1833,8 +1838,15 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         int32_t* hrow = d.hc + (size_t)(qoff + l.target) * d.TGH;
         for (uint32_t k = 0; k < lv.sel_n; k++) {
           const uint32_t e = d.tg_list[lv.sel_off + k];
-          if ((e >> 24) & TK_HOST) hrow[e & 0xFFFFFFu] = 0;
+          if ((e >> 24) & TK_HOST) hrow[e & (((e >> 24) & TK_LAZY) ? 0xFFFFu : 0xFFFFFFu)] = 0;
         }
+      }
+      // and the cells a lazy hostname group created in this simulation marked
+      // HC_UNKNOWN on the NodeClaims that existed before it
+      const uint64_t lz = ts.lazy[0] & d.lazy_host;
+      if (lz) {
+        __syncthreads();
+        topo_mark_unknown(d, lz, d.hc + (size_t)qoff * d.TGH, S.hb[par ^ 1u].M, tid, FB, 0);
       }
     }
     if (SIM) {

@@ -495,13 +495,17 @@ struct TopoS {
   int64_t* tmin;    // [OWNMAX]
   int32_t* zcnt;    // [TGZ][ZS]
   int32_t* htot;    // [TGH]
+  uint64_t* lazy;   // [1] the lazy groups (TK_LAZY) some pod has relaxed into
+  int32_t* lmind;   // [64] their minDomains (the creating pod's)
 };
-__device__ __forceinline__ TopoS topo_lds(char* base, uint32_t tgz, uint32_t zs) {
+__device__ __forceinline__ TopoS topo_lds(char* base, uint32_t tgz, uint32_t zs, uint32_t tgh) {
   TopoS t;
   t.known = (uint64_t*)base;
   t.tmin = (int64_t*)(base + tgz * 8u);
   t.zcnt = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u);
   t.htot = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u);
+  t.lazy = (uint64_t*)(base + topo_lds_bytes(tgz, zs, tgh) - 8u - 64u * 4u);
+  t.lmind = (int32_t*)(base + topo_lds_bytes(tgz, zs, tgh) - 64u * 4u);
   return t;
 }
 
@@ -511,6 +515,37 @@ __device__ __forceinline__ void topo_init(const DP& d, const TopoS& ts, uint64_t
   for (uint32_t k = i; k < d.TGZ * d.ZS; k += stride) ts.zcnt[k] = d.zcnt0[k];
   for (uint32_t k = i; k < d.TGZ; k += stride) ts.known[k] = known0;
   for (uint32_t k = i; k < d.TGH; k += stride) ts.htot[k] = d.htot0[k];
+  if (i == 0) ts.lazy[0] = 0;
+}
+
+// <U> Topology.Update after Relax: the lazy groups the pod's new variant
+// owns and no pod created before exist from now on (Record counts into them;
+// the caller sets ts.lazy).  Returns them
+template <class DP>
+__device__ __forceinline__ uint64_t topo_relaxed(const DP& d, const TopoS& ts, uint32_t new_var) {
+  return d.n_lazy ? d.var_lazy[new_var] & ~ts.lazy[0] : 0ull;
+}
+// ... which exist from now on, with the minDomains of the variant that
+// created them (one thread)
+template <class DP>
+__device__ __forceinline__ void topo_activate(const DP& d, const TopoS& ts, uint32_t new_var, uint64_t fresh) {
+  const uint64_t all = d.var_lazy[new_var];
+  const uint32_t off = d.var_lmind_off[new_var];
+  for (uint64_t x = fresh; x; x &= x - 1) {
+    const uint32_t b = (uint32_t)__ffsll((long long)x) - 1u;
+    ts.lmind[b] = d.lmind[off + (uint32_t)__popcll(all & ((1ull << b) - 1ull))];
+  }
+  ts.lazy[0] |= fresh;
+}
+// ... and the in-flight NodeClaims [0, M) are no domains of the new hostname
+// groups among them (i / stride: this thread's share)
+template <class DP>
+__device__ __forceinline__ void topo_mark_unknown(const DP& d, uint64_t fresh, int32_t* hc_rows, uint32_t M, uint32_t i,
+                                                  uint32_t stride, int32_t value = HC_UNKNOWN) {
+  for (uint64_t x = fresh & d.lazy_host; x; x &= x - 1) {
+    const uint32_t slot = d.lazy_slot[(uint32_t)__ffsll((long long)x) - 1u];
+    for (uint32_t j = i; j < M; j += stride) hc_rows[(size_t)j * d.TGH + slot] = value;
+  }
 }
 
 // domainMinCount of every owned zone spread group over the pod's strict zone
@@ -529,7 +564,8 @@ __device__ __forceinline__ void topo_tmin(const DP& d, const TopoS& ts, uint32_t
     const int64_t c = ts.zcnt[tr.slot * d.ZS + (uint32_t)__ffsll((long long)m) - 1u];
     mn = c < mn ? c : mn;
   }
-  if (tr.mind && n < tr.mind) mn = 0;
+  const int32_t mind = tr.mind < 0 ? ts.lmind[-tr.mind - 1] : tr.mind;
+  if (mind && n < mind) mn = 0;
   ts.tmin[lane] = mn;
 }
 
@@ -664,7 +700,12 @@ __device__ __forceinline__ void topo_record_g(const DP& d, const TopoS& ts, uint
   zf &= zmask;
   for (uint32_t k = 0; k < sel_n; k++) {
     const uint32_t e = sel(k);
-    const uint32_t slot = e & 0xFFFFFFu, kind = e >> 24;
+    uint32_t slot = e & 0xFFFFFFu;
+    const uint32_t kind = e >> 24;
+    if (kind & TK_LAZY) {
+      if (!((ts.lazy[0] >> ((e >> 16) & 63u)) & 1ull)) continue;  // not created yet
+      slot = e & 0xFFFFu;
+    }
     if (kind & TK_HOST) {
       hinc(slot);
       ts.htot[slot]++;

@@ -701,7 +701,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     __builtin_assume(W <= WREG);
   const uint32_t nthr = d.thr_off[R];
   const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
-  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH);
   // existing nodes (wave_node_lds_bytes): slack codes (upper bound), room
   // codes (lower bound) of available - requests per resource 0..3, and a
   // flag byte: bit 0 = plain (ok, no taints, resources 4.. not over)
@@ -2266,7 +2266,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             cr->zfull = zf;
             cr->zflags = zl;
             int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
-            topo_record(KD, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs]++; });
+            topo_record(KD, ts, sel_off, sel_n, zf, zl, [&](uint32_t hs) { hrow[hs] = (hrow[hs] & HC_COUNT) + 1; });
           }
           FK* cf = KD.c_fk + (size_t)j * F;
           for (uint32_t k = 0; k < fk_count; k++) {
@@ -2325,7 +2325,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
               const auto& KD = *karg();
               const ClaimRec* cr = KD.c_rec + j;
               int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
-              topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
+              topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs] = (hrow[hs] & HC_COUNT) + 1; });
             }
           }
         }
@@ -2516,7 +2516,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         if (TOPO && sel_n) {
           // <U> Topology.Record
           int32_t* hrow = KD.hc + (size_t)j * KD.TGH;
-          topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs]++; });
+          topo_record(KD, ts, sel_off, sel_n, cr->zfull, cr->zflags, [&](uint32_t hs) { hrow[hs] = (hrow[hs] & HC_COUNT) + 1; });
         }
         FK* cf = KD.c_fk + (size_t)j * F;
         for (uint32_t s = 0; s < F; s++) cf[s] = KD.t_fk[(size_t)t * F + s];
@@ -2563,6 +2563,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       uint32_t tail = qhead + qlen;
       if (tail >= P) tail -= P;
       qlen++;
+      if (TOPO && relaxed && KD.n_lazy) {
+        const uint64_t fresh = topo_relaxed(KD, ts, v + 1);
+        if (fresh) {
+          topo_mark_unknown(KD, fresh, KD.hc, M, lane, 64u);
+          if (lane == 0) topo_activate(KD, ts, v + 1, fresh);
+        }
+      }
       if (lane == 0) {
         if (relaxed) KD.cur_var[p] = v + 1;
         KD.queue[tail] = p;

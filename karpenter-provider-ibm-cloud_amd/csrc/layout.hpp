@@ -47,7 +47,15 @@ constexpr int TGMAX = 4096;    // topology groups (spread, pod (anti-)affinity, 
 constexpr int OWNMAX = 64;     // topology groups one pod variant owns
 constexpr int ZVMAX = 64;      // zone vocabulary (topology domains) when zone groups are used
 // topology group kinds (TGroupRec.kind, and the top byte of a selection-list entry)
-enum : uint32_t { TK_HOST = 1u, TK_AFF = 2u, TK_ANTI = 4u };
+// selection-list kind bits (entry >> 24); TK_LAZY: a spread group created by
+// a relaxation (Topology.Update), lazy index in entry bits 16..21, slot in
+// bits 0..15; Record skips it until some pod has relaxed into it
+enum : uint32_t { TK_HOST = 1u, TK_AFF = 2u, TK_ANTI = 4u, TK_LAZY = 8u };
+// a NodeClaim's count cell of a lazy hostname group created after the claim:
+// the claim is no domain of it (Topology.Register ran before the group
+// existed), so every owner check fails there; Record makes it a domain with
+// count 1 (TopologyGroup.Record), hence count = (cell & HC_COUNT) + 1
+constexpr int32_t HC_UNKNOWN = 0x40000000, HC_COUNT = 0x3FFFFFFF;
 // own-list entry: group id | TL_SELF (the owner is counted by the group itself)
 constexpr uint32_t TL_SELF = 0x80000000u;
 constexpr uint32_t TL_GID = 0xFFFFu;
@@ -125,7 +133,7 @@ struct TmplRec {
 // one topology group (<U> TopologyGroup, empty node filter)
 struct TGroupRec {
   int32_t skew;          // maxSkew (hostname anti-affinity / host ports: self, so the rule is count == 0)
-  int32_t mind;          // minDomains (0 = unset)
+  int32_t mind;          // minDomains (0 = unset; -(k + 1): lazy group k's, set when a relaxation creates it)
   uint32_t slot;         // TK_HOST: row in hn / column in hc; zone groups: row in the zone count table
   uint32_t kind;         // TK_HOST (hostname key, else zone), TK_AFF (pod affinity), TK_ANTI (anti-affinity / inverse)
   uint64_t known0;       // zone groups: domains known before the Solve (universe + counted)
@@ -141,7 +149,7 @@ __host__ __device__ inline uint32_t wave_node_lds_bytes(uint32_t nn) { return nn
 // hostname totals [TGH] i32
 __host__ __device__ inline uint32_t topo_lds_bytes(uint32_t tgz, uint32_t zs, uint32_t tgh) {
   if (!tgz && !tgh) return 0;
-  return (tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u;
+  return ((tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u) + 8u + 64u * 4u;  // + lazy mask, minDomains
 }
 
 // per-claim record (device-owned, AoS: one candidate = one 192-B record read
@@ -330,10 +338,15 @@ struct DevProblem {
   uint32_t TGZ, ZS;            // zone groups, zone-count stride (max(NZV, 1))
   uint32_t dom_ct;             // the "zone" groups' domain key is the capacity type (zone_cat -> catalog capacity types)
   uint32_t dom_np;             // ... is the NodePool (a template's fixed domain: no catalog narrowing)
-  uint32_t pad_tg;
+  uint32_t n_lazy;             // spread groups created by relaxations (<= 64)
   uint64_t zknown0;            // zone domains known before the Solve (universe + counted), every zone group
   const TGroupRec* tgroups;    // [TG]
   const uint32_t* tg_list;     // own / selection list arena (VarRec own_off / sel_off)
+  const uint64_t* var_lazy;    // [V] (n_lazy > 0): the lazy groups a variant owns, activated when a pod relaxes into it
+  const uint32_t* lazy_slot;   // [64] a lazy group's slot (hostname groups: column in hc)
+  uint64_t lazy_host;          // the lazy groups on the hostname key
+  const uint32_t* var_lmind_off;  // [V] the variant's lazy minDomains in lmind (one per set bit of var_lazy)
+  const int32_t* lmind;
   const int32_t* zcnt0;        // [TGZ][ZS] zone counts before the Solve
   const int32_t* htot0;        // [TGH] hostname groups: counted pods over all domains before the Solve
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)

@@ -605,7 +605,7 @@ def random_consolidation(seed, n_nodes=None, n_pending=None, inflight=False, par
 
 
 def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignore", multi_term=False,
-                    domain_key="topology.kubernetes.io/zone", tol_by_app=False):
+                    domain_key="topology.kubernetes.io/zone", tol_by_app=False, pns_frac=0.3):
     """small adversarial topology-spread problems: zone / hostname spreads
     (DoNotSchedule and ScheduleAnyway, maxSkew 1-3, minDomains, matchLabels
     and matchExpressions selectors, nil selectors, nodeAffinityPolicy Ignore
@@ -649,7 +649,7 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
             reqs.append(("topology.kubernetes.io/zone", "In", zs))
         if cts is not None and cts.random() < 0.8:
             reqs.append((ctk, "In", [["spot"], ["on-demand"], ["on-demand", "spot"]][int(cts.integers(0, 3))]))
-        taints = [("dedicated", "x", "PreferNoSchedule")] if rng.random() < 0.3 else []
+        taints = [("dedicated", "x", "PreferNoSchedule")] if rng.random() < pns_frac else []
         limits = {"cpu": int(rng.choice([8, 32])) * 1000} if rng.random() < 0.2 else None
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, taints=taints, limits=limits,
                        daemon={"cpu": 100, "pods": 1000})
@@ -729,6 +729,16 @@ def random_topology(seed, n_pods=None, taint_policy=None, affinity_policy="Ignor
                   node_selector=sel, required_terms=required, tolerations=tols, labels=labels,
                   namespace=str(rng.choice(["default", "default", "other"])), spreads=spreads)
     return b.build()
+
+
+def random_relax(seed, n_pods=None):
+    """relax-heavy topology problems (<U> Topology.Update re-keying): most
+    NodePools carry a PreferNoSchedule taint, so pods without the toleration
+    relax into it, and spread owners with node affinity carry two OR'd zone
+    terms, so relaxation drops one; both change the spread groups' node filter
+    and so their TopologyGroup.Hash.  nodeAffinityPolicy alternates by seed."""
+    return random_topology(seed, n_pods=n_pods, multi_term=True, pns_frac=0.85,
+                           affinity_policy="Honor" if seed % 2 else "Ignore")
 
 
 def random_honor_filter(seed, n_pods=None, affinity_policy="Honor", consolidation=False):
@@ -1074,15 +1084,18 @@ def random_volumes(seed, n_pods=None):
 
 
 def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=None, ct_spreads=False,
-                                 np_spreads=False):
+                                 np_spreads=False, pns=False):
     """small adversarial consolidation clusters for the general simulation
     variant: bound and pending pods with zone / hostname topology spread,
     hostname and zone pod anti-affinity (required, preferred, inverse
     carriers), hostname pod affinity, host ports, CSI volumes (shared and
     per-pod, node attach limits) and NodePools with minValues.  ct_spreads:
     the spreads use the capacity-type key instead of the zone (anti-affinity
-    then stays on the hostname key); np_spreads: the NodePool key"""
+    then stays on the hostname key); np_spreads: the NodePool key; pns: most
+    NodePools carry a PreferNoSchedule taint (rescheduled pods relax into its
+    toleration, re-keying their spread groups; its own random stream)"""
     rng = np.random.default_rng(0xC0A50000 + seed)
+    prng = np.random.default_rng(0x9A5 + seed)
     b = ProblemBuilder()
     zones = FAKE_ZONES[: int(rng.integers(2, 4))]
     profs = []
@@ -1101,8 +1114,9 @@ def random_consolidation_general(seed, n_nodes=None, n_pending=None, min_values=
         if mv and j == 0:
             reqs.append(("karpenter-ibm.sh/instance-family", "Exists", [], int(rng.integers(1, 3))))
         limits = {"cpu": int(rng.choice([16, 64, 256])) * 1000} if rng.random() < 0.2 else None
+        taints = [("dedicated", "x", "PreferNoSchedule")] if pns and prng.random() < 0.75 else []
         b.add_nodepool(f"np{j}", weight=int(rng.choice([0, 10])), requirements=reqs, limits=limits,
-                       daemon={"cpu": 100, "pods": 1000})
+                       daemon={"cpu": 100, "pods": 1000}, taints=taints)
     apps = ["web", "db", "cache"]
     dkey = ("karpenter.sh/capacity-type" if ct_spreads else "karpenter.sh/nodepool" if np_spreads
             else "topology.kubernetes.io/zone")

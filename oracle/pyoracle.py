@@ -92,6 +92,14 @@ def solve(problem):
     return st, abi.result_to_dict(res, problem), res
 
 
+def last_groups_created():
+    """Spread groups the last solve() created mid-Solve (Topology.Update
+    after a relaxation that changed an owner's node filter)."""
+    L = lib()
+    L.oracle_last_groups_created.restype = C.c_uint64
+    return int(L.oracle_last_groups_created())
+
+
 def feasibility(problem):
     res = abi.GsFeasResult()
     st = lib().oracle_feasibility(C.byref(problem.struct), C.byref(res))

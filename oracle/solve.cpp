@@ -497,6 +497,7 @@ struct ExistingNode {
   string name;
   bool initialized;
   Reqs reqs;
+  Reqs label_reqs;  // NewLabelRequirements(node.Labels) + hostname: countDomains reads the Node, not the Solve's state
   vector<Taint> taints;
   Res available, requests;
   vector<const Pod*> pods;
@@ -650,7 +651,74 @@ struct OracleState {
   std::map<string, size_t> group_index;
   vector<TGroup> inverse;           // t.inverseTopologies (required anti-affinity)
   std::map<string, size_t> inverse_index;
+  // NewTopology's inputs, kept for the groups Topology.Update creates
+  // mid-Solve (a relaxation that changes a spread owner's node filter gives
+  // it a new TopologyGroup.Hash): the domain universe and the bound pods
+  vector<Reqs> np_reqs;
+  vector<bool> np_has_its;
+  vector<vector<Taint>> np_taints;
+  vector<Pod> bound;
+  vector<uint32_t> bound_node;
+  vector<vector<Taint>> bound_node_taints;  // the Node's own taints (countDomains' filter)
 };
+
+// <U> a group's domains before any count: the In values of the requirements
+// (+labels) of NodePools that have instance types, and of the existing
+// nodes' labels, with the taints of each provider (TopologyDomainGroup)
+void group_universe(const OracleState& st, TGroup& g) {
+  for (size_t i = 0; i < st.np_reqs.size(); i++) {
+    if (!st.np_has_its[i] || !st.np_reqs[i].has_key(g.key)) continue;
+    const Req q = st.np_reqs[i].get(g.key);
+    if (q.op() == GS_OP_IN)
+      for (auto& v : q.values) {
+        g.domains.emplace(v, 0);
+        g.dom_taints[v].push_back(st.np_taints[i]);
+      }
+  }
+  for (auto& n : st.nodes) {
+    if (!n.label_reqs.has_key(g.key)) continue;
+    const Req q = n.label_reqs.get(g.key);
+    if (q.op() == GS_OP_IN)
+      for (auto& v : q.values) {
+        g.domains.emplace(v, 0);
+        g.dom_taints[v].push_back(n.taints);
+      }
+  }
+}
+
+// <U> Topology.countDomains: selected bound pods on their nodes' domains,
+// where the node passes the group's filter (the Node's own taints and
+// labels, strict Compatible)
+void count_domains(const OracleState& st, TGroup& g) {
+  for (size_t b = 0; b < st.bound.size(); b++) {
+    const Pod& bp = st.bound[b];
+    const ExistingNode& n = st.nodes[st.bound_node[b]];
+    if (!g.selects(bp) || !n.label_reqs.has_key(g.key)) continue;
+    if (!g.filter_matches(st.bound_node_taints[b], n.label_reqs, false)) continue;
+    const Req q = n.label_reqs.get(g.key);
+    if (q.op() != GS_OP_IN) continue;
+    if (g.anti)
+      for (auto& v : q.values) g.domains[v]++;
+    else if (q.values.size() == 1)
+      g.domains[*q.values.begin()]++;
+  }
+}
+
+// <U> NewTopologyGroup for a spread constraint of a pod in namespace ns
+TGroup spread_group(const Spread& sp, const string& ns) {
+  TGroup g;
+  g.key = sp.key;
+  g.max_skew = sp.max_skew;
+  g.min_domains = sp.min_domains;
+  g.ns = ns;
+  g.sel = sp;
+  g.spread = true;
+  g.honor_affinity = !sp.ignore_affinity;
+  g.honor_taints = sp.honor_taints;
+  g.filter = sp.filter;
+  g.filter_tols = sp.filter_tols;
+  return g;
+}
 
 struct Builder {
   const gs_problem* p;
@@ -910,32 +978,16 @@ struct Builder {
   // scheduled; domain universe = In values of NodePool (+labels, + instance
   // type) requirements of NodePools that have instance types, plus existing
   // nodes' labels; counts = selected bound pods on existing nodes
-  void build_topology(const vector<Reqs>& np_reqs, const vector<bool>& np_has_its,
-                      const vector<vector<Taint>>& np_taints) {
+  void build_topology() {
     for (auto& pd : st.pods)
       for (auto& sp : pd.spreads) {
         const string h = sp.hash(pd.ns);
         auto f = st.group_index.find(h);
-        size_t gi;
         if (f == st.group_index.end()) {
-          gi = st.groups.size();
-          st.group_index[h] = gi;
-          TGroup g;
-          g.key = sp.key;
-          g.max_skew = sp.max_skew;
-          g.min_domains = sp.min_domains;
-          g.ns = pd.ns;
-          g.sel = sp;
-          g.spread = true;
-          g.honor_affinity = !sp.ignore_affinity;
-          g.honor_taints = sp.honor_taints;
-          g.filter = sp.filter;
-          g.filter_tols = sp.filter_tols;
-          st.groups.push_back(std::move(g));
-        } else {
-          gi = f->second;
+          f = st.group_index.emplace(h, st.groups.size()).first;
+          st.groups.push_back(spread_group(sp, pd.ns));
         }
-        st.groups[gi].owners.insert(pd.index);
+        st.groups[f->second].owners.insert(pd.index);
       }
     // <U> newForTopologies: required and preferred anti-affinity terms
     for (auto& pd : st.pods)
@@ -962,61 +1014,33 @@ struct Builder {
     };
     for (auto& pd : st.pods)
       for (auto& a : pd.anti_required) inverse_of(a).owners.insert(pd.index);
-    vector<Pod> bound(p->n_bound_pods);
+    st.bound.assign(p->n_bound_pods, Pod{});
+    st.bound_node.assign(p->n_bound_pods, 0);
+    st.bound_node_taints.assign(p->n_bound_pods, {});
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
       if (p->bound_pod_node[b] >= st.nodes.size()) throw Unsupported{GS_E_INVALID, "bound pod node out of range"};
-      bound[b].index = UINT32_MAX;
-      pod_meta(p->bound_pods[b], bound[b], false);
-      for (auto& a : bound[b].anti_required) inverse_of(a);
+      Pod& bp = st.bound[b];
+      bp.index = UINT32_MAX;
+      pod_meta(p->bound_pods[b], bp, false);
+      st.bound_node[b] = p->bound_pod_node[b];
+      st.bound_node_taints[b] = taints_of(p->nodes[p->bound_pod_node[b]].taints);
+      for (auto& a : bp.anti_required) inverse_of(a);
       // ExistingNode hostPortUsage and VolumeUsage
       auto& n = st.nodes[p->bound_pod_node[b]];
-      n.ports.insert(n.ports.end(), bound[b].ports.begin(), bound[b].ports.end());
-      for (auto& v : bound[b].volumes) n.vols[v.first].insert(v.second);
+      n.ports.insert(n.ports.end(), bp.ports.begin(), bp.ports.end());
+      for (auto& v : bp.volumes) n.vols[v.first].insert(v.second);
     }
     if (st.groups.empty() && st.inverse.empty()) return;
     for (auto* gs : {&st.groups, &st.inverse})
-    for (auto& g : *gs) {
-      for (size_t i = 0; i < np_reqs.size(); i++) {
-        if (!np_has_its[i] || !np_reqs[i].has_key(g.key)) continue;
-        const Req q = np_reqs[i].get(g.key);
-        if (q.op() == GS_OP_IN)
-          for (auto& v : q.values) {
-            g.domains.emplace(v, 0);
-            g.dom_taints[v].push_back(np_taints[i]);
-          }
-      }
-      for (auto& n : st.nodes) {
-        if (!n.reqs.has_key(g.key)) continue;
-        const Req q = n.reqs.get(g.key);
-        if (q.op() == GS_OP_IN)
-          for (auto& v : q.values) {
-            g.domains.emplace(v, 0);
-            g.dom_taints[v].push_back(n.taints);
-          }
-      }
-    }
+      for (auto& g : *gs) group_universe(st, g);
+    for (auto& g : st.groups) count_domains(st, g);
+    // updateInverseAffinities: a bound carrier of a required term blocks its node
     for (uint32_t b = 0; b < p->n_bound_pods; b++) {
-      const Pod& bp = bound[b];
-      const ExistingNode& n = st.nodes[p->bound_pod_node[b]];
-      // countDomains: selected bound pods on their nodes' domains, where
-      // the node passes the group's filter (the Node's own taints and labels,
-      // strict Compatible)
-      const vector<Taint> node_taints = taints_of(p->nodes[p->bound_pod_node[b]].taints);
-      for (auto& g : st.groups) {
-        if (!g.selects(bp) || !n.reqs.has_key(g.key)) continue;
-        if (!g.filter_matches(node_taints, n.reqs, false)) continue;
-        const Req q = n.reqs.get(g.key);
-        if (q.op() != GS_OP_IN) continue;
-        if (g.anti)
-          for (auto& v : q.values) g.domains[v]++;
-        else if (q.values.size() == 1)
-          g.domains[*q.values.begin()]++;
-      }
-      // updateInverseAffinities: a bound carrier of a required term blocks its node
-      for (auto& a : bp.anti_required) {
+      const ExistingNode& n = st.nodes[st.bound_node[b]];
+      for (auto& a : st.bound[b].anti_required) {
         TGroup& g = st.inverse[st.inverse_index.at(a.hash())];
-        if (!n.reqs.has_key(g.key)) continue;
-        const Req q = n.reqs.get(g.key);
+        if (!n.label_reqs.has_key(g.key)) continue;
+        const Req q = n.label_reqs.get(g.key);
         if (q.op() == GS_OP_IN)
           for (auto& v : q.values) g.domains[v]++;
       }
@@ -1052,9 +1076,9 @@ struct Builder {
       if (A.weight == B.weight) return str(A.name) < str(B.name);
       return A.weight > B.weight;
     });
-    vector<Reqs> np_reqs;
-    vector<bool> np_has_its;
-    vector<vector<Taint>> np_taints;
+    auto& np_reqs = st.np_reqs;
+    auto& np_has_its = st.np_has_its;
+    auto& np_taints = st.np_taints;
     for (uint32_t npi : order) {
       auto& np = p->nodepools[npi];
       Template t;
@@ -1133,6 +1157,7 @@ struct Builder {
       n.initialized = g.initialized != 0;
       for (auto& kv : labels_of(g.labels)) n.reqs.add(make_req(kv.first, GS_OP_IN, {kv.second}, std::nullopt));
       n.reqs.add(make_req(kHostname, GS_OP_IN, {n.name}, std::nullopt));
+      n.label_reqs = n.reqs;
       n.taints = state_taints(g);
       n.available = res_of(g.available);
       n.requests = res_of(g.requests);
@@ -1150,7 +1175,7 @@ struct Builder {
       if (A.initialized != B.initialized) return A.initialized;
       return A.name < B.name;
     });
-    build_topology(np_reqs, np_has_its, np_taints);
+    build_topology();
     // resource vocabulary (for dense claim requests)
     std::set<string> rn;
     for (uint32_t i = 0; i < p->n_quantities; i++) rn.insert(str(p->quantities[i].resource));
@@ -1348,12 +1373,28 @@ struct Scheduler {
       for (auto& g : *gs)
         if (g.key == kHostname) g.domains.emplace(h, 0);
   }
-  // Topology.Update after a relaxation: ownership follows the remaining constraints
-  void topo_update(const Pod& pod) {
+  // <U> Topology.Update after a relaxation: the pod leaves every group, then
+  // owns the groups of its remaining constraints.  A spread's node filter
+  // (MakeTopologyNodeFilter) is rebuilt from the relaxed pod: a dropped
+  // required node-affinity term or the added PreferNoSchedule toleration
+  // changes TopologyGroup.Hash, and a hash not seen yet is a group created
+  // now, whose countDomains sees the cluster's bound pods only -- none of this
+  // Solve's placements so far, and none of the hostname placeholders
+  // registered before it
+  uint64_t groups_created_in_solve = 0;
+  void topo_update(Pod& pod) {
     for (auto& g : st.groups) g.owners.erase(pod.index);
     for (auto& sp : pod.spreads) {
+      Builder::node_filter(pod, sp);
       auto f = st.group_index.find(sp.hash(pod.ns));
-      if (f != st.group_index.end()) st.groups[f->second].owners.insert(pod.index);
+      if (f == st.group_index.end()) {
+        f = st.group_index.emplace(sp.hash(pod.ns), st.groups.size()).first;
+        st.groups.push_back(spread_group(sp, pod.ns));
+        group_universe(st, st.groups.back());
+        count_domains(st, st.groups.back());
+        groups_created_in_solve++;
+      }
+      st.groups[f->second].owners.insert(pod.index);
     }
     for (auto* terms : {&pod.anti_required, &pod.anti_preferred, &pod.aff_required, &pod.aff_preferred})
       for (auto& a : *terms) {
@@ -1579,6 +1620,7 @@ struct ResultStore {
 };
 ResultStore g_res;
 OracleState* g_state = nullptr;
+uint64_t g_groups_created = 0;  // the last oracle_solve's groups created by Topology.Update
 
 }  // namespace
 
@@ -1648,9 +1690,14 @@ extern "C" gs_status oracle_solve(const gs_problem* problem, gs_result* out) {
   out->claim_prefix = s.claim_calls;
   out->t_encode_ms = build_ms;  // the oracle's own input build (string sets)
   out->node_prefix = s.node_calls;
+  g_groups_created = s.groups_created_in_solve;
   out->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GS_OK;
 }
+
+// instrumentation for the KATs: spread groups the last oracle_solve created
+// mid-Solve (a relaxation re-keyed a spread owner)
+extern "C" uint64_t oracle_last_groups_created(void) { return g_groups_created; }
 
 extern "C" gs_status oracle_feasibility(const gs_problem* problem, gs_feas_result* out) {
   auto t0 = std::chrono::steady_clock::now();
