@@ -1297,6 +1297,24 @@ struct Ctx {
       for (uint32_t z = 0; z < e.Z; z++)
         if (e.cat_zone[z] < (uint32_t)gsd::ZVMAX) e.zone_cat[e.cat_zone[z]] = z;
     }
+    // <U> buildDomainGroups inserts Requirement.Values() of each NodePool's
+    // requirements combined with each of its instance types': for a NotIn
+    // those are the excluded values (this restatement takes In values only),
+    // and an instance type's own requirement on the key would add its values.
+    // The IBM catalog's instance types carry neither a zone nor a capacity
+    // type (instancetype.go:719-724), so an unconstrained NodePool provides
+    // no domain either way; the two ambiguous forms are refused, not guessed
+    if (any_zone) {
+      for (auto& u : np_universe) {
+        if (!u.second) continue;
+        auto f = u.first.find(e.k_dom);
+        if (f != u.first.end() && f->second.comp && !f->second.excl.none())
+          throw Fail{GS_E_UNSUPPORTED, "a NodePool NotIn requirement on the topology spread key " + e.keys[e.k_dom].name};
+      }
+      for (uint32_t k : e.it_keys)
+        if (k == e.k_dom)
+          throw Fail{GS_E_UNSUPPORTED, "instance types with a requirement on the topology spread key " + e.keys[e.k_dom].name};
+    }
     uint64_t known_zone = 0;
     for (auto& u : np_universe) {
       if (!u.second) continue;

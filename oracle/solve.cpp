@@ -1031,6 +1031,19 @@ struct Builder {
       for (auto& v : bp.volumes) n.vols[v.first].insert(v.second);
     }
     if (st.groups.empty() && st.inverse.empty()) return;
+    // <U> buildDomainGroups takes Requirement.Values() of NodePool x instance
+    // type requirements: a NotIn's excluded values, an instance type's own
+    // values.  The IBM instance types carry no zone / capacity type
+    // (instancetype.go:719-724); the two ambiguous forms are refused
+    for (auto* gs : {&st.groups, &st.inverse})
+      for (auto& g : *gs) {
+        if (g.key == kHostname) continue;
+        for (size_t i = 0; i < st.np_reqs.size(); i++)
+          if (st.np_has_its[i] && st.np_reqs[i].has_key(g.key) && st.np_reqs[i].get(g.key).op() == GS_OP_NOTIN)
+            throw Unsupported{GS_E_UNSUPPORTED, "NodePool NotIn requirement on a topology key"};
+        for (auto& it : st.its)
+          if (it.reqs.has_key(g.key)) throw Unsupported{GS_E_UNSUPPORTED, "instance type requirement on a topology key"};
+      }
     for (auto* gs : {&st.groups, &st.inverse})
       for (auto& g : *gs) group_universe(st, g);
     for (auto& g : st.groups) count_domains(st, g);

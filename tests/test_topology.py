@@ -340,6 +340,56 @@ def test_filter_taint_honor_drops_intolerable_domain_from_minimum():
     assert lib.validate(p)[0] == abi.GS_OK  # applied by the product too (GPU: test_gpu_topology_kats)
 
 
+def _unconstrained_pool_case(pol):
+    """NodePool "a" has no requirement and no taint, NodePool "b"
+    names us-south-3 only and carries a taint the pods do not tolerate, and
+    an existing node in us-south-1 has room for every pod.  <U>
+    buildDomainGroups combines each NodePool's requirements with each of its
+    instance types'; the IBM instance types carry no zone requirement
+    (pkg/providers/common/instancetype/instancetype.go:719-724), so "a"
+    provides no zone domain and us-south-3's only provider is intolerable"""
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}, "node_taints_policy": pol}
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("a")
+    b.add_nodepool("b", requirements=[(Z, "In", synth.FAKE_ZONES[2:])], taints=[("dedicated", "x", "NoSchedule")])
+    b.add_node("n0", {Z: "us-south-1", H: "n0"}, {"cpu": 64000, "memory": 64 << 40, "pods": 100_000})
+    for i in range(4):
+        b.add_pod(f"p{i}", i, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    return b.build()
+
+
+def test_taint_honor_unconstrained_pool_provides_no_domain():
+    """Honor: us-south-3 leaves domainMinCount, so the minimum is the node's
+    zone's own count and every pod joins n0; Ignore keeps us-south-3 (count 0)
+    in the minimum, so n0 and NodeClaims in us-south-3 (through the
+    unconstrained NodePool "a") alternate"""
+    st, res, _ = pyoracle.solve(_unconstrained_pool_case("Honor"))
+    assert st == abi.GS_OK and not res["errors"] and not res["claims"]
+    assert res["nodes"][0] == [0, 1, 2, 3]
+    st, res, _ = pyoracle.solve(_unconstrained_pool_case("Ignore"))
+    assert st == abi.GS_OK and res["nodes"][0] == [0, 2]
+    assert sorted(p for pods, z in _zones(res) for p in pods if z == "us-south-3") == [1, 3]
+    for pol in ("Honor", "Ignore"):
+        assert lib.validate(_unconstrained_pool_case(pol)) == (abi.GS_OK, "")
+
+
+def test_ambiguous_domain_universe_refused():
+    """a NodePool NotIn on the spread key (buildDomainGroups would insert the
+    excluded values) and instance types with a zone requirement (their values
+    would enter the universe) are refused by oracle and product alike"""
+    sp = {"key": Z, "max_skew": 1, "selector": {"labels": {"app": "web"}}}
+    b = ProblemBuilder()
+    synth.build_catalog(b, synth.FAKE_PROFILES, synth.FAKE_ZONES, spot=False,
+                        prices=synth.price_table(synth.FAKE_PROFILES))
+    b.add_nodepool("a", requirements=[(Z, "NotIn", synth.FAKE_ZONES[2:])])
+    b.add_pod("p0", 0, {"cpu": 500, "memory": 1 << 30, "pods": 1000}, labels={"app": "web"}, spreads=[sp])
+    assert pyoracle.solve(b.build())[0] == abi.GS_E_UNSUPPORTED
+    st, msg = lib.validate(b.build())
+    assert st == abi.GS_E_UNSUPPORTED and "NotIn" in msg
+
+
 def test_taint_honor_counted_pod_tolerating_more_than_owner_refused():
     """a counted pod that tolerates a taint the owner does not may land where
     upstream does not count it: refused (the oracle computes it)"""
@@ -646,6 +696,8 @@ def test_gpu_topology_kats(solver):
         _check(solver, _np_case(npools, node_pool=node_pool))
     _check(solver, _tainted_node_case("Honor"))
     _check(solver, _tainted_pool_case("Honor"))
+    for pol in ("Honor", "Ignore"):
+        _check(solver, _unconstrained_pool_case(pol))
     _check(solver, _family_counted_case({"karpenter-ibm.sh/instance-family": "bx2"}))
     _check(solver, _base(n_pods=5, spread={"key": H, "max_skew": 2, "selector": {"labels": {"app": "web"}}}).build())
 
