@@ -515,7 +515,7 @@ __device__ __forceinline__ void topo_init(const DP& d, const TopoS& ts, uint64_t
   for (uint32_t k = i; k < d.TGZ * d.ZS; k += stride) ts.zcnt[k] = d.zcnt0[k];
   for (uint32_t k = i; k < d.TGZ; k += stride) ts.known[k] = known0;
   for (uint32_t k = i; k < d.TGH; k += stride) ts.htot[k] = d.htot0[k];
-  if (i == 0) ts.lazy[0] = 0;
+  if (i == 0 && (d.TGZ || d.TGH)) ts.lazy[0] = 0;  // no groups: no topology LDS (topo_lds_bytes)
 }
 
 // <U> Topology.Update after Relax: the lazy groups the pod's new variant

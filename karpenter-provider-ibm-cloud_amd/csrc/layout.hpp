@@ -146,7 +146,8 @@ __host__ __device__ inline uint32_t wave_node_lds_bytes(uint32_t nn) { return nn
 
 // LDS bytes of the Solve kernels' topology state: known domains [TGZ] u64,
 // per-owned-group minimum counts [OWNMAX] i64, zone counts [TGZ][ZS] i32,
-// hostname totals [TGH] i32
+// hostname totals [TGH] i32, the lazy groups' mask u64 and minDomains [64]
+// i32 (none of it without groups)
 __host__ __device__ inline uint32_t topo_lds_bytes(uint32_t tgz, uint32_t zs, uint32_t tgh) {
   if (!tgz && !tgh) return 0;
   return ((tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u) + 8u + 64u * 4u;  // + lazy mask, minDomains
