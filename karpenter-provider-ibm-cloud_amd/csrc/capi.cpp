@@ -39,7 +39,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     // (single-wave kernel) the existing nodes' slack codes
     // (the block kernel's capacity; the single-wave kernel's is smaller by the
     // node codes -- a Solve that outgrows it reruns on the block kernel)
-    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) + 8;
+    const uint32_t other = gsk_ffd_lds_bytes(0, (uint32_t)e.thr_val.size(), 0, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH, e.n_lazy)) + 8;
     const uint32_t dyn = std::min(gsk_ffd_dyn_lds_max(), gsk_ffdw_dyn_lds_max());
     auto claims_fit = [&](uint32_t extra) {
       const uint32_t fit = dyn > other + extra ? (dyn - other - extra) / 23 : 0;
@@ -123,11 +123,10 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
   c->upload(d.tgroups, e.tgroups);
   c->upload(d.tg_list, e.tg_list);
   d.n_lazy = e.n_lazy;
-  c->upload(d.var_lazy, e.var_lazy);
   c->upload(d.lazy_slot, e.lazy_slot);
-  d.lazy_host = e.lazy_host;
-  c->upload(d.var_lmind_off, e.var_lmind_off);
-  c->upload(d.lmind, e.lmind);
+  c->upload(d.var_lz_off, e.var_lz_off);
+  c->upload(d.lz_idx, e.lz_idx);
+  c->upload(d.lz_mind, e.lz_mind);
   c->upload(d.zcnt0, e.zcnt0);
   c->upload(d.htot0, e.htot0);
   c->upload(d.zone_order, e.zone_order);

@@ -316,7 +316,7 @@ gs_status plan_sims(gs_ctx* c, const gs_consolidation* in, std::string* err) {
     return GS_E_CAPACITY;
   }
   const uint32_t lds = gsk_ffd_lds_bytes(std::max<uint32_t>(sp.max_pods, 1), (uint32_t)e.thr_val.size(),
-                                         (e.NN + 31) / 32, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH)) +
+                                         (e.NN + 31) / 32, gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH, e.n_lazy)) +
                        8u * gsd::ovh_slots_for(sp.ov_cap);
   if (lds > gsk_ffd_dyn_lds_max()) {
     *err = "simulation exceeds the workgroup LDS (pods per simulation or state nodes)";

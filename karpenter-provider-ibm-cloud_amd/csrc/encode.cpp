@@ -1272,10 +1272,10 @@ struct Ctx {
   // pod the selection list (layout.hpp VarRec own_off / sel_off)
   void build_topology() {
     e.TG = (uint32_t)groups.size();
-    e.var_lazy.assign(1, 0);
-    e.lazy_slot.assign(64, 0);
-    e.var_lmind_off.assign(1, 0);
-    e.lmind.assign(1, 0);
+    e.lazy_slot.assign(1, 0);
+    e.var_lz_off.assign(2, 0);
+    e.lz_idx.assign(1, 0);
+    e.lz_mind.assign(1, 0);
     if (!e.TG) return;
     const Vocab& zv = e.keys[e.k_dom].vocab;
     bool any_zone = false;
@@ -1401,7 +1401,7 @@ struct Ctx {
                                              " label beside a pod owning several topology groups on that key"};
         }
     }
-    if (gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH) > 64u * 1024u)
+    if (gsd::topo_lds_bytes(e.TGZ, e.ZS, e.TGH, n_lazy) > 64u * 1024u)
       throw Fail{GS_E_UNSUPPORTED, "topology group state exceeds 64 KiB of LDS (zone groups x zones)"};
     e.zcnt0.assign((size_t)std::max<uint32_t>(e.TGZ, 1) * e.ZS, 0);
     e.htot0.assign(std::max<uint32_t>(e.TGH, 1), 0);
@@ -1508,8 +1508,8 @@ struct Ctx {
       sel_n[s] = (uint32_t)mine.size();
       for (uint32_t g : mine) {
         selected[g] = 1;
-        if (groups[g].lazy)  // slots < 4096: the lazy index rides in bits 16..21
-          e.tg_list.push_back(e.tgroups[g].slot | (groups[g].lazy_idx << 16) | ((e.tgroups[g].kind | gsd::TK_LAZY) << 24));
+        if (groups[g].lazy)  // slots and lazy indices < 4096: slot in bits 0..11, lazy index in 12..23
+          e.tg_list.push_back(e.tgroups[g].slot | (groups[g].lazy_idx << 12) | ((e.tgroups[g].kind | gsd::TK_LAZY) << 24));
         else
           e.tg_list.push_back(e.tgroups[g].slot | (e.tgroups[g].kind << 24));
       }
@@ -1534,30 +1534,36 @@ struct Ctx {
     // per device variant: the lazy groups a pod owns once it relaxes into it
     // (the kernels activate them at that Relax)
     e.n_lazy = n_lazy;
-    e.lazy_host = 0;
-    e.lazy_slot.assign(64, 0);
+    e.lazy_slot.assign(std::max<uint32_t>(n_lazy, 1), 0);
     for (uint32_t g = 0; g < e.TG; g++)
-      if (groups[g].lazy) {
-        e.lazy_slot[groups[g].lazy_idx] = e.tgroups[g].slot;
-        if (e.tgroups[g].kind & gsd::TK_HOST) e.lazy_host |= 1ull << groups[g].lazy_idx;
-      }
-    e.var_lazy.assign(n_lazy ? e.V : 1, 0);
-    e.var_lmind_off.assign(n_lazy ? e.V : 1, 0);
-    e.lmind.assign(1, 0);
+      if (groups[g].lazy)
+        e.lazy_slot[groups[g].lazy_idx] = e.tgroups[g].slot | ((e.tgroups[g].kind & gsd::TK_HOST) ? gsd::LZ_HOST : 0u);
     if (n_lazy) {
-      // per spec variant its lazy groups' minDomains in lazy-index order
-      std::vector<uint32_t> sv_off(e.variants.size(), 0);
+      // per spec variant its lazy groups (ascending, unique) with its
+      // minDomains for each; device variants share their spec variant's run
+      std::vector<uint32_t> sv_off(e.variants.size() + 1, 0);
+      e.lz_idx.clear();
+      e.lz_mind.clear();
       for (size_t sv = 0; sv < e.variants.size(); sv++) {
         auto lm = e.variants[sv].lazy_mind;
         std::sort(lm.begin(), lm.end());
-        lm.erase(std::unique(lm.begin(), lm.end(), [](auto& a, auto& b) { return a.first == b.first; }), lm.end());
-        sv_off[sv] = (uint32_t)e.lmind.size();
-        for (auto& x : lm) e.lmind.push_back(x.second);
+        lm.erase(std::unique(lm.begin(), lm.end(), [](auto& x, auto& y) { return x.first == y.first; }), lm.end());
+        sv_off[sv] = (uint32_t)e.lz_idx.size();
+        for (auto& x : lm) {
+          e.lz_idx.push_back(x.first);
+          e.lz_mind.push_back(x.second);
+        }
+        sv_off[sv + 1] = (uint32_t)e.lz_idx.size();
       }
+      // device variant v: [var_lz_off[2v], var_lz_off[2v + 1])
+      e.var_lz_off.assign(2 * (size_t)e.V, 0);
       for (uint32_t v = 0; v < e.V; v++) {
-        for (uint32_t g : e.variants[e.var_sv[v]].own)
-          if (groups[g].lazy) e.var_lazy[v] |= 1ull << groups[g].lazy_idx;
-        e.var_lmind_off[v] = sv_off[e.var_sv[v]];
+        e.var_lz_off[2 * (size_t)v] = sv_off[e.var_sv[v]];
+        e.var_lz_off[2 * (size_t)v + 1] = sv_off[e.var_sv[v] + 1];
+      }
+      if (e.lz_idx.empty()) {
+        e.lz_idx.assign(1, 0);
+        e.lz_mind.assign(1, 0);
       }
     }
   }
@@ -2302,7 +2308,8 @@ struct Ctx {
           // (a hostname group also lacks the in-flight NodeClaims registered
           // before it: the kernels mark those HC_UNKNOWN when it is created)
           if (groups.size() >= (size_t)gsd::TGMAX) throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology groups"};
-          if (n_lazy >= 64) throw Fail{GS_E_UNSUPPORTED, "more than 64 topology spread groups created by relaxation"};
+          if (n_lazy >= (uint32_t)gsd::TGMAX)
+            throw Fail{GS_E_UNSUPPORTED, "more than 4096 topology spread groups created by relaxation"};
           f = group_idx.emplace(w.st_hash[st][k], (uint32_t)groups.size()).first;
           groups.push_back(GroupEnc{sp, pns});
           GroupEnc& g = groups.back();

@@ -147,12 +147,11 @@ struct Encoded {
   std::vector<uint32_t> tg_list;     // own / selection list arena
   std::vector<int32_t> zcnt0;        // [TGZ][ZS]
   std::vector<int32_t> htot0;        // [TGH]
-  uint32_t n_lazy = 0;               // spread groups Topology.Update creates on a relaxation
-  std::vector<uint64_t> var_lazy;    // [V] (or [1]): the lazy groups a variant owns
-  std::vector<uint32_t> lazy_slot;   // [64] slot per lazy index
-  std::vector<uint32_t> var_lmind_off;  // [V] (or [1]): offset of the variant's lazy minDomains in lmind
-  std::vector<int32_t> lmind;        // per variant, one minDomains per set bit of var_lazy (ascending)
-  uint64_t lazy_host = 0;            // lazy groups on the hostname key
+  uint32_t n_lazy = 0;               // spread groups Topology.Update creates on a relaxation (<= TGMAX)
+  std::vector<uint32_t> lazy_slot;   // [n_lazy] slot | LZ_HOST for hostname groups
+  std::vector<uint32_t> var_lz_off;  // [V + 1] (or [2]): CSR of the lazy groups each variant owns
+  std::vector<uint32_t> lz_idx;      // their lazy indices
+  std::vector<int32_t> lz_mind;      // and this variant's minDomains for each (the creator's, at the Relax)
   std::vector<uint32_t> zone_order;  // zone vocabulary ids by name
   std::vector<uint32_t> zone_cat;    // [64]
   std::vector<int32_t> hn0;          // [TGH][NN]

@@ -610,11 +610,11 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
   uint32_t* const ov_map = SIM ? d.ov_map + (size_t)blockIdx.x * d.NN : nullptr;
   // topology: known domains, per-pod minimum counts, zone counts, hostname totals
   const uint32_t tg_off = (((23u * MC + 7u) & ~7u) + (nthr + 4u) * 8u + d.nb_words * 4u + 7u) & ~7u;
-  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH, d.n_lazy);
   // SIM, small simulations: node -> overlay entry in an LDS hash (keys node + 1,
   // open addressing), after the topology state
   const uint32_t ovh = SIM ? d.ovh_slots : 0u, ovh_mask = ovh - 1u;
-  uint32_t* const s_ovk = (uint32_t*)((char*)lds64 + ((tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u));
+  uint32_t* const s_ovk = (uint32_t*)((char*)lds64 + ((tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH, d.n_lazy) + 7u) & ~7u));
   uint32_t* const s_ovv = s_ovk + ovh;
   // SIM with d.sim_lds: each simulation's queue, staleness (last epoch /
   // length), current variant and add log in LDS after the hash (4 x u32 +
@@ -1803,11 +1803,7 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         if (v + 1 < d.var_begin[gp] + d.var_count[gp]) {
           cur_var[p] = v + 1;
           relaxed = true;
-          if (TOPO && d.n_lazy) {
-            const uint64_t fresh = topo_relaxed(d, ts, v + 1);
-            topo_mark_unknown(d, fresh, d.hc + (size_t)(SIM ? qoff : 0u) * d.TGH, M, 0u, 1u);
-            topo_activate(d, ts, v + 1, fresh);
-          }
+          if (TOPO && d.n_lazy) topo_relaxed(d, ts, v + 1, d.hc + (size_t)(SIM ? qoff : 0u) * d.TGH, M, 0u, 1u);
         }
         uint32_t tail = HN.qhead + HN.qlen;
         if (tail >= P) tail -= P;
@@ -1838,15 +1834,14 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
         int32_t* hrow = d.hc + (size_t)(qoff + l.target) * d.TGH;
         for (uint32_t k = 0; k < lv.sel_n; k++) {
           const uint32_t e = d.tg_list[lv.sel_off + k];
-          if ((e >> 24) & TK_HOST) hrow[e & (((e >> 24) & TK_LAZY) ? 0xFFFFu : 0xFFFFFFu)] = 0;
+          if ((e >> 24) & TK_HOST) hrow[e & (((e >> 24) & TK_LAZY) ? 0xFFFu : 0xFFFFFFu)] = 0;
         }
       }
       // and the cells a lazy hostname group created in this simulation marked
       // HC_UNKNOWN on the NodeClaims that existed before it
-      const uint64_t lz = ts.lazy[0] & d.lazy_host;
-      if (lz) {
+      if (d.n_lazy) {
         __syncthreads();
-        topo_mark_unknown(d, lz, d.hc + (size_t)qoff * d.TGH, S.hb[par ^ 1u].M, tid, FB, 0);
+        topo_unmark(d, ts, d.hc + (size_t)qoff * d.TGH, S.hb[par ^ 1u].M, tid, FB);
       }
     }
     if (SIM) {
@@ -2001,7 +1996,7 @@ extern "C" uint32_t gsk_ffd_sim_blocks_per_cu(uint32_t R, uint32_t lds, uint32_t
 // grid: 1 workgroup (provisioning Solve) or `blocks` persistent workgroups
 // draining the simulation counter (consolidation)
 extern "C" hipError_t gsk_ffd(const DevProblem* d, uint32_t blocks, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+  const uint32_t lds = gsk_ffd_lds_bytes(d->max_claims, d->n_thr, d->nb_words, topo_lds_bytes(d->TGZ, d->ZS, d->TGH, d->n_lazy)) +
                        (d->n_sims ? 8u * d->ovh_slots + (d->sim_lds ? 32u * d->max_claims : 0u) : 0u);
   if (lds > g_ffd_dyn_max) return hipErrorInvalidConfiguration;
   const bool sim = d->n_sims > 0;

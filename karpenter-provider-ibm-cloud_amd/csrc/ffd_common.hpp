@@ -495,17 +495,17 @@ struct TopoS {
   int64_t* tmin;    // [OWNMAX]
   int32_t* zcnt;    // [TGZ][ZS]
   int32_t* htot;    // [TGH]
-  uint64_t* lazy;   // [1] the lazy groups (TK_LAZY) some pod has relaxed into
-  int32_t* lmind;   // [64] their minDomains (the creating pod's)
+  uint64_t* lazy;   // [(n_lazy + 63) / 64] the lazy groups (TK_LAZY) some pod has relaxed into
+  int32_t* lmind;   // [n_lazy] their minDomains (the creating pod's)
 };
-__device__ __forceinline__ TopoS topo_lds(char* base, uint32_t tgz, uint32_t zs, uint32_t tgh) {
+__device__ __forceinline__ TopoS topo_lds(char* base, uint32_t tgz, uint32_t zs, uint32_t tgh, uint32_t nl) {
   TopoS t;
   t.known = (uint64_t*)base;
   t.tmin = (int64_t*)(base + tgz * 8u);
   t.zcnt = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u);
   t.htot = (int32_t*)(base + tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u);
-  t.lazy = (uint64_t*)(base + topo_lds_bytes(tgz, zs, tgh) - 8u - 64u * 4u);
-  t.lmind = (int32_t*)(base + topo_lds_bytes(tgz, zs, tgh) - 64u * 4u);
+  t.lazy = (uint64_t*)(base + topo_lazy_off(tgz, zs, tgh));
+  t.lmind = (int32_t*)(base + topo_lazy_off(tgz, zs, tgh) + ((nl + 63u) / 64u) * 8u);
   return t;
 }
 
@@ -515,37 +515,43 @@ __device__ __forceinline__ void topo_init(const DP& d, const TopoS& ts, uint64_t
   for (uint32_t k = i; k < d.TGZ * d.ZS; k += stride) ts.zcnt[k] = d.zcnt0[k];
   for (uint32_t k = i; k < d.TGZ; k += stride) ts.known[k] = known0;
   for (uint32_t k = i; k < d.TGH; k += stride) ts.htot[k] = d.htot0[k];
-  if (i == 0 && (d.TGZ || d.TGH)) ts.lazy[0] = 0;  // no groups: no topology LDS (topo_lds_bytes)
+  for (uint32_t k = i; k < (d.n_lazy + 63u) / 64u; k += stride) ts.lazy[k] = 0;
 }
 
 // <U> Topology.Update after Relax: the lazy groups the pod's new variant
-// owns and no pod created before exist from now on (Record counts into them;
-// the caller sets ts.lazy).  Returns them
+// owns that no pod created before exist from now on, with that pod's
+// minDomains: Record counts into them, and the in-flight NodeClaims [0, M)
+// are no domains of the hostname ones among them (Topology.Register ran
+// before the group existed).  i / stride: this thread's share of the marks;
+// thread i == 0 sets the created bits (the caller orders the threads: a
+// wave's own program order, or a barrier)
 template <class DP>
-__device__ __forceinline__ uint64_t topo_relaxed(const DP& d, const TopoS& ts, uint32_t new_var) {
-  return d.n_lazy ? d.var_lazy[new_var] & ~ts.lazy[0] : 0ull;
-}
-// ... which exist from now on, with the minDomains of the variant that
-// created them (one thread)
-template <class DP>
-__device__ __forceinline__ void topo_activate(const DP& d, const TopoS& ts, uint32_t new_var, uint64_t fresh) {
-  const uint64_t all = d.var_lazy[new_var];
-  const uint32_t off = d.var_lmind_off[new_var];
-  for (uint64_t x = fresh; x; x &= x - 1) {
-    const uint32_t b = (uint32_t)__ffsll((long long)x) - 1u;
-    ts.lmind[b] = d.lmind[off + (uint32_t)__popcll(all & ((1ull << b) - 1ull))];
+__device__ __forceinline__ void topo_relaxed(const DP& d, const TopoS& ts, uint32_t new_var, int32_t* hc_rows, uint32_t M,
+                                             uint32_t i, uint32_t stride) {
+  const uint32_t b = d.var_lz_off[2u * new_var], e = d.var_lz_off[2u * new_var + 1u];
+  for (uint32_t k = b; k < e; k++) {
+    const uint32_t li = d.lz_idx[k];
+    if ((ts.lazy[li >> 6] >> (li & 63u)) & 1ull) continue;
+    const uint32_t s = d.lazy_slot[li];
+    if (s & LZ_HOST)
+      for (uint32_t j = i; j < M; j += stride) hc_rows[(size_t)j * d.TGH + (s & 0xFFFFu)] = HC_UNKNOWN;
+    if (i == 0) {
+      ts.lmind[li] = d.lz_mind[k];
+      ts.lazy[li >> 6] |= 1ull << (li & 63u);
+    }
   }
-  ts.lazy[0] |= fresh;
 }
-// ... and the in-flight NodeClaims [0, M) are no domains of the new hostname
-// groups among them (i / stride: this thread's share)
+// a simulation's end: the cells topo_relaxed marked go back to zero (the
+// NodeClaims' hostname rows are zero at rest)
 template <class DP>
-__device__ __forceinline__ void topo_mark_unknown(const DP& d, uint64_t fresh, int32_t* hc_rows, uint32_t M, uint32_t i,
-                                                  uint32_t stride, int32_t value = HC_UNKNOWN) {
-  for (uint64_t x = fresh & d.lazy_host; x; x &= x - 1) {
-    const uint32_t slot = d.lazy_slot[(uint32_t)__ffsll((long long)x) - 1u];
-    for (uint32_t j = i; j < M; j += stride) hc_rows[(size_t)j * d.TGH + slot] = value;
-  }
+__device__ __forceinline__ void topo_unmark(const DP& d, const TopoS& ts, int32_t* hc_rows, uint32_t M, uint32_t i,
+                                            uint32_t stride) {
+  for (uint32_t w = 0; w < (d.n_lazy + 63u) / 64u; w++)
+    for (uint64_t x = ts.lazy[w]; x; x &= x - 1) {
+      const uint32_t s = d.lazy_slot[w * 64u + (uint32_t)__ffsll((long long)x) - 1u];
+      if (s & LZ_HOST)
+        for (uint32_t j = i; j < M; j += stride) hc_rows[(size_t)j * d.TGH + (s & 0xFFFFu)] = 0;
+    }
 }
 
 // domainMinCount of every owned zone spread group over the pod's strict zone
@@ -703,8 +709,9 @@ __device__ __forceinline__ void topo_record_g(const DP& d, const TopoS& ts, uint
     uint32_t slot = e & 0xFFFFFFu;
     const uint32_t kind = e >> 24;
     if (kind & TK_LAZY) {
-      if (!((ts.lazy[0] >> ((e >> 16) & 63u)) & 1ull)) continue;  // not created yet
-      slot = e & 0xFFFFu;
+      const uint32_t li = (e >> 12) & 0xFFFu;
+      if (!((ts.lazy[li >> 6] >> (li & 63u)) & 1ull)) continue;  // not created yet
+      slot = e & 0xFFFu;
     }
     if (kind & TK_HOST) {
       hinc(slot);

@@ -58,7 +58,7 @@ extern "C" uint32_t gsk_ffdw_dyn_lds_max(void) { return g_ffdw_dyn_max; }
 // the single-wave provisioning Solve: grid-wide state reset, then one wave;
 // ch: the claim scan state in HBM (d->ch_* allocated, claim_cap slots)
 extern "C" hipError_t gsk_ffdw(const DevProblem* d, uint32_t ch, hipStream_t s) {
-  const uint32_t lds = gsk_ffd_lds_bytes(ch ? 0u : d->max_claims_wave, d->n_thr, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH)) +
+  const uint32_t lds = gsk_ffd_lds_bytes(ch ? 0u : d->max_claims_wave, d->n_thr, 0, topo_lds_bytes(d->TGZ, d->ZS, d->TGH, d->n_lazy)) +
                        wave_node_lds_bytes(d->NN);
   if (lds > g_ffdw_dyn_max) return hipErrorInvalidConfiguration;
   if (d->n_sims) return hipErrorInvalidValue;

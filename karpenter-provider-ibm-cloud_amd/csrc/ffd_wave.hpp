@@ -701,11 +701,11 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     __builtin_assume(W <= WREG);
   const uint32_t nthr = d.thr_off[R];
   const uint32_t tg_off = (thr_base + (nthr + 4u) * 8u + 7u) & ~7u;
-  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH);
+  const TopoS ts = topo_lds((char*)lds64 + tg_off, d.TGZ, d.ZS, d.TGH, d.n_lazy);
   // existing nodes (wave_node_lds_bytes): slack codes (upper bound), room
   // codes (lower bound) of available - requests per resource 0..3, and a
   // flag byte: bit 0 = plain (ok, no taints, resources 4.. not over)
-  const uint32_t nd_off = (tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH) + 7u) & ~7u;
+  const uint32_t nd_off = (tg_off + topo_lds_bytes(d.TGZ, d.ZS, d.TGH, d.n_lazy) + 7u) & ~7u;
   uint64_t* s_nslk = (uint64_t*)((char*)lds64 + nd_off);
   uint64_t* s_nrm = (uint64_t*)((char*)lds64 + nd_off + d.NN * 8u);
   uint8_t* s_nflag = (uint8_t*)((char*)lds64 + nd_off + d.NN * 16u);
@@ -2563,13 +2563,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       uint32_t tail = qhead + qlen;
       if (tail >= P) tail -= P;
       qlen++;
-      if (TOPO && relaxed && KD.n_lazy) {
-        const uint64_t fresh = topo_relaxed(KD, ts, v + 1);
-        if (fresh) {
-          topo_mark_unknown(KD, fresh, KD.hc, M, lane, 64u);
-          if (lane == 0) topo_activate(KD, ts, v + 1, fresh);
-        }
-      }
+      if (TOPO && relaxed && KD.n_lazy) topo_relaxed(KD, ts, v + 1, KD.hc, M, lane, 64u);
       if (lane == 0) {
         if (relaxed) KD.cur_var[p] = v + 1;
         KD.queue[tail] = p;

@@ -48,9 +48,10 @@ constexpr int OWNMAX = 64;     // topology groups one pod variant owns
 constexpr int ZVMAX = 64;      // zone vocabulary (topology domains) when zone groups are used
 // topology group kinds (TGroupRec.kind, and the top byte of a selection-list entry)
 // selection-list kind bits (entry >> 24); TK_LAZY: a spread group created by
-// a relaxation (Topology.Update), lazy index in entry bits 16..21, slot in
-// bits 0..15; Record skips it until some pod has relaxed into it
+// a relaxation (Topology.Update), lazy index in entry bits 12..23, slot in
+// bits 0..11; Record skips it until some pod has relaxed into it
 enum : uint32_t { TK_HOST = 1u, TK_AFF = 2u, TK_ANTI = 4u, TK_LAZY = 8u };
+constexpr uint32_t LZ_HOST = 1u << 31;  // lazy_slot: a hostname group (its slot is a column of hc)
 // a NodeClaim's count cell of a lazy hostname group created after the claim:
 // the claim is no domain of it (Topology.Register ran before the group
 // existed), so every owner check fails there; Record makes it a domain with
@@ -146,11 +147,14 @@ __host__ __device__ inline uint32_t wave_node_lds_bytes(uint32_t nn) { return nn
 
 // LDS bytes of the Solve kernels' topology state: known domains [TGZ] u64,
 // per-owned-group minimum counts [OWNMAX] i64, zone counts [TGZ][ZS] i32,
-// hostname totals [TGH] i32, the lazy groups' mask u64 and minDomains [64]
-// i32 (none of it without groups)
-__host__ __device__ inline uint32_t topo_lds_bytes(uint32_t tgz, uint32_t zs, uint32_t tgh) {
+// hostname totals [TGH] i32, then the lazy groups' created bitset and their
+// minDomains [nl] i32 (none of it without groups)
+__host__ __device__ inline uint32_t topo_lazy_off(uint32_t tgz, uint32_t zs, uint32_t tgh) {
+  return (tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u;
+}
+__host__ __device__ inline uint32_t topo_lds_bytes(uint32_t tgz, uint32_t zs, uint32_t tgh, uint32_t nl) {
   if (!tgz && !tgh) return 0;
-  return ((tgz * 8u + (uint32_t)OWNMAX * 8u + tgz * zs * 4u + tgh * 4u + 7u) & ~7u) + 8u + 64u * 4u;  // + lazy mask, minDomains
+  return topo_lazy_off(tgz, zs, tgh) + ((nl + 63u) / 64u) * 8u + ((nl * 4u + 7u) & ~7u);
 }
 
 // per-claim record (device-owned, AoS: one candidate = one 192-B record read
@@ -339,15 +343,14 @@ struct DevProblem {
   uint32_t TGZ, ZS;            // zone groups, zone-count stride (max(NZV, 1))
   uint32_t dom_ct;             // the "zone" groups' domain key is the capacity type (zone_cat -> catalog capacity types)
   uint32_t dom_np;             // ... is the NodePool (a template's fixed domain: no catalog narrowing)
-  uint32_t n_lazy;             // spread groups created by relaxations (<= 64)
+  uint32_t n_lazy;             // spread groups created by relaxations (<= TGMAX)
   uint64_t zknown0;            // zone domains known before the Solve (universe + counted), every zone group
   const TGroupRec* tgroups;    // [TG]
   const uint32_t* tg_list;     // own / selection list arena (VarRec own_off / sel_off)
-  const uint64_t* var_lazy;    // [V] (n_lazy > 0): the lazy groups a variant owns, activated when a pod relaxes into it
-  const uint32_t* lazy_slot;   // [64] a lazy group's slot (hostname groups: column in hc)
-  uint64_t lazy_host;          // the lazy groups on the hostname key
-  const uint32_t* var_lmind_off;  // [V] the variant's lazy minDomains in lmind (one per set bit of var_lazy)
-  const int32_t* lmind;
+  const uint32_t* lazy_slot;   // [n_lazy] slot | LZ_HOST
+  const uint32_t* var_lz_off;  // [2V]: variant v owns the lazy groups lz_idx[var_lz_off[2v] .. var_lz_off[2v + 1])
+  const uint32_t* lz_idx;
+  const int32_t* lz_mind;      // the variant's minDomains for each (a group takes its creator's)
   const int32_t* zcnt0;        // [TGZ][ZS] zone counts before the Solve
   const int32_t* htot0;        // [TGH] hostname groups: counted pods over all domains before the Solve
   const uint32_t* zone_order;  // [NZV] zone vocabulary ids in name order (omega excluded)
