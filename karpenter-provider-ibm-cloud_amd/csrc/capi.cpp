@@ -109,6 +109,7 @@ void upload_problem(gs_ctx* c, const SimPlan* sims) {
     c->alloc(d.qvars, std::max<uint32_t>(e.P, 1));
     c->alloc(d.qreqs, (size_t)std::max<uint32_t>(e.P, 1) * std::max<uint32_t>(e.R, 1));
     c->alloc(d.qcodes, (size_t)std::max<uint32_t>(e.P, 1) * 4);
+    c->alloc(d.qrun, std::max<uint32_t>(e.P, 1));
   }
   d.NN = e.NN;
   // topology spread groups

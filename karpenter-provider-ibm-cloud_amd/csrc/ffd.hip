@@ -2058,8 +2058,31 @@ __global__ __launch_bounds__(256) void queue_records_kernel(DevProblem d) {
   ((uint4*)const_cast<uint32_t*>(d.qcodes))[k] = c;
 }
 
+// qrun[k]: how many records from k on (at most the ring's 16) equal record k
+// in every dword the wave Solve's run mode compares (all but the pod and the
+// variant index): the batch of a run's pods reads it from the ring
+// (ffd_wave.hpp GS_RUN_BATCH) instead of comparing 16 staged records
+__device__ __forceinline__ bool queue_record_same(const DevProblem& d, uint32_t a, uint32_t b) {
+  const uint32_t* va = (const uint32_t*)(d.qvars + a);
+  const uint32_t* vb = (const uint32_t*)(d.qvars + b);
+  for (uint32_t i = 1; i < sizeof(VarRec) / 4 - 1; i++)
+    if (va[i] != vb[i]) return false;
+  for (uint32_t r = 0; r < d.R; r++)
+    if (d.qreqs[(size_t)a * d.R + r] != d.qreqs[(size_t)b * d.R + r]) return false;
+  // the codes follow from the requests
+  return true;
+}
+__global__ __launch_bounds__(256) void queue_runs_kernel(DevProblem d) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= d.P) return;
+  uint32_t n = 1;
+  while (n < 16 && k + n < d.P && queue_record_same(d, k, k + n)) n++;
+  const_cast<uint32_t*>(d.qrun)[k] = n;
+}
+
 extern "C" hipError_t gsk_queue_records(const DevProblem* d, hipStream_t s) {
   if (!d->P) return hipSuccess;
   hipLaunchKernelGGL(queue_records_kernel, dim3((d->P + 255) / 256), dim3(256), 0, s, *d);
+  hipLaunchKernelGGL(queue_runs_kernel, dim3((d->P + 255) / 256), dim3(256), 0, s, *d);
   return hipGetLastError();
 }

@@ -57,8 +57,9 @@ constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
 #endif
 // solver <-> memory-agent wave channels (LDS)
 constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the solver
-constexpr uint32_t RING_DW = 52; // VarRec (32 dwords) + requests (<= 16 dwords) + request codes (4 dwords)
+constexpr uint32_t RING_DW = 53; // VarRec (32 dwords) + requests (<= 16 dwords) + request codes (4 dwords) + qrun
 constexpr uint32_t RING_CODES = 48;  // lanes 48..51: floor codes lo/hi dword, ceil codes lo/hi dword
+constexpr uint32_t RING_QRUN = 52;   // lane 52: qrun (records from here on with this one's spec, <= 16)
 constexpr uint32_t WQ = 32;      // global-memory write requests in flight
 constexpr uint32_t WQ_DW = 16;
 enum : uint32_t { WQ_LOG = 1, WQ_FA = 2, WQ_STOP = 3, WQ_NFA = 4 };
@@ -609,6 +610,74 @@ struct WaveSort {
   }
 };
 
+// The run batch's placement (GS_RUN_BATCH, the pod loop below): out of line,
+// so its registers do not weigh on the rest of the loop.  Pods 2..k of the
+// batch (lane j < k: pod bp / variant bv) join the claims U_1..U_{k-1} at
+// lanes fl + 1..; returns the window after the k - 1 rotations
+struct RunWin {
+  uint32_t ow, wtok;
+  uint64_t wsl, wrm;
+};
+template <uint32_t RR>
+__device__ __noinline__ RunWin run_batch_place(RunWin w, uint64_t rq, uint32_t bp, uint32_t bv, uint32_t fl, uint32_t m,
+                                               uint32_t k, uint32_t nlog, uint32_t rqn, LogRec* log, ClaimRec* c_rec) {
+  const uint32_t lane = threadIdx.x & 63u;
+  fl = __builtin_amdgcn_readfirstlane(fl);
+  m = __builtin_amdgcn_readfirstlane(m);
+  k = __builtin_amdgcn_readfirstlane(k);
+  nlog = __builtin_amdgcn_readfirstlane(nlog);
+  rqn = __builtin_amdgcn_readfirstlane(rqn);
+  // lane j < k: its pod's log entry (claim U_j); lanes 4i + r:
+  // pod i + 2's request r into U_{i+1}'s totals
+  const uint32_t cj = (uint32_t)__shfl((int)w.ow, (int)((fl + lane) & 63u)) >> 16;
+  if (lane >= 1 && lane < k) log[nlog + lane - 1] = LogRec{bp, bv, cj, 0};
+  {
+    const uint32_t j = 1u + (lane >> 2), r = lane & 3u;
+    const uint32_t ci = (uint32_t)__shfl((int)w.ow, (int)((fl + j) & 63u)) >> 16;
+    const int64_t rqr = (int64_t)shfl_u64(rq, r);
+    if (j < k && r < RR && rqr != 0)
+      atomicAdd((unsigned long long*)&c_rec[ci].tot_lo[r], (unsigned long long)rqr);
+  }
+  // lanes 4i + r re-quantize resource r of U_{i+1} (as this
+  // pod's lanes r did for U_0), packed across the quad with
+  // DPP and moved back to U_{i+1}'s lane
+  {
+    const uint32_t i = lane >> 2, r = lane & 3u, src_l = (fl + 1u + i) & 63u;
+    const uint64_t rm_i = shfl_u64(w.wrm, src_l), sl_i = shfl_u64(w.wsl, src_l);
+    uint32_t q_rm = 0, q_sl = 0;
+    if (r < rqn) {
+      const int64_t rqr = (int64_t)shfl_u64(rq, r);
+      q_rm = qcode_floor(qcode_value((uint32_t)(rm_i >> (16 * r)) & 0xFFFFu) - rqr);
+      q_sl = qcode_ceil(qcode_value((uint32_t)(sl_i >> (16 * r)) & 0xFFFFu) - rqr);
+    }
+    uint32_t prm2 = (lane & 1u) ? q_rm << 16 : q_rm, psl2 = (lane & 1u) ? q_sl << 16 : q_sl;
+    prm2 |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm2, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    psl2 |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl2, 0xB1, 0xF, 0xF, false);
+    const uint32_t hrm2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)prm2, 0x102, 0xF, 0xF, false);  // row_shl:2
+    const uint32_t hsl2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)psl2, 0x102, 0xF, 0xF, false);
+    // lane 4i now holds U_{i+1}'s packed codes (lo dword, hi dword)
+    const uint32_t back = 4u * ((lane - fl - 1u) & 15u);
+    const uint32_t rm_lo = (uint32_t)__shfl((int)prm2, (int)back), rm_hi = (uint32_t)__shfl((int)hrm2, (int)back);
+    const uint32_t sl_lo = (uint32_t)__shfl((int)psl2, (int)back), sl_hi = (uint32_t)__shfl((int)hsl2, (int)back);
+    if (lane > fl && lane < fl + k) {
+      w.wrm = ((uint64_t)rm_hi << 32) | rm_lo;
+      w.wsl = ((uint64_t)sl_hi << 32) | sl_lo;
+      w.ow = w.ow + 1u;
+    }
+  }
+  // the window after k - 1 rotations with the k-th pending:
+  // lane fl holds U_{k-1}, then U_k..U_{m-1} (count c), then
+  // U_{k-2}..U_0 (count c + 1, each placed in front of the last)
+  const uint32_t rel = lane - fl;
+  uint32_t src = lane;
+  if (lane >= fl && lane < fl + m) src = fl + (rel == 0 ? k - 1 : (rel <= m - k ? k - 1 + rel : m - 1 - rel));
+  w.ow = (uint32_t)__shfl((int)w.ow, (int)src);
+  w.wsl = shfl_u64(w.wsl, src);
+  w.wrm = shfl_u64(w.wrm, src);
+  w.wtok = (uint32_t)__shfl((int)w.wtok, (int)src);
+  return w;
+}
+
 // The generic sort's one out-of-line body: the members arrive as scalar
 // arguments and the sorter is rebuilt locally, so they stay in registers (a
 // member function would reload them through a `this` pointer in scratch
@@ -795,6 +864,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
             if (lane < VR_DW) val[i] = qv_dw[k * VR_DW + lane];
             else if (lane < 32 + 2 * R) val[i] = qr_dw[k * 2 * R + (lane - 32)];
             else if (lane >= RING_CODES && lane < RING_CODES + 4) val[i] = d.qcodes[k * 4 + (lane - RING_CODES)];
+            else if (lane == RING_QRUN) val[i] = d.qrun[k];
           }
         }
 #pragma unroll
@@ -916,7 +986,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   // instrumentation counters, lane k = counter k (no scalar registers)
   enum { C_GEN = 0, C_FAST, C_CAND, C_FULL, C_NEV, C_NPRE, C_FA, C_ALG,
          // run mode (diagnostics, Ctrl.dbg[8..13] outside the timeline build)
-         C_RPODS, C_RENTER, C_RX_PIVOT, C_RX_WIN, C_RX_SPEC, C_RX_SCAN, C_RX_XC };
+         C_RPODS, C_RENTER, C_RX_PIVOT, C_RX_WIN, C_RX_SPEC, C_RX_SCAN, C_RX_XC, C_RBATCH, C_RBPODS, C_RBT0, C_RBT1 };
   uint64_t ctr = 0;
 #ifdef GS_NO_CTR  // experiment builds: the counters' cost
 #define CTR(k, x) ((void)0)
@@ -965,6 +1035,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #endif
 #ifndef GS_RUN_NODES
 #define GS_RUN_NODES 1
+#endif
+#ifndef GS_RUN_BATCH  // up to RING pods of a run placed in one step
+#define GS_RUN_BATCH 1
 #endif
 #ifndef GS_RUN_WIDE  // the wide-row instantiation in run mode
 #define GS_RUN_WIDE 0
@@ -1025,7 +1098,7 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
         (d.NN == 0 || (GS_RUN_NODES && nhint_ok && nhint >= d.NN))) {
       run_prev = false;
       auto same_spec = [&](uint32_t x) {
-        return __ballot(lane >= 1 && lane < RING_DW && lane != VR_DW - 1 && x != run_rec) == 0;
+        return __ballot(lane >= 1 && lane < RING_QRUN && lane != VR_DW - 1 && x != run_rec) == 0;
       };
       if (__builtin_amdgcn_readfirstlane(pf_seq) == qhead + 1 && same_spec(pf_x)) {
         // the run's spec: tolerated templates, request codes and requests
@@ -1429,6 +1502,88 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           modkind = MOD_INC;
           modpos = f;
           lf = fl;
+#if GS_RUN_BATCH
+          // A batch of the run's next pods.  This pod
+          // joined U_0, the claim at lane fl (count c -> c + 1); U_1.. at
+          // lanes fl + 1.. are the other count-c claims (up to lane e2).
+          // sort.Slice moves U_0 behind them, so the next pod's scan (from
+          // position f: the prefix before it stays infeasible) finds U_1 at f;
+          // if U_1 is a fast accept (its bit in this scan's fab) the pod joins
+          // it, its sort.Slice is the same one rotation from the same position
+          // f (one choosePivot check for all), and so on: pod j joins U_j.
+          // While U_j is a fast accept and the ring holds the next record of
+          // the run's spec (qrun), up to 16 pods are placed here at once --
+          // log entries and request atomics lane-parallel, U_j's codes
+          // re-quantized on its own lane, the window permuted once -- and the
+          // last pod's rotation stays pending as after a single Add.
+          // Bit-identical to placing them one by one.
+          {
+#ifdef GS_RUN_TL
+            const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
+            const uint32_t c = e & 0xFFFFu;
+            const uint64_t after = __ballot(lane > fl && (ow & 0xFFFFu) > c);
+            uint32_t k = 1;
+            if (after && c + 2u < 0xFFFFu && !pivot_touched(MOD_INC, f, M)) {
+              const uint32_t m = ffs64(after) - fl;  // U_0..U_{m-1} at lanes fl..fl + m - 1
+              k = 1u + (uint32_t)__builtin_ctzll(~(fab >> (fl + 1)));
+              k = k < m ? k : m;
+              const uint32_t nrun = rlane(x_rec, RING_QRUN);
+              k = k < nrun ? k : nrun;
+              const uint32_t q1 = qhead - 1;  // this pod's queue position
+              if (q1 + k > P - 1) k = P - 1 - q1;
+              if (pops + k > max_pops) k = 1;
+              if (k >= 2) {
+                // pods 2..k (lanes j = 1..k-1, queue position q1 + j): the
+                // sequence word, pod and variant in one LDS round trip
+                const bool jl = lane >= 1 && lane < k;
+                const uint32_t slot = (q1 + lane) % RING;
+                const uint32_t sq = jl ? vld(&s_ring_seq[slot]) : 0u;
+                const uint32_t bp = jl ? vld(&s_ring[slot][0]) : 0u;
+                const uint32_t bv = jl ? vld(&s_ring[slot][VR_DW - 1]) : 0u;
+                k = 1u + (uint32_t)__builtin_ctzll(~(__ballot(jl && sq == q1 + lane + 1) >> 1));
+#ifdef GS_RUN_TL
+                const uint64_t tb1 = __builtin_amdgcn_s_memtime();
+#endif
+                if (k >= 2) {
+                  const auto& KD = *karg();
+                  RunWin rw{ow, wtok, wsl, wrm};
+                  rw = run_batch_place<RR>(rw, (uint64_t)r_rq, bp, bv, fl, m, k, nlog, d.RQ, KD.log, KD.c_rec);
+                  ow = rw.ow;
+                  wtok = rw.wtok;
+                  wsl = rw.wsl;
+                  wrm = rw.wrm;
+                  // Queue.Pop of pods 2..k: their ring slots may be refilled
+                  wsyncT<CH>();
+                  if (lane == 0) {
+                    vst(&s_ctl[0], q1 + k);
+                    vst(&s_ctl[3], (uint32_t)(pops + k - 1));
+                  }
+                  qhead = q1 + k;
+                  qlen -= k - 1;
+                  pops += k - 1;
+                  nlog += k - 1;
+                  pf_seq = vld(&s_ring_seq[qhead % RING]);
+                  pf_x = lane < RING_DW ? vld(&s_ring[qhead % RING][lane]) : 0u;
+                  CTR(C_FAST, k - 1);
+                  CTR(C_CAND, (uint64_t)(k - 1) * (M - f < 64 ? M - f : 64));
+                  CTR(C_FA, k - 1);
+                  CTR(C_ALG, (uint64_t)(k - 1) * (f + 1));
+                  CTR(C_NPRE, (uint64_t)(k - 1) * d.NN);
+                  CTR(C_RPODS, k - 1);
+                  CTR(C_RBATCH, 1);
+                  CTR(C_RBPODS, k - 1);
+#ifdef GS_RUN_TL
+                  CTR(C_RBT1, __builtin_amdgcn_s_memtime() - tb1);
+#endif
+                }
+              }
+            }
+#ifdef GS_RUN_TL
+            CTR(C_RBT0, __builtin_amdgcn_s_memtime() - tb0);
+#endif
+          }
+#endif
         }
         if (dirty) {
           // the window back to LDS: positions, and the codes of its claims
@@ -2632,6 +2787,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.dbg[14] = run_cyc;
 #else
     c.dbg[14] = ctr_run[6];  // run-mode exact batches
+#endif
+    c.dbg[5] = ctr_at(C_RBPODS);  // pods placed in run batches (GS_RUN_BATCH)
+    c.dbg[6] = ctr_at(C_RBATCH);  // run batches
+#ifdef GS_RUN_TL
+    c.dbg[3] = ctr_at(C_RBT0);  // ticks in the batch step, check included
+    c.dbg[4] = ctr_at(C_RBT1);  // ticks in the batches' placement
 #endif
 #endif
     c.t_sort = c.t_scan = c.t_tmpl = ~0ull;  // not measured: gs_result reports -1

@@ -303,6 +303,7 @@ struct DevProblem {
   const VarRec* qvars;         // [P] first variant of queue0[k], in queue order (first-pass prefetch)
   const int64_t* qreqs;        // [P][R] requests of queue0[k]
   const uint32_t* qcodes;      // [P][4] their slack-test codes: floor lo/hi dword, ceil lo/hi dword (16 bits per resource 0..3)
+  const uint32_t* qrun;        // [P] first-pass records k.. (<= 16) equal to record k but for pod and variant index
   const NodeRec* nodes0;       // [NN] in <U> order: initialized first, then name
   const FK* n_fk0;             // [NN][F] free-key requirement state per node
   NodeRec* nodes;              // working copies (reset at every run)

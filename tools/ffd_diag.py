@@ -62,6 +62,10 @@ else:
                                                             "x_scan"])}
     # dbg[14]: s_memtime ticks in run mode (GS_RUN_TL builds), else run-mode exact batches
     base["runs"]["exact_batches_or_run_ticks"] = int(out[14])
+    base["runs"]["batches"] = int(out[6])
+    base["runs"]["batch_pods"] = int(out[5])
+    base["runs"]["batch_ticks_all_or_sort_decide"] = int(out[3])
+    base["runs"]["batch_ticks_placed_or_pop"] = int(out[4])
     if "--cat" in sys.argv:  # GS_CAT_TL build: shader cycles per pod category
         names = ["run_mode", "simple_claim", "-", "other_claim", "new_claim", "failed", "existing_node", "unknown"]
         base["categories"] = {n: {"pods": int(out[8 + i]), "mcycles": round(out[i] / 1e6, 2),
