@@ -479,7 +479,7 @@ struct Blk {
     for (int k = (int)tid; k < n; k += FB) swap(a + k, b - 1 - k);
     sync();
   }
-  __device__ void pdqsort(int n) {
+  __device__ __forceinline__ void pdqsort_body(int n) {
     SeqSort seq{{sc, ord}};
     if (n <= SEQ) {
       if (tid == 0) seq.pdq_frame(Frame{0, n, bits_len((uint64_t)n), 1, 1});
@@ -553,6 +553,21 @@ struct Blk {
     sync();
   }
 };
+
+// The generic sort's one out-of-line body (ROUND 6): the
+// helper's fields arrive as scalar arguments with the LDS pointers
+// LDS-qualified and the helper is rebuilt locally.  As a member function its
+// `this` pointed at a per-lane copy in scratch: every workgroup stored the
+// helper at start-up (~7 KB of the ~11.9 KB per-workgroup prologue writes of
+// the simulation kernel, profiles/r5/sim_writes_per_wg.txt) and the sort's
+// LDS accesses compiled to flat_* instructions.  Returns the reduction toggle.
+template <uint32_t NT, int SEQ>
+__device__ __noinline__ uint32_t blk_pdqsort(lds_u16* sc, lds_u16* ord, lds_u16* scr, __attribute__((address_space(3))) Shared* S,
+                                             uint32_t tid, uint32_t tog, uint32_t half, int n) {
+  Blk<NT, SEQ> b{(uint16_t*)sc, (uint16_t*)ord, (uint16_t*)scr, *(Shared*)S, tid, tid & 63u, tid >> 6, tog, half};
+  b.pdqsort_body(n);
+  return b.tog;
+}
 
 
 }  // namespace
@@ -1193,7 +1208,8 @@ __global__ __launch_bounds__(NT, SIM ? sim_waves_per_eu(NT) : 1) void ffd_kernel
           }
           blk.rotate_right(e, (int)M - 1);
         } else if (fp == FP_GENERIC) {
-          blk.pdqsort((int)M);
+          blk.tog = blk_pdqsort<NT, SEQ_SORT>((lds_u16*)s_sc, (lds_u16*)s_ord, (lds_u16*)s_scr,
+                                             (__attribute__((address_space(3))) Shared*)&S, tid, blk.tog, blk.half, (int)M);
         }
         if (fp) __syncthreads();  // the new order before the scan reads it
         TL(5);  // rotation / pdqsort + barrier
