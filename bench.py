@@ -820,7 +820,7 @@ def main():
     ap.add_argument("--only", default=None, help="run one leg only: cm | c1 | c2 | c3 | e2e | e2e200 | c5_solve | cm_c4 | "
                                                  "c4 | c4_mixed | c4_multi | c4_e2e | c4_e2e_multi | c5 | filter | "
                                                  "ranking (profiling passes)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r5", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r6", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per leg (tools/pmc_traffic.py, committed under profiles/)")
     ap.add_argument("--detail-json", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="the whole record (every leg); stdout's last line is the compact headline")

@@ -2077,22 +2077,34 @@ __global__ __launch_bounds__(256) void queue_records_kernel(DevProblem d) {
 // qrun[k]: how many records from k on (at most the ring's 16) equal record k
 // in every dword the wave Solve's run mode compares (all but the pod and the
 // variant index): the batch of a run's pods reads it from the ring
-// (ffd_wave.hpp GS_RUN_BATCH) instead of comparing 16 staged records
+// (ffd_wave.hpp GS_RUN_BATCH) instead of comparing 16 staged records.  One
+// comparison per adjacent pair (same[x]: record x equals record x + 1) into
+// LDS, block range plus a 15-entry halo, then a scan of at most 15 bits
 __device__ __forceinline__ bool queue_record_same(const DevProblem& d, uint32_t a, uint32_t b) {
-  const uint32_t* va = (const uint32_t*)(d.qvars + a);
-  const uint32_t* vb = (const uint32_t*)(d.qvars + b);
-  for (uint32_t i = 1; i < sizeof(VarRec) / 4 - 1; i++)
-    if (va[i] != vb[i]) return false;
-  for (uint32_t r = 0; r < d.R; r++)
-    if (d.qreqs[(size_t)a * d.R + r] != d.qreqs[(size_t)b * d.R + r]) return false;
-  // the codes follow from the requests
-  return true;
+  const uint4* va = (const uint4*)(d.qvars + a);
+  const uint4* vb = (const uint4*)(d.qvars + b);
+  bool same = true;
+#pragma unroll
+  for (uint32_t q = 0; q < sizeof(VarRec) / 16; q++) {
+    const uint4 x = va[q], y = vb[q];
+    // dword 0 (pod) and the last dword (variant index) may differ
+    same = same && (q == 0 || x.x == y.x) && x.y == y.y && x.z == y.z && (q == sizeof(VarRec) / 16 - 1 || x.w == y.w);
+  }
+  for (uint32_t r = 0; r < d.R; r++) same = same && d.qreqs[(size_t)a * d.R + r] == d.qreqs[(size_t)b * d.R + r];
+  return same;  // the codes follow from the requests
 }
 __global__ __launch_bounds__(256) void queue_runs_kernel(DevProblem d) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  __shared__ uint8_t s_same[256 + 16];
+  const uint32_t b0 = blockIdx.x * 256;
+  for (uint32_t t = threadIdx.x; t < 256 + 16; t += 256) {
+    const uint32_t x = b0 + t;
+    s_same[t] = x + 1 < d.P && queue_record_same(d, x, x + 1);
+  }
+  __syncthreads();
+  const uint32_t k = b0 + threadIdx.x;
   if (k >= d.P) return;
   uint32_t n = 1;
-  while (n < 16 && k + n < d.P && queue_record_same(d, k, k + n)) n++;
+  while (n < 16 && s_same[threadIdx.x + n - 1]) n++;
   const_cast<uint32_t*>(d.qrun)[k] = n;
 }
 

@@ -56,7 +56,10 @@ constexpr uint32_t WREG = 4;  // option words a scoring lane keeps in registers
 #define GS_ADD_LANES 1
 #endif
 // solver <-> memory-agent wave channels (LDS)
-constexpr uint32_t RING = 16;    // first-pass pod records staged ahead of the solver
+#ifndef GS_RING
+#define GS_RING 16
+#endif
+constexpr uint32_t RING = GS_RING;  // first-pass pod records staged ahead of the solver
 constexpr uint32_t RING_DW = 53; // VarRec (32 dwords) + requests (<= 16 dwords) + request codes (4 dwords) + qrun
 constexpr uint32_t RING_CODES = 48;  // lanes 48..51: floor codes lo/hi dword, ceil codes lo/hi dword
 constexpr uint32_t RING_QRUN = 52;   // lane 52: qrun (records from here on with this one's spec, <= 16)

@@ -11,6 +11,8 @@
 #   only:<leg>     bench.py --only <leg> (5 steps)
 #   ffd            tools/ffd_diag.py FFD device ms on cm / c3 / e2e / c2
 #   prof           tools/profile_round.sh (kernel stats + PMC traffic)
+#   sqpmc          SQ instruction / stall counters of the wave Solve on CM, two
+#                  rocprofv3 passes per library (VARIANTS; base = libgpusched.so)
 #   lib:<name>     use gpusched/libgpusched_<name>.so for the steps after it
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -48,6 +50,14 @@ for step in "$@"; do
       tail -20 $O/ffd_diag.txt ;;
     prof)
       bash tools/profile_round.sh ;;
+    sqpmc)
+      for v in ${VARIANTS:-} base; do
+        lib=libgpusched_$v.so
+        [ "$v" = base ] && lib=libgpusched.so
+        (cd /tmp && TMPDIR=/tmp GPUSCHED_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH --output-format csv -d $O/sq_${v}_a -o pmc -- python3 $R/tools/ffd_diag.py > $O/sq_${v}_a.json 2> $O/sq_${v}_a.err)
+        (cd /tmp && TMPDIR=/tmp GPUSCHED_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $O/sq_${v}_b -o pmc -- python3 $R/tools/ffd_diag.py > $O/sq_${v}_b.json 2> $O/sq_${v}_b.err)
+        echo "sqpmc $v done"
+      done ;;
     lib:*)
       export GPUSCHED_LIB=$R/karpenter-provider-ibm-cloud_amd/gpusched/libgpusched_${step#lib:}.so ;;
     *)

@@ -9,7 +9,7 @@ O=$R/gpurun_out/prof
 mkdir -p $O
 cd /tmp
 export TMPDIR=/tmp
-LEGS=${LEGS:-"cm c3 c4 c4_mixed c4_multi c5"}
+LEGS=${LEGS:-"cm c3 c4 c4_mixed c4_e2e c4_multi c5"}
 if [ -z "${SKIP_KT:-}" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- \
     python3 $R/bench.py --steps 3 --warmup 1 --latency-steps 1 --no-cpu-baseline > $O/bench_kt.json 2> $O/kt.err
