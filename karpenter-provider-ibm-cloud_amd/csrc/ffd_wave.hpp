@@ -1039,8 +1039,13 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
 #ifndef GS_RUN_NODES
 #define GS_RUN_NODES 1
 #endif
-#ifndef GS_RUN_BATCH  // up to RING pods of a run placed in one step
-#define GS_RUN_BATCH 1
+// GS_RUN_BATCH=1: up to 16 pods of a run placed in one step (round 6,
+// bit-exact).  Off by default: it cuts run-mode cycles per pod 4,225 -> 3,914
+// on CM, but the pod loop's register allocation around the added code costs
+// the general path as much (same session, FFD ms: CM 283.2 -> 282.9, C2
+// 36.4 -> 37.7, C1 3.18 -> 3.51; profiles/r6/run_batch_*.txt)
+#ifndef GS_RUN_BATCH
+#define GS_RUN_BATCH 0
 #endif
 #ifndef GS_RUN_WIDE  // the wide-row instantiation in run mode
 #define GS_RUN_WIDE 0
