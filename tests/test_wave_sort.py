@@ -97,6 +97,24 @@ def test_random_sorted_runs_with_swaps(seed):
     check(a)
 
 
+@pytest.mark.parametrize("n", range(0, 65))
+def test_register_frames_every_size(n):
+    """arrays of <= 64 NodeClaims sort in registers (RegSort, ffd_wave.hpp):
+    every length, keys from two values to distinct, sorted-with-swaps and
+    reversed inputs (choosePivot's decreasing hint), permutation for permutation"""
+    rng = np.random.default_rng(400 + n)
+    for vals in (2, 3, 8, 1000):
+        check(rng.integers(0, vals, size=n))
+    a = np.sort(rng.integers(0, 6, size=n))
+    for _ in range(2):
+        if n:
+            i, j = rng.integers(0, n, size=2)
+            a[i], a[j] = a[j], a[i]
+    check(a)
+    check(np.sort(rng.integers(0, 50, size=n))[::-1])
+    check(list(range(n)))
+
+
 @pytest.mark.parametrize("seed", range(20))
 def test_random_keys(seed):
     rng = np.random.default_rng(300 + seed)
