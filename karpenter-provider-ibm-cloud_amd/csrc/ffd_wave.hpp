@@ -366,6 +366,12 @@ struct RegSort {
     int sp = 0;
     for (;;) {
       for (;;) {
+        // wave-uniform loop state (scalar registers and branches)
+        a = __builtin_amdgcn_readfirstlane(a);
+        b = __builtin_amdgcn_readfirstlane(b);
+        limit = __builtin_amdgcn_readfirstlane(limit);
+        wb = __builtin_amdgcn_readfirstlane(wb);
+        wp = __builtin_amdgcn_readfirstlane(wp);
         const int length = b - a;
         if (length <= 12) {
           insertion_sort(a, b);
@@ -417,6 +423,7 @@ struct RegSort {
         wb = 1;
         wp = 1;
       }
+      sp = __builtin_amdgcn_readfirstlane(sp);
       if (sp == 0) break;
       sp--;
       const uint32_t e = rlane(stk, (uint32_t)sp);
@@ -432,10 +439,17 @@ struct RegSort {
 // line, scalar arguments (no `this` in scratch)
 template <class U32, bool G>
 __device__ __noinline__ void reg_pdq_frame(U32* so, int fa, int fb, int limit, int wb, int wp) {
+  // arguments arrive in VGPRs: made wave-uniform, so the control flow below
+  // compiles to scalar branches instead of exec-masked divergent loops
+  fa = __builtin_amdgcn_readfirstlane(fa);
+  fb = __builtin_amdgcn_readfirstlane(fb);
+  limit = __builtin_amdgcn_readfirstlane(limit);
+  wb = __builtin_amdgcn_readfirstlane(wb);
+  wp = __builtin_amdgcn_readfirstlane(wp);
   const uint32_t lane = threadIdx.x & 63u;
   const int n = fb - fa;
-  RegSort<U32, G> r{(int)lane < n ? (uint32_t)so[fa + (int)lane] : 0u, lane, fa,
-                    fa > 0 ? (uint32_t)so[fa - 1] & 0xFFFFu : 0u};
+  const uint32_t prevk = fa > 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)so[fa - 1]) & 0xFFFFu : 0u;
+  RegSort<U32, G> r{(int)lane < n ? (uint32_t)so[fa + (int)lane] : 0u, lane, fa, prevk};
   r.run(so, Frame{fa, fb, limit, wb, wp, 0});
   if ((int)lane < n) so[fa + (int)lane] = r.v;
   wsyncT<G>();
@@ -969,6 +983,8 @@ __device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uin
                                           , uint64_t* stl = nullptr
 #endif
 ) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  half = __builtin_amdgcn_readfirstlane(half);
 #ifdef GS_SORT_TL
   WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
   w.stl = stl;
