@@ -2261,8 +2261,12 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
       inversion = __builtin_amdgcn_readfirstlane(inversion ? 1u : 0u) != 0;
       if (inversion) {
         if (M <= 12) {
-          if (lane == 0) SeqSortT<PackedAccT<U32>>{{(U32*)s_so}}.insertion_sort(0, (int)M);
-          wsyncT<CH>();
+          if (GS_REG_SORT) {
+            reg_pdq_frame<U32, CH>((U32*)s_so, 0, (int)M, bits_len((uint64_t)M), 1, 1);  // insertionSort
+          } else {
+            if (lane == 0) SeqSortT<PackedAccT<U32>>{{(U32*)s_so}}.insertion_sort(0, (int)M);
+            wsyncT<CH>();
+          }
           hint_ok = false;
         } else if (M >= 50 && (!pivot_touched(modkind, modpos, M) || pivot_hint_wave(acc, (int)M, lane) == 1)) {
           // partialInsertionSort fixes the single inversion: one rotation
