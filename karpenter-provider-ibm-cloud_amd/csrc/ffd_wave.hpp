@@ -538,42 +538,42 @@ struct WaveSort {
   // masks (lists_from_masks) instead of two more passes over the keys
   template <bool LE>
   __device__ uint32_t count_split(int lo, int hi, uint32_t p, bool* lo_uni, bool* hi_uni, uint64_t* mk) const {
-    uint32_t c = 0, amin = 0xFFFFu, amax = 0, bmin = 0xFFFFu, bmax = 0;
-    uint64_t mine = 0;
+    // side uniformity: the first key seen on a side is its representative
+    // (readlane), and a ballot of keys that differ from it; no cross-lane
+    // reductions
+    uint32_t c = 0, ra = 0, rb = 0;
+    bool ha = false, hb = false;
+    uint64_t da = 0, db = 0, mine = 0;
     for (int base = lo; base < hi; base += 64 * RW) {
-      bool in[RW];
+      uint32_t kk[RW];
+#pragma unroll
+      for (int u = 0; u < RW; u++) {
+        const int k = base + u * 64 + (int)lane;
+        kk[u] = key(k < hi ? k : hi - 1);  // unconditional read: no exec-masked load
+      }
 #pragma unroll
       for (int u = 0; u < RW; u++) {
         const int k = base + u * 64 + (int)lane;
         const bool valid = k < hi;
-        const uint32_t kk = valid ? key(k) : 0u;
-        in[u] = valid && (LE ? kk <= p : kk < p);
-        if (in[u]) {
-          amin = kk < amin ? kk : amin;
-          amax = kk > amax ? kk : amax;
-        } else if (valid) {
-          bmin = kk < bmin ? kk : bmin;
-          bmax = kk > bmax ? kk : bmax;
+        const bool in = valid && (LE ? kk[u] <= p : kk[u] < p);
+        const uint64_t bi = __ballot(in), bo = __ballot(valid && !in);
+        c += (uint32_t)__popcll(bi);
+        if (lane == (uint32_t)((base - lo) / 64 + u)) mine = bi;
+        if (!ha && bi) {
+          ra = rlane(kk[u], ffs64(bi));
+          ha = true;
         }
-      }
-#pragma unroll
-      for (int u = 0; u < RW; u++) {
-        const uint64_t b = __ballot(in[u]);
-        c += (uint32_t)__popcll(b);
-        if (lane == (uint32_t)((base - lo) / 64 + u)) mine = b;
+        if (!hb && bo) {
+          rb = rlane(kk[u], ffs64(bo));
+          hb = true;
+        }
+        da |= __ballot(in && kk[u] != ra);
+        db |= __ballot(valid && !in && kk[u] != rb);
       }
     }
     *mk = mine;
-    for (int m = 32; m >= 1; m >>= 1) {
-      const uint32_t x0 = (uint32_t)__shfl_xor((int)amin, m), x1 = (uint32_t)__shfl_xor((int)amax, m);
-      const uint32_t x2 = (uint32_t)__shfl_xor((int)bmin, m), x3 = (uint32_t)__shfl_xor((int)bmax, m);
-      amin = x0 < amin ? x0 : amin;
-      amax = x1 > amax ? x1 : amax;
-      bmin = x2 < bmin ? x2 : bmin;
-      bmax = x3 > bmax ? x3 : bmax;
-    }
-    *lo_uni = amin >= amax;  // empty (0xFFFF > 0) or one key value
-    *hi_uni = bmin >= bmax;
+    *lo_uni = da == 0;  // empty or one key value
+    *hi_uni = db == 0;
     return c;
   }
   static constexpr int MASK_MAX = 64 * 64;  // positions the lanes' chunk masks cover
@@ -590,13 +590,19 @@ struct WaveSort {
     const uint64_t left = x0 >= nl ? 0ull : (nl - x0 >= 64u ? ~0ull : ((1ull << (nl - x0)) - 1ull));
     const uint64_t lm = ~mk & left & valid, rm = mk & ~left & valid;
     const uint32_t lc = (uint32_t)__popcll(lm), rc = (uint32_t)__popcll(rm);
-    uint32_t lpre = lc, rsuf = rc;  // inclusive: lanes <= this one / lanes >= this one
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)lpre, d), z = (uint32_t)__shfl_down((int)rsuf, d);
-      if ((int)lane >= d) lpre += y;
-      if ((int)lane + d < 64) rsuf += z;
-    }
-    const uint32_t total = (uint32_t)__shfl((int)lpre, 63);
+    // inclusive prefix over lanes of (lc | rc << 16), row scans and row
+    // broadcasts in DPP (no LDS round trip)
+    uint32_t x = lc | rc << 16;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    const uint32_t tot = rlane(x, 63u);
+    const uint32_t lpre = x & 0xFFFFu;                          // lanes <= this one
+    const uint32_t rsuf = (tot >> 16) - (x >> 16) + rc;         // lanes >= this one
+    const uint32_t total = tot & 0xFFFFu;
     uint32_t k = lpre - lc;
     for (uint64_t m = lm; m; m &= m - 1) scr[k++] = (uint16_t)(lo + (int)(x0 + ffs64(m)));
     k = rsuf - rc;
@@ -696,11 +702,15 @@ struct WaveSort {
   __device__ int first_inversion(int from, int b) const {
     for (int base = from; base < b; base += 64 * RW) {
       bool hit[RW];
+      uint32_t kc[RW], kp[RW];
 #pragma unroll
       for (int u = 0; u < RW; u++) {
-        const int k = base + u * 64 + (int)lane;
-        hit[u] = k < b && key(k) < key(k - 1);
+        const int k = base + u * 64 + (int)lane, kk = k < b ? k : b - 1;  // unconditional reads
+        kc[u] = key(kk);
+        kp[u] = key(kk - 1);
       }
+#pragma unroll
+      for (int u = 0; u < RW; u++) hit[u] = base + u * 64 + (int)lane < b && kc[u] < kp[u];
 #pragma unroll
       for (int u = 0; u < RW; u++) {
         const uint64_t m = __ballot(hit[u]);
@@ -790,9 +800,17 @@ struct WaveSort {
       return;
     }
     int sp = 0;
+    uint32_t stk_ab = 0, stk_fl = 0;
     Frame f{0, n, bits_len((uint64_t)n), 1, 1};
     for (;;) {
       for (;;) {
+        // wave-uniform frame state: scalar registers and branches
+        f.a = __builtin_amdgcn_readfirstlane(f.a);
+        f.b = __builtin_amdgcn_readfirstlane(f.b);
+        f.limit = __builtin_amdgcn_readfirstlane(f.limit);
+        f.wb = __builtin_amdgcn_readfirstlane(f.wb);
+        f.wp = __builtin_amdgcn_readfirstlane(f.wp);
+        f.uni = __builtin_amdgcn_readfirstlane(f.uni);
         const int length = f.b - f.a;
         STL(6);  // frame bookkeeping
         if (GS_REG_SORT ? length <= 64 : length <= SEQ) {
@@ -880,26 +898,23 @@ struct WaveSort {
           f.b = mid;
           f.uni = luni;
         }
-        if (lane == 0) {
-          stk[sp].a = f.a;
-          stk[sp].b = f.b;
-          stk[sp].limit = f.limit;
-          stk[sp].wb = f.wb;
-          stk[sp].wp = f.wp;
-          stk[sp].uni = f.uni;
-        }
-        wsyncT<G>();
+        // the continuing frame waits in lane sp of two VGPRs (depth <= 12
+        // for 4,096 NodeClaims)
+        stk_ab = wlane(stk_ab, sp, (uint32_t)f.a | (uint32_t)f.b << 16);
+        stk_fl = wlane(stk_fl, sp, (uint32_t)f.limit | (uint32_t)f.wb << 8 | (uint32_t)f.wp << 9 | (uint32_t)f.uni << 10);
         sp++;
         f = child;
       }
+      sp = __builtin_amdgcn_readfirstlane(sp);
       if (sp == 0) break;
       sp--;
-      f.a = __builtin_amdgcn_readfirstlane(stk[sp].a);
-      f.b = __builtin_amdgcn_readfirstlane(stk[sp].b);
-      f.limit = __builtin_amdgcn_readfirstlane(stk[sp].limit);
-      f.wb = __builtin_amdgcn_readfirstlane(stk[sp].wb);
-      f.wp = __builtin_amdgcn_readfirstlane(stk[sp].wp);
-      f.uni = __builtin_amdgcn_readfirstlane(stk[sp].uni);
+      const uint32_t ab = rlane(stk_ab, (uint32_t)sp), fl = rlane(stk_fl, (uint32_t)sp);
+      f.a = (int)(ab & 0xFFFFu);
+      f.b = (int)(ab >> 16);
+      f.limit = (int)(fl & 0xFFu);
+      f.wb = (int)((fl >> 8) & 1u);
+      f.wp = (int)((fl >> 9) & 1u);
+      f.uni = (int)((fl >> 10) & 1u);
     }
     wsyncT<G>();
   }
