@@ -174,6 +174,19 @@ __device__ __forceinline__ uint64_t wave_swar_max(uint64_t x) {
   return x;
 }
 
+// wave maximum of an unsigned value, uniform result: row prefix maxima and
+// row broadcasts in DPP, lane 63 read out (no LDS round trip)
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t x, uint32_t y) { return x > y ? x : y; }
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t x) {
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));  // row_shr:1
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));  // row_shr:2
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));  // row_shr:4
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));  // row_shr:8
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  x = dpp_max_step(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return rlane(x, 63u);
+}
+
 // ------------------------------------------------- register-resident sort
 // Go's pdqsort_func loop (src/sort/zsortfunc.go, restated sequentially in
 // SeqSortT) over a frame of <= 64 elements held one per lane: lane x holds the
@@ -538,42 +551,41 @@ struct WaveSort {
   // masks (lists_from_masks) instead of two more passes over the keys
   template <bool LE>
   __device__ uint32_t count_split(int lo, int hi, uint32_t p, bool* lo_uni, bool* hi_uni, uint64_t* mk) const {
-    // side uniformity: the first key seen on a side is its representative
-    // (readlane), and a ballot of keys that differ from it; no cross-lane
-    // reductions
-    uint32_t c = 0, ra = 0, rb = 0;
-    bool ha = false, hb = false;
-    uint64_t da = 0, db = 0, mine = 0;
-    for (int base = lo; base < hi; base += 64 * RW) {
-      uint32_t kk[RW];
+    // branch-free: every lane keeps the side maxima of keys and of
+    // complemented keys (VALU), reduced once per partition in DPP
+    constexpr int RC = 2 * RW;  // positions read per lane before the first wait
+    uint32_t c = 0, amax = 0, anot = 0, bmax = 0, bnot = 0;
+    uint64_t mine = 0;
+    for (int base = lo; base < hi; base += 64 * RC) {
+      uint32_t kk[RC];
 #pragma unroll
-      for (int u = 0; u < RW; u++) {
+      for (int u = 0; u < RC; u++) {
         const int k = base + u * 64 + (int)lane;
         kk[u] = key(k < hi ? k : hi - 1);  // unconditional read: no exec-masked load
       }
 #pragma unroll
-      for (int u = 0; u < RW; u++) {
+      for (int u = 0; u < RC; u++) {
         const int k = base + u * 64 + (int)lane;
         const bool valid = k < hi;
         const bool in = valid && (LE ? kk[u] <= p : kk[u] < p);
-        const uint64_t bi = __ballot(in), bo = __ballot(valid && !in);
+        const bool out = valid && !in;
+        const uint64_t bi = __ballot(in);
         c += (uint32_t)__popcll(bi);
-        if (lane == (uint32_t)((base - lo) / 64 + u)) mine = bi;
-        if (!ha && bi) {
-          ra = rlane(kk[u], ffs64(bi));
-          ha = true;
-        }
-        if (!hb && bo) {
-          rb = rlane(kk[u], ffs64(bo));
-          hb = true;
-        }
-        da |= __ballot(in && kk[u] != ra);
-        db |= __ballot(valid && !in && kk[u] != rb);
+        mine = lane == (uint32_t)((base - lo) / 64 + u) ? bi : mine;
+        const uint32_t nk = 0xFFFFu - kk[u];
+        amax = in && kk[u] > amax ? kk[u] : amax;
+        anot = in && nk > anot ? nk : anot;
+        bmax = out && kk[u] > bmax ? kk[u] : bmax;
+        bnot = out && nk > bnot ? nk : bnot;
       }
     }
     *mk = mine;
-    *lo_uni = da == 0;  // empty or one key value
-    *hi_uni = db == 0;
+    amax = wave_max_dpp(amax);
+    anot = wave_max_dpp(anot);
+    bmax = wave_max_dpp(bmax);
+    bnot = wave_max_dpp(bnot);
+    *lo_uni = c == 0 || amax == 0xFFFFu - anot;  // empty or one key value
+    *hi_uni = c == (uint32_t)(hi - lo) || bmax == 0xFFFFu - bnot;
     return c;
   }
   static constexpr int MASK_MAX = 64 * 64;  // positions the lanes' chunk masks cover
@@ -614,12 +626,29 @@ struct WaveSort {
     wsyncT<G>();
     return total;
   }
+#ifdef GS_SORT_TL2
+#define PTL(k)                                                                  \
+  do {                                                                          \
+    const uint64_t n_ = __builtin_amdgcn_s_memtime();                           \
+    if (lane == 0 && stl) stl[8 + (k)] += n_ - p_last;                          \
+    p_last = n_;                                                                \
+  } while (0)
+#else
+#define PTL(k) \
+  do {         \
+  } while (0)
+#endif
   __device__ int partition(int a, int b, int pivot, bool* already, bool* luni, bool* runi) const {
+#ifdef GS_SORT_TL2
+    uint64_t p_last = __builtin_amdgcn_s_memtime();
+#endif
     if (lane == 0) swap(a, pivot);
     wsyncT<G>();
     const uint32_t p = key(a);
+    PTL(0);
     uint64_t mk;
     const int mid = a + (int)count_split<false>(a + 1, b, p, luni, runi, &mk);
+    PTL(1);
     uint32_t s;
     if (GS_MASK_LISTS && b - a - 1 <= MASK_MAX) {
       s = lists_from_masks(a + 1, (uint32_t)(mid - a), (uint32_t)(b - a - 1), mk);
@@ -627,9 +656,11 @@ struct WaveSort {
       s = compact(a + 1, mid + 1, false, scr, [&](int k) { return key(k) >= p; });
       compact(mid + 1, b, true, scr + half, [&](int k) { return key(k) < p; });
     }
+    PTL(2);
     swap_lists(s);
     if (lane == 0) swap(mid, a);
     wsyncT<G>();
+    PTL(3);
     *already = s == 0;
     return mid;
   }
@@ -1049,8 +1080,8 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
 #ifdef GS_SORT_TL
-  __shared__ uint64_t s_stl[8];
-  if (threadIdx.x < 8) s_stl[threadIdx.x] = 0;
+  __shared__ uint64_t s_stl[12];
+  if (threadIdx.x < 12) s_stl[threadIdx.x] = 0;
 #endif
   __shared__ uint64_t s_slot[SLOT_LDS_MAX];
   __shared__ uint64_t s_tzm[TMAX], s_tcm[TMAX];
@@ -3122,6 +3153,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
     c.dbg[8] = n_gen_cyc;  // shader cycles in Go's full pdqsort (generic sorts)
 #ifdef GS_SORT_TL
     for (int q = 0; q < 7; q++) c.dbg[9 + q] = s_stl[q];  // generic sort: seq, uniform, pivot, partial, peq, part, frames
+#ifdef GS_SORT_TL2
+    for (int q = 0; q < 4; q++) c.dbg[q] = s_stl[8 + q];  // partition: swap in, count, lists, swaps out
+#endif
 #else
     c.dbg[9] = n_xns;
     c.dbg[10] = n_xb;

@@ -43,6 +43,9 @@ if "--tl" in sys.argv and "--block" not in sys.argv:
     if "--sorttl" in sys.argv:  # GS_SORT_TL build: the generic sort's parts (shader cycles per generic sort)
         base["generic_sort_parts_per_sort"] = {n: round(out[9 + i] / max(res.sorts_generic, 1), 1) for i, n in enumerate(
             ["seq_breakpatterns", "uniform", "pivot", "partial_insertion", "partition_equal", "partition", "frames"])}
+    if "--sorttl2" in sys.argv:  # GS_SORT_TL2 build: the wave partition's parts (shader cycles per generic sort)
+        base["partition_parts_per_sort"] = {n: round(out[i] / max(res.sorts_generic, 1), 1) for i, n in enumerate(
+            ["swap_in", "count_split", "lists", "swaps_out"])}
     base["exact_cands_nonsimple"] = out[9]
     base["exact_batches"] = out[10]
     base["exact_wins"] = out[11]
