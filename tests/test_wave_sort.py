@@ -7,13 +7,17 @@ key values, the e2e shape (a long run of low counts, then the raised claim and
 the active runs), and random keys.  Ties decide which NodeClaim a pod lands
 on, so the permutation -- not just the sorted keys -- must match."""
 import ctypes as C
+import json
+import os
+import sys
 
 import numpy as np
 import pytest
 
 from oracle import pyoracle
 
-pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+HEAP_INPUTS = json.load(open(os.path.join(HERE, "golden", "heapsort_inputs.json")))
 
 
 def go_perm(keys):
@@ -49,6 +53,7 @@ def raised(runs, pos):
     return a
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [13, 20, 49, 50, 51, 64, 100, 200, 333])
 def test_one_raised_key_every_position(n):
     rng = np.random.default_rng(n)
@@ -58,6 +63,7 @@ def test_one_raised_key_every_position(n):
         check(a)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [100, 250, 1000, 1999, 4096])
 def test_raised_on_pivot_samples(n):
     q = n // 4
@@ -70,6 +76,7 @@ def test_raised_on_pivot_samples(n):
 
 @pytest.mark.parametrize("low,mid,m", [(500, 1, 19), (500, 1, 2), (500, 1, 100), (250, 1, 40), (10, 1, 5),
                                        (700, 1, 150)])
+@pytest.mark.gpu
 def test_e2e_shape(low, mid, m):
     """a run of idle claims at a low count, then the raised claim and the
     active runs (tests/golden e2e Solve: 12,494 of 30k sorts look like this)"""
@@ -78,6 +85,7 @@ def test_e2e_shape(low, mid, m):
     check(a[:n])
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(60))
 def test_random_few_values(seed):
     rng = np.random.default_rng(100 + seed)
@@ -86,6 +94,7 @@ def test_random_few_values(seed):
     check(rng.integers(0, vals, size=n))
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(30))
 def test_random_sorted_runs_with_swaps(seed):
     rng = np.random.default_rng(200 + seed)
@@ -97,6 +106,7 @@ def test_random_sorted_runs_with_swaps(seed):
     check(a)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", range(0, 65))
 def test_register_frames_every_size(n):
     """arrays of <= 64 NodeClaims sort in registers (RegSort, ffd_wave.hpp):
@@ -115,8 +125,39 @@ def test_register_frames_every_size(n):
     check(list(range(n)))
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(20))
 def test_random_keys(seed):
     rng = np.random.default_rng(300 + seed)
     n = int(rng.integers(0, 4096))
     check(rng.integers(0, 65535, size=n))
+
+
+def test_heapsort_inputs_reach_heapsort_on_the_oracle():
+    """CPU: the committed inputs do reach Go's heapSort fallback (the Python
+    restatement in make_heapsort_inputs.py counts it), and the oracle's
+    permutation of them equals that restatement's"""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_heapsort_inputs as M
+    assert set(HEAP_INPUTS) == {"30", "45", "64", "100"}
+    for keys in HEAP_INPUTS.values():
+        class K:  # sort (key, index) pairs by key only, as sort.Slice's Less
+            __slots__ = ("k", "i")
+
+            def __init__(self, k, i):
+                self.k, self.i = k, i
+
+            def __lt__(self, o):
+                return self.k < o.k
+        d = [K(k, i) for i, k in enumerate(keys)]
+        heap, _ = M.go_pdqsort(d)
+        assert heap >= 1
+        assert [x.i for x in d] == go_perm(keys)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", ["30", "45", "64", "100"])
+def test_heapsort_inputs(n):
+    """the heapSort fallback: in registers' frame (<= 64: RegSort stores the
+    frame and runs lane 0's heapSort) and on the wave path (100)"""
+    check(HEAP_INPUTS[n])
