@@ -290,6 +290,324 @@ struct SeqSortT {
   }
 };
 
+// ------------------------------------------------------------ wave helpers
+// compiler barrier for LDS hand-offs between lanes of the one wave: the
+// hardware keeps a wave's LDS accesses in order, the compiler must too
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// the claim scan state's hand-offs between lanes: in LDS the wave's in-order
+// LDS queue orders them (wsync); in HBM (G) every store must have completed
+// before another lane's load (s_waitcnt 0: a wave's stores and loads share
+// the vector memory counter on gfx9, and the CU's write-through L1 serves the
+// completed store)
+template <bool G>
+__device__ __forceinline__ void wsyncT() {
+  if (G) __builtin_amdgcn_s_waitcnt(0);
+  wsync();
+}
+
+// readlane as an unsigned dword (the builtin returns int: widening it
+// directly would sign-extend a low dword with bit 31 set)
+__device__ __forceinline__ uint32_t rlane(uint32_t x, uint32_t i) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)i);
+}
+
+__device__ __forceinline__ uint32_t ffs64(uint64_t m) { return (uint32_t)__ffsll((long long)m) - 1u; }
+
+
+// ------------------------------------------------- register-resident sort
+// Go's pdqsort_func loop (src/sort/zsortfunc.go, restated sequentially in
+// SeqSortT) over a frame of <= 64 elements held one per lane: lane x holds the
+// packed element at g + x (key = low 16 bits).  Every data access is a
+// readlane / writelane or a cross-lane permute, so the control stays scalar
+// and no step waits on an LDS round trip.  The parallel steps are exact:
+//  - insertionSort is stable, so a rank (keys below + equal keys before) is
+//    its permutation;
+//  - partition / partitionEqual swap the k-th misplaced element of the left
+//    side (ascending) with the k-th of the right side (descending), as the
+//    wave sort's lists do (WaveSort::partition);
+//  - partialInsertionSort's two shifts are one rotation each.
+// heapSort (limit exhausted, rare) runs SeqSortT on lane 0 over the array.
+// A shift left never passes the frame start: every key before it is <= the
+// frame's keys (pdqsort's partitions), and Less is strict.
+__device__ __forceinline__ uint32_t wlane(uint32_t v, int i, uint32_t x) {
+  return (int)(threadIdx.x & 63u) == i ? x : v;  // v_cmp + v_cndmask
+}
+// position of the r-th (0-based) set bit of m from the bottom; r < popc(m)
+__device__ __forceinline__ uint32_t nth_bit(uint64_t m, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    m = up ? m >> w : m;
+    pos += up ? (uint32_t)w : 0u;
+  }
+  return pos;
+}
+// the array a RegSort frame lives in: packed u32 words (the wave Solve's
+// order, LDS or HBM)
+template <class U32, bool G>
+struct PackedArr {
+  U32* so;
+  __device__ __forceinline__ uint32_t load(int i) const { return (uint32_t)so[i]; }
+  __device__ __forceinline__ void store(int i, uint32_t v) const { so[i] = v; }
+  __device__ __forceinline__ void heap_sort(int a, int b) const { SeqSortT<PackedAccT<U32>>{{so}}.heap_sort(a, b); }
+  __device__ __forceinline__ void sync() const { wsyncT<G>(); }
+};
+template <class Arr>
+struct RegSort {
+  uint32_t v;      // lane x: element g + x
+  uint32_t lane;
+  int g;           // the frame's first array position
+  uint32_t prevk;  // key at g - 1 (g > 0): never moved while this frame runs
+
+  __device__ __forceinline__ uint32_t key(int i) const { return rlane(v, (uint32_t)i) & 0xFFFFu; }
+  __device__ __forceinline__ void swap(int i, int j) {
+    const uint32_t x = rlane(v, (uint32_t)i), y = rlane(v, (uint32_t)j);
+    v = wlane(v, i, y);
+    v = wlane(v, j, x);
+  }
+  // stable: rank = keys below + equal keys at lower positions
+  __device__ void insertion_sort(int a, int b) {
+    const uint32_t k = v & 0xFFFFu;
+    int r = a;
+    for (int j = a; j < b; j++) {
+      const uint32_t kj = key(j);
+      r += (kj < k || (kj == k && j < (int)lane)) ? 1 : 0;
+    }
+    const bool in = (int)lane >= a && (int)lane < b;
+    v = (uint32_t)__builtin_amdgcn_ds_permute((in ? r : (int)lane) * 4, (int)v);
+  }
+  // the misplaced pairs of a partition with left side (a, mid]: lanes of lm
+  // (ascending) trade with lanes of rm (descending), k-th with k-th
+  __device__ void swap_misplaced(uint64_t lm, uint64_t rm) {
+    const uint64_t me = 1ull << lane;
+    const uint64_t below = me - 1ull;
+    uint32_t partner = lane;
+    if (lm & me) {
+      const uint32_t r = (uint32_t)__popcll(lm & below);
+      partner = nth_bit(rm, (uint32_t)__popcll(rm) - 1u - r);
+    } else if (rm & me) {
+      const uint32_t r = (uint32_t)__popcll(rm & ~below & ~me);
+      partner = nth_bit(lm, r);
+    }
+    v = (uint32_t)__shfl((int)v, (int)partner);
+  }
+  __device__ int partition(int a, int b, int pivot, bool* already) {
+    swap(a, pivot);
+    const uint32_t p = key(a), k = v & 0xFFFFu;
+    const bool inr = (int)lane > a && (int)lane < b;
+    const bool lt = k < p;
+    const int mid = a + (int)__popcll(__ballot(inr && lt));
+    const bool inl = (int)lane > a && (int)lane <= mid;
+    const uint64_t lm = __ballot(inl && !lt), rm = __ballot(inr && !inl && lt);
+    if (lm) swap_misplaced(lm, rm);
+    swap(mid, a);
+    *already = lm == 0;
+    return mid;
+  }
+  __device__ int partition_equal(int a, int b, int pivot) {
+    swap(a, pivot);
+    const uint32_t p = key(a), k = v & 0xFFFFu;
+    const bool inr = (int)lane > a && (int)lane < b;
+    const bool le = k <= p;
+    const int mid = a + (int)__popcll(__ballot(inr && le));
+    const bool inl = (int)lane > a && (int)lane <= mid;
+    const uint64_t lm = __ballot(inl && !le), rm = __ballot(inr && !inl && le);
+    if (lm) swap_misplaced(lm, rm);
+    return mid + 1;
+  }
+  __device__ void reverse_range(int a, int b) {
+    const bool in = (int)lane >= a && (int)lane < b;
+    v = (uint32_t)__shfl((int)v, in ? a + b - 1 - (int)lane : (int)lane);
+  }
+  // the element at hi moves to lo, [lo, hi) one position up
+  __device__ void rotate_up(int lo, int hi) {
+    const uint32_t x = rlane(v, (uint32_t)hi);
+    const bool in = (int)lane > lo && (int)lane <= hi;
+    const uint32_t y = (uint32_t)__shfl((int)v, in ? (int)lane - 1 : (int)lane);
+    v = (int)lane == lo ? x : y;
+  }
+  // the element at lo moves to hi, (lo, hi] one position down
+  __device__ void rotate_down(int lo, int hi) {
+    const uint32_t x = rlane(v, (uint32_t)lo);
+    const bool in = (int)lane >= lo && (int)lane < hi;
+    const uint32_t y = (uint32_t)__shfl((int)v, in ? (int)lane + 1 : (int)lane);
+    v = (int)lane == hi ? x : y;
+  }
+  __device__ bool partial_insertion_sort(int a, int b) {
+    int i = a + 1;
+    for (int j = 0; j < 5; j++) {
+      const uint32_t k = v & 0xFFFFu;
+      const uint32_t pk = (uint32_t)__shfl((int)v, (int)lane - 1) & 0xFFFFu;
+      const uint64_t inv = __ballot((int)lane >= i && (int)lane < b && k < pk);
+      if (!inv) return true;
+      i = (int)ffs64(inv);
+      if (b - a < 50) return false;
+      swap(i, i - 1);
+      if (i - a >= 2) {
+        // the smaller element (at i - 1) passes the strictly greater ones
+        const uint32_t x = key(i - 1);
+        const uint64_t hm = __ballot((int)lane <= i - 2 && (v & 0xFFFFu) <= x);
+        const int q = hm ? 63 - (int)__clzll((long long)hm) : -1;
+        rotate_up(q + 1, i - 1);
+      }
+      if (b - i >= 2) {
+        // the greater element (at i) passes the strictly smaller ones
+        const uint32_t y = key(i);
+        const uint64_t em = __ballot((int)lane > i && (int)lane < b && (v & 0xFFFFu) >= y);
+        const int e = em ? (int)ffs64(em) : b;
+        rotate_down(i, e - 1);
+      }
+    }
+    return false;
+  }
+  __device__ void break_patterns(int a, int b) {
+    const int length = b - a;
+    if (length >= 8) {
+      uint64_t r = (uint64_t)length;
+      const uint64_t modulus = 1ull << bits_len((uint64_t)length);
+      const int idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; i++) {
+        r ^= r << 13;
+        r ^= r >> 7;
+        r ^= r << 17;
+        int other = (int)(r & (modulus - 1));
+        if (other >= length) other -= length;
+        swap(idx - 1 + i, a + other);
+      }
+    }
+  }
+  __device__ int choose_pivot(int a, int b, int* hint) const {
+    const int l = b - a;
+    int swaps = 0;
+    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    auto med = [&](int x, int y, int z) {
+      if (key(y) < key(x)) { swaps++; const int t = x; x = y; y = t; }
+      if (key(z) < key(y)) { swaps++; const int t = y; y = z; z = t; }
+      if (key(y) < key(x)) { swaps++; const int t = x; x = y; y = t; }
+      return y;
+    };
+    if (l >= 8) {
+      if (l >= 50) {
+        i = med(i - 1, i, i + 1);
+        j = med(j - 1, j, j + 1);
+        k = med(k - 1, k, k + 1);
+      }
+      j = med(i, j, k);
+    }
+    *hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    return j;
+  }
+  __device__ void heap_sort(const Arr& arr, int a, int b) {
+    if ((int)lane < b && (int)lane >= a) arr.store(g + (int)lane, v);
+    arr.sync();
+    if (lane == 0) arr.heap_sort(g + a, g + b);
+    arr.sync();
+    if ((int)lane < b && (int)lane >= a) v = arr.load(g + (int)lane);
+    arr.sync();
+  }
+  // pdqsort_func's loop from frame f (array positions), recursion on a stack
+  // of packed frames in one VGPR (depth <= 6 for 64 elements)
+  __device__ void run(const Arr& arr, Frame f) {
+    int a = f.a - g, b = f.b - g, limit = f.limit, wb = f.wb, wp = f.wp;
+    uint32_t stk = 0;
+    int sp = 0;
+    for (;;) {
+      for (;;) {
+        // wave-uniform loop state (scalar registers and branches)
+        a = __builtin_amdgcn_readfirstlane(a);
+        b = __builtin_amdgcn_readfirstlane(b);
+        limit = __builtin_amdgcn_readfirstlane(limit);
+        wb = __builtin_amdgcn_readfirstlane(wb);
+        wp = __builtin_amdgcn_readfirstlane(wp);
+        const int length = b - a;
+        if (length <= 12) {
+          insertion_sort(a, b);
+          break;
+        }
+        if (limit == 0) {
+          heap_sort(arr, a, b);
+          break;
+        }
+        if (!wb) {
+          break_patterns(a, b);
+          limit--;
+        }
+        int hint;
+        int pivot = choose_pivot(a, b, &hint);
+        if (hint == 2) {
+          reverse_range(a, b);
+          pivot = (b - 1) - (pivot - a);
+          hint = 1;
+        }
+        if (wb && wp && hint == 1 && partial_insertion_sort(a, b)) break;
+        if (g + a > 0 && !((a > 0 ? key(a - 1) : prevk) < key(pivot))) {
+          a = partition_equal(a, b, pivot);
+          continue;
+        }
+        bool already;
+        const int mid = partition(a, b, pivot, &already);
+        wp = already ? 1 : 0;
+        const int left_len = mid - a, right_len = b - mid, bal = length / 8;
+        int ca, cb;
+        if (left_len < right_len) {
+          wb = left_len >= bal;
+          ca = a;
+          cb = mid;
+          a = mid + 1;
+        } else {
+          wb = right_len >= bal;
+          ca = mid + 1;
+          cb = b;
+          b = mid;
+        }
+        // Go recurses into the smaller side first (fresh wasBalanced /
+        // wasPartitioned), then continues this frame
+        stk = wlane(stk, sp, (uint32_t)a | (uint32_t)b << 8 | (uint32_t)limit << 16 | (uint32_t)wb << 24 |
+                                 (uint32_t)wp << 25);
+        sp++;
+        a = ca;
+        b = cb;
+        wb = 1;
+        wp = 1;
+      }
+      sp = __builtin_amdgcn_readfirstlane(sp);
+      if (sp == 0) break;
+      sp--;
+      const uint32_t e = rlane(stk, (uint32_t)sp);
+      a = (int)(e & 0xFFu);
+      b = (int)((e >> 8) & 0xFFu);
+      limit = (int)((e >> 16) & 0xFFu);
+      wb = (int)((e >> 24) & 1u);
+      wp = (int)((e >> 25) & 1u);
+    }
+  }
+};
+// the frame [f.a, f.b) (f.b - f.a <= 64) through RegSort, on one wave: out
+// of line, scalar arguments (no `this` in scratch)
+template <class Arr>
+__device__ __noinline__ void reg_pdq_frame(Arr arr, int fa, int fb, int limit, int wb, int wp) {
+  // arguments arrive in VGPRs: made wave-uniform, so the control flow below
+  // compiles to scalar branches instead of exec-masked divergent loops
+  fa = __builtin_amdgcn_readfirstlane(fa);
+  fb = __builtin_amdgcn_readfirstlane(fb);
+  limit = __builtin_amdgcn_readfirstlane(limit);
+  wb = __builtin_amdgcn_readfirstlane(wb);
+  wp = __builtin_amdgcn_readfirstlane(wp);
+  const uint32_t lane = threadIdx.x & 63u;
+  const int n = fb - fa;
+  const uint32_t prevk = fa > 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)arr.load(fa - 1)) & 0xFFFFu : 0u;
+  RegSort<Arr> r{(int)lane < n ? arr.load(fa + (int)lane) : 0u, lane, fa, prevk};
+  r.run(arr, Frame{fa, fb, limit, wb, wp, 0});
+  if ((int)lane < n) arr.store(fa + (int)lane, r.v);
+  arr.sync();
+}
+
 // first m in [m0, n) with thr[m] >= x (thresholds ascending); n if none
 // Cursor advance over one resource's ascending thresholds: the first m >= m0
 // with thr[m] >= x.  A 4-wide window read in one LDS round trip covers the

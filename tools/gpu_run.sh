@@ -14,6 +14,7 @@
 #   sqpmc          SQ instruction / stall counters of the wave Solve on CM, two
 #                  rocprofv3 passes per library (VARIANTS; base = libgpusched.so)
 #   lib:<name>     use gpusched/libgpusched_<name>.so for the steps after it
+#                  (lib:base: the default library again); their outputs carry _<name>
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:?tag}
@@ -21,6 +22,7 @@ shift
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+LS=
 PYT="python -u -m pytest -m gpu -x -q --timeout 240 --timeout-method thread"
 for step in "$@"; do
   case $step in
@@ -43,8 +45,8 @@ for step in "$@"; do
       tail -c 700 $O/bench.out ;;
     only:*)
       leg=${step#only:}
-      timeout -k 10 300 python -u bench.py --only $leg --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$leg.out 2> $O/bench_$leg.err
-      tail -c 400 $O/bench_$leg.out ;;
+      timeout -k 10 300 python -u bench.py --only $leg --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$leg$LS.out 2> $O/bench_$leg$LS.err
+      tail -c 400 $O/bench_$leg$LS.out ;;
     ffd)
       timeout -k 10 400 python -u tools/ffd_diag.py > $O/ffd_diag.txt 2>&1
       tail -20 $O/ffd_diag.txt ;;
@@ -58,7 +60,11 @@ for step in "$@"; do
         (cd /tmp && TMPDIR=/tmp GPUSCHED_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $O/sq_${v}_b -o pmc -- python3 $R/tools/ffd_diag.py > $O/sq_${v}_b.json 2> $O/sq_${v}_b.err)
         echo "sqpmc $v done"
       done ;;
+    lib:base)
+      LS=_base
+      unset GPUSCHED_LIB ;;
     lib:*)
+      LS=_${step#lib:}  # output files of the steps after it carry the library's name
       export GPUSCHED_LIB=$R/karpenter-provider-ibm-cloud_amd/gpusched/libgpusched_${step#lib:}.so ;;
     *)
       echo "unknown step $step"; exit 2 ;;
