@@ -86,7 +86,7 @@ extern "C" hipError_t gsk_ffdw(const DevProblem* d, uint32_t ch, hipStream_t s) 
 // position; both sorted in place.  *np = the kept count (written by
 // rank_kernel on the same stream); cap bounds it (<= GS_RANK_MAX).
 extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys, uint16_t* pos, const uint32_t* np,
-                                                                  uint32_t cap) {
+                                                                  uint32_t cap, int x) {
   extern __shared__ uint32_t rs_lds[];  // so[cap] (key | position << 16) | scr u16[cap + 2]
   __shared__ Frame rs_stk[64];
   const uint32_t n = __builtin_amdgcn_readfirstlane(*np <= cap ? *np : 0u);
@@ -95,7 +95,7 @@ extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys
   lds_u16* scr = (lds_u16*)(rs_lds + cap);
   for (uint32_t k = lane; k < n; k += 64) so[k] = (uint32_t)keys[k] | ((uint32_t)pos[k] << 16);
   wsync();
-  wave_pdqsort<GS_WAVE_SEQ>(so, scr, (lds_frame*)rs_stk, lane, (n + 1) / 2, (int)n);
+  wave_pdqsort<GS_WAVE_SEQ>(so, scr, (lds_frame*)rs_stk, lane, (n + 1) / 2, (int)n, x < (int)n ? x : -1);
   for (uint32_t k = lane; k < n; k += 64) {
     const uint32_t x = so[k];
     keys[k] = (uint16_t)(x & 0xFFFFu);
@@ -103,9 +103,11 @@ extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys
   }
 }
 
-extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, hipStream_t s) {
+// x: a position known to be the only one out of order (the test hook's
+// one-change inputs: the Solve's partition_known path), or -1
+extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, int x, hipStream_t s) {
   const size_t lds = (size_t)cap * sizeof(uint32_t) + (size_t)(cap + 2) * sizeof(uint16_t);
-  hipLaunchKernelGGL(rank_sort_kernel, dim3(1), dim3(64), lds, s, keys, pos, np, cap);
+  hipLaunchKernelGGL(rank_sort_kernel, dim3(1), dim3(64), lds, s, keys, pos, np, cap, x);
   return hipGetLastError();
 }
 

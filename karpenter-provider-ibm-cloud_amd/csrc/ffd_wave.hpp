@@ -72,6 +72,14 @@ enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 #ifndef GS_WAVE_SEQ
 #define GS_WAVE_SEQ 32
 #endif
+// GS_KNOWN_PARTITION=1: the first partition of a one-change sort searches the
+// boundary (partition_known) instead of counting every key.  Bit-exact (the
+// GPU suite and tests/test_wave_sort.py's one-change inputs passed with it
+// on), but off: same session, E2E 243.9 -> 240.6 ms and CM 268.7 -> 273.5 ms
+// (profiles/r6/known_partition_ab.txt)
+#ifndef GS_KNOWN_PARTITION
+#define GS_KNOWN_PARTITION 0
+#endif
 #ifndef GS_REG_SORT  // 1: sort frames of <= 64 NodeClaims in registers (RegSort); 0: lane 0 over LDS (<= SEQ)
 #define GS_REG_SORT 1
 #endif
@@ -358,6 +366,147 @@ struct WaveSort {
     *already = s == 0;
     return mid;
   }
+  // partition of the whole array [0, n) when the caller knows its shape:
+  // every position but x (the NodeClaim the last Add raised, or the appended
+  // one) holds a non-decreasing sequence.  After swap(0, pivot) the positions
+  // of (0, n) outside E = {x, pivot} still do, so the keys below the pivot's
+  // are those before a boundary t (a 64-ary search, two LDS round trips)
+  // plus E's, and each misplaced list has at most |E| + |E| entries near t /
+  // mid and at E.  Same permutation as partition(): the k-th misplaced
+  // position of the left side (ascending) trades with the k-th of the right
+  // side (descending).  n > 64.
+  __device__ int partition_known(int n, int pivot, int x, bool* already, bool* luni, bool* runi) const {
+    if (lane == 0) swap(0, pivot);
+    wsyncT<G>();
+    const uint32_t p = key(0);
+    const int e0 = x >= 1 && x < n ? x : -1;
+    const int e1 = pivot != x && pivot >= 1 && pivot < n ? pivot : -1;
+    auto in_e = [&](int k) { return k == e0 || k == e1; };
+    auto skip_e = [&](int k) {  // the first position >= k outside E
+      k += in_e(k) ? 1 : 0;
+      k += in_e(k) ? 1 : 0;
+      return k;
+    };
+    // t: the first position of [1, n) outside E with key >= p (n if none)
+    const int step = (n - 1 + 63) / 64;
+    const int q = skip_e(1 + (int)lane * step);
+    const bool qv = 1 + (int)lane * step < n && q < n;
+    const uint64_t m1 = __ballot(qv && key(qv ? q : 0) >= p);
+    int lo, hi;  // t is in [lo, hi]
+    if (m1) {
+      const int l = (int)ffs64(m1);
+      lo = l == 0 ? 1 : (int)rlane((uint32_t)q, (uint32_t)(l - 1)) + 1;
+      hi = (int)rlane((uint32_t)q, (uint32_t)l);
+    } else {
+      const int lv = 63 - (int)__clzll((long long)__ballot(qv));
+      lo = (int)rlane((uint32_t)q, (uint32_t)lv) + 1;
+      hi = n;
+    }
+    int t = hi;
+    for (int base = lo; base < hi; base += 64) {
+      const int k = base + (int)lane;
+      const bool ok = k < hi && k < n && !in_e(k);
+      const uint64_t m2 = __ballot(ok && key(ok ? k : 0) >= p);
+      if (m2) {
+        t = base + (int)ffs64(m2);
+        break;
+      }
+    }
+    // E's keys, read by every lane (uniform)
+    const uint32_t k0 = e0 >= 0 ? key(e0) : 0u, k1 = e1 >= 0 ? key(e1) : 0u;
+    const int e_lt = (e0 >= 0 && k0 < p ? 1 : 0) + (e1 >= 0 && k1 < p ? 1 : 0);
+    const int e_before_t = (e0 >= 1 && e0 < t ? 1 : 0) + (e1 >= 1 && e1 < t ? 1 : 0);
+    const int mid = (t - 1) - e_before_t + e_lt;
+    // side uniformity (before any swap): the sorted part's first and last
+    // keys on each side, and E's keys
+    {
+      auto prev_out = [&](int k) {
+        k -= in_e(k) ? 1 : 0;
+        k -= in_e(k) ? 1 : 0;
+        return k;
+      };
+      uint32_t amin = 0xFFFFu, amax = 0, bmin = 0xFFFFu, bmax = 0;
+      const int f1 = skip_e(1), l1 = prev_out(t - 1);
+      if (f1 < t && l1 >= 1 && f1 <= l1) {
+        amin = key(f1);
+        amax = key(l1);
+      }
+      const int l2 = prev_out(n - 1);
+      if (t < n && l2 >= t) {
+        bmin = key(t);
+        bmax = key(l2);
+      }
+      if (e0 >= 0) {
+        if (k0 < p) {
+          amin = k0 < amin ? k0 : amin;
+          amax = k0 > amax ? k0 : amax;
+        } else {
+          bmin = k0 < bmin ? k0 : bmin;
+          bmax = k0 > bmax ? k0 : bmax;
+        }
+      }
+      if (e1 >= 0) {
+        if (k1 < p) {
+          amin = k1 < amin ? k1 : amin;
+          amax = k1 > amax ? k1 : amax;
+        } else {
+          bmin = k1 < bmin ? k1 : bmin;
+          bmax = k1 > bmax ? k1 : bmax;
+        }
+      }
+      *luni = amin >= amax;  // empty or one key value
+      *runi = bmin >= bmax;
+    }
+    // candidates: lanes 0..3 positions from t (left side past the boundary),
+    // lanes 4..7 positions from mid + 1 (right side before it), lanes 8, 9 E
+    int pos = -1;
+    bool left = false, right = false;
+    if (lane < 4) {
+      pos = t + (int)lane;
+      left = pos <= mid && pos < n && !in_e(pos);
+    } else if (lane < 8) {
+      pos = mid + 1 + (int)(lane - 4);
+      right = pos < t && pos < n && !in_e(pos);
+    } else if (lane == 8 || lane == 9) {
+      pos = lane == 8 ? e0 : e1;
+      if (pos >= 1) {
+        const uint32_t ke = lane == 8 ? k0 : k1;
+        left = pos <= mid && ke >= p;
+        right = pos > mid && ke < p;
+      }
+    }
+    const uint64_t lm = __ballot(left), rm = __ballot(right);
+    const uint32_t s = (uint32_t)__popcll(lm);
+    if (s) {
+      // ranks (left ascending, right descending by position) and partners
+      // (the other side's lane of the same rank): uniform loops over the
+      // flagged lanes
+      const uint64_t fl = lm | rm;
+      int r = 0;
+      for (uint64_t mm = fl; mm; mm &= mm - 1) {
+        const uint32_t j = ffs64(mm);
+        const int pj = (int)rlane((uint32_t)pos, j);
+        const bool lj = (lm >> j) & 1ull;
+        r += (left && lj && pj < pos) || (right && !lj && pj > pos) ? 1 : 0;
+      }
+      int partner = (int)lane;
+      for (uint64_t mm = fl; mm; mm &= mm - 1) {
+        const uint32_t j = ffs64(mm);
+        const int rj = (int)rlane((uint32_t)r, j);
+        const bool lj = (lm >> j) & 1ull;
+        if (((left && !lj) || (right && lj)) && rj == r) partner = (int)j;
+      }
+      const uint32_t wv = (left || right) ? (uint32_t)so[pos] : 0u;
+      const uint32_t pv = (uint32_t)__shfl((int)wv, partner);
+      wsyncT<G>();
+      if (left || right) so[pos] = pv;
+      wsyncT<G>();
+    }
+    if (lane == 0) swap(mid, 0);
+    wsyncT<G>();
+    *already = s == 0;
+    return mid;
+  }
   __device__ int partition_equal(int a, int b, int pivot, bool* runi) const {
     if (lane == 0) swap(a, pivot);
     wsyncT<G>();
@@ -510,7 +659,9 @@ struct WaveSort {
   do {         \
   } while (0)
 #endif
-  __device__ __forceinline__ void pdqsort_body(int n) const {
+  // x: the one position known to break the order (GS_KNOWN_PARTITION: the
+  // first partition then runs partition_known), or -1
+  __device__ __forceinline__ void pdqsort_body(int n, int x = -1) const {
 #ifdef GS_SORT_TL
     uint64_t t_last_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -527,6 +678,7 @@ struct WaveSort {
     int sp = 0;
     uint32_t stk_ab = 0, stk_fl = 0;
     Frame f{0, n, bits_len((uint64_t)n), 1, 1};
+    bool pristine = GS_KNOWN_PARTITION && x >= 0;  // the array is still sorted but for x
     for (;;) {
       for (;;) {
         // wave-uniform frame state: scalar registers and branches
@@ -591,12 +743,14 @@ struct WaveSort {
           reverse_range(f.a, f.b);
           pivot = (f.b - 1) - (pivot - f.a);
           hint = 1;
+          pristine = false;
         }
         STL(2);
         if (f.wb && f.wp && hint == 1) {
           const bool done = partial_insertion_sort(f.a, f.b);
           STL(3);
           if (done) break;
+          pristine = false;
         }
         if (f.a > 0 && !(key(f.a - 1) < key(pivot))) {
           bool runi;
@@ -606,7 +760,9 @@ struct WaveSort {
           continue;
         }
         bool already, luni, runi;
-        const int mid = partition(f.a, f.b, pivot, &already, &luni, &runi);
+        const int mid = pristine && f.a == 0 && f.b == n ? partition_known(n, pivot, x, &already, &luni, &runi)
+                                                         : partition(f.a, f.b, pivot, &already, &luni, &runi);
+        pristine = false;
         STL(5);
         f.wp = already;
         const int leftLen = mid - f.a, rightLen = f.b - mid;
@@ -718,12 +874,13 @@ __device__ __noinline__ RunWin run_batch_place(RunWin w, uint64_t rq, uint32_t b
 // member function would reload them through a `this` pointer in scratch
 // after every LDS store)
 template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
-__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n
+__device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n, int x
 #ifdef GS_SORT_TL
                                           , uint64_t* stl = nullptr
 #endif
 ) {
   n = __builtin_amdgcn_readfirstlane(n);
+  x = __builtin_amdgcn_readfirstlane(x);
   half = __builtin_amdgcn_readfirstlane(half);
 #ifdef GS_SORT_TL
   WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
@@ -731,7 +888,7 @@ __device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uin
 #else
   const WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
 #endif
-  w.pdqsort_body(n);
+  w.pdqsort_body(n, x);
 }
 
 // <U> Requirements.Compatible over the variant's free-key entries
@@ -2033,13 +2190,15 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           }
         } else {
           CTR(C_GEN, 1);
+          // the one position the last Add moved out of order
+          const int known_x = modkind == MOD_INC ? (int)modpos : (int)M - 1;
 #ifdef GS_FFD_TL
           const uint64_t g0_ = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef GS_SORT_TL
-          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, s_stl);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x, s_stl);
 #else
-          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x);
 #endif
 #ifdef GS_FFD_TL
           n_gen_cyc += __builtin_amdgcn_s_memtime() - g0_;

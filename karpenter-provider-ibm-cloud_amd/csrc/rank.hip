@@ -141,7 +141,8 @@ __global__ __launch_bounds__(RK_NT) void rank_gather_kernel(RankArgs a) {
 
 }  // namespace
 
-extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, hipStream_t s);
+extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, int x,
+                                    hipStream_t s);
 
 extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli, const int64_t* memory_bytes,
                                             const double* price, const uint32_t* arch, uint32_t want_arch,
@@ -212,7 +213,7 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
   if (hipMemcpy(d, hin.data(), in_bytes, hipMemcpyHostToDevice) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(RK_NT), lds, 0, a);
   hipLaunchKernelGGL(rank_key_kernel, dim3((n + 63) / 64), dim3(RK_NT), nn * sizeof(double), 0, a);
-  if (hipGetLastError() != hipSuccess || gsk_rank_sort(a.keys, a.pos, a.out_n, n, 0) != hipSuccess) return GS_E_HIP;
+  if (hipGetLastError() != hipSuccess || gsk_rank_sort(a.keys, a.pos, a.out_n, n, -1, 0) != hipSuccess) return GS_E_HIP;
   hipLaunchKernelGGL(rank_gather_kernel, dim3((n + RK_NT - 1) / RK_NT), dim3(RK_NT), 0, 0, a);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpy(hout.data(), dout, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)  // null stream: after the kernel
@@ -231,7 +232,13 @@ extern "C" gs_status gs_rank_instance_types(uint32_t n, const int64_t* cpu_milli
 // over n u16 keys on the current device; perm[k] = the input index that lands
 // at position k.  Parity with Go's pdqsort is checked against the oracle's
 // restatement on adversarial key arrays (one raised key, two or three values).
+extern "C" gs_status gs_debug_go_sort_known(const uint16_t* keys, uint32_t n, int32_t x, uint32_t* perm);
 extern "C" gs_status gs_debug_go_sort(const uint16_t* keys, uint32_t n, uint32_t* perm) {
+  return gs_debug_go_sort_known(keys, n, -1, perm);
+}
+// ... with x: the caller states that every position but x is in order (the
+// Solve's one-change sorts), so the first partition takes partition_known
+extern "C" gs_status gs_debug_go_sort_known(const uint16_t* keys, uint32_t n, int32_t x, uint32_t* perm) {
   if (n && (!keys || !perm)) return GS_E_INVALID;
   if (n > GS_RANK_MAX) return GS_E_CAPACITY;
   if (n == 0) return GS_OK;
@@ -248,7 +255,7 @@ extern "C" gs_status gs_debug_go_sort(const uint16_t* keys, uint32_t n, uint32_t
   uint32_t* dn = (uint32_t*)((char*)d + (((size_t)n * 4 + 3) & ~(size_t)3));
   gs_status st = GS_OK;
   if (hipMemcpy(dk, h.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(dn, &n, 4, hipMemcpyHostToDevice) != hipSuccess || gsk_rank_sort(dk, dp, dn, n, 0) != hipSuccess ||
+      hipMemcpy(dn, &n, 4, hipMemcpyHostToDevice) != hipSuccess || gsk_rank_sort(dk, dp, dn, n, x, 0) != hipSuccess ||
       hipMemcpy(h.data(), dk, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess)
     st = GS_E_HIP;
   (void)hipFree(d);

@@ -41,9 +41,28 @@ def wave_perm(keys):
     return list(p)[:n]
 
 
-def check(keys):
-    keys = [int(x) for x in keys]
-    assert wave_perm(keys) == go_perm(keys), keys if len(keys) < 80 else len(keys)
+def wave_perm_known(keys, x):
+    from gpusched import lib
+    L = lib.load()
+    n = len(keys)
+    f = L.gs_debug_go_sort_known
+    f.argtypes = [C.POINTER(C.c_uint16), C.c_uint32, C.c_int32, C.POINTER(C.c_uint32)]
+    f.restype = C.c_int
+    k = (C.c_uint16 * max(1, n))(*keys)
+    p = (C.c_uint32 * max(1, n))()
+    assert f(k, n, x, p) == 0
+    return list(p)[:n]
+
+
+def check(keys, x=None):
+    """x: the one position out of order (the Solve's one-change sorts: in a
+    GS_KNOWN_PARTITION=1 build the first partition then searches the
+    boundary, WaveSort::partition_known; the default build ignores x)"""
+    keys = [int(v) for v in keys]
+    want = go_perm(keys)
+    assert wave_perm(keys) == want, keys if len(keys) < 80 else len(keys)
+    if x is not None:
+        assert wave_perm_known(keys, x) == want, (x, keys if len(keys) < 80 else len(keys))
 
 
 def raised(runs, pos):
@@ -60,7 +79,7 @@ def test_one_raised_key_every_position(n):
     for pos in range(n):
         runs = [(3, int(rng.integers(1, n))), (4, n)]
         a = raised(runs, pos)[:n]
-        check(a)
+        check(a, pos)
 
 
 @pytest.mark.gpu
@@ -71,7 +90,8 @@ def test_raised_on_pivot_samples(n):
         for d in (-2, -1, 0, 1):
             for lo in (0, n // 8, n // 2, n - 3):
                 runs = [(16, lo), (17, n - lo)]
-                check(raised(runs, max(0, min(n - 1, s + d))))
+                x = max(0, min(n - 1, s + d))
+                check(raised(runs, x), x)
 
 
 @pytest.mark.parametrize("low,mid,m", [(500, 1, 19), (500, 1, 2), (500, 1, 100), (250, 1, 40), (10, 1, 5),
@@ -82,7 +102,7 @@ def test_e2e_shape(low, mid, m):
     active runs (tests/golden e2e Solve: 12,494 of 30k sorts look like this)"""
     n = 1000
     a = [16] * low + [18] * mid + [17] * m + [18] * (n - low - mid - m)
-    check(a[:n])
+    check(a[:n], low if mid == 1 else None)
 
 
 @pytest.mark.gpu
@@ -161,3 +181,23 @@ def test_heapsort_inputs(n):
     """the heapSort fallback: in registers' frame (<= 64: RegSort stores the
     frame and runs lane 0's heapSort) and on the wave path (100)"""
     check(HEAP_INPUTS[n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_one_change_random_runs(seed):
+    """the Solve's one-change inputs over many runs of pod counts: one count
+    raised by one (MOD_INC) anywhere, or a NodeClaim appended with any count
+    (MOD_APPEND), through the boundary-search first partition"""
+    rng = np.random.default_rng(500 + seed)
+    n = int(rng.integers(65, 2500))
+    a = np.sort(rng.integers(0, int(rng.integers(2, 60)), size=n))
+    for _ in range(6):
+        x = int(rng.integers(0, n))
+        b = a.copy()
+        b[x] += 1
+        check(b, x)
+    for _ in range(3):
+        b = a.copy()
+        b[n - 1] = int(rng.integers(0, int(a.max()) + 2))
+        check(b, n - 1)
