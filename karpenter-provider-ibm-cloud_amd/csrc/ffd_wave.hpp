@@ -72,10 +72,12 @@ enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 #ifndef GS_WAVE_SEQ
 #define GS_WAVE_SEQ 32
 #endif
-// GS_KNOWN_PARTITION=1: the first partition of a one-change sort searches the
-// boundary (partition_known) instead of counting every key.  Bit-exact (the
-// GPU suite and tests/test_wave_sort.py's one-change inputs passed with it
-// on), but off: same session, E2E 243.9 -> 240.6 ms and CM 268.7 -> 273.5 ms
+// GS_KNOWN_PARTITION: the first partition of a one-change sort searches the
+// boundary (partition_known) instead of counting every key; 0 never, 1 every
+// instantiation, 2 the topology ones.  Bit-exact (the GPU suite and
+// tests/test_wave_sort.py's one-change inputs passed with it on everywhere),
+// but off: same session, 1: E2E 243.9 -> 240.6 ms, CM 268.7 -> 273.5 ms;
+// 2: E2E 243.9 -> 240.0, C3 382.6 -> 389.8, CM unchanged
 // (profiles/r6/known_partition_ab.txt)
 #ifndef GS_KNOWN_PARTITION
 #define GS_KNOWN_PARTITION 0
@@ -175,7 +177,7 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t x) {
 // restatement of pdqsort_func (ffd.hip Blk) with one wave, so every block
 // reduction is a ballot and every barrier an in-order LDS queue.  Ranges up
 // to SEQ elements run the sequential port on lane 0.
-template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false, bool KNOWN = false>
 struct WaveSort {
   static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
   U32* so;
@@ -678,7 +680,7 @@ struct WaveSort {
     int sp = 0;
     uint32_t stk_ab = 0, stk_fl = 0;
     Frame f{0, n, bits_len((uint64_t)n), 1, 1};
-    bool pristine = GS_KNOWN_PARTITION && x >= 0;  // the array is still sorted but for x
+    bool pristine = KNOWN && x >= 0;  // the array is still sorted but for x
     for (;;) {
       for (;;) {
         // wave-uniform frame state: scalar registers and branches
@@ -873,7 +875,7 @@ __device__ __noinline__ RunWin run_batch_place(RunWin w, uint64_t rq, uint32_t b
 // arguments and the sorter is rebuilt locally, so they stay in registers (a
 // member function would reload them through a `this` pointer in scratch
 // after every LDS store)
-template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false>
+template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false, bool KNOWN = false>
 __device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uint32_t lane, uint32_t half, int n, int x
 #ifdef GS_SORT_TL
                                           , uint64_t* stl = nullptr
@@ -883,10 +885,10 @@ __device__ __noinline__ void wave_pdqsort(U32* so, U16* scr, lds_frame* stk, uin
   x = __builtin_amdgcn_readfirstlane(x);
   half = __builtin_amdgcn_readfirstlane(half);
 #ifdef GS_SORT_TL
-  WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
+  WaveSort<SEQ, U32, U16, G, KNOWN> w{so, scr, stk, lane, half};
   w.stl = stl;
 #else
-  const WaveSort<SEQ, U32, U16, G> w{so, scr, stk, lane, half};
+  const WaveSort<SEQ, U32, U16, G, KNOWN> w{so, scr, stk, lane, half};
 #endif
   w.pdqsort_body(n, x);
 }
@@ -928,6 +930,7 @@ __device__ __forceinline__ bool pivot_touched(uint32_t modkind, uint32_t modpos,
 // carries none of the wide rows' lane-split code, and the other way round
 template <uint32_t RR, bool TOPO, bool CH = false, bool WIDE = false>
 __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
+  constexpr bool KNOWN_PART = GS_KNOWN_PARTITION == 1 || (GS_KNOWN_PARTITION == 2 && TOPO);
   extern __shared__ uint64_t lds64[];
   __shared__ Frame s_stk[64];
 #ifdef GS_SORT_TL
@@ -2196,9 +2199,9 @@ __global__ __launch_bounds__(128, 1) void ffdw_kernel(DevProblem d) {
           const uint64_t g0_ = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef GS_SORT_TL
-          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x, s_stl);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH, KNOWN_PART>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x, s_stl);
 #else
-          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x);
+          wave_pdqsort<GS_WAVE_SEQ, U32, U16, CH, KNOWN_PART>(ws.so, ws.scr, ws.stk, ws.lane, ws.half, (int)M, known_x);
 #endif
 #ifdef GS_FFD_TL
           n_gen_cyc += __builtin_amdgcn_s_memtime() - g0_;
