@@ -201,3 +201,32 @@ def test_one_change_random_runs(seed):
         b = a.copy()
         b[n - 1] = int(rng.integers(0, int(a.max()) + 2))
         check(b, n - 1)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_oracle_gosort_matches_python_restatement(seed):
+    """CPU: the oracle's pdqsort_func restatement (oracle/gosort.h, the
+    checker of every wave-sort test above) against the independent Python
+    restatement in tests/golden/make_heapsort_inputs.py, permutation for
+    permutation, on random keys with many ties and on one-change orders"""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_heapsort_inputs as M
+    rng = np.random.default_rng(900 + seed)
+
+    class K:
+        __slots__ = ("k", "i")
+
+        def __init__(self, k, i):
+            self.k, self.i = k, i
+
+        def __lt__(self, o):
+            return self.k < o.k
+    for _ in range(10):
+        n = int(rng.integers(0, 400))
+        keys = [int(v) for v in rng.integers(0, int(rng.integers(1, 50)), size=n)]
+        if rng.random() < 0.5 and n:
+            keys = sorted(keys)
+            keys[int(rng.integers(0, n))] += 1
+        d = [K(k, i) for i, k in enumerate(keys)]
+        M.go_pdqsort(d)
+        assert [x.i for x in d] == go_perm(keys)
