@@ -95,7 +95,8 @@ extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys
   lds_u16* scr = (lds_u16*)(rs_lds + cap);
   for (uint32_t k = lane; k < n; k += 64) so[k] = (uint32_t)keys[k] | ((uint32_t)pos[k] << 16);
   wsync();
-  wave_pdqsort<GS_WAVE_SEQ>(so, scr, (lds_frame*)rs_stk, lane, (n + 1) / 2, (int)n, x < (int)n ? x : -1);
+  wave_pdqsort<GS_WAVE_SEQ, lds_u32, lds_u16, false, true>(so, scr, (lds_frame*)rs_stk, lane, (n + 1) / 2, (int)n,
+                                                          x < (int)n ? x : -1);
   for (uint32_t k = lane; k < n; k += 64) {
     const uint32_t x = so[k];
     keys[k] = (uint16_t)(x & 0xFFFFu);
@@ -104,7 +105,8 @@ extern "C" __global__ __launch_bounds__(64) void rank_sort_kernel(uint16_t* keys
 }
 
 // x: a position known to be the only one out of order (the test hook's
-// one-change inputs: the Solve's partition_known path), or -1
+// one-change inputs take WaveSort::partition_known whatever the Solve's
+// GS_KNOWN_PARTITION), or -1 (the ranking)
 extern "C" hipError_t gsk_rank_sort(uint16_t* keys, uint16_t* pos, const uint32_t* np, uint32_t cap, int x, hipStream_t s) {
   const size_t lds = (size_t)cap * sizeof(uint32_t) + (size_t)(cap + 2) * sizeof(uint16_t);
   hipLaunchKernelGGL(rank_sort_kernel, dim3(1), dim3(64), lds, s, keys, pos, np, cap, x);

@@ -73,14 +73,16 @@ enum : uint32_t { MOD_NONE = 0, MOD_INC = 1, MOD_APPEND = 2 };
 #define GS_WAVE_SEQ 32
 #endif
 // GS_KNOWN_PARTITION: the first partition of a one-change sort searches the
-// boundary (partition_known) instead of counting every key; 0 never, 1 every
-// instantiation, 2 the topology ones.  Bit-exact (the GPU suite and
-// tests/test_wave_sort.py's one-change inputs passed with it on everywhere),
-// but off: same session, 1: E2E 243.9 -> 240.6 ms, CM 268.7 -> 273.5 ms;
-// 2: E2E 243.9 -> 240.0, C3 382.6 -> 389.8, CM unchanged
+// boundary (known_partition, out of line) instead of counting every key; 0
+// never, 1 every instantiation, 2 the topology ones.  Bit-exact (the GPU
+// suite; tests/test_wave_sort.py's one-change inputs through the rank
+// kernel's instantiation, which always has it).  Inlined into the sort it
+// changed the CM kernel's code shape (59.5 -> 60.7 KB) and CM got slower
+// (268.7 -> 273.5 ms); out of line the kernel keeps its shape: same session
+// CM 268.7 -> 264.6, E2E 243.4 -> 238.4, C3 383.3 -> 381.6 ms
 // (profiles/r6/known_partition_ab.txt)
 #ifndef GS_KNOWN_PARTITION
-#define GS_KNOWN_PARTITION 0
+#define GS_KNOWN_PARTITION 1
 #endif
 #ifndef GS_REG_SORT  // 1: sort frames of <= 64 NodeClaims in registers (RegSort); 0: lane 0 over LDS (<= SEQ)
 #define GS_REG_SORT 1
@@ -177,6 +179,167 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t x) {
 // restatement of pdqsort_func (ffd.hip Blk) with one wave, so every block
 // reduction is a ballot and every barrier an in-order LDS queue.  Ranges up
 // to SEQ elements run the sequential port on lane 0.
+// partition of the whole array [0, n) when the caller knows its shape:
+// every position but x (the NodeClaim the last Add raised, or the appended
+// one) holds a non-decreasing sequence.  After swap(0, pivot) the positions
+// of (0, n) outside E = {x, pivot} still do, so the keys below the pivot's
+// are those before a boundary t (a 64-ary search, two LDS round trips)
+// plus E's, and each misplaced list has at most |E| + |E| entries near t /
+// mid and at E.  Same permutation as partition(): the k-th misplaced
+// position of the left side (ascending) trades with the k-th of the right
+// side (descending).  n > 64.
+struct KnownPart {
+  int mid;
+  int flags;  // 1 already partitioned, 2 left side uniform, 4 right side uniform
+};
+template <class U32, bool G>
+__device__ __noinline__ KnownPart known_partition(U32* so, int n, int pivot, int x) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  pivot = __builtin_amdgcn_readfirstlane(pivot);
+  x = __builtin_amdgcn_readfirstlane(x);
+  const uint32_t lane = threadIdx.x & 63u;
+  auto key = [&](int i) { return (uint32_t)so[i] & 0xFFFFu; };
+  auto swap = [&](int i, int j) {
+    const uint32_t a = so[i];
+    so[i] = so[j];
+    so[j] = a;
+  };
+  bool already_, luni_, runi_;
+  bool* already = &already_;
+  bool* luni = &luni_;
+  bool* runi = &runi_;
+  if (lane == 0) swap(0, pivot);
+  wsyncT<G>();
+  const uint32_t p = key(0);
+  const int e0 = x >= 1 && x < n ? x : -1;
+  const int e1 = pivot != x && pivot >= 1 && pivot < n ? pivot : -1;
+  auto in_e = [&](int k) { return k == e0 || k == e1; };
+  auto skip_e = [&](int k) {  // the first position >= k outside E
+    k += in_e(k) ? 1 : 0;
+    k += in_e(k) ? 1 : 0;
+    return k;
+  };
+  // t: the first position of [1, n) outside E with key >= p (n if none)
+  const int step = (n - 1 + 63) / 64;
+  const int q = skip_e(1 + (int)lane * step);
+  const bool qv = 1 + (int)lane * step < n && q < n;
+  const uint64_t m1 = __ballot(qv && key(qv ? q : 0) >= p);
+  int lo, hi;  // t is in [lo, hi]
+  if (m1) {
+    const int l = (int)ffs64(m1);
+    lo = l == 0 ? 1 : (int)rlane((uint32_t)q, (uint32_t)(l - 1)) + 1;
+    hi = (int)rlane((uint32_t)q, (uint32_t)l);
+  } else {
+    const int lv = 63 - (int)__clzll((long long)__ballot(qv));
+    lo = (int)rlane((uint32_t)q, (uint32_t)lv) + 1;
+    hi = n;
+  }
+  int t = hi;
+  for (int base = lo; base < hi; base += 64) {
+    const int k = base + (int)lane;
+    const bool ok = k < hi && k < n && !in_e(k);
+    const uint64_t m2 = __ballot(ok && key(ok ? k : 0) >= p);
+    if (m2) {
+      t = base + (int)ffs64(m2);
+      break;
+    }
+  }
+  // E's keys, read by every lane (uniform)
+  const uint32_t k0 = e0 >= 0 ? key(e0) : 0u, k1 = e1 >= 0 ? key(e1) : 0u;
+  const int e_lt = (e0 >= 0 && k0 < p ? 1 : 0) + (e1 >= 0 && k1 < p ? 1 : 0);
+  const int e_before_t = (e0 >= 1 && e0 < t ? 1 : 0) + (e1 >= 1 && e1 < t ? 1 : 0);
+  const int mid = (t - 1) - e_before_t + e_lt;
+  // side uniformity (before any swap): the sorted part's first and last
+  // keys on each side, and E's keys
+  {
+    auto prev_out = [&](int k) {
+      k -= in_e(k) ? 1 : 0;
+      k -= in_e(k) ? 1 : 0;
+      return k;
+    };
+    uint32_t amin = 0xFFFFu, amax = 0, bmin = 0xFFFFu, bmax = 0;
+    const int f1 = skip_e(1), l1 = prev_out(t - 1);
+    if (f1 < t && l1 >= 1 && f1 <= l1) {
+      amin = key(f1);
+      amax = key(l1);
+    }
+    const int l2 = prev_out(n - 1);
+    if (t < n && l2 >= t) {
+      bmin = key(t);
+      bmax = key(l2);
+    }
+    if (e0 >= 0) {
+      if (k0 < p) {
+        amin = k0 < amin ? k0 : amin;
+        amax = k0 > amax ? k0 : amax;
+      } else {
+        bmin = k0 < bmin ? k0 : bmin;
+        bmax = k0 > bmax ? k0 : bmax;
+      }
+    }
+    if (e1 >= 0) {
+      if (k1 < p) {
+        amin = k1 < amin ? k1 : amin;
+        amax = k1 > amax ? k1 : amax;
+      } else {
+        bmin = k1 < bmin ? k1 : bmin;
+        bmax = k1 > bmax ? k1 : bmax;
+      }
+    }
+    *luni = amin >= amax;  // empty or one key value
+    *runi = bmin >= bmax;
+  }
+  // candidates: lanes 0..3 positions from t (left side past the boundary),
+  // lanes 4..7 positions from mid + 1 (right side before it), lanes 8, 9 E
+  int pos = -1;
+  bool left = false, right = false;
+  if (lane < 4) {
+    pos = t + (int)lane;
+    left = pos <= mid && pos < n && !in_e(pos);
+  } else if (lane < 8) {
+    pos = mid + 1 + (int)(lane - 4);
+    right = pos < t && pos < n && !in_e(pos);
+  } else if (lane == 8 || lane == 9) {
+    pos = lane == 8 ? e0 : e1;
+    if (pos >= 1) {
+      const uint32_t ke = lane == 8 ? k0 : k1;
+      left = pos <= mid && ke >= p;
+      right = pos > mid && ke < p;
+    }
+  }
+  const uint64_t lm = __ballot(left), rm = __ballot(right);
+  const uint32_t s = (uint32_t)__popcll(lm);
+  if (s) {
+    // ranks (left ascending, right descending by position) and partners
+    // (the other side's lane of the same rank): uniform loops over the
+    // flagged lanes
+    const uint64_t fl = lm | rm;
+    int r = 0;
+    for (uint64_t mm = fl; mm; mm &= mm - 1) {
+      const uint32_t j = ffs64(mm);
+      const int pj = (int)rlane((uint32_t)pos, j);
+      const bool lj = (lm >> j) & 1ull;
+      r += (left && lj && pj < pos) || (right && !lj && pj > pos) ? 1 : 0;
+    }
+    int partner = (int)lane;
+    for (uint64_t mm = fl; mm; mm &= mm - 1) {
+      const uint32_t j = ffs64(mm);
+      const int rj = (int)rlane((uint32_t)r, j);
+      const bool lj = (lm >> j) & 1ull;
+      if (((left && !lj) || (right && lj)) && rj == r) partner = (int)j;
+    }
+    const uint32_t wv = (left || right) ? (uint32_t)so[pos] : 0u;
+    const uint32_t pv = (uint32_t)__shfl((int)wv, partner);
+    wsyncT<G>();
+    if (left || right) so[pos] = pv;
+    wsyncT<G>();
+  }
+  if (lane == 0) swap(mid, 0);
+  wsyncT<G>();
+  *already = s == 0;
+  return KnownPart{mid, (already_ ? 1 : 0) | (luni_ ? 2 : 0) | (runi_ ? 4 : 0)};
+}
+
 template <int SEQ, class U32 = lds_u32, class U16 = lds_u16, bool G = false, bool KNOWN = false>
 struct WaveSort {
   static_assert(SEQ >= 12, "ranges <= 12 must reach Go's insertion sort");
@@ -368,147 +531,9 @@ struct WaveSort {
     *already = s == 0;
     return mid;
   }
-  // partition of the whole array [0, n) when the caller knows its shape:
-  // every position but x (the NodeClaim the last Add raised, or the appended
-  // one) holds a non-decreasing sequence.  After swap(0, pivot) the positions
-  // of (0, n) outside E = {x, pivot} still do, so the keys below the pivot's
-  // are those before a boundary t (a 64-ary search, two LDS round trips)
-  // plus E's, and each misplaced list has at most |E| + |E| entries near t /
-  // mid and at E.  Same permutation as partition(): the k-th misplaced
-  // position of the left side (ascending) trades with the k-th of the right
-  // side (descending).  n > 64.
-  __device__ int partition_known(int n, int pivot, int x, bool* already, bool* luni, bool* runi) const {
-    if (lane == 0) swap(0, pivot);
-    wsyncT<G>();
-    const uint32_t p = key(0);
-    const int e0 = x >= 1 && x < n ? x : -1;
-    const int e1 = pivot != x && pivot >= 1 && pivot < n ? pivot : -1;
-    auto in_e = [&](int k) { return k == e0 || k == e1; };
-    auto skip_e = [&](int k) {  // the first position >= k outside E
-      k += in_e(k) ? 1 : 0;
-      k += in_e(k) ? 1 : 0;
-      return k;
-    };
-    // t: the first position of [1, n) outside E with key >= p (n if none)
-    const int step = (n - 1 + 63) / 64;
-    const int q = skip_e(1 + (int)lane * step);
-    const bool qv = 1 + (int)lane * step < n && q < n;
-    const uint64_t m1 = __ballot(qv && key(qv ? q : 0) >= p);
-    int lo, hi;  // t is in [lo, hi]
-    if (m1) {
-      const int l = (int)ffs64(m1);
-      lo = l == 0 ? 1 : (int)rlane((uint32_t)q, (uint32_t)(l - 1)) + 1;
-      hi = (int)rlane((uint32_t)q, (uint32_t)l);
-    } else {
-      const int lv = 63 - (int)__clzll((long long)__ballot(qv));
-      lo = (int)rlane((uint32_t)q, (uint32_t)lv) + 1;
-      hi = n;
-    }
-    int t = hi;
-    for (int base = lo; base < hi; base += 64) {
-      const int k = base + (int)lane;
-      const bool ok = k < hi && k < n && !in_e(k);
-      const uint64_t m2 = __ballot(ok && key(ok ? k : 0) >= p);
-      if (m2) {
-        t = base + (int)ffs64(m2);
-        break;
-      }
-    }
-    // E's keys, read by every lane (uniform)
-    const uint32_t k0 = e0 >= 0 ? key(e0) : 0u, k1 = e1 >= 0 ? key(e1) : 0u;
-    const int e_lt = (e0 >= 0 && k0 < p ? 1 : 0) + (e1 >= 0 && k1 < p ? 1 : 0);
-    const int e_before_t = (e0 >= 1 && e0 < t ? 1 : 0) + (e1 >= 1 && e1 < t ? 1 : 0);
-    const int mid = (t - 1) - e_before_t + e_lt;
-    // side uniformity (before any swap): the sorted part's first and last
-    // keys on each side, and E's keys
-    {
-      auto prev_out = [&](int k) {
-        k -= in_e(k) ? 1 : 0;
-        k -= in_e(k) ? 1 : 0;
-        return k;
-      };
-      uint32_t amin = 0xFFFFu, amax = 0, bmin = 0xFFFFu, bmax = 0;
-      const int f1 = skip_e(1), l1 = prev_out(t - 1);
-      if (f1 < t && l1 >= 1 && f1 <= l1) {
-        amin = key(f1);
-        amax = key(l1);
-      }
-      const int l2 = prev_out(n - 1);
-      if (t < n && l2 >= t) {
-        bmin = key(t);
-        bmax = key(l2);
-      }
-      if (e0 >= 0) {
-        if (k0 < p) {
-          amin = k0 < amin ? k0 : amin;
-          amax = k0 > amax ? k0 : amax;
-        } else {
-          bmin = k0 < bmin ? k0 : bmin;
-          bmax = k0 > bmax ? k0 : bmax;
-        }
-      }
-      if (e1 >= 0) {
-        if (k1 < p) {
-          amin = k1 < amin ? k1 : amin;
-          amax = k1 > amax ? k1 : amax;
-        } else {
-          bmin = k1 < bmin ? k1 : bmin;
-          bmax = k1 > bmax ? k1 : bmax;
-        }
-      }
-      *luni = amin >= amax;  // empty or one key value
-      *runi = bmin >= bmax;
-    }
-    // candidates: lanes 0..3 positions from t (left side past the boundary),
-    // lanes 4..7 positions from mid + 1 (right side before it), lanes 8, 9 E
-    int pos = -1;
-    bool left = false, right = false;
-    if (lane < 4) {
-      pos = t + (int)lane;
-      left = pos <= mid && pos < n && !in_e(pos);
-    } else if (lane < 8) {
-      pos = mid + 1 + (int)(lane - 4);
-      right = pos < t && pos < n && !in_e(pos);
-    } else if (lane == 8 || lane == 9) {
-      pos = lane == 8 ? e0 : e1;
-      if (pos >= 1) {
-        const uint32_t ke = lane == 8 ? k0 : k1;
-        left = pos <= mid && ke >= p;
-        right = pos > mid && ke < p;
-      }
-    }
-    const uint64_t lm = __ballot(left), rm = __ballot(right);
-    const uint32_t s = (uint32_t)__popcll(lm);
-    if (s) {
-      // ranks (left ascending, right descending by position) and partners
-      // (the other side's lane of the same rank): uniform loops over the
-      // flagged lanes
-      const uint64_t fl = lm | rm;
-      int r = 0;
-      for (uint64_t mm = fl; mm; mm &= mm - 1) {
-        const uint32_t j = ffs64(mm);
-        const int pj = (int)rlane((uint32_t)pos, j);
-        const bool lj = (lm >> j) & 1ull;
-        r += (left && lj && pj < pos) || (right && !lj && pj > pos) ? 1 : 0;
-      }
-      int partner = (int)lane;
-      for (uint64_t mm = fl; mm; mm &= mm - 1) {
-        const uint32_t j = ffs64(mm);
-        const int rj = (int)rlane((uint32_t)r, j);
-        const bool lj = (lm >> j) & 1ull;
-        if (((left && !lj) || (right && lj)) && rj == r) partner = (int)j;
-      }
-      const uint32_t wv = (left || right) ? (uint32_t)so[pos] : 0u;
-      const uint32_t pv = (uint32_t)__shfl((int)wv, partner);
-      wsyncT<G>();
-      if (left || right) so[pos] = pv;
-      wsyncT<G>();
-    }
-    if (lane == 0) swap(mid, 0);
-    wsyncT<G>();
-    *already = s == 0;
-    return mid;
-  }
+  // partition of the whole array [0, n) when the caller knows its shape
+  // (known_partition below, out of line)
+  __device__ int partition_known(int n, int pivot, int x, bool* already, bool* luni, bool* runi) const;
   __device__ int partition_equal(int a, int b, int pivot, bool* runi) const {
     if (lane == 0) swap(a, pivot);
     wsyncT<G>();
@@ -802,6 +827,16 @@ struct WaveSort {
     wsyncT<G>();
   }
 };
+
+template <int SEQ, class U32, class U16, bool G, bool KNOWN>
+__device__ int WaveSort<SEQ, U32, U16, G, KNOWN>::partition_known(int n, int pivot, int x, bool* already, bool* luni,
+                                                                 bool* runi) const {
+  const KnownPart kp = known_partition<U32, G>(so, n, pivot, x);
+  *already = (kp.flags & 1) != 0;
+  *luni = (kp.flags & 2) != 0;
+  *runi = (kp.flags & 4) != 0;
+  return kp.mid;
+}
 
 // The run batch's placement (GS_RUN_BATCH, the pod loop below): out of line,
 // so its registers do not weigh on the rest of the loop.  Pods 2..k of the
